@@ -1,0 +1,359 @@
+"""Benchmark of the SmaQ 6/8-bit compress->decompress round trip on MI355X (BASELINE.json metric).
+
+Default workload (BASELINE.json configs[1]): one contiguous 268,435,456-element fp32 tensor
+(1 GiB, x ~ N(0,1), generated on the device), SmartFP defaults (6/8 bits, thresholds 1.0/2.5,
+full statistics, stochastic rounding), through the drop-in SmartFP.__call__ -> libsmq C-ABI.
+A "step" = one round trip of that tensor (stats launch + apply launch, output tensor allocated by
+the codec like the reference). value = algorithmic bytes (12 B/elem: stats read + apply read +
+write) over all ranks / max-over-ranks wall time of the K timed steps.
+
+Multi-GPU: one process per GPU (torchrun), each rank owns its own 256M tensor (independent
+units, "weak" scaling, no data-path collective; the only collectives are the timing barrier and
+the max-over-ranks reduction of the elapsed time).
+
+Other configs (--config fp8 | s2fp8 | multi | smaq_sampled) are measurement aids, not the line
+the driver records.
+
+roofline: the dominant kernel is smaq_apply_kernel (8 B/elem algorithmic); its average duration is
+measured with events on the codec's stream around every launch inside the timed region.
+cpu_baseline: the oracle (numpy restatement of smart.py, single thread) on a bounded sample.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "smart-quantization_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "SmaQ 6/8-bit quant+dequant round-trip GB/s (and % HBM peak), 256M fp32"
+
+
+class EventTrace:
+    """Events recorded on the current stream around each named kernel launch."""
+
+    def __init__(self):
+        self.pairs = {}
+        self.enabled = True
+
+    def begin(self, name):
+        if self.enabled:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.pairs.setdefault(name, []).append([ev, None])
+
+    def end(self, name):
+        if self.enabled:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.pairs[name][-1][1] = ev
+
+    def mean_ms(self, name):
+        ps = self.pairs.get(name, [])
+        if not ps:
+            return None
+        return float(np.mean([a.elapsed_time(b) for a, b in ps]))
+
+    def reset(self):
+        self.pairs = {}
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        backend = os.environ.get("SMQ_BENCH_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(value, world, device):
+    if world == 1:
+        return value
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(value, world, device):
+    if world == 1:
+        return value
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def smaq_hparams(**over):
+    from argparse import ArgumentParser
+
+    from smart_compress_amd.compress.smart import SmartFP
+
+    hp = SmartFP.add_argparse_args(ArgumentParser()).parse_args([])
+    hp.precision = 32
+    for k, v in over.items():
+        setattr(hp, k, v)
+    return hp
+
+
+def time_steps(step, steps, warmup, world, device):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    return max_over_ranks(elapsed, world, device)
+
+
+def cpu_baseline_smaq(sample_elems, budget_s):
+    """Oracle (numpy, 1 thread) SmaQ 6/8 round trip incl. RNG on a bounded sample."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+
+    rs = np.random.default_rng(0)
+    x = rs.standard_normal(sample_elems).astype(np.float32)
+    cfg = osmaq.SmaqConfig()
+    reps, t_tot = 0, 0.0
+    while t_tot < budget_s or reps < 2:
+        t0 = time.perf_counter()
+        u = orng.uniforms(1, reps * sample_elems, sample_elems)
+        osmaq.roundtrip(x, cfg, uniforms=u)
+        t_tot += time.perf_counter() - t0
+        reps += 1
+    gbps = 12.0 * sample_elems * reps / t_tot / 1e9
+    return {"value": round(gbps, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} x {sample_elems} fp32 N(0,1), numpy oracle/smaq.py (full stats + "
+                      f"SR incl. counter RNG), single thread, {t_tot:.1f} s"}
+
+
+def traffic_from_profile(config):
+    path = os.path.join(REPO, "profiles", f"traffic_{config}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("apply_bytes_per_launch")
+
+
+def run_smaq(args, world, rank, device):
+    from smart_compress_amd.compress.smart import SmartFP
+
+    n = args.n or (1 << 28)
+    sampled = args.config == "smaq_sampled"
+    hp = smaq_hparams(use_sample_stats=sampled)
+    codec = SmartFP(hp)
+    codec.rng.seed = 1000 + rank
+    gen = torch.Generator(device=device).manual_seed(rank)
+    x = torch.randn(n, generator=gen, device=device)
+    trace = EventTrace()
+    codec._trace = trace
+    out = {}
+
+    def step():
+        out["y"] = codec(x)
+
+    trace.enabled = False
+    for _ in range(args.warmup):
+        step()
+    trace.enabled = True
+    elapsed = time_steps(step, args.steps, 0, world, device)
+    alg_per_elem = 8 if sampled else 12
+    total_bytes = sum_over_ranks(alg_per_elem * n * args.steps, world, device)
+    value = total_bytes / elapsed / 1e9
+    apply_ms = trace.mean_ms("apply")
+    stats_ms = trace.mean_ms("stats")
+    apply_gbps = 8.0 * n / (apply_ms * 1e-3) / 1e9
+    res = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": "smaq_6_8_roundtrip_256M_fp32" if not sampled else
+                   "smaq_6_8_roundtrip_sampled_stats", "elements_per_gpu": n,
+                   "stats": "sampled(16)" if sampled else "full", "rounding": "stochastic",
+                   "bits": "6/8", "alg_bytes_per_elem": alg_per_elem,
+                   "parallelism": f"replicas{world}"},
+        "pct_hbm_peak": round(100.0 * value / world / HBM_PEAK_GBPS, 2),
+        "roofline": {"bound": "hbm", "kernel": "smaq_apply_kernel",
+                     "achieved": round(apply_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(apply_gbps / HBM_PEAK_GBPS, 4),
+                     "alg_bytes_per_launch": 8 * n,
+                     "avg_launch_ms": round(apply_ms, 5),
+                     "traffic": traffic_from_profile(args.config)},
+        "kernels_ms": {"smaq_stats_kernel": None if stats_ms is None else round(stats_ms, 5),
+                       "smaq_apply_kernel": round(apply_ms, 5)},
+    }
+    if stats_ms is not None:
+        res["kernels_gbps"] = {"smaq_stats_kernel": round(4.0 * n / (stats_ms * 1e-3) / 1e9, 1),
+                               "smaq_apply_kernel": round(apply_gbps, 1)}
+    return res
+
+
+def run_fp8(args, world, rank, device):
+    """Config 3: FP8 (E5M2, fp8.py) on [128,256,28,28], rotating 8 buffer pairs (> MALL)."""
+    from smart_compress_amd import _native as N
+
+    shape = (128, 256, 28, 28)
+    n = int(np.prod(shape))
+    nbuf = 8
+    gen = torch.Generator(device=device).manual_seed(rank)
+    xs = [torch.relu(torch.randn(shape, generator=gen, device=device)) for _ in range(nbuf)]
+    ys = [torch.empty_like(x) for x in xs]
+    lib = N.lib()
+    st = torch.cuda.current_stream(device).cuda_stream
+    trace = EventTrace()
+    it = [0]
+
+    def step():
+        i = it[0] % nbuf
+        it[0] += 1
+        trace.begin("apply")
+        N.check(lib.smq_float_quant_f32(xs[i].data_ptr(), ys[i].data_ptr(), n, 5, 2,
+                                        N.SMQ_ROUND_STOCHASTIC, 1, None, 7, it[0] * n, st), "fq")
+        trace.end("apply")
+
+    trace.enabled = False
+    for _ in range(args.warmup):
+        step()
+    trace.enabled = True
+    elapsed = time_steps(step, args.steps, 0, world, device)
+    total = sum_over_ranks(8.0 * n * args.steps, world, device)
+    k_ms = trace.mean_ms("apply")
+    gbps = 8.0 * n / (k_ms * 1e-3) / 1e9
+    return {"metric": "FP8 E5M2 round-trip GB/s, [128,256,28,28] fp32", "value": round(total / elapsed / 1e9, 2),
+            "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "fp8_e5m2_roundtrip_resnet34_act", "shape": list(shape),
+                       "rotating_buffers": nbuf},
+            "roofline": {"bound": "hbm", "kernel": "float_quant_kernel", "achieved": round(gbps, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
+                         "avg_launch_ms": round(k_ms, 5), "traffic": traffic_from_profile("fp8")}}
+
+
+def run_s2fp8(args, world, rank, device):
+    """Config 4: S2FP8 on [32,128,768], rotating 48 buffers (> MALL)."""
+    from smart_compress_amd.compress.s2fp8 import S2FP8
+    from argparse import ArgumentParser
+
+    shape = (32, 128, 768)
+    n = int(np.prod(shape))
+    nbuf = 48
+    hp = S2FP8.add_argparse_args(ArgumentParser()).parse_args([])
+    hp.precision = 32
+    codec = S2FP8(hp)
+    gen = torch.Generator(device=device).manual_seed(rank)
+    xs = [torch.randn(shape, generator=gen, device=device) for _ in range(nbuf)]
+    it = [0]
+
+    def step():
+        codec(xs[it[0] % nbuf])
+        it[0] += 1
+
+    elapsed = time_steps(step, args.steps, args.warmup, world, device)
+    total = sum_over_ranks(12.0 * n * args.steps, world, device)
+    return {"metric": "S2FP8 round-trip GB/s, [32,128,768] fp32", "value": round(total / elapsed / 1e9, 2),
+            "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "s2fp8_roundtrip_bert_hidden", "shape": list(shape),
+                       "rotating_buffers": nbuf}}
+
+
+RESNET34_PARAMS = (
+    [(512, 512, 3, 3)] * 5 + [(512, 256, 3, 3)] + [(256, 256, 3, 3)] * 11 + [(256, 128, 3, 3)]
+    + [(128, 128, 3, 3)] * 7 + [(512, 256, 1, 1), (128, 64, 3, 3)] + [(64, 64, 3, 3)] * 6
+    + [(256, 128, 1, 1), (128, 64, 1, 1), (10, 512), (64, 3, 3, 3)] + [(512,)] * 14
+    + [(256,)] * 26 + [(128,)] * 18 + [(64,)] * 14 + [(10,)]
+)
+
+
+def run_multi(args, world, rank, device):
+    """Config 5: fused multi-tensor SmaQ over ResNet-34 (CIFAR) grads (110) + non-BN weights (38)."""
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    gen = torch.Generator(device=device).manual_seed(rank)
+    grads = [torch.randn(s, generator=gen, device=device) * 1e-3 for s in RESNET34_PARAMS]
+    weights = [torch.randn(s, generator=gen, device=device) * 0.05 for s in RESNET34_PARAMS
+               if len(s) != 1]
+    tensors = grads + weights
+    n = sum(t.numel() for t in tensors)
+    outs = [torch.empty_like(t) for t in tensors]
+    m = SmaqMulti(smaq_hparams(), seed=rank)
+
+    def step():
+        m(tensors, outs)
+
+    elapsed = time_steps(step, args.steps, args.warmup, world, device)
+    total = sum_over_ranks(12.0 * n * args.steps, world, device)
+    return {"metric": "Fused multi-tensor SmaQ GB/s, ResNet-34 weights+grads per step",
+            "value": round(total / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "smaq_multi_resnet34_weights_grads", "tensors": len(tensors),
+                       "elements_per_gpu": n}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="smaq",
+                    choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi"])
+    ap.add_argument("--n", type=int, default=0, help="override elements (smaq configs)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 22)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world, rank, local = dist_setup()
+    device = torch.device("cuda", local)
+    runner = {"smaq": run_smaq, "smaq_sampled": run_smaq, "fp8": run_fp8, "s2fp8": run_s2fp8,
+              "multi": run_multi}[args.config]
+    res = runner(args, world, rank, device)
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline and args.config.startswith("smaq"):
+            res["cpu_baseline"] = cpu_baseline_smaq(args.cpu_sample, args.cpu_budget)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+/*
+ * smq.h — C-ABI of the MI355X (gfx950) SmaQ / FP8 / S2FP8 round-trip library (libsmq.so).
+ *
+ * Plain C: raw device pointers, sizes, and an opaque stream handle (a hipStream_t passed as
+ * void*, e.g. torch.cuda.current_stream().cuda_stream). No torch types, no HIP headers needed
+ * by a caller. Every entry point is re-entrant, never synchronises the host, and launches all of
+ * its work on the given stream, so it can be called from the autograd engine's device thread and
+ * captured into a hipGraph.
+ *
+ * Each compute entry point replaces an ATen op sequence inside a reference plugin
+ * (paths relative to nimashoghi/smart-quantization):
+ *
+ *   smq_smaq_stats_f32      smart_compress/compress/smart.py:130-134, 86-91, 100-108, 151-152
+ *                           (mean / unbiased std, range-std, sampled stats, std==0 -> 1)
+ *   smq_smaq_apply_f32      smart_compress/compress/smart.py:154-182
+ *                           (z-score, outlier split, N-bit scale, stochastic/trunc rounding,
+ *                            dequantisation, all_positive) + the outlier count of 184-188
+ *   smq_smaq_roundtrip_f32  smart.py:130-182 (stats + apply, two launches, no host sync)
+ *   smq_smaq_multi_f32      smart.py:110-190 applied to a list of tensors in two launches
+ *                           (the per-parameter calls of util/pytorch/optimizer.py:79-127)
+ *   smq_float_quant_f32     smart_compress/util/pytorch/quantization.py:187-204 and the
+ *                           qtorch 0.2.0 float_quantize it calls (quantization.py:3) —
+ *                           used by compress/fp8.py:31, fp16.py:31, bf16.py:31
+ *   smq_s2fp8_roundtrip_f32 smart_compress/compress/s2fp8.py:27-48
+ *
+ * Errors: every function returns SMQ_OK (0) or a negative SMQ_ERR_* code; the message of the
+ * last failure on the calling thread is returned by smq_last_error(). Nothing aborts.
+ *
+ * Workspaces are caller-allocated device memory. A workspace must be zero-filled ONCE when it is
+ * allocated (the library leaves its arrival counters at zero after every call) and must not be
+ * used by two streams at the same time.
+ */
+#ifndef SMQ_H_
+#define SMQ_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMQ_ABI_VERSION 1
+
+#define SMQ_OK 0
+#define SMQ_ERR_INVALID -1  /* bad argument */
+#define SMQ_ERR_WORKSPACE -2 /* workspace missing or too small */
+#define SMQ_ERR_LAUNCH -3   /* HIP reported an error on launch */
+
+#define SMQ_MAX_SAMPLES 64
+
+/* Where smq_smaq_apply_f32 takes (mean, std) from. */
+#define SMQ_STATS_WORKSPACE 0 /* written by smq_smaq_stats_f32 into the workspace header */
+#define SMQ_STATS_SAMPLED 1   /* computed in-kernel from params.sample_idx (smart.py:86-91) */
+#define SMQ_STATS_INJECTED 2  /* read from the stats_in device pointer (parity tests) */
+
+/* Rounding modes of smq_float_quant_f32 (qtorch float_quantize rounding=...). */
+#define SMQ_ROUND_NEAREST 0
+#define SMQ_ROUND_STOCHASTIC 1
+
+/*
+ * SmaQ parameters. Fill with smq_smaq_params_init() (reference defaults, smart.py:11-84) and
+ * override fields as the hparams Namespace says. Floating constants are the fp32 roundings of the
+ * Python doubles the reference computes (smart.py:72-84).
+ */
+typedef struct SmqSmaqParams {
+  int32_t num_bits_main;        /* --num_bits_main (6) */
+  int32_t num_bits_outlier;     /* --num_bits_outlier (8) */
+  float main_std_dev_threshold; /* fp32(T_m) (1.0) */
+  float range_main;             /* fp32((2^(bm-2)-1)/T_m)             smart.py:76-78 */
+  float range_outlier;          /* fp32((2^(bo-2)-1)/(T_o-T_m))       smart.py:72-75 */
+  float clamp_lo;               /* fp32(1e-38) or fp32(1e-4) at precision 16, smart.py:80-84 */
+  float clamp_hi;               /* fp32(1e38)  or fp32(1e4) */
+  float range_std_coef;         /* 1/sqrt(2 ln n) in fp32 for --use_range_std_dev; <=0: library computes it */
+  int32_t stochastic_rounding;  /* 1 = smart.py:93-98, 0 = trunc (smart.py:168-169) */
+  int32_t all_positive;         /* clamp_min(0) after dequantisation (smart.py:181-182) */
+  int32_t use_range_std_dev;    /* --use_range_std_dev */
+  int32_t stats_source;         /* SMQ_STATS_* */
+  int32_t count_outliers;       /* accumulate the outlier count into the workspace header */
+  int32_t num_samples;          /* k = min(n, --num_samples) entries of sample_idx are used */
+  uint64_t seed;                /* counter-based RNG key (stochastic rounding) */
+  uint64_t offset;              /* RNG counter of element 0; element i uses offset + i */
+  /* --use_batch_norm (smart.py:136-149, 174-179): per-channel (x - beta[c]) / gamma[c] before the
+   * z-score and y * gamma[c] + beta[c] after de-quantisation, c = (i / bn_inner) % bn_channels
+   * (channel dim 1 of NCHW; bn_channels = 1 for --bn_scalar_params). NULL gamma = off. */
+  const float* bn_gamma;        /* device [bn_channels] */
+  const float* bn_beta;         /* device [bn_channels] */
+  int64_t bn_channels;
+  int64_t bn_inner;             /* H * W */
+  int64_t sample_idx[SMQ_MAX_SAMPLES]; /* distinct flat indices for SMQ_STATS_SAMPLED */
+} SmqSmaqParams;
+
+/*
+ * Header of a SmaQ workspace (first 64 bytes). Written on the device; read it after the stream
+ * has reached the call (e.g. by the Python wrapper's lazy log_size).
+ */
+typedef struct SmqSmaqStats {
+  float mean;          /* data.mean() */
+  float std_dev;       /* std after the `std == 0 -> 1` rule (used by the de-normalisation) */
+  float std_clamped;   /* std_dev.clamp(clamp_lo, clamp_hi) (used by the normalisation) */
+  float raw_std;       /* std before the `std == 0` rule */
+  float min_val;       /* min / max (valid in range-std mode) */
+  float max_val;
+  uint32_t n_used;     /* elements the statistics were computed over */
+  uint32_t reserved0;
+  unsigned long long n_outlier; /* outlier count (when params.count_outliers) */
+  uint32_t reserved[6];
+} SmqSmaqStats;
+
+/* One tensor of a multi-tensor call. y may alias x (in-place, the optimizer path). */
+typedef struct SmqTensorDesc {
+  const float* x;
+  float* y;
+  int64_t n;
+  int32_t all_positive;
+  int32_t reserved;
+  uint64_t rng_offset; /* RNG counter of element 0, relative to params.offset */
+} SmqTensorDesc;
+
+/* Header of an S2FP8 workspace. */
+typedef struct SmqS2fp8Stats {
+  float mu;        /* mean(log2|x|), zeros counted as 0 (s2fp8.py:35-40) */
+  float m;         /* max(log2|x|) */
+  float alpha;     /* 15 / (m - mu) */
+  float beta;      /* -alpha * mu */
+  float beta_pow2; /* 2 ** beta */
+  float inv_beta_pow2;
+  float inv_alpha;
+  uint32_t n_used;
+  uint32_t reserved[8];
+} SmqS2fp8Stats;
+
+/* ---- library ---- */
+int smq_abi_version(void);
+const char* smq_last_error(void);
+
+/* Fill p with the reference defaults (smart.py:11-84, precision 32). */
+void smq_smaq_params_init(SmqSmaqParams* p);
+/* Recompute range_main / range_outlier / clamp_* from bit widths, thresholds and precision. */
+int smq_smaq_params_set(SmqSmaqParams* p, int num_bits_main, int num_bits_outlier,
+                        double main_std_dev_threshold, double outlier_std_dev_threshold,
+                        int precision);
+/* Draw k = min(n, num_samples) distinct indices in [0, n) into p->sample_idx (host only; a
+ * deterministic function of (seed, offset)). Replaces torch.randperm(n)[:k] at smart.py:88. */
+int smq_smaq_draw_samples(SmqSmaqParams* p, int64_t n, int num_samples);
+
+/* ---- SmaQ single tensor ---- */
+size_t smq_smaq_workspace_bytes(int64_t n);
+int smq_smaq_stats_f32(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,
+                       size_t ws_bytes, void* stream);
+/* uniforms: optional device array of n U[0,1) floats replacing the in-kernel RNG (parity tests
+ * replay torch.rand_like draws, smart.py:94). stats_in: device pointer, SMQ_STATS_INJECTED only. */
+int smq_smaq_apply_f32(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
+                       const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
+                       size_t ws_bytes, void* stream);
+int smq_smaq_roundtrip_f32(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
+                           const float* uniforms, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- SmaQ multi tensor ---- */
+/* A plan is a descriptor table plus a chunk map. smq_smaq_multi_plan_build writes it into a host
+ * buffer of smq_smaq_multi_plan_bytes; the caller uploads a device copy once and reuses both while
+ * the tensor list (pointers and sizes) is unchanged. Tensors with n < min_size must be left out
+ * (the reference returns them untouched, smart.py:123-128). */
+size_t smq_smaq_multi_plan_bytes(const int64_t* sizes, int count);
+int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_plan,
+                              size_t plan_bytes);
+size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count);
+/* Two launches for the whole list. Statistics of tensor t land in ((SmqSmaqStats*)ws)[t]. Only
+ * full statistics (SMQ_STATS_WORKSPACE, no range-std) are supported. host_plan is read for its
+ * header only. */
+int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan, const SmqSmaqParams* p,
+                       void* ws, size_t ws_bytes, void* stream);
+
+/* ---- qtorch-style float quantisation (FP8 E5M2, FP16, BF16, any exp/man) ---- */
+/* rand_bits: optional device array of n uint32 random words (qtorch's randint_like draws);
+ * else the counter-based RNG keyed by (seed, offset + i) is used. check_inf: quantization.py:195-199. */
+int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int man_bits,
+                        int rounding, int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                        uint64_t offset, void* stream);
+/* fp32 value of qtorch nearest-quantising FLT_MAX (quantization.py:138-150), host only. */
+float smq_float_quant_max_value(int exp_bits, int man_bits);
+
+/* ---- S2FP8 ---- */
+size_t smq_s2fp8_workspace_bytes(int64_t n);
+/* stats_in: optional device SmqS2fp8Stats whose mu and m are used instead of computing them. */
+int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
+                            const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
+                            const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
+                            void* stream);
+
+/* ---- host reference helpers shared with the oracle (pure functions, no GPU) ---- */
+uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SMQ_H_ */

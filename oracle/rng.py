@@ -1,0 +1,43 @@
+"""Counter-based RNG of libsmq, restated in numpy (bit-exact with smq_common.h: mix32, rng_key,
+rng_u32, u32_to_unit). Element i of a call with (seed, offset) uses counter offset + i."""
+
+import numpy as np
+
+_M32 = 0xFFFFFFFF
+
+
+def mix32(x):
+    x = np.asarray(x, dtype=np.uint32).copy()
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def _mix32_int(v: int) -> int:
+    return int(mix32(np.array([v & _M32], dtype=np.uint32))[0])
+
+
+def rng_key(seed: int) -> int:
+    seed &= (1 << 64) - 1
+    return _mix32_int((seed & _M32) ^ _mix32_int(((seed >> 32) ^ 0x9E3779B9) & _M32))
+
+
+def rng_u32(seed: int, offset: int, n: int, start: int = 0) -> np.ndarray:
+    """Random words for elements start..start+n-1 of a call keyed by (seed, offset)."""
+    key = np.uint32(rng_key(seed))
+    ctr = (np.uint64(offset) + np.arange(start, start + n, dtype=np.uint64))
+    lo = (ctr & np.uint64(_M32)).astype(np.uint32)
+    hi = (ctr >> np.uint64(32)).astype(np.uint32)
+    rot = (hi << np.uint32(16)) | (hi >> np.uint32(16))
+    return mix32(lo ^ rot ^ key)
+
+
+def u32_to_unit(h: np.ndarray) -> np.ndarray:
+    return (h >> np.uint32(8)).astype(np.float32) * np.float32(2.0**-24)
+
+
+def uniforms(seed: int, offset: int, n: int, start: int = 0) -> np.ndarray:
+    return u32_to_unit(rng_u32(seed, offset, n, start))

@@ -1,0 +1,441 @@
+// float_quant.hip — qtorch-style bit-level float quantisation (FP8 E5M2 / FP16 / BF16 / any
+// exp,man) and the S2FP8 shift-and-squeeze round trip, for gfx950.
+//
+// Reference:
+//   smart_compress/util/pytorch/quantization.py:187-204  float_quantize (+ check_inf, 195-199)
+//   smart_compress/util/pytorch/quantization.py:138-150  _get_max_value (nearest-quantised FLT_MAX)
+//   smart_compress/compress/fp8.py:27-31                 exp=5, man=2 (E5M2), stochastic
+//   smart_compress/compress/s2fp8.py:27-48               log2-domain mean/max, power squeeze
+//   qtorch 0.2.0 (un-vendored dependency, poetry.lock:773-781): quant_function.float_quantize ->
+//     float_kernel_stochastic / float_kernel_nearest + bit_helper round_bitwise_* / clip_exponent.
+//     Restated here from its published algorithm (integer arithmetic on the fp32 bit pattern).
+//
+// One launch of 8 B/elem for float_quantize: the reference materialises a randint_like int32
+// tensor (+8 B/elem), runs the quantiser and then 3-4 more passes for check_inf; here the random
+// word comes from the counter-based RNG in registers and check_inf is fused.
+#include <float.h>
+#include <math.h>
+#include <string.h>
+
+#include "smq_common.h"
+
+namespace smq {
+
+// ---- qtorch bit helpers (restated) --------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t f2u(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+__host__ __device__ __forceinline__ float u2f(uint32_t u) {
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+__host__ __device__ __forceinline__ uint32_t round_bitwise(uint32_t target, uint32_t rand_bits,
+                                                           int man_bits, bool stochastic) {
+  const uint32_t mask = (1u << (23 - man_bits)) - 1u;
+  const uint32_t add = stochastic ? (rand_bits & mask) : (1u << (23 - man_bits - 1));
+  return (target + add) & ~mask;
+}
+
+__host__ __device__ __forceinline__ uint32_t clip_exponent(int exp_bits, int man_bits,
+                                                           uint32_t old_num, uint32_t q) {
+  const int qexp = (int)((q << 1) >> 24);
+  const int min_store = -((1 << (exp_bits - 1)) - 2) - 1 + 127;
+  const int max_store = ((1 << (exp_bits - 1)) - 1) + 127;
+  if (qexp > max_store) {
+    const uint32_t max_man = ((0xffffffffu << 9) >> 9) >> (23 - man_bits) << (23 - man_bits);
+    const uint32_t max_num = ((uint32_t)max_store << 23) | max_man;
+    q = (old_num & 0x80000000u) | max_num;
+  } else if (qexp < min_store) {
+    const uint32_t min_num = (uint32_t)min_store << 23;
+    const uint32_t middle = (uint32_t)(min_store - 1) << 23;
+    const uint32_t uq = q & 0x7fffffffu;
+    q = uq > middle ? ((old_num & 0x80000000u) | min_num) : 0u;
+  }
+  return q;
+}
+
+// qtorch float_kernel_{stochastic,nearest} for one element.
+__host__ __device__ __forceinline__ float qtorch_quant(float a, uint32_t rand_bits, int exp_bits,
+                                                      int man_bits, bool stochastic) {
+  uint32_t target = f2u(a);
+  const int target_exp = (int)((target << 1) >> 24) - 127;
+  const int min_exp = -((1 << (exp_bits - 1)) - 2);
+  if (target_exp < min_exp) {  // subnormal in the target format
+    const uint32_t shift_bits = ((uint32_t)(127 + min_exp) << 23) | (target & 0x80000000u);
+    const float shift = u2f(shift_bits);
+    const float val = a + shift;
+    const uint32_t qb = round_bitwise(f2u(val), rand_bits, man_bits, stochastic);
+    return u2f(qb) - shift;
+  }
+  uint32_t qb = round_bitwise(target, rand_bits, man_bits, stochastic);
+  qb = clip_exponent(exp_bits, man_bits, target, qb);
+  return u2f(qb);
+}
+
+struct FQArgs {
+  const float* x;
+  float* y;
+  int64_t n;
+  const uint32_t* rand_bits;
+  uint32_t key;
+  uint64_t offset;
+  int exp_bits, man_bits;
+  int check_inf;
+  float max_value;
+};
+
+// abs(y - max) <= FLT_EPSILON -> +inf (quantization.py:195-199)
+__device__ __forceinline__ float check_inf_fn(float y, const FQArgs& A) {
+  return (A.check_inf && fabsf(y - A.max_value) <= FLT_EPSILON) ? INFINITY : y;
+}
+
+template <bool SR, bool RARR, bool VEC>
+__global__ __launch_bounds__(kBlock) void float_quant_kernel(FQArgs A) {
+  const int64_t n = A.n;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  auto rb = [&](int64_t e) -> uint32_t {
+    if (!SR) return 0u;
+    return RARR ? A.rand_bits[e] : rng_u32(A.key, A.offset + (uint64_t)e);
+  };
+  if (VEC) {
+    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
+    float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
+    const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(A.rand_bits);
+    const int64_t nv = n >> 2;
+    for (; i < nv; i += stride) {
+      const float4 v = x4[i];
+      uint32_t r0, r1, r2, r3;
+      if (SR && RARR) {
+        const uint4 rr = r4[i];
+        r0 = rr.x; r1 = rr.y; r2 = rr.z; r3 = rr.w;
+      } else {
+        r0 = rb(4 * i); r1 = rb(4 * i + 1); r2 = rb(4 * i + 2); r3 = rb(4 * i + 3);
+      }
+      float4 o;
+      o.x = check_inf_fn(qtorch_quant(v.x, r0, A.exp_bits, A.man_bits, SR), A);
+      o.y = check_inf_fn(qtorch_quant(v.y, r1, A.exp_bits, A.man_bits, SR), A);
+      o.z = check_inf_fn(qtorch_quant(v.z, r2, A.exp_bits, A.man_bits, SR), A);
+      o.w = check_inf_fn(qtorch_quant(v.w, r3, A.exp_bits, A.man_bits, SR), A);
+      store_nt(y4 + i, o);
+    }
+    i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  }
+  for (; i < n; i += stride)
+    A.y[i] = check_inf_fn(qtorch_quant(A.x[i], rb(i), A.exp_bits, A.man_bits, SR), A);
+}
+
+// ---- S2FP8 ---------------------------------------------------------------------------------------
+struct alignas(16) S2Partial {
+  double s;  // sum of log2|x| (zeros as 0)
+  float m;   // max (NaN-propagating)
+  float pad;
+};
+
+__device__ __forceinline__ float nan_max(float a, float b) {
+  return (b > a || b != b) ? b : a;  // torch.max propagates NaN
+}
+
+__device__ __forceinline__ float s2_log(float x) {
+  const float a = fabsf(x);
+  return (a == 0.0f) ? a : log2f(a);  // torch.where(X_abs == 0.0, X_abs, torch.log2(X_abs))
+}
+
+__device__ void s2fp8_finalize(double s, float m, int64_t n, SmqS2fp8Stats* out) {
+  const float mu = (float)(s / (double)n);  // torch.mean(X_abs_log2)
+  // s2fp8.py:42 `15.0 / (m - mu)`: Python scalar / tensor is Tensor.__rtruediv__ =
+  // reciprocal() * 15.0 — two fp32 roundings, not one division.
+  const float alpha = (1.0f / (m - mu)) * 15.0f;
+  const float beta = (-alpha) * mu;         // s2fp8.py:43
+  const float bp2 = (float)exp2((double)beta);  // 2.0 ** beta, correctly rounded
+  out->mu = mu;
+  out->m = m;
+  out->alpha = alpha;
+  out->beta = beta;
+  out->beta_pow2 = bp2;
+  out->inv_beta_pow2 = 1.0f / bp2;  // beta_pow2.reciprocal_()
+  out->inv_alpha = 1.0f / alpha;    // alpha.reciprocal_()
+  out->n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
+}
+
+constexpr int kS2GridCap = 2048;
+
+__global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const float* __restrict__ x, int64_t n,
+                                                             int vec, S2Partial* partials,
+                                                             uint32_t* counter,
+                                                             SmqS2fp8Stats* out) {
+  __shared__ double shs[kBlock / kWave];
+  __shared__ float shm[kBlock / kWave];
+  __shared__ uint32_t slot;
+  double s = 0.0;
+  float m = -INFINITY;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (vec) {
+    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+    const int64_t nv = n >> 2;
+    for (; i < nv; i += stride) {
+      const float4 v = x4[i];
+      const float l0 = s2_log(v.x), l1 = s2_log(v.y), l2 = s2_log(v.z), l3 = s2_log(v.w);
+      s += (double)l0;
+      s += (double)l1;
+      s += (double)l2;
+      s += (double)l3;
+      m = nan_max(nan_max(m, l0), nan_max(l1, nan_max(l2, l3)));
+    }
+    i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  }
+  for (; i < n; i += stride) {
+    const float l = s2_log(x[i]);
+    s += (double)l;
+    m = nan_max(m, l);
+  }
+  // workgroup reduce
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  s = wave_sum(s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o, kWave));
+  if (lane == 0) {
+    shs[wave] = s;
+    shm[wave] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    S2Partial p;
+    p.s = (shs[0] + shs[1]) + (shs[2] + shs[3]);
+    p.m = nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3]));
+    p.pad = 0.0f;
+    partials[blockIdx.x] = p;
+  }
+  const uint32_t prev = block_arrive(counter, &slot);
+  if (prev != gridDim.x - 1) return;
+  block_acquire();
+  double ts = 0.0;
+  float tm = -INFINITY;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
+    const S2Partial p = partials[b];
+    ts += p.s;
+    tm = nan_max(tm, p.m);
+  }
+  ts = wave_sum(ts);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tm = nan_max(tm, __shfl_xor(tm, o, kWave));
+  __syncthreads();
+  if (lane == 0) {
+    shs[wave] = ts;
+    shm[wave] = tm;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double S = (shs[0] + shs[1]) + (shs[2] + shs[3]);
+    const float M = nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3]));
+    s2fp8_finalize(S, M, n, out);
+    *counter = 0u;
+  }
+}
+
+// Injected (mu, m): derive the rest exactly like the finaliser (parity tests).
+__global__ void s2fp8_derive_kernel(const SmqS2fp8Stats* in, SmqS2fp8Stats* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float mu = in->mu, m = in->m;
+    const float alpha = (1.0f / (m - mu)) * 15.0f;  // see s2fp8_finalize
+    const float beta = (-alpha) * mu;
+    const float bp2 = (float)exp2((double)beta);
+    out->mu = mu;
+    out->m = m;
+    out->alpha = alpha;
+    out->beta = beta;
+    out->beta_pow2 = bp2;
+    out->inv_beta_pow2 = 1.0f / bp2;
+    out->inv_alpha = 1.0f / alpha;
+    out->n_used = in->n_used;
+  }
+}
+
+struct S2Args {
+  const float* x;
+  float* y;
+  int64_t n;
+  const uint32_t* rand_bits;
+  const SmqS2fp8Stats* st;
+  uint32_t key;
+  uint64_t offset;
+  int check_inf;
+  float max_value;
+};
+
+// s2fp8.py:45-48 for one element.
+__device__ __forceinline__ float s2fp8_elem(float xv, uint32_t r, float alpha, float bp2,
+                                            float ibp2, float ialpha, int check_inf,
+                                            float max_value) {
+  // torch.sign: +1 / -1, and +0.0 for +-0 and NaN (measured on torch 2.10 CPU)
+  const float sgn = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
+  const float a = fabsf(xv);
+  float Y = powf(a, alpha);   // X_abs.pow_(alpha)
+  Y = Y * bp2;                // .mul_(beta_pow2)
+  float T = qtorch_quant(Y, r, 5, 2, true);
+  if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
+  const float t1 = T * ibp2;           // truncated * beta_pow2.reciprocal_()
+  const float t2 = powf(t1, ialpha);   // ** alpha.reciprocal_()
+  return t2 * sgn;                     // * signs
+}
+
+template <bool RARR, bool VEC>
+__global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
+  const float alpha = A.st->alpha, bp2 = A.st->beta_pow2, ibp2 = A.st->inv_beta_pow2,
+              ialpha = A.st->inv_alpha;
+  const int64_t n = A.n;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  auto rb = [&](int64_t e) -> uint32_t {
+    return RARR ? A.rand_bits[e] : rng_u32(A.key, A.offset + (uint64_t)e);
+  };
+  if (VEC) {
+    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
+    float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
+    const int64_t nv = n >> 2;
+    for (; i < nv; i += stride) {
+      const float4 v = x4[i];
+      float4 o;
+      o.x = s2fp8_elem(v.x, rb(4 * i), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
+      o.y = s2fp8_elem(v.y, rb(4 * i + 1), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
+      o.z = s2fp8_elem(v.z, rb(4 * i + 2), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
+      o.w = s2fp8_elem(v.w, rb(4 * i + 3), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
+      store_nt(y4 + i, o);
+    }
+    i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  }
+  for (; i < n; i += stride)
+    A.y[i] = s2fp8_elem(A.x[i], rb(i), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
+}
+
+static inline bool aligned16f(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+static int fq_grid(int64_t n) {
+  int64_t g = (n + kBlock * 4 * 4 - 1) / (kBlock * 4 * 4);
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  return (int)g;
+}
+
+static float host_max_value(int exp_bits, int man_bits) {
+  return qtorch_quant(FLT_MAX, 0u, exp_bits, man_bits, false);
+}
+
+static size_t s2_ws_bytes() { return 128 + sizeof(S2Partial) * (size_t)kS2GridCap; }
+
+}  // namespace smq
+
+using namespace smq;
+
+extern "C" {
+
+float smq_float_quant_max_value(int exp_bits, int man_bits) {
+  return host_max_value(exp_bits, man_bits);
+}
+
+int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int man_bits,
+                        int rounding, int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                        uint64_t offset, void* stream) {
+  if (n < 0 || (n > 0 && (!x || !y))) {
+    set_error("float_quant: bad tensor arguments");
+    return SMQ_ERR_INVALID;
+  }
+  if (exp_bits < 2 || exp_bits > 8 || man_bits < 0 || man_bits > 22) {
+    set_error("float_quant: exp_bits in [2,8] and man_bits in [0,22] required (got %d,%d)",
+              exp_bits, man_bits);
+    return SMQ_ERR_INVALID;
+  }
+  if (rounding != SMQ_ROUND_NEAREST && rounding != SMQ_ROUND_STOCHASTIC) {
+    set_error("float_quant: rounding must be SMQ_ROUND_NEAREST or SMQ_ROUND_STOCHASTIC");
+    return SMQ_ERR_INVALID;
+  }
+  if (n == 0) return SMQ_OK;
+  FQArgs A;
+  A.x = x;
+  A.y = y;
+  A.n = n;
+  A.rand_bits = rand_bits;
+  A.key = rng_key(seed);
+  A.offset = offset;
+  A.exp_bits = exp_bits;
+  A.man_bits = man_bits;
+  A.check_inf = check_inf;
+  A.max_value = host_max_value(exp_bits, man_bits);
+  const bool sr = rounding == SMQ_ROUND_STOCHASTIC;
+  const bool rarr = sr && rand_bits != nullptr;
+  const bool vec = aligned16f(x) && aligned16f(y) && (!rarr || aligned16f(rand_bits));
+  const int grid = fq_grid(n);
+  hipStream_t st = (hipStream_t)stream;
+#define SMQ_FQ(S, R, V) \
+  hipLaunchKernelGGL((float_quant_kernel<S, R, V>), dim3(grid), dim3(kBlock), 0, st, A)
+  if (!sr) {
+    if (vec) SMQ_FQ(false, false, true); else SMQ_FQ(false, false, false);
+  } else if (rarr) {
+    if (vec) SMQ_FQ(true, true, true); else SMQ_FQ(true, true, false);
+  } else {
+    if (vec) SMQ_FQ(true, false, true); else SMQ_FQ(true, false, false);
+  }
+#undef SMQ_FQ
+  return check_launch("float_quant_kernel");
+}
+
+size_t smq_s2fp8_workspace_bytes(int64_t n) {
+  (void)n;
+  return s2_ws_bytes();
+}
+
+int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
+                            const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
+                            const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
+                            void* stream) {
+  if (n < 1 || !x || !y) {
+    set_error("s2fp8: n >= 1 and non-NULL x, y required");
+    return SMQ_ERR_INVALID;
+  }
+  if (!ws || ws_bytes < s2_ws_bytes()) {
+    set_error("s2fp8: workspace too small: need %zu bytes", s2_ws_bytes());
+    return SMQ_ERR_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  char* base = (char*)ws;
+  SmqS2fp8Stats* hdr = (SmqS2fp8Stats*)base;
+  uint32_t* counter = (uint32_t*)(base + 64);
+  S2Partial* partials = (S2Partial*)(base + 128);
+  if (stats_in) {
+    hipLaunchKernelGGL(s2fp8_derive_kernel, dim3(1), dim3(64), 0, st, stats_in, hdr);
+  } else {
+    const int grid = fq_grid(n);
+    hipLaunchKernelGGL(s2fp8_stats_kernel, dim3(grid), dim3(kBlock), 0, st, x, n,
+                       aligned16f(x) ? 1 : 0, partials, counter, hdr);
+  }
+  int rc = check_launch("s2fp8_stats_kernel");
+  if (rc) return rc;
+  S2Args A;
+  A.x = x;
+  A.y = y;
+  A.n = n;
+  A.rand_bits = rand_bits;
+  A.st = hdr;
+  A.key = rng_key(seed);
+  A.offset = offset;
+  A.check_inf = check_inf;
+  A.max_value = host_max_value(5, 2);
+  const bool rarr = rand_bits != nullptr;
+  const bool vec = aligned16f(x) && aligned16f(y);
+  const int grid = fq_grid(n);
+  if (rarr) {
+    if (vec) hipLaunchKernelGGL((s2fp8_apply_kernel<true, true>), dim3(grid), dim3(kBlock), 0, st, A);
+    else hipLaunchKernelGGL((s2fp8_apply_kernel<true, false>), dim3(grid), dim3(kBlock), 0, st, A);
+  } else {
+    if (vec) hipLaunchKernelGGL((s2fp8_apply_kernel<false, true>), dim3(grid), dim3(kBlock), 0, st, A);
+    else hipLaunchKernelGGL((s2fp8_apply_kernel<false, false>), dim3(grid), dim3(kBlock), 0, st, A);
+  }
+  return check_launch("s2fp8_apply_kernel");
+}
+
+}  // extern "C"

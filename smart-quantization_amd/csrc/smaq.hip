@@ -1,0 +1,560 @@
+// smaq.hip — SmaQ compress->decompress round trip for gfx950 (MI355X).
+//
+// Reference: smart_compress/compress/smart.py:110-190 (SmartFP.__call__). The reference issues
+// ~24 ATen kernels and one host sync per call; here a call is two launches and no sync:
+//
+//   smaq_stats_kernel  one HBM read (4 B/elem): shifted fp64 sums (+ fp32 min/max in range-std
+//                      mode) per workgroup; the last workgroup to arrive reduces the partials in a
+//                      fixed order and writes SmqSmaqStats (mean, std, std==0->1, clamp) into the
+//                      workspace header.                            smart.py:130-134, 100-108, 151-152
+//   smaq_apply_kernel  read + write (8 B/elem), float4 (dwordx4) coalesced streams, per element:
+//                      z-score, main/outlier split, N-bit scale, stochastic rounding from the
+//                      counter-based RNG (or trunc), de-quantisation, all_positive.  smart.py:154-182
+//
+// Sampled statistics (smart.py:86-91) need no stats launch: every workgroup of the apply kernel
+// gathers the k <= 64 sampled elements itself (L2-resident after the first workgroup) and reduces
+// them in the same fixed order, so the whole call is ONE launch of 8 B/elem.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "smq_common.h"
+#include "smaq_elem.h"
+
+namespace smq {
+
+// ------------------------------------------------------------------------------------------------
+// error reporting
+// ------------------------------------------------------------------------------------------------
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: HIP launch failed: %s", what, hipGetErrorString(e));
+    return SMQ_ERR_LAUNCH;
+  }
+  return SMQ_OK;
+}
+
+static int grid_for(int64_t work_items, int per_block_items, int cap) {
+  int64_t g = (work_items + per_block_items - 1) / per_block_items;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// Persistent-ish grid caps: 256 CUs x 8 workgroups of 256 threads.
+constexpr int kStatsGridCap = 2048;
+constexpr int kApplyGridCap = 2048;
+constexpr int kUnroll = 4;  // float4 loads in flight per thread per iteration
+
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+template <bool RANGE>
+__global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const float* __restrict__ x, int64_t n,
+                                                            int vec, FinalizeArgs fin,
+                                                            StatPartial* __restrict__ partials,
+                                                            uint32_t* counter,
+                                                            SmqSmaqStats* out) {
+  __shared__ uint32_t arrive_slot;
+  // Shift = median of three fixed elements: keeps sum(x-K)^2 - (sum(x-K))^2/n well conditioned
+  // unless the mean is > 2^14 standard deviations away from all three.
+  const float k0 = x[0], k1 = x[n >> 1], k2 = x[n - 1];
+  const float kmed = fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));
+  const double shift = (double)kmed;
+
+  StatAcc acc;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int64_t done = 0;
+  if (vec) {
+    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+    const int64_t nv = n >> 2;
+    for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
+      float4 v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = load_nt(x4 + i + u * stride);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        acc.add<RANGE>(v[u].x, shift);
+        acc.add<RANGE>(v[u].y, shift);
+        acc.add<RANGE>(v[u].z, shift);
+        acc.add<RANGE>(v[u].w, shift);
+      }
+    }
+    for (; i < nv; i += stride) {
+      const float4 v = x4[i];
+      acc.add<RANGE>(v.x, shift);
+      acc.add<RANGE>(v.y, shift);
+      acc.add<RANGE>(v.z, shift);
+      acc.add<RANGE>(v.w, shift);
+    }
+    done = nv << 2;
+    i = done + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  }
+  for (; i < n; i += stride) acc.add<RANGE>(x[i], shift);
+
+  block_reduce_stats<RANGE>(acc);
+  if (threadIdx.x == 0) {
+    StatPartial p;
+    p.s1 = acc.s1;
+    p.s2 = acc.s2;
+    p.mn = acc.mn;
+    p.mx = acc.mx;
+    p.cnt = 0;
+    partials[blockIdx.x] = p;
+  }
+  const uint32_t prev = block_arrive(counter, &arrive_slot);
+  if (prev != gridDim.x - 1) return;
+
+  // Last workgroup: ordered reduction of all partials (deterministic for a given n).
+  block_acquire();
+  StatAcc tot;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
+    const StatPartial p = partials[b];
+    tot.s1 += p.s1;
+    tot.s2 += p.s2;
+    if (RANGE) {
+      tot.mn = fminf(tot.mn, p.mn);
+      tot.mx = fmaxf(tot.mx, p.mx);
+    }
+  }
+  block_reduce_stats<RANGE>(tot);
+  if (threadIdx.x == 0) {
+    finalize_stats<RANGE>(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, fin, out);
+    *counter = 0u;  // leave the workspace ready for the next call
+  }
+}
+
+struct ApplyArgs {
+  const float* x;
+  float* y;
+  int64_t n;
+  const float* uniforms;
+  const SmqSmaqStats* stats;     // workspace header or injected
+  SmqSmaqStats* ws_stats;        // outlier count destination
+  float thr, r_main, r_out, clamp_lo, clamp_hi, range_coef;
+  uint32_t key;
+  int all_pos;
+  int count;
+  int use_range;
+  int k;                         // sampled mode
+  uint64_t offset;
+  const float* bn_gamma;         // BN variant
+  const float* bn_beta;
+  int64_t bn_channels, bn_inner;
+  int64_t sample_idx[SMQ_MAX_SAMPLES];
+};
+
+template <bool BN>
+__device__ __forceinline__ BnTerm bn_term(const ApplyArgs& A, int64_t e) {
+  if (!BN) return BnTerm{1.0f, 0.0f};
+  const int64_t ch = (e / A.bn_inner) % A.bn_channels;
+  return BnTerm{A.bn_gamma[ch], A.bn_beta[ch]};
+}
+
+// Sampled statistics (smart.py:86-91): mean and biased std (or range-std) of k gathered elements,
+// computed by wave 0 of every workgroup in the same order -> identical in all workgroups.
+__device__ __forceinline__ void sampled_stats(const ApplyArgs& A, SmqSmaqStats* sh) {
+  if (threadIdx.x < kWave) {
+    const int lane = threadIdx.x;
+    const bool valid = lane < A.k;
+    const float v = valid ? A.x[A.sample_idx[lane]] : 0.0f;
+    const double kd = (double)A.k;
+    const double mean = wave_sum(valid ? (double)v : 0.0) / kd;
+    const double dv = valid ? ((double)v - mean) : 0.0;
+    const double m2 = wave_sum(dv * dv);
+    const float mn = wave_min(valid ? v : INFINITY);
+    const float mx = wave_max(valid ? v : -INFINITY);
+    if (lane == 0) {
+      FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef};
+      // finalize_stats expects shifted sums; pass shift = mean, s1 = 0, s2 = m2.
+      if (A.use_range)
+        finalize_stats<true>(0.0, m2, mn, mx, A.k, mean, true, f, sh);
+      else
+        finalize_stats<false>(0.0, m2, mn, mx, A.k, mean, true, f, sh);
+    }
+  }
+  __syncthreads();
+}
+
+template <int SRC, int RM, bool VEC, bool BN>
+__global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
+  __shared__ SmqSmaqStats sh_stats;
+  __shared__ unsigned long long sh_cnt[kBlock / kWave];
+  ElemConsts c;
+  if (SRC == SMQ_STATS_SAMPLED) {
+    sampled_stats(A, &sh_stats);
+    c.mean = sh_stats.mean;
+    c.sd = sh_stats.std_dev;
+    c.sc = sh_stats.std_clamped;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      A.ws_stats->mean = sh_stats.mean;
+      A.ws_stats->std_dev = sh_stats.std_dev;
+      A.ws_stats->std_clamped = sh_stats.std_clamped;
+      A.ws_stats->raw_std = sh_stats.raw_std;
+      A.ws_stats->min_val = sh_stats.min_val;
+      A.ws_stats->max_val = sh_stats.max_val;
+      A.ws_stats->n_used = sh_stats.n_used;
+    }
+  } else {
+    c.mean = A.stats->mean;
+    c.sd = A.stats->std_dev;
+    c.sc = A.stats->std_clamped;
+  }
+  c.thr = A.thr;
+  c.nthr = -A.thr;
+  c.zh = 0.0f * c.nthr;
+  c.zl = 0.0f * c.thr;
+  c.r_main = A.r_main;
+  c.r_out = A.r_out;
+  const bool all_pos = A.all_pos != 0;
+
+  unsigned long long n_out = 0;
+  const int64_t n = A.n;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int64_t vec_end = 0;
+  if (VEC) {
+    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
+    float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
+    const float4* __restrict__ u4 = reinterpret_cast<const float4*>(A.uniforms);
+    const int64_t nv = n >> 2;
+    auto body = [&](int64_t j, const float4& v, const float4& uu) {
+      float4 o;
+      bool b0, b1, b2, b3;
+      float u0, u1, u2, u3;
+      if (RM == kRoundHash) {
+        const uint64_t ctr = A.offset + ((uint64_t)j << 2);
+        u0 = u32_to_unit(rng_u32(A.key, ctr));
+        u1 = u32_to_unit(rng_u32(A.key, ctr + 1));
+        u2 = u32_to_unit(rng_u32(A.key, ctr + 2));
+        u3 = u32_to_unit(rng_u32(A.key, ctr + 3));
+      } else {
+        u0 = uu.x; u1 = uu.y; u2 = uu.z; u3 = uu.w;
+      }
+      o.x = smaq_elem<RM, BN>(v.x, u0, c, all_pos, b0, bn_term<BN>(A, 4 * j + 0));
+      o.y = smaq_elem<RM, BN>(v.y, u1, c, all_pos, b1, bn_term<BN>(A, 4 * j + 1));
+      o.z = smaq_elem<RM, BN>(v.z, u2, c, all_pos, b2, bn_term<BN>(A, 4 * j + 2));
+      o.w = smaq_elem<RM, BN>(v.w, u3, c, all_pos, b3, bn_term<BN>(A, 4 * j + 3));
+      n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
+      store_nt(y4 + j, o);
+    };
+    for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
+      float4 v[kUnroll], uu[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        v[u] = x4[i + u * stride];
+        if (RM == kRoundUniform) uu[u] = u4[i + u * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) body(i + u * stride, v[u], uu[u]);
+    }
+    for (; i < nv; i += stride) {
+      float4 uu = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (RM == kRoundUniform) uu = u4[i];
+      body(i, x4[i], uu);
+    }
+    vec_end = nv << 2;
+    i = vec_end + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  }
+  for (; i < n; i += stride) {
+    float u = 0.0f;
+    if (RM == kRoundHash) u = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)i));
+    if (RM == kRoundUniform) u = A.uniforms[i];
+    bool b;
+    A.y[i] = smaq_elem<RM, BN>(A.x[i], u, c, all_pos, b, bn_term<BN>(A, i));
+    n_out += (unsigned)b;
+  }
+
+  if (A.count) {  // outlier count for log_size (smart.py:184-188), one atomic per workgroup
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    double t = wave_sum((double)n_out);
+    if (lane == 0) sh_cnt[wave] = (unsigned long long)t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long s = sh_cnt[0] + sh_cnt[1] + sh_cnt[2] + sh_cnt[3];
+      if (s) atomicAdd(&A.ws_stats->n_outlier, s);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+static int validate_params(const SmqSmaqParams* p) {
+  if (!p) {
+    set_error("params is NULL");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->stats_source < 0 || p->stats_source > 2) {
+    set_error("stats_source %d invalid", p->stats_source);
+    return SMQ_ERR_INVALID;
+  }
+  return SMQ_OK;
+}
+
+static float range_coef_for(const SmqSmaqParams* p, int64_t n) {
+  if (p->range_std_coef > 0.0f) return p->range_std_coef;
+  // smart.py:101-106: C = 1 / sqrt(2.0 * log(tensor(n).float())) in fp32 ops
+  const float lg = logf((float)n);
+  const float t = 2.0f * lg;
+  return 1.0f / sqrtf(t);
+}
+
+static size_t stats_ws_bytes(int64_t n) {
+  (void)n;
+  return SmaqWsLayout::kPartials + sizeof(StatPartial) * (size_t)kStatsGridCap;
+}
+
+static int launch_stats(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,
+                        size_t ws_bytes, hipStream_t st) {
+  if (!ws || ws_bytes < stats_ws_bytes(n)) {
+    set_error("workspace too small: need %zu bytes, got %zu", stats_ws_bytes(n), ws_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  char* base = (char*)ws;
+  SmqSmaqStats* hdr = (SmqSmaqStats*)base;
+  uint32_t* counter = (uint32_t*)(base + SmaqWsLayout::kHeader);
+  StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
+  const int vec = aligned16(x) ? 1 : 0;
+  const int grid = grid_for(n, kBlock * 4 * kUnroll, kStatsGridCap);
+  FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n)};
+  if (p->use_range_std_dev)
+    hipLaunchKernelGGL(smaq_stats_kernel<true>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, fin,
+                       partials, counter, hdr);
+  else
+    hipLaunchKernelGGL(smaq_stats_kernel<false>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, fin,
+                       partials, counter, hdr);
+  return check_launch("smaq_stats_kernel");
+}
+
+template <int SRC, bool BN>
+static void launch_apply_src(const ApplyArgs& A, int rm, bool vec, int grid, hipStream_t st) {
+#define SMQ_APPLY(RMV, VECV) \
+  hipLaunchKernelGGL((smaq_apply_kernel<SRC, RMV, VECV, BN>), dim3(grid), dim3(kBlock), 0, st, A)
+  if (vec) {
+    if (rm == kRoundHash) SMQ_APPLY(kRoundHash, true);
+    else if (rm == kRoundUniform) SMQ_APPLY(kRoundUniform, true);
+    else SMQ_APPLY(kRoundTrunc, true);
+  } else {
+    if (rm == kRoundHash) SMQ_APPLY(kRoundHash, false);
+    else if (rm == kRoundUniform) SMQ_APPLY(kRoundUniform, false);
+    else SMQ_APPLY(kRoundTrunc, false);
+  }
+#undef SMQ_APPLY
+}
+
+static int launch_apply(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
+                        const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
+                        size_t ws_bytes, hipStream_t st) {
+  if (!ws || ws_bytes < SmaqWsLayout::kPartials) {
+    set_error("workspace too small: need >= %zu bytes", (size_t)SmaqWsLayout::kPartials);
+    return SMQ_ERR_WORKSPACE;
+  }
+  ApplyArgs A;
+  memset(&A, 0, sizeof(A));
+  A.x = x;
+  A.y = y;
+  A.n = n;
+  A.uniforms = uniforms;
+  A.ws_stats = (SmqSmaqStats*)ws;
+  A.stats = (p->stats_source == SMQ_STATS_INJECTED) ? stats_in : (const SmqSmaqStats*)ws;
+  A.thr = p->main_std_dev_threshold;
+  A.r_main = p->range_main;
+  A.r_out = p->range_outlier;
+  A.clamp_lo = p->clamp_lo;
+  A.clamp_hi = p->clamp_hi;
+  A.key = rng_key(p->seed);
+  A.offset = p->offset;
+  A.all_pos = p->all_positive;
+  A.count = p->count_outliers;
+  A.use_range = p->use_range_std_dev;
+  if (p->bn_gamma) {
+    if (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1) {
+      set_error("BN variant needs bn_beta, bn_channels >= 1 and bn_inner >= 1");
+      return SMQ_ERR_INVALID;
+    }
+    A.bn_gamma = p->bn_gamma;
+    A.bn_beta = p->bn_beta;
+    A.bn_channels = p->bn_channels;
+    A.bn_inner = p->bn_inner;
+  }
+  if (p->stats_source == SMQ_STATS_INJECTED && !stats_in) {
+    set_error("SMQ_STATS_INJECTED needs stats_in");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->stats_source == SMQ_STATS_SAMPLED) {
+    const int64_t k = p->num_samples < n ? p->num_samples : n;
+    if (k < 1 || k > SMQ_MAX_SAMPLES) {
+      set_error("sampled stats need 1 <= k <= %d, got %lld", SMQ_MAX_SAMPLES, (long long)k);
+      return SMQ_ERR_INVALID;
+    }
+    for (int j = 0; j < (int)k; ++j) {
+      if (p->sample_idx[j] < 0 || p->sample_idx[j] >= n) {
+        set_error("sample_idx[%d] = %lld out of range [0, %lld)", j, (long long)p->sample_idx[j],
+                  (long long)n);
+        return SMQ_ERR_INVALID;
+      }
+      A.sample_idx[j] = p->sample_idx[j];
+    }
+    A.k = (int)k;
+    A.range_coef = range_coef_for(p, k);
+  }
+  const int rm = !p->stochastic_rounding ? kRoundTrunc : (uniforms ? kRoundUniform : kRoundHash);
+  const bool vec = aligned16(x) && aligned16(y) && (rm != kRoundUniform || aligned16(uniforms));
+  if (p->count_outliers && p->stats_source != SMQ_STATS_WORKSPACE) {
+    if (hipMemsetAsync(&A.ws_stats->n_outlier, 0, sizeof(unsigned long long), st) != hipSuccess) {
+      set_error("hipMemsetAsync of the outlier counter failed");
+      return SMQ_ERR_LAUNCH;
+    }
+  }
+  const int grid = grid_for(n, kBlock * 4 * kUnroll, kApplyGridCap);
+  const bool bn = A.bn_gamma != nullptr;
+  switch (p->stats_source) {
+    case SMQ_STATS_WORKSPACE:
+      if (bn) launch_apply_src<SMQ_STATS_WORKSPACE, true>(A, rm, vec, grid, st);
+      else launch_apply_src<SMQ_STATS_WORKSPACE, false>(A, rm, vec, grid, st);
+      break;
+    case SMQ_STATS_SAMPLED:
+      if (bn) launch_apply_src<SMQ_STATS_SAMPLED, true>(A, rm, vec, grid, st);
+      else launch_apply_src<SMQ_STATS_SAMPLED, false>(A, rm, vec, grid, st);
+      break;
+    default:
+      if (bn) launch_apply_src<SMQ_STATS_INJECTED, true>(A, rm, vec, grid, st);
+      else launch_apply_src<SMQ_STATS_INJECTED, false>(A, rm, vec, grid, st);
+      break;
+  }
+  return check_launch("smaq_apply_kernel");
+}
+
+static int check_tensor_args(const float* x, const float* y, int64_t n) {
+  if (n < 1) {
+    set_error("n must be >= 1 (got %lld); the caller passes n < min_size through", (long long)n);
+    return SMQ_ERR_INVALID;
+  }
+  if (!x || !y) {
+    set_error("x and y must be device pointers");
+    return SMQ_ERR_INVALID;
+  }
+  return SMQ_OK;
+}
+
+}  // namespace smq
+
+using namespace smq;
+
+extern "C" {
+
+int smq_abi_version(void) { return SMQ_ABI_VERSION; }
+const char* smq_last_error(void) { return g_err; }
+
+uint32_t smq_rng_u32(uint64_t seed, uint64_t counter) { return rng_u32(rng_key(seed), counter); }
+
+void smq_smaq_params_init(SmqSmaqParams* p) {
+  memset(p, 0, sizeof(*p));
+  smq_smaq_params_set(p, 6, 8, 1.0, 2.5, 32);
+  p->stochastic_rounding = 1;
+  p->num_samples = 16;
+  p->stats_source = SMQ_STATS_WORKSPACE;
+}
+
+int smq_smaq_params_set(SmqSmaqParams* p, int num_bits_main, int num_bits_outlier,
+                        double main_thr, double outlier_thr, int precision) {
+  if (!p) {
+    set_error("params is NULL");
+    return SMQ_ERR_INVALID;
+  }
+  if (main_thr == 0.0 || outlier_thr - main_thr == 0.0) {
+    set_error("thresholds give a division by zero (smart.py:72-78)");
+    return SMQ_ERR_INVALID;
+  }
+  p->num_bits_main = num_bits_main;
+  p->num_bits_outlier = num_bits_outlier;
+  p->main_std_dev_threshold = (float)main_thr;
+  // Python: ((2 ** (bits - 2)) - 1) / threshold, in double, rounded to fp32 when used.
+  p->range_outlier = (float)((pow(2.0, num_bits_outlier - 2) - 1.0) / (outlier_thr - main_thr));
+  p->range_main = (float)((pow(2.0, num_bits_main - 2) - 1.0) / main_thr);
+  p->clamp_lo = precision == 16 ? 1e-4f : 1e-38f;
+  p->clamp_hi = precision == 16 ? 1e4f : 1e38f;
+  return SMQ_OK;
+}
+
+int smq_smaq_draw_samples(SmqSmaqParams* p, int64_t n, int num_samples) {
+  if (!p || n < 1 || num_samples < 1) {
+    set_error("draw_samples: bad arguments");
+    return SMQ_ERR_INVALID;
+  }
+  const int64_t k = num_samples < n ? num_samples : n;
+  if (k > SMQ_MAX_SAMPLES) {
+    set_error("num_samples %d exceeds SMQ_MAX_SAMPLES", num_samples);
+    return SMQ_ERR_INVALID;
+  }
+  // Floyd's algorithm: k distinct indices, O(k^2), keyed off a stream separate from rounding.
+  const uint32_t key = rng_key(p->seed ^ 0xd1b54a32d192ed03ull);
+  uint64_t ctr = p->offset * 2;
+  int m = 0;
+  for (int64_t j = n - k; j < n; ++j) {
+    const uint64_t h = ((uint64_t)rng_u32(key, ctr) << 32) | rng_u32(key, ctr + 1);
+    ctr += 2;
+    int64_t t = (int64_t)(h % (uint64_t)(j + 1));
+    for (int q = 0; q < m; ++q)
+      if (p->sample_idx[q] == t) {
+        t = j;
+        break;
+      }
+    p->sample_idx[m++] = t;
+  }
+  p->num_samples = (int32_t)k;
+  return SMQ_OK;
+}
+
+size_t smq_smaq_workspace_bytes(int64_t n) { return stats_ws_bytes(n); }
+
+int smq_smaq_stats_f32(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,
+                       size_t ws_bytes, void* stream) {
+  int rc = validate_params(p);
+  if (rc) return rc;
+  if (n < 1 || !x) {
+    set_error("stats: n must be >= 1 and x non-NULL");
+    return SMQ_ERR_INVALID;
+  }
+  return launch_stats(x, n, p, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int smq_smaq_apply_f32(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
+                       const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
+                       size_t ws_bytes, void* stream) {
+  int rc = validate_params(p);
+  if (rc) return rc;
+  rc = check_tensor_args(x, y, n);
+  if (rc) return rc;
+  return launch_apply(x, y, n, p, uniforms, stats_in, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int smq_smaq_roundtrip_f32(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
+                           const float* uniforms, void* ws, size_t ws_bytes, void* stream) {
+  int rc = validate_params(p);
+  if (rc) return rc;
+  rc = check_tensor_args(x, y, n);
+  if (rc) return rc;
+  if (p->stats_source == SMQ_STATS_WORKSPACE) {
+    rc = launch_stats(x, n, p, ws, ws_bytes, (hipStream_t)stream);
+    if (rc) return rc;
+  } else if (p->stats_source == SMQ_STATS_INJECTED) {
+    set_error("roundtrip: use smq_smaq_apply_f32 for injected statistics");
+    return SMQ_ERR_INVALID;
+  }
+  return launch_apply(x, y, n, p, uniforms, nullptr, ws, ws_bytes, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,141 @@
+// smaq_elem.h — SmaQ statistics accumulation/finalisation and the per-element transform, shared by
+// the single-tensor (smaq.hip) and multi-tensor (smaq_multi.hip) kernels.
+// Reference: smart_compress/compress/smart.py:100-108, 130-134, 151-182.
+#pragma once
+
+#include <math.h>
+
+#include "smq_common.h"
+
+namespace smq {
+
+// ------------------------------------------------------------------------------------------------
+// statistics
+// ------------------------------------------------------------------------------------------------
+struct StatAcc {
+  double s1 = 0.0, s2 = 0.0;
+  float mn = INFINITY, mx = -INFINITY;
+  template <bool RANGE>
+  __device__ __forceinline__ void add(float v, double shift) {
+    const double d = (double)v - shift;
+    s1 += d;
+    s2 = fma(d, d, s2);
+    if (RANGE) {
+      mn = fminf(mn, v);
+      mx = fmaxf(mx, v);
+    }
+  }
+};
+
+// Workgroup reduction of (s1, s2, mn, mx); result valid in thread 0.
+template <bool RANGE>
+__device__ __forceinline__ void block_reduce_stats(StatAcc& a) {
+  __shared__ double sh1[kBlock / kWave], sh2[kBlock / kWave];
+  __shared__ float shmn[kBlock / kWave], shmx[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  a.s1 = wave_sum(a.s1);
+  a.s2 = wave_sum(a.s2);
+  if (RANGE) {
+    a.mn = wave_min(a.mn);
+    a.mx = wave_max(a.mx);
+  }
+  if (lane == 0) {
+    sh1[wave] = a.s1;
+    sh2[wave] = a.s2;
+    shmn[wave] = a.mn;
+    shmx[wave] = a.mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.s1 = ((sh1[0] + sh1[1]) + (sh1[2] + sh1[3]));
+    a.s2 = ((sh2[0] + sh2[1]) + (sh2[2] + sh2[3]));
+    if (RANGE) {
+      a.mn = fminf(fminf(shmn[0], shmn[1]), fminf(shmn[2], shmn[3]));
+      a.mx = fmaxf(fmaxf(shmx[0], shmx[1]), fmaxf(shmx[2], shmx[3]));
+    }
+  }
+  __syncthreads();
+}
+
+struct FinalizeArgs {
+  float clamp_lo, clamp_hi, range_coef;
+};
+
+// mean / std from shifted sums -> SmqSmaqStats (smart.py:130-134, 100-108, 151-152, 154).
+template <bool RANGE>
+__device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, float mx, int64_t n,
+                                               double shift, bool biased, FinalizeArgs f,
+                                               SmqSmaqStats* out) {
+  const double nd = (double)n;
+  const double mean = shift + s1 / nd;
+  float sd;
+  if (RANGE) {
+    const float range = mx - mn;  // data.max() - data.min()
+    sd = range * f.range_coef;    // range_ * C
+  } else {
+    double var = (s2 - s1 * (s1 / nd)) / (biased ? nd : (nd - 1.0));
+    if (var < 0.0) var = 0.0;
+    sd = (float)sqrt(var);
+  }
+  const float std_dev = (sd == 0.0f) ? 1.0f : sd;  // smart.py:151-152
+  float sc = std_dev < f.clamp_lo ? f.clamp_lo : std_dev;  // .clamp(*clamped_range)
+  sc = sc > f.clamp_hi ? f.clamp_hi : sc;
+  out->mean = (float)mean;
+  out->std_dev = std_dev;
+  out->std_clamped = sc;
+  out->raw_std = sd;
+  out->min_val = mn;
+  out->max_val = mx;
+  out->n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
+  out->n_outlier = 0ull;
+}
+
+// ------------------------------------------------------------------------------------------------
+// element transform
+// ------------------------------------------------------------------------------------------------
+struct ElemConsts {
+  float mean, sd, sc;     // mean, std (after ==0 rule), clamped std
+  float thr, nthr;        // fp32(T_m), -fp32(T_m)
+  float zh, zl;           // 0 * -T_m, 0 * T_m  (the bool*float zero terms, smart.py:159-161)
+  float r_main, r_out;    // ranges
+};
+
+enum RoundMode { kRoundHash = 0, kRoundUniform = 1, kRoundTrunc = 2 };
+
+// One element of smart.py:154-182. Each statement is one rounded fp32 op of the reference.
+// Per-channel BatchNorm fold (smart.py:144-149 before, 174-179 after); scale = gamma[c].
+struct BnTerm {
+  float gamma, beta;
+};
+
+// One element of smart.py:154-182. Each statement is one rounded fp32 op of the reference.
+template <int RM, bool BN = false>
+__device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c, bool all_pos,
+                                           bool& is_outlier, BnTerm bn = BnTerm{1.0f, 0.0f}) {
+  if (BN) v = (v - bn.beta) / bn.gamma;                 // (data - beta) / gamma
+  const float z = (v - c.mean) / c.sc;                  // (data - mean) / std.clamp(...)
+  const bool hi = z > c.thr;                            // is_outlier_higher
+  const bool lo = z < c.nthr;                           // is_outlier_lower
+  const bool o = hi | lo;                               // is_outlier
+  const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);  // scalars
+  const float r = o ? c.r_out : c.r_main;               // ranges
+  const float d = (z + a) * r;
+  float q;
+  if (RM == kRoundTrunc) {
+    q = truncf(d);
+  } else {
+    const float f = floorf(d);                          // _round_stochastic, smart.py:93-98
+    const float fr = d - f;
+    float t = (fr - u) + 0.5f;
+    t = (t < 0.0f) ? 0.0f : t;                          // F.relu
+    q = f + __builtin_rintf(t);                         // .round() = half to even
+  }
+  float out = (q / r) - a;
+  out = (out * c.sd) + c.mean;
+  if (BN) out = (out * bn.gamma) + bn.beta;             // (data * gamma) + beta
+  if (all_pos) out = (out < 0.0f) ? 0.0f : out;         // clamp_min(0.0)
+  is_outlier = o;
+  return out;
+}
+
+}  // namespace smq

@@ -1,0 +1,323 @@
+// smaq_multi.hip — SmaQ over a list of tensors in two launches (gfx950).
+//
+// Reference: the per-parameter SmartFP calls of smart_compress/util/pytorch/optimizer.py:79-127
+// (grads, weights, momenta), each of which runs smart.py:110-190 separately (~24 ATen launches
+// + 1 host sync per tensor; a ResNet-34 step has 148 such tensors, median 256 elements).
+//
+// Design: the tensors are cut into fixed chunks (kChunk elements); one workgroup per chunk.
+//   launch 1 (stats): per-chunk shifted fp64 sums; a tensor with one chunk finalises in place,
+//            a larger tensor's last-arriving chunk reduces that tensor's partials in chunk order.
+//   launch 2 (apply): per chunk, the tensor's SmqSmaqStats + the element transform of smaq.hip,
+//            RNG counter = params.offset + desc.rng_offset + element index (so a multi call equals
+//            the sequence of single-tensor calls at those offsets, and a plan is reusable).
+// y may alias x: every element is read once by the apply launch before it is written.
+#include <stdlib.h>
+#include <string.h>
+
+#include "smq_common.h"
+#include "smaq_elem.h"
+
+namespace smq {
+
+constexpr int64_t kChunk = 32768;  // elements per workgroup (128 KiB of fp32)
+
+struct MultiHeader {
+  int32_t count;
+  int32_t n_chunks;
+  int64_t chunk;
+  int64_t reserved[2];
+};
+
+struct ChunkDesc {
+  int32_t tensor;
+  int32_t first_chunk;  // global index of the tensor's first chunk
+  int32_t n_chunks;     // chunks of this tensor
+  int32_t pad;
+  int64_t begin, end;   // element range within the tensor
+};
+
+static_assert(sizeof(MultiHeader) == 32, "plan header");
+static_assert(sizeof(ChunkDesc) == 32, "chunk desc");
+
+struct MultiArgs {
+  const MultiHeader* hdr;
+  const SmqTensorDesc* descs;
+  const ChunkDesc* chunks;
+  SmqSmaqStats* stats;       // [count]
+  uint32_t* counters;        // [count]
+  StatPartial* partials;     // [n_chunks]
+  float thr, r_main, r_out, clamp_lo, clamp_hi;
+  uint32_t key;
+  uint64_t offset;           // params.offset; tensor t draws from offset + desc.rng_offset + i
+  int sr;
+  int count_outliers;
+};
+
+__global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
+  __shared__ uint32_t slot;
+  const ChunkDesc ch = A.chunks[blockIdx.x];
+  const SmqTensorDesc d = A.descs[ch.tensor];
+  const float* __restrict__ x = d.x;
+  const int64_t n = d.n;
+  const float k0 = x[0], k1 = x[n >> 1], k2 = x[n - 1];
+  const double shift = (double)fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));
+  StatAcc acc;
+  int64_t i = ch.begin + threadIdx.x * 4;
+  if (((uintptr_t)x & 15u) == 0) {
+    for (; i + 3 < ch.end; i += kBlock * 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + i);
+      acc.add<false>(v.x, shift);
+      acc.add<false>(v.y, shift);
+      acc.add<false>(v.z, shift);
+      acc.add<false>(v.w, shift);
+    }
+    for (; i < ch.end; ++i) acc.add<false>(x[i], shift);  // ragged tail: one thread, <4 elems
+  } else {
+    for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) acc.add<false>(x[j], shift);
+  }
+  block_reduce_stats<false>(acc);
+  const FinalizeArgs fin{A.clamp_lo, A.clamp_hi, 0.0f};
+  if (ch.n_chunks == 1) {
+    if (threadIdx.x == 0)
+      finalize_stats<false>(acc.s1, acc.s2, 0.f, 0.f, n, shift, false, fin, &A.stats[ch.tensor]);
+    return;
+  }
+  if (threadIdx.x == 0) {
+    StatPartial p;
+    p.s1 = acc.s1;
+    p.s2 = acc.s2;
+    p.mn = 0.f;
+    p.mx = 0.f;
+    p.cnt = 0;
+    A.partials[blockIdx.x] = p;
+  }
+  const uint32_t prev = block_arrive(&A.counters[ch.tensor], &slot);
+  if (prev != (uint32_t)ch.n_chunks - 1) return;
+  block_acquire();
+  StatAcc tot;
+  for (int b = threadIdx.x; b < ch.n_chunks; b += kBlock) {
+    const StatPartial p = A.partials[ch.first_chunk + b];
+    tot.s1 += p.s1;
+    tot.s2 += p.s2;
+  }
+  block_reduce_stats<false>(tot);
+  if (threadIdx.x == 0) {
+    finalize_stats<false>(tot.s1, tot.s2, 0.f, 0.f, n, shift, false, fin, &A.stats[ch.tensor]);
+    A.counters[ch.tensor] = 0u;
+  }
+}
+
+template <bool SR>
+__global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
+  __shared__ unsigned long long sh_cnt[kBlock / kWave];
+  const ChunkDesc ch = A.chunks[blockIdx.x];
+  const SmqTensorDesc d = A.descs[ch.tensor];
+  const SmqSmaqStats* st = &A.stats[ch.tensor];
+  ElemConsts c;
+  c.mean = st->mean;
+  c.sd = st->std_dev;
+  c.sc = st->std_clamped;
+  c.thr = A.thr;
+  c.nthr = -A.thr;
+  c.zh = 0.0f * c.nthr;
+  c.zl = 0.0f * c.thr;
+  c.r_main = A.r_main;
+  c.r_out = A.r_out;
+  const bool all_pos = d.all_positive != 0;
+  const float* __restrict__ x = d.x;
+  float* y = d.y;  // may alias x
+  unsigned long long n_out = 0;
+  constexpr int RM = SR ? kRoundHash : kRoundTrunc;
+  int64_t i = ch.begin + threadIdx.x * 4;
+  if ((((uintptr_t)x | (uintptr_t)y) & 15u) == 0) {
+    for (; i + 3 < ch.end; i += kBlock * 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + i);
+      const uint64_t ctr = A.offset + d.rng_offset + (uint64_t)i;
+      float u0 = 0.f, u1 = 0.f, u2 = 0.f, u3 = 0.f;
+      if (SR) {
+        u0 = u32_to_unit(rng_u32(A.key, ctr));
+        u1 = u32_to_unit(rng_u32(A.key, ctr + 1));
+        u2 = u32_to_unit(rng_u32(A.key, ctr + 2));
+        u3 = u32_to_unit(rng_u32(A.key, ctr + 3));
+      }
+      bool b0, b1, b2, b3;
+      float4 o;
+      o.x = smaq_elem<RM>(v.x, u0, c, all_pos, b0);
+      o.y = smaq_elem<RM>(v.y, u1, c, all_pos, b1);
+      o.z = smaq_elem<RM>(v.z, u2, c, all_pos, b2);
+      o.w = smaq_elem<RM>(v.w, u3, c, all_pos, b3);
+      n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
+      *reinterpret_cast<float4*>(y + i) = o;
+    }
+    for (; i < ch.end; ++i) {
+      const float u = SR ? u32_to_unit(rng_u32(A.key, A.offset + d.rng_offset + (uint64_t)i)) : 0.f;
+      bool b;
+      y[i] = smaq_elem<RM>(x[i], u, c, all_pos, b);
+      n_out += (unsigned)b;
+    }
+  } else {
+    for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) {
+      const float u = SR ? u32_to_unit(rng_u32(A.key, A.offset + d.rng_offset + (uint64_t)j)) : 0.f;
+      bool b;
+      y[j] = smaq_elem<RM>(x[j], u, c, all_pos, b);
+      n_out += (unsigned)b;
+    }
+  }
+  if (A.count_outliers) {
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    const double t = wave_sum((double)n_out);
+    if (lane == 0) sh_cnt[wave] = (unsigned long long)t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long s = sh_cnt[0] + sh_cnt[1] + sh_cnt[2] + sh_cnt[3];
+      if (s) atomicAdd((unsigned long long*)&A.stats[ch.tensor].n_outlier, s);
+    }
+  }
+}
+
+static int64_t chunks_of(int64_t n) { return (n + kChunk - 1) / kChunk; }
+
+struct PlanSizes {
+  size_t hdr, descs, chunks, total;
+  int64_t n_chunks;
+};
+
+static bool plan_sizes(const int64_t* sizes, int count, PlanSizes* ps) {
+  int64_t nc = 0;
+  for (int t = 0; t < count; ++t) {
+    if (sizes[t] < 1) return false;
+    nc += chunks_of(sizes[t]);
+  }
+  ps->n_chunks = nc;
+  ps->hdr = sizeof(MultiHeader);
+  ps->descs = ((sizeof(SmqTensorDesc) * (size_t)count) + 31) & ~(size_t)31;
+  ps->chunks = sizeof(ChunkDesc) * (size_t)nc;
+  ps->total = ps->hdr + ps->descs + ps->chunks;
+  return true;
+}
+
+}  // namespace smq
+
+using namespace smq;
+
+extern "C" {
+
+size_t smq_smaq_multi_plan_bytes(const int64_t* sizes, int count) {
+  PlanSizes ps;
+  if (!sizes || count < 1 || !plan_sizes(sizes, count, &ps)) return 0;
+  return ps.total;
+}
+
+int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_plan,
+                              size_t plan_bytes) {
+  if (!descs || count < 1 || !host_plan) {
+    set_error("multi_plan_build: bad arguments");
+    return SMQ_ERR_INVALID;
+  }
+  int64_t* sizes = (int64_t*)malloc(sizeof(int64_t) * (size_t)count);
+  for (int t = 0; t < count; ++t) {
+    sizes[t] = descs[t].n;
+    if (!descs[t].x || !descs[t].y || descs[t].n < 1) {
+      free(sizes);
+      set_error("multi_plan_build: tensor %d has NULL pointer or n < 1", t);
+      return SMQ_ERR_INVALID;
+    }
+  }
+  PlanSizes ps;
+  plan_sizes(sizes, count, &ps);
+  free(sizes);
+  if (plan_bytes < ps.total) {
+    set_error("multi_plan_build: plan buffer too small (%zu < %zu)", plan_bytes, ps.total);
+    return SMQ_ERR_INVALID;
+  }
+  if (ps.n_chunks > 0x7fffffffLL) {
+    set_error("multi_plan_build: too many chunks");
+    return SMQ_ERR_INVALID;
+  }
+  char* base = (char*)host_plan;
+  memset(base, 0, ps.total);
+  MultiHeader* h = (MultiHeader*)base;
+  h->count = count;
+  h->n_chunks = (int32_t)ps.n_chunks;
+  h->chunk = kChunk;
+  memcpy(base + ps.hdr, descs, sizeof(SmqTensorDesc) * (size_t)count);
+  ChunkDesc* ch = (ChunkDesc*)(base + ps.hdr + ps.descs);
+  int32_t g = 0;
+  for (int t = 0; t < count; ++t) {
+    const int64_t nc = chunks_of(descs[t].n);
+    const int32_t first = g;
+    for (int64_t c = 0; c < nc; ++c, ++g) {
+      ch[g].tensor = t;
+      ch[g].first_chunk = first;
+      ch[g].n_chunks = (int32_t)nc;
+      ch[g].begin = c * kChunk;
+      ch[g].end = (c + 1) * kChunk < descs[t].n ? (c + 1) * kChunk : descs[t].n;
+    }
+  }
+  return SMQ_OK;
+}
+
+size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count) {
+  PlanSizes ps;
+  if (!sizes || count < 1 || !plan_sizes(sizes, count, &ps)) return 0;
+  const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
+  const size_t counters = ((sizeof(uint32_t) * (size_t)count) + 63) & ~(size_t)63;
+  return stats + counters + sizeof(StatPartial) * (size_t)ps.n_chunks;
+}
+
+}  // extern "C"
+
+extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
+                                  const SmqSmaqParams* p, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  if (!dev_plan || !host_plan) {
+    set_error("multi: dev_plan and host_plan are required");
+    return SMQ_ERR_INVALID;
+  }
+  const MultiHeader* hh = (const MultiHeader*)host_plan;
+  const int count = hh->count;
+  const int n_chunks = hh->n_chunks;
+  if (!dev_plan || count < 1 || n_chunks < 1 || !p || !ws) {
+    set_error("multi: bad arguments");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->stats_source != SMQ_STATS_WORKSPACE || p->use_range_std_dev) {
+    set_error("multi: only full statistics (no sampled / range-std) are supported");
+    return SMQ_ERR_INVALID;
+  }
+  const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
+  const size_t counters = ((sizeof(uint32_t) * (size_t)count) + 63) & ~(size_t)63;
+  const size_t need = stats + counters + sizeof(StatPartial) * (size_t)n_chunks;
+  if (ws_bytes < need) {
+    set_error("multi: workspace too small: need %zu bytes, got %zu", need, ws_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  const char* pb = (const char*)dev_plan;
+  const size_t descs_bytes = ((sizeof(SmqTensorDesc) * (size_t)count) + 31) & ~(size_t)31;
+  MultiArgs A;
+  A.hdr = (const MultiHeader*)pb;
+  A.descs = (const SmqTensorDesc*)(pb + sizeof(MultiHeader));
+  A.chunks = (const ChunkDesc*)(pb + sizeof(MultiHeader) + descs_bytes);
+  char* wb = (char*)ws;
+  A.stats = (SmqSmaqStats*)wb;
+  A.counters = (uint32_t*)(wb + stats);
+  A.partials = (StatPartial*)(wb + stats + counters);
+  A.thr = p->main_std_dev_threshold;
+  A.r_main = p->range_main;
+  A.r_out = p->range_outlier;
+  A.clamp_lo = p->clamp_lo;
+  A.clamp_hi = p->clamp_hi;
+  A.key = rng_key(p->seed);
+  A.offset = p->offset;
+  A.sr = p->stochastic_rounding;
+  A.count_outliers = p->count_outliers;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(smaq_multi_stats_kernel, dim3(n_chunks), dim3(kBlock), 0, st, A);
+  int rc = check_launch("smaq_multi_stats_kernel");
+  if (rc) return rc;
+  if (A.sr)
+    hipLaunchKernelGGL(smaq_multi_apply_kernel<true>, dim3(n_chunks), dim3(kBlock), 0, st, A);
+  else
+    hipLaunchKernelGGL(smaq_multi_apply_kernel<false>, dim3(n_chunks), dim3(kBlock), 0, st, A);
+  return check_launch("smaq_multi_apply_kernel");
+}

@@ -1,0 +1,126 @@
+// smq_common.h — shared device/host helpers of libsmq (gfx950 only).
+//
+// Numerics contract: every fp32 operation of the reference's ATen op
+// chain is issued as its own IEEE-754 round-to-nearest operation in the same order. The library is
+// compiled with -ffp-contract=off so `a * b + c` never fuses into an FMA, and `/` lowers to the
+// correctly rounded v_div_scale / v_div_fmas / v_div_fixup sequence.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "smq.h"
+
+namespace smq {
+
+constexpr int kBlock = 256;  // 4 wave64 per workgroup
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------------------------
+// Counter-based RNG. Element i of a call draws from counter c = offset + i, so the value of an
+// element never depends on the launch geometry and the CPU oracle reproduces it bit for bit
+// (oracle/rng.py). One "lowbias32" finaliser (C. Wellons) = 2 v_mul_lo_u32 per element.
+// The 64-bit seed is folded into a 32-bit key once per launch on the host.
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t rng_key(uint64_t seed) {
+  return mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) ^ 0x9e3779b9U));
+}
+
+__host__ __device__ __forceinline__ uint32_t rng_u32(uint32_t key, uint64_t ctr) {
+  const uint32_t lo = (uint32_t)ctr;
+  const uint32_t hi = (uint32_t)(ctr >> 32);
+  return mix32(lo ^ ((hi << 16) | (hi >> 16)) ^ key);
+}
+
+// U[0,1) with 24 random bits, the resolution of torch.rand_like for fp32.
+__host__ __device__ __forceinline__ float u32_to_unit(uint32_t h) {
+  return (float)(h >> 8) * 5.9604644775390625e-08f;  // 2^-24
+}
+
+// ---------------------------------------------------------------------------------------------
+// 16-byte streaming accesses (global_load/store_dwordx4, optionally with the nt hint)
+// ---------------------------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 load_nt(const float4* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void store_nt(float4* p, const float4& v) {
+  f32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(p));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave64 / workgroup reductions
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Agent-scope release of this workgroup's plain stores, then an arrival on `counter`.
+// Returns the pre-increment value (same in every thread of the block).
+// Protocol: MI355X_MICROARCH.md §inter-workgroup visibility (producer: stores, vmcnt(0), barrier,
+// lane-0 release + asm vmcnt(0), relaxed agent atomic).
+__device__ __forceinline__ uint32_t block_arrive(uint32_t* counter, uint32_t* lds_slot) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *lds_slot = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return *lds_slot;
+}
+
+// Consumer side after the last arrival: one agent acquire per wave, then plain loads.
+__device__ __forceinline__ void block_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// Stats partial of one workgroup: shifted fp64 sums plus fp32 extrema.
+struct alignas(32) StatPartial {
+  double s1;  // sum (x - shift)
+  double s2;  // sum (x - shift)^2
+  float mn, mx;
+  int64_t cnt;
+};
+
+// Workspace layout of a single-tensor SmaQ call.
+struct SmaqWsLayout {
+  static constexpr size_t kHeader = 64;     // SmqSmaqStats
+  static constexpr size_t kCounter = 64;    // arrival counter (own 64-B line)
+  static constexpr size_t kPartials = 128;  // StatPartial[grid]
+};
+
+}  // namespace smq
+
+// Thread-local error reporting shared by all translation units.
+namespace smq {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace smq

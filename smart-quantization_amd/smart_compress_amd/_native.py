@@ -1,0 +1,234 @@
+"""ctypes binding of libsmq.so, the C-ABI declared in include/smq.h.
+
+This is the only place the Python host touches the native library. There is no fallback: if the
+library is missing or a device tensor is not on a ROCm GPU, the codecs raise. The structures below
+mirror include/smq.h field for field.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Dict, Tuple
+
+import torch
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "SMQ_LIB", os.path.join(os.path.dirname(_PKG_DIR), "lib", "libsmq.so")
+)
+
+SMQ_ABI_VERSION = 1
+SMQ_MAX_SAMPLES = 64
+SMQ_STATS_WORKSPACE = 0
+SMQ_STATS_SAMPLED = 1
+SMQ_STATS_INJECTED = 2
+SMQ_ROUND_NEAREST = 0
+SMQ_ROUND_STOCHASTIC = 1
+
+
+class SmqSmaqParams(ctypes.Structure):
+    _fields_ = [
+        ("num_bits_main", ctypes.c_int32),
+        ("num_bits_outlier", ctypes.c_int32),
+        ("main_std_dev_threshold", ctypes.c_float),
+        ("range_main", ctypes.c_float),
+        ("range_outlier", ctypes.c_float),
+        ("clamp_lo", ctypes.c_float),
+        ("clamp_hi", ctypes.c_float),
+        ("range_std_coef", ctypes.c_float),
+        ("stochastic_rounding", ctypes.c_int32),
+        ("all_positive", ctypes.c_int32),
+        ("use_range_std_dev", ctypes.c_int32),
+        ("stats_source", ctypes.c_int32),
+        ("count_outliers", ctypes.c_int32),
+        ("num_samples", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("offset", ctypes.c_uint64),
+        ("bn_gamma", ctypes.c_void_p),
+        ("bn_beta", ctypes.c_void_p),
+        ("bn_channels", ctypes.c_int64),
+        ("bn_inner", ctypes.c_int64),
+        ("sample_idx", ctypes.c_int64 * SMQ_MAX_SAMPLES),
+    ]
+
+
+class SmqSmaqStats(ctypes.Structure):
+    _fields_ = [
+        ("mean", ctypes.c_float),
+        ("std_dev", ctypes.c_float),
+        ("std_clamped", ctypes.c_float),
+        ("raw_std", ctypes.c_float),
+        ("min_val", ctypes.c_float),
+        ("max_val", ctypes.c_float),
+        ("n_used", ctypes.c_uint32),
+        ("reserved0", ctypes.c_uint32),
+        ("n_outlier", ctypes.c_ulonglong),
+        ("reserved", ctypes.c_uint32 * 6),
+    ]
+
+
+class SmqTensorDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", ctypes.c_void_p),
+        ("y", ctypes.c_void_p),
+        ("n", ctypes.c_int64),
+        ("all_positive", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("rng_offset", ctypes.c_uint64),
+    ]
+
+
+class SmqS2fp8Stats(ctypes.Structure):
+    _fields_ = [
+        ("mu", ctypes.c_float),
+        ("m", ctypes.c_float),
+        ("alpha", ctypes.c_float),
+        ("beta", ctypes.c_float),
+        ("beta_pow2", ctypes.c_float),
+        ("inv_beta_pow2", ctypes.c_float),
+        ("inv_alpha", ctypes.c_float),
+        ("n_used", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 8),
+    ]
+
+
+assert ctypes.sizeof(SmqSmaqStats) == 64
+assert ctypes.sizeof(SmqTensorDesc) == 40
+assert ctypes.sizeof(SmqS2fp8Stats) == 64
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int
+_U64 = ctypes.c_uint64
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); every function declared in include/smq.h
+SIGNATURES = {
+    "smq_abi_version": (_I32, []),
+    "smq_last_error": (ctypes.c_char_p, []),
+    "smq_smaq_params_init": (None, [ctypes.POINTER(SmqSmaqParams)]),
+    "smq_smaq_params_set": (
+        _I32,
+        [ctypes.POINTER(SmqSmaqParams), _I32, _I32, ctypes.c_double, ctypes.c_double, _I32],
+    ),
+    "smq_smaq_draw_samples": (_I32, [ctypes.POINTER(SmqSmaqParams), _I64, _I32]),
+    "smq_smaq_workspace_bytes": (_SZ, [_I64]),
+    "smq_smaq_stats_f32": (_I32, [_P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P]),
+    "smq_smaq_apply_f32": (
+        _I32,
+        [_P, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _P, _SZ, _P],
+    ),
+    "smq_smaq_roundtrip_f32": (
+        _I32,
+        [_P, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _SZ, _P],
+    ),
+    "smq_smaq_multi_plan_bytes": (_SZ, [ctypes.POINTER(_I64), _I32]),
+    "smq_smaq_multi_plan_build": (_I32, [ctypes.POINTER(SmqTensorDesc), _I32, _P, _SZ]),
+    "smq_smaq_multi_workspace_bytes": (_SZ, [ctypes.POINTER(_I64), _I32]),
+    "smq_smaq_multi_f32": (_I32, [_P, _P, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P]),
+    "smq_float_quant_f32": (
+        _I32,
+        [_P, _P, _I64, _I32, _I32, _I32, _I32, _P, _U64, _U64, _P],
+    ),
+    "smq_float_quant_max_value": (ctypes.c_float, [_I32, _I32]),
+    "smq_s2fp8_workspace_bytes": (_SZ, [_I64]),
+    "smq_s2fp8_roundtrip_f32": (
+        _I32,
+        [_P, _P, _I64, _I32, _P, _U64, _U64, _P, _P, _SZ, _P],
+    ),
+    "smq_rng_u32": (ctypes.c_uint32, [_U64, _U64]),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsmq.so once. Raises NativeLibraryError if it is missing: there is no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeLibraryError(
+                    f"libsmq.so not found at {LIB_PATH}; build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)"
+                )
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            if handle.smq_abi_version() != SMQ_ABI_VERSION:
+                raise NativeLibraryError("libsmq ABI version mismatch")
+            _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().smq_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (rc={rc}): {msg}")
+
+
+def require_device_f32(t: torch.Tensor, who: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(
+            f"{who}: smart_compress_amd runs on ROCm device tensors only (got device={t.device}); "
+            "move the tensor to the GPU"
+        )
+    if t.dtype != torch.float32:
+        raise NotImplementedError(
+            f"{who}: dtype {t.dtype} is not supported by the gfx950 kernels yet (float32 only)"
+        )
+
+
+def stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+# ---- per (device, stream) workspaces; zero-filled once at allocation (smq.h contract) ----------
+_ws: Dict[Tuple[str, int, int], torch.Tensor] = {}
+_ws_lock = threading.Lock()
+
+
+def workspace(kind: str, device: torch.device, nbytes: int) -> torch.Tensor:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (kind, idx, stream_ptr(device))
+    with _ws_lock:
+        buf = _ws.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
+            _ws[key] = buf
+    return buf
+
+
+class RngState:
+    """(seed, offset) of a counter-based RNG stream; offset advances by the elements consumed."""
+
+    def __init__(self, seed: int | None = None):
+        if seed is None:
+            seed = int(torch.randint(0, 2**62, (1,), generator=torch.default_generator).item())
+        self.seed = int(seed) & (2**64 - 1)
+        self.offset = 0
+        self._lock = threading.Lock()
+
+    def take(self, n: int) -> Tuple[int, int]:
+        with self._lock:
+            off = self.offset
+            self.offset = (self.offset + int(n)) & (2**64 - 1)
+        return self.seed, off
+
+    def state_dict(self):
+        return {"seed": self.seed, "offset": self.offset}
+
+    def load_state_dict(self, d):
+        self.seed = int(d["seed"])
+        self.offset = int(d["offset"])

