@@ -93,40 +93,61 @@ __device__ __forceinline__ float check_inf_fn(float y, const FQArgs& A) {
   return (A.check_inf && fabsf(y - A.max_value) <= FLT_EPSILON) ? INFINITY : y;
 }
 
+constexpr int kFqTileV = 4;  // float4 per lane per tile (flat contiguous tiles, see smaq.hip)
+constexpr int kFqTileElems = kBlock * kFqTileV * 4;
+
 template <bool SR, bool RARR, bool VEC>
 __global__ __launch_bounds__(kBlock) void float_quant_kernel(FQArgs A) {
   const int64_t n = A.n;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   auto rb = [&](int64_t e) -> uint32_t {
     if (!SR) return 0u;
     return RARR ? A.rand_bits[e] : rng_u32(A.key, A.offset + (uint64_t)e);
+  };
+  auto q1 = [&](float v, uint32_t r) {
+    return check_inf_fn(qtorch_quant(v, r, A.exp_bits, A.man_bits, SR), A);
   };
   if (VEC) {
     const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
     float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
     const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(A.rand_bits);
     const int64_t nv = n >> 2;
-    for (; i < nv; i += stride) {
-      const float4 v = x4[i];
+    const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kFqTileV) + threadIdx.x;
+    float4 v[kFqTileV];
+#pragma unroll
+    for (int u = 0; u < kFqTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j < nv) v[u] = x4[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kFqTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j >= nv) continue;
       uint32_t r0, r1, r2, r3;
       if (SR && RARR) {
-        const uint4 rr = r4[i];
+        const uint4 rr = r4[j];
         r0 = rr.x; r1 = rr.y; r2 = rr.z; r3 = rr.w;
       } else {
-        r0 = rb(4 * i); r1 = rb(4 * i + 1); r2 = rb(4 * i + 2); r3 = rb(4 * i + 3);
+        r0 = rb(4 * j); r1 = rb(4 * j + 1); r2 = rb(4 * j + 2); r3 = rb(4 * j + 3);
       }
       float4 o;
-      o.x = check_inf_fn(qtorch_quant(v.x, r0, A.exp_bits, A.man_bits, SR), A);
-      o.y = check_inf_fn(qtorch_quant(v.y, r1, A.exp_bits, A.man_bits, SR), A);
-      o.z = check_inf_fn(qtorch_quant(v.z, r2, A.exp_bits, A.man_bits, SR), A);
-      o.w = check_inf_fn(qtorch_quant(v.w, r3, A.exp_bits, A.man_bits, SR), A);
-      store_nt(y4 + i, o);
+      o.x = q1(v[u].x, r0);
+      o.y = q1(v[u].y, r1);
+      o.z = q1(v[u].z, r2);
+      o.w = q1(v[u].w, r3);
+      store_nt(y4 + j, o);
     }
-    i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
+      const int64_t e = (nv << 2) + threadIdx.x;
+      A.y[e] = q1(A.x[e], rb(e));
+    }
+  } else {
+    const int64_t e0 = (int64_t)blockIdx.x * kFqTileElems + threadIdx.x;
+    for (int k = 0; k < kFqTileElems / kBlock; ++k) {
+      const int64_t e = e0 + (int64_t)k * kBlock;
+      if (e >= n) break;
+      A.y[e] = q1(A.x[e], rb(e));
+    }
   }
-  for (; i < n; i += stride)
-    A.y[i] = check_inf_fn(qtorch_quant(A.x[i], rb(i), A.exp_bits, A.man_bits, SR), A);
 }
 
 // ---- S2FP8 ---------------------------------------------------------------------------------------
@@ -162,7 +183,7 @@ __device__ void s2fp8_finalize(double s, float m, int64_t n, SmqS2fp8Stats* out)
   out->n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
 }
 
-constexpr int kS2GridCap = 2048;
+constexpr int kS2GridCap = 1024;  // one sweep front, <= 1024 partials (smaq.hip)
 
 __global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const float* __restrict__ x, int64_t n,
                                                              int vec, S2Partial* partials,
@@ -289,36 +310,59 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   const float alpha = A.st->alpha, bp2 = A.st->beta_pow2, ibp2 = A.st->inv_beta_pow2,
               ialpha = A.st->inv_alpha;
   const int64_t n = A.n;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   auto rb = [&](int64_t e) -> uint32_t {
     return RARR ? A.rand_bits[e] : rng_u32(A.key, A.offset + (uint64_t)e);
+  };
+  auto q1 = [&](float v, uint32_t r) {
+    return s2fp8_elem(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
   };
   if (VEC) {
     const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
     float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
     const int64_t nv = n >> 2;
-    for (; i < nv; i += stride) {
-      const float4 v = x4[i];
-      float4 o;
-      o.x = s2fp8_elem(v.x, rb(4 * i), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
-      o.y = s2fp8_elem(v.y, rb(4 * i + 1), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
-      o.z = s2fp8_elem(v.z, rb(4 * i + 2), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
-      o.w = s2fp8_elem(v.w, rb(4 * i + 3), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
-      store_nt(y4 + i, o);
+    const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kFqTileV) + threadIdx.x;
+    float4 v[kFqTileV];
+#pragma unroll
+    for (int u = 0; u < kFqTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j < nv) v[u] = x4[j];
     }
-    i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < kFqTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j >= nv) continue;
+      float4 o;
+      o.x = q1(v[u].x, rb(4 * j));
+      o.y = q1(v[u].y, rb(4 * j + 1));
+      o.z = q1(v[u].z, rb(4 * j + 2));
+      o.w = q1(v[u].w, rb(4 * j + 3));
+      store_nt(y4 + j, o);
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
+      const int64_t e = (nv << 2) + threadIdx.x;
+      A.y[e] = q1(A.x[e], rb(e));
+    }
+  } else {
+    const int64_t e0 = (int64_t)blockIdx.x * kFqTileElems + threadIdx.x;
+    for (int k = 0; k < kFqTileElems / kBlock; ++k) {
+      const int64_t e = e0 + (int64_t)k * kBlock;
+      if (e >= n) break;
+      A.y[e] = q1(A.x[e], rb(e));
+    }
   }
-  for (; i < n; i += stride)
-    A.y[i] = s2fp8_elem(A.x[i], rb(i), alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
 }
 
 static inline bool aligned16f(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-static int fq_grid(int64_t n) {
-  int64_t g = (n + kBlock * 4 * 4 - 1) / (kBlock * 4 * 4);
+static int fq_grid(int64_t n) {  // flat tiles
+  int64_t g = (n + kFqTileElems - 1) / kFqTileElems;
+  return (int)(g < 1 ? 1 : g);
+}
+
+static int s2_stats_grid(int64_t n) {  // grid-stride, one float4 per lane per step
+  int64_t g = (n + kBlock * 4 - 1) / (kBlock * 4);
   if (g < 1) g = 1;
-  if (g > 2048) g = 2048;
+  if (g > kS2GridCap) g = kS2GridCap;
   return (int)g;
 }
 
@@ -409,7 +453,7 @@ int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
   if (stats_in) {
     hipLaunchKernelGGL(s2fp8_derive_kernel, dim3(1), dim3(64), 0, st, stats_in, hdr);
   } else {
-    const int grid = fq_grid(n);
+    const int grid = s2_stats_grid(n);
     hipLaunchKernelGGL(s2fp8_stats_kernel, dim3(grid), dim3(kBlock), 0, st, x, n,
                        aligned16f(x) ? 1 : 0, partials, counter, hdr);
   }

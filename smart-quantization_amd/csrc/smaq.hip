@@ -52,10 +52,14 @@ static int grid_for(int64_t work_items, int per_block_items, int cap) {
   return (int)g;
 }
 
-// Persistent-ish grid caps: 256 CUs x 8 workgroups of 256 threads.
-constexpr int kStatsGridCap = 2048;
-constexpr int kApplyGridCap = 2048;
-constexpr int kUnroll = 4;  // float4 loads in flight per thread per iteration
+// Memory shapes measured on MI355X (tools/membench.hip, profiles/): a read stream peaks with ONE
+// dwordx4 per lane in flight and the whole grid sweeping the buffer in address order (grid-stride,
+// ~1024 workgroups: 6.4 TB/s); several loads per lane at grid-stride distance (4 MB apart) open
+// several sweep fronts and fall to ~5.2 TB/s. A read+write stream is fastest as flat contiguous
+// tiles, one tile per workgroup, tiles in dispatch order (~6.1 TB/s).
+constexpr int kStatsGridCap = 1024;  // also the number of fp64 partials the last workgroup sums
+constexpr int kTileV = 4;            // apply: float4 per lane per tile -> 16 KiB read per workgroup
+constexpr int kTileElems = kBlock * kTileV * 4;
 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
@@ -75,31 +79,17 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const float* __restr
   StatAcc acc;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  int64_t done = 0;
   if (vec) {
     const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
     const int64_t nv = n >> 2;
-    for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
-      float4 v[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = load_nt(x4 + i + u * stride);
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        acc.add<RANGE>(v[u].x, shift);
-        acc.add<RANGE>(v[u].y, shift);
-        acc.add<RANGE>(v[u].z, shift);
-        acc.add<RANGE>(v[u].w, shift);
-      }
-    }
-    for (; i < nv; i += stride) {
+    for (; i < nv; i += stride) {  // one dwordx4 in flight per lane: a single sweep front
       const float4 v = x4[i];
       acc.add<RANGE>(v.x, shift);
       acc.add<RANGE>(v.y, shift);
       acc.add<RANGE>(v.z, shift);
       acc.add<RANGE>(v.w, shift);
     }
-    done = nv << 2;
-    i = done + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
   }
   for (; i < n; i += stride) acc.add<RANGE>(x[i], shift);
 
@@ -211,27 +201,31 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
     c.sd = A.stats->std_dev;
     c.sc = A.stats->std_clamped;
   }
-  c.thr = A.thr;
-  c.nthr = -A.thr;
-  c.zh = 0.0f * c.nthr;
-  c.zl = 0.0f * c.thr;
-  c.r_main = A.r_main;
-  c.r_out = A.r_out;
+  init_consts(c, c.mean, c.sd, c.sc, A.thr, A.r_main, A.r_out);
   const bool all_pos = A.all_pos != 0;
 
   unsigned long long n_out = 0;
   const int64_t n = A.n;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  int64_t vec_end = 0;
   if (VEC) {
+    // flat tile: this workgroup owns float4 [t0, t0 + kBlock * kTileV), kTileV coalesced sweeps
     const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
     float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
     const float4* __restrict__ u4 = reinterpret_cast<const float4*>(A.uniforms);
     const int64_t nv = n >> 2;
-    auto body = [&](int64_t j, const float4& v, const float4& uu) {
-      float4 o;
-      bool b0, b1, b2, b3;
+    const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kTileV) + threadIdx.x;
+    float4 v[kTileV], uu[kTileV];
+#pragma unroll
+    for (int u = 0; u < kTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j < nv) {
+        v[u] = x4[j];
+        if (RM == kRoundUniform) uu[u] = u4[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j >= nv) continue;
       float u0, u1, u2, u3;
       if (RM == kRoundHash) {
         const uint64_t ctr = A.offset + ((uint64_t)j << 2);
@@ -239,41 +233,44 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
         u1 = u32_to_unit(rng_u32(A.key, ctr + 1));
         u2 = u32_to_unit(rng_u32(A.key, ctr + 2));
         u3 = u32_to_unit(rng_u32(A.key, ctr + 3));
+      } else if (RM == kRoundUniform) {
+        u0 = uu[u].x; u1 = uu[u].y; u2 = uu[u].z; u3 = uu[u].w;
       } else {
-        u0 = uu.x; u1 = uu.y; u2 = uu.z; u3 = uu.w;
+        u0 = u1 = u2 = u3 = 0.0f;
       }
-      o.x = smaq_elem<RM, BN>(v.x, u0, c, all_pos, b0, bn_term<BN>(A, 4 * j + 0));
-      o.y = smaq_elem<RM, BN>(v.y, u1, c, all_pos, b1, bn_term<BN>(A, 4 * j + 1));
-      o.z = smaq_elem<RM, BN>(v.z, u2, c, all_pos, b2, bn_term<BN>(A, 4 * j + 2));
-      o.w = smaq_elem<RM, BN>(v.w, u3, c, all_pos, b3, bn_term<BN>(A, 4 * j + 3));
+      bool b0, b1, b2, b3;
+      float4 o;
+      o.x = smaq_elem<RM, BN>(v[u].x, u0, c, all_pos, b0, bn_term<BN>(A, 4 * j + 0));
+      o.y = smaq_elem<RM, BN>(v[u].y, u1, c, all_pos, b1, bn_term<BN>(A, 4 * j + 1));
+      o.z = smaq_elem<RM, BN>(v[u].z, u2, c, all_pos, b2, bn_term<BN>(A, 4 * j + 2));
+      o.w = smaq_elem<RM, BN>(v[u].w, u3, c, all_pos, b3, bn_term<BN>(A, 4 * j + 3));
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
       store_nt(y4 + j, o);
-    };
-    for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
-      float4 v[kUnroll], uu[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        v[u] = x4[i + u * stride];
-        if (RM == kRoundUniform) uu[u] = u4[i + u * stride];
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) body(i + u * stride, v[u], uu[u]);
     }
-    for (; i < nv; i += stride) {
-      float4 uu = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (RM == kRoundUniform) uu = u4[i];
-      body(i, x4[i], uu);
+    // ragged tail (n % 4 elements): the last workgroup
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
+      const int64_t e = (nv << 2) + threadIdx.x;
+      float uf = 0.0f;
+      if (RM == kRoundHash) uf = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)e));
+      if (RM == kRoundUniform) uf = A.uniforms[e];
+      bool bt;
+      A.y[e] = smaq_elem<RM, BN>(A.x[e], uf, c, all_pos, bt, bn_term<BN>(A, e));
+      n_out += (unsigned)bt;
     }
-    vec_end = nv << 2;
-    i = vec_end + (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  }
-  for (; i < n; i += stride) {
-    float u = 0.0f;
-    if (RM == kRoundHash) u = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)i));
-    if (RM == kRoundUniform) u = A.uniforms[i];
-    bool b;
-    A.y[i] = smaq_elem<RM, BN>(A.x[i], u, c, all_pos, b, bn_term<BN>(A, i));
-    n_out += (unsigned)b;
+  } else {
+    // unaligned pointers: the same tile of kTileElems elements with dword accesses
+    const int64_t e0 = (int64_t)blockIdx.x * kTileElems + threadIdx.x;
+#pragma unroll 4
+    for (int k = 0; k < kTileElems / kBlock; ++k) {
+      const int64_t e = e0 + (int64_t)k * kBlock;
+      if (e >= n) break;
+      float uf = 0.0f;
+      if (RM == kRoundHash) uf = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)e));
+      if (RM == kRoundUniform) uf = A.uniforms[e];
+      bool bt;
+      A.y[e] = smaq_elem<RM, BN>(A.x[e], uf, c, all_pos, bt, bn_term<BN>(A, e));
+      n_out += (unsigned)bt;
+    }
   }
 
   if (A.count) {  // outlier count for log_size (smart.py:184-188), one atomic per workgroup
@@ -327,7 +324,7 @@ static int launch_stats(const float* x, int64_t n, const SmqSmaqParams* p, void*
   uint32_t* counter = (uint32_t*)(base + SmaqWsLayout::kHeader);
   StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
   const int vec = aligned16(x) ? 1 : 0;
-  const int grid = grid_for(n, kBlock * 4 * kUnroll, kStatsGridCap);
+  const int grid = grid_for(n, kBlock * 4, kStatsGridCap);
   FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n)};
   if (p->use_range_std_dev)
     hipLaunchKernelGGL(smaq_stats_kernel<true>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, fin,
@@ -418,7 +415,12 @@ static int launch_apply(const float* x, float* y, int64_t n, const SmqSmaqParams
       return SMQ_ERR_LAUNCH;
     }
   }
-  const int grid = grid_for(n, kBlock * 4 * kUnroll, kApplyGridCap);
+  const int64_t tiles = (n + kTileElems - 1) / kTileElems;
+  if (tiles > 0x7fffffffLL) {
+    set_error("tensor too large: %lld elements", (long long)n);
+    return SMQ_ERR_INVALID;
+  }
+  const int grid = (int)tiles;
   const bool bn = A.bn_gamma != nullptr;
   switch (p->stats_source) {
     case SMQ_STATS_WORKSPACE:

@@ -98,11 +98,39 @@ struct ElemConsts {
   float thr, nthr;        // fp32(T_m), -fp32(T_m)
   float zh, zl;           // 0 * -T_m, 0 * T_m  (the bool*float zero terms, smart.py:159-161)
   float r_main, r_out;    // ranges
+  double inv_sc;          // RN64(1 / sc)
+  double inv_r_main, inv_r_out;  // RN64(1 / range)
 };
+
+// Correctly rounded fp32 quotient a / b from a double reciprocal: RN32(RN64(a * RN64(1/b))).
+// Why this equals IEEE a / b: for normal fp32 a, b and a normal result, an exact quotient a/b is
+// never closer than 2^-49 (relative) to an fp32 rounding boundary (a midpoint needs 25 significant
+// bits, a = b * M would need >= 25 bits in a), while the double evaluation is within 2^-52; the
+// overflow threshold is such a midpoint too. Subnormal results lose that margin, so the caller
+// re-does those with IEEE division (never taken for realistic data). Division by 0 -> +-inf / NaN
+// as IEEE (1/0 = inf in double). Cost: 3 VALU (cvt, v_mul_f64, cvt) instead of ~10.
+__device__ __forceinline__ float div_by_const(float a, double inv_b) {
+  return (float)((double)a * inv_b);
+}
+
+__device__ __forceinline__ void init_consts(ElemConsts& c, float mean, float sd, float sc, float thr,
+                                            float r_main, float r_out) {
+  c.mean = mean;
+  c.sd = sd;
+  c.sc = sc;
+  c.thr = thr;
+  c.nthr = -thr;
+  c.zh = 0.0f * c.nthr;
+  c.zl = 0.0f * c.thr;
+  c.r_main = r_main;
+  c.r_out = r_out;
+  c.inv_sc = 1.0 / (double)sc;
+  c.inv_r_main = 1.0 / (double)r_main;
+  c.inv_r_out = 1.0 / (double)r_out;
+}
 
 enum RoundMode { kRoundHash = 0, kRoundUniform = 1, kRoundTrunc = 2 };
 
-// One element of smart.py:154-182. Each statement is one rounded fp32 op of the reference.
 // Per-channel BatchNorm fold (smart.py:144-149 before, 174-179 after); scale = gamma[c].
 struct BnTerm {
   float gamma, beta;
@@ -113,12 +141,15 @@ template <int RM, bool BN = false>
 __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c, bool all_pos,
                                            bool& is_outlier, BnTerm bn = BnTerm{1.0f, 0.0f}) {
   if (BN) v = (v - bn.beta) / bn.gamma;                 // (data - beta) / gamma
-  const float z = (v - c.mean) / c.sc;                  // (data - mean) / std.clamp(...)
+  const float dm = v - c.mean;                          // data - mean
+  float z = div_by_const(dm, c.inv_sc);                 // / std.clamp(...)
+  if (__builtin_expect(fabsf(z) < 1.17549435e-38f && z != 0.0f, 0)) z = dm / c.sc;
   const bool hi = z > c.thr;                            // is_outlier_higher
   const bool lo = z < c.nthr;                           // is_outlier_lower
   const bool o = hi | lo;                               // is_outlier
   const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);  // scalars
   const float r = o ? c.r_out : c.r_main;               // ranges
+  const double inv_r = o ? c.inv_r_out : c.inv_r_main;
   const float d = (z + a) * r;
   float q;
   if (RM == kRoundTrunc) {
@@ -130,7 +161,7 @@ __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c
     t = (t < 0.0f) ? 0.0f : t;                          // F.relu
     q = f + __builtin_rintf(t);                         // .round() = half to even
   }
-  float out = (q / r) - a;
+  float out = div_by_const(q, inv_r) - a;               // (data / ranges) - scalars
   out = (out * c.sd) + c.mean;
   if (BN) out = (out * bn.gamma) + bn.beta;             // (data * gamma) + beta
   if (all_pos) out = (out < 0.0f) ? 0.0f : out;         // clamp_min(0.0)

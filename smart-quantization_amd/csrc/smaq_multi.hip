@@ -114,15 +114,7 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
   const SmqTensorDesc d = A.descs[ch.tensor];
   const SmqSmaqStats* st = &A.stats[ch.tensor];
   ElemConsts c;
-  c.mean = st->mean;
-  c.sd = st->std_dev;
-  c.sc = st->std_clamped;
-  c.thr = A.thr;
-  c.nthr = -A.thr;
-  c.zh = 0.0f * c.nthr;
-  c.zl = 0.0f * c.thr;
-  c.r_main = A.r_main;
-  c.r_out = A.r_out;
+  init_consts(c, st->mean, st->std_dev, st->std_clamped, A.thr, A.r_main, A.r_out);
   const bool all_pos = d.all_positive != 0;
   const float* __restrict__ x = d.x;
   float* y = d.y;  // may alias x

@@ -1,0 +1,151 @@
+"""The C-ABI library (no GPU): it loads, exports every function include/smq.h declares, struct
+layouts agree, and the host-only functions behave (RNG == oracle, parameter helpers, sample
+drawing, multi-tensor plan layout, argument validation without touching the device)."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "smq.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w \*]*?\b(smq_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    declared = _declared_functions()
+    assert len(declared) >= 18
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(N.SIGNATURES), set(declared) ^ set(N.SIGNATURES)
+    assert lib.smq_abi_version() == N.SMQ_ABI_VERSION
+
+
+def test_struct_layouts_match_header():
+    """Compile a tiny C program against include/smq.h and compare sizeof/offsetof with ctypes."""
+    import subprocess
+    import tempfile
+
+    from smart_compress_amd import _native as N
+
+    prog = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "smq.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(SmqSmaqParams), sizeof(SmqSmaqStats),
+         sizeof(SmqTensorDesc), sizeof(SmqS2fp8Stats), offsetof(SmqSmaqParams, seed),
+         offsetof(SmqSmaqParams, bn_gamma), offsetof(SmqSmaqParams, sample_idx));
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "l")
+        subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), c, "-o", exe])
+        got = list(map(int, subprocess.check_output([exe]).split()))
+    want = [ctypes.sizeof(N.SmqSmaqParams), ctypes.sizeof(N.SmqSmaqStats),
+            ctypes.sizeof(N.SmqTensorDesc), ctypes.sizeof(N.SmqS2fp8Stats),
+            N.SmqSmaqParams.seed.offset, N.SmqSmaqParams.bn_gamma.offset,
+            N.SmqSmaqParams.sample_idx.offset]
+    assert got == want
+
+
+def test_host_rng_equals_oracle():
+    from oracle import rng
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    for seed in (0, 1, 2**40 + 7, 2**64 - 1):
+        for off in (0, 5, 2**32 - 2, 2**33 + 1):
+            got = [lib.smq_rng_u32(seed, off + i) for i in range(6)]
+            assert got == list(rng.rng_u32(seed, off, 6))
+
+
+def test_max_values():
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    assert lib.smq_float_quant_max_value(5, 2) == 57344.0
+    assert lib.smq_float_quant_max_value(5, 10) == 65504.0
+    assert lib.smq_float_quant_max_value(4, 3) == 240.0
+    assert np.float32(lib.smq_float_quant_max_value(8, 7)) == np.float32(3.3895314e38)
+
+
+def test_draw_samples():
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    seen = set()
+    for off in range(50):
+        p = N.SmqSmaqParams()
+        lib.smq_smaq_params_init(p)
+        p.seed, p.offset = 9, off * 1000
+        assert lib.smq_smaq_draw_samples(p, 1000, 16) == 0
+        idx = list(p.sample_idx[: p.num_samples])
+        assert p.num_samples == 16 and len(set(idx)) == 16 and all(0 <= i < 1000 for i in idx)
+        seen.update(idx)
+    assert len(seen) > 400  # covers the range
+    p = N.SmqSmaqParams()
+    lib.smq_smaq_params_init(p)
+    assert lib.smq_smaq_draw_samples(p, 10, 16) == 0 and p.num_samples == 10
+    assert sorted(p.sample_idx[:10]) == list(range(10))
+    assert lib.smq_smaq_draw_samples(p, 1000, 65) != 0
+    assert b"SMQ_MAX_SAMPLES" in lib.smq_last_error()
+
+
+def test_validation_errors_without_device():
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    p = N.SmqSmaqParams()
+    lib.smq_smaq_params_init(p)
+    assert lib.smq_smaq_apply_f32(None, None, 0, p, None, None, None, 0, None) == N.SMQ_STATS_SAMPLED * -1
+    assert b"n must be >= 1" in lib.smq_last_error()
+    assert lib.smq_smaq_stats_f32(None, 10, p, None, 0, None) == -1
+    assert lib.smq_float_quant_f32(None, None, 5, 5, 2, 1, 1, None, 0, 0, None) == -1
+    assert lib.smq_float_quant_f32(None, None, 0, 9, 2, 1, 1, None, 0, 0, None) == -1
+    assert b"exp_bits" in lib.smq_last_error()
+    assert lib.smq_s2fp8_roundtrip_f32(None, None, 0, 1, None, 0, 0, None, None, 0, None) == -1
+    assert lib.smq_smaq_params_set(p, 6, 8, 1.0, 1.0, 32) == -1
+
+
+def test_multi_plan_layout():
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    sizes = [10, 32768, 32769, 100000]
+    count = len(sizes)
+    arr = (ctypes.c_int64 * count)(*sizes)
+    nbytes = lib.smq_smaq_multi_plan_bytes(arr, count)
+    chunks = [1, 1, 2, 4]
+    assert nbytes == 32 + ((40 * count + 31) // 32) * 32 + 32 * sum(chunks)
+    descs = (N.SmqTensorDesc * count)()
+    for i, n in enumerate(sizes):
+        descs[i].x = descs[i].y = 0x1000 * (i + 1)
+        descs[i].n = n
+    host = (ctypes.c_uint8 * nbytes)()
+    assert lib.smq_smaq_multi_plan_build(descs, count, host, nbytes) == 0
+    raw = np.frombuffer(bytes(host), dtype=np.uint8)
+    hdr = raw[:8].view(np.int32)
+    assert list(hdr) == [count, sum(chunks)]
+    cstart = 32 + ((40 * count + 31) // 32) * 32
+    ch = raw[cstart:].view(np.int64).reshape(-1, 4)
+    tensor = (ch[:, 0] & 0xFFFFFFFF).astype(np.int32)
+    assert list(tensor) == [0, 1, 2, 2, 3, 3, 3, 3]
+    assert list(ch[:, 3]) == [10, 32768, 32768, 32769, 32768, 65536, 98304, 100000]
+    assert lib.smq_smaq_multi_workspace_bytes(arr, count) >= 64 * count + 32 * sum(chunks)
+    descs[1].n = 0
+    assert lib.smq_smaq_multi_plan_build(descs, count, host, nbytes) == -1

@@ -131,7 +131,9 @@ def test_golden_s2fp8(key):
     assert ok.all(), int((~ok).sum())
     # end to end with device statistics
     y2, st2 = g.s2fp8(x, check_inf=m["check_inf"], rand_bits=r)
-    assert ulp_diff(st2["mu"], d["mu"]) <= 4
+    # the reference's mu is a float32 cascade sum of float32 log2 values; ours is an fp64 sum of
+    # device log2f values: agree to the accumulated rounding of the reference's sum
+    assert abs(float(st2["mu"]) - float(d["mu"])) <= 2.0**-20 * max(1.0, abs(float(d["mu"])))
     assert ulp_diff(st2["m"], d["m"]) <= 1
     ref = os2.roundtrip(d["x"], d["q_rand"], m["check_inf"], st=os2.derive(st2["mu"], st2["m"]))
     T_ref = ref[3]

@@ -1,0 +1,152 @@
+"""Host-side drop-in surface (no GPU): flags, defaults, constants, metrics, passthrough, errors."""
+
+from argparse import ArgumentParser
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import float_meta, smaq_cases, smaq_hparams
+
+
+def test_smartfp_flags_match_reference():
+    from smart_compress_amd.compress.smart import SmartFP
+
+    ours = vars(SmartFP.add_argparse_args(ArgumentParser()).parse_args([]))
+    ref = smaq_cases()["normal"]
+    for k, v in ours.items():
+        if k == "measure_compression_ratio":
+            continue  # golden cases were run with it on
+        assert ref[k] == v, k
+    # every reference flag parses the same way
+    argv = ["--num_samples", "32", "--use_sample_stats", "--no_stochastic_rounding",
+            "--num_bits_main", "5", "--num_bits_outlier", "7", "--main_std_dev_threshold", "0.8",
+            "--outlier_std_dev_threshold", "3.0", "--min_size", "4", "--use_range_std_dev",
+            "--use_batch_norm", "--bn_scalar_params", "--measure_compression_ratio"]
+    hp = SmartFP.add_argparse_args(ArgumentParser()).parse_args(argv)
+    assert hp.num_samples == 32 and hp.use_sample_stats and not hp.stochastic_rounding
+    assert (hp.num_bits_main, hp.num_bits_outlier) == (5, 7)
+    assert hp.min_size == 4 and hp.use_range_std_dev and hp.use_batch_norm and hp.bn_scalar_params
+
+
+def test_float_codec_flags_match_reference():
+    from smart_compress_amd.compress import BF16, FP8, FP16, S2FP8
+
+    ref = float_meta()["argparse_defaults"]
+    for cls in (FP8, FP16, BF16, S2FP8):
+        assert vars(cls.add_argparse_args(ArgumentParser()).parse_args([])) == ref[cls.__name__]
+        hp = cls.add_argparse_args(ArgumentParser()).parse_args(["--no_float_quantize_check_inf"])
+        assert hp.float_quantize_check_inf is False
+
+
+@pytest.mark.parametrize("name", sorted(smaq_cases()))
+def test_constants_match_reference(name):
+    from smart_compress_amd.compress.smart import SmartFP
+
+    meta = smaq_cases()[name]
+    c = SmartFP(smaq_hparams(meta))
+    assert c.range_outlier == meta["range_outlier"] and c.range_normal == meta["range_normal"]
+    assert c.clamped_range == (1e-38, 1e38)
+
+
+def test_params_block():
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.smart import SmartFP
+
+    for bm, bo, ro, rn in ((6, 8, 42.0, 15.0), (4, 6, 10.0, 3.0), (5, 7, 20.666666, 7.0),
+                           (3, 5, 4.6666665, 1.0), (2, 3, 0.6666667, 0.0)):
+        c = SmartFP(smaq_hparams(num_bits_main=bm, num_bits_outlier=bo))
+        p = c._params(1000, False)
+        assert np.float32(p.range_outlier) == np.float32(ro)
+        assert np.float32(p.range_main) == np.float32(rn)
+        # the C helper computes the same fp32 constants
+        q = N.SmqSmaqParams()
+        N.lib().smq_smaq_params_init(q)
+        N.lib().smq_smaq_params_set(q, bm, bo, 1.0, 2.5, 32)
+        assert q.range_outlier == p.range_outlier and q.range_main == p.range_main
+    c16 = SmartFP(smaq_hparams(precision=16))
+    p = c16._params(10, True)
+    assert np.float32(p.clamp_lo) == np.float32(1e-4) and p.all_positive == 1
+
+
+def test_rng_offsets_advance():
+    from smart_compress_amd.compress.smart import SmartFP
+
+    c = SmartFP(smaq_hparams(smq_seed=5))
+    p1 = c._params(1000, False)
+    p2 = c._params(24, False)
+    assert (p1.seed, p1.offset, p2.offset) == (5, 0, 1000)
+
+
+def test_range_coef_matches_torch():
+    from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import range_std_coef
+
+    for n in (8, 16, 1001, 16384, 1 << 28, 25690112):
+        t = torch.tensor(n).type_as(torch.tensor(0.0))
+        ref = float(1 / torch.sqrt(2.0 * torch.log(t)))
+        assert range_std_coef(n) == ref
+        assert np.float32(osmaq.range_coef(n)) == np.float32(ref)
+
+
+def test_passthrough_and_cpu_rejection():
+    from smart_compress_amd.compress.smart import SmartFP
+
+    c = SmartFP(smaq_hparams())
+    x = torch.randn(7)
+    assert c(x) is x  # smart.py:123-128, no device needed
+    with pytest.raises(RuntimeError, match="ROCm device tensors only"):
+        c(torch.randn(100))
+
+
+def test_log_size_routing():
+    from smart_compress_amd.compress.fp32 import FP32
+
+    hp = FP32.add_argparse_args(ArgumentParser()).parse_args(["--measure_compression_ratio"])
+    c = FP32(hp)
+    logged, custom = [], []
+    c.log = lambda k, v, **kw: logged.append((k, v, tuple(sorted(kw))))
+    c.log_custom = lambda d: custom.append(d)
+    x = torch.randn(10)
+    assert c(x, tag="forward_hook") is x
+    keys = {k for k, _, _ in logged}
+    assert keys == {"compression_ratio", "compression_ratio_forward_hook", "new_size",
+                    "new_size_forward_hook", "orig_size", "orig_size_forward_hook"}
+    assert all(kw == ("reduce_fx", "tbptt_reduce_fx") for k, _, kw in logged if "size" in k)
+    c(x, tag="optimizer_grad")
+    assert custom and custom[0]["compression_ratio_optimizer_grad"] == 1.0
+
+
+def test_globals_profiler_tolerated():
+    from smart_compress_amd.util.globals import Globals, profile
+
+    with profile("smaq"):
+        pass
+
+    class P:
+        def __init__(self):
+            self.names = []
+
+        def profile(self, name):
+            import contextlib
+
+            self.names.append(name)
+            return contextlib.nullcontext()
+
+    Globals.profiler = P()
+    try:
+        from smart_compress_amd.compress.smart import SmartFP
+
+        SmartFP(smaq_hparams())(torch.randn(3))
+        assert Globals.profiler.names == ["smaq"]
+    finally:
+        Globals.profiler = None
+
+
+def test_reduce_fx():
+    from smart_compress_amd.compress.base import _reduce_fx
+
+    assert _reduce_fx([]) == 0
+    assert _reduce_fx([1.0, 2.0]) == 3.0
+    assert float(_reduce_fx([torch.tensor(1.0), torch.tensor(2.5)])) == 3.5
+    assert float(_reduce_fx(torch.tensor([1.0, 2.0]))) == 3.0

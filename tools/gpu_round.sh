@@ -16,6 +16,8 @@ for s in "$@"; do
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -k "not slow" ;;
     tests_all) step pytest_gpu_all 1200 python -m pytest tests -m gpu -q ;;
     slow) step pytest_slow 600 python -m pytest tests -m "gpu and slow" -q ;;
+    membench) step membench 300 ./tools/membench ;;
+    kbench) step kbench 300 python tools/kbench.py ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 --cpu-budget 8 ;;
     bench_all) step bench_fp8 300 python bench.py --config fp8 --steps 50 --warmup 5 &&

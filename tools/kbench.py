@@ -1,0 +1,90 @@
+"""Per-kernel timing of libsmq launches through the C-ABI (hipEvents on the launch stream).
+
+python tools/kbench.py [--n N] [--reps R]  ->  one JSON object with ms and GB/s per variant.
+"""
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "smart-quantization_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from smart_compress_amd import _native as N  # noqa: E402
+
+
+def timed(fn, reps):
+    ts = []
+    for r in range(reps + 3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        if r >= 3:
+            ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 28)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    n = args.n
+    lib = N.lib()
+    x = torch.randn(n, device="cuda")
+    y = torch.empty_like(x)
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.zeros(lib.smq_smaq_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    out = {"n": n}
+
+    def params(**kw):
+        p = N.SmqSmaqParams()
+        lib.smq_smaq_params_init(p)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+    p = params()
+    stats = lambda: N.check(lib.smq_smaq_stats_f32(x.data_ptr(), n, p, ws.data_ptr(), ws.numel(), st), "s")
+    ms = timed(stats, args.reps)
+    out["stats"] = dict(ms=ms, GBps=4 * n / ms / 1e6)
+    for name, pp in (("apply_sr", params()), ("apply_trunc", params(stochastic_rounding=0)),
+                     ("apply_sr_allpos", params(all_positive=1)),
+                     ("apply_sr_count", params(count_outliers=1))):
+        f = lambda pp=pp: N.check(lib.smq_smaq_apply_f32(x.data_ptr(), y.data_ptr(), n, pp, None, None,
+                                                         ws.data_ptr(), ws.numel(), st), "a")
+        ms = timed(f, args.reps)
+        out[name] = dict(ms=ms, GBps=8 * n / ms / 1e6)
+    ps = params(stats_source=N.SMQ_STATS_SAMPLED)
+    lib.smq_smaq_draw_samples(ps, n, 16)
+    f = lambda: N.check(lib.smq_smaq_apply_f32(x.data_ptr(), y.data_ptr(), n, ps, None, None,
+                                               ws.data_ptr(), ws.numel(), st), "a")
+    ms = timed(f, args.reps)
+    out["apply_sampled"] = dict(ms=ms, GBps=8 * n / ms / 1e6)
+    rt = lambda: N.check(lib.smq_smaq_roundtrip_f32(x.data_ptr(), y.data_ptr(), n, p, None,
+                                                    ws.data_ptr(), ws.numel(), st), "r")
+    ms = timed(rt, args.reps)
+    out["roundtrip"] = dict(ms=ms, GBps=12 * n / ms / 1e6)
+    for e, m in ((5, 2), (5, 10), (8, 7)):
+        f = lambda e=e, m=m: N.check(lib.smq_float_quant_f32(x.data_ptr(), y.data_ptr(), n, e, m, 1, 1,
+                                                             None, 1, 0, st), "f")
+        ms = timed(f, args.reps)
+        out[f"float_quant_{e}_{m}"] = dict(ms=ms, GBps=8 * n / ms / 1e6)
+    ws2 = torch.zeros(lib.smq_s2fp8_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    f = lambda: N.check(lib.smq_s2fp8_roundtrip_f32(x.data_ptr(), y.data_ptr(), n, 1, None, 1, 0, None,
+                                                    ws2.data_ptr(), ws2.numel(), st), "s2")
+    ms = timed(f, args.reps)
+    out["s2fp8_roundtrip"] = dict(ms=ms, GBps=12 * n / ms / 1e6)
+    torch.cuda.synchronize()
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
