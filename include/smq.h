@@ -49,6 +49,13 @@ extern "C" {
 
 #define SMQ_MAX_SAMPLES 64
 
+/* Single-tensor SmaQ workspace layout (bytes): [0, 64) SmqSmaqStats header, [64, 128) arrival
+ * counter, [128, 640) SMQ_WS_OUTLIER_SLOTS uint64 outlier-count slots (params.count_outliers:
+ * the count is their sum; spread so 10^5 workgroups do not serialise on one address), then the
+ * statistics partials. */
+#define SMQ_WS_OUTLIER_SLOTS_OFFSET 128
+#define SMQ_WS_OUTLIER_SLOTS 64
+
 /* Where smq_smaq_apply_f32 takes (mean, std) from. */
 #define SMQ_STATS_WORKSPACE 0 /* written by smq_smaq_stats_f32 into the workspace header */
 #define SMQ_STATS_SAMPLED 1   /* computed in-kernel from params.sample_idx (smart.py:86-91) */
@@ -103,7 +110,8 @@ typedef struct SmqSmaqStats {
   float max_val;
   uint32_t n_used;     /* elements the statistics were computed over */
   uint32_t reserved0;
-  unsigned long long n_outlier; /* outlier count (when params.count_outliers) */
+  unsigned long long n_outlier; /* multi-tensor calls: this tensor's outlier count (single-tensor
+                                   calls: see SMQ_WS_OUTLIER_SLOTS_OFFSET) */
   uint32_t reserved[6];
 } SmqSmaqStats;
 

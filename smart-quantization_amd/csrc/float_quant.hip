@@ -226,21 +226,20 @@ __global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const float* __rest
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    S2Partial p;
-    p.s = (shs[0] + shs[1]) + (shs[2] + shs[3]);
-    p.m = nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3]));
-    p.pad = 0.0f;
-    partials[blockIdx.x] = p;
+    S2Partial* p = partials + blockIdx.x;
+    st_sc1_f64(&p->s, (shs[0] + shs[1]) + (shs[2] + shs[3]));
+    st_sc1_f32x2(&p->m, nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3])), 0.0f);
   }
   const uint32_t prev = block_arrive(counter, &slot);
   if (prev != gridDim.x - 1) return;
-  block_acquire();
   double ts = 0.0;
   float tm = -INFINITY;
   for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
-    const S2Partial p = partials[b];
-    ts += p.s;
-    tm = nan_max(tm, p.m);
+    const S2Partial* p = partials + b;
+    ts += ld_sc1_f64(&p->s);
+    float pm, pad;
+    ld_sc1_f32x2(&p->m, pm, pad);
+    tm = nan_max(tm, pm);
   }
   ts = wave_sum(ts);
 #pragma unroll

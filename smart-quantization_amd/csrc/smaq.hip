@@ -17,6 +17,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "smq_common.h"
@@ -57,9 +58,8 @@ static int grid_for(int64_t work_items, int per_block_items, int cap) {
 // ~1024 workgroups: 6.4 TB/s); several loads per lane at grid-stride distance (4 MB apart) open
 // several sweep fronts and fall to ~5.2 TB/s. A read+write stream is fastest as flat contiguous
 // tiles, one tile per workgroup, tiles in dispatch order (~6.1 TB/s).
-constexpr int kStatsGridCap = 1024;  // also the number of fp64 partials the last workgroup sums
-constexpr int kTileV = 4;            // apply: float4 per lane per tile -> 16 KiB read per workgroup
-constexpr int kTileElems = kBlock * kTileV * 4;
+constexpr int kStatsGridCap = 2048;  // also the number of fp64 partials the last workgroup sums
+constexpr int kDefaultTileV = 4;     // apply: float4 per lane per tile (SMQ_APPLY_TILE=1|2|4)
 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
@@ -76,7 +76,9 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const float* __restr
   const float kmed = fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));
   const double shift = (double)kmed;
 
-  StatAcc acc;
+  // four independent fp64 chains (one per float4 component) so the adds of one iteration do
+  // not serialise behind each other while the next load is in flight
+  StatAcc acc, ay, az, aw;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (vec) {
@@ -85,37 +87,41 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const float* __restr
     for (; i < nv; i += stride) {  // one dwordx4 in flight per lane: a single sweep front
       const float4 v = x4[i];
       acc.add<RANGE>(v.x, shift);
-      acc.add<RANGE>(v.y, shift);
-      acc.add<RANGE>(v.z, shift);
-      acc.add<RANGE>(v.w, shift);
+      ay.add<RANGE>(v.y, shift);
+      az.add<RANGE>(v.z, shift);
+      aw.add<RANGE>(v.w, shift);
     }
     i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
   }
   for (; i < n; i += stride) acc.add<RANGE>(x[i], shift);
+  acc.s1 = (acc.s1 + ay.s1) + (az.s1 + aw.s1);
+  acc.s2 = (acc.s2 + ay.s2) + (az.s2 + aw.s2);
+  if (RANGE) {
+    acc.mn = fminf(fminf(acc.mn, ay.mn), fminf(az.mn, aw.mn));
+    acc.mx = fmaxf(fmaxf(acc.mx, ay.mx), fmaxf(az.mx, aw.mx));
+  }
 
   block_reduce_stats<RANGE>(acc);
   if (threadIdx.x == 0) {
-    StatPartial p;
-    p.s1 = acc.s1;
-    p.s2 = acc.s2;
-    p.mn = acc.mn;
-    p.mx = acc.mx;
-    p.cnt = 0;
-    partials[blockIdx.x] = p;
+    StatPartial* p = partials + blockIdx.x;
+    st_sc1_f64(&p->s1, acc.s1);
+    st_sc1_f64(&p->s2, acc.s2);
+    if (RANGE) st_sc1_f32x2(&p->mn, acc.mn, acc.mx);
   }
   const uint32_t prev = block_arrive(counter, &arrive_slot);
   if (prev != gridDim.x - 1) return;
 
   // Last workgroup: ordered reduction of all partials (deterministic for a given n).
-  block_acquire();
   StatAcc tot;
   for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
-    const StatPartial p = partials[b];
-    tot.s1 += p.s1;
-    tot.s2 += p.s2;
+    const StatPartial* p = partials + b;
+    tot.s1 += ld_sc1_f64(&p->s1);
+    tot.s2 += ld_sc1_f64(&p->s2);
     if (RANGE) {
-      tot.mn = fminf(tot.mn, p.mn);
-      tot.mx = fmaxf(tot.mx, p.mx);
+      float mn, mx;
+      ld_sc1_f32x2(&p->mn, mn, mx);
+      tot.mn = fminf(tot.mn, mn);
+      tot.mx = fmaxf(tot.mx, mx);
     }
   }
   block_reduce_stats<RANGE>(tot);
@@ -131,13 +137,15 @@ struct ApplyArgs {
   int64_t n;
   const float* uniforms;
   const SmqSmaqStats* stats;     // workspace header or injected
-  SmqSmaqStats* ws_stats;        // outlier count destination
+  SmqSmaqStats* ws_stats;        // sampled-stats destination
+  unsigned long long* out_slots; // outlier count slots
   float thr, r_main, r_out, clamp_lo, clamp_hi, range_coef;
   uint32_t key;
   int all_pos;
   int count;
   int use_range;
   int k;                         // sampled mode
+  int reverse;                   // tile order (see smaq_apply_kernel)
   uint64_t offset;
   const float* bn_gamma;         // BN variant
   const float* bn_beta;
@@ -177,10 +185,11 @@ __device__ __forceinline__ void sampled_stats(const ApplyArgs& A, SmqSmaqStats* 
   __syncthreads();
 }
 
-template <int SRC, int RM, bool VEC, bool BN>
+template <int SRC, int RM, bool VEC, bool BN, int kTileV>
 __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
+  constexpr int kTileElems = kBlock * kTileV * 4;
   __shared__ SmqSmaqStats sh_stats;
-  __shared__ unsigned long long sh_cnt[kBlock / kWave];
+  __shared__ uint32_t sh_cnt[kBlock / kWave];
   ElemConsts c;
   if (SRC == SMQ_STATS_SAMPLED) {
     sampled_stats(A, &sh_stats);
@@ -204,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
   init_consts(c, c.mean, c.sd, c.sc, A.thr, A.r_main, A.r_out);
   const bool all_pos = A.all_pos != 0;
 
-  unsigned long long n_out = 0;
+  uint32_t n_out = 0;
   const int64_t n = A.n;
   if (VEC) {
     // flat tile: this workgroup owns float4 [t0, t0 + kBlock * kTileV), kTileV coalesced sweeps
@@ -212,7 +221,10 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
     float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
     const float4* __restrict__ u4 = reinterpret_cast<const float4*>(A.uniforms);
     const int64_t nv = n >> 2;
-    const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kTileV) + threadIdx.x;
+    // Tiles run in REVERSE address order: the statistics launch just swept x forward, so the
+    // last ~256 MB of x are still in the Infinity Cache (MALL) when this launch starts.
+    const int64_t tile = A.reverse ? (int64_t)(gridDim.x - 1 - blockIdx.x) : (int64_t)blockIdx.x;
+    const int64_t t0 = tile * (kBlock * kTileV) + threadIdx.x;
     float4 v[kTileV], uu[kTileV];
 #pragma unroll
     for (int u = 0; u < kTileV; ++u) {
@@ -247,8 +259,8 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
       store_nt(y4 + j, o);
     }
-    // ragged tail (n % 4 elements): the last workgroup
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
+    // ragged tail (n % 4 elements): the workgroup owning the last tile
+    if (tile == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
       const int64_t e = (nv << 2) + threadIdx.x;
       float uf = 0.0f;
       if (RM == kRoundHash) uf = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)e));
@@ -273,14 +285,15 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
     }
   }
 
-  if (A.count) {  // outlier count for log_size (smart.py:184-188), one atomic per workgroup
+  if (A.count) {  // outlier count for log_size (smart.py:184-188): one atomic per workgroup,
+                  // spread over SMQ_WS_OUTLIER_SLOTS addresses
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-    double t = wave_sum((double)n_out);
-    if (lane == 0) sh_cnt[wave] = (unsigned long long)t;
+    const uint32_t t = wave_sum_u32(n_out);
+    if (lane == 0) sh_cnt[wave] = t;
     __syncthreads();
     if (threadIdx.x == 0) {
-      const unsigned long long s = sh_cnt[0] + sh_cnt[1] + sh_cnt[2] + sh_cnt[3];
-      if (s) atomicAdd(&A.ws_stats->n_outlier, s);
+      const unsigned long long s = (unsigned long long)sh_cnt[0] + sh_cnt[1] + sh_cnt[2] + sh_cnt[3];
+      if (s) atomicAdd(A.out_slots + (blockIdx.x & (SMQ_WS_OUTLIER_SLOTS - 1)), s);
     }
   }
 }
@@ -335,10 +348,10 @@ static int launch_stats(const float* x, int64_t n, const SmqSmaqParams* p, void*
   return check_launch("smaq_stats_kernel");
 }
 
-template <int SRC, bool BN>
+template <int SRC, bool BN, int TV>
 static void launch_apply_src(const ApplyArgs& A, int rm, bool vec, int grid, hipStream_t st) {
 #define SMQ_APPLY(RMV, VECV) \
-  hipLaunchKernelGGL((smaq_apply_kernel<SRC, RMV, VECV, BN>), dim3(grid), dim3(kBlock), 0, st, A)
+  hipLaunchKernelGGL((smaq_apply_kernel<SRC, RMV, VECV, BN, TV>), dim3(grid), dim3(kBlock), 0, st, A)
   if (vec) {
     if (rm == kRoundHash) SMQ_APPLY(kRoundHash, true);
     else if (rm == kRoundUniform) SMQ_APPLY(kRoundUniform, true);
@@ -409,33 +422,51 @@ static int launch_apply(const float* x, float* y, int64_t n, const SmqSmaqParams
   }
   const int rm = !p->stochastic_rounding ? kRoundTrunc : (uniforms ? kRoundUniform : kRoundHash);
   const bool vec = aligned16(x) && aligned16(y) && (rm != kRoundUniform || aligned16(uniforms));
-  if (p->count_outliers && p->stats_source != SMQ_STATS_WORKSPACE) {
-    if (hipMemsetAsync(&A.ws_stats->n_outlier, 0, sizeof(unsigned long long), st) != hipSuccess) {
-      set_error("hipMemsetAsync of the outlier counter failed");
+  A.out_slots = (unsigned long long*)((char*)ws + SmaqWsLayout::kSlots);
+  if (p->count_outliers) {
+    if (hipMemsetAsync(A.out_slots, 0, 8 * SMQ_WS_OUTLIER_SLOTS, st) != hipSuccess) {
+      set_error("hipMemsetAsync of the outlier slots failed");
       return SMQ_ERR_LAUNCH;
     }
   }
-  const int64_t tiles = (n + kTileElems - 1) / kTileElems;
+  static const int rev_env = [] {
+    const char* e = getenv("SMQ_APPLY_REVERSE");
+    return e ? atoi(e) : 1;
+  }();
+  // reverse only pays after a forward statistics sweep of the same tensor
+  A.reverse = (p->stats_source == SMQ_STATS_WORKSPACE) ? rev_env : 0;
+  static const int tile_v = [] {
+    const char* e = getenv("SMQ_APPLY_TILE");
+    const int v = e ? atoi(e) : kDefaultTileV;
+    return (v == 1 || v == 2 || v == 4) ? v : kDefaultTileV;
+  }();
+  const int64_t tile_elems = (int64_t)kBlock * tile_v * 4;
+  const int64_t tiles = (n + tile_elems - 1) / tile_elems;
   if (tiles > 0x7fffffffLL) {
     set_error("tensor too large: %lld elements", (long long)n);
     return SMQ_ERR_INVALID;
   }
   const int grid = (int)tiles;
   const bool bn = A.bn_gamma != nullptr;
+#define SMQ_SRC(SRCV)                                                             \
+  do {                                                                            \
+    if (tile_v == 1) {                                                            \
+      if (bn) launch_apply_src<SRCV, true, 1>(A, rm, vec, grid, st);              \
+      else launch_apply_src<SRCV, false, 1>(A, rm, vec, grid, st);                \
+    } else if (tile_v == 2) {                                                     \
+      if (bn) launch_apply_src<SRCV, true, 2>(A, rm, vec, grid, st);              \
+      else launch_apply_src<SRCV, false, 2>(A, rm, vec, grid, st);                \
+    } else {                                                                      \
+      if (bn) launch_apply_src<SRCV, true, 4>(A, rm, vec, grid, st);              \
+      else launch_apply_src<SRCV, false, 4>(A, rm, vec, grid, st);                \
+    }                                                                             \
+  } while (0)
   switch (p->stats_source) {
-    case SMQ_STATS_WORKSPACE:
-      if (bn) launch_apply_src<SMQ_STATS_WORKSPACE, true>(A, rm, vec, grid, st);
-      else launch_apply_src<SMQ_STATS_WORKSPACE, false>(A, rm, vec, grid, st);
-      break;
-    case SMQ_STATS_SAMPLED:
-      if (bn) launch_apply_src<SMQ_STATS_SAMPLED, true>(A, rm, vec, grid, st);
-      else launch_apply_src<SMQ_STATS_SAMPLED, false>(A, rm, vec, grid, st);
-      break;
-    default:
-      if (bn) launch_apply_src<SMQ_STATS_INJECTED, true>(A, rm, vec, grid, st);
-      else launch_apply_src<SMQ_STATS_INJECTED, false>(A, rm, vec, grid, st);
-      break;
+    case SMQ_STATS_WORKSPACE: SMQ_SRC(SMQ_STATS_WORKSPACE); break;
+    case SMQ_STATS_SAMPLED: SMQ_SRC(SMQ_STATS_SAMPLED); break;
+    default: SMQ_SRC(SMQ_STATS_INJECTED); break;
   }
+#undef SMQ_SRC
   return check_launch("smaq_apply_kernel");
 }
 

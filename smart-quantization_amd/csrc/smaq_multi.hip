@@ -83,22 +83,17 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
     return;
   }
   if (threadIdx.x == 0) {
-    StatPartial p;
-    p.s1 = acc.s1;
-    p.s2 = acc.s2;
-    p.mn = 0.f;
-    p.mx = 0.f;
-    p.cnt = 0;
-    A.partials[blockIdx.x] = p;
+    StatPartial* p = A.partials + blockIdx.x;
+    st_sc1_f64(&p->s1, acc.s1);
+    st_sc1_f64(&p->s2, acc.s2);
   }
   const uint32_t prev = block_arrive(&A.counters[ch.tensor], &slot);
   if (prev != (uint32_t)ch.n_chunks - 1) return;
-  block_acquire();
   StatAcc tot;
   for (int b = threadIdx.x; b < ch.n_chunks; b += kBlock) {
-    const StatPartial p = A.partials[ch.first_chunk + b];
-    tot.s1 += p.s1;
-    tot.s2 += p.s2;
+    const StatPartial* p = A.partials + ch.first_chunk + b;
+    tot.s1 += ld_sc1_f64(&p->s1);
+    tot.s2 += ld_sc1_f64(&p->s2);
   }
   block_reduce_stats<false>(tot);
   if (threadIdx.x == 0) {

@@ -79,27 +79,44 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Agent-scope release of this workgroup's plain stores, then an arrival on `counter`.
-// Returns the pre-increment value (same in every thread of the block).
-// Protocol: MI355X_MICROARCH.md §inter-workgroup visibility (producer: stores, vmcnt(0), barrier,
-// lane-0 release + asm vmcnt(0), relaxed agent atomic).
+// Cross-workgroup hand-off of per-workgroup partials WITHOUT release/acquire fences
+// (MI355X_MICROARCH.md §inter-workgroup visibility, "Valid forms", table row 1): the partial is
+// stored write-through (sc1, relaxed agent-scope atomic stores), the storing wave drains vmcnt,
+// then ONE lane adds to ONE counter; the workgroup whose add returned count-1 is last and reads
+// every partial with sc1 loads (bypassing its L1). A per-workgroup release fence (buffer_wbl2)
+// instead measured ~30 % slower on a 1 GiB statistics sweep (2048 fences piling up at the tail).
+__device__ __forceinline__ void st_sc1_u64(void* p, uint64_t v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1_u64(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_f64(void* p, double v) {
+  st_sc1_u64(p, __builtin_bit_cast(uint64_t, v));
+}
+__device__ __forceinline__ double ld_sc1_f64(const void* p) {
+  return __builtin_bit_cast(double, ld_sc1_u64(p));
+}
+__device__ __forceinline__ void st_sc1_f32x2(void* p, float a, float b) {
+  st_sc1_u64(p, (uint64_t)__builtin_bit_cast(uint32_t, a) |
+                    ((uint64_t)__builtin_bit_cast(uint32_t, b) << 32));
+}
+__device__ __forceinline__ void ld_sc1_f32x2(const void* p, float& a, float& b) {
+  const uint64_t v = ld_sc1_u64(p);
+  a = __builtin_bit_cast(float, (uint32_t)v);
+  b = __builtin_bit_cast(float, (uint32_t)(v >> 32));
+}
+
+// Thread 0 has stored this workgroup's partial with st_sc1_*; count the arrival. Returns the
+// pre-increment value in every thread (== expected - 1 in the last workgroup).
 __device__ __forceinline__ uint32_t block_arrive(uint32_t* counter, uint32_t* lds_slot) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 partial stores have landed
     *lds_slot = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   return *lds_slot;
-}
-
-// Consumer side after the last arrival: one agent acquire per wave, then plain loads.
-__device__ __forceinline__ void block_acquire() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 }
 
 // Stats partial of one workgroup: shifted fp64 sums plus fp32 extrema.
@@ -114,8 +131,15 @@ struct alignas(32) StatPartial {
 struct SmaqWsLayout {
   static constexpr size_t kHeader = 64;     // SmqSmaqStats
   static constexpr size_t kCounter = 64;    // arrival counter (own 64-B line)
-  static constexpr size_t kPartials = 128;  // StatPartial[grid]
+  static constexpr size_t kSlots = SMQ_WS_OUTLIER_SLOTS_OFFSET;  // uint64[SMQ_WS_OUTLIER_SLOTS]
+  static constexpr size_t kPartials = kSlots + 8 * SMQ_WS_OUTLIER_SLOTS;  // StatPartial[grid]
 };
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
 
 }  // namespace smq
 

@@ -21,6 +21,8 @@ LIB_PATH = os.environ.get(
 
 SMQ_ABI_VERSION = 1
 SMQ_MAX_SAMPLES = 64
+SMQ_WS_OUTLIER_SLOTS_OFFSET = 128
+SMQ_WS_OUTLIER_SLOTS = 64
 SMQ_STATS_WORKSPACE = 0
 SMQ_STATS_SAMPLED = 1
 SMQ_STATS_INJECTED = 2

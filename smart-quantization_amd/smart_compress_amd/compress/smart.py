@@ -169,7 +169,7 @@ class SmartFP(CompressionAlgorithmBase):
             del keep
 
             def new_size():
-                n_out = int(ws[:64].cpu().numpy().view(np.uint64)[3])
+                n_out = self.outlier_count(ws)
                 return n_out * hp.num_bits_outlier + (numel - n_out) * hp.num_bits_main
 
             self.log_size(tag, numel * 32, new_size)
@@ -198,6 +198,13 @@ class SmartFP(CompressionAlgorithmBase):
 
     # -- inspection helpers (tests / bench) --------------------------------------------------------
     @staticmethod
+    def outlier_count(ws: torch.Tensor) -> int:
+        """Sum of the SMQ_WS_OUTLIER_SLOTS outlier-count slots (include/smq.h)."""
+        off = N.SMQ_WS_OUTLIER_SLOTS_OFFSET
+        slots = ws[off: off + 8 * N.SMQ_WS_OUTLIER_SLOTS].cpu().numpy().view(np.uint64)
+        return int(slots.sum())
+
+    @staticmethod
     def read_stats(ws: torch.Tensor) -> dict:
         raw = ws[:64].cpu().numpy()
         f = raw[:24].view(np.float32)
@@ -205,5 +212,5 @@ class SmartFP(CompressionAlgorithmBase):
             "mean": float(f[0]), "std_dev": float(f[1]), "std_clamped": float(f[2]),
             "raw_std": float(f[3]), "min": float(f[4]), "max": float(f[5]),
             "n_used": int(raw[24:28].view(np.uint32)[0]),
-            "n_outlier": int(raw[32:40].view(np.uint64)[0]),
+            "n_outlier": SmartFP.outlier_count(ws),
         }

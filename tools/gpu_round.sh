@@ -17,7 +17,11 @@ for s in "$@"; do
     tests_all) step pytest_gpu_all 1200 python -m pytest tests -m gpu -q ;;
     slow) step pytest_slow 600 python -m pytest tests -m "gpu and slow" -q ;;
     membench) step membench 300 ./tools/membench ;;
+    statsbench) step statsbench 300 ./tools/statsbench ;;
     kbench) step kbench 300 python tools/kbench.py ;;
+    rev) for r in 0 1; do SMQ_APPLY_REVERSE=$r step kbench_rev$r 300 python tools/kbench.py --quick; done ;;
+    tiles) for v in 1 2 4; do SMQ_APPLY_TILE=$v step kbench_tile$v 300 python tools/kbench.py --quick; done ;;
+    profile) step profile 1500 bash tools/profile_round.sh r01 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 --cpu-budget 8 ;;
     bench_all) step bench_fp8 300 python bench.py --config fp8 --steps 50 --warmup 5 &&

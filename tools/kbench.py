@@ -31,10 +31,31 @@ def timed(fn, reps):
     return float(np.median(ts))
 
 
+class Interleaved:
+    """Variants timed in interleaved rounds in one process (methodology rule: A/B deltas only
+    from interleaved runs); reports the median over all rounds."""
+
+    def __init__(self):
+        self.fns, self.ts = {}, {}
+
+    def add(self, name, fn, bytes_):
+        self.fns[name] = (fn, bytes_)
+        self.ts[name] = []
+
+    def run(self, rounds, reps):
+        for _ in range(rounds):
+            for name, (fn, _) in self.fns.items():
+                self.ts[name].append(timed(fn, reps))
+        return {k: dict(ms=float(np.median(v)), GBps=self.fns[k][1] / float(np.median(v)) / 1e6)
+                for k, v in self.ts.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 28)
-    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--quick", action="store_true", help="SmaQ variants only")
     args = ap.parse_args()
     n = args.n
     lib = N.lib()
@@ -42,7 +63,7 @@ def main():
     y = torch.empty_like(x)
     st = torch.cuda.current_stream().cuda_stream
     ws = torch.zeros(lib.smq_smaq_workspace_bytes(n), dtype=torch.uint8, device="cuda")
-    out = {"n": n}
+    out = {"n": n, "SMQ_APPLY_TILE": os.environ.get("SMQ_APPLY_TILE", "default")}
 
     def params(**kw):
         p = N.SmqSmaqParams()
@@ -52,26 +73,24 @@ def main():
         return p
 
     p = params()
-    stats = lambda: N.check(lib.smq_smaq_stats_f32(x.data_ptr(), n, p, ws.data_ptr(), ws.numel(), st), "s")
-    ms = timed(stats, args.reps)
-    out["stats"] = dict(ms=ms, GBps=4 * n / ms / 1e6)
+    iv = Interleaved()
+    iv.add("stats", lambda: N.check(lib.smq_smaq_stats_f32(x.data_ptr(), n, p, ws.data_ptr(),
+                                                           ws.numel(), st), "s"), 4 * n)
     for name, pp in (("apply_sr", params()), ("apply_trunc", params(stochastic_rounding=0)),
                      ("apply_sr_allpos", params(all_positive=1)),
                      ("apply_sr_count", params(count_outliers=1))):
-        f = lambda pp=pp: N.check(lib.smq_smaq_apply_f32(x.data_ptr(), y.data_ptr(), n, pp, None, None,
-                                                         ws.data_ptr(), ws.numel(), st), "a")
-        ms = timed(f, args.reps)
-        out[name] = dict(ms=ms, GBps=8 * n / ms / 1e6)
+        iv.add(name, lambda pp=pp: N.check(lib.smq_smaq_apply_f32(
+            x.data_ptr(), y.data_ptr(), n, pp, None, None, ws.data_ptr(), ws.numel(), st), "a"), 8 * n)
     ps = params(stats_source=N.SMQ_STATS_SAMPLED)
     lib.smq_smaq_draw_samples(ps, n, 16)
-    f = lambda: N.check(lib.smq_smaq_apply_f32(x.data_ptr(), y.data_ptr(), n, ps, None, None,
-                                               ws.data_ptr(), ws.numel(), st), "a")
-    ms = timed(f, args.reps)
-    out["apply_sampled"] = dict(ms=ms, GBps=8 * n / ms / 1e6)
-    rt = lambda: N.check(lib.smq_smaq_roundtrip_f32(x.data_ptr(), y.data_ptr(), n, p, None,
-                                                    ws.data_ptr(), ws.numel(), st), "r")
-    ms = timed(rt, args.reps)
-    out["roundtrip"] = dict(ms=ms, GBps=12 * n / ms / 1e6)
+    iv.add("apply_sampled", lambda: N.check(lib.smq_smaq_apply_f32(
+        x.data_ptr(), y.data_ptr(), n, ps, None, None, ws.data_ptr(), ws.numel(), st), "a"), 8 * n)
+    iv.add("roundtrip", lambda: N.check(lib.smq_smaq_roundtrip_f32(
+        x.data_ptr(), y.data_ptr(), n, p, None, ws.data_ptr(), ws.numel(), st), "r"), 12 * n)
+    out.update(iv.run(args.rounds, args.reps))
+    if args.quick:
+        print(json.dumps(out, indent=1))
+        return
     for e, m in ((5, 2), (5, 10), (8, 7)):
         f = lambda e=e, m=m: N.check(lib.smq_float_quant_f32(x.data_ptr(), y.data_ptr(), n, e, m, 1, 1,
                                                              None, 1, 0, st), "f")
