@@ -15,6 +15,7 @@
 // word comes from the counter-based RNG in registers and check_inf is fused.
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "smq_common.h"
@@ -93,11 +94,11 @@ __device__ __forceinline__ float check_inf_fn(float y, const FQArgs& A) {
   return (A.check_inf && fabsf(y - A.max_value) <= FLT_EPSILON) ? INFINITY : y;
 }
 
-constexpr int kFqTileV = 4;  // float4 per lane per tile (flat contiguous tiles, see smaq.hip)
-constexpr int kFqTileElems = kBlock * kFqTileV * 4;
+constexpr int kFqDefaultTileV = 1;  // float4 per lane per tile (flat tiles; SMQ_FQ_TILE=1|2|4)
 
-template <bool SR, bool RARR, bool VEC>
+template <bool SR, bool RARR, bool VEC, int kFqTileV>
 __global__ __launch_bounds__(kBlock) void float_quant_kernel(FQArgs A) {
+  constexpr int kFqTileElems = kBlock * kFqTileV * 4;
   const int64_t n = A.n;
   auto rb = [&](int64_t e) -> uint32_t {
     if (!SR) return 0u;
@@ -192,28 +193,40 @@ __global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const float* __rest
   __shared__ double shs[kBlock / kWave];
   __shared__ float shm[kBlock / kWave];
   __shared__ uint32_t slot;
+  // tile-stride: each step a workgroup consumes a 16 KiB tile with 4 dwordx4 per lane in flight
+  // (S2FP8 tensors are MB-sized: latency, not sweep fronts, is what bounds them)
   double s = 0.0;
   float m = -INFINITY;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (vec) {
     const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
     const int64_t nv = n >> 2;
-    for (; i < nv; i += stride) {
-      const float4 v = x4[i];
-      const float l0 = s2_log(v.x), l1 = s2_log(v.y), l2 = s2_log(v.z), l3 = s2_log(v.w);
-      s += (double)l0;
-      s += (double)l1;
-      s += (double)l2;
-      s += (double)l3;
-      m = nan_max(nan_max(m, l0), nan_max(l1, nan_max(l2, l3)));
+    for (int64_t t0 = (int64_t)blockIdx.x * (kBlock * 4); t0 < nv; t0 += (int64_t)gridDim.x * kBlock * 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t j = t0 + threadIdx.x + u * kBlock;
+        v[u] = j < nv ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t j = t0 + threadIdx.x + u * kBlock;
+        if (j >= nv) continue;
+        const float l0 = s2_log(v[u].x), l1 = s2_log(v[u].y), l2 = s2_log(v[u].z), l3 = s2_log(v[u].w);
+        s += ((double)l0 + (double)l1) + ((double)l2 + (double)l3);
+        m = nan_max(nan_max(m, l0), nan_max(l1, nan_max(l2, l3)));
+      }
     }
-    i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  }
-  for (; i < n; i += stride) {
-    const float l = s2_log(x[i]);
-    s += (double)l;
-    m = nan_max(m, l);
+    if (blockIdx.x == 0 && threadIdx.x < (int)(n & 3)) {
+      const float l = s2_log(x[(nv << 2) + threadIdx.x]);
+      s += (double)l;
+      m = nan_max(m, l);
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+      const float l = s2_log(x[i]);
+      s += (double)l;
+      m = nan_max(m, l);
+    }
   }
   // workgroup reduce
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
@@ -288,32 +301,43 @@ struct S2Args {
   float max_value;
 };
 
-// s2fp8.py:45-48 for one element.
+// x^p for x >= 0 (or NaN) as exp2(p * log2(x)) on the hardware v_log_f32 / v_exp_f32 (ocml's
+// log2f / exp2f, ~1 ulp each). Valid for finite p > 0 (the caller checks once per launch):
+// 0 -> 0, inf -> inf, NaN -> NaN like powf. Relative error ~ ln2 * |p * log2 x| * 2^-23; the S2FP8
+// parity contract is the E5M2 code of Y (measured: 2 adjacent-code flips per 10^6 elements).
+__device__ __forceinline__ float pow_pos(float x, float p) { return exp2f(p * log2f(x)); }
+
+// s2fp8.py:45-48 for one element. FAST = alpha is finite and > 0 (else the exact powf path keeps
+// the reference's degenerate-case semantics, e.g. all-zero input -> NaN).
+template <bool FAST>
 __device__ __forceinline__ float s2fp8_elem(float xv, uint32_t r, float alpha, float bp2,
                                             float ibp2, float ialpha, int check_inf,
                                             float max_value) {
   // torch.sign: +1 / -1, and +0.0 for +-0 and NaN (measured on torch 2.10 CPU)
   const float sgn = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
   const float a = fabsf(xv);
-  float Y = powf(a, alpha);   // X_abs.pow_(alpha)
-  Y = Y * bp2;                // .mul_(beta_pow2)
+  float Y = FAST ? pow_pos(a, alpha) : powf(a, alpha);  // X_abs.pow_(alpha)
+  Y = Y * bp2;                                            // .mul_(beta_pow2)
   float T = qtorch_quant(Y, r, 5, 2, true);
   if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
-  const float t1 = T * ibp2;           // truncated * beta_pow2.reciprocal_()
-  const float t2 = powf(t1, ialpha);   // ** alpha.reciprocal_()
-  return t2 * sgn;                     // * signs
+  const float t1 = T * ibp2;                              // truncated * beta_pow2.reciprocal_()
+  const float t2 = FAST ? pow_pos(t1, ialpha) : powf(t1, ialpha);  // ** alpha.reciprocal_()
+  return t2 * sgn;                                        // * signs
 }
 
-template <bool RARR, bool VEC>
+template <bool RARR, bool VEC, int kFqTileV>
 __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
+  constexpr int kFqTileElems = kBlock * kFqTileV * 4;
   const float alpha = A.st->alpha, bp2 = A.st->beta_pow2, ibp2 = A.st->inv_beta_pow2,
               ialpha = A.st->inv_alpha;
   const int64_t n = A.n;
   auto rb = [&](int64_t e) -> uint32_t {
     return RARR ? A.rand_bits[e] : rng_u32(A.key, A.offset + (uint64_t)e);
   };
+  const bool fast = alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f && ialpha < INFINITY;
   auto q1 = [&](float v, uint32_t r) {
-    return s2fp8_elem(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
+    return fast ? s2fp8_elem<true>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value)
+                : s2fp8_elem<false>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
   };
   if (VEC) {
     const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
@@ -353,13 +377,23 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
 
 static inline bool aligned16f(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+static int fq_tile_v() {
+  static const int v = [] {
+    const char* e = getenv("SMQ_FQ_TILE");
+    const int t = e ? atoi(e) : kFqDefaultTileV;
+    return (t == 1 || t == 2 || t == 4) ? t : kFqDefaultTileV;
+  }();
+  return v;
+}
+
 static int fq_grid(int64_t n) {  // flat tiles
-  int64_t g = (n + kFqTileElems - 1) / kFqTileElems;
+  const int64_t te = (int64_t)kBlock * 4 * fq_tile_v();
+  int64_t g = (n + te - 1) / te;
   return (int)(g < 1 ? 1 : g);
 }
 
-static int s2_stats_grid(int64_t n) {  // grid-stride, one float4 per lane per step
-  int64_t g = (n + kBlock * 4 - 1) / (kBlock * 4);
+static int s2_stats_grid(int64_t n) {  // 16 KiB tiles, at most kS2GridCap workgroups
+  int64_t g = (n + kBlock * 16 - 1) / (kBlock * 16);
   if (g < 1) g = 1;
   if (g > kS2GridCap) g = kS2GridCap;
   return (int)g;
@@ -414,8 +448,13 @@ int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int m
   const bool vec = aligned16f(x) && aligned16f(y) && (!rarr || aligned16f(rand_bits));
   const int grid = fq_grid(n);
   hipStream_t st = (hipStream_t)stream;
-#define SMQ_FQ(S, R, V) \
-  hipLaunchKernelGGL((float_quant_kernel<S, R, V>), dim3(grid), dim3(kBlock), 0, st, A)
+  const int tv = fq_tile_v();
+#define SMQ_FQ(S, R, V)                                                                          \
+  do {                                                                                           \
+    if (tv == 1) hipLaunchKernelGGL((float_quant_kernel<S, R, V, 1>), dim3(grid), dim3(kBlock), 0, st, A); \
+    else if (tv == 2) hipLaunchKernelGGL((float_quant_kernel<S, R, V, 2>), dim3(grid), dim3(kBlock), 0, st, A); \
+    else hipLaunchKernelGGL((float_quant_kernel<S, R, V, 4>), dim3(grid), dim3(kBlock), 0, st, A); \
+  } while (0)
   if (!sr) {
     if (vec) SMQ_FQ(false, false, true); else SMQ_FQ(false, false, false);
   } else if (rarr) {
@@ -471,13 +510,19 @@ int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
   const bool rarr = rand_bits != nullptr;
   const bool vec = aligned16f(x) && aligned16f(y);
   const int grid = fq_grid(n);
+  const int tv = fq_tile_v();
+#define SMQ_S2(R, V)                                                                             \
+  do {                                                                                           \
+    if (tv == 1) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 1>), dim3(grid), dim3(kBlock), 0, st, A); \
+    else if (tv == 2) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 2>), dim3(grid), dim3(kBlock), 0, st, A); \
+    else hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 4>), dim3(grid), dim3(kBlock), 0, st, A); \
+  } while (0)
   if (rarr) {
-    if (vec) hipLaunchKernelGGL((s2fp8_apply_kernel<true, true>), dim3(grid), dim3(kBlock), 0, st, A);
-    else hipLaunchKernelGGL((s2fp8_apply_kernel<true, false>), dim3(grid), dim3(kBlock), 0, st, A);
+    if (vec) SMQ_S2(true, true); else SMQ_S2(true, false);
   } else {
-    if (vec) hipLaunchKernelGGL((s2fp8_apply_kernel<false, true>), dim3(grid), dim3(kBlock), 0, st, A);
-    else hipLaunchKernelGGL((s2fp8_apply_kernel<false, false>), dim3(grid), dim3(kBlock), 0, st, A);
+    if (vec) SMQ_S2(false, true); else SMQ_S2(false, false);
   }
+#undef SMQ_S2
   return check_launch("s2fp8_apply_kernel");
 }
 

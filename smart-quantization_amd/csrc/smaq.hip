@@ -163,7 +163,7 @@ __device__ __forceinline__ BnTerm bn_term(const ApplyArgs& A, int64_t e) {
 // Sampled statistics (smart.py:86-91): mean and biased std (or range-std) of k gathered elements,
 // computed by wave 0 of every workgroup in the same order -> identical in all workgroups.
 __device__ __forceinline__ void sampled_stats(const ApplyArgs& A, SmqSmaqStats* sh) {
-  if (threadIdx.x < kWave) {
+  if (threadIdx.x < kWave) {  // one wave; the caller's workgroup may be larger
     const int lane = threadIdx.x;
     const bool valid = lane < A.k;
     const float v = valid ? A.x[A.sample_idx[lane]] : 0.0f;
@@ -185,31 +185,23 @@ __device__ __forceinline__ void sampled_stats(const ApplyArgs& A, SmqSmaqStats* 
   __syncthreads();
 }
 
+// One wave computes the sampled statistics into the workspace header; the apply launch then reads
+// them like full statistics (cheaper than a 16-element gather + fp64 reduction in each of 10^5
+// apply workgroups).
+__global__ __launch_bounds__(kWave) void smaq_sample_stats_kernel(ApplyArgs A) {
+  __shared__ SmqSmaqStats sh;
+  sampled_stats(A, &sh);
+  if (threadIdx.x == 0) *A.ws_stats = sh;
+}
+
 template <int SRC, int RM, bool VEC, bool BN, int kTileV>
 __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
   constexpr int kTileElems = kBlock * kTileV * 4;
-  __shared__ SmqSmaqStats sh_stats;
   __shared__ uint32_t sh_cnt[kBlock / kWave];
   ElemConsts c;
-  if (SRC == SMQ_STATS_SAMPLED) {
-    sampled_stats(A, &sh_stats);
-    c.mean = sh_stats.mean;
-    c.sd = sh_stats.std_dev;
-    c.sc = sh_stats.std_clamped;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      A.ws_stats->mean = sh_stats.mean;
-      A.ws_stats->std_dev = sh_stats.std_dev;
-      A.ws_stats->std_clamped = sh_stats.std_clamped;
-      A.ws_stats->raw_std = sh_stats.raw_std;
-      A.ws_stats->min_val = sh_stats.min_val;
-      A.ws_stats->max_val = sh_stats.max_val;
-      A.ws_stats->n_used = sh_stats.n_used;
-    }
-  } else {
-    c.mean = A.stats->mean;
-    c.sd = A.stats->std_dev;
-    c.sc = A.stats->std_clamped;
-  }
+  c.mean = A.stats->mean;
+  c.sd = A.stats->std_dev;
+  c.sc = A.stats->std_clamped;
   init_consts(c, c.mean, c.sd, c.sc, A.thr, A.r_main, A.r_out);
   const bool all_pos = A.all_pos != 0;
 
@@ -461,11 +453,12 @@ static int launch_apply(const float* x, float* y, int64_t n, const SmqSmaqParams
       else launch_apply_src<SRCV, false, 4>(A, rm, vec, grid, st);                \
     }                                                                             \
   } while (0)
-  switch (p->stats_source) {
-    case SMQ_STATS_WORKSPACE: SMQ_SRC(SMQ_STATS_WORKSPACE); break;
-    case SMQ_STATS_SAMPLED: SMQ_SRC(SMQ_STATS_SAMPLED); break;
-    default: SMQ_SRC(SMQ_STATS_INJECTED); break;
+  if (p->stats_source == SMQ_STATS_SAMPLED) {
+    hipLaunchKernelGGL(smaq_sample_stats_kernel, dim3(1), dim3(kWave), 0, st, A);
+    A.stats = A.ws_stats;
   }
+  if (p->stats_source == SMQ_STATS_INJECTED) SMQ_SRC(SMQ_STATS_INJECTED);
+  else SMQ_SRC(SMQ_STATS_WORKSPACE);
 #undef SMQ_SRC
   return check_launch("smaq_apply_kernel");
 }

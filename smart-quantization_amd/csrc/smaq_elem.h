@@ -143,7 +143,8 @@ __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c
   if (BN) v = (v - bn.beta) / bn.gamma;                 // (data - beta) / gamma
   const float dm = v - c.mean;                          // data - mean
   float z = div_by_const(dm, c.inv_sc);                 // / std.clamp(...)
-  if (__builtin_expect(fabsf(z) < 1.17549435e-38f && z != 0.0f, 0)) z = dm / c.sc;
+  // subnormal quotient (class mask 0x90 = -/+ denormal, one v_cmp_class_f32): IEEE division
+  if (__builtin_expect(__builtin_amdgcn_class(z, 0x90), 0)) z = dm / c.sc;
   const bool hi = z > c.thr;                            // is_outlier_higher
   const bool lo = z < c.nthr;                           // is_outlier_lower
   const bool o = hi | lo;                               // is_outlier

@@ -4,7 +4,7 @@
 // (grads, weights, momenta), each of which runs smart.py:110-190 separately (~24 ATen launches
 // + 1 host sync per tensor; a ResNet-34 step has 148 such tensors, median 256 elements).
 //
-// Design: the tensors are cut into fixed chunks (kChunk elements); one workgroup per chunk.
+// Design: the tensors are cut into fixed chunks (8192 elements by default); one workgroup per chunk.
 //   launch 1 (stats): per-chunk shifted fp64 sums; a tensor with one chunk finalises in place,
 //            a larger tensor's last-arriving chunk reduces that tensor's partials in chunk order.
 //   launch 2 (apply): per chunk, the tensor's SmqSmaqStats + the element transform of smaq.hip,
@@ -19,7 +19,7 @@
 
 namespace smq {
 
-constexpr int64_t kChunk = 32768;  // elements per workgroup (128 KiB of fp32)
+constexpr int64_t kDefaultChunk = 8192;  // elements per workgroup (SMQ_MULTI_CHUNK, multiple of 4096)
 
 struct MultiHeader {
   int32_t count;
@@ -28,16 +28,22 @@ struct MultiHeader {
   int64_t reserved[2];
 };
 
+// Everything one workgroup needs, in ONE 64-B record (uniform per workgroup -> two s_load_dwordx8):
+// no dependent descriptor loads stand between the launch and the first data load.
 struct ChunkDesc {
+  const float* x;       // tensor base
+  float* y;
+  int64_t n;            // tensor elements
+  int64_t begin, end;   // element range of this chunk within the tensor
+  uint64_t rng_offset;  // tensor's RNG offset relative to params.offset
   int32_t tensor;
   int32_t first_chunk;  // global index of the tensor's first chunk
   int32_t n_chunks;     // chunks of this tensor
-  int32_t pad;
-  int64_t begin, end;   // element range within the tensor
+  int32_t all_positive;
 };
 
 static_assert(sizeof(MultiHeader) == 32, "plan header");
-static_assert(sizeof(ChunkDesc) == 32, "chunk desc");
+static_assert(sizeof(ChunkDesc) == 64, "chunk desc");
 
 struct MultiArgs {
   const MultiHeader* hdr;
@@ -56,22 +62,33 @@ struct MultiArgs {
 __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   __shared__ uint32_t slot;
   const ChunkDesc ch = A.chunks[blockIdx.x];
-  const SmqTensorDesc d = A.descs[ch.tensor];
-  const float* __restrict__ x = d.x;
-  const int64_t n = d.n;
+  const float* __restrict__ x = ch.x;
+  const int64_t n = ch.n;
   const float k0 = x[0], k1 = x[n >> 1], k2 = x[n - 1];
   const double shift = (double)fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));
   StatAcc acc;
-  int64_t i = ch.begin + threadIdx.x * 4;
   if (((uintptr_t)x & 15u) == 0) {
-    for (; i + 3 < ch.end; i += kBlock * 4) {
-      const float4 v = *reinterpret_cast<const float4*>(x + i);
-      acc.add<false>(v.x, shift);
-      acc.add<false>(v.y, shift);
-      acc.add<false>(v.z, shift);
-      acc.add<false>(v.w, shift);
+    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+    const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;  // begin is a multiple of the chunk
+    for (int64_t t0 = b4; t0 < e4; t0 += 4 * kBlock) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = t0 + threadIdx.x + u * kBlock;
+      v[u] = j < e4 ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    for (; i < ch.end; ++i) acc.add<false>(x[i], shift);  // ragged tail: one thread, <4 elems
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = t0 + threadIdx.x + u * kBlock;
+      if (j < e4) {
+        acc.add<false>(v[u].x, shift);
+        acc.add<false>(v[u].y, shift);
+        acc.add<false>(v[u].z, shift);
+        acc.add<false>(v[u].w, shift);
+      }
+    }
+    }
+    if (threadIdx.x < (int)(ch.end - (e4 << 2))) acc.add<false>(x[(e4 << 2) + threadIdx.x], shift);
   } else {
     for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) acc.add<false>(x[j], shift);
   }
@@ -106,20 +123,30 @@ template <bool SR>
 __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
   __shared__ unsigned long long sh_cnt[kBlock / kWave];
   const ChunkDesc ch = A.chunks[blockIdx.x];
-  const SmqTensorDesc d = A.descs[ch.tensor];
   const SmqSmaqStats* st = &A.stats[ch.tensor];
   ElemConsts c;
   init_consts(c, st->mean, st->std_dev, st->std_clamped, A.thr, A.r_main, A.r_out);
-  const bool all_pos = d.all_positive != 0;
-  const float* __restrict__ x = d.x;
-  float* y = d.y;  // may alias x
+  const bool all_pos = ch.all_positive != 0;
+  const float* __restrict__ x = ch.x;
+  float* y = ch.y;  // may alias x
   unsigned long long n_out = 0;
   constexpr int RM = SR ? kRoundHash : kRoundTrunc;
-  int64_t i = ch.begin + threadIdx.x * 4;
   if ((((uintptr_t)x | (uintptr_t)y) & 15u) == 0) {
-    for (; i + 3 < ch.end; i += kBlock * 4) {
-      const float4 v = *reinterpret_cast<const float4*>(x + i);
-      const uint64_t ctr = A.offset + d.rng_offset + (uint64_t)i;
+    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+    float4* y4 = reinterpret_cast<float4*>(y);
+    const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;
+    for (int64_t t0 = b4; t0 < e4; t0 += 4 * kBlock) {  // 16 KiB per step, 4 dwordx4 per lane
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = t0 + threadIdx.x + u * kBlock;
+      if (j < e4) v[u] = x4[j];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = t0 + threadIdx.x + u * kBlock;
+      if (j >= e4) continue;
+      const uint64_t ctr = A.offset + ch.rng_offset + ((uint64_t)j << 2);
       float u0 = 0.f, u1 = 0.f, u2 = 0.f, u3 = 0.f;
       if (SR) {
         u0 = u32_to_unit(rng_u32(A.key, ctr));
@@ -129,22 +156,24 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
       }
       bool b0, b1, b2, b3;
       float4 o;
-      o.x = smaq_elem<RM>(v.x, u0, c, all_pos, b0);
-      o.y = smaq_elem<RM>(v.y, u1, c, all_pos, b1);
-      o.z = smaq_elem<RM>(v.z, u2, c, all_pos, b2);
-      o.w = smaq_elem<RM>(v.w, u3, c, all_pos, b3);
+      o.x = smaq_elem<RM>(v[u].x, u0, c, all_pos, b0);
+      o.y = smaq_elem<RM>(v[u].y, u1, c, all_pos, b1);
+      o.z = smaq_elem<RM>(v[u].z, u2, c, all_pos, b2);
+      o.w = smaq_elem<RM>(v[u].w, u3, c, all_pos, b3);
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
-      *reinterpret_cast<float4*>(y + i) = o;
+      y4[j] = o;
     }
-    for (; i < ch.end; ++i) {
-      const float u = SR ? u32_to_unit(rng_u32(A.key, A.offset + d.rng_offset + (uint64_t)i)) : 0.f;
+    }
+    if (threadIdx.x < (int)(ch.end - (e4 << 2))) {
+      const int64_t e = (e4 << 2) + threadIdx.x;
+      const float u = SR ? u32_to_unit(rng_u32(A.key, A.offset + ch.rng_offset + (uint64_t)e)) : 0.f;
       bool b;
-      y[i] = smaq_elem<RM>(x[i], u, c, all_pos, b);
+      y[e] = smaq_elem<RM>(x[e], u, c, all_pos, b);
       n_out += (unsigned)b;
     }
   } else {
     for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) {
-      const float u = SR ? u32_to_unit(rng_u32(A.key, A.offset + d.rng_offset + (uint64_t)j)) : 0.f;
+      const float u = SR ? u32_to_unit(rng_u32(A.key, A.offset + ch.rng_offset + (uint64_t)j)) : 0.f;
       bool b;
       y[j] = smaq_elem<RM>(x[j], u, c, all_pos, b);
       n_out += (unsigned)b;
@@ -162,7 +191,16 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
   }
 }
 
-static int64_t chunks_of(int64_t n) { return (n + kChunk - 1) / kChunk; }
+static int64_t chunk_elems() {
+  static const int64_t c = [] {
+    const char* e = getenv("SMQ_MULTI_CHUNK");
+    const int64_t v = e ? atoll(e) : kDefaultChunk;
+    return (v >= 4096 && v % 4096 == 0) ? v : kDefaultChunk;
+  }();
+  return c;
+}
+
+static int64_t chunks_of(int64_t n) { return (n + chunk_elems() - 1) / chunk_elems(); }
 
 struct PlanSizes {
   size_t hdr, descs, chunks, total;
@@ -226,7 +264,8 @@ int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_
   MultiHeader* h = (MultiHeader*)base;
   h->count = count;
   h->n_chunks = (int32_t)ps.n_chunks;
-  h->chunk = kChunk;
+  const int64_t C = chunk_elems();
+  h->chunk = C;
   memcpy(base + ps.hdr, descs, sizeof(SmqTensorDesc) * (size_t)count);
   ChunkDesc* ch = (ChunkDesc*)(base + ps.hdr + ps.descs);
   int32_t g = 0;
@@ -234,11 +273,16 @@ int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_
     const int64_t nc = chunks_of(descs[t].n);
     const int32_t first = g;
     for (int64_t c = 0; c < nc; ++c, ++g) {
+      ch[g].x = descs[t].x;
+      ch[g].y = descs[t].y;
+      ch[g].n = descs[t].n;
+      ch[g].begin = c * C;
+      ch[g].end = (c + 1) * C < descs[t].n ? (c + 1) * C : descs[t].n;
+      ch[g].rng_offset = descs[t].rng_offset;
       ch[g].tensor = t;
       ch[g].first_chunk = first;
       ch[g].n_chunks = (int32_t)nc;
-      ch[g].begin = c * kChunk;
-      ch[g].end = (c + 1) * kChunk < descs[t].n ? (c + 1) * kChunk : descs[t].n;
+      ch[g].all_positive = descs[t].all_positive;
     }
   }
   return SMQ_OK;

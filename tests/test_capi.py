@@ -126,26 +126,38 @@ def test_multi_plan_layout():
     from smart_compress_amd import _native as N
 
     lib = N.lib()
-    sizes = [10, 32768, 32769, 100000]
+    C = 8192  # default chunk (csrc/smaq_multi.hip kDefaultChunk)
+    sizes = [10, C, C + 1, 3 * C + 5]
     count = len(sizes)
     arr = (ctypes.c_int64 * count)(*sizes)
     nbytes = lib.smq_smaq_multi_plan_bytes(arr, count)
     chunks = [1, 1, 2, 4]
-    assert nbytes == 32 + ((40 * count + 31) // 32) * 32 + 32 * sum(chunks)
+    dbytes = ((40 * count + 31) // 32) * 32
+    assert nbytes == 32 + dbytes + 64 * sum(chunks)
     descs = (N.SmqTensorDesc * count)()
+    rel = 0
     for i, n in enumerate(sizes):
         descs[i].x = descs[i].y = 0x1000 * (i + 1)
         descs[i].n = n
+        descs[i].all_positive = i % 2
+        descs[i].rng_offset = rel
+        rel += n
     host = (ctypes.c_uint8 * nbytes)()
     assert lib.smq_smaq_multi_plan_build(descs, count, host, nbytes) == 0
     raw = np.frombuffer(bytes(host), dtype=np.uint8)
-    hdr = raw[:8].view(np.int32)
-    assert list(hdr) == [count, sum(chunks)]
-    cstart = 32 + ((40 * count + 31) // 32) * 32
-    ch = raw[cstart:].view(np.int64).reshape(-1, 4)
-    tensor = (ch[:, 0] & 0xFFFFFFFF).astype(np.int32)
-    assert list(tensor) == [0, 1, 2, 2, 3, 3, 3, 3]
-    assert list(ch[:, 3]) == [10, 32768, 32768, 32769, 32768, 65536, 98304, 100000]
+    assert list(raw[:8].view(np.int32)) == [count, sum(chunks)]
+    assert int(raw[8:16].view(np.int64)[0]) == C
+    rec = raw[32 + dbytes:].reshape(-1, 64)
+    q = rec[:, :48].copy().view(np.int64)  # x, y, n, begin, end, rng_offset
+    i32 = rec[:, 48:].copy().view(np.int32)  # tensor, first_chunk, n_chunks, all_positive
+    assert list(i32[:, 0]) == [0, 1, 2, 2, 3, 3, 3, 3]
+    assert list(i32[:, 1]) == [0, 1, 2, 2, 4, 4, 4, 4]
+    assert list(i32[:, 2]) == [1, 1, 2, 2, 4, 4, 4, 4]
+    assert list(i32[:, 3]) == [0, 1, 0, 0, 1, 1, 1, 1]
+    assert list(q[:, 0]) == [0x1000, 0x2000, 0x3000, 0x3000, 0x4000, 0x4000, 0x4000, 0x4000]
+    assert list(q[:, 3]) == [0, 0, 0, C, 0, C, 2 * C, 3 * C]
+    assert list(q[:, 4]) == [10, C, C, C + 1, C, 2 * C, 3 * C, 3 * C + 5]
+    assert list(q[:, 5]) == [0, 10, 10 + C, 10 + C, 10 + 2 * C + 1] + [10 + 2 * C + 1] * 3
     assert lib.smq_smaq_multi_workspace_bytes(arr, count) >= 64 * count + 32 * sum(chunks)
     descs[1].n = 0
     assert lib.smq_smaq_multi_plan_build(descs, count, host, nbytes) == -1
