@@ -70,6 +70,8 @@ def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SMQ_BENCH_SHARE_DEVICE") == "1":
+        local = 0  # rehearsal of the N>1 flow on a 1-GPU box (gloo collectives, shared card)
     if world > 1:
         import torch.distributed as dist
 
@@ -91,12 +93,18 @@ def barrier(world):
         dist.barrier()
 
 
+def _coll_device(device):
+    import torch.distributed as dist
+
+    return device if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
 def max_over_ranks(value, world, device):
     if world == 1:
         return value
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -106,7 +114,7 @@ def sum_over_ranks(value, world, device):
         return value
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
@@ -187,7 +195,7 @@ def traffic_from_profile(config):
 def run_smaq(args, world, rank, device):
     from smart_compress_amd.compress.smart import SmartFP
 
-    n = args.n or (1 << 28)
+    n = args.elements or (1 << 28)
     sampled = args.config == "smaq_sampled"
     hp = smaq_hparams(use_sample_stats=sampled)
     codec = SmartFP(hp)
@@ -356,7 +364,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="smaq",
                     choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi"])
-    ap.add_argument("--n", type=int, default=0, help="override elements (smaq configs)")
+    ap.add_argument("--elements", type=int, default=0, help="override elements (smaq configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 22)
     ap.add_argument("--cpu-budget", type=float, default=12.0)

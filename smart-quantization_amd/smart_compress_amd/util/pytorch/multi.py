@@ -10,6 +10,7 @@ The plan (descriptor table + chunk map) is cached by the list's pointers and siz
 loop whose parameter and gradient buffers stay put uploads it once.
 """
 
+import copy
 import ctypes
 from typing import List, Optional, Sequence
 
@@ -21,12 +22,16 @@ from ...compress.smart import SmartFP
 
 
 class SmaqMulti:
-    def __init__(self, hparams, seed: Optional[int] = None):
+    def __init__(self, hparams, seed: Optional[int] = None, rng: Optional[N.RngState] = None):
         if hparams.use_sample_stats or hparams.use_range_std_dev:
             raise NotImplementedError("SmaqMulti supports full statistics only")
         self.hparams = hparams
-        self._codec = SmartFP(hparams)  # constants + parameter block
-        self.rng = N.RngState(seed if seed is not None else getattr(hparams, "smq_seed", None))
+        internal = copy.copy(hparams)
+        internal.smq_seed = 0  # the internal codec only builds parameter blocks: no torch RNG draw
+        self._codec = SmartFP(internal)
+        if rng is None:
+            rng = N.RngState(seed if seed is not None else getattr(hparams, "smq_seed", None))
+        self.rng = rng  # shared with a SmartFP codec when fused into its optimizer calls
         self._plans = {}
         self._last = None
 
@@ -93,6 +98,7 @@ class SmaqMulti:
         plan = self._plan(sx, sy, sa, device)
         p = self._codec._params(1, False)
         p.stats_source = N.SMQ_STATS_WORKSPACE
+        p.count_outliers = 1 if self.hparams.measure_compression_ratio else 0
         p.seed, p.offset = self.rng.take(plan["total"])
         N.check(N.lib().smq_smaq_multi_f32(
             plan["dev"].data_ptr(), ctypes.addressof(plan["host"]), p, plan["ws"].data_ptr(),
@@ -100,7 +106,12 @@ class SmaqMulti:
         self._last = dict(plan=plan, sel=sel, base=p.offset)
         return list(ys)
 
-    # -- inspection (tests) ----------------------------------------------------------------------
+    # -- inspection (tests, logging) ---------------------------------------------------------------
+    @property
+    def last_selected(self) -> bool:
+        """Whether the last call quantised at least one tensor (others were below min_size)."""
+        return self._last is not None
+
     def index_of(self, t: int) -> int:
         return self._last["sel"].index(t)
 

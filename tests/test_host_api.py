@@ -150,3 +150,37 @@ def test_reduce_fx():
     assert _reduce_fx([1.0, 2.0]) == 3.0
     assert float(_reduce_fx([torch.tensor(1.0), torch.tensor(2.5)])) == 3.5
     assert float(_reduce_fx(torch.tensor([1.0, 2.0]))) == 3.0
+
+
+def test_optimlp_host_contract():
+    from argparse import Namespace
+
+    import torch.nn as nn
+
+    from smart_compress_amd.util.pytorch.optimizer import OptimLP, TaggedQuant, wrap_optimizer
+
+    m = nn.Linear(4, 2)
+    sgd = torch.optim.SGD(m.parameters(), lr=0.1)
+    flags = Namespace(compress_weights=False, compress_gradients=False,
+                      compress_momentum_vectors=False)
+    assert wrap_optimizer(sgd, lambda t, **k: t, flags) is sgd
+    flags.compress_gradients = True
+    o = wrap_optimizer(sgd, lambda t, **k: t, flags)
+    assert isinstance(o, OptimLP) and isinstance(o.grad_quant, TaggedQuant)
+    assert o.grad_quant.tag == "optimizer_grad" and o.weight_quant is None
+    assert o.momentum_keys == [("momentum_buffer", {})]
+    a = OptimLP(torch.optim.AdamW(m.parameters()))
+    assert a.momentum_keys[1] == ("exp_avg_sq", {"all_positive": True})
+    with pytest.raises(NotImplementedError):
+        OptimLP(torch.optim.RMSprop(m.parameters()))
+    assert str(o).startswith("LP Optimizer:")
+    # CPU quantiser (identity) runs the per-tensor path end to end
+    seen = []
+    o = OptimLP(torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9),
+                grad_quant=lambda t, **k: seen.append(("g", t.shape)) or t,
+                weight_quant=lambda t, **k: seen.append(("w", t.shape)) or t,
+                momentum_quant=lambda t, **k: seen.append(("m", t.shape, k)) or t)
+    m(torch.randn(3, 4)).sum().backward()
+    o.step(lambda: None)
+    kinds = [s[0] for s in seen]
+    assert kinds.count("g") == 4 and kinds.count("w") == 2 and kinds.count("m") == 2

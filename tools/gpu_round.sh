@@ -27,6 +27,7 @@ for s in "$@"; do
     warm) step bench_w3 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline &&
           step bench_w20 300 python bench.py --steps 50 --warmup 20 --no-cpu-baseline &&
           step bench_w50 300 python bench.py --steps 100 --warmup 50 --no-cpu-baseline ;;
+    dist2) SMQ_BENCH_SHARE_DEVICE=1 SMQ_BENCH_BACKEND=gloo step bench_dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --elements 67108864 ;;
     tiles) for v in 1 2 4; do SMQ_APPLY_TILE=$v step kbench_tile$v 300 python tools/kbench.py --quick; done ;;
     profile) step profile 1500 bash tools/profile_round.sh r01 smaq ;;
     profile_*) c=${s#profile_}; step profile_$c 1500 bash tools/profile_round.sh r01_$c $c 50 10 ;;
