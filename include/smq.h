@@ -61,6 +61,13 @@ extern "C" {
 #define SMQ_STATS_SAMPLED 1   /* computed in-kernel from params.sample_idx (smart.py:86-91) */
 #define SMQ_STATS_INJECTED 2  /* read from the stats_in device pointer (parity tests) */
 
+/* Input element types of the SmaQ entry points with a dtype argument. fp16 / bf16 inputs follow
+ * the reference's dtype flow: statistics and z-score in the input type, the rest of the chain
+ * (and the output) in fp32 (smart.py:154-172 with torch type promotion). */
+#define SMQ_DTYPE_F32 0
+#define SMQ_DTYPE_F16 1
+#define SMQ_DTYPE_BF16 2
+
 /* Rounding modes of smq_float_quant_f32 (qtorch float_quantize rounding=...). */
 #define SMQ_ROUND_NEAREST 0
 #define SMQ_ROUND_STOCHASTIC 1
@@ -78,7 +85,7 @@ typedef struct SmqSmaqParams {
   float range_outlier;          /* fp32((2^(bo-2)-1)/(T_o-T_m))       smart.py:72-75 */
   float clamp_lo;               /* fp32(1e-38) or fp32(1e-4) at precision 16, smart.py:80-84 */
   float clamp_hi;               /* fp32(1e38)  or fp32(1e4) */
-  float range_std_coef;         /* 1/sqrt(2 ln n) in fp32 for --use_range_std_dev; <=0: library computes it */
+  float range_std_coef;         /* C = 1/sqrt(2 ln n) for --use_range_std_dev; <0: library computes it (fp32) */
   int32_t stochastic_rounding;  /* 1 = smart.py:93-98, 0 = trunc (smart.py:168-169) */
   int32_t all_positive;         /* clamp_min(0) after dequantisation (smart.py:181-182) */
   int32_t use_range_std_dev;    /* --use_range_std_dev */
@@ -163,6 +170,17 @@ int smq_smaq_apply_f32(const float* x, float* y, int64_t n, const SmqSmaqParams*
                        size_t ws_bytes, void* stream);
 int smq_smaq_roundtrip_f32(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
                            const float* uniforms, void* ws, size_t ws_bytes, void* stream);
+
+/* Same as the _f32 entry points for an input x of element type `dtype` (SMQ_DTYPE_*); the output
+ * y is always fp32. For SMQ_DTYPE_F16 / BF16 params.clamp_lo/hi and range_std_coef are the values
+ * the reference's torch ops produce in that dtype (the library rounds clamp bounds to it). */
+int smq_smaq_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
+                   size_t ws_bytes, void* stream);
+int smq_smaq_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                   const float* uniforms, const SmqSmaqStats* stats_in, void* ws, size_t ws_bytes,
+                   void* stream);
+int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                       const float* uniforms, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- SmaQ multi tensor ---- */
 /* A plan is a descriptor table plus a chunk map. smq_smaq_multi_plan_build writes it into a host

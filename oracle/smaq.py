@@ -13,6 +13,21 @@ import numpy as np
 F32 = np.float32
 
 
+def round_to(v, dtype: str = "f32"):
+    """Round float32 value(s) to the input type and back (RN-even): 'f32' | 'f16' | 'bf16'.
+    One input-type op = the float32 op + this rounding (exact: double rounding is innocuous when
+    the wide format has >= 2p + 2 bits)."""
+    a = np.asarray(v, dtype=F32)
+    if dtype == "f16":
+        with np.errstate(over="ignore"):
+            return a.astype(np.float16).astype(F32)
+    if dtype == "bf16":
+        u = a.view(np.uint32).astype(np.uint64)
+        r = ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000).astype(np.uint32).view(F32)
+        return np.where(np.isnan(a), a, r).astype(F32)
+    return a
+
+
 @dataclass
 class SmaqConfig:
     """hparams of smart.py:11-70 and the constants of smart.py:72-84 (Python doubles)."""
@@ -42,42 +57,55 @@ class SmaqConfig:
         return (1e-4, 1e4) if self.precision == 16 else (1e-38, 1e38)
 
 
-def range_coef(n: int) -> np.float32:
-    """1 / sqrt(2 * log(float32(n))) in float32 ops (smart.py:101-106)."""
-    return F32(1) / np.sqrt(F32(2.0) * np.log(F32(n)))
+def range_coef(n: int, dtype: str = "f32") -> np.float32:
+    """1 / sqrt(2 * log(T(n))) with every op in the data's type T (smart.py:101-106)."""
+    with np.errstate(all="ignore"):
+        t = round_to(F32(n), dtype)
+        t = round_to(np.log(t), dtype)
+        t = round_to(F32(2.0) * t, dtype)
+        t = round_to(np.sqrt(t), dtype)
+        return F32(round_to(F32(1) / t, dtype))
 
 
-def full_stats(x: np.ndarray, cfg: SmaqConfig) -> Tuple[np.float32, np.float32]:
-    """(data.mean(), self._get_std(data)) — smart.py:131, 100-108 (unbiased std)."""
+def full_stats(x: np.ndarray, cfg: SmaqConfig, dtype: str = "f32") -> Tuple[np.float32, np.float32]:
+    """(data.mean(), self._get_std(data)) — smart.py:131, 100-108 (unbiased std); for half data
+    the 0-dim results are rounded to the data's type (through float32, as torch does)."""
     x64 = x.astype(np.float64).ravel()
-    mean = F32(np.mean(x64))
+    mean = F32(round_to(F32(np.mean(x64)), dtype))
     if cfg.use_range_std_dev:
-        rng = F32(x.max()) - F32(x.min())
-        return mean, F32(rng * range_coef(x.size))
+        rng = round_to(F32(x.max()) - F32(x.min()), dtype)
+        return mean, F32(round_to(rng * range_coef(x.size, dtype), dtype))
     d = x64 - np.mean(x64)
     var = float(np.dot(d, d)) / (x64.size - 1) if x64.size > 1 else float("nan")
-    return mean, F32(np.sqrt(var))
+    return mean, F32(round_to(F32(np.sqrt(var)), dtype))
 
 
-def sampled_stats(x: np.ndarray, idx: np.ndarray, cfg: SmaqConfig):
+def sampled_stats(x: np.ndarray, idx: np.ndarray, cfg: SmaqConfig, dtype: str = "f32"):
     """smart.py:86-91: mean and biased std (or range-std) of x.view(-1)[idx]."""
     s = x.ravel()[np.asarray(idx, dtype=np.int64)]
     s64 = s.astype(np.float64)
-    mean = F32(np.mean(s64))
+    mean = F32(round_to(F32(np.mean(s64)), dtype))
     if cfg.use_range_std_dev:
-        return mean, F32((F32(s.max()) - F32(s.min())) * range_coef(s.size))
+        rng = round_to(F32(s.max()) - F32(s.min()), dtype)
+        return mean, F32(round_to(rng * range_coef(s.size, dtype), dtype))
     d = s64 - np.mean(s64)
-    return mean, F32(np.sqrt(float(np.dot(d, d)) / s64.size))
+    return mean, F32(round_to(F32(np.sqrt(float(np.dot(d, d)) / s64.size)), dtype))
 
 
 def apply(x: np.ndarray, mean, std, cfg: SmaqConfig, uniforms: Optional[np.ndarray] = None,
-          all_positive: bool = False, bn: Optional[Tuple[np.ndarray, np.ndarray]] = None):
-    """smart.py:144-182 given (mean, std). Returns (y, is_outlier)."""
+          all_positive: bool = False, bn: Optional[Tuple[np.ndarray, np.ndarray]] = None,
+          dtype: str = "f32"):
+    """smart.py:144-182 given (mean, std). Returns (y, is_outlier). For dtype 'f16' / 'bf16' the
+    z-score is computed in that type (x, mean, std hold values of it) and the rest in float32 —
+    the reference's torch type promotion; the output is float32."""
     x = np.asarray(x, dtype=F32)
     shape = x.shape
     mean, std = F32(mean), F32(std)
     thr = F32(cfg.main_std_dev_threshold)
-    lo_c, hi_c = F32(cfg.clamped_range[0]), F32(cfg.clamped_range[1])
+    zt = "f32" if bn is not None else dtype  # fp32 BN parameters promote the data to fp32
+    cthr = F32(round_to(thr, zt))
+    lo_c = F32(round_to(F32(cfg.clamped_range[0]), dtype))
+    hi_c = F32(round_to(F32(cfg.clamped_range[1]), dtype))
     r_out, r_main = F32(cfg.range_outlier), F32(cfg.range_normal)
     data = x
     if bn is not None:  # smart.py:144-149, per channel of dim 1
@@ -91,9 +119,9 @@ def apply(x: np.ndarray, mean, std, cfg: SmaqConfig, uniforms: Optional[np.ndarr
     if sc > hi_c:
         sc = hi_c
     with np.errstate(all="ignore"):
-        z = (data - mean) / sc
-        hi = z > thr
-        lo = z < -thr
+        z = round_to(round_to(data - mean, zt) / sc, zt)
+        hi = z > cthr
+        lo = z < -cthr
         o = hi | lo
         scal = np.where(hi, -thr, F32(0) * -thr) + np.where(lo, thr, F32(0) * thr)
         scal = scal.astype(F32)
@@ -118,15 +146,15 @@ def apply(x: np.ndarray, mean, std, cfg: SmaqConfig, uniforms: Optional[np.ndarr
 
 
 def roundtrip(x: np.ndarray, cfg: SmaqConfig, uniforms=None, sample_idx=None,
-              all_positive=False, bn=None, stats=None):
+              all_positive=False, bn=None, stats=None, dtype: str = "f32"):
     """Full smart.py:110-182. Returns (y, mean, std, n_outlier); n < min_size passes through."""
     if x.size < cfg.min_size:
         return x, None, None, 0
     if stats is not None:
         mean, std = stats
     elif cfg.use_sample_stats:
-        mean, std = sampled_stats(x, sample_idx, cfg)
+        mean, std = sampled_stats(x, sample_idx, cfg, dtype)
     else:
-        mean, std = full_stats(x, cfg)
-    y, o = apply(x, mean, std, cfg, uniforms, all_positive, bn)
+        mean, std = full_stats(x, cfg, dtype)
+    y, o = apply(x, mean, std, cfg, uniforms, all_positive, bn, dtype)
     return y, mean, std, int(o.sum())

@@ -53,18 +53,18 @@ static int grid_for(int64_t work_items, int per_block_items, int cap) {
   return (int)g;
 }
 
-// Memory shapes measured on MI355X (tools/membench.hip, profiles/): a read stream peaks with ONE
-// dwordx4 per lane in flight and the whole grid sweeping the buffer in address order (grid-stride,
-// ~1024 workgroups: 6.4 TB/s); several loads per lane at grid-stride distance (4 MB apart) open
-// several sweep fronts and fall to ~5.2 TB/s. A read+write stream is fastest as flat contiguous
-// tiles, one tile per workgroup, tiles in dispatch order (~6.1 TB/s).
+// Memory shapes measured on MI355X (tools/membench.hip, tools/statsbench.hip, profiles/): a read
+// stream peaks with ONE 16-B load per lane in flight and the whole grid sweeping the buffer in
+// address order (grid-stride over ~1-2k workgroups); several loads per lane at grid-stride
+// distance open several sweep fronts (-20 %). A read+write stream is fastest as flat contiguous
+// tiles, one per workgroup; with the stochastic-rounding ALU chain 2 vector slots per lane beat 1
+// and 4 (cold-cache sweep, profiles/r02_kbench_cold_tile*.json), truncation prefers 1.
 constexpr int kStatsGridCap = 2048;  // also the number of fp64 partials the last workgroup sums
-constexpr int kDefaultTileV = 4;     // apply: float4 per lane per tile (SMQ_APPLY_TILE=1|2|4)
 
-static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+static inline bool aligned(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
-template <bool RANGE>
-__global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const float* __restrict__ x, int64_t n,
+template <bool RANGE, int TIN>
+__global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restrict__ x, int64_t n,
                                                             int vec, FinalizeArgs fin,
                                                             StatPartial* __restrict__ partials,
                                                             uint32_t* counter,
@@ -72,20 +72,19 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const float* __restr
   __shared__ uint32_t arrive_slot;
   // Shift = median of three fixed elements: keeps sum(x-K)^2 - (sum(x-K))^2/n well conditioned
   // unless the mean is > 2^14 standard deviations away from all three.
-  const float k0 = x[0], k1 = x[n >> 1], k2 = x[n - 1];
+  const float k0 = load1<TIN>(x, 0), k1 = load1<TIN>(x, n >> 1), k2 = load1<TIN>(x, n - 1);
   const float kmed = fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));
   const double shift = (double)kmed;
 
-  // four independent fp64 chains (one per float4 component) so the adds of one iteration do
-  // not serialise behind each other while the next load is in flight
+  // four independent fp64 chains (one per vector component) so the adds of one iteration do not
+  // serialise behind each other while the next load is in flight
   StatAcc acc, ay, az, aw;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (vec) {
-    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
     const int64_t nv = n >> 2;
-    for (; i < nv; i += stride) {  // one dwordx4 in flight per lane: a single sweep front
-      const float4 v = x4[i];
+    for (; i < nv; i += stride) {  // one load in flight per lane: a single sweep front
+      const float4 v = load4<TIN>(x, i);
       acc.add<RANGE>(v.x, shift);
       ay.add<RANGE>(v.y, shift);
       az.add<RANGE>(v.z, shift);
@@ -93,7 +92,7 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const float* __restr
     }
     i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
   }
-  for (; i < n; i += stride) acc.add<RANGE>(x[i], shift);
+  for (; i < n; i += stride) acc.add<RANGE>(load1<TIN>(x, i), shift);
   acc.s1 = (acc.s1 + ay.s1) + (az.s1 + aw.s1);
   acc.s2 = (acc.s2 + ay.s2) + (az.s2 + aw.s2);
   if (RANGE) {
@@ -126,13 +125,13 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const float* __restr
   }
   block_reduce_stats<RANGE>(tot);
   if (threadIdx.x == 0) {
-    finalize_stats<RANGE>(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, fin, out);
+    finalize_stats<RANGE, TIN>(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, fin, out);
     *counter = 0u;  // leave the workspace ready for the next call
   }
 }
 
 struct ApplyArgs {
-  const float* x;
+  const void* x;
   float* y;
   int64_t n;
   const float* uniforms;
@@ -160,61 +159,51 @@ __device__ __forceinline__ BnTerm bn_term(const ApplyArgs& A, int64_t e) {
   return BnTerm{A.bn_gamma[ch], A.bn_beta[ch]};
 }
 
-// Sampled statistics (smart.py:86-91): mean and biased std (or range-std) of k gathered elements,
-// computed by wave 0 of every workgroup in the same order -> identical in all workgroups.
-__device__ __forceinline__ void sampled_stats(const ApplyArgs& A, SmqSmaqStats* sh) {
-  if (threadIdx.x < kWave) {  // one wave; the caller's workgroup may be larger
-    const int lane = threadIdx.x;
-    const bool valid = lane < A.k;
-    const float v = valid ? A.x[A.sample_idx[lane]] : 0.0f;
-    const double kd = (double)A.k;
-    const double mean = wave_sum(valid ? (double)v : 0.0) / kd;
-    const double dv = valid ? ((double)v - mean) : 0.0;
-    const double m2 = wave_sum(dv * dv);
-    const float mn = wave_min(valid ? v : INFINITY);
-    const float mx = wave_max(valid ? v : -INFINITY);
-    if (lane == 0) {
-      FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef};
-      // finalize_stats expects shifted sums; pass shift = mean, s1 = 0, s2 = m2.
-      if (A.use_range)
-        finalize_stats<true>(0.0, m2, mn, mx, A.k, mean, true, f, sh);
-      else
-        finalize_stats<false>(0.0, m2, mn, mx, A.k, mean, true, f, sh);
-    }
-  }
-  __syncthreads();
-}
-
-// One wave computes the sampled statistics into the workspace header; the apply launch then reads
-// them like full statistics (cheaper than a 16-element gather + fp64 reduction in each of 10^5
-// apply workgroups).
+// Sampled statistics (smart.py:86-91): mean and biased std (or range-std) of the k gathered
+// elements, by ONE wave into the workspace header; the apply launch reads them like full stats.
+template <int TIN>
 __global__ __launch_bounds__(kWave) void smaq_sample_stats_kernel(ApplyArgs A) {
-  __shared__ SmqSmaqStats sh;
-  sampled_stats(A, &sh);
-  if (threadIdx.x == 0) *A.ws_stats = sh;
+  const int lane = threadIdx.x;
+  const bool valid = lane < A.k;
+  const float v = valid ? load1<TIN>(A.x, A.sample_idx[lane]) : 0.0f;
+  const double kd = (double)A.k;
+  const double mean = wave_sum(valid ? (double)v : 0.0) / kd;
+  const double dv = valid ? ((double)v - mean) : 0.0;
+  const double m2 = wave_sum(dv * dv);
+  const float mn = wave_min(valid ? v : INFINITY);
+  const float mx = wave_max(valid ? v : -INFINITY);
+  if (lane == 0) {
+    SmqSmaqStats st;
+    FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef};
+    // finalize_stats takes shifted sums: shift = mean, s1 = 0, s2 = m2 (biased)
+    if (A.use_range)
+      finalize_stats<true, TIN>(0.0, m2, mn, mx, A.k, mean, true, f, &st);
+    else
+      finalize_stats<false, TIN>(0.0, m2, mn, mx, A.k, mean, true, f, &st);
+    *A.ws_stats = st;
+  }
 }
 
-template <int SRC, int RM, bool VEC, bool BN, int kTileV>
+// RM = rounding mode, TIN = input element type; VT = 4-element vector slots per lane per tile.
+template <int RM, bool VEC, bool BN, int TIN>
 __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
+  constexpr int kTileV = (RM == kRoundTrunc) ? 1 : 2;
   constexpr int kTileElems = kBlock * kTileV * 4;
   __shared__ uint32_t sh_cnt[kBlock / kWave];
   ElemConsts c;
-  c.mean = A.stats->mean;
-  c.sd = A.stats->std_dev;
-  c.sc = A.stats->std_clamped;
-  init_consts(c, c.mean, c.sd, c.sc, A.thr, A.r_main, A.r_out);
+  const float cthr = (BN || TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
+  init_consts(c, A.stats->mean, A.stats->std_dev, A.stats->std_clamped, A.thr, A.r_main, A.r_out,
+              cthr);
   const bool all_pos = A.all_pos != 0;
 
   uint32_t n_out = 0;
   const int64_t n = A.n;
   if (VEC) {
-    // flat tile: this workgroup owns float4 [t0, t0 + kBlock * kTileV), kTileV coalesced sweeps
-    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
+    // Tiles run in REVERSE address order after a forward statistics sweep of the same tensor:
+    // the last ~256 MB of x are then still in the Infinity Cache (MALL) when this launch starts.
     float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
     const float4* __restrict__ u4 = reinterpret_cast<const float4*>(A.uniforms);
     const int64_t nv = n >> 2;
-    // Tiles run in REVERSE address order: the statistics launch just swept x forward, so the
-    // last ~256 MB of x are still in the Infinity Cache (MALL) when this launch starts.
     const int64_t tile = A.reverse ? (int64_t)(gridDim.x - 1 - blockIdx.x) : (int64_t)blockIdx.x;
     const int64_t t0 = tile * (kBlock * kTileV) + threadIdx.x;
     float4 v[kTileV], uu[kTileV];
@@ -222,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
     for (int u = 0; u < kTileV; ++u) {
       const int64_t j = t0 + u * kBlock;
       if (j < nv) {
-        v[u] = x4[j];
+        v[u] = load4<TIN>(A.x, j);
         if (RM == kRoundUniform) uu[u] = u4[j];
       }
     }
@@ -244,10 +233,10 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
       }
       bool b0, b1, b2, b3;
       float4 o;
-      o.x = smaq_elem<RM, BN>(v[u].x, u0, c, all_pos, b0, bn_term<BN>(A, 4 * j + 0));
-      o.y = smaq_elem<RM, BN>(v[u].y, u1, c, all_pos, b1, bn_term<BN>(A, 4 * j + 1));
-      o.z = smaq_elem<RM, BN>(v[u].z, u2, c, all_pos, b2, bn_term<BN>(A, 4 * j + 2));
-      o.w = smaq_elem<RM, BN>(v[u].w, u3, c, all_pos, b3, bn_term<BN>(A, 4 * j + 3));
+      o.x = smaq_elem<RM, BN, TIN>(v[u].x, u0, c, all_pos, b0, bn_term<BN>(A, 4 * j + 0));
+      o.y = smaq_elem<RM, BN, TIN>(v[u].y, u1, c, all_pos, b1, bn_term<BN>(A, 4 * j + 1));
+      o.z = smaq_elem<RM, BN, TIN>(v[u].z, u2, c, all_pos, b2, bn_term<BN>(A, 4 * j + 2));
+      o.w = smaq_elem<RM, BN, TIN>(v[u].w, u3, c, all_pos, b3, bn_term<BN>(A, 4 * j + 3));
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
       store_nt(y4 + j, o);
     }
@@ -258,11 +247,11 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
       if (RM == kRoundHash) uf = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)e));
       if (RM == kRoundUniform) uf = A.uniforms[e];
       bool bt;
-      A.y[e] = smaq_elem<RM, BN>(A.x[e], uf, c, all_pos, bt, bn_term<BN>(A, e));
+      A.y[e] = smaq_elem<RM, BN, TIN>(load1<TIN>(A.x, e), uf, c, all_pos, bt, bn_term<BN>(A, e));
       n_out += (unsigned)bt;
     }
   } else {
-    // unaligned pointers: the same tile of kTileElems elements with dword accesses
+    // unaligned pointers: the same tile of kTileElems elements with element accesses
     const int64_t e0 = (int64_t)blockIdx.x * kTileElems + threadIdx.x;
 #pragma unroll 4
     for (int k = 0; k < kTileElems / kBlock; ++k) {
@@ -272,7 +261,7 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
       if (RM == kRoundHash) uf = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)e));
       if (RM == kRoundUniform) uf = A.uniforms[e];
       bool bt;
-      A.y[e] = smaq_elem<RM, BN>(A.x[e], uf, c, all_pos, bt, bn_term<BN>(A, e));
+      A.y[e] = smaq_elem<RM, BN, TIN>(load1<TIN>(A.x, e), uf, c, all_pos, bt, bn_term<BN>(A, e));
       n_out += (unsigned)bt;
     }
   }
@@ -306,7 +295,8 @@ static int validate_params(const SmqSmaqParams* p) {
 }
 
 static float range_coef_for(const SmqSmaqParams* p, int64_t n) {
-  if (p->range_std_coef > 0.0f) return p->range_std_coef;
+  // 0 is a real value (fp16 data with n > 65504: half(n) = inf -> C = 0 -> std 0 -> 1)
+  if (p->range_std_coef >= 0.0f) return p->range_std_coef;
   // smart.py:101-106: C = 1 / sqrt(2.0 * log(tensor(n).float())) in fp32 ops
   const float lg = logf((float)n);
   const float t = 2.0f * lg;
@@ -318,7 +308,15 @@ static size_t stats_ws_bytes(int64_t n) {
   return SmaqWsLayout::kPartials + sizeof(StatPartial) * (size_t)kStatsGridCap;
 }
 
-static int launch_stats(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,
+static int check_dtype(int dtype) {
+  if (dtype != SMQ_DTYPE_F32 && dtype != SMQ_DTYPE_F16 && dtype != SMQ_DTYPE_BF16) {
+    set_error("dtype %d is not one of SMQ_DTYPE_F32/F16/BF16", dtype);
+    return SMQ_ERR_INVALID;
+  }
+  return SMQ_OK;
+}
+
+static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
                         size_t ws_bytes, hipStream_t st) {
   if (!ws || ws_bytes < stats_ws_bytes(n)) {
     set_error("workspace too small: need %zu bytes, got %zu", stats_ws_bytes(n), ws_bytes);
@@ -328,35 +326,44 @@ static int launch_stats(const float* x, int64_t n, const SmqSmaqParams* p, void*
   SmqSmaqStats* hdr = (SmqSmaqStats*)base;
   uint32_t* counter = (uint32_t*)(base + SmaqWsLayout::kHeader);
   StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
-  const int vec = aligned16(x) ? 1 : 0;
+  const int vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) ? 1 : 0;
   const int grid = grid_for(n, kBlock * 4, kStatsGridCap);
   FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n)};
-  if (p->use_range_std_dev)
-    hipLaunchKernelGGL(smaq_stats_kernel<true>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, fin,
-                       partials, counter, hdr);
-  else
-    hipLaunchKernelGGL(smaq_stats_kernel<false>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, fin,
-                       partials, counter, hdr);
+#define SMQ_STATS(RANGE, TIN)                                                                    \
+  hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n, vec, \
+                     fin, partials, counter, hdr)
+  if (dtype == SMQ_DTYPE_F32) {
+    if (p->use_range_std_dev) SMQ_STATS(true, kF32); else SMQ_STATS(false, kF32);
+  } else if (dtype == SMQ_DTYPE_F16) {
+    if (p->use_range_std_dev) SMQ_STATS(true, kF16); else SMQ_STATS(false, kF16);
+  } else {
+    if (p->use_range_std_dev) SMQ_STATS(true, kBF16); else SMQ_STATS(false, kBF16);
+  }
+#undef SMQ_STATS
   return check_launch("smaq_stats_kernel");
 }
 
-template <int SRC, bool BN, int TV>
-static void launch_apply_src(const ApplyArgs& A, int rm, bool vec, int grid, hipStream_t st) {
-#define SMQ_APPLY(RMV, VECV) \
-  hipLaunchKernelGGL((smaq_apply_kernel<SRC, RMV, VECV, BN, TV>), dim3(grid), dim3(kBlock), 0, st, A)
+template <int TIN>
+static void launch_apply_t(const ApplyArgs& A, int rm, bool vec, bool bn, int grid,
+                           hipStream_t st) {
+#define SMQ_APPLY(RMV, VECV, BNV) \
+  hipLaunchKernelGGL((smaq_apply_kernel<RMV, VECV, BNV, TIN>), dim3(grid), dim3(kBlock), 0, st, A)
+#define SMQ_APPLY_RM(VECV, BNV)                                 \
+  do {                                                          \
+    if (rm == kRoundHash) SMQ_APPLY(kRoundHash, VECV, BNV);     \
+    else if (rm == kRoundUniform) SMQ_APPLY(kRoundUniform, VECV, BNV); \
+    else SMQ_APPLY(kRoundTrunc, VECV, BNV);                     \
+  } while (0)
   if (vec) {
-    if (rm == kRoundHash) SMQ_APPLY(kRoundHash, true);
-    else if (rm == kRoundUniform) SMQ_APPLY(kRoundUniform, true);
-    else SMQ_APPLY(kRoundTrunc, true);
+    if (bn) SMQ_APPLY_RM(true, true); else SMQ_APPLY_RM(true, false);
   } else {
-    if (rm == kRoundHash) SMQ_APPLY(kRoundHash, false);
-    else if (rm == kRoundUniform) SMQ_APPLY(kRoundUniform, false);
-    else SMQ_APPLY(kRoundTrunc, false);
+    if (bn) SMQ_APPLY_RM(false, true); else SMQ_APPLY_RM(false, false);
   }
+#undef SMQ_APPLY_RM
 #undef SMQ_APPLY
 }
 
-static int launch_apply(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
+static int launch_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                         const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
                         size_t ws_bytes, hipStream_t st) {
   if (!ws || ws_bytes < SmaqWsLayout::kPartials) {
@@ -413,7 +420,8 @@ static int launch_apply(const float* x, float* y, int64_t n, const SmqSmaqParams
     A.range_coef = range_coef_for(p, k);
   }
   const int rm = !p->stochastic_rounding ? kRoundTrunc : (uniforms ? kRoundUniform : kRoundHash);
-  const bool vec = aligned16(x) && aligned16(y) && (rm != kRoundUniform || aligned16(uniforms));
+  const bool vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) && aligned(y, 16) &&
+                   (rm != kRoundUniform || aligned(uniforms, 16));
   A.out_slots = (unsigned long long*)((char*)ws + SmaqWsLayout::kSlots);
   if (p->count_outliers) {
     if (hipMemsetAsync(A.out_slots, 0, 8 * SMQ_WS_OUTLIER_SLOTS, st) != hipSuccess) {
@@ -427,43 +435,30 @@ static int launch_apply(const float* x, float* y, int64_t n, const SmqSmaqParams
   }();
   // reverse only pays after a forward statistics sweep of the same tensor
   A.reverse = (p->stats_source == SMQ_STATS_WORKSPACE) ? rev_env : 0;
-  static const int tile_v = [] {
-    const char* e = getenv("SMQ_APPLY_TILE");
-    const int v = e ? atoi(e) : kDefaultTileV;
-    return (v == 1 || v == 2 || v == 4) ? v : kDefaultTileV;
-  }();
-  const int64_t tile_elems = (int64_t)kBlock * tile_v * 4;
+  const int64_t tile_elems = (int64_t)kBlock * 4 * (rm == kRoundTrunc ? 1 : 2);
   const int64_t tiles = (n + tile_elems - 1) / tile_elems;
   if (tiles > 0x7fffffffLL) {
     set_error("tensor too large: %lld elements", (long long)n);
     return SMQ_ERR_INVALID;
   }
   const int grid = (int)tiles;
-  const bool bn = A.bn_gamma != nullptr;
-#define SMQ_SRC(SRCV)                                                             \
-  do {                                                                            \
-    if (tile_v == 1) {                                                            \
-      if (bn) launch_apply_src<SRCV, true, 1>(A, rm, vec, grid, st);              \
-      else launch_apply_src<SRCV, false, 1>(A, rm, vec, grid, st);                \
-    } else if (tile_v == 2) {                                                     \
-      if (bn) launch_apply_src<SRCV, true, 2>(A, rm, vec, grid, st);              \
-      else launch_apply_src<SRCV, false, 2>(A, rm, vec, grid, st);                \
-    } else {                                                                      \
-      if (bn) launch_apply_src<SRCV, true, 4>(A, rm, vec, grid, st);              \
-      else launch_apply_src<SRCV, false, 4>(A, rm, vec, grid, st);                \
-    }                                                                             \
-  } while (0)
   if (p->stats_source == SMQ_STATS_SAMPLED) {
-    hipLaunchKernelGGL(smaq_sample_stats_kernel, dim3(1), dim3(kWave), 0, st, A);
+    if (dtype == SMQ_DTYPE_F32)
+      hipLaunchKernelGGL(smaq_sample_stats_kernel<kF32>, dim3(1), dim3(kWave), 0, st, A);
+    else if (dtype == SMQ_DTYPE_F16)
+      hipLaunchKernelGGL(smaq_sample_stats_kernel<kF16>, dim3(1), dim3(kWave), 0, st, A);
+    else
+      hipLaunchKernelGGL(smaq_sample_stats_kernel<kBF16>, dim3(1), dim3(kWave), 0, st, A);
     A.stats = A.ws_stats;
   }
-  if (p->stats_source == SMQ_STATS_INJECTED) SMQ_SRC(SMQ_STATS_INJECTED);
-  else SMQ_SRC(SMQ_STATS_WORKSPACE);
-#undef SMQ_SRC
+  const bool bn = A.bn_gamma != nullptr;
+  if (dtype == SMQ_DTYPE_F32) launch_apply_t<kF32>(A, rm, vec, bn, grid, st);
+  else if (dtype == SMQ_DTYPE_F16) launch_apply_t<kF16>(A, rm, vec, bn, grid, st);
+  else launch_apply_t<kBF16>(A, rm, vec, bn, grid, st);
   return check_launch("smaq_apply_kernel");
 }
 
-static int check_tensor_args(const float* x, const float* y, int64_t n) {
+static int check_tensor_args(const void* x, const float* y, int64_t n) {
   if (n < 1) {
     set_error("n must be >= 1 (got %lld); the caller passes n < min_size through", (long long)n);
     return SMQ_ERR_INVALID;
@@ -492,6 +487,7 @@ void smq_smaq_params_init(SmqSmaqParams* p) {
   p->stochastic_rounding = 1;
   p->num_samples = 16;
   p->stats_source = SMQ_STATS_WORKSPACE;
+  p->range_std_coef = -1.0f;  // library computes the fp32 coefficient
 }
 
 int smq_smaq_params_set(SmqSmaqParams* p, int num_bits_main, int num_bits_outlier,
@@ -546,41 +542,58 @@ int smq_smaq_draw_samples(SmqSmaqParams* p, int64_t n, int num_samples) {
 
 size_t smq_smaq_workspace_bytes(int64_t n) { return stats_ws_bytes(n); }
 
-int smq_smaq_stats_f32(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,
-                       size_t ws_bytes, void* stream) {
+int smq_smaq_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
+                   size_t ws_bytes, void* stream) {
   int rc = validate_params(p);
+  if (!rc) rc = check_dtype(dtype);
   if (rc) return rc;
   if (n < 1 || !x) {
     set_error("stats: n must be >= 1 and x non-NULL");
     return SMQ_ERR_INVALID;
   }
-  return launch_stats(x, n, p, ws, ws_bytes, (hipStream_t)stream);
+  return launch_stats(x, dtype, n, p, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int smq_smaq_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                   const float* uniforms, const SmqSmaqStats* stats_in, void* ws, size_t ws_bytes,
+                   void* stream) {
+  int rc = validate_params(p);
+  if (!rc) rc = check_dtype(dtype);
+  if (!rc) rc = check_tensor_args(x, y, n);
+  if (rc) return rc;
+  return launch_apply(x, dtype, y, n, p, uniforms, stats_in, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                       const float* uniforms, void* ws, size_t ws_bytes, void* stream) {
+  int rc = validate_params(p);
+  if (!rc) rc = check_dtype(dtype);
+  if (!rc) rc = check_tensor_args(x, y, n);
+  if (rc) return rc;
+  if (p->stats_source == SMQ_STATS_WORKSPACE) {
+    rc = launch_stats(x, dtype, n, p, ws, ws_bytes, (hipStream_t)stream);
+    if (rc) return rc;
+  } else if (p->stats_source == SMQ_STATS_INJECTED) {
+    set_error("roundtrip: use smq_smaq_apply for injected statistics");
+    return SMQ_ERR_INVALID;
+  }
+  return launch_apply(x, dtype, y, n, p, uniforms, nullptr, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int smq_smaq_stats_f32(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,
+                       size_t ws_bytes, void* stream) {
+  return smq_smaq_stats(x, SMQ_DTYPE_F32, n, p, ws, ws_bytes, stream);
 }
 
 int smq_smaq_apply_f32(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
                        const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
                        size_t ws_bytes, void* stream) {
-  int rc = validate_params(p);
-  if (rc) return rc;
-  rc = check_tensor_args(x, y, n);
-  if (rc) return rc;
-  return launch_apply(x, y, n, p, uniforms, stats_in, ws, ws_bytes, (hipStream_t)stream);
+  return smq_smaq_apply(x, SMQ_DTYPE_F32, y, n, p, uniforms, stats_in, ws, ws_bytes, stream);
 }
 
 int smq_smaq_roundtrip_f32(const float* x, float* y, int64_t n, const SmqSmaqParams* p,
                            const float* uniforms, void* ws, size_t ws_bytes, void* stream) {
-  int rc = validate_params(p);
-  if (rc) return rc;
-  rc = check_tensor_args(x, y, n);
-  if (rc) return rc;
-  if (p->stats_source == SMQ_STATS_WORKSPACE) {
-    rc = launch_stats(x, n, p, ws, ws_bytes, (hipStream_t)stream);
-    if (rc) return rc;
-  } else if (p->stats_source == SMQ_STATS_INJECTED) {
-    set_error("roundtrip: use smq_smaq_apply_f32 for injected statistics");
-    return SMQ_ERR_INVALID;
-  }
-  return launch_apply(x, y, n, p, uniforms, nullptr, ws, ws_bytes, (hipStream_t)stream);
+  return smq_smaq_roundtrip(x, SMQ_DTYPE_F32, y, n, p, uniforms, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

@@ -3,11 +3,64 @@
 // Reference: smart_compress/compress/smart.py:100-108, 130-134, 151-182.
 #pragma once
 
+#include <hip/hip_fp16.h>
 #include <math.h>
 
 #include "smq_common.h"
 
 namespace smq {
+
+// ---- input element types (SMQ_DTYPE_*) ------------------------------------------------------------
+// A half / bfloat16 input keeps the reference's dtype flow (verified on torch CPU with smart.py):
+// statistics and the z-score `(data - mean) / std.clamp(...)` are computed in the input type
+// (each op rounded to it), the bool*float scalars / ranges tensors are fp32 and promote the rest of
+// the chain to fp32, so the output is fp32. One input-type op is emulated as the fp32 op followed
+// by a rounding to the input type: exact, since fp32 has p' = 24 >= 2p + 2 bits for fp16 (p = 11)
+// and bf16 (p = 8) (double rounding is innocuous for +, -, *, / at that margin).
+enum InType { kF32 = SMQ_DTYPE_F32, kF16 = SMQ_DTYPE_F16, kBF16 = SMQ_DTYPE_BF16 };
+
+template <int T>
+__device__ __forceinline__ float round_in(float v) {
+  if (T == kF16) return __half2float(__float2half_rn(v));
+  if (T == kBF16) {  // round to nearest even, NaN stays NaN
+    uint32_t u = __builtin_bit_cast(uint32_t, v);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return v;
+    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+    return __builtin_bit_cast(float, u);
+  }
+  return v;
+}
+
+template <int T>
+__device__ __forceinline__ float load1(const void* p, int64_t e) {
+  if (T == kF32) return static_cast<const float*>(p)[e];
+  const uint16_t h = static_cast<const uint16_t*>(p)[e];
+  if (T == kF16) return __half2float(__builtin_bit_cast(__half, h));
+  return __builtin_bit_cast(float, (uint32_t)h << 16);
+}
+
+// elements 4j .. 4j+3 with one 16-B (fp32) or 8-B (fp16 / bf16) load
+template <int T>
+__device__ __forceinline__ float4 load4(const void* p, int64_t j) {
+  if (T == kF32) return static_cast<const float4*>(p)[j];
+  const uint2 w = static_cast<const uint2*>(p)[j];
+  float4 o;
+  if (T == kF16) {
+    o.x = __half2float(__builtin_bit_cast(__half, (uint16_t)(w.x & 0xffffu)));
+    o.y = __half2float(__builtin_bit_cast(__half, (uint16_t)(w.x >> 16)));
+    o.z = __half2float(__builtin_bit_cast(__half, (uint16_t)(w.y & 0xffffu)));
+    o.w = __half2float(__builtin_bit_cast(__half, (uint16_t)(w.y >> 16)));
+  } else {
+    o.x = __builtin_bit_cast(float, w.x << 16);
+    o.y = __builtin_bit_cast(float, w.x & 0xffff0000u);
+    o.z = __builtin_bit_cast(float, w.y << 16);
+    o.w = __builtin_bit_cast(float, w.y & 0xffff0000u);
+  }
+  return o;
+}
+
+template <int T>
+constexpr int in_bytes() { return T == kF32 ? 4 : 2; }
 
 // ------------------------------------------------------------------------------------------------
 // statistics
@@ -58,11 +111,13 @@ __device__ __forceinline__ void block_reduce_stats(StatAcc& a) {
 }
 
 struct FinalizeArgs {
-  float clamp_lo, clamp_hi, range_coef;
+  float clamp_lo, clamp_hi, range_coef;  // range_coef is representable in the input type
 };
 
 // mean / std from shifted sums -> SmqSmaqStats (smart.py:130-134, 100-108, 151-152, 154).
-template <bool RANGE>
+// T = input type: torch reduces half tensors in fp32/fp64 and rounds the 0-dim result to half
+// (through fp32, i.e. RN_T(RN32(.))), exactly what round_in<T>((float)x) does.
+template <bool RANGE, int T = kF32>
 __device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, float mx, int64_t n,
                                                double shift, bool biased, FinalizeArgs f,
                                                SmqSmaqStats* out) {
@@ -70,17 +125,18 @@ __device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, f
   const double mean = shift + s1 / nd;
   float sd;
   if (RANGE) {
-    const float range = mx - mn;  // data.max() - data.min()
-    sd = range * f.range_coef;    // range_ * C
+    const float range = round_in<T>(mx - mn);  // data.max() - data.min()
+    sd = round_in<T>(range * f.range_coef);    // range_ * C
   } else {
     double var = (s2 - s1 * (s1 / nd)) / (biased ? nd : (nd - 1.0));
     if (var < 0.0) var = 0.0;
-    sd = (float)sqrt(var);
+    sd = round_in<T>((float)sqrt(var));
   }
   const float std_dev = (sd == 0.0f) ? 1.0f : sd;  // smart.py:151-152
-  float sc = std_dev < f.clamp_lo ? f.clamp_lo : std_dev;  // .clamp(*clamped_range)
-  sc = sc > f.clamp_hi ? f.clamp_hi : sc;
-  out->mean = (float)mean;
+  const float lo = round_in<T>(f.clamp_lo), hi = round_in<T>(f.clamp_hi);
+  float sc = std_dev < lo ? lo : std_dev;          // .clamp(*clamped_range) in the input type
+  sc = sc > hi ? hi : sc;
+  out->mean = round_in<T>((float)mean);
   out->std_dev = std_dev;
   out->std_clamped = sc;
   out->raw_std = sd;
@@ -95,7 +151,8 @@ __device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, f
 // ------------------------------------------------------------------------------------------------
 struct ElemConsts {
   float mean, sd, sc;     // mean, std (after ==0 rule), clamped std
-  float thr, nthr;        // fp32(T_m), -fp32(T_m)
+  float thr, nthr;        // fp32(T_m), -fp32(T_m): the values of the scalars tensor (fp32)
+  float cthr, cnthr;      // thresholds as compared with z: rounded to z's type
   float zh, zl;           // 0 * -T_m, 0 * T_m  (the bool*float zero terms, smart.py:159-161)
   float r_main, r_out;    // ranges
   double inv_sc;          // RN64(1 / sc)
@@ -114,12 +171,14 @@ __device__ __forceinline__ float div_by_const(float a, double inv_b) {
 }
 
 __device__ __forceinline__ void init_consts(ElemConsts& c, float mean, float sd, float sc, float thr,
-                                            float r_main, float r_out) {
+                                            float r_main, float r_out, float cthr) {
   c.mean = mean;
   c.sd = sd;
   c.sc = sc;
   c.thr = thr;
   c.nthr = -thr;
+  c.cthr = cthr;
+  c.cnthr = -cthr;
   c.zh = 0.0f * c.nthr;
   c.zl = 0.0f * c.thr;
   c.r_main = r_main;
@@ -137,16 +196,19 @@ struct BnTerm {
 };
 
 // One element of smart.py:154-182. Each statement is one rounded fp32 op of the reference.
-template <int RM, bool BN = false>
+// T = input type (z-score rounded to it unless BN already promoted the data to fp32).
+template <int RM, bool BN = false, int T = kF32>
 __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c, bool all_pos,
                                            bool& is_outlier, BnTerm bn = BnTerm{1.0f, 0.0f}) {
+  constexpr int TZ = BN ? kF32 : T;  // fp32 BN parameters promote the data to fp32
   if (BN) v = (v - bn.beta) / bn.gamma;                 // (data - beta) / gamma
-  const float dm = v - c.mean;                          // data - mean
+  const float dm = round_in<TZ>(v - c.mean);            // data - mean
   float z = div_by_const(dm, c.inv_sc);                 // / std.clamp(...)
   // subnormal quotient (class mask 0x90 = -/+ denormal, one v_cmp_class_f32): IEEE division
   if (__builtin_expect(__builtin_amdgcn_class(z, 0x90), 0)) z = dm / c.sc;
-  const bool hi = z > c.thr;                            // is_outlier_higher
-  const bool lo = z < c.nthr;                           // is_outlier_lower
+  z = round_in<TZ>(z);
+  const bool hi = z > c.cthr;                           // is_outlier_higher
+  const bool lo = z < c.cnthr;                          // is_outlier_lower
   const bool o = hi | lo;                               // is_outlier
   const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);  // scalars
   const float r = o ? c.r_out : c.r_main;               // ranges

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
   const ChunkDesc ch = A.chunks[blockIdx.x];
   const SmqSmaqStats* st = &A.stats[ch.tensor];
   ElemConsts c;
-  init_consts(c, st->mean, st->std_dev, st->std_clamped, A.thr, A.r_main, A.r_out);
+  init_consts(c, st->mean, st->std_dev, st->std_clamped, A.thr, A.r_main, A.r_out, A.thr);
   const bool all_pos = ch.all_positive != 0;
   const float* __restrict__ x = ch.x;
   float* y = ch.y;  // may alias x

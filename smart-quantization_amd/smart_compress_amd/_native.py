@@ -26,6 +26,9 @@ SMQ_WS_OUTLIER_SLOTS = 64
 SMQ_STATS_WORKSPACE = 0
 SMQ_STATS_SAMPLED = 1
 SMQ_STATS_INJECTED = 2
+SMQ_DTYPE_F32 = 0
+SMQ_DTYPE_F16 = 1
+SMQ_DTYPE_BF16 = 2
 SMQ_ROUND_NEAREST = 0
 SMQ_ROUND_STOCHASTIC = 1
 
@@ -126,6 +129,15 @@ SIGNATURES = {
         _I32,
         [_P, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _SZ, _P],
     ),
+    "smq_smaq_stats": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P]),
+    "smq_smaq_apply": (
+        _I32,
+        [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _P, _SZ, _P],
+    ),
+    "smq_smaq_roundtrip": (
+        _I32,
+        [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _SZ, _P],
+    ),
     "smq_smaq_multi_plan_bytes": (_SZ, [ctypes.POINTER(_I64), _I32]),
     "smq_smaq_multi_plan_build": (_I32, [ctypes.POINTER(SmqTensorDesc), _I32, _P, _SZ]),
     "smq_smaq_multi_workspace_bytes": (_SZ, [ctypes.POINTER(_I64), _I32]),
@@ -180,12 +192,20 @@ def check(rc: int, what: str) -> None:
         raise RuntimeError(f"{what} failed (rc={rc}): {msg}")
 
 
-def require_device_f32(t: torch.Tensor, who: str) -> None:
+DTYPE_CODES = {torch.float32: SMQ_DTYPE_F32, torch.float16: SMQ_DTYPE_F16,
+               torch.bfloat16: SMQ_DTYPE_BF16}
+
+
+def require_device(t: torch.Tensor, who: str) -> None:
     if not t.is_cuda:
         raise RuntimeError(
             f"{who}: smart_compress_amd runs on ROCm device tensors only (got device={t.device}); "
             "move the tensor to the GPU"
         )
+
+
+def require_device_f32(t: torch.Tensor, who: str) -> None:
+    require_device(t, who)
     if t.dtype != torch.float32:
         raise NotImplementedError(
             f"{who}: dtype {t.dtype} is not supported by the gfx950 kernels yet (float32 only)"

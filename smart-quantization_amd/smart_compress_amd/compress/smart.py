@@ -54,13 +54,16 @@ _SMAQ_FLAGS = (
 _range_coef_cache = {}
 
 
-def range_std_coef(n: int) -> float:
-    """C = 1 / sqrt(2 log n) evaluated with the reference's fp32 torch ops (smart.py:101-106)."""
-    c = _range_coef_cache.get(n)
+def range_std_coef(n: int, dtype: torch.dtype = torch.float32) -> float:
+    """C = 1 / sqrt(2 log n) evaluated with the reference's torch ops in the data's dtype
+    (smart.py:101-106: ``torch.tensor(numel).type_as(range_)``; for half data n > 65504 becomes
+    inf and C = 0, which the std == 0 rule then turns into std = 1, as in the reference)."""
+    key = (n, dtype)
+    c = _range_coef_cache.get(key)
     if c is None:
-        t = torch.tensor(n).type_as(torch.tensor(0.0))
+        t = torch.tensor(n).type_as(torch.tensor(0.0, dtype=dtype))
         c = float(1 / torch.sqrt(2.0 * torch.log(t)))
-        _range_coef_cache[n] = c
+        _range_coef_cache[key] = c
     return c
 
 
@@ -88,7 +91,8 @@ class SmartFP(CompressionAlgorithmBase):
         self.rng = N.RngState(getattr(hp, "smq_seed", None))
 
     # -- parameter block -------------------------------------------------------------------------
-    def _params(self, numel: int, all_positive: bool) -> N.SmqSmaqParams:
+    def _params(self, numel: int, all_positive: bool,
+                dtype: torch.dtype = torch.float32) -> N.SmqSmaqParams:
         hp = self.hparams
         p = N.SmqSmaqParams()
         p.num_bits_main = hp.num_bits_main
@@ -103,6 +107,7 @@ class SmartFP(CompressionAlgorithmBase):
         p.use_range_std_dev = 1 if hp.use_range_std_dev else 0
         p.count_outliers = 1 if hp.measure_compression_ratio else 0
         p.seed, p.offset = self.rng.take(numel)
+        p.range_std_coef = -1.0  # set below in range mode (0.0 is a valid coefficient)
         if hp.use_sample_stats:
             k = min(numel, hp.num_samples)
             if k > N.SMQ_MAX_SAMPLES:
@@ -112,11 +117,11 @@ class SmartFP(CompressionAlgorithmBase):
             p.stats_source = N.SMQ_STATS_SAMPLED
             N.check(N.lib().smq_smaq_draw_samples(p, numel, hp.num_samples), "draw_samples")
             if hp.use_range_std_dev:
-                p.range_std_coef = range_std_coef(k)
+                p.range_std_coef = range_std_coef(k, dtype)
         else:
             p.stats_source = N.SMQ_STATS_WORKSPACE
             if hp.use_range_std_dev:
-                p.range_std_coef = range_std_coef(numel)
+                p.range_std_coef = range_std_coef(numel, dtype)
         return p
 
     def _bind_batch_norm(self, p, data: torch.Tensor, bn: Tuple[torch.Tensor, torch.Tensor]):
@@ -157,15 +162,23 @@ class SmartFP(CompressionAlgorithmBase):
                 self.log_ratio(tag, numel * 32, 32, 32)
                 return data
 
-            N.require_device_f32(data, "SmartFP")
+            N.require_device(data, "SmartFP")
+            code = N.DTYPE_CODES.get(data.dtype)
+            if code is None:
+                raise NotImplementedError(
+                    f"SmartFP: dtype {data.dtype} is not supported (float32/float16/bfloat16)")
+            if data.dtype == torch.float16 and hp.precision != 16:
+                # the reference's std.clamp(1e-38, 1e38) on a half tensor (smart.py:154)
+                raise RuntimeError("value cannot be converted to type c10::Half without overflow")
             x = data.contiguous()
-            y = torch.empty_like(x)
-            p = self._params(numel, all_positive)
+            # half inputs: the bool*float scalars/ranges tensors promote the chain to fp32
+            y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+            p = self._params(numel, all_positive, x.dtype)
             keep = None
             if hp.use_batch_norm and batch_norm_stats is not None:
                 keep = self._bind_batch_norm(p, x, batch_norm_stats)
             ws = N.workspace("smaq", x.device, N.lib().smq_smaq_workspace_bytes(numel))
-            self._launch(x, y, numel, p, ws)
+            self._launch(x, y, numel, p, ws, code)
             del keep
 
             def new_size():
@@ -178,17 +191,18 @@ class SmartFP(CompressionAlgorithmBase):
     # bench.py sets an event recorder here to time the apply launch on the codec's stream
     _trace = None
 
-    def _launch(self, x: torch.Tensor, y: torch.Tensor, numel: int, p, ws: torch.Tensor):
+    def _launch(self, x: torch.Tensor, y: torch.Tensor, numel: int, p, ws: torch.Tensor,
+                code: int = N.SMQ_DTYPE_F32):
         lib = N.lib()
         st = N.stream_ptr(x.device)
         tr = self._trace
         if p.stats_source == N.SMQ_STATS_WORKSPACE:
-            N.check(lib.smq_smaq_stats_f32(x.data_ptr(), numel, p, ws.data_ptr(), ws.numel(), st),
-                    "smq_smaq_stats_f32")
+            N.check(lib.smq_smaq_stats(x.data_ptr(), code, numel, p, ws.data_ptr(), ws.numel(), st),
+                    "smq_smaq_stats")
         if tr is not None:
             tr.begin("apply")
-        N.check(lib.smq_smaq_apply_f32(x.data_ptr(), y.data_ptr(), numel, p, None, None,
-                                       ws.data_ptr(), ws.numel(), st), "smq_smaq_apply_f32")
+        N.check(lib.smq_smaq_apply(x.data_ptr(), code, y.data_ptr(), numel, p, None, None,
+                                   ws.data_ptr(), ws.numel(), st), "smq_smaq_apply")
         if tr is not None:
             tr.end("apply")
 

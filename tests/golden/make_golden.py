@@ -102,9 +102,9 @@ class Capture:
         torch.rand_like, torch.randperm = self._rl, self._rp
 
 
-def smaq_hparams(SmartFP, argv):
+def smaq_hparams(SmartFP, argv, precision=32):
     hp = SmartFP.add_argparse_args(ArgumentParser()).parse_args(argv)
-    hp.precision = 32
+    hp.precision = precision
     return hp
 
 
@@ -118,8 +118,8 @@ def gen_smaq(out_dir):
 
     cases = []
 
-    def case(name, x, argv=(), all_positive=False, bn=None):
-        cases.append((name, x, list(argv), all_positive, bn))
+    def case(name, x, argv=(), all_positive=False, bn=None, dtype=torch.float32, precision=32):
+        cases.append((name, x.to(dtype), list(argv), all_positive, bn, precision))
 
     n = 16384
     case("normal", normal(n))
@@ -154,10 +154,27 @@ def gen_smaq(out_dir):
     case("bn", x4, ["--use_batch_norm"], bn=(gam, bet))
     case("bn_scalar", x4, ["--use_batch_norm", "--bn_scalar_params"], bn=(gam, bet))
     case("bn_trunc", x4, ["--use_batch_norm", "--no_stochastic_rounding"], bn=(gam, bet))
+    # half inputs (Lightning precision=16): stats and z-score in the input type, fp32 output
+    h16 = dict(dtype=torch.float16, precision=16)
+    case("f16_normal", normal(n), **h16)
+    case("f16_trunc", normal(n, 0.5, 3.0), ["--no_stochastic_rounding"], **h16)
+    case("f16_sampled", normal(n), ["--use_sample_stats"], **h16)
+    case("f16_range", normal(n), ["--use_range_std_dev"], **h16)
+    case("f16_range_big", normal(70000), ["--use_range_std_dev"], **h16)  # half(n) = inf -> std 1
+    case("f16_relu_allpos", torch.relu(normal(n)), all_positive=True, **h16)
+    case("f16_constant", torch.full((4096,), 0.75), **h16)
+    case("f16_thresholds", normal(n), ["--main_std_dev_threshold", "0.8",
+                                       "--outlier_std_dev_threshold", "3.0"], **h16)
+    case("f16_bn", x4, ["--use_batch_norm"], bn=(gam, bet), **h16)
+    case("bf16_normal", normal(n), dtype=torch.bfloat16, precision=16)
+    case("bf16_normal_p32", normal(n, 0.1, 2.0), dtype=torch.bfloat16, precision=32)
+    case("bf16_trunc", normal(n), ["--no_stochastic_rounding"], dtype=torch.bfloat16, precision=16)
+    case("bf16_sampled", normal(n), ["--use_sample_stats"], dtype=torch.bfloat16, precision=16)
+    case("bf16_range", normal(n), ["--use_range_std_dev"], dtype=torch.bfloat16, precision=16)
 
     index = {}
-    for name, x, argv, allpos, bn in cases:
-        hp = smaq_hparams(SmartFP, argv + ["--measure_compression_ratio"])
+    for name, x, argv, allpos, bn, precision in cases:
+        hp = smaq_hparams(SmartFP, argv + ["--measure_compression_ratio"], precision)
         codec = SmartFP(hp)
         logged = {}
         codec.log = lambda k, v, **kw: logged.__setitem__(k, v)
@@ -167,7 +184,8 @@ def gen_smaq(out_dir):
             if bn is not None:
                 kwargs["batch_norm_stats"] = bn
             y = codec(x, tag="golden", **kwargs)
-        rec = dict(x=x.numpy(), y=y.numpy(), passthrough=np.array(y is x))
+        rec = dict(x=x.float().numpy(), y=y.float().numpy(), passthrough=np.array(y is x),
+                   y_dtype=np.array(str(y.dtype)))
         if cap.uniforms:
             rec["uniforms"] = cap.uniforms[0].astype(np.float32)
         if x.numel() >= hp.min_size:
@@ -178,8 +196,8 @@ def gen_smaq(out_dir):
                 mean, std = sample.mean(), codec._get_std(sample, unbiased=False)
             else:
                 mean, std = x.mean(), codec._get_std(x)
-            rec["mean"] = np.float32(mean.item())
-            rec["std"] = np.float32(std.item())
+            rec["mean"] = np.float32(mean.float().item())
+            rec["std"] = np.float32(std.float().item())
         if bn is not None:
             rec["bn_gamma"], rec["bn_beta"] = bn[0].numpy(), bn[1].numpy()
             if hp.bn_scalar_params:  # what smart.py:146-148 actually applies
@@ -194,7 +212,8 @@ def gen_smaq(out_dir):
         np.savez_compressed(os.path.join(out_dir, f"smaq_{name}.npz"), **rec)
         meta = vars(hp).copy()
         meta.update(all_positive=allpos, logged={k: float(v) for k, v in logged.items()},
-                    range_outlier=codec.range_outlier, range_normal=codec.range_normal)
+                    range_outlier=codec.range_outlier, range_normal=codec.range_normal,
+                    dtype={torch.float32: "f32", torch.float16: "f16", torch.bfloat16: "bf16"}[x.dtype])
         index[name] = meta
     with open(os.path.join(out_dir, "smaq_cases.json"), "w") as f:
         json.dump(index, f, indent=1, sort_keys=True)

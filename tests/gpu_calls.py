@@ -16,17 +16,22 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def smaq_params(hp, numel, all_positive=False, seed=0, offset=0):
+TORCH_DT = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}
+
+
+def smaq_params(hp, numel, all_positive=False, seed=0, offset=0, dtype=torch.float32):
     codec = SmartFP(hp)
     codec.rng.seed, codec.rng.offset = seed, offset
-    return codec._params(numel, all_positive)
+    return codec._params(numel, all_positive, dtype)
 
 
-def stats_struct(mean, std, hp):
+def stats_struct(mean, std, hp, dtype="f32"):
     """SmqSmaqStats as the kernel's finaliser would write it for (mean, std) (smart.py:151-154)."""
+    from oracle.smaq import round_to
+
     s = N.SmqSmaqStats()
-    lo = np.float32(1e-4 if hp.precision == 16 else 1e-38)
-    hi = np.float32(1e4 if hp.precision == 16 else 1e38)
+    lo = np.float32(round_to(np.float32(1e-4 if hp.precision == 16 else 1e-38), dtype))
+    hi = np.float32(round_to(np.float32(1e4 if hp.precision == 16 else 1e38), dtype))
     sd = np.float32(std)
     std_dev = np.float32(1.0) if sd == 0 else sd
     sc = std_dev
@@ -44,14 +49,14 @@ def read_stats(ws):
 
 
 def smaq_apply(x, p, uniforms=None, stats_in=None, y=None):
-    """One smq_smaq_apply_f32 launch; returns (y, ws)."""
+    """One smq_smaq_apply launch (input dtype from x, fp32 output); returns (y, ws)."""
     n = x.numel()
-    y = torch.empty_like(x) if y is None else y
+    y = torch.empty(x.shape, dtype=torch.float32, device=x.device) if y is None else y
     ws = torch.zeros(N.lib().smq_smaq_workspace_bytes(n), dtype=torch.uint8, device=x.device)
     if stats_in is not None:
         p.stats_source = N.SMQ_STATS_INJECTED
-    N.check(N.lib().smq_smaq_apply_f32(
-        x.data_ptr(), y.data_ptr(), n, p,
+    N.check(N.lib().smq_smaq_apply(
+        x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), n, p,
         uniforms.data_ptr() if uniforms is not None else None,
         stats_in.data_ptr() if stats_in is not None else None,
         ws.data_ptr(), ws.numel(), stream()), "apply")
@@ -60,10 +65,10 @@ def smaq_apply(x, p, uniforms=None, stats_in=None, y=None):
 
 def smaq_roundtrip(x, p, uniforms=None, y=None):
     n = x.numel()
-    y = torch.empty_like(x) if y is None else y
+    y = torch.empty(x.shape, dtype=torch.float32, device=x.device) if y is None else y
     ws = torch.zeros(N.lib().smq_smaq_workspace_bytes(n), dtype=torch.uint8, device=x.device)
-    N.check(N.lib().smq_smaq_roundtrip_f32(
-        x.data_ptr(), y.data_ptr(), n, p,
+    N.check(N.lib().smq_smaq_roundtrip(
+        x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), n, p,
         uniforms.data_ptr() if uniforms is not None else None,
         ws.data_ptr(), ws.numel(), stream()), "roundtrip")
     return y, ws
@@ -98,6 +103,11 @@ def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None):
     stats = dict(mu=hdr[0], m=hdr[1], alpha=hdr[2], beta=hdr[3], beta_pow2=hdr[4],
                  inv_beta_pow2=hdr[5], inv_alpha=hdr[6])
     return y, stats
+
+
+def golden_x(d, meta):
+    """The golden input on the device in the case's dtype (fixtures store exact float32 values)."""
+    return to_dev(d["x"].astype(np.float32), TORCH_DT[meta.get("dtype", "f32")])
 
 
 def to_dev(a, dtype=None):

@@ -38,6 +38,7 @@ def oracle_cfg(meta):
         stochastic_rounding=meta["stochastic_rounding"],
         use_sample_stats=meta["use_sample_stats"], num_samples=meta["num_samples"],
         use_range_std_dev=meta["use_range_std_dev"], min_size=meta["min_size"],
+        precision=meta.get("precision", 32),
     )
 
 

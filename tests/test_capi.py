@@ -88,6 +88,9 @@ def test_draw_samples():
     from smart_compress_amd import _native as N
 
     lib = N.lib()
+    q = N.SmqSmaqParams()
+    lib.smq_smaq_params_init(q)
+    assert q.range_std_coef < 0  # "library computes C"; 0.0 is a real coefficient (fp16, n>65504)
     seen = set()
     for off in range(50):
         p = N.SmqSmaqParams()

@@ -54,12 +54,12 @@ def test_golden_injected_bitexact(name):
     g = _gpu()
     meta, d = CASES[name], load_smaq(name)
     hp = smaq_hparams(meta)
-    x = g.to_dev(d["x"].astype(np.float32))
-    p = g.smaq_params(hp, x.numel(), all_positive=meta["all_positive"])
+    x = g.golden_x(d, meta)
+    p = g.smaq_params(hp, x.numel(), all_positive=meta["all_positive"], dtype=x.dtype)
     p.count_outliers = 1
     keep = []
     _bind_bn(p, d, meta, d["x"].shape, keep)
-    stats = g.stats_struct(d["mean"], d["std"], hp)
+    stats = g.stats_struct(d["mean"], d["std"], hp, meta["dtype"])
     u = g.to_dev(d["uniforms"].ravel()) if "uniforms" in d else None
     y, ws = g.smaq_apply(x.reshape(-1), p, uniforms=u, stats_in=stats)
     yh = y.cpu().numpy().reshape(d["y"].shape)
@@ -74,8 +74,8 @@ def test_golden_sampled_indices(name):
     g = _gpu()
     meta, d = CASES[name], load_smaq(name)
     hp = smaq_hparams(meta)
-    x = g.to_dev(d["x"].astype(np.float32))
-    p = g.smaq_params(hp, x.numel())
+    x = g.golden_x(d, meta)
+    p = g.smaq_params(hp, x.numel(), dtype=x.dtype)
     idx = d["sample_idx"]
     for j, v in enumerate(idx):
         p.sample_idx[j] = int(v)
@@ -83,13 +83,22 @@ def test_golden_sampled_indices(name):
     u = g.to_dev(d["uniforms"].ravel()) if "uniforms" in d else None
     y, ws = g.smaq_apply(x, p, uniforms=u)
     st = g.read_stats(ws)
-    assert ulp_diff(st["mean"], d["mean"]) <= 1
-    assert ulp_diff(st["raw_std"], d["std"]) <= 1
+    _assert_stats_close(st["mean"], d["mean"], meta["dtype"])
+    _assert_stats_close(st["raw_std"], d["std"], meta["dtype"])
     yh = y.cpu().numpy()
     if st["mean"] == d["mean"] and st["raw_std"] == d["std"]:
         assert same_f32(yh, d["y"])
     else:
         _assert_within_step(yh, d["y"], d["x"], st["raw_std"], hp)
+
+
+def _assert_stats_close(ours, ref, dtype):
+    """fp32: within 1 ulp; half types: equal or one step of the half type apart."""
+    if dtype == "f32":
+        assert ulp_diff(ours, ref) <= 1, (ours, ref)
+    else:
+        step = float(np.spacing(np.float16(ref))) if dtype == "f16" else abs(float(ref)) * 2.0**-7
+        assert abs(float(ours) - float(ref)) <= step + 1e-30, (ours, ref)
 
 
 def _assert_within_step(y, y_ref, x, std, hp, max_frac=1.0):
@@ -114,8 +123,8 @@ def test_golden_full_pipeline(name):
     g = _gpu()
     meta, d = CASES[name], load_smaq(name)
     hp = smaq_hparams(meta)
-    x = g.to_dev(d["x"].astype(np.float32)).reshape(-1)
-    p = g.smaq_params(hp, x.numel(), all_positive=meta["all_positive"])
+    x = g.golden_x(d, meta).reshape(-1)
+    p = g.smaq_params(hp, x.numel(), all_positive=meta["all_positive"], dtype=x.dtype)
     keep = []
     _bind_bn(p, d, meta, d["x"].shape, keep)
     u = g.to_dev(d["uniforms"].ravel()) if "uniforms" in d else None
@@ -123,9 +132,9 @@ def test_golden_full_pipeline(name):
     st = g.read_stats(ws)
     from oracle import smaq as osmaq
 
-    mo, so = osmaq.full_stats(d["x"], oracle_cfg(meta))
-    assert ulp_diff(st["mean"], mo) <= 1, (st["mean"], mo)
-    assert ulp_diff(st["raw_std"], so) <= 1, (st["raw_std"], so)
+    mo, so = osmaq.full_stats(d["x"], oracle_cfg(meta), meta["dtype"])
+    _assert_stats_close(st["mean"], mo, meta["dtype"])
+    _assert_stats_close(st["raw_std"], so, meta["dtype"])
     if meta["num_bits_main"] == 2:  # range_normal == 0 -> NaN like the reference
         assert np.isnan(y.cpu().numpy()).sum() == np.isnan(d["y"]).sum()
         return
@@ -303,3 +312,44 @@ def _oracle_window(xw, y, st, hp, lo, hi):
     u = orng.uniforms(5, 0, hi - lo, start=lo)
     y_or, _ = osmaq.apply(xw, st["mean"], st["raw_std"], osmaq.SmaqConfig(), u)
     assert same_f32(y[lo:hi].cpu().numpy(), y_or)
+
+
+@pytest.mark.parametrize("dt", ["f16", "bf16"])
+def test_half_inputs_end_to_end(dt):
+    """SmartFP on fp16 / bf16 tensors (Lightning precision=16): fp32 output, stats in the input
+    type, bit-exact vs the oracle fed the device statistics and counter RNG."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import SmartFP
+
+    g = _gpu()
+    tdt = g.TORCH_DT[dt]
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    x = (torch.randn(1 << 18, generator=gen, device="cuda") * 1.5 - 0.2).to(tdt)
+    hp = smaq_hparams(precision=16)
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = 3, 10
+    y = codec(x)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.float32 and y.shape == x.shape
+    st = g.read_stats(_smaq_ws())
+    xn = x.float().cpu().numpy()
+    cfg = osmaq.SmaqConfig(precision=16)
+    mo, so = osmaq.full_stats(xn, cfg, dt)
+    _assert_stats_close(st["mean"], mo, dt)
+    _assert_stats_close(st["raw_std"], so, dt)
+    y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], cfg, orng.uniforms(3, 10, xn.size),
+                          dtype=dt)
+    assert same_f32(y.cpu().numpy(), y_or)
+
+
+def test_half_precision_rules():
+    from smart_compress_amd.compress.smart import SmartFP
+
+    x = torch.randn(100, device="cuda").half()
+    with pytest.raises(RuntimeError, match="Half without overflow"):
+        SmartFP(smaq_hparams(precision=32))(x)  # std.clamp(1e-38, 1e38) overflows half
+    y = SmartFP(smaq_hparams(precision=32))(x.bfloat16())  # bf16 holds 1e38
+    assert y.dtype == torch.float32
+    with pytest.raises(NotImplementedError):
+        SmartFP(smaq_hparams())(torch.randn(100, device="cuda").double())

@@ -46,7 +46,7 @@ def test_constants_match_reference(name):
     meta = smaq_cases()[name]
     c = SmartFP(smaq_hparams(meta))
     assert c.range_outlier == meta["range_outlier"] and c.range_normal == meta["range_normal"]
-    assert c.clamped_range == (1e-38, 1e38)
+    assert c.clamped_range == ((1e-4, 1e4) if meta["precision"] == 16 else (1e-38, 1e38))
 
 
 def test_params_block():

@@ -36,7 +36,8 @@ def test_smaq_oracle_bitexact(name):
     if "bn_gamma" in d:
         bn = (d["bn_gamma_used"], d["bn_beta_used"]) if meta["bn_scalar_params"] else (
             d["bn_gamma"], d["bn_beta"])
-    y, o = smaq.apply(d["x"], d["mean"], d["std"], cfg, d.get("uniforms"), meta["all_positive"], bn)
+    y, o = smaq.apply(d["x"], d["mean"], d["std"], cfg, d.get("uniforms"), meta["all_positive"], bn,
+                      dtype=meta["dtype"])
     assert same_f32(y, d["y"]), n_diff_f32(y, d["y"])
     if int(d.get("n_outlier", -1)) >= 0:
         assert int(o.sum()) == int(d["n_outlier"])
@@ -48,13 +49,19 @@ def test_smaq_oracle_stats(name):
 
     meta, d = CASES[name], load_smaq(name)
     cfg = oracle_cfg(meta)
+    dt = meta["dtype"]
     if meta["use_sample_stats"]:
-        m, s = smaq.sampled_stats(d["x"], d["sample_idx"], cfg)
+        m, s = smaq.sampled_stats(d["x"], d["sample_idx"], cfg, dt)
     else:
-        m, s = smaq.full_stats(d["x"], cfg)
-    assert ulp_diff(s, d["std"]) <= 1
-    bound = 2.0**-21 * (abs(float(d["mean"])) + float(d["std"]))
-    assert abs(float(m) - float(d["mean"])) <= bound
+        m, s = smaq.full_stats(d["x"], cfg, dt)
+    if dt == "f32":
+        assert ulp_diff(s, d["std"]) <= 1
+        bound = 2.0**-21 * (abs(float(d["mean"])) + float(d["std"]))
+        assert abs(float(m) - float(d["mean"])) <= bound
+    else:  # 0-dim results rounded to the half type: equal, or one half-ulp step apart
+        for ours, ref in ((m, d["mean"]), (s, d["std"])):
+            step = np.spacing(np.float16(ref)) if dt == "f16" else abs(float(ref)) * 2.0**-7
+            assert abs(float(ours) - float(ref)) <= float(step) + 1e-30, (ours, ref)
 
 
 def test_smaq_logged_sizes():
