@@ -119,7 +119,11 @@ typedef struct SmqSmaqStats {
   uint32_t reserved0;
   unsigned long long n_outlier; /* multi-tensor calls: this tensor's outlier count (single-tensor
                                    calls: see SMQ_WS_OUTLIER_SLOTS_OFFSET) */
-  uint32_t reserved[6];
+  double inv_std_clamped;      /* RN64(1 / std_clamped); written by the library (injected stats:
+                                  ignored, the library derives it from std_clamped) */
+  uint32_t quot_check;         /* library-internal: 1 if (x - mean) / std_clamped can need the
+                                  IEEE subnormal path (see smaq_elem.h); derived like the above */
+  uint32_t reserved[3];
 } SmqSmaqStats;
 
 /* One tensor of a multi-tensor call. y may alias x (in-place, the optimizer path). */

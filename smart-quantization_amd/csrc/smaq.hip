@@ -139,6 +139,8 @@ struct ApplyArgs {
   SmqSmaqStats* ws_stats;        // sampled-stats destination
   unsigned long long* out_slots; // outlier count slots
   float thr, r_main, r_out, clamp_lo, clamp_hi, range_coef;
+  double inv_r_main, inv_r_out;  // host-computed reciprocals of the ranges
+  int safe_q;
   uint32_t key;
   int all_pos;
   int count;
@@ -184,18 +186,24 @@ __global__ __launch_bounds__(kWave) void smaq_sample_stats_kernel(ApplyArgs A) {
   }
 }
 
-// RM = rounding mode, TIN = input element type; VT = 4-element vector slots per lane per tile.
-template <int RM, bool VEC, bool BN, int TIN>
-__global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
-  constexpr int kTileV = (RM == kRoundTrunc) ? 1 : 2;
-  constexpr int kTileElems = kBlock * kTileV * 4;
-  __shared__ uint32_t sh_cnt[kBlock / kWave];
-  ElemConsts c;
-  const float cthr = (BN || TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
-  init_consts(c, A.stats->mean, A.stats->std_dev, A.stats->std_clamped, A.thr, A.r_main, A.r_out,
-              cthr);
-  const bool all_pos = A.all_pos != 0;
+// Injected statistics (parity tests, callers with their own mean/std): copy the record into the
+// workspace header with the fp64 reciprocal the element transform reads.
+__global__ void smaq_prep_injected_kernel(const SmqSmaqStats* in, SmqSmaqStats* out) {
+  if (threadIdx.x == 0) {
+    SmqSmaqStats s = *in;
+    s.inv_std_clamped = 1.0 / (double)s.std_clamped;
+    s.quot_check = quot_check_for(s.std_clamped);
+    *out = s;
+  }
+}
 
+// One workgroup's share of the apply launch. TV = float4 slots per lane per tile: flat tiles of
+// kBlock * TV float4 dispatched in (reverse) address order, one front across the grid.
+// SUB: see quot_check_for. The unaligned (!VEC) variant always keeps the subnormal check and
+// divides q / range by IEEE division (the launcher routes safe_q calls to it).
+template <int RM, bool VEC, bool BN, int TIN, int TV, bool AP, bool SUB>
+__device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemConsts& c) {
+  constexpr int kTileElems = kBlock * TV * 4;
   uint32_t n_out = 0;
   const int64_t n = A.n;
   if (VEC) {
@@ -205,10 +213,10 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
     const float4* __restrict__ u4 = reinterpret_cast<const float4*>(A.uniforms);
     const int64_t nv = n >> 2;
     const int64_t tile = A.reverse ? (int64_t)(gridDim.x - 1 - blockIdx.x) : (int64_t)blockIdx.x;
-    const int64_t t0 = tile * (kBlock * kTileV) + threadIdx.x;
-    float4 v[kTileV], uu[kTileV];
+    const int64_t t0 = tile * (kBlock * TV) + threadIdx.x;
+    float4 v[TV], uu[TV];
 #pragma unroll
-    for (int u = 0; u < kTileV; ++u) {
+    for (int u = 0; u < TV; ++u) {
       const int64_t j = t0 + u * kBlock;
       if (j < nv) {
         v[u] = load4<TIN>(A.x, j);
@@ -216,27 +224,21 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < kTileV; ++u) {
+    for (int u = 0; u < TV; ++u) {
       const int64_t j = t0 + u * kBlock;
       if (j >= nv) continue;
-      float u0, u1, u2, u3;
+      float u0 = 0.0f, u1 = 0.0f, u2 = 0.0f, u3 = 0.0f;
       if (RM == kRoundHash) {
-        const uint64_t ctr = A.offset + ((uint64_t)j << 2);
-        u0 = u32_to_unit(rng_u32(A.key, ctr));
-        u1 = u32_to_unit(rng_u32(A.key, ctr + 1));
-        u2 = u32_to_unit(rng_u32(A.key, ctr + 2));
-        u3 = u32_to_unit(rng_u32(A.key, ctr + 3));
+        rng_hu4(A.key, A.offset + ((uint64_t)j << 2), u0, u1, u2, u3);
       } else if (RM == kRoundUniform) {
         u0 = uu[u].x; u1 = uu[u].y; u2 = uu[u].z; u3 = uu[u].w;
-      } else {
-        u0 = u1 = u2 = u3 = 0.0f;
       }
       bool b0, b1, b2, b3;
       float4 o;
-      o.x = smaq_elem<RM, BN, TIN>(v[u].x, u0, c, all_pos, b0, bn_term<BN>(A, 4 * j + 0));
-      o.y = smaq_elem<RM, BN, TIN>(v[u].y, u1, c, all_pos, b1, bn_term<BN>(A, 4 * j + 1));
-      o.z = smaq_elem<RM, BN, TIN>(v[u].z, u2, c, all_pos, b2, bn_term<BN>(A, 4 * j + 2));
-      o.w = smaq_elem<RM, BN, TIN>(v[u].w, u3, c, all_pos, b3, bn_term<BN>(A, 4 * j + 3));
+      o.x = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].x, u0, c, b0, bn_term<BN>(A, 4 * j + 0));
+      o.y = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].y, u1, c, b1, bn_term<BN>(A, 4 * j + 1));
+      o.z = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].z, u2, c, b2, bn_term<BN>(A, 4 * j + 2));
+      o.w = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].w, u3, c, b3, bn_term<BN>(A, 4 * j + 3));
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
       store_nt(y4 + j, o);
     }
@@ -244,10 +246,10 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
     if (tile == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
       const int64_t e = (nv << 2) + threadIdx.x;
       float uf = 0.0f;
-      if (RM == kRoundHash) uf = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)e));
+      if (RM == kRoundHash) uf = rng_hu(A.key, A.offset + (uint64_t)e);
       if (RM == kRoundUniform) uf = A.uniforms[e];
       bool bt;
-      A.y[e] = smaq_elem<RM, BN, TIN>(load1<TIN>(A.x, e), uf, c, all_pos, bt, bn_term<BN>(A, e));
+      A.y[e] = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(load1<TIN>(A.x, e), uf, c, bt, bn_term<BN>(A, e));
       n_out += (unsigned)bt;
     }
   } else {
@@ -258,12 +260,34 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
       const int64_t e = e0 + (int64_t)k * kBlock;
       if (e >= n) break;
       float uf = 0.0f;
-      if (RM == kRoundHash) uf = u32_to_unit(rng_u32(A.key, A.offset + (uint64_t)e));
+      if (RM == kRoundHash) uf = rng_hu(A.key, A.offset + (uint64_t)e);
       if (RM == kRoundUniform) uf = A.uniforms[e];
       bool bt;
-      A.y[e] = smaq_elem<RM, BN, TIN>(load1<TIN>(A.x, e), uf, c, all_pos, bt, bn_term<BN>(A, e));
+      A.y[e] = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(load1<TIN>(A.x, e), uf, c, bt, bn_term<BN>(A, e));
       n_out += (unsigned)bt;
     }
+  }
+  return n_out;
+}
+
+// RM = rounding mode, TIN = input element type, TV = float4 slots per lane per tile.
+template <int RM, bool VEC, bool BN, int TIN, int TV>
+__global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
+  __shared__ uint32_t sh_cnt[kBlock / kWave];
+  ElemConsts c;
+  const float cthr = (BN || TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
+  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+  // uniform per launch: pick the body once (all_positive, subnormal-quotient check)
+  uint32_t n_out;
+  if (!VEC) {
+    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c)
+                      : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c);
+  } else if (A.stats->quot_check) {
+    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c)
+                      : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c);
+  } else {
+    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, false>(A, c)
+                      : apply_body<RM, VEC, BN, TIN, TV, false, false>(A, c);
   }
 
   if (A.count) {  // outlier count for log_size (smart.py:184-188): one atomic per workgroup,
@@ -343,18 +367,32 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   return check_launch("smaq_stats_kernel");
 }
 
+// Float4 slots per lane per tile for the stochastic-rounding kernels (env SMQ_APPLY_TILE = 1 | 2,
+// measurement knob). 2: two loads in flight per lane hide the longer SR element chain (256M, r03:
+// 0.358 vs 0.368 ms) and halve the outlier-count atomics; truncation always uses 1.
+static int sr_tile_v() {
+  static const int v = [] {
+    const char* e = getenv("SMQ_APPLY_TILE");
+    return (e && atoi(e) == 1) ? 1 : 2;
+  }();
+  return v;
+}
+
 template <int TIN>
-static void launch_apply_t(const ApplyArgs& A, int rm, bool vec, bool bn, int grid,
+static void launch_apply_t(const ApplyArgs& A, int rm, bool vec, bool bn, int tv, int grid,
                            hipStream_t st) {
-#define SMQ_APPLY(RMV, VECV, BNV) \
-  hipLaunchKernelGGL((smaq_apply_kernel<RMV, VECV, BNV, TIN>), dim3(grid), dim3(kBlock), 0, st, A)
-#define SMQ_APPLY_RM(VECV, BNV)                                 \
-  do {                                                          \
-    if (rm == kRoundHash) SMQ_APPLY(kRoundHash, VECV, BNV);     \
-    else if (rm == kRoundUniform) SMQ_APPLY(kRoundUniform, VECV, BNV); \
-    else SMQ_APPLY(kRoundTrunc, VECV, BNV);                     \
+#define SMQ_APPLY(RMV, VECV, BNV, TVV)                                                         \
+  hipLaunchKernelGGL((smaq_apply_kernel<RMV, VECV, BNV, TIN, TVV>), dim3(grid), dim3(kBlock), 0, \
+                     st, A)
+#define SMQ_APPLY_RM(VECV, BNV)                                         \
+  do {                                                                  \
+    if (rm == kRoundHash) SMQ_APPLY(kRoundHash, VECV, BNV, 1);          \
+    else if (rm == kRoundUniform) SMQ_APPLY(kRoundUniform, VECV, BNV, 1); \
+    else SMQ_APPLY(kRoundTrunc, VECV, BNV, 1);                          \
   } while (0)
-  if (vec) {
+  if (vec && !bn && rm == kRoundHash && tv == 2) {
+    SMQ_APPLY(kRoundHash, true, false, 2);
+  } else if (vec) {
     if (bn) SMQ_APPLY_RM(true, true); else SMQ_APPLY_RM(true, false);
   } else {
     if (bn) SMQ_APPLY_RM(false, true); else SMQ_APPLY_RM(false, false);
@@ -383,6 +421,10 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   A.r_out = p->range_outlier;
   A.clamp_lo = p->clamp_lo;
   A.clamp_hi = p->clamp_hi;
+  const RangeRecips R = range_recips(p->range_main, p->range_outlier);
+  A.inv_r_main = R.inv_main;
+  A.inv_r_out = R.inv_out;
+  A.safe_q = R.safe_q;
   A.key = rng_key(p->seed);
   A.offset = p->offset;
   A.all_pos = p->all_positive;
@@ -421,7 +463,7 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   }
   const int rm = !p->stochastic_rounding ? kRoundTrunc : (uniforms ? kRoundUniform : kRoundHash);
   const bool vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) && aligned(y, 16) &&
-                   (rm != kRoundUniform || aligned(uniforms, 16));
+                   (rm != kRoundUniform || aligned(uniforms, 16)) && !A.safe_q;
   A.out_slots = (unsigned long long*)((char*)ws + SmaqWsLayout::kSlots);
   if (p->count_outliers) {
     if (hipMemsetAsync(A.out_slots, 0, 8 * SMQ_WS_OUTLIER_SLOTS, st) != hipSuccess) {
@@ -435,13 +477,19 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   }();
   // reverse only pays after a forward statistics sweep of the same tensor
   A.reverse = (p->stats_source == SMQ_STATS_WORKSPACE) ? rev_env : 0;
-  const int64_t tile_elems = (int64_t)kBlock * 4 * (rm == kRoundTrunc ? 1 : 2);
+  const int tv = (rm == kRoundHash && vec && !A.bn_gamma) ? sr_tile_v() : 1;
+  const int64_t tile_elems = (int64_t)kBlock * 4 * tv;
   const int64_t tiles = (n + tile_elems - 1) / tile_elems;
   if (tiles > 0x7fffffffLL) {
     set_error("tensor too large: %lld elements", (long long)n);
     return SMQ_ERR_INVALID;
   }
   const int grid = (int)tiles;
+  if (p->stats_source == SMQ_STATS_INJECTED) {
+    hipLaunchKernelGGL(smaq_prep_injected_kernel, dim3(1), dim3(kWave), 0, st, stats_in,
+                       A.ws_stats);
+    A.stats = A.ws_stats;
+  }
   if (p->stats_source == SMQ_STATS_SAMPLED) {
     if (dtype == SMQ_DTYPE_F32)
       hipLaunchKernelGGL(smaq_sample_stats_kernel<kF32>, dim3(1), dim3(kWave), 0, st, A);
@@ -452,9 +500,9 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
     A.stats = A.ws_stats;
   }
   const bool bn = A.bn_gamma != nullptr;
-  if (dtype == SMQ_DTYPE_F32) launch_apply_t<kF32>(A, rm, vec, bn, grid, st);
-  else if (dtype == SMQ_DTYPE_F16) launch_apply_t<kF16>(A, rm, vec, bn, grid, st);
-  else launch_apply_t<kBF16>(A, rm, vec, bn, grid, st);
+  if (dtype == SMQ_DTYPE_F32) launch_apply_t<kF32>(A, rm, vec, bn, tv, grid, st);
+  else if (dtype == SMQ_DTYPE_F16) launch_apply_t<kF16>(A, rm, vec, bn, tv, grid, st);
+  else launch_apply_t<kBF16>(A, rm, vec, bn, tv, grid, st);
   return check_launch("smaq_apply_kernel");
 }
 

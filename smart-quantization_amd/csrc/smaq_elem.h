@@ -117,6 +117,20 @@ struct FinalizeArgs {
 // mean / std from shifted sums -> SmqSmaqStats (smart.py:130-134, 100-108, 151-152, 154).
 // T = input type: torch reduces half tensors in fp32/fp64 and rounds the 0-dim result to half
 // (through fp32, i.e. RN_T(RN32(.))), exactly what round_in<T>((float)x) does.
+// Does z = RN32(RN64(dm * RN64(1/sc))) need the IEEE fallback when z is subnormal?
+// dm is a multiple of 2^-149 (every fp32 / fp16 / bf16 difference is). Write sc = S * 2^e, S odd.
+// The distance of dm / sc from a midpoint of the subnormal grid (2m+1) * 2^-150 is
+// |dm * 2^150 - sc * (2m+1)| / (sc * 2^150). For e <= 0 the numerator is a nonzero multiple of 2^e
+// (even minus odd after scaling by 2^-e), so the distance is >= 2^-174 > 2^-48 * |z| for |z| <
+// 2^-126, while the double product is within 2^-52 * |z|: the fp32 rounding is the IEEE one. For
+// e >= 1 (sc an even integer) exact midpoints exist, and sc >= 2^24 is excluded for margin: those
+// calls keep the per-element check.
+__host__ __device__ __forceinline__ uint32_t quot_check_for(float sc) {
+  const float h = sc * 0.5f;
+  const bool even_int = (h == truncf(h)) && h != 0.0f;  // sc = odd * 2^e with e >= 1
+  return (even_int || !(fabsf(sc) < 0x1p24f)) ? 1u : 0u;
+}
+
 template <bool RANGE, int T = kF32>
 __device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, float mx, int64_t n,
                                                double shift, bool biased, FinalizeArgs f,
@@ -144,6 +158,8 @@ __device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, f
   out->max_val = mx;
   out->n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
   out->n_outlier = 0ull;
+  out->inv_std_clamped = 1.0 / (double)sc;  // once per call, for the element transform
+  out->quot_check = quot_check_for(sc);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -155,8 +171,8 @@ struct ElemConsts {
   float cthr, cnthr;      // thresholds as compared with z: rounded to z's type
   float zh, zl;           // 0 * -T_m, 0 * T_m  (the bool*float zero terms, smart.py:159-161)
   float r_main, r_out;    // ranges
-  double inv_sc;          // RN64(1 / sc)
-  double inv_r_main, inv_r_out;  // RN64(1 / range)
+  double inv_sc;          // RN64(1 / sc): written by the statistics finaliser
+  double inv_r_main, inv_r_out;  // RN64(1 / range): computed on the host
 };
 
 // Correctly rounded fp32 quotient a / b from a double reciprocal: RN32(RN64(a * RN64(1/b))).
@@ -170,11 +186,15 @@ __device__ __forceinline__ float div_by_const(float a, double inv_b) {
   return (float)((double)a * inv_b);
 }
 
-__device__ __forceinline__ void init_consts(ElemConsts& c, float mean, float sd, float sc, float thr,
-                                            float r_main, float r_out, float cthr) {
-  c.mean = mean;
-  c.sd = sd;
-  c.sc = sc;
+// The reciprocals come precomputed (statistics record / kernel arguments): a per-workgroup fp64
+// division costs ~15 dependent VALU, more than the elements of a one-vector tile.
+__device__ __forceinline__ void init_consts(ElemConsts& c, const SmqSmaqStats* st, float thr,
+                                            float r_main, float r_out, double inv_r_main,
+                                            double inv_r_out, float cthr) {
+  c.mean = st->mean;
+  c.sd = st->std_dev;
+  c.sc = st->std_clamped;
+  c.inv_sc = st->inv_std_clamped;
   c.thr = thr;
   c.nthr = -thr;
   c.cthr = cthr;
@@ -183,11 +203,53 @@ __device__ __forceinline__ void init_consts(ElemConsts& c, float mean, float sd,
   c.zl = 0.0f * c.thr;
   c.r_main = r_main;
   c.r_out = r_out;
-  c.inv_sc = 1.0 / (double)sc;
-  c.inv_r_main = 1.0 / (double)r_main;
-  c.inv_r_out = 1.0 / (double)r_out;
+  c.inv_r_main = inv_r_main;
+  c.inv_r_out = inv_r_out;
 }
 
+// Host: reciprocals of the two ranges (IEEE double division, as the device would compute them).
+// safe_q: with a range beyond 2^100 (absurd flags) a quotient q / range can be subnormal, where the
+// reciprocal product is not exact; the element transform then takes an IEEE division.
+struct RangeRecips {
+  double inv_main, inv_out;
+  int safe_q;
+};
+static inline RangeRecips range_recips(float r_main, float r_out) {
+  RangeRecips R;
+  R.inv_main = 1.0 / (double)r_main;
+  R.inv_out = 1.0 / (double)r_out;
+  const double lim = 0x1p100;
+  R.safe_q = !(fabs((double)r_main) <= lim && fabs((double)r_out) <= lim);
+  return R;
+}
+
+// kRoundHash draws: h >> 8 of the counter hash as a float (exact, < 2^24), see smaq_elem.
+__device__ __forceinline__ float rng_hu(uint32_t key, uint64_t ctr) {
+  return (float)(rng_u32(key, ctr) >> 8);
+}
+
+// Draws for counters ctr .. ctr+3 (one float4 of elements): the same values as four rng_hu calls;
+// the high counter word is rotated once unless the low word wraps inside the group.
+__device__ __forceinline__ void rng_hu4(uint32_t key, uint64_t ctr, float& u0, float& u1, float& u2,
+                                        float& u3) {
+  const uint32_t lo = (uint32_t)ctr;
+  if (__builtin_expect(lo <= 0xfffffffcu, 1)) {
+    const uint32_t hi = (uint32_t)(ctr >> 32);
+    const uint32_t kk = ((hi << 16) | (hi >> 16)) ^ key;
+    u0 = (float)(mix32(lo ^ kk) >> 8);
+    u1 = (float)(mix32((lo + 1u) ^ kk) >> 8);
+    u2 = (float)(mix32((lo + 2u) ^ kk) >> 8);
+    u3 = (float)(mix32((lo + 3u) ^ kk) >> 8);
+  } else {
+    u0 = rng_hu(key, ctr);
+    u1 = rng_hu(key, ctr + 1);
+    u2 = rng_hu(key, ctr + 2);
+    u3 = rng_hu(key, ctr + 3);
+  }
+}
+
+// kRoundHash: u arrives as the integer h >> 8 (a float in [0, 2^24)); fr - u is then the single
+// rounding fma(h, -2^-24, fr) == RN(fr - h * 2^-24) (the product is exact), one op fewer.
 enum RoundMode { kRoundHash = 0, kRoundUniform = 1, kRoundTrunc = 2 };
 
 // Per-channel BatchNorm fold (smart.py:144-149 before, 174-179 after); scale = gamma[c].
@@ -197,15 +259,18 @@ struct BnTerm {
 
 // One element of smart.py:154-182. Each statement is one rounded fp32 op of the reference.
 // T = input type (z-score rounded to it unless BN already promoted the data to fp32).
-template <int RM, bool BN = false, int T = kF32>
-__device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c, bool all_pos,
+// AP: all_positive; SUB: keep the subnormal-quotient check (quot_check_for); SQ: divide q / range
+// by IEEE division (RangeRecips::safe_q).
+template <int RM, bool BN = false, int T = kF32, bool AP = false, bool SUB = true, bool SQ = false>
+__device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c,
                                            bool& is_outlier, BnTerm bn = BnTerm{1.0f, 0.0f}) {
   constexpr int TZ = BN ? kF32 : T;  // fp32 BN parameters promote the data to fp32
   if (BN) v = (v - bn.beta) / bn.gamma;                 // (data - beta) / gamma
   const float dm = round_in<TZ>(v - c.mean);            // data - mean
   float z = div_by_const(dm, c.inv_sc);                 // / std.clamp(...)
-  // subnormal quotient (class mask 0x90 = -/+ denormal, one v_cmp_class_f32): IEEE division
-  if (__builtin_expect(__builtin_amdgcn_class(z, 0x90), 0)) z = dm / c.sc;
+  // subnormal quotient (class mask 0x90 = -/+ denormal, one v_cmp_class_f32): IEEE division.
+  // (classf: the unsuffixed builtin takes a double, where a promoted float is never subnormal.)
+  if (SUB && __builtin_expect(__builtin_amdgcn_classf(z, 0x90), 0)) z = dm / c.sc;
   z = round_in<TZ>(z);
   const bool hi = z > c.cthr;                           // is_outlier_higher
   const bool lo = z < c.cnthr;                          // is_outlier_lower
@@ -220,14 +285,15 @@ __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c
   } else {
     const float f = floorf(d);                          // _round_stochastic, smart.py:93-98
     const float fr = d - f;
-    float t = (fr - u) + 0.5f;
+    float t = ((RM == kRoundHash) ? __builtin_fmaf(u, -0x1p-24f, fr) : (fr - u)) + 0.5f;
     t = (t < 0.0f) ? 0.0f : t;                          // F.relu
     q = f + __builtin_rintf(t);                         // .round() = half to even
   }
-  float out = div_by_const(q, inv_r) - a;               // (data / ranges) - scalars
+  const float qr = SQ ? q / r : div_by_const(q, inv_r);  // data / ranges
+  float out = qr - a;                                   //   - scalars
   out = (out * c.sd) + c.mean;
   if (BN) out = (out * bn.gamma) + bn.beta;             // (data * gamma) + beta
-  if (all_pos) out = (out < 0.0f) ? 0.0f : out;         // clamp_min(0.0)
+  if (AP) out = (out < 0.0f) ? 0.0f : out;              // clamp_min(0.0)
   is_outlier = o;
   return out;
 }

@@ -53,6 +53,8 @@ struct MultiArgs {
   uint32_t* counters;        // [count]
   StatPartial* partials;     // [n_chunks]
   float thr, r_main, r_out, clamp_lo, clamp_hi;
+  double inv_r_main, inv_r_out;
+  int safe_q;
   uint32_t key;
   uint64_t offset;           // params.offset; tensor t draws from offset + desc.rng_offset + i
   int sr;
@@ -119,14 +121,18 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   }
 }
 
-template <bool SR>
-__global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
-  __shared__ unsigned long long sh_cnt[kBlock / kWave];
-  const ChunkDesc ch = A.chunks[blockIdx.x];
-  const SmqSmaqStats* st = &A.stats[ch.tensor];
-  ElemConsts c;
-  init_consts(c, st->mean, st->std_dev, st->std_clamped, A.thr, A.r_main, A.r_out, A.thr);
-  const bool all_pos = ch.all_positive != 0;
+// all_positive varies per tensor here (one chunk = one tensor): a per-element select.
+template <int RM, bool SUB, bool SQ>
+__device__ __forceinline__ float elem_ap(float v, float u, const ElemConsts& c, bool all_pos,
+                                         bool& b) {
+  const float o = smaq_elem<RM, false, kF32, false, SUB, SQ>(v, u, c, b);
+  return (all_pos && o < 0.0f) ? 0.0f : o;  // clamp_min(0.0)
+}
+
+// One chunk. SUB: subnormal-quotient check (per tensor, quot_check_for); SQ: RangeRecips::safe_q.
+template <bool SR, bool SUB, bool SQ>
+__device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, const ChunkDesc& ch,
+                                                          const ElemConsts& c, bool all_pos) {
   const float* __restrict__ x = ch.x;
   float* y = ch.y;  // may alias x
   unsigned long long n_out = 0;
@@ -148,37 +154,45 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
       if (j >= e4) continue;
       const uint64_t ctr = A.offset + ch.rng_offset + ((uint64_t)j << 2);
       float u0 = 0.f, u1 = 0.f, u2 = 0.f, u3 = 0.f;
-      if (SR) {
-        u0 = u32_to_unit(rng_u32(A.key, ctr));
-        u1 = u32_to_unit(rng_u32(A.key, ctr + 1));
-        u2 = u32_to_unit(rng_u32(A.key, ctr + 2));
-        u3 = u32_to_unit(rng_u32(A.key, ctr + 3));
-      }
+      if (SR) rng_hu4(A.key, ctr, u0, u1, u2, u3);
       bool b0, b1, b2, b3;
       float4 o;
-      o.x = smaq_elem<RM>(v[u].x, u0, c, all_pos, b0);
-      o.y = smaq_elem<RM>(v[u].y, u1, c, all_pos, b1);
-      o.z = smaq_elem<RM>(v[u].z, u2, c, all_pos, b2);
-      o.w = smaq_elem<RM>(v[u].w, u3, c, all_pos, b3);
+      o.x = elem_ap<RM, SUB, SQ>(v[u].x, u0, c, all_pos, b0);
+      o.y = elem_ap<RM, SUB, SQ>(v[u].y, u1, c, all_pos, b1);
+      o.z = elem_ap<RM, SUB, SQ>(v[u].z, u2, c, all_pos, b2);
+      o.w = elem_ap<RM, SUB, SQ>(v[u].w, u3, c, all_pos, b3);
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
       y4[j] = o;
     }
     }
     if (threadIdx.x < (int)(ch.end - (e4 << 2))) {
       const int64_t e = (e4 << 2) + threadIdx.x;
-      const float u = SR ? u32_to_unit(rng_u32(A.key, A.offset + ch.rng_offset + (uint64_t)e)) : 0.f;
+      const float u = SR ? rng_hu(A.key, A.offset + ch.rng_offset + (uint64_t)e) : 0.f;
       bool b;
-      y[e] = smaq_elem<RM>(x[e], u, c, all_pos, b);
+      y[e] = elem_ap<RM, SUB, SQ>(x[e], u, c, all_pos, b);
       n_out += (unsigned)b;
     }
   } else {
     for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) {
-      const float u = SR ? u32_to_unit(rng_u32(A.key, A.offset + ch.rng_offset + (uint64_t)j)) : 0.f;
+      const float u = SR ? rng_hu(A.key, A.offset + ch.rng_offset + (uint64_t)j) : 0.f;
       bool b;
-      y[j] = smaq_elem<RM>(x[j], u, c, all_pos, b);
+      y[j] = elem_ap<RM, SUB, SQ>(x[j], u, c, all_pos, b);
       n_out += (unsigned)b;
     }
   }
+  return n_out;
+}
+
+template <bool SR, bool SQ>
+__global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
+  __shared__ unsigned long long sh_cnt[kBlock / kWave];
+  const ChunkDesc ch = A.chunks[blockIdx.x];
+  const SmqSmaqStats* st = &A.stats[ch.tensor];
+  ElemConsts c;
+  init_consts(c, st, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, A.thr);
+  const bool all_pos = ch.all_positive != 0;
+  const unsigned long long n_out = st->quot_check ? multi_chunk<SR, true, SQ>(A, ch, c, all_pos)
+                                                  : multi_chunk<SR, false, SQ>(A, ch, c, all_pos);
   if (A.count_outliers) {
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
     const double t = wave_sum((double)n_out);
@@ -338,6 +352,10 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   A.r_out = p->range_outlier;
   A.clamp_lo = p->clamp_lo;
   A.clamp_hi = p->clamp_hi;
+  const RangeRecips R = range_recips(p->range_main, p->range_outlier);
+  A.inv_r_main = R.inv_main;
+  A.inv_r_out = R.inv_out;
+  A.safe_q = R.safe_q;
   A.key = rng_key(p->seed);
   A.offset = p->offset;
   A.sr = p->stochastic_rounding;
@@ -346,9 +364,13 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   hipLaunchKernelGGL(smaq_multi_stats_kernel, dim3(n_chunks), dim3(kBlock), 0, st, A);
   int rc = check_launch("smaq_multi_stats_kernel");
   if (rc) return rc;
-  if (A.sr)
-    hipLaunchKernelGGL(smaq_multi_apply_kernel<true>, dim3(n_chunks), dim3(kBlock), 0, st, A);
-  else
-    hipLaunchKernelGGL(smaq_multi_apply_kernel<false>, dim3(n_chunks), dim3(kBlock), 0, st, A);
+#define SMQ_MULTI_APPLY(SRV, SQV) \
+  hipLaunchKernelGGL((smaq_multi_apply_kernel<SRV, SQV>), dim3(n_chunks), dim3(kBlock), 0, st, A)
+  if (A.sr) {
+    if (A.safe_q) SMQ_MULTI_APPLY(true, true); else SMQ_MULTI_APPLY(true, false);
+  } else {
+    if (A.safe_q) SMQ_MULTI_APPLY(false, true); else SMQ_MULTI_APPLY(false, false);
+  }
+#undef SMQ_MULTI_APPLY
   return check_launch("smaq_multi_apply_kernel");
 }

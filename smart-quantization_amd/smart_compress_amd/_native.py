@@ -70,7 +70,9 @@ class SmqSmaqStats(ctypes.Structure):
         ("n_used", ctypes.c_uint32),
         ("reserved0", ctypes.c_uint32),
         ("n_outlier", ctypes.c_ulonglong),
-        ("reserved", ctypes.c_uint32 * 6),
+        ("inv_std_clamped", ctypes.c_double),
+        ("quot_check", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 3),
     ]
 
 

@@ -54,6 +54,15 @@ _SMAQ_FLAGS = (
 _range_coef_cache = {}
 
 
+def quot_check_for(sc: float) -> int:
+    """Host mirror of smaq_elem.h ``quot_check_for`` (tests): 1 when the element transform keeps
+    the subnormal-quotient check for this clamped std (an even integer, or >= 2^24)."""
+    sc = float(np.float32(sc))
+    h = float(np.float32(sc * 0.5))
+    even_int = h == float(np.trunc(h)) and h != 0.0
+    return 1 if (even_int or not abs(sc) < 2.0**24) else 0
+
+
 def range_std_coef(n: int, dtype: torch.dtype = torch.float32) -> float:
     """C = 1 / sqrt(2 log n) evaluated with the reference's torch ops in the data's dtype
     (smart.py:101-106: ``torch.tensor(numel).type_as(range_)``; for half data n > 65504 becomes

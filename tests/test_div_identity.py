@@ -19,3 +19,16 @@ def test_div_identity(tmp_path):
     assert r["mismatches"] == 0 and r["checked"] > 4.9e7
     r = json.loads(subprocess.check_output([exe, "all", "15"]))
     assert r["mismatches"] == 0 and r["checked"] > 4.2e9
+
+
+def test_div_identity_subnormal_quotients(tmp_path):
+    """Subnormal quotients (smaq_elem.h quot_check_for): exact for every divisor that is neither an
+    even integer nor >= 2^24, so those calls skip the per-element check; the checked divisors are
+    exercised too (they keep the IEEE fallback on the GPU)."""
+    exe = str(tmp_path / "div_check")
+    subprocess.check_call(["gcc", "-O2", "-fopenmp", "-ffp-contract=off",
+                           os.path.join(REPO, "oracle", "csrc", "div_check.c"), "-o", exe, "-lm"])
+    r = json.loads(subprocess.check_output([exe, "subrand", "1000000"]))
+    assert r["mismatches"] == 0 and r["checked"] > 2.5e7
+    r = json.loads(subprocess.check_output([exe, "sub", "3", "0.7", "1.3e-5"]))
+    assert r["mismatches"] == 0 and r["checked"] > 5e7

@@ -353,3 +353,56 @@ def test_half_precision_rules():
     assert y.dtype == torch.float32
     with pytest.raises(NotImplementedError):
         SmartFP(smaq_hparams())(torch.randn(100, device="cuda").double())
+
+
+def _subnormal_mix(n, seed):
+    """Subnormal floats, tiny normals and ordinary values, both signs."""
+    rs = np.random.default_rng(seed)
+    bits = rs.integers(1, 1 << 23, n, dtype=np.uint32)  # subnormal patterns
+    x = bits.view(np.float32).copy()
+    x[1::4] = rs.uniform(1e-38, 1e-30, x[1::4].size).astype(np.float32)
+    x[2::4] = rs.normal(0, 1, x[2::4].size).astype(np.float32)
+    x[rs.random(n) < 0.5] *= -1
+    return x
+
+
+@pytest.mark.parametrize("sc", [3.0, 0.7, 6.0, 2.0**25])
+def test_subnormal_z_paths(sc):
+    """z = (x - mean) / std subnormal: the guard-free body (sc neither an even integer nor >= 2^24,
+    proven exact by oracle/csrc/div_check.c) and the checked body both match IEEE division."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import quot_check_for
+
+    g = _gpu()
+    hp = smaq_hparams()
+    x = _subnormal_mix(1 << 16, int(sc * 10))
+    xd = g.to_dev(x)
+    p = g.smaq_params(hp, x.size, seed=5, offset=11)
+    stats = g.stats_struct(0.0, sc, hp)
+    y, ws = g.smaq_apply(xd, p, stats_in=stats)
+    torch.cuda.synchronize()
+    flag = int(ws[48:52].cpu().numpy().view(np.uint32)[0])
+    assert flag == quot_check_for(sc) == (1 if sc in (6.0, 2.0**25) else 0)
+    y_or, _ = osmaq.apply(x, 0.0, sc, osmaq.SmaqConfig(), orng.uniforms(5, 11, x.size))
+    assert same_f32(y.cpu().numpy(), y_or), n_diff_f32(y.cpu().numpy(), y_or)
+
+
+def test_huge_range_ieee_quotient():
+    """A range beyond 2^100 (main threshold 1e-37 -> r_main ~ 1.5e38) makes q / range subnormal:
+    the launcher routes it to the IEEE-division variant; bit-exact vs the oracle."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+
+    g = _gpu()
+    hp = smaq_hparams(main_std_dev_threshold=1e-37)
+    x = _subnormal_mix(1 << 14, 3)
+    x[2::4] *= 1e-30
+    p = g.smaq_params(hp, x.size, seed=9, offset=0)
+    y, _ = g.smaq_apply(g.to_dev(x), p, stats_in=g.stats_struct(0.0, 1.0, hp))
+    torch.cuda.synchronize()
+    cfg = osmaq.SmaqConfig(main_std_dev_threshold=1e-37)
+    y_or, _ = osmaq.apply(x, 0.0, 1.0, cfg, orng.uniforms(9, 0, x.size))
+    yh = y.cpu().numpy()
+    assert same_f32(yh, y_or), n_diff_f32(yh, y_or)
+    assert np.any((np.abs(yh) < np.finfo(np.float32).tiny) & (yh != 0))  # subnormal q / range hit

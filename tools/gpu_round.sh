@@ -20,15 +20,15 @@ for s in "$@"; do
     statsbench) step statsbench 300 ./tools/statsbench ;;
     kbench) step kbench 300 python tools/kbench.py ;;
     rev) for r in 0 1; do SMQ_APPLY_REVERSE=$r step kbench_rev$r 300 python tools/kbench.py --quick; done ;;
-    fqtiles) for v in 1 2 4; do SMQ_FQ_TILE=$v step bench_fp8_t$v 300 python bench.py --config fp8 --steps 50 --warmup 5; SMQ_FQ_TILE=$v step bench_s2fp8_t$v 300 python bench.py --config s2fp8 --steps 200 --warmup 20; done ;;
-    cold) for v in 1 2 4; do SMQ_APPLY_TILE=$v step kbench_cold_t$v 300 python tools/kbench.py --quick --cold; done ;;
+    fqtiles) for v in 1 2; do SMQ_FQ_TILE=$v step bench_fp8_t$v 300 python bench.py --config fp8 --steps 50 --warmup 5; SMQ_FQ_TILE=$v step bench_s2fp8_t$v 300 python bench.py --config s2fp8 --steps 200 --warmup 20; done ;;
+    cold) for v in 1 2; do SMQ_APPLY_TILE=$v step kbench_cold_t$v 300 python tools/kbench.py --quick --cold; done ;;
     chunks) for c in 4096 8192 16384 32768; do SMQ_MULTI_CHUNK=$c step bench_multi_c$c 300 python bench.py --config multi --steps 100 --warmup 10; done ;;
     diag) step bench_diag 300 python tools/bench_diag.py ;;
     warm) step bench_w3 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline &&
           step bench_w20 300 python bench.py --steps 50 --warmup 20 --no-cpu-baseline &&
           step bench_w50 300 python bench.py --steps 100 --warmup 50 --no-cpu-baseline ;;
     dist2) SMQ_BENCH_SHARE_DEVICE=1 SMQ_BENCH_BACKEND=gloo step bench_dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --elements 67108864 ;;
-    tiles) for v in 1 2 4; do SMQ_APPLY_TILE=$v step kbench_tile$v 300 python tools/kbench.py --quick; done ;;
+    tiles) for v in 1 2; do SMQ_APPLY_TILE=$v step kbench_tile$v 300 python tools/kbench.py --quick; done ;;
     profile) step profile 1500 bash tools/profile_round.sh r01 smaq ;;
     profile_*) c=${s#profile_}; step profile_$c 1500 bash tools/profile_round.sh r01_$c $c 50 10 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
