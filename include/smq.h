@@ -22,6 +22,11 @@
  *                           qtorch 0.2.0 float_quantize it calls (quantization.py:3) —
  *                           used by compress/fp8.py:31, fp16.py:31, bf16.py:31
  *   smq_s2fp8_roundtrip_f32 smart_compress/compress/s2fp8.py:27-48
+ *   smq_smaq_compress /     the packed SmaQ container: the codes smart.py:154-169
+ *   smq_smaq_decompress     computes, stored in the [outlier flag][sign][N-2 magnitude] layout
+ *                           of README.md:25-28 (6 bits per main element, 8 per outlier by
+ *                           default) with an escape list for codes outside the budget, so
+ *                           decompress(compress(x)) is bit-identical to smart.py:171-182
  *
  * Errors: every function returns SMQ_OK (0) or a negative SMQ_ERR_* code; the message of the
  * last failure on the calling thread is returned by smq_last_error(). Nothing aborts.
@@ -220,6 +225,63 @@ int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
 
 /* ---- host reference helpers shared with the oracle (pure functions, no GPU) ---- */
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
+
+
+/* ---------------------------------------------------------------------------------------------
+ * Packed SmaQ container (format version 1)
+ *
+ * stream = SmqPackedHeader (128 B) | directory: n_blocks x uint64 (word offset of each block in
+ *          the data region) | data region (uint32 words)
+ * block  = SMQ_PACK_BLOCK elements (the last one may be shorter); its words:
+ *   w[0]                 n_out (bits 0-15) | n_esc (bits 16-31)
+ *   w[1 .. 128]          outlier mask: bit (e % 32) of word e / 32 = element e is an outlier
+ *   main plane           one (num_bits_main - 1)-bit two's-complement code q per main element,
+ *                        in element order, LSB-first across words (k-th main code at bits
+ *                        [k * wm, (k + 1) * wm)); ceil(wm * n_main / 32) words
+ *   outlier plane        one (num_bits_outlier - 1)-bit code per outlier: top bit = side
+ *                        (1: z < -T, the code is -q; 0: z > T, the code is q), the rest = |q|;
+ *                        ceil(wo * n_out / 32) words
+ *   escapes              n_esc x {element index in the block, q as float32 bits}, in element
+ *                        order: codes outside the budget (|q| too large, a negative q for z > T,
+ *                        a positive q for z < -T, inf / NaN); their plane slots hold 0
+ * Decoding: q -> (q / range) - scalars, * std + mean (smart.py:171-182), bit-identical to
+ * smq_smaq_apply for the same statistics, rounding mode and random stream. Needs T_m > 0.
+ * ------------------------------------------------------------------------------------------- */
+#define SMQ_PACK_MAGIC 0x50514d53u /* "SMQP" */
+#define SMQ_PACK_VERSION 1u
+#define SMQ_PACK_BLOCK 4096
+
+typedef struct SmqPackedHeader {
+  uint32_t magic;             /* SMQ_PACK_MAGIC */
+  uint32_t version;           /* SMQ_PACK_VERSION */
+  int64_t n;                  /* elements */
+  uint32_t block_elems;       /* SMQ_PACK_BLOCK */
+  uint32_t n_blocks;
+  int32_t num_bits_main, num_bits_outlier;
+  uint32_t flags;             /* bit 0: all_positive, bit 1: IEEE q / range (absurd ranges) */
+  float thr;                  /* T_m (fp32) */
+  float range_main, range_outlier;
+  float mean, std_dev;        /* de-normalisation statistics (std after the ==0 rule) */
+  double inv_range_main, inv_range_outlier;
+  uint64_t data_words;        /* size of the data region in uint32 words */
+  uint64_t total_bytes;       /* header + directory + data */
+  uint32_t error;             /* nonzero: the packing launch gave up waiting on a predecessor */
+  uint32_t reserved[9];
+} SmqPackedHeader;
+
+/* Worst-case stream size (every element an outlier and escaped) for n elements. */
+size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier);
+/* Workspace of smq_smaq_compress (statistics + look-back status words). */
+size_t smq_smaq_pack_workspace_bytes(int64_t n);
+/* Statistics (full / sampled / range, params as smq_smaq_stats) then one packing launch. Writes the
+ * whole stream incl. header.total_bytes on the device; packed_bytes >= smq_smaq_pack_bound. The BN
+ * variant and injected uniforms are not supported (SMQ_ERR_INVALID). */
+int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
+                      void* packed, size_t packed_bytes, void* workspace, size_t workspace_bytes,
+                      void* stream);
+/* Decode a stream of n elements into y (fp32). n must equal the header's n (a stream with another
+ * n or a bad magic leaves y untouched). */
+int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -92,12 +92,10 @@ def sampled_stats(x: np.ndarray, idx: np.ndarray, cfg: SmaqConfig, dtype: str = 
     return mean, F32(round_to(F32(np.sqrt(float(np.dot(d, d)) / s64.size)), dtype))
 
 
-def apply(x: np.ndarray, mean, std, cfg: SmaqConfig, uniforms: Optional[np.ndarray] = None,
-          all_positive: bool = False, bn: Optional[Tuple[np.ndarray, np.ndarray]] = None,
-          dtype: str = "f32"):
-    """smart.py:144-182 given (mean, std). Returns (y, is_outlier). For dtype 'f16' / 'bf16' the
-    z-score is computed in that type (x, mean, std hold values of it) and the rest in float32 —
-    the reference's torch type promotion; the output is float32."""
+def codes(x: np.ndarray, mean, std, cfg: SmaqConfig, uniforms: Optional[np.ndarray] = None,
+          bn: Optional[Tuple[np.ndarray, np.ndarray]] = None, dtype: str = "f32"):
+    """smart.py:144-169 given (mean, std): the integer-valued codes q and the outlier sides.
+    Returns (q, hi, lo, std) with std after the ==0 rule (smart.py:151-152)."""
     x = np.asarray(x, dtype=F32)
     shape = x.shape
     mean, std = F32(mean), F32(std)
@@ -122,10 +120,7 @@ def apply(x: np.ndarray, mean, std, cfg: SmaqConfig, uniforms: Optional[np.ndarr
         z = round_to(round_to(data - mean, zt) / sc, zt)
         hi = z > cthr
         lo = z < -cthr
-        o = hi | lo
-        scal = np.where(hi, -thr, F32(0) * -thr) + np.where(lo, thr, F32(0) * thr)
-        scal = scal.astype(F32)
-        ranges = np.where(o, r_out, r_main).astype(F32)
+        scal, ranges = _scalars_ranges(hi, lo, thr, r_main, r_out)
         d = (z + scal) * ranges
         if cfg.stochastic_rounding:  # smart.py:93-98
             u = np.asarray(uniforms, dtype=F32).reshape(shape)
@@ -136,13 +131,43 @@ def apply(x: np.ndarray, mean, std, cfg: SmaqConfig, uniforms: Optional[np.ndarr
             q = f + np.rint(t)
         else:
             q = np.trunc(d)
-        y = (q / ranges) - scal
+    return q.astype(F32), hi, lo, std
+
+
+def _scalars_ranges(hi, lo, thr, r_main, r_out):
+    """smart.py:159-162: scalars = hi * -T + lo * T (bool * float: +-0 zero terms), ranges."""
+    scal = np.where(hi, -thr, F32(0) * -thr) + np.where(lo, thr, F32(0) * thr)
+    ranges = np.where(hi | lo, r_out, r_main)
+    return scal.astype(F32), ranges.astype(F32)
+
+
+def dequant(q, hi, lo, mean, std, cfg: SmaqConfig, all_positive: bool = False,
+            bn: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+    """smart.py:171-182: (q / ranges - scalars) * std + mean (std after the ==0 rule)."""
+    thr = F32(cfg.main_std_dev_threshold)
+    scal, ranges = _scalars_ranges(hi, lo, thr, F32(cfg.range_normal), F32(cfg.range_outlier))
+    mean, std = F32(mean), F32(std)
+    with np.errstate(all="ignore"):
+        y = (np.asarray(q, dtype=F32) / ranges) - scal
         y = (y * std) + mean
         if bn is not None:  # smart.py:174-179
+            g, b = [np.asarray(t, dtype=F32).reshape((1, -1, 1, 1)) for t in bn]
             y = (y * g) + b
         if all_positive:
             y = np.where(y < F32(0), F32(0), y)
-    return y.astype(F32).reshape(shape), o.reshape(shape)
+    return y.astype(F32)
+
+
+def apply(x: np.ndarray, mean, std, cfg: SmaqConfig, uniforms: Optional[np.ndarray] = None,
+          all_positive: bool = False, bn: Optional[Tuple[np.ndarray, np.ndarray]] = None,
+          dtype: str = "f32"):
+    """smart.py:144-182 given (mean, std). Returns (y, is_outlier). For dtype 'f16' / 'bf16' the
+    z-score is computed in that type (x, mean, std hold values of it) and the rest in float32 —
+    the reference's torch type promotion; the output is float32."""
+    shape = np.shape(x)
+    q, hi, lo, std1 = codes(x, mean, std, cfg, uniforms, bn, dtype)
+    y = dequant(q, hi, lo, mean, std1, cfg, all_positive, bn)
+    return y.reshape(shape), (hi | lo).reshape(shape)
 
 
 def roundtrip(x: np.ndarray, cfg: SmaqConfig, uniforms=None, sample_idx=None,

@@ -401,6 +401,34 @@ static void launch_apply_t(const ApplyArgs& A, int rm, bool vec, bool bn, int tv
 #undef SMQ_APPLY
 }
 
+static int fill_sampled(ApplyArgs& A, const SmqSmaqParams* p, int64_t n) {
+  const int64_t k = p->num_samples < n ? p->num_samples : n;
+  if (k < 1 || k > SMQ_MAX_SAMPLES) {
+    set_error("sampled stats need 1 <= k <= %d, got %lld", SMQ_MAX_SAMPLES, (long long)k);
+    return SMQ_ERR_INVALID;
+  }
+  for (int j = 0; j < (int)k; ++j) {
+    if (p->sample_idx[j] < 0 || p->sample_idx[j] >= n) {
+      set_error("sample_idx[%d] = %lld out of range [0, %lld)", j, (long long)p->sample_idx[j],
+                (long long)n);
+      return SMQ_ERR_INVALID;
+    }
+    A.sample_idx[j] = p->sample_idx[j];
+  }
+  A.k = (int)k;
+  A.range_coef = range_coef_for(p, k);
+  return SMQ_OK;
+}
+
+static void launch_sample_stats(const ApplyArgs& A, int dtype, hipStream_t st) {
+  if (dtype == SMQ_DTYPE_F32)
+    hipLaunchKernelGGL(smaq_sample_stats_kernel<kF32>, dim3(1), dim3(kWave), 0, st, A);
+  else if (dtype == SMQ_DTYPE_F16)
+    hipLaunchKernelGGL(smaq_sample_stats_kernel<kF16>, dim3(1), dim3(kWave), 0, st, A);
+  else
+    hipLaunchKernelGGL(smaq_sample_stats_kernel<kBF16>, dim3(1), dim3(kWave), 0, st, A);
+}
+
 static int launch_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                         const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
                         size_t ws_bytes, hipStream_t st) {
@@ -445,21 +473,8 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
     return SMQ_ERR_INVALID;
   }
   if (p->stats_source == SMQ_STATS_SAMPLED) {
-    const int64_t k = p->num_samples < n ? p->num_samples : n;
-    if (k < 1 || k > SMQ_MAX_SAMPLES) {
-      set_error("sampled stats need 1 <= k <= %d, got %lld", SMQ_MAX_SAMPLES, (long long)k);
-      return SMQ_ERR_INVALID;
-    }
-    for (int j = 0; j < (int)k; ++j) {
-      if (p->sample_idx[j] < 0 || p->sample_idx[j] >= n) {
-        set_error("sample_idx[%d] = %lld out of range [0, %lld)", j, (long long)p->sample_idx[j],
-                  (long long)n);
-        return SMQ_ERR_INVALID;
-      }
-      A.sample_idx[j] = p->sample_idx[j];
-    }
-    A.k = (int)k;
-    A.range_coef = range_coef_for(p, k);
+    const int rc = fill_sampled(A, p, n);
+    if (rc) return rc;
   }
   const int rm = !p->stochastic_rounding ? kRoundTrunc : (uniforms ? kRoundUniform : kRoundHash);
   const bool vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) && aligned(y, 16) &&
@@ -491,12 +506,7 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
     A.stats = A.ws_stats;
   }
   if (p->stats_source == SMQ_STATS_SAMPLED) {
-    if (dtype == SMQ_DTYPE_F32)
-      hipLaunchKernelGGL(smaq_sample_stats_kernel<kF32>, dim3(1), dim3(kWave), 0, st, A);
-    else if (dtype == SMQ_DTYPE_F16)
-      hipLaunchKernelGGL(smaq_sample_stats_kernel<kF16>, dim3(1), dim3(kWave), 0, st, A);
-    else
-      hipLaunchKernelGGL(smaq_sample_stats_kernel<kBF16>, dim3(1), dim3(kWave), 0, st, A);
+    launch_sample_stats(A, dtype, st);
     A.stats = A.ws_stats;
   }
   const bool bn = A.bn_gamma != nullptr;
@@ -516,6 +526,40 @@ static int check_tensor_args(const void* x, const float* y, int64_t n) {
     return SMQ_ERR_INVALID;
   }
   return SMQ_OK;
+}
+
+// Statistics for a consumer other than the apply kernel (the packed codec): full or sampled
+// statistics of x into the workspace header (smaq_host.h).
+int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
+                  size_t ws_bytes, hipStream_t st) {
+  if (p->stats_source == SMQ_STATS_WORKSPACE) return launch_stats(x, dtype, n, p, ws, ws_bytes, st);
+  if (p->stats_source != SMQ_STATS_SAMPLED) {
+    set_error("this entry point computes its statistics (SMQ_STATS_WORKSPACE or _SAMPLED)");
+    return SMQ_ERR_INVALID;
+  }
+  if (!ws || ws_bytes < SmaqWsLayout::kPartials) {
+    set_error("workspace too small: need >= %zu bytes", (size_t)SmaqWsLayout::kPartials);
+    return SMQ_ERR_WORKSPACE;
+  }
+  ApplyArgs A;
+  memset(&A, 0, sizeof(A));
+  A.x = x;
+  A.n = n;
+  A.ws_stats = (SmqSmaqStats*)ws;
+  A.clamp_lo = p->clamp_lo;
+  A.clamp_hi = p->clamp_hi;
+  A.use_range = p->use_range_std_dev;
+  const int rc = fill_sampled(A, p, n);
+  if (rc) return rc;
+  launch_sample_stats(A, dtype, st);
+  return check_launch("smaq_sample_stats_kernel");
+}
+
+size_t smaq_stats_ws_bytes(int64_t n) { return stats_ws_bytes(n); }
+int smaq_validate(const SmqSmaqParams* p, int dtype) {
+  int rc = validate_params(p);
+  if (!rc) rc = check_dtype(dtype);
+  return rc;
 }
 
 }  // namespace smq

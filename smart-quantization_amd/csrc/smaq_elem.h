@@ -257,13 +257,13 @@ struct BnTerm {
   float gamma, beta;
 };
 
-// One element of smart.py:154-182. Each statement is one rounded fp32 op of the reference.
-// T = input type (z-score rounded to it unless BN already promoted the data to fp32).
-// AP: all_positive; SUB: keep the subnormal-quotient check (quot_check_for); SQ: divide q / range
-// by IEEE division (RangeRecips::safe_q).
-template <int RM, bool BN = false, int T = kF32, bool AP = false, bool SUB = true, bool SQ = false>
-__device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c,
-                                           bool& is_outlier, BnTerm bn = BnTerm{1.0f, 0.0f}) {
+// Template flags: AP all_positive; SUB keep the subnormal-quotient check (quot_check_for); SQ
+// divide q / range by IEEE division (RangeRecips::safe_q).
+
+// smart.py:144-169: the integer-valued code q and the outlier sides of one element.
+template <int RM, bool BN = false, int T = kF32, bool SUB = true>
+__device__ __forceinline__ float smaq_quant(float v, float u, const ElemConsts& c, bool& hi,
+                                            bool& lo, BnTerm bn = BnTerm{1.0f, 0.0f}) {
   constexpr int TZ = BN ? kF32 : T;  // fp32 BN parameters promote the data to fp32
   if (BN) v = (v - bn.beta) / bn.gamma;                 // (data - beta) / gamma
   const float dm = round_in<TZ>(v - c.mean);            // data - mean
@@ -272,12 +272,11 @@ __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c
   // (classf: the unsuffixed builtin takes a double, where a promoted float is never subnormal.)
   if (SUB && __builtin_expect(__builtin_amdgcn_classf(z, 0x90), 0)) z = dm / c.sc;
   z = round_in<TZ>(z);
-  const bool hi = z > c.cthr;                           // is_outlier_higher
-  const bool lo = z < c.cnthr;                          // is_outlier_lower
+  hi = z > c.cthr;                                      // is_outlier_higher
+  lo = z < c.cnthr;                                     // is_outlier_lower
   const bool o = hi | lo;                               // is_outlier
   const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);  // scalars
   const float r = o ? c.r_out : c.r_main;               // ranges
-  const double inv_r = o ? c.inv_r_out : c.inv_r_main;
   const float d = (z + a) * r;
   float q;
   if (RM == kRoundTrunc) {
@@ -289,13 +288,34 @@ __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c
     t = (t < 0.0f) ? 0.0f : t;                          // F.relu
     q = f + __builtin_rintf(t);                         // .round() = half to even
   }
+  return q;
+}
+
+// smart.py:171-182: de-quantise a code q with its outlier sides.
+template <bool BN = false, bool AP = false, bool SQ = false>
+__device__ __forceinline__ float smaq_dequant(float q, bool hi, bool lo, const ElemConsts& c,
+                                              BnTerm bn = BnTerm{1.0f, 0.0f}) {
+  const bool o = hi | lo;
+  const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);  // scalars
+  const float r = o ? c.r_out : c.r_main;               // ranges
+  const double inv_r = o ? c.inv_r_out : c.inv_r_main;
   const float qr = SQ ? q / r : div_by_const(q, inv_r);  // data / ranges
   float out = qr - a;                                   //   - scalars
   out = (out * c.sd) + c.mean;
   if (BN) out = (out * bn.gamma) + bn.beta;             // (data * gamma) + beta
   if (AP) out = (out < 0.0f) ? 0.0f : out;              // clamp_min(0.0)
-  is_outlier = o;
   return out;
+}
+
+// One element of smart.py:154-182 (quant then dequant, every statement one rounded fp32 op of the
+// reference). T = input type (z-score rounded to it unless BN already promoted the data to fp32).
+template <int RM, bool BN = false, int T = kF32, bool AP = false, bool SUB = true, bool SQ = false>
+__device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c,
+                                           bool& is_outlier, BnTerm bn = BnTerm{1.0f, 0.0f}) {
+  bool hi, lo;
+  const float q = smaq_quant<RM, BN, T, SUB>(v, u, c, hi, lo, bn);
+  is_outlier = hi | lo;
+  return smaq_dequant<BN, AP, SQ>(q, hi, lo, c, bn);
 }
 
 }  // namespace smq

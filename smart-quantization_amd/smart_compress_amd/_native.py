@@ -76,6 +76,34 @@ class SmqSmaqStats(ctypes.Structure):
     ]
 
 
+class SmqPackedHeader(ctypes.Structure):
+    _fields_ = [
+        ("magic", ctypes.c_uint32),
+        ("version", ctypes.c_uint32),
+        ("n", ctypes.c_int64),
+        ("block_elems", ctypes.c_uint32),
+        ("n_blocks", ctypes.c_uint32),
+        ("num_bits_main", ctypes.c_int32),
+        ("num_bits_outlier", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("thr", ctypes.c_float),
+        ("range_main", ctypes.c_float),
+        ("range_outlier", ctypes.c_float),
+        ("mean", ctypes.c_float),
+        ("std_dev", ctypes.c_float),
+        ("inv_range_main", ctypes.c_double),
+        ("inv_range_outlier", ctypes.c_double),
+        ("data_words", ctypes.c_uint64),
+        ("total_bytes", ctypes.c_uint64),
+        ("error", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 9),
+    ]
+
+
+SMQ_PACK_MAGIC = 0x50514D53
+SMQ_PACK_BLOCK = 4096
+
+
 class SmqTensorDesc(ctypes.Structure):
     _fields_ = [
         ("x", ctypes.c_void_p),
@@ -155,6 +183,11 @@ SIGNATURES = {
         [_P, _P, _I64, _I32, _P, _U64, _U64, _P, _P, _SZ, _P],
     ),
     "smq_rng_u32": (ctypes.c_uint32, [_U64, _U64]),
+    "smq_smaq_pack_bound": (_SZ, [_I64, _I32, _I32]),
+    "smq_smaq_pack_workspace_bytes": (_SZ, [_I64]),
+    "smq_smaq_compress": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams),
+                                         _P, _SZ, _P, _SZ, _P]),
+    "smq_smaq_decompress": (_I32, [_P, _P, _I64, _P]),
 }
 
 _lib = None

@@ -1,0 +1,122 @@
+"""Packed SmaQ: the codes of smart.py stored for real.
+
+The reference's ``SmartFP`` (smart.py:110-190) only *simulates* SmaQ: it quantises and immediately
+de-quantises in fp32, and reports the size the codes would take (smart.py:184-188). The paper's
+memory saving (README.md:25-28: ``[outlier flag][sign][N-2 magnitude bits]``, 6 bits per main
+element and 8 per outlier by default) needs the codes to be kept. ``SmartFPPacked`` keeps them in
+the container of include/smq.h ("Packed SmaQ container"):
+
+* ``compress(x)`` -> ``SmaqPacked``: device bytes (header, block directory, bit-packed planes,
+  escape list for codes outside the budget), built by ``smq_smaq_compress`` (statistics + one
+  packing launch);
+* ``decompress(p)`` -> fp32 tensor, bit-identical to what ``SmartFP`` returns for the same input,
+  flags and random stream (``smq_smaq_decompress``, one launch);
+* ``__call__`` = decompress(compress(x)), a drop-in SmaQ codec whose ``new_size`` log is the real
+  stream size.
+
+Same flags as ``SmartFP`` (it is a subclass); not supported: the BatchNorm variant and
+``main_std_dev_threshold <= 0`` (outlier sides must be exclusive). ``compress`` reads the stream
+size back from the device (one host synchronisation) to return a right-sized buffer.
+"""
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from ..util.globals import profile
+from .smart import SmartFP
+
+__all__ = ["SmaqPacked", "SmartFPPacked"]
+
+_HDR_BYTES = ctypes.sizeof(N.SmqPackedHeader)
+_TOTAL_OFF = N.SmqPackedHeader.total_bytes.offset
+_ERROR_OFF = N.SmqPackedHeader.error.offset
+
+
+class SmaqPacked:
+    """A packed SmaQ tensor: ``data`` (uint8, on the device) plus the original shape.
+    ``raw``: a tensor below ``min_size``, kept as its original fp32 bytes (smart.py:123-128)."""
+
+    def __init__(self, data: torch.Tensor, shape: torch.Size, n: int, raw: bool = False):
+        self.data = data
+        self.shape = torch.Size(shape)
+        self.n = int(n)
+        self.raw = raw
+
+    @property
+    def nbytes(self) -> int:
+        return int(self.data.numel())
+
+    @property
+    def bits_per_element(self) -> float:
+        return 8.0 * self.nbytes / max(1, self.n)
+
+    def compression_ratio(self, orig_bits: int = 32) -> float:
+        return orig_bits * self.n / (8.0 * self.nbytes)
+
+    def header(self) -> dict:
+        """The stream header as a dict (reads 128 bytes from the device)."""
+        if self.raw:
+            return {"raw": True, "n": self.n}
+        raw = bytes(self.data[:_HDR_BYTES].cpu().numpy())
+        h = N.SmqPackedHeader.from_buffer_copy(raw)
+        return {k: getattr(h, k) for k, _ in N.SmqPackedHeader._fields_ if k != "reserved"}
+
+
+class SmartFPPacked(SmartFP):
+    def compress(self, data: torch.Tensor, all_positive: bool = False,
+                 batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SmaqPacked:
+        hp = self.hparams
+        numel = data.numel()
+        if numel < hp.min_size:  # smart.py:123-128: kept as is
+            raw = data.detach().to(torch.float32).contiguous().reshape(-1).view(torch.uint8)
+            return SmaqPacked(raw.clone(), data.shape, numel, raw=True)
+        if batch_norm_stats is not None and hp.use_batch_norm:
+            raise NotImplementedError("SmartFPPacked: the BatchNorm variant is not supported")
+        if not hp.main_std_dev_threshold > 0:
+            raise NotImplementedError("SmartFPPacked: needs main_std_dev_threshold > 0")
+        N.require_device(data, "SmartFPPacked")
+        code = N.DTYPE_CODES.get(data.dtype)
+        if code is None:
+            raise NotImplementedError(
+                f"SmartFPPacked: dtype {data.dtype} is not supported (float32/float16/bfloat16)")
+        if data.dtype == torch.float16 and hp.precision != 16:
+            raise RuntimeError("value cannot be converted to type c10::Half without overflow")
+        x = data.contiguous()
+        lib = N.lib()
+        p = self._params(numel, all_positive, x.dtype)
+        bound = lib.smq_smaq_pack_bound(numel, hp.num_bits_main, hp.num_bits_outlier)
+        scratch = N.workspace("smaq_pack_out", x.device, bound)
+        ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(numel))
+        N.check(lib.smq_smaq_compress(x.data_ptr(), code, numel, p, scratch.data_ptr(),
+                                      scratch.numel(), ws.data_ptr(), ws.numel(),
+                                      N.stream_ptr(x.device)), "smq_smaq_compress")
+        tail = scratch[_TOTAL_OFF:_ERROR_OFF + 4].cpu().numpy()  # host sync: the stream size
+        total = int(tail[:8].view(np.uint64)[0])
+        if int(tail[_ERROR_OFF - _TOTAL_OFF:].view(np.uint32)[0]) != 0:
+            raise RuntimeError("smq_smaq_compress: block scan gave up (stream marked broken)")
+        return SmaqPacked(scratch[:total].clone(), data.shape, numel)
+
+    def decompress(self, packed: SmaqPacked) -> torch.Tensor:
+        if packed.raw:
+            return packed.data.view(torch.float32).reshape(packed.shape).clone()
+        N.require_device(packed.data, "SmartFPPacked.decompress")
+        y = torch.empty(packed.shape, dtype=torch.float32, device=packed.data.device)
+        N.check(N.lib().smq_smaq_decompress(packed.data.data_ptr(), y.data_ptr(), packed.n,
+                                            N.stream_ptr(y.device)), "smq_smaq_decompress")
+        return y
+
+    def __call__(self, data: torch.Tensor, tag: str = None, all_positive=False,
+                 batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, **_):
+        with profile("smaq"):
+            numel = data.numel()
+            if numel < self.hparams.min_size:
+                self.log_ratio(tag, numel * 32, 32, 32)  # smart.py:125
+                return data
+            packed = self.compress(data, all_positive, batch_norm_stats)
+            y = self.decompress(packed)
+            self.log_size(tag, numel * 32, packed.nbytes * 8)
+            return y

@@ -44,9 +44,12 @@ def test_struct_layouts_match_header():
 #include <stddef.h>
 #include "smq.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(SmqSmaqParams), sizeof(SmqSmaqStats),
-         sizeof(SmqTensorDesc), sizeof(SmqS2fp8Stats), offsetof(SmqSmaqParams, seed),
-         offsetof(SmqSmaqParams, bn_gamma), offsetof(SmqSmaqParams, sample_idx));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(SmqSmaqParams),
+         sizeof(SmqSmaqStats), sizeof(SmqTensorDesc), sizeof(SmqS2fp8Stats),
+         offsetof(SmqSmaqParams, seed), offsetof(SmqSmaqParams, bn_gamma),
+         offsetof(SmqSmaqParams, sample_idx), offsetof(SmqSmaqStats, inv_std_clamped),
+         offsetof(SmqSmaqStats, quot_check), sizeof(SmqPackedHeader),
+         offsetof(SmqPackedHeader, inv_range_main), offsetof(SmqPackedHeader, error));
   return 0;
 }
 """
@@ -59,8 +62,13 @@ int main(void) {
     want = [ctypes.sizeof(N.SmqSmaqParams), ctypes.sizeof(N.SmqSmaqStats),
             ctypes.sizeof(N.SmqTensorDesc), ctypes.sizeof(N.SmqS2fp8Stats),
             N.SmqSmaqParams.seed.offset, N.SmqSmaqParams.bn_gamma.offset,
-            N.SmqSmaqParams.sample_idx.offset]
+            N.SmqSmaqParams.sample_idx.offset, N.SmqSmaqStats.inv_std_clamped.offset,
+            N.SmqSmaqStats.quot_check.offset, ctypes.sizeof(N.SmqPackedHeader),
+            N.SmqPackedHeader.inv_range_main.offset, N.SmqPackedHeader.error.offset]
     assert got == want
+    from oracle import smaq_packed as P  # the oracle's header struct matches the C layout
+
+    assert P.HEADER_BYTES == got[9] and P._HDR.size == got[9]
 
 
 def test_host_rng_equals_oracle():

@@ -1,0 +1,202 @@
+"""Packed SmaQ container on the GPU (smq_smaq_compress / smq_smaq_decompress, SmartFPPacked).
+
+* The device stream equals the oracle's byte for byte (oracle/smaq_packed.py fed the device
+  statistics and the same counter RNG): header, directory, every block image, escapes.
+* decompress(compress(x)) equals SmartFP(x) bit for bit for the same flags and random stream,
+  and equals the oracle's unpack of the same stream.
+* Large tensors (16k+ blocks, the decoupled look-back under load): the round-trip identity, the
+  directory (monotone, consistent with each block's size) and sampled block images vs the oracle.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import n_diff_f32, same_f32, smaq_hparams
+
+pytestmark = pytest.mark.gpu
+
+
+def _codecs(seed=21, offset=3, **over):
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+
+    hp = smaq_hparams(**over)
+    a, b = SmartFPPacked(hp), SmartFP(hp)
+    a.rng.seed, a.rng.offset = seed, offset
+    b.rng.seed, b.rng.offset = seed, offset
+    return hp, a, b
+
+
+def _stats_of(packed):
+    h = packed.header()
+    return h["mean"], h["std_dev"]
+
+
+def _oracle_stream(x_np, packed, hp, seed, offset, all_positive=False, dtype="f32"):
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from oracle import smaq_packed as P
+
+    h = packed.header()
+    cfg = osmaq.SmaqConfig(num_bits_main=hp.num_bits_main, num_bits_outlier=hp.num_bits_outlier,
+                           main_std_dev_threshold=hp.main_std_dev_threshold,
+                           outlier_std_dev_threshold=hp.outlier_std_dev_threshold,
+                           stochastic_rounding=hp.stochastic_rounding, precision=hp.precision)
+    u = orng.uniforms(seed, offset, x_np.size) if hp.stochastic_rounding else None
+    # header.std_dev is after the ==0 rule; the codes only depend on it through std_clamped
+    return P.pack(x_np, h["mean"], h["std_dev"], cfg, u, all_positive, dtype), cfg, u
+
+
+def _heavy(n, seed):
+    rs = np.random.default_rng(seed)
+    x = (rs.standard_t(2.0, n) * 1.3 + 0.1).astype(np.float32)
+    x[rs.random(n) < 0.001] = np.nan
+    x[rs.random(n) < 0.001] = np.inf
+    x[rs.random(n) < 0.001] = -np.inf
+    return x
+
+
+@pytest.mark.parametrize("n", [8, 1000, 4095, 4096, 4097, 1 << 16, 1000003])
+@pytest.mark.parametrize("sr", [True, False])
+def test_stream_bytes_and_roundtrip(n, sr):
+    hp, pk, ref = _codecs(stochastic_rounding=sr)
+    gen = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(n, generator=gen, device="cuda") * 2.0 + 0.5
+    packed = pk.compress(x)
+    y = pk.decompress(packed)
+    y_ref = ref(x)
+    torch.cuda.synchronize()
+    assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
+    stream, _, _ = _oracle_stream(x.cpu().numpy(), packed, hp, 21, 3)
+    got = packed.data.cpu().numpy()
+    assert got.size == stream.size, (got.size, stream.size)
+    assert np.array_equal(got, stream), int(np.argmax(got != stream))
+    assert packed.bits_per_element < 8.0 or n < (1 << 16)  # per-block header amortised
+
+
+@pytest.mark.parametrize("bits", [(6, 8), (4, 6), (2, 3), (5, 7), (9, 12)])
+def test_escapes_bits_and_all_positive(bits):
+    from oracle import smaq_packed as P
+
+    hp, pk, ref = _codecs(num_bits_main=bits[0], num_bits_outlier=bits[1])
+    x_np = _heavy(50_000, bits[0])
+    x = torch.from_numpy(x_np).cuda()
+    for all_pos in (False, True):
+        packed = pk.compress(x, all_positive=all_pos)
+        y = pk.decompress(packed)
+        y_ref = ref(x, all_positive=all_pos)
+        torch.cuda.synchronize()
+        assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), n_diff_f32(
+            y.cpu().numpy(), y_ref.cpu().numpy())
+        got = packed.data.cpu().numpy()
+        assert P.header(got)["n"] == x_np.size
+        assert same_f32(P.unpack(got), y.cpu().numpy())  # the oracle decodes the device stream
+
+
+@pytest.mark.parametrize("dt", ["f16", "bf16"])
+def test_half_inputs(dt):
+    tdt = {"f16": torch.float16, "bf16": torch.bfloat16}[dt]
+    hp, pk, ref = _codecs(precision=16)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    x = (torch.randn(70_001, generator=gen, device="cuda") * 3).to(tdt)
+    packed = pk.compress(x)
+    y = pk.decompress(packed)
+    y_ref = ref(x)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.float32 and same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
+    stream, _, _ = _oracle_stream(x.float().cpu().numpy(), packed, hp, 21, 3, dtype=dt)
+    assert np.array_equal(packed.data.cpu().numpy(), stream)
+
+
+def test_sampled_and_range_stats():
+    for over in (dict(use_sample_stats=True), dict(use_range_std_dev=True),
+                 dict(use_sample_stats=True, use_range_std_dev=True)):
+        hp, pk, ref = _codecs(**over)
+        x = torch.randn(123_457, device="cuda") * 0.3
+        packed = pk.compress(x)
+        y = pk.decompress(packed)
+        y_ref = ref(x)
+        torch.cuda.synchronize()
+        assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), over
+
+
+def test_codec_call_logs_real_size_and_passthrough():
+    from argparse import Namespace
+
+    hp, pk, ref = _codecs(measure_compression_ratio=True)
+    logged = []
+    pk.log = lambda k, v, **kw: logged.append((k, v))
+    x = torch.randn(1 << 18, device="cuda")
+    y = pk(x, tag="forward_autograd")
+    ref.log = lambda k, v, **kw: None
+    y_ref = ref(x, tag="forward_autograd")  # (the reference's log_size needs a tag, base.py:101)
+    assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
+    d = dict(logged)
+    assert d["orig_size"] == 32 * x.numel()
+    assert 6.0 * x.numel() < d["new_size"] < 8.0 * x.numel()  # real stream bits
+    small = torch.randn(5, device="cuda")
+    assert pk(small, tag="forward_autograd") is small  # smart.py:123-128
+    p = pk.compress(small)
+    assert p.raw and torch.equal(pk.decompress(p), small)
+
+
+def test_rejections():
+    from smart_compress_amd.compress import SmartFPPacked
+
+    with pytest.raises(NotImplementedError):
+        SmartFPPacked(smaq_hparams(main_std_dev_threshold=-1.0)).compress(
+            torch.randn(100, device="cuda"))
+    with pytest.raises(NotImplementedError):
+        SmartFPPacked(smaq_hparams(use_batch_norm=True)).compress(
+            torch.randn(2, 3, 4, 4, device="cuda"),
+            batch_norm_stats=(torch.ones(3, device="cuda"), torch.zeros(3, device="cuda")))
+
+
+def test_large_multiblock_lookback():
+    """64M elements = 16384 blocks compacted by the look-back scan: round trip == SmartFP, the
+    directory matches each block's size, sampled block images equal the oracle's."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from oracle import smaq_packed as P
+
+    n = 1 << 26
+    hp, pk, ref = _codecs(seed=77, offset=1000)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(n, generator=gen, device="cuda")
+    x[::997] *= 40.0  # escapes sprinkled over every block
+    packed = pk.compress(x)
+    y = pk.decompress(packed)
+    y_ref = ref(x)
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(torch.int32), y_ref.view(torch.int32))
+    del y, y_ref
+    raw = packed.data.cpu().numpy()
+    h = P.header(raw)
+    nb = h["n_blocks"]
+    assert nb == n // 4096 and h["error"] == 0 and h["total_bytes"] == raw.size
+    dirs = raw[128: 128 + 8 * nb].view(np.uint64).astype(np.int64)
+    data = raw[128 + 8 * nb:].view(np.uint32)
+    w0 = data[dirs]
+    n_out, n_esc = (w0 & 0xFFFF).astype(np.int64), (w0 >> 16).astype(np.int64)
+    size = 129 + (5 * (4096 - n_out) + 31) // 32 + (7 * n_out + 31) // 32 + 2 * n_esc
+    assert dirs[0] == 0 and np.array_equal(np.diff(dirs), size[:-1])
+    assert dirs[-1] + size[-1] == h["data_words"]
+    assert n_esc.sum() > nb  # escapes present throughout
+    cfg = osmaq.SmaqConfig()
+    xh = x.cpu().numpy()
+    for b in (0, 1, 2, nb // 2, nb - 2, nb - 1):
+        s = slice(b * 4096, (b + 1) * 4096)
+        u = orng.uniforms(77, 1000 + b * 4096, 4096)
+        img = P.pack_block(xh[s], h["mean"], h["std_dev"], cfg, u)
+        got = data[dirs[b]: dirs[b] + img.size]
+        assert np.array_equal(got, img), b
+
+
+def test_compress_is_repeatable():
+    """Same seed/offset twice (workspace counters reset by the last block): identical streams."""
+    hp, pk, _ = _codecs(seed=4, offset=0)
+    x = torch.randn(3 * 4096 + 77, device="cuda")
+    a = pk.compress(x).data.clone()
+    pk.rng.offset = 0
+    b = pk.compress(x).data
+    assert torch.equal(a, b)
