@@ -357,13 +357,75 @@ def run_multi(args, world, rank, device):
                        "elements_per_gpu": n}}
 
 
+def run_packed(args, world, rank, device):
+    """Packed SmaQ container on the 256M config: compress (statistics + packing
+    launch) then decompress, both through the C-ABI into preallocated buffers (no host sync)."""
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.packed import SmartFPPacked
+
+    n = args.elements or (1 << 28)
+    hp = smaq_hparams()
+    codec = SmartFPPacked(hp)
+    codec.rng.seed = 2000 + rank
+    gen = torch.Generator(device=device).manual_seed(rank)
+    xs = [torch.randn(n, generator=gen, device=device) for _ in range(2)]
+    lib = N.lib()
+    bound = lib.smq_smaq_pack_bound(n, hp.num_bits_main, hp.num_bits_outlier)
+    packed = torch.empty(bound, dtype=torch.uint8, device=device)
+    ws = torch.zeros(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8, device=device)
+    y = torch.empty(n, dtype=torch.float32, device=device)
+    st = torch.cuda.current_stream(device).cuda_stream
+    trace = EventTrace()
+    it = [0]
+
+    def step():
+        x = xs[it[0] & 1]
+        it[0] += 1
+        p = codec._params(n, False)
+        trace.begin("compress")
+        N.check(lib.smq_smaq_compress(x.data_ptr(), N.SMQ_DTYPE_F32, n, p, packed.data_ptr(),
+                                      bound, ws.data_ptr(), ws.numel(), st), "compress")
+        trace.end("compress")
+        trace.begin("unpack")
+        N.check(lib.smq_smaq_decompress(packed.data_ptr(), y.data_ptr(), n, st), "decompress")
+        trace.end("unpack")
+
+    trace.enabled = False
+    prewarm(step, device)
+    for _ in range(args.warmup):
+        step()
+    trace.enabled = True
+    elapsed = time_steps(step, args.steps, 0, world, device)
+    hdr = N.SmqPackedHeader.from_buffer_copy(bytes(packed[:128].cpu().numpy()))
+    sbytes = int(hdr.total_bytes)
+    # algorithmic bytes: stats read 4n, pack read 4n + stream write, unpack stream read + 4n write
+    alg = 12.0 * n + 2.0 * sbytes
+    total = sum_over_ranks(alg * args.steps, world, device)
+    c_ms, u_ms = trace.mean_ms("compress"), trace.mean_ms("unpack")
+    u_gbps = (sbytes + 4.0 * n) / (u_ms * 1e-3) / 1e9
+    return {"metric": "Packed SmaQ 6/8 compress+decompress GB/s, 256M fp32",
+            "value": round(total / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "smaq_6_8_packed_256M_fp32", "elements_per_gpu": n,
+                       "stream_bytes": sbytes, "bits_per_element": round(8.0 * sbytes / n, 3),
+                       "compression_ratio_vs_fp32": round(32.0 * n / (8.0 * sbytes), 3)},
+            "compress_ms": round(c_ms, 4), "decompress_ms": round(u_ms, 4),
+            "roofline": {"bound": "hbm", "kernel": "smaq_unpack_kernel",
+                         "achieved": round(u_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(u_gbps / HBM_PEAK_GBPS, 4),
+                         "alg_bytes_per_launch": sbytes + 4 * n, "avg_launch_ms": round(u_ms, 5),
+                         "traffic": None}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="smaq",
-                    choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi"])
+                    choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi", "packed"])
     ap.add_argument("--elements", type=int, default=0, help="override elements (smaq configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 22)
@@ -373,7 +435,7 @@ def main():
     world, rank, local = dist_setup()
     device = torch.device("cuda", local)
     runner = {"smaq": run_smaq, "smaq_sampled": run_smaq, "fp8": run_fp8, "s2fp8": run_s2fp8,
-              "multi": run_multi}[args.config]
+              "multi": run_multi, "packed": run_packed}[args.config]
     res = runner(args, world, rank, device)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and args.config.startswith("smaq"):

@@ -17,6 +17,7 @@
 //   then smaq_dequant — the same arithmetic as the simulated round trip, so the result is
 //   bit-identical to smq_smaq_apply for the same statistics and random stream.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "smaq_elem.h"
@@ -44,7 +45,8 @@ struct PackArgs {
   uint64_t* dir;
   uint32_t* data;
   const SmqSmaqStats* stats;
-  uint64_t* status;
+  uint64_t* status;          // [n_blocks] block aggregates
+  uint64_t* gstatus;         // [n_groups] group aggregates / inclusive prefixes
   uint32_t* counter;
   float thr, r_main, r_out;
   double inv_r_main, inv_r_out;
@@ -53,6 +55,8 @@ struct PackArgs {
   int wm, wo, bm, bo;
   uint32_t n_blocks;
   uint32_t flags;
+  int place_atomic;          // measurement knob (SMQ_PACK_PLACE=atomic): see smq_smaq_compress
+  unsigned long long* cursor;
 };
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
@@ -80,99 +84,133 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
-// OR a width-bit code into an LSB-first bit stream in LDS (codes may straddle two words).
-__device__ __forceinline__ void put_bits(uint32_t* base, uint32_t pos, uint32_t code, int width) {
-  const uint32_t w = pos >> 5, sh = pos & 31u;
-  atomicOr(base + w, code << sh);
-  if (sh + (uint32_t)width > 32u) atomicOr(base + w + 1, code >> (32u - sh));
-}
-
-__device__ __forceinline__ uint32_t get_bits(const uint32_t* base, uint32_t pos, int width) {
-  const uint32_t w = pos >> 5, sh = pos & 31u;
-  uint32_t v = base[w] >> sh;
-  if (sh + (uint32_t)width > 32u) v |= base[w + 1] << (32u - sh);
-  return v & ((1u << width) - 1u);
-}
-
-// Plane code of one element (smq.h rules); esc = the code does not fit the budget.
+// Plane code of one element (smq.h rules), branch-free; esc = the code does not fit the budget.
 __device__ __forceinline__ uint32_t classify(float q, bool hi, bool lo, int wm, int wo, bool& esc) {
-  if (!(hi | lo)) {
-    const float lim = (float)(1 << (wm - 1));
-    const bool ok = (q >= -lim) && (q <= lim - 1.0f);  // false for NaN
-    esc = !ok;
-    return ok ? ((uint32_t)(int32_t)q & ((1u << wm) - 1u)) : 0u;
-  }
-  const float mag_max = (float)((1 << (wo - 1)) - 1);
-  const uint32_t side = lo ? (1u << (wo - 1)) : 0u;
-  const bool ok = hi ? (q >= 0.0f && q <= mag_max) : (q <= 0.0f && -q <= mag_max);
+  const bool o = hi | lo;
+  const float lim = (float)(1 << (wm - 1));
+  const bool ok_m = (q >= -lim) && (q <= lim - 1.0f);          // false for NaN
+  const float mag = hi ? q : -q;                                // hi: q >= 0, lo: q <= 0
+  const bool ok_o = (mag >= 0.0f) && (mag <= (float)((1 << (wo - 1)) - 1));
+  const uint32_t code_m = (uint32_t)(int32_t)q & ((1u << wm) - 1u);
+  const uint32_t code_o = (lo ? (1u << (wo - 1)) : 0u) | (ok_o ? (uint32_t)(int32_t)mag : 0u);
+  const bool ok = o ? ok_o : ok_m;
   esc = !ok;
-  return ok ? (side | (uint32_t)(int32_t)(hi ? q : -q)) : side;
+  return o ? code_o : (ok_m ? code_m : 0u);
 }
 
-// Decoupled look-back (wave 0). Returns the exclusive prefix (words) of block b.
+// One 32-bit word of a plane of width-bit codes (LSB-first), assembled from the rank-ordered code
+// array: codes r with bits [r * width, (r + 1) * width) overlapping [32 j, 32 j + 32).
+template <int WIDTH>
+__device__ __forceinline__ uint32_t plane_word(const uint32_t* codes, uint32_t count, int width_rt,
+                                               uint32_t j) {
+  const int width = WIDTH > 0 ? WIDTH : width_rt;  // compile-time widths: no integer division
+  const uint32_t b0 = 32u * j;
+  const uint32_t r0 = b0 / (uint32_t)width;
+  uint32_t r1 = (b0 + 31u) / (uint32_t)width;
+  if (r1 >= count) r1 = count - 1u;
+  uint32_t word = 0u;
+  for (uint32_t r = r0; r <= r1; ++r) {
+    const int sh = (int)(r * (uint32_t)width) - (int)b0;  // >= -(width - 1)
+    const uint32_t cd = codes[r];
+    word |= sh >= 0 ? (cd << sh) : (cd >> -sh);
+  }
+  return word;
+}
+
+constexpr int kGroup = 64;  // blocks per look-back group (one status word per lane)
+
+// Poll until lanes [0, count) hold a published status (flag != 0); returns this lane's value.
+__device__ __forceinline__ uint64_t wait_all(const PackArgs& A, const uint64_t* st, int count,
+                                             uint32_t& spins) {
+  const int lane = threadIdx.x & (kWave - 1);
+  for (;;) {
+    const uint64_t v = lane < count ? ld_sc1_u64(st + lane) : kAgg;
+    if (!__ballot((v >> 62) == 0ull)) return v;
+    if (++spins >= kSpinLimit) {
+      if (lane == 0) atomicOr(&A.hdr->error, 1u);  // give up: the stream is marked broken
+      return v;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// Two-level decoupled look-back (wave 0). Returns the exclusive prefix (words) of block b.
+// Level 1: the blocks of b's group of 64 publish their sizes (one window read). Level 2: the
+// group's last block publishes the group aggregate, walks back over group words (64 groups =
+// 4096 blocks per read) to the nearest inclusive prefix and publishes its own; every block of the
+// group walks the same group words. A single-level scan advances one 64-block window per memory
+// round trip (~1 us): 65536 blocks took 1.1 ms; two levels move 4096 blocks per round trip.
 __device__ uint64_t look_back(const PackArgs& A, uint32_t b, uint64_t size) {
   const int lane = threadIdx.x & (kWave - 1);
-  if (b == 0) {
-    if (lane == 0) st_sc1_u64(A.status, kIncl | size);
-    return 0;
-  }
-  if (lane == 0) st_sc1_u64(A.status + b, kAgg | size);
-  uint64_t acc = 0;
-  int64_t j = (int64_t)b - 1;
+  const uint32_t g = b / kGroup, i = b % kGroup;
+  const bool last = (i == kGroup - 1) || (b == A.n_blocks - 1);
   uint32_t spins = 0;
-  for (;;) {
-    const int64_t idx = j - lane;
-    const uint64_t v = idx >= 0 ? ld_sc1_u64(A.status + idx) : kIncl;  // before block 0: 0
-    const uint32_t flag = (uint32_t)(v >> 62);
-    const uint64_t incl = __ballot(flag == 2u);
-    const uint64_t invalid = __ballot(flag == 0u);
-    const int first = incl ? __builtin_ctzll(incl) : 64;
-    const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
-    if (invalid & need) {
-      if (++spins < kSpinLimit) {
+  if (lane == 0) st_sc1_u64(A.status + b, kAgg | size);
+  // level 1: sizes of the group's earlier blocks
+  uint64_t lp = 0;
+  if (i > 0) {
+    const uint64_t v = wait_all(A, A.status + (uint64_t)g * kGroup, (int)i, spins);
+    lp = wave_sum_u64(lane < (int)i ? (v & kValMask) : 0ull);
+  }
+  if (last && lane == 0) st_sc1_u64(A.gstatus + g, (g == 0 ? kIncl : kAgg) | (lp + size));
+  // level 2: prefix of the groups before g
+  uint64_t gp = 0;
+  if (g > 0) {
+    int64_t j = (int64_t)g - 1;
+    for (;;) {
+      const int64_t idx = j - lane;
+      const uint64_t v = idx >= 0 ? ld_sc1_u64(A.gstatus + idx) : kIncl;  // before group 0: 0
+      const uint32_t flag = (uint32_t)(v >> 62);
+      const uint64_t incl = __ballot(flag == 2u);
+      const uint64_t invalid = __ballot(flag == 0u);
+      const int first = incl ? __builtin_ctzll(incl) : 64;
+      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
+      if ((invalid & need) && ++spins < kSpinLimit) {
         __builtin_amdgcn_s_sleep(2);
         continue;
       }
-      if (lane == 0) atomicOr(&A.hdr->error, 1u);  // give up: the stream is marked broken
+      if (spins >= kSpinLimit && lane == 0) atomicOr(&A.hdr->error, 1u);
+      gp += wave_sum_u64(lane <= first ? (v & kValMask) : 0ull);
+      if (first < 64 || spins >= kSpinLimit) break;
+      j -= 64;
     }
-    acc += wave_sum_u64(lane <= first ? (v & kValMask) : 0ull);
-    if (first < 64 || spins >= kSpinLimit) break;
-    j -= 64;
+    if (last && lane == 0) st_sc1_u64(A.gstatus + g, kIncl | (gp + lp + size));
   }
-  if (lane == 0) st_sc1_u64(A.status + b, kIncl | (acc + size));
-  return acc;
+  return gp + lp;
 }
 
-template <int RM, int TIN, bool SUB, bool VEC>
+// FULL: the block holds SMQ_PACK_BLOCK elements (every block but a ragged last one).
+template <int RM, int TIN, bool SUB, bool VEC, bool FULL, int WM, int WO>
 __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c, uint32_t b,
-                                          uint32_t* stage) {
+                                          uint32_t* codes) {
+  const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
+  __shared__ uint32_t maskw[kMaskWords];
   __shared__ uint32_t seg_cnt[2][16];
   __shared__ uint32_t seg_pre[2][17];
   __shared__ uint64_t s_prefix;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int64_t e0 = (int64_t)b * kPB;
-  const int n_el = (int)(A.n - e0 < kPB ? A.n - e0 : kPB);
+  const int n_el = FULL ? kPB : (int)(A.n - e0);
 
-  // 1. codes of this lane's 16 elements: local index el = 1024 k + 4 tid + c
+  // 1. codes of this lane's 16 elements: local index el = 1024 k + 4 tid + i
   uint32_t code[16];
-  float qv[16];
-  uint32_t om[4] = {0, 0, 0, 0}, xm[4] = {0, 0, 0, 0};
+  uint32_t om[4], xm[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int el = 1024 * k + 4 * tid;
     float v[4] = {0.f, 0.f, 0.f, 0.f}, u[4] = {0.f, 0.f, 0.f, 0.f};
-    const bool full = el + 3 < n_el;
-    if (VEC && full) {
+    const bool full4 = FULL || el + 3 < n_el;
+    if (VEC && full4) {
       const float4 t = load4<TIN>(A.x, (e0 + el) >> 2);
       v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (el + i < n_el) v[i] = load1<TIN>(A.x, e0 + el + i);
+        if (FULL || el + i < n_el) v[i] = load1<TIN>(A.x, e0 + el + i);
     }
     if (RM == kRoundHash) {
       const uint64_t ctr = A.offset + (uint64_t)(e0 + el);
-      if (full) {
+      if (full4) {
         rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
       } else {
 #pragma unroll
@@ -180,35 +218,37 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
           if (el + i < n_el) u[i] = rng_hu(A.key, ctr + i);
       }
     }
+    om[k] = 0u;
+    xm[k] = 0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      bool hi = false, lo = false, esc = false;
-      float q = 0.f;
-      uint32_t cd = 0;
-      if (el + i < n_el) {
-        q = smaq_quant<RM, false, TIN, SUB>(v[i], u[i], c, hi, lo);
-        cd = classify(q, hi, lo, A.wm, A.wo, esc);
-      }
-      code[4 * k + i] = cd;
-      qv[4 * k + i] = q;
-      om[k] |= (uint32_t)(hi | lo) << i;
-      xm[k] |= (uint32_t)esc << i;
+      bool hi, lo, esc;
+      const float q = smaq_quant<RM, false, TIN, SUB>(v[i], u[i], c, hi, lo);
+      code[4 * k + i] = classify(q, hi, lo, wm, wo, esc);
+      const bool valid = FULL || el + i < n_el;
+      om[k] |= (uint32_t)((hi | lo) && valid) << i;
+      xm[k] |= (uint32_t)(esc && valid) << i;
     }
   }
 
-  // 2. ranks: per 256-element segment s = 4 k + wave, exclusive lane prefixes by ballots
+  // 2. ranks: per 256-element segment s = 4 k + wave, exclusive lane prefixes by ballots;
+  //    mask words from nibbles (8 lanes per word) by three xor-shuffles
   uint32_t pre_o[4], pre_x[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     uint32_t to, tx;
     pre_o[k] = wave_prefix_small<3>(__popc(om[k]), to);
     pre_x[k] = wave_prefix_small<3>(__popc(xm[k]), tx);
+    uint32_t mw = om[k] << (4 * (lane & 7));
+    mw |= __shfl_xor(mw, 1, kWave);
+    mw |= __shfl_xor(mw, 2, kWave);
+    mw |= __shfl_xor(mw, 4, kWave);
+    if ((lane & 7) == 0) maskw[(1024 * k + 4 * tid) >> 5] = mw;
     if (lane == 0) {
       seg_cnt[0][4 * k + w] = to;
       seg_cnt[1][4 * k + w] = tx;
     }
   }
-  for (int i = tid; i < kStageWords; i += kBlock) stage[i] = 0u;
   __syncthreads();
   if (tid < 2) {
     uint32_t run = 0;
@@ -221,54 +261,60 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   __syncthreads();
   const uint32_t n_out = seg_pre[0][16], n_esc = seg_pre[1][16];
   const uint32_t n_main = (uint32_t)n_el - n_out;
-  const uint32_t main_words = (A.wm * n_main + 31u) / 32u;
-  const uint32_t out_words = (A.wo * n_out + 31u) / 32u;
+  const uint32_t main_words = (wm * n_main + 31u) / 32u;
+  const uint32_t out_words = (wo * n_out + 31u) / 32u;
   const uint32_t img_words = kHdrWords + main_words + out_words;
   const uint64_t size = (uint64_t)img_words + 2ull * n_esc;
 
-  // 3. wave 0 starts the look-back while the other waves build the block image
-  if (w == 0) {
+  // 3. wave 0 starts the look-back; every lane files its codes in rank order (mains, then
+  //    outliers) — plain LDS stores, no atomics
+  if (A.place_atomic) {
+    if (tid == 0) s_prefix = atomicAdd(A.cursor, (unsigned long long)size);
+  } else if (w == 0) {
     const uint64_t p = look_back(A, b, size);
     if (lane == 0) s_prefix = p;
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int el0 = 1024 * k + 4 * tid;
-    if (om[k]) atomicOr(stage + 1 + (el0 >> 5), om[k] << (el0 & 31));
+    const uint32_t el0 = 1024u * k + 4u * tid;
     const uint32_t base_o = seg_pre[0][4 * k + w] + pre_o[k];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int el = el0 + i;
-      if (el >= n_el) continue;
+      if (!FULL && (int)el0 + i >= n_el) continue;
       const uint32_t r_out = base_o + __popc(om[k] & ((1u << i) - 1u));
-      if ((om[k] >> i) & 1u)
-        put_bits(stage + kHdrWords + main_words, r_out * A.wo, code[4 * k + i], A.wo);
-      else
-        put_bits(stage + kHdrWords, ((uint32_t)el - r_out) * A.wm, code[4 * k + i], A.wm);
+      const bool o = (om[k] >> i) & 1u;
+      codes[o ? n_main + r_out : el0 + i - r_out] = code[4 * k + i];
     }
   }
   __syncthreads();
 
-  // 4. the block image, its escapes and its directory entry at the prefix
+  // 4. the block image at its prefix: w[0] + mask, plane words assembled from the code array,
+  //    escapes (their q recomputed: rare), directory entry
   const uint64_t P = s_prefix;
   uint32_t* out = A.data + P;
-  for (uint32_t i = tid; i < img_words; i += kBlock)
-    out[i] = i == 0 ? (n_out | (n_esc << 16)) : stage[i];
+  if (tid < kHdrWords) out[tid] = tid == 0 ? (n_out | (n_esc << 16)) : maskw[tid - 1];
+  for (uint32_t j = tid; j < main_words; j += kBlock)
+    out[kHdrWords + j] = plane_word<WM>(codes, n_main, wm, j);
+  for (uint32_t j = tid; j < out_words; j += kBlock)
+    out[kHdrWords + main_words + j] = plane_word<WO>(codes + n_main, n_out, wo, j);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (!xm[k]) continue;
     const uint32_t base_x = seg_pre[1][4 * k + w] + pre_x[k];
-#pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (!((xm[k] >> i) & 1u)) continue;
+      const uint32_t el = 1024u * k + 4u * tid + i;
+      const float uf = RM == kRoundHash ? rng_hu(A.key, A.offset + (uint64_t)(e0 + el)) : 0.f;
+      bool hi, lo;
+      const float q = smaq_quant<RM, false, TIN, SUB>(load1<TIN>(A.x, e0 + el), uf, c, hi, lo);
       const uint32_t r = base_x + __popc(xm[k] & ((1u << i) - 1u));
-      out[img_words + 2 * r] = (uint32_t)(1024 * k + 4 * tid + i);
-      out[img_words + 2 * r + 1] = __float_as_uint(qv[4 * k + i]);
+      out[img_words + 2 * r] = el;
+      out[img_words + 2 * r + 1] = __float_as_uint(q);
     }
   }
   if (tid == 0) {
     A.dir[b] = P;
-    if (b == A.n_blocks - 1) {
+    if (!A.place_atomic && b == A.n_blocks - 1) {
       A.hdr->data_words = P + size;
       A.hdr->total_bytes = sizeof(SmqPackedHeader) + 8ull * A.n_blocks + 4ull * (P + size);
     }
@@ -295,7 +341,7 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
 
 template <int RM, int TIN, bool VEC>
 __global__ __launch_bounds__(kBlock) void smaq_pack_kernel(PackArgs A) {
-  __shared__ uint32_t stage[kStageWords];
+  __shared__ uint32_t codes[kPB];
   __shared__ uint32_t s_b;
   if (threadIdx.x == 0) {
     const uint32_t id = atomicAdd(A.counter, 1u);  // block ids in start order
@@ -307,10 +353,28 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_kernel(PackArgs A) {
   ElemConsts c;
   const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);  // z is compared in its type
   init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
-  if (A.stats->quot_check)
-    pack_body<RM, TIN, true, VEC>(A, c, b, stage);
-  else
-    pack_body<RM, TIN, false, VEC>(A, c, b, stage);
+  const bool full = (int64_t)(b + 1) * kPB <= A.n;
+  const bool w57 = A.wm == 5 && A.wo == 7;  // the default 6/8-bit budget, widths compiled in
+#define SMQ_PACK_BODY(SUBV, FULLV)                                          \
+  do {                                                                      \
+    if (w57) pack_body<RM, TIN, SUBV, VEC, FULLV, 5, 7>(A, c, b, codes);   \
+    else pack_body<RM, TIN, SUBV, VEC, FULLV, 0, 0>(A, c, b, codes);       \
+  } while (0)
+  if (A.stats->quot_check) {
+    if (full) SMQ_PACK_BODY(true, true); else SMQ_PACK_BODY(true, false);
+  } else {
+    if (full) SMQ_PACK_BODY(false, true); else SMQ_PACK_BODY(false, false);
+  }
+#undef SMQ_PACK_BODY
+}
+
+// SMQ_PACK_PLACE=atomic: the stream size is the cursor (written after the packing launch).
+__global__ void smaq_pack_total_kernel(SmqPackedHeader* h, const unsigned long long* cursor,
+                                       uint32_t n_blocks) {
+  if (threadIdx.x == 0) {
+    h->data_words = *cursor;
+    h->total_bytes = sizeof(SmqPackedHeader) + 8ull * n_blocks + 4ull * *cursor;
+  }
 }
 
 struct UnpackArgs {
@@ -331,14 +395,14 @@ __device__ __forceinline__ float find_escape(const uint32_t* esc, uint32_t n_esc
   return __uint_as_float(esc[2 * lo + 1]);
 }
 
-template <bool AP, bool SQ>
+template <bool AP, bool SQ, bool FULL>
 __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
                                             int wm, int wo, uint32_t* stage) {
   __shared__ uint32_t pc[kMaskWords];
   __shared__ uint32_t esc_mask[kMaskWords];
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int64_t e0 = (int64_t)b * kPB;
-  const int n_el = (int)(A.n - e0 < kPB ? A.n - e0 : kPB);
+  const int n_el = FULL ? kPB : (int)(A.n - e0);
   const uint32_t* blk = A.data + A.dir[b];
   const uint32_t w0 = blk[0];
   const uint32_t n_out = w0 & 0xffffu, n_esc = w0 >> 16;
@@ -361,13 +425,14 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
     atomicOr(esc_mask + (el >> 5), 1u << (el & 31));
   }
   __syncthreads();
-  const uint32_t* mplane = stage + kHdrWords;
-  const uint32_t* oplane = stage + kHdrWords + main_words;
-  const uint32_t side_bit = 1u << (wo - 1);
+  // the planes as ONE bit stream: mains at bit 0, outliers at bit 32 * main_words
+  const uint32_t* bits = stage + kHdrWords;
+  const uint32_t obase = 32u * main_words;
+  const uint32_t mmask = (1u << wm) - 1u, omask = (1u << wo) - 1u, side_bit = 1u << (wo - 1);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int el0 = 1024 * k + 4 * tid;
-    if (el0 >= n_el) break;
+    if (!FULL && el0 >= n_el) break;
     const uint32_t mw = stage[1 + (el0 >> 5)], em = esc_mask[el0 >> 5], base = pc[el0 >> 5];
     float o[4];
 #pragma unroll
@@ -375,28 +440,26 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
       const uint32_t el = (uint32_t)(el0 + i);
       const uint32_t sh = el & 31u;
       const uint32_t r_out = base + __popc(mw & ((1u << sh) - 1u));
-      bool hi = false, lo = false;
-      float q;
-      if ((mw >> sh) & 1u) {
-        const uint32_t cd = get_bits(oplane, r_out * wo, wo);
-        const int mag = (int)(cd & (side_bit - 1u));
-        lo = (cd & side_bit) != 0u;
-        hi = !lo;
-        q = (float)(lo ? -mag : mag);
-      } else {
-        const uint32_t cd = get_bits(mplane, (el - r_out) * wm, wm);
-        q = (float)(((int32_t)(cd << (32 - wm))) >> (32 - wm));  // sign-extend wm bits
-      }
+      const bool is_o = (mw >> sh) & 1u;
+      const uint32_t pos = is_o ? obase + r_out * wo : (el - r_out) * wm;
+      const uint32_t wi = pos >> 5;
+      const uint32_t v = __builtin_amdgcn_alignbit(bits[wi + 1], bits[wi], pos & 31u);
+      const uint32_t cm = v & mmask, co = v & omask;
+      const float qm = (float)(((int32_t)(cm << (32 - wm))) >> (32 - wm));  // sign-extend
+      const int mag = (int)(co & (side_bit - 1u));
+      const bool lo = is_o && (co & side_bit);
+      const bool hi = is_o && !(co & side_bit);
+      float q = is_o ? (float)(lo ? -mag : mag) : qm;
       if (__builtin_expect((em >> sh) & 1u, 0)) q = find_escape(esc, n_esc, el);
       o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
     }
     float* y = A.y + e0 + el0;
-    if (A.vec && el0 + 3 < n_el) {
+    if (A.vec && (FULL || el0 + 3 < n_el)) {
       store_nt(reinterpret_cast<float4*>(y), make_float4(o[0], o[1], o[2], o[3]));
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (el0 + i < n_el) y[i] = o[i];
+        if (FULL || el0 + i < n_el) y[i] = o[i];
     }
   }
 }
@@ -420,13 +483,18 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   c.inv_r_out = h->inv_range_outlier;
   const uint32_t f = h->flags;
   const uint32_t b = blockIdx.x;
+  const bool full = (int64_t)(b + 1) * kPB <= A.n;
+#define SMQ_UNPACK(APV, SQV)                                          \
+  do {                                                                \
+    if (full) unpack_body<APV, SQV, true>(A, c, b, wm, wo, stage);    \
+    else unpack_body<APV, SQV, false>(A, c, b, wm, wo, stage);        \
+  } while (0)
   if (f & 2u) {
-    if (f & 1u) unpack_body<true, true>(A, c, b, wm, wo, stage);
-    else unpack_body<false, true>(A, c, b, wm, wo, stage);
+    if (f & 1u) SMQ_UNPACK(true, true); else SMQ_UNPACK(false, true);
   } else {
-    if (f & 1u) unpack_body<true, false>(A, c, b, wm, wo, stage);
-    else unpack_body<false, false>(A, c, b, wm, wo, stage);
+    if (f & 1u) SMQ_UNPACK(true, false); else SMQ_UNPACK(false, false);
   }
+#undef SMQ_UNPACK
 }
 
 inline bool aligned_to(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
@@ -454,7 +522,8 @@ size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier) {
 
 size_t smq_smaq_pack_workspace_bytes(int64_t n) {
   const size_t nb = (size_t)n_blocks_of(n < 1 ? 1 : n);
-  return pack_ws_status_offset(n) + 64 + 8 * nb;
+  const size_t ng = (nb + kGroup - 1) / kGroup;
+  return pack_ws_status_offset(n) + 64 + 8 * nb + 8 * ng + 64;
 }
 
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* packed,
@@ -514,6 +583,16 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
   A.stats = (const SmqSmaqStats*)ws;
   A.counter = (uint32_t*)(wb + so);
   A.status = (uint64_t*)(wb + so + 64);
+  A.gstatus = A.status + nb;
+  const size_t ng = ((size_t)nb + kGroup - 1) / kGroup;
+  A.cursor = (unsigned long long*)(A.gstatus + ng);
+  // measurement knob: place blocks by one atomicAdd (valid, decodable stream; block ORDER then
+  // depends on timing, so the bytes are not reproducible) instead of the ordered look-back
+  static const int place_env = [] {
+    const char* e = getenv("SMQ_PACK_PLACE");
+    return (e && !strcmp(e, "atomic")) ? 1 : 0;
+  }();
+  A.place_atomic = place_env;
   A.thr = p->main_std_dev_threshold;
   A.r_main = p->range_main;
   A.r_out = p->range_outlier;
@@ -528,7 +607,7 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
   A.wo = A.bo - 1;
   A.n_blocks = (uint32_t)nb;
   A.flags = (p->all_positive ? 1u : 0u) | (R.safe_q ? 2u : 0u);
-  if (hipMemsetAsync(A.status, 0, 8 * (size_t)nb, st) != hipSuccess ||
+  if (hipMemsetAsync(A.status, 0, 8 * ((size_t)nb + ng) + 64, st) != hipSuccess ||
       hipMemsetAsync(A.hdr, 0, sizeof(SmqPackedHeader), st) != hipSuccess) {
     set_error("compress: hipMemsetAsync failed");
     return SMQ_ERR_LAUNCH;
@@ -553,6 +632,9 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
   else SMQ_PACK_T(kBF16);
 #undef SMQ_PACK_T
 #undef SMQ_PACK
+  if (A.place_atomic)
+    hipLaunchKernelGGL(smaq_pack_total_kernel, dim3(1), dim3(kWave), 0, st, A.hdr, A.cursor,
+                       A.n_blocks);
   return check_launch("smaq_pack_kernel");
 }
 

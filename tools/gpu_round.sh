@@ -29,13 +29,15 @@ for s in "$@"; do
           step bench_w50 300 python bench.py --steps 100 --warmup 50 --no-cpu-baseline ;;
     dist2) SMQ_BENCH_SHARE_DEVICE=1 SMQ_BENCH_BACKEND=gloo step bench_dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --elements 67108864 ;;
     tiles) for v in 1 2; do SMQ_APPLY_TILE=$v step kbench_tile$v 300 python tools/kbench.py --quick; done ;;
-    profile) step profile 1500 bash tools/profile_round.sh r01 smaq ;;
-    profile_*) c=${s#profile_}; step profile_$c 1500 bash tools/profile_round.sh r01_$c $c 50 10 ;;
+    profile) step profile 1500 bash tools/profile_round.sh ${ROUND:-r03} smaq ;;
+    profile_*) c=${s#profile_}; step profile_$c 1500 bash tools/profile_round.sh ${ROUND:-r03}_$c $c 50 10 ;;
+    bench_packed) step bench_packed 600 python bench.py --config packed --steps 20 --warmup 3 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 --cpu-budget 8 ;;
     bench_all) step bench_fp8 300 python bench.py --config fp8 --steps 50 --warmup 5 &&
                step bench_s2fp8 300 python bench.py --config s2fp8 --steps 200 --warmup 20 &&
                step bench_multi 300 python bench.py --config multi --steps 100 --warmup 10 &&
-               step bench_sampled 300 python bench.py --config smaq_sampled --steps 20 --warmup 3 --no-cpu-baseline ;;
+               step bench_sampled 300 python bench.py --config smaq_sampled --steps 20 --warmup 3 --no-cpu-baseline &&
+               step bench_packed 600 python bench.py --config packed --steps 20 --warmup 3 ;;
   esac
 done
