@@ -235,15 +235,16 @@ uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
  * block  = SMQ_PACK_BLOCK elements (the last one may be shorter); its words:
  *   w[0]                 n_out (bits 0-15) | n_esc (bits 16-31)
  *   w[1 .. 128]          outlier mask: bit (e % 32) of word e / 32 = element e is an outlier
- *   main plane           one (num_bits_main - 1)-bit two's-complement code q per main element,
- *                        in element order, LSB-first across words (k-th main code at bits
- *                        [k * wm, (k + 1) * wm)); ceil(wm * n_main / 32) words
- *   outlier plane        one (num_bits_outlier - 1)-bit code per outlier: top bit = side
- *                        (1: z < -T, the code is -q; 0: z > T, the code is q), the rest = |q|;
- *                        ceil(wo * n_out / 32) words
+ *   codes                one code per element in ELEMENT order, LSB-first across words:
+ *                        element e's code starts at bit wm * e + (wo - wm) * (outliers before e),
+ *                        wm = num_bits_main - 1, wo = num_bits_outlier - 1;
+ *                        main: wm-bit two's-complement q; outlier: top bit = side (1: z < -T,
+ *                        the code is -q; 0: z > T, the code is q), the rest = |q|;
+ *                        ceil((wm * n + (wo - wm) * n_out) / 32) words
  *   escapes              n_esc x {element index in the block, q as float32 bits}, in element
  *                        order: codes outside the budget (|q| too large, a negative q for z > T,
- *                        a positive q for z < -T, inf / NaN); their plane slots hold 0
+ *                        a positive q for z < -T, inf / NaN); their codes hold 0 (main) or
+ *                        the side bit alone (outlier)
  * Decoding: q -> (q / range) - scalars, * std + mean (smart.py:171-182), bit-identical to
  * smq_smaq_apply for the same statistics, rounding mode and random stream. Needs T_m > 0.
  * ------------------------------------------------------------------------------------------- */

@@ -73,8 +73,25 @@ def _unpack_bits(words: np.ndarray, width: int, n: int) -> np.ndarray:
     return (bits << np.arange(width, dtype=np.uint64)).sum(axis=1)
 
 
+def _code_stream(cb, ob, wm: int, wo: int) -> np.ndarray:
+    """Codes concatenated LSB-first in ELEMENT order: element e's code (wm bits if main, wo bits if
+    outlier) starts at bit wm * e + (wo - wm) * (outliers before e)."""
+    widths = np.where(ob, wo, wm).astype(np.int64)
+    n = cb.size
+    total = int(widths.sum())
+    words = (total + 31) // 32
+    if n == 0:
+        return np.zeros(0, np.uint32)
+    wmax = max(wm, wo)
+    bits = ((cb[:, None] >> np.arange(wmax, dtype=np.uint64)) & 1).astype(np.uint8)
+    keep = np.arange(wmax)[None, :] < widths[:, None]
+    flat = bits[keep]  # row-major: element order, LSB first within each code
+    flat = np.concatenate([flat, np.zeros(words * 32 - flat.size, np.uint8)])
+    return np.packbits(flat.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").ravel().astype(np.uint32)
+
+
 def block_words(cb, ob, eb, qb, wm: int, wo: int) -> np.ndarray:
-    """The uint32 image of one block (w[0], mask, main plane, outlier plane, escapes)."""
+    """The uint32 image of one block (w[0], mask, code stream, escapes)."""
     n_out, n_esc = int(ob.sum()), int(eb.sum())
     mask = np.zeros(BLOCK, np.uint8)
     mask[: ob.size] = ob
@@ -82,8 +99,8 @@ def block_words(cb, ob, eb, qb, wm: int, wo: int) -> np.ndarray:
     esc_idx = np.nonzero(eb)[0].astype(np.uint32)
     esc_words = np.stack([esc_idx, qb[esc_idx].view(np.uint32)], axis=1).ravel()
     return np.concatenate([np.array([n_out | (n_esc << 16)], np.uint32),
-                           mask_words.astype(np.uint32), _pack_bits(cb[~ob], wm),
-                           _pack_bits(cb[ob], wo), esc_words.astype(np.uint32)])
+                           mask_words.astype(np.uint32), _code_stream(cb, ob, wm, wo),
+                           esc_words.astype(np.uint32)])
 
 
 def pack_block(xb, mean, std, cfg: osmaq.SmaqConfig, uniforms=None, dtype: str = "f32"):
@@ -152,24 +169,26 @@ def unpack(stream: np.ndarray) -> np.ndarray:
         mask_bits = np.unpackbits(data[base + 1: base + 129].astype(">u4").view(np.uint8)
                                   .reshape(-1, 4), axis=1).reshape(-1, 32)[:, ::-1].ravel()
         ob = mask_bits[:m].astype(bool)
-        n_main = m - n_out
         p = base + 129
-        mw = (wm * n_main + 31) // 32
-        ow = (wo * n_out + 31) // 32
-        mc = _unpack_bits(data[p: p + mw], wm, n_main).astype(np.int64)
-        oc = _unpack_bits(data[p + mw: p + mw + ow], wo, n_out).astype(np.int64)
-        qm = np.where(mc >= 2 ** (wm - 1), mc - 2**wm, mc)
-        side = (oc >> (wo - 1)) & 1
-        mag = oc & ((1 << (wo - 1)) - 1)
+        nw = (wm * m + (wo - wm) * n_out + 31) // 32
+        bits = np.unpackbits(data[p: p + nw].astype(">u4").view(np.uint8).reshape(-1, 4),
+                             axis=1).reshape(-1, 32)[:, ::-1].ravel().astype(np.uint64)
+        r_out = np.concatenate([[0], np.cumsum(ob)[:-1]]).astype(np.int64)
+        pos = wm * np.arange(m, dtype=np.int64) + (wo - wm) * r_out
+        widths = np.where(ob, wo, wm)
+        cd = np.zeros(m, np.uint64)
+        for t in range(max(wm, wo)):
+            sel = t < widths
+            cd[sel] |= bits[pos[sel] + t] << np.uint64(t)
+        cd = cd.astype(np.int64)
+        qm = np.where(cd >= 2 ** (wm - 1), cd - 2**wm, cd)
+        side = (cd >> (wo - 1)) & 1
+        mag = cd & ((1 << (wo - 1)) - 1)
         qo = np.where(side == 1, -mag, mag)
-        qb = np.zeros(m, F32)
-        qb[~ob] = qm.astype(F32)
-        qb[ob] = qo.astype(F32)
-        hb = np.zeros(m, bool)
-        lb = np.zeros(m, bool)
-        hb[ob] = side == 0
-        lb[ob] = side == 1
-        e = data[p + mw + ow: p + mw + ow + 2 * n_esc].reshape(-1, 2)
+        qb = np.where(ob, qo, qm).astype(F32)
+        hb = ob & (side == 0)
+        lb = ob & (side == 1)
+        e = data[p + nw: p + nw + 2 * n_esc].reshape(-1, 2)
         qb[e[:, 0].astype(np.int64)] = e[:, 1].view(F32)
         s = slice(b * BLOCK, b * BLOCK + m)
         q[s], hi[s], lo[s] = qb, hb, lb

@@ -98,25 +98,6 @@ __device__ __forceinline__ uint32_t classify(float q, bool hi, bool lo, int wm, 
   return o ? code_o : (ok_m ? code_m : 0u);
 }
 
-// One 32-bit word of a plane of width-bit codes (LSB-first), assembled from the rank-ordered code
-// array: codes r with bits [r * width, (r + 1) * width) overlapping [32 j, 32 j + 32).
-template <int WIDTH>
-__device__ __forceinline__ uint32_t plane_word(const uint32_t* codes, uint32_t count, int width_rt,
-                                               uint32_t j) {
-  const int width = WIDTH > 0 ? WIDTH : width_rt;  // compile-time widths: no integer division
-  const uint32_t b0 = 32u * j;
-  const uint32_t r0 = b0 / (uint32_t)width;
-  uint32_t r1 = (b0 + 31u) / (uint32_t)width;
-  if (r1 >= count) r1 = count - 1u;
-  uint32_t word = 0u;
-  for (uint32_t r = r0; r <= r1; ++r) {
-    const int sh = (int)(r * (uint32_t)width) - (int)b0;  // >= -(width - 1)
-    const uint32_t cd = codes[r];
-    word |= sh >= 0 ? (cd << sh) : (cd >> -sh);
-  }
-  return word;
-}
-
 constexpr int kGroup = 64;  // blocks per look-back group (one status word per lane)
 
 // Poll until lanes [0, count) hold a published status (flag != 0); returns this lane's value.
@@ -179,18 +160,28 @@ __device__ uint64_t look_back(const PackArgs& A, uint32_t b, uint64_t size) {
   return gp + lp;
 }
 
+// OR a code chunk (< 2^32) at bit pos of an LDS bit stream (two words; ORing 0 is harmless).
+__device__ __forceinline__ void or_bits(uint32_t* base, uint32_t pos, uint32_t chunk) {
+  const uint64_t v = (uint64_t)chunk << (pos & 31u);
+  atomicOr(base + (pos >> 5), (uint32_t)v);
+  atomicOr(base + (pos >> 5) + 1, (uint32_t)(v >> 32));
+}
+
 // FULL: the block holds SMQ_PACK_BLOCK elements (every block but a ragged last one).
+// WM / WO: code widths compiled in (0: runtime widths). With WO <= 8 a lane's four codes form one
+// chunk of at most 28 bits written by two LDS ORs.
 template <int RM, int TIN, bool SUB, bool VEC, bool FULL, int WM, int WO>
 __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c, uint32_t b,
-                                          uint32_t* codes) {
-  const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
-  __shared__ uint32_t maskw[kMaskWords];
+                                          uint32_t* stage) {
   __shared__ uint32_t seg_cnt[2][16];
   __shared__ uint32_t seg_pre[2][17];
   __shared__ uint64_t s_prefix;
+  constexpr bool kChunk = WO > 0 && WO <= 8;
+  const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
+  uint32_t* codes_lds = stage + kHdrWords;
 
   // 1. codes of this lane's 16 elements: local index el = 1024 k + 4 tid + i
   uint32_t code[16];
@@ -224,14 +215,14 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
     for (int i = 0; i < 4; ++i) {
       bool hi, lo, esc;
       const float q = smaq_quant<RM, false, TIN, SUB>(v[i], u[i], c, hi, lo);
-      code[4 * k + i] = classify(q, hi, lo, wm, wo, esc);
       const bool valid = FULL || el + i < n_el;
+      code[4 * k + i] = valid ? classify(q, hi, lo, wm, wo, esc) : 0u;
       om[k] |= (uint32_t)((hi | lo) && valid) << i;
       xm[k] |= (uint32_t)(esc && valid) << i;
     }
   }
 
-  // 2. ranks: per 256-element segment s = 4 k + wave, exclusive lane prefixes by ballots;
+  // 2. outlier / escape ranks: per 256-element segment s = 4 k + wave, lane prefixes by ballots;
   //    mask words from nibbles (8 lanes per word) by three xor-shuffles
   uint32_t pre_o[4], pre_x[4];
 #pragma unroll
@@ -243,12 +234,14 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
     mw |= __shfl_xor(mw, 1, kWave);
     mw |= __shfl_xor(mw, 2, kWave);
     mw |= __shfl_xor(mw, 4, kWave);
-    if ((lane & 7) == 0) maskw[(1024 * k + 4 * tid) >> 5] = mw;
+    if ((lane & 7) == 0) stage[1 + ((1024 * k + 4 * tid) >> 5)] = mw;
     if (lane == 0) {
       seg_cnt[0][4 * k + w] = to;
       seg_cnt[1][4 * k + w] = tx;
     }
   }
+  const uint32_t code_cap = (uint32_t)(wo * kPB + 31) / 32u + 1u;
+  for (uint32_t i = tid; i < code_cap; i += kBlock) codes_lds[i] = 0u;
   __syncthreads();
   if (tid < 2) {
     uint32_t run = 0;
@@ -260,14 +253,12 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   }
   __syncthreads();
   const uint32_t n_out = seg_pre[0][16], n_esc = seg_pre[1][16];
-  const uint32_t n_main = (uint32_t)n_el - n_out;
-  const uint32_t main_words = (wm * n_main + 31u) / 32u;
-  const uint32_t out_words = (wo * n_out + 31u) / 32u;
-  const uint32_t img_words = kHdrWords + main_words + out_words;
+  const uint32_t code_words = ((uint32_t)wm * (uint32_t)n_el + (uint32_t)(wo - wm) * n_out + 31u) / 32u;
+  const uint32_t img_words = kHdrWords + code_words;
   const uint64_t size = (uint64_t)img_words + 2ull * n_esc;
 
-  // 3. wave 0 starts the look-back; every lane files its codes in rank order (mains, then
-  //    outliers) — plain LDS stores, no atomics
+  // 3. wave 0 starts the look-back; every lane ORs its codes into the LDS code stream at
+  //    pos(el) = wm * el + (wo - wm) * (outliers before el)
   if (A.place_atomic) {
     if (tid == 0) s_prefix = atomicAdd(A.cursor, (unsigned long long)size);
   } else if (w == 0) {
@@ -277,26 +268,33 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t el0 = 1024u * k + 4u * tid;
-    const uint32_t base_o = seg_pre[0][4 * k + w] + pre_o[k];
+    if (!FULL && (int)el0 >= n_el) continue;
+    const uint32_t r0 = seg_pre[0][4 * k + w] + pre_o[k];
+    const uint32_t pos0 = (uint32_t)wm * el0 + (uint32_t)(wo - wm) * r0;
+    if (kChunk) {
+      uint32_t chunk = 0u, off = 0u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (!FULL && (int)el0 + i >= n_el) continue;
-      const uint32_t r_out = base_o + __popc(om[k] & ((1u << i) - 1u));
-      const bool o = (om[k] >> i) & 1u;
-      codes[o ? n_main + r_out : el0 + i - r_out] = code[4 * k + i];
+      for (int i = 0; i < 4; ++i) {
+        chunk |= code[4 * k + i] << off;  // invalid tail elements carry code 0, width wm
+        off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
+      }
+      or_bits(codes_lds, pos0, chunk);
+    } else {
+      uint32_t off = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        or_bits(codes_lds, pos0 + off, code[4 * k + i]);
+        off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
+      }
     }
   }
   __syncthreads();
 
-  // 4. the block image at its prefix: w[0] + mask, plane words assembled from the code array,
-  //    escapes (their q recomputed: rare), directory entry
+  // 4. the block image at its prefix, its escapes (q recomputed: rare) and directory entry
   const uint64_t P = s_prefix;
   uint32_t* out = A.data + P;
-  if (tid < kHdrWords) out[tid] = tid == 0 ? (n_out | (n_esc << 16)) : maskw[tid - 1];
-  for (uint32_t j = tid; j < main_words; j += kBlock)
-    out[kHdrWords + j] = plane_word<WM>(codes, n_main, wm, j);
-  for (uint32_t j = tid; j < out_words; j += kBlock)
-    out[kHdrWords + main_words + j] = plane_word<WO>(codes + n_main, n_out, wo, j);
+  for (uint32_t i = tid; i < img_words; i += kBlock)
+    out[i] = i == 0 ? (n_out | (n_esc << 16)) : stage[i];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (!xm[k]) continue;
@@ -341,7 +339,7 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
 
 template <int RM, int TIN, bool VEC>
 __global__ __launch_bounds__(kBlock) void smaq_pack_kernel(PackArgs A) {
-  __shared__ uint32_t codes[kPB];
+  __shared__ uint32_t stage[kStageWords];
   __shared__ uint32_t s_b;
   if (threadIdx.x == 0) {
     const uint32_t id = atomicAdd(A.counter, 1u);  // block ids in start order
@@ -357,8 +355,8 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_kernel(PackArgs A) {
   const bool w57 = A.wm == 5 && A.wo == 7;  // the default 6/8-bit budget, widths compiled in
 #define SMQ_PACK_BODY(SUBV, FULLV)                                          \
   do {                                                                      \
-    if (w57) pack_body<RM, TIN, SUBV, VEC, FULLV, 5, 7>(A, c, b, codes);   \
-    else pack_body<RM, TIN, SUBV, VEC, FULLV, 0, 0>(A, c, b, codes);       \
+    if (w57) pack_body<RM, TIN, SUBV, VEC, FULLV, 5, 7>(A, c, b, stage);   \
+    else pack_body<RM, TIN, SUBV, VEC, FULLV, 0, 0>(A, c, b, stage);       \
   } while (0)
   if (A.stats->quot_check) {
     if (full) SMQ_PACK_BODY(true, true); else SMQ_PACK_BODY(true, false);
@@ -395,20 +393,33 @@ __device__ __forceinline__ float find_escape(const uint32_t* esc, uint32_t n_esc
   return __uint_as_float(esc[2 * lo + 1]);
 }
 
-template <bool AP, bool SQ, bool FULL>
+// Decode one code (width wm main / wo outlier) to q and the outlier sides.
+__device__ __forceinline__ float decode_code(uint32_t v, bool is_o, int wm, int wo, bool& hi,
+                                             bool& lo) {
+  const uint32_t side_bit = 1u << (wo - 1);
+  const uint32_t cm = v & ((1u << wm) - 1u);
+  const float qm = (float)(((int32_t)(cm << (32 - wm))) >> (32 - wm));  // sign-extend
+  const int mag = (int)(v & (side_bit - 1u));
+  lo = is_o && (v & side_bit);
+  hi = is_o && !(v & side_bit);
+  return is_o ? (float)(lo ? -mag : mag) : qm;
+}
+
+template <bool AP, bool SQ, bool FULL, int WM, int WO>
 __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
-                                            int wm, int wo, uint32_t* stage) {
+                                            int wm_rt, int wo_rt, uint32_t* stage) {
   __shared__ uint32_t pc[kMaskWords];
   __shared__ uint32_t esc_mask[kMaskWords];
+  constexpr bool kWindow = WO > 0 && WO <= 8;  // a lane's 4 codes fit one 32-bit window
+  const int wm = WM > 0 ? WM : wm_rt, wo = WO > 0 ? WO : wo_rt;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
   const uint32_t* blk = A.data + A.dir[b];
   const uint32_t w0 = blk[0];
   const uint32_t n_out = w0 & 0xffffu, n_esc = w0 >> 16;
-  const uint32_t main_words = (wm * ((uint32_t)n_el - n_out) + 31u) / 32u;
-  const uint32_t out_words = (wo * n_out + 31u) / 32u;
-  const uint32_t img_words = kHdrWords + main_words + out_words;
+  const uint32_t code_words = ((uint32_t)wm * (uint32_t)n_el + (uint32_t)(wo - wm) * n_out + 31u) / 32u;
+  const uint32_t img_words = kHdrWords + code_words;
   for (uint32_t i = tid; i < img_words; i += kBlock) stage[i] = blk[i];
   if (tid < kMaskWords) esc_mask[tid] = 0u;
   __syncthreads();
@@ -425,32 +436,35 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
     atomicOr(esc_mask + (el >> 5), 1u << (el & 31));
   }
   __syncthreads();
-  // the planes as ONE bit stream: mains at bit 0, outliers at bit 32 * main_words
   const uint32_t* bits = stage + kHdrWords;
-  const uint32_t obase = 32u * main_words;
-  const uint32_t mmask = (1u << wm) - 1u, omask = (1u << wo) - 1u, side_bit = 1u << (wo - 1);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int el0 = 1024 * k + 4 * tid;
     if (!FULL && el0 >= n_el) break;
-    const uint32_t mw = stage[1 + (el0 >> 5)], em = esc_mask[el0 >> 5], base = pc[el0 >> 5];
+    const uint32_t mw = stage[1 + (el0 >> 5)], em = esc_mask[el0 >> 5];
+    const uint32_t sh0 = (uint32_t)el0 & 31u;
+    const uint32_t r0 = pc[el0 >> 5] + __popc(mw & ((1u << sh0) - 1u));
+    const uint32_t nib = (mw >> sh0) & 15u, enib = (em >> sh0) & 15u;
+    const uint32_t pos0 = (uint32_t)wm * (uint32_t)el0 + (uint32_t)(wo - wm) * r0;
+    uint32_t window = 0u;
+    if (kWindow)
+      window = __builtin_amdgcn_alignbit(bits[(pos0 >> 5) + 1], bits[pos0 >> 5], pos0 & 31u);
     float o[4];
+    uint32_t off = 0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t el = (uint32_t)(el0 + i);
-      const uint32_t sh = el & 31u;
-      const uint32_t r_out = base + __popc(mw & ((1u << sh) - 1u));
-      const bool is_o = (mw >> sh) & 1u;
-      const uint32_t pos = is_o ? obase + r_out * wo : (el - r_out) * wm;
-      const uint32_t wi = pos >> 5;
-      const uint32_t v = __builtin_amdgcn_alignbit(bits[wi + 1], bits[wi], pos & 31u);
-      const uint32_t cm = v & mmask, co = v & omask;
-      const float qm = (float)(((int32_t)(cm << (32 - wm))) >> (32 - wm));  // sign-extend
-      const int mag = (int)(co & (side_bit - 1u));
-      const bool lo = is_o && (co & side_bit);
-      const bool hi = is_o && !(co & side_bit);
-      float q = is_o ? (float)(lo ? -mag : mag) : qm;
-      if (__builtin_expect((em >> sh) & 1u, 0)) q = find_escape(esc, n_esc, el);
+      const bool is_o = (nib >> i) & 1u;
+      uint32_t v;
+      if (kWindow) {
+        v = window >> off;
+      } else {
+        const uint32_t pos = pos0 + off;
+        v = __builtin_amdgcn_alignbit(bits[(pos >> 5) + 1], bits[pos >> 5], pos & 31u);
+      }
+      off += is_o ? (uint32_t)wo : (uint32_t)wm;
+      bool hi, lo;
+      float q = decode_code(v, is_o, wm, wo, hi, lo);
+      if (__builtin_expect((enib >> i) & 1u, 0)) q = find_escape(esc, n_esc, (uint32_t)(el0 + i));
       o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
     }
     float* y = A.y + e0 + el0;
@@ -484,10 +498,16 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   const uint32_t f = h->flags;
   const uint32_t b = blockIdx.x;
   const bool full = (int64_t)(b + 1) * kPB <= A.n;
-#define SMQ_UNPACK(APV, SQV)                                          \
-  do {                                                                \
-    if (full) unpack_body<APV, SQV, true>(A, c, b, wm, wo, stage);    \
-    else unpack_body<APV, SQV, false>(A, c, b, wm, wo, stage);        \
+  const bool w57 = wm == 5 && wo == 7;
+#define SMQ_UNPACK_W(APV, SQV, FULLV)                                                 \
+  do {                                                                                \
+    if (w57) unpack_body<APV, SQV, FULLV, 5, 7>(A, c, b, wm, wo, stage);             \
+    else unpack_body<APV, SQV, FULLV, 0, 0>(A, c, b, wm, wo, stage);                 \
+  } while (0)
+#define SMQ_UNPACK(APV, SQV)                                  \
+  do {                                                        \
+    if (full) SMQ_UNPACK_W(APV, SQV, true);                   \
+    else SMQ_UNPACK_W(APV, SQV, false);                       \
   } while (0)
   if (f & 2u) {
     if (f & 1u) SMQ_UNPACK(true, true); else SMQ_UNPACK(false, true);
@@ -495,6 +515,7 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
     if (f & 1u) SMQ_UNPACK(true, false); else SMQ_UNPACK(false, false);
   }
 #undef SMQ_UNPACK
+#undef SMQ_UNPACK_W
 }
 
 inline bool aligned_to(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }

@@ -13,6 +13,9 @@ from argparse import ArgumentParser
 import torch
 
 from ... import _native as N
+from .layers import (ACTIVATION_LAYERS, CONV_LAYERS, DEFAULT_LAYER_TYPES, DICT_LAYERS,  # noqa: F401
+                     DROPOUT_LAYERS, LAYERS_TYPES, LINEAR_LAYERS, LOSS_LAYERS, NORM_LAYERS,
+                     PAD_LAYERS, POOL_LAYERS, SEQUENTIAL_LAYERS, is_valid_layer_type)
 
 TORCH_FLOAT_MAX = torch.tensor(torch.finfo(torch.float32).max, dtype=torch.float32)
 TORCH_FLOAT_EPS = torch.tensor(torch.finfo(torch.float32).eps, dtype=torch.float32)

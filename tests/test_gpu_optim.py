@@ -8,7 +8,7 @@ import pytest
 import torch
 import torch.nn as nn
 
-from helpers import smaq_hparams
+from helpers import n_diff_f32, same_f32, smaq_hparams
 
 pytestmark = pytest.mark.gpu
 
@@ -130,3 +130,64 @@ def test_autograd_compressor_path():
     assert abs(out.item() - ref.item()) / ref.item() < 0.05
     cos = torch.nn.functional.cosine_similarity(x.grad.flatten(), gref.flatten(), dim=0).item()
     assert cos > 0.95
+
+
+def _cnn():
+    def block(cin, cout):
+        return nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1, bias=False), nn.BatchNorm2d(cout),
+                             nn.ReLU())
+
+    return nn.Sequential(block(3, 16), block(16, 16), nn.MaxPool2d(2), block(16, 32),
+                         block(32, 32), nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 10))
+
+
+def test_register_autograd_module_every_call_bitexact():
+    """autograd.py:50-77 at model scale: a CNN's forward activations and backward grad-maps all go
+    through SmartFP (BN variant on); every recorded call equals the oracle bit for bit (device
+    statistics, counter RNG); the packed codec gives the identical training step."""
+    from argparse import Namespace
+
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import register_autograd_module
+
+    flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=True)
+    hp = smaq_hparams(use_batch_norm=True)
+
+    def run(cls, record):
+        torch.manual_seed(3)
+        net = _cnn().cuda()
+        codec = cls(hp)
+        codec.rng.seed, codec.rng.offset = 99, 0
+        calls = []
+
+        def compress(x, tag=None, **kw):
+            seed, off = codec.rng.seed, codec.rng.offset
+            y = codec(x, tag=tag, **kw)
+            if record and y is not x:
+                ws = next(v for k, v in N._ws.items() if k[0] == "smaq")
+                calls.append((x.detach().clone(), y.detach().clone(), seed, off,
+                              SmartFP.read_stats(ws), kw.get("batch_norm_stats")))
+            return y
+
+        register_autograd_module(net, compress, flags)
+        x = torch.randn(32, 3, 32, 32, device="cuda", requires_grad=True)
+        loss = torch.nn.functional.cross_entropy(net(x), torch.arange(32, device="cuda") % 10)
+        loss.backward()
+        return loss.detach(), x.grad.detach().clone(), calls
+
+    loss, grad, calls = run(SmartFP, True)
+    assert torch.isfinite(loss) and len(calls) >= 20
+    for xin, y, seed, off, st, bn in calls:
+        xn = xin.cpu().numpy()
+        u = orng.uniforms(seed, off, xn.size).reshape(xn.shape)
+        bn_np = None if bn is None else (bn[0].cpu().numpy(), bn[1].cpu().numpy())
+        y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], osmaq.SmaqConfig(), u, bn=bn_np)
+        assert same_f32(y.cpu().numpy(), y_or), (xin.shape, n_diff_f32(y.cpu().numpy(), y_or))
+    hp.use_batch_norm = False  # the packed container has no BN variant
+    flags.use_batch_norm = False
+    l1, g1, _ = run(SmartFP, False)
+    l2, g2, _ = run(SmartFPPacked, False)
+    assert torch.equal(l1, l2) and torch.equal(g1.view(torch.int32), g2.view(torch.int32))

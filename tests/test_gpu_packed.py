@@ -178,7 +178,7 @@ def test_large_multiblock_lookback():
     data = raw[128 + 8 * nb:].view(np.uint32)
     w0 = data[dirs]
     n_out, n_esc = (w0 & 0xFFFF).astype(np.int64), (w0 >> 16).astype(np.int64)
-    size = 129 + (5 * (4096 - n_out) + 31) // 32 + (7 * n_out + 31) // 32 + 2 * n_esc
+    size = 129 + (5 * 4096 + 2 * n_out + 31) // 32 + 2 * n_esc
     assert dirs[0] == 0 and np.array_equal(np.diff(dirs), size[:-1])
     assert dirs[-1] + size[-1] == h["data_words"]
     assert n_esc.sum() > nb  # escapes present throughout

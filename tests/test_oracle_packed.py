@@ -56,14 +56,18 @@ def test_packed_escapes_and_sizes(n, bits):
         assert same_f32(P.unpack(st), y_ref)
 
 
-def test_bit_planes_roundtrip():
+def test_code_stream_layout():
+    """Codes in element order, LSB-first, width wm (main) or wo (outlier): element e at bit
+    wm * e + (wo - wm) * (outliers before e)."""
     from oracle import smaq_packed as P
 
+    cb = np.array([1, 0x45, 2, 3], np.uint64)
+    ob = np.array([False, True, False, False])
+    w = P._code_stream(cb, ob, 5, 7)
+    assert w.size == 1 and w[0] == (1 | (0x45 << 5) | (2 << 12) | (3 << 17))
     rs = np.random.default_rng(0)
-    for w in (1, 5, 7, 13, 24):
-        c = rs.integers(0, 2**w, 1000, dtype=np.uint64)
-        words = P._pack_bits(c, w)
-        assert words.size == (w * 1000 + 31) // 32
-        assert np.array_equal(P._unpack_bits(words, w, 1000), c)
-    # LSB-first: code k at bits [k*w, (k+1)*w)
-    assert P._pack_bits(np.array([1, 2, 3], np.uint64), 5)[0] == (1 | (2 << 5) | (3 << 10))
+    for wm, wo in ((5, 7), (1, 2), (13, 24)):
+        ob = rs.random(1000) < 0.3
+        cb = np.where(ob, rs.integers(0, 2**wo, 1000), rs.integers(0, 2**wm, 1000)).astype(np.uint64)
+        words = P._code_stream(cb, ob, wm, wo)
+        assert words.size == (wm * 1000 + (wo - wm) * int(ob.sum()) + 31) // 32
