@@ -19,13 +19,21 @@
 
 namespace smq {
 
-constexpr int64_t kDefaultChunk = 8192;  // elements per workgroup (SMQ_MULTI_CHUNK, multiple of 4096)
+// Elements per workgroup, separately for the two launches (env SMQ_MULTI_CHUNK / _STATS_CHUNK,
+// multiples of 4096). Measured on the ResNet-34 set (42.5M elements, 148 tensors): the statistics
+// launch wants few, long chunks (each chunk's partial hand-off is a store-drain + atomic round
+// trip: 8K chunks 62 us, 32K chunks 34 us), the apply launch wants many short ones (8K 60 us,
+// 32K 80 us).
+constexpr int64_t kDefaultChunk = 8192;
+constexpr int64_t kDefaultStatsChunk = 32768;
 
 struct MultiHeader {
   int32_t count;
-  int32_t n_chunks;
+  int32_t n_chunks;       // apply chunks
   int64_t chunk;
-  int64_t reserved[2];
+  int32_t n_stat_chunks;  // statistics chunks (their records follow the apply chunk records)
+  int32_t reserved0;
+  int64_t stat_chunk;
 };
 
 // Everything one workgroup needs, in ONE 64-B record (uniform per workgroup -> two s_load_dwordx8):
@@ -48,7 +56,8 @@ static_assert(sizeof(ChunkDesc) == 64, "chunk desc");
 struct MultiArgs {
   const MultiHeader* hdr;
   const SmqTensorDesc* descs;
-  const ChunkDesc* chunks;
+  const ChunkDesc* chunks;       // apply chunks
+  const ChunkDesc* stat_chunks;  // statistics chunks
   SmqSmaqStats* stats;       // [count]
   uint32_t* counters;        // [count]
   StatPartial* partials;     // [n_chunks]
@@ -63,7 +72,7 @@ struct MultiArgs {
 
 __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   __shared__ uint32_t slot;
-  const ChunkDesc ch = A.chunks[blockIdx.x];
+  const ChunkDesc ch = A.stat_chunks[blockIdx.x];
   const float* __restrict__ x = ch.x;
   const int64_t n = ch.n;
   const float k0 = x[0], k1 = x[n >> 1], k2 = x[n - 1];
@@ -130,14 +139,16 @@ __device__ __forceinline__ float elem_ap(float v, float u, const ElemConsts& c, 
 }
 
 // One chunk. SUB: subnormal-quotient check (per tensor, quot_check_for); SQ: RangeRecips::safe_q.
+// pre: the first step's data, loaded by the caller before the tensor's statistics arrive.
 template <bool SR, bool SUB, bool SQ>
 __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, const ChunkDesc& ch,
-                                                          const ElemConsts& c, bool all_pos) {
+                                                          const ElemConsts& c, bool all_pos,
+                                                          bool vec, const float4 (&pre)[4]) {
   const float* __restrict__ x = ch.x;
   float* y = ch.y;  // may alias x
   unsigned long long n_out = 0;
   constexpr int RM = SR ? kRoundHash : kRoundTrunc;
-  if ((((uintptr_t)x | (uintptr_t)y) & 15u) == 0) {
+  if (vec) {
     const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
     float4* y4 = reinterpret_cast<float4*>(y);
     const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;
@@ -146,7 +157,8 @@ __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, co
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t j = t0 + threadIdx.x + u * kBlock;
-      if (j < e4) v[u] = x4[j];
+      if (t0 == b4) v[u] = pre[u];
+      else if (j < e4) v[u] = x4[j];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -187,12 +199,25 @@ template <bool SR, bool SQ>
 __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
   __shared__ unsigned long long sh_cnt[kBlock / kWave];
   const ChunkDesc ch = A.chunks[blockIdx.x];
+  // the first 16 KiB of the chunk is requested before the statistics (they do not depend on them)
+  const bool vec = (((uintptr_t)ch.x | (uintptr_t)ch.y) & 15u) == 0;
+  float4 pre[4];
+  if (vec) {
+    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(ch.x);
+    const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = b4 + threadIdx.x + u * kBlock;
+      pre[u] = j < e4 ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
   const SmqSmaqStats* st = &A.stats[ch.tensor];
   ElemConsts c;
   init_consts(c, st, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, A.thr);
   const bool all_pos = ch.all_positive != 0;
-  const unsigned long long n_out = st->quot_check ? multi_chunk<SR, true, SQ>(A, ch, c, all_pos)
-                                                  : multi_chunk<SR, false, SQ>(A, ch, c, all_pos);
+  const unsigned long long n_out =
+      st->quot_check ? multi_chunk<SR, true, SQ>(A, ch, c, all_pos, vec, pre)
+                     : multi_chunk<SR, false, SQ>(A, ch, c, all_pos, vec, pre);
   if (A.count_outliers) {
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
     const double t = wave_sum((double)n_out);
@@ -214,25 +239,58 @@ static int64_t chunk_elems() {
   return c;
 }
 
-static int64_t chunks_of(int64_t n) { return (n + chunk_elems() - 1) / chunk_elems(); }
+static int64_t stats_chunk_elems() {
+  static const int64_t c = [] {
+    const char* e = getenv("SMQ_MULTI_STATS_CHUNK");
+    const int64_t v = e ? atoll(e) : kDefaultStatsChunk;
+    return (v >= 4096 && v % 4096 == 0) ? v : kDefaultStatsChunk;
+  }();
+  return c;
+}
+
+static int64_t chunks_of(int64_t n, int64_t c) { return (n + c - 1) / c; }
 
 struct PlanSizes {
-  size_t hdr, descs, chunks, total;
-  int64_t n_chunks;
+  size_t hdr, descs, chunks, stat_chunks, total;
+  int64_t n_chunks, n_stat_chunks;
 };
 
 static bool plan_sizes(const int64_t* sizes, int count, PlanSizes* ps) {
-  int64_t nc = 0;
+  int64_t nc = 0, ns = 0;
   for (int t = 0; t < count; ++t) {
     if (sizes[t] < 1) return false;
-    nc += chunks_of(sizes[t]);
+    nc += chunks_of(sizes[t], chunk_elems());
+    ns += chunks_of(sizes[t], stats_chunk_elems());
   }
   ps->n_chunks = nc;
+  ps->n_stat_chunks = ns;
   ps->hdr = sizeof(MultiHeader);
   ps->descs = ((sizeof(SmqTensorDesc) * (size_t)count) + 31) & ~(size_t)31;
   ps->chunks = sizeof(ChunkDesc) * (size_t)nc;
-  ps->total = ps->hdr + ps->descs + ps->chunks;
+  ps->stat_chunks = sizeof(ChunkDesc) * (size_t)ns;
+  ps->total = ps->hdr + ps->descs + ps->chunks + ps->stat_chunks;
   return true;
+}
+
+// Chunk records of one map (element chunks of C) for every tensor, starting at ch.
+static void fill_chunks(ChunkDesc* ch, const SmqTensorDesc* descs, int count, int64_t C) {
+  int32_t g = 0;
+  for (int t = 0; t < count; ++t) {
+    const int64_t nc = chunks_of(descs[t].n, C);
+    const int32_t first = g;
+    for (int64_t c = 0; c < nc; ++c, ++g) {
+      ch[g].x = descs[t].x;
+      ch[g].y = descs[t].y;
+      ch[g].n = descs[t].n;
+      ch[g].begin = c * C;
+      ch[g].end = (c + 1) * C < descs[t].n ? (c + 1) * C : descs[t].n;
+      ch[g].rng_offset = descs[t].rng_offset;
+      ch[g].tensor = t;
+      ch[g].first_chunk = first;
+      ch[g].n_chunks = (int32_t)nc;
+      ch[g].all_positive = descs[t].all_positive;
+    }
+  }
 }
 
 }  // namespace smq
@@ -278,27 +336,12 @@ int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_
   MultiHeader* h = (MultiHeader*)base;
   h->count = count;
   h->n_chunks = (int32_t)ps.n_chunks;
-  const int64_t C = chunk_elems();
-  h->chunk = C;
+  h->chunk = chunk_elems();
+  h->n_stat_chunks = (int32_t)ps.n_stat_chunks;
+  h->stat_chunk = stats_chunk_elems();
   memcpy(base + ps.hdr, descs, sizeof(SmqTensorDesc) * (size_t)count);
-  ChunkDesc* ch = (ChunkDesc*)(base + ps.hdr + ps.descs);
-  int32_t g = 0;
-  for (int t = 0; t < count; ++t) {
-    const int64_t nc = chunks_of(descs[t].n);
-    const int32_t first = g;
-    for (int64_t c = 0; c < nc; ++c, ++g) {
-      ch[g].x = descs[t].x;
-      ch[g].y = descs[t].y;
-      ch[g].n = descs[t].n;
-      ch[g].begin = c * C;
-      ch[g].end = (c + 1) * C < descs[t].n ? (c + 1) * C : descs[t].n;
-      ch[g].rng_offset = descs[t].rng_offset;
-      ch[g].tensor = t;
-      ch[g].first_chunk = first;
-      ch[g].n_chunks = (int32_t)nc;
-      ch[g].all_positive = descs[t].all_positive;
-    }
-  }
+  fill_chunks((ChunkDesc*)(base + ps.hdr + ps.descs), descs, count, h->chunk);
+  fill_chunks((ChunkDesc*)(base + ps.hdr + ps.descs + ps.chunks), descs, count, h->stat_chunk);
   return SMQ_OK;
 }
 
@@ -307,7 +350,7 @@ size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count) {
   if (!sizes || count < 1 || !plan_sizes(sizes, count, &ps)) return 0;
   const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
   const size_t counters = ((sizeof(uint32_t) * (size_t)count) + 63) & ~(size_t)63;
-  return stats + counters + sizeof(StatPartial) * (size_t)ps.n_chunks;
+  return stats + counters + sizeof(StatPartial) * (size_t)ps.n_stat_chunks;
 }
 
 }  // extern "C"
@@ -322,7 +365,8 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   const MultiHeader* hh = (const MultiHeader*)host_plan;
   const int count = hh->count;
   const int n_chunks = hh->n_chunks;
-  if (!dev_plan || count < 1 || n_chunks < 1 || !p || !ws) {
+  const int n_stat_chunks = hh->n_stat_chunks;
+  if (!dev_plan || count < 1 || n_chunks < 1 || n_stat_chunks < 1 || !p || !ws) {
     set_error("multi: bad arguments");
     return SMQ_ERR_INVALID;
   }
@@ -332,7 +376,7 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   }
   const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
   const size_t counters = ((sizeof(uint32_t) * (size_t)count) + 63) & ~(size_t)63;
-  const size_t need = stats + counters + sizeof(StatPartial) * (size_t)n_chunks;
+  const size_t need = stats + counters + sizeof(StatPartial) * (size_t)n_stat_chunks;
   if (ws_bytes < need) {
     set_error("multi: workspace too small: need %zu bytes, got %zu", need, ws_bytes);
     return SMQ_ERR_WORKSPACE;
@@ -343,6 +387,7 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   A.hdr = (const MultiHeader*)pb;
   A.descs = (const SmqTensorDesc*)(pb + sizeof(MultiHeader));
   A.chunks = (const ChunkDesc*)(pb + sizeof(MultiHeader) + descs_bytes);
+  A.stat_chunks = A.chunks + n_chunks;
   char* wb = (char*)ws;
   A.stats = (SmqSmaqStats*)wb;
   A.counters = (uint32_t*)(wb + stats);
@@ -361,7 +406,7 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   A.sr = p->stochastic_rounding;
   A.count_outliers = p->count_outliers;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(smaq_multi_stats_kernel, dim3(n_chunks), dim3(kBlock), 0, st, A);
+  hipLaunchKernelGGL(smaq_multi_stats_kernel, dim3(n_stat_chunks), dim3(kBlock), 0, st, A);
   int rc = check_launch("smaq_multi_stats_kernel");
   if (rc) return rc;
 #define SMQ_MULTI_APPLY(SRV, SQV) \

@@ -108,6 +108,14 @@ __device__ __forceinline__ void ld_sc1_f32x2(const void* p, float& a, float& b) 
   b = __builtin_bit_cast(float, (uint32_t)(v >> 32));
 }
 
+__device__ __forceinline__ void st_sc1_u32(void* p, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1_u32(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Thread 0 has stored this workgroup's partial with st_sc1_*; count the arrival. Returns the
 // pre-increment value in every thread (== expected - 1 in the last workgroup).
 __device__ __forceinline__ uint32_t block_arrive(uint32_t* counter, uint32_t* lds_slot) {

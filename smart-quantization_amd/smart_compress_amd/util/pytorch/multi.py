@@ -34,6 +34,7 @@ class SmaqMulti:
         self.rng = rng  # shared with a SmartFP codec when fused into its optimizer calls
         self._plans = {}
         self._last = None
+        self._p = None
 
     def _plan(self, xs, ys, allpos, device):
         key = tuple((x.data_ptr(), y.data_ptr(), x.numel(), a) for x, y, a in zip(xs, ys, allpos))
@@ -65,14 +66,8 @@ class SmaqMulti:
         self._plans[key] = plan
         return plan
 
-    @torch.no_grad()
-    def __call__(self, xs: Sequence[torch.Tensor], ys: Optional[Sequence[torch.Tensor]] = None,
-                 all_positive=None) -> List[torch.Tensor]:
-        """Quantise-dequantise every ``xs[i]`` into ``ys[i]`` (new tensors if ``ys`` is None; may
-        alias ``xs`` for in-place). Tensors below ``min_size`` are passed through."""
+    def _select(self, xs, ys, all_positive):
         hp = self.hparams
-        if ys is None:
-            ys = [torch.empty_like(x) if x.numel() >= hp.min_size else x for x in xs]
         if all_positive is None:
             all_positive = [False] * len(xs)
         elif isinstance(all_positive, bool):
@@ -91,20 +86,48 @@ class SmaqMulti:
             sx.append(x)
             sy.append(y)
             sa.append(bool(all_positive[i]))
-        self._last = None
-        if not sel:
-            return list(ys)
-        device = sx[0].device
-        plan = self._plan(sx, sy, sa, device)
-        p = self._codec._params(1, False)
-        p.stats_source = N.SMQ_STATS_WORKSPACE
-        p.count_outliers = 1 if self.hparams.measure_compression_ratio else 0
+        return sel, sx, sy, sa
+
+    def _launch(self, plan, sel, device):
+        p = self._p
+        if p is None:  # built once: the C call reads it synchronously, only seed/offset change
+            p = self._p = self._codec._params(1, False)
+            p.stats_source = N.SMQ_STATS_WORKSPACE
+            p.count_outliers = 1 if self.hparams.measure_compression_ratio else 0
         p.seed, p.offset = self.rng.take(plan["total"])
         N.check(N.lib().smq_smaq_multi_f32(
             plan["dev"].data_ptr(), ctypes.addressof(plan["host"]), p, plan["ws"].data_ptr(),
             plan["ws"].numel(), N.stream_ptr(device)), "smq_smaq_multi_f32")
         self._last = dict(plan=plan, sel=sel, base=p.offset)
+
+    @torch.no_grad()
+    def __call__(self, xs: Sequence[torch.Tensor], ys: Optional[Sequence[torch.Tensor]] = None,
+                 all_positive=None) -> List[torch.Tensor]:
+        """Quantise-dequantise every ``xs[i]`` into ``ys[i]`` (new tensors if ``ys`` is None; may
+        alias ``xs`` for in-place). Tensors below ``min_size`` are passed through."""
+        hp = self.hparams
+        if ys is None:
+            ys = [torch.empty_like(x) if x.numel() >= hp.min_size else x for x in xs]
+        sel, sx, sy, sa = self._select(xs, ys, all_positive)
+        self._last = None
+        if not sel:
+            return list(ys)
+        device = sx[0].device
+        self._launch(self._plan(sx, sy, sa, device), sel, device)
         return list(ys)
+
+    def bind(self, xs: Sequence[torch.Tensor], ys: Sequence[torch.Tensor],
+             all_positive=None) -> "BoundSmaqMulti":
+        """Validate a FIXED list of buffers once (parameters, optimizer state, preallocated
+        outputs) and return a callable that only draws the random stream and launches: no
+        per-tensor Python work per call. The buffers must keep their storage while bound."""
+        sel, sx, sy, sa = self._select(xs, ys, all_positive)
+        for i, (x, y) in enumerate(zip(xs, ys)):
+            if i not in sel and y is not x:
+                raise RuntimeError("bind: tensors below min_size must be passed as ys[i] = xs[i]")
+        device = sx[0].device if sx else None
+        plan = self._plan(sx, sy, sa, device) if sel else None
+        return BoundSmaqMulti(self, plan, sel, device, list(ys))
 
     # -- inspection (tests, logging) ---------------------------------------------------------------
     @property
@@ -129,3 +152,16 @@ class SmaqMulti:
             out.append(dict(mean=float(f[0]), std_dev=float(f[1]), std_clamped=float(f[2]),
                             raw_std=float(f[3]), n_outlier=int(r[32:40].view(np.uint64)[0])))
         return out
+
+
+class BoundSmaqMulti:
+    """``SmaqMulti.bind`` result: one call = the two launches of the bound list."""
+
+    def __init__(self, multi: SmaqMulti, plan, sel, device, ys):
+        self.multi, self.plan, self.sel, self.device, self.ys = multi, plan, sel, device, ys
+
+    @torch.no_grad()
+    def __call__(self) -> List[torch.Tensor]:
+        if self.plan is not None:
+            self.multi._launch(self.plan, self.sel, self.device)
+        return self.ys

@@ -137,14 +137,15 @@ def test_multi_plan_layout():
     from smart_compress_amd import _native as N
 
     lib = N.lib()
-    C = 8192  # default chunk (csrc/smaq_multi.hip kDefaultChunk)
-    sizes = [10, C, C + 1, 3 * C + 5]
+    C, S = 8192, 32768  # default apply / statistics chunks (csrc/smaq_multi.hip)
+    sizes = [10, C, C + 1, 3 * C + 5, S + 1]
     count = len(sizes)
     arr = (ctypes.c_int64 * count)(*sizes)
     nbytes = lib.smq_smaq_multi_plan_bytes(arr, count)
-    chunks = [1, 1, 2, 4]
+    chunks = [1, 1, 2, 4, 5]
+    schunks = [1, 1, 1, 1, 2]
     dbytes = ((40 * count + 31) // 32) * 32
-    assert nbytes == 32 + dbytes + 64 * sum(chunks)
+    assert nbytes == 32 + dbytes + 64 * (sum(chunks) + sum(schunks))
     descs = (N.SmqTensorDesc * count)()
     rel = 0
     for i, n in enumerate(sizes):
@@ -158,17 +159,25 @@ def test_multi_plan_layout():
     raw = np.frombuffer(bytes(host), dtype=np.uint8)
     assert list(raw[:8].view(np.int32)) == [count, sum(chunks)]
     assert int(raw[8:16].view(np.int64)[0]) == C
+    assert int(raw[16:20].view(np.int32)[0]) == sum(schunks)
+    assert int(raw[24:32].view(np.int64)[0]) == S
     rec = raw[32 + dbytes:].reshape(-1, 64)
+    assert rec.shape[0] == sum(chunks) + sum(schunks)
     q = rec[:, :48].copy().view(np.int64)  # x, y, n, begin, end, rng_offset
     i32 = rec[:, 48:].copy().view(np.int32)  # tensor, first_chunk, n_chunks, all_positive
-    assert list(i32[:, 0]) == [0, 1, 2, 2, 3, 3, 3, 3]
-    assert list(i32[:, 1]) == [0, 1, 2, 2, 4, 4, 4, 4]
-    assert list(i32[:, 2]) == [1, 1, 2, 2, 4, 4, 4, 4]
-    assert list(i32[:, 3]) == [0, 1, 0, 0, 1, 1, 1, 1]
-    assert list(q[:, 0]) == [0x1000, 0x2000, 0x3000, 0x3000, 0x4000, 0x4000, 0x4000, 0x4000]
-    assert list(q[:, 3]) == [0, 0, 0, C, 0, C, 2 * C, 3 * C]
-    assert list(q[:, 4]) == [10, C, C, C + 1, C, 2 * C, 3 * C, 3 * C + 5]
-    assert list(q[:, 5]) == [0, 10, 10 + C, 10 + C, 10 + 2 * C + 1] + [10 + 2 * C + 1] * 3
-    assert lib.smq_smaq_multi_workspace_bytes(arr, count) >= 64 * count + 32 * sum(chunks)
+    a = slice(0, sum(chunks))
+    assert list(i32[a, 0]) == [0, 1, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4]
+    assert list(i32[a, 1]) == [0, 1, 2, 2, 4, 4, 4, 4, 8, 8, 8, 8, 8]
+    assert list(i32[a, 2]) == [1, 1, 2, 2, 4, 4, 4, 4, 5, 5, 5, 5, 5]
+    assert list(i32[a, 3]) == [0, 1, 0, 0, 1, 1, 1, 1, 0, 0, 0, 0, 0]
+    assert list(q[a, 3])[:8] == [0, 0, 0, C, 0, C, 2 * C, 3 * C]
+    assert list(q[a, 4])[:8] == [10, C, C, C + 1, C, 2 * C, 3 * C, 3 * C + 5]
+    assert list(q[a, 5])[:5] == [0, 10, 10 + C, 10 + C, 10 + 2 * C + 1]
+    b = slice(sum(chunks), None)  # the statistics map
+    assert list(i32[b, 0]) == [0, 1, 2, 3, 4, 4]
+    assert list(i32[b, 1]) == [0, 1, 2, 3, 4, 4]
+    assert list(i32[b, 2]) == [1, 1, 1, 1, 2, 2]
+    assert list(q[b, 3]) == [0, 0, 0, 0, 0, S] and list(q[b, 4]) == [10, C, C + 1, 3 * C + 5, S, S + 1]
+    assert lib.smq_smaq_multi_workspace_bytes(arr, count) >= 64 * count + 32 * sum(schunks)
     descs[1].n = 0
     assert lib.smq_smaq_multi_plan_build(descs, count, host, nbytes) == -1

@@ -160,3 +160,24 @@ def test_s2fp8_edge_cases():
     yh = y.cpu().numpy()
     assert (yh[::5] == 0).all()
     assert np.isfinite(yh).all()
+
+
+@pytest.mark.parametrize("n", [3 * 2**20 + 3, 12 * 2**20 + 1])
+def test_s2fp8_single_launch_and_two_launch_paths(n):
+    """n that fits in registers across the grid (one cooperative launch) and n that does not (stats
+    + apply launches): both match the oracle with the device's own statistics and counter RNG."""
+    from oracle import rng as orng
+    from oracle import s2fp8 as os2
+
+    g = _g()
+    gen = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(n, generator=gen, device="cuda")
+    x[::7] = 0.0
+    y, st = g.s2fp8(x, check_inf=True, seed=11, offset=5)
+    xh = x.cpu().numpy()
+    own = os2.stats(xh)
+    assert abs(float(st["mu"]) - float(own["mu"])) <= 2.0**-20 * max(1.0, abs(float(own["mu"])))
+    assert ulp_diff(st["m"], own["m"]) <= 1
+    words = orng.rng_u32(11, 5, n)
+    ref = os2.roundtrip(xh, words, True, st=os2.derive(st["mu"], st["m"]))
+    _assert_code_domain(y.cpu().numpy(), ref[0])

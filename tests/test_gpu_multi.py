@@ -59,3 +59,22 @@ def test_multi_repeated_calls_reuse_plan():
         m(xs, ys)
     torch.cuda.synchronize()
     assert all(torch.isfinite(y).all() for y in ys)
+
+
+def test_bound_multi_equals_per_call():
+    """SmaqMulti.bind (fixed buffers, no per-call Python checks) computes what the per-call path
+    computes for the same random stream."""
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    torch.manual_seed(0)
+    xs = [torch.randn(s, device="cuda") for s in ((300, 7), (5,), (4096 * 3 + 1,), (64, 64))]
+    ys1 = [torch.empty_like(x) if x.numel() >= 8 else x for x in xs]
+    ys2 = [torch.empty_like(x) if x.numel() >= 8 else x for x in xs]
+    a, b = SmaqMulti(smaq_hparams(), seed=5), SmaqMulti(smaq_hparams(), seed=5)
+    bound = b.bind(xs, ys2, all_positive=[False, False, True, False])
+    for _ in range(2):
+        a(xs, ys1, all_positive=[False, False, True, False])
+        bound()
+        torch.cuda.synchronize()
+        for u, v in zip(ys1, ys2):
+            assert torch.equal(u.view(torch.int32), v.view(torch.int32))
