@@ -110,17 +110,32 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
   const uint32_t prev = block_arrive(counter, &arrive_slot);
   if (prev != gridDim.x - 1) return;
 
-  // Last workgroup: ordered reduction of all partials (deterministic for a given n).
+  // Last workgroup: ordered reduction of all partials (deterministic for a given n). Every load
+  // of a lane is issued before any is consumed: a loop that adds as it loads waits out one memory
+  // round trip per partial (8 serial ~1.5 us trips at 2048 partials).
+  constexpr int K = kStatsGridCap / kBlock;
+  double s1v[K], s2v[K];
+  float mnv[K], mxv[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int b = threadIdx.x + i * kBlock;
+    if (b < (int)gridDim.x) {
+      const StatPartial* p = partials + b;
+      s1v[i] = ld_sc1_f64(&p->s1);
+      s2v[i] = ld_sc1_f64(&p->s2);
+      if (RANGE) ld_sc1_f32x2(&p->mn, mnv[i], mxv[i]);
+    }
+  }
   StatAcc tot;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
-    const StatPartial* p = partials + b;
-    tot.s1 += ld_sc1_f64(&p->s1);
-    tot.s2 += ld_sc1_f64(&p->s2);
-    if (RANGE) {
-      float mn, mx;
-      ld_sc1_f32x2(&p->mn, mn, mx);
-      tot.mn = fminf(tot.mn, mn);
-      tot.mx = fmaxf(tot.mx, mx);
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    if (threadIdx.x + i * kBlock < (int)gridDim.x) {
+      tot.s1 += s1v[i];
+      tot.s2 += s2v[i];
+      if (RANGE) {
+        tot.mn = fminf(tot.mn, mnv[i]);
+        tot.mx = fmaxf(tot.mx, mxv[i]);
+      }
     }
   }
   block_reduce_stats<RANGE>(tot);

@@ -117,11 +117,27 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   }
   const uint32_t prev = block_arrive(&A.counters[ch.tensor], &slot);
   if (prev != (uint32_t)ch.n_chunks - 1) return;
+  // batches of loads issued before they are consumed (one round trip per batch, not per partial)
+  constexpr int K = 8;
   StatAcc tot;
-  for (int b = threadIdx.x; b < ch.n_chunks; b += kBlock) {
-    const StatPartial* p = A.partials + ch.first_chunk + b;
-    tot.s1 += ld_sc1_f64(&p->s1);
-    tot.s2 += ld_sc1_f64(&p->s2);
+  for (int b0 = 0; b0 < ch.n_chunks; b0 += K * kBlock) {
+    double s1v[K], s2v[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int b = b0 + threadIdx.x + i * kBlock;
+      if (b < ch.n_chunks) {
+        const StatPartial* p = A.partials + ch.first_chunk + b;
+        s1v[i] = ld_sc1_f64(&p->s1);
+        s2v[i] = ld_sc1_f64(&p->s2);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      if (b0 + threadIdx.x + i * kBlock < ch.n_chunks) {
+        tot.s1 += s1v[i];
+        tot.s2 += s2v[i];
+      }
+    }
   }
   block_reduce_stats<false>(tot);
   if (threadIdx.x == 0) {
