@@ -366,7 +366,12 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   uint32_t* counter = (uint32_t*)(base + SmaqWsLayout::kHeader);
   StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
   const int vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) ? 1 : 0;
-  const int grid = grid_for(n, kBlock * 4, kStatsGridCap);
+  static const int cap = [] {  // measurement knob SMQ_STATS_GRID (<= kStatsGridCap)
+    const char* e = getenv("SMQ_STATS_GRID");
+    const int v = e ? atoi(e) : kStatsGridCap;
+    return (v >= 64 && v <= kStatsGridCap) ? v : kStatsGridCap;
+  }();
+  const int grid = grid_for(n, kBlock * 4, cap);
   FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n)};
 #define SMQ_STATS(RANGE, TIN)                                                                    \
   hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n, vec, \

@@ -28,6 +28,8 @@ SHORT = {
     "float_quant_kernel": "float_quant_kernel",
     "s2fp8_stats_kernel": "s2fp8_stats_kernel",
     "s2fp8_apply_kernel": "s2fp8_apply_kernel",
+    "smaq_pack_kernel": "smaq_pack_kernel",
+    "smaq_unpack_kernel": "smaq_unpack_kernel",
 }
 
 
@@ -83,7 +85,7 @@ def main():
         json.dump(summary, f, indent=1)
     main_k = {"smaq": "smaq_apply_kernel", "smaq_sampled": "smaq_apply_kernel",
               "fp8": "float_quant_kernel", "s2fp8": "s2fp8_apply_kernel",
-              "multi": "smaq_multi_apply_kernel"}[config]
+              "multi": "smaq_multi_apply_kernel", "packed": "smaq_unpack_kernel"}[config]
     if main_k in kernels and "hbm_bytes_per_launch" in kernels[main_k]:
         with open(os.path.join(REPO, "profiles", f"traffic_{config}.json"), "w") as f:
             json.dump(dict(source=f"profiles/{tag}_summary.json", kernel=main_k,
