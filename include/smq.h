@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define SMQ_ABI_VERSION 1
+#define SMQ_ABI_VERSION 2
 
 #define SMQ_OK 0
 #define SMQ_ERR_INVALID -1  /* bad argument */
@@ -107,6 +107,11 @@ typedef struct SmqSmaqParams {
   int64_t bn_channels;
   int64_t bn_inner;             /* H * W */
   int64_t sample_idx[SMQ_MAX_SAMPLES]; /* distinct flat indices for SMQ_STATS_SAMPLED */
+  /* Graph-safe random stream: if non-NULL, a device uint64 holding the stream position. The first
+   * kernel of the call reads it into the statistics record (SmqSmaqStats.rng_offset) and advances
+   * it by n; element i then draws counter offset + rng_offset + i. Nothing on the host changes
+   * between calls, so a captured hipGraph replays with fresh, consecutive random streams. */
+  uint64_t* offset_counter;
 } SmqSmaqParams;
 
 /*
@@ -121,14 +126,15 @@ typedef struct SmqSmaqStats {
   float min_val;       /* min / max (valid in range-std mode) */
   float max_val;
   uint32_t n_used;     /* elements the statistics were computed over */
-  uint32_t reserved0;
+  uint32_t quot_check; /* library-internal: 1 if (x - mean) / std_clamped can need the IEEE
+                          subnormal path (see smaq_elem.h quot_check_for) */
   unsigned long long n_outlier; /* multi-tensor calls: this tensor's outlier count (single-tensor
                                    calls: see SMQ_WS_OUTLIER_SLOTS_OFFSET) */
   double inv_std_clamped;      /* RN64(1 / std_clamped); written by the library (injected stats:
-                                  ignored, the library derives it from std_clamped) */
-  uint32_t quot_check;         /* library-internal: 1 if (x - mean) / std_clamped can need the
-                                  IEEE subnormal path (see smaq_elem.h); derived like the above */
-  uint32_t reserved[3];
+                                  ignored, the library derives it and quot_check itself) */
+  unsigned long long rng_offset; /* the call's stream position when params.offset_counter is set
+                                    (else 0), added to params.offset by the element kernels */
+  uint32_t reserved[2];
 } SmqSmaqStats;
 
 /* One tensor of a multi-tensor call. y may alias x (in-place, the optimizer path). */

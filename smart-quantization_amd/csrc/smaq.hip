@@ -156,6 +156,7 @@ struct ApplyArgs {
   float thr, r_main, r_out, clamp_lo, clamp_hi, range_coef;
   double inv_r_main, inv_r_out;  // host-computed reciprocals of the ranges
   int safe_q;
+  unsigned long long* rng_ctr;   // params.offset_counter (graph-safe stream) or NULL
   uint32_t key;
   int all_pos;
   int count;
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(kWave) void smaq_sample_stats_kernel(ApplyArgs A) {
   const float mx = wave_max(valid ? v : -INFINITY);
   if (lane == 0) {
     SmqSmaqStats st;
-    FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef};
+    FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, A.rng_ctr, A.n};
     // finalize_stats takes shifted sums: shift = mean, s1 = 0, s2 = m2 (biased)
     if (A.use_range)
       finalize_stats<true, TIN>(0.0, m2, mn, mx, A.k, mean, true, f, &st);
@@ -203,11 +204,17 @@ __global__ __launch_bounds__(kWave) void smaq_sample_stats_kernel(ApplyArgs A) {
 
 // Injected statistics (parity tests, callers with their own mean/std): copy the record into the
 // workspace header with the fp64 reciprocal the element transform reads.
-__global__ void smaq_prep_injected_kernel(const SmqSmaqStats* in, SmqSmaqStats* out) {
+__global__ void smaq_prep_injected_kernel(const SmqSmaqStats* in, SmqSmaqStats* out,
+                                          unsigned long long* rng_ctr, int64_t n) {
   if (threadIdx.x == 0) {
     SmqSmaqStats s = *in;
     s.inv_std_clamped = 1.0 / (double)s.std_clamped;
     s.quot_check = quot_check_for(s.std_clamped);
+    s.rng_offset = 0ull;
+    if (rng_ctr) {
+      s.rng_offset = *rng_ctr;
+      *rng_ctr = s.rng_offset + (unsigned long long)n;
+    }
     *out = s;
   }
 }
@@ -217,7 +224,8 @@ __global__ void smaq_prep_injected_kernel(const SmqSmaqStats* in, SmqSmaqStats* 
 // SUB: see quot_check_for. The unaligned (!VEC) variant always keeps the subnormal check and
 // divides q / range by IEEE division (the launcher routes safe_q calls to it).
 template <int RM, bool VEC, bool BN, int TIN, int TV, bool AP, bool SUB>
-__device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemConsts& c) {
+__device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemConsts& c,
+                                               uint64_t off) {
   constexpr int kTileElems = kBlock * TV * 4;
   uint32_t n_out = 0;
   const int64_t n = A.n;
@@ -244,7 +252,7 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemCon
       if (j >= nv) continue;
       float u0 = 0.0f, u1 = 0.0f, u2 = 0.0f, u3 = 0.0f;
       if (RM == kRoundHash) {
-        rng_hu4(A.key, A.offset + ((uint64_t)j << 2), u0, u1, u2, u3);
+        rng_hu4(A.key, off + ((uint64_t)j << 2), u0, u1, u2, u3);
       } else if (RM == kRoundUniform) {
         u0 = uu[u].x; u1 = uu[u].y; u2 = uu[u].z; u3 = uu[u].w;
       }
@@ -261,7 +269,7 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemCon
     if (tile == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
       const int64_t e = (nv << 2) + threadIdx.x;
       float uf = 0.0f;
-      if (RM == kRoundHash) uf = rng_hu(A.key, A.offset + (uint64_t)e);
+      if (RM == kRoundHash) uf = rng_hu(A.key, off + (uint64_t)e);
       if (RM == kRoundUniform) uf = A.uniforms[e];
       bool bt;
       A.y[e] = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(load1<TIN>(A.x, e), uf, c, bt, bn_term<BN>(A, e));
@@ -275,7 +283,7 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemCon
       const int64_t e = e0 + (int64_t)k * kBlock;
       if (e >= n) break;
       float uf = 0.0f;
-      if (RM == kRoundHash) uf = rng_hu(A.key, A.offset + (uint64_t)e);
+      if (RM == kRoundHash) uf = rng_hu(A.key, off + (uint64_t)e);
       if (RM == kRoundUniform) uf = A.uniforms[e];
       bool bt;
       A.y[e] = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(load1<TIN>(A.x, e), uf, c, bt, bn_term<BN>(A, e));
@@ -292,17 +300,18 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
   ElemConsts c;
   const float cthr = (BN || TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
   init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+  const uint64_t off = A.offset + A.stats->rng_offset;  // + graph-safe stream position
   // uniform per launch: pick the body once (all_positive, subnormal-quotient check)
   uint32_t n_out;
   if (!VEC) {
-    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c)
-                      : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c);
+    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c, off)
+                      : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c, off);
   } else if (A.stats->quot_check) {
-    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c)
-                      : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c);
+    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c, off)
+                      : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c, off);
   } else {
-    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, false>(A, c)
-                      : apply_body<RM, VEC, BN, TIN, TV, false, false>(A, c);
+    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, false>(A, c, off)
+                      : apply_body<RM, VEC, BN, TIN, TV, false, false>(A, c, off);
   }
 
   if (A.count) {  // outlier count for log_size (smart.py:184-188): one atomic per workgroup,
@@ -372,7 +381,8 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
     return (v >= 64 && v <= kStatsGridCap) ? v : kStatsGridCap;
   }();
   const int grid = grid_for(n, kBlock * 4, cap);
-  FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n)};
+  FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n),
+                   (unsigned long long*)p->offset_counter, n};
 #define SMQ_STATS(RANGE, TIN)                                                                    \
   hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n, vec, \
                      fin, partials, counter, hdr)
@@ -475,6 +485,7 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   A.safe_q = R.safe_q;
   A.key = rng_key(p->seed);
   A.offset = p->offset;
+  A.rng_ctr = (unsigned long long*)p->offset_counter;
   A.all_pos = p->all_positive;
   A.count = p->count_outliers;
   A.use_range = p->use_range_std_dev;
@@ -522,7 +533,7 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   const int grid = (int)tiles;
   if (p->stats_source == SMQ_STATS_INJECTED) {
     hipLaunchKernelGGL(smaq_prep_injected_kernel, dim3(1), dim3(kWave), 0, st, stats_in,
-                       A.ws_stats);
+                       A.ws_stats, A.rng_ctr, n);
     A.stats = A.ws_stats;
   }
   if (p->stats_source == SMQ_STATS_SAMPLED) {
@@ -569,6 +580,7 @@ int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, v
   A.clamp_lo = p->clamp_lo;
   A.clamp_hi = p->clamp_hi;
   A.use_range = p->use_range_std_dev;
+  A.rng_ctr = (unsigned long long*)p->offset_counter;
   const int rc = fill_sampled(A, p, n);
   if (rc) return rc;
   launch_sample_stats(A, dtype, st);

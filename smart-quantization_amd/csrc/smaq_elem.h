@@ -112,6 +112,8 @@ __device__ __forceinline__ void block_reduce_stats(StatAcc& a) {
 
 struct FinalizeArgs {
   float clamp_lo, clamp_hi, range_coef;  // range_coef is representable in the input type
+  unsigned long long* rng_ctr = nullptr;  // graph-safe stream position (params.offset_counter)
+  int64_t rng_n = 0;                      // elements the call consumes from it
 };
 
 // mean / std from shifted sums -> SmqSmaqStats (smart.py:130-134, 100-108, 151-152, 154).
@@ -160,6 +162,13 @@ __device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, f
   out->n_outlier = 0ull;
   out->inv_std_clamped = 1.0 / (double)sc;  // once per call, for the element transform
   out->quot_check = quot_check_for(sc);
+  // graph-safe random stream: snapshot the position for this call's element kernels, advance it
+  unsigned long long base = 0ull;
+  if (f.rng_ctr) {
+    base = *f.rng_ctr;
+    *f.rng_ctr = base + (unsigned long long)f.rng_n;
+  }
+  out->rng_offset = base;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -173,6 +182,7 @@ struct ElemConsts {
   float r_main, r_out;    // ranges
   double inv_sc;          // RN64(1 / sc): written by the statistics finaliser
   double inv_r_main, inv_r_out;  // RN64(1 / range): computed on the host
+  uint64_t rng_off;       // the call's graph-safe stream position (SmqSmaqStats.rng_offset)
 };
 
 // Correctly rounded fp32 quotient a / b from a double reciprocal: RN32(RN64(a * RN64(1/b))).
@@ -205,6 +215,7 @@ __device__ __forceinline__ void init_consts(ElemConsts& c, const SmqSmaqStats* s
   c.r_out = r_out;
   c.inv_r_main = inv_r_main;
   c.inv_r_out = inv_r_out;
+  c.rng_off = st->rng_offset;
 }
 
 // Host: reciprocals of the two ranges (IEEE double division, as the device would compute them).

@@ -200,7 +200,7 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
         if (FULL || el + i < n_el) v[i] = load1<TIN>(A.x, e0 + el + i);
     }
     if (RM == kRoundHash) {
-      const uint64_t ctr = A.offset + (uint64_t)(e0 + el);
+      const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
       if (full4) {
         rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
       } else {
@@ -302,7 +302,8 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
     for (int i = 0; i < 4; ++i) {
       if (!((xm[k] >> i) & 1u)) continue;
       const uint32_t el = 1024u * k + 4u * tid + i;
-      const float uf = RM == kRoundHash ? rng_hu(A.key, A.offset + (uint64_t)(e0 + el)) : 0.f;
+      const float uf =
+          RM == kRoundHash ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)(e0 + el)) : 0.f;
       bool hi, lo;
       const float q = smaq_quant<RM, false, TIN, SUB>(load1<TIN>(A.x, e0 + el), uf, c, hi, lo);
       const uint32_t r = base_x + __popc(xm[k] & ((1u << i) - 1u));

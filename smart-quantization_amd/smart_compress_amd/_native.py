@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get(
     "SMQ_LIB", os.path.join(os.path.dirname(_PKG_DIR), "lib", "libsmq.so")
 )
 
-SMQ_ABI_VERSION = 1
+SMQ_ABI_VERSION = 2
 SMQ_MAX_SAMPLES = 64
 SMQ_WS_OUTLIER_SLOTS_OFFSET = 128
 SMQ_WS_OUTLIER_SLOTS = 64
@@ -56,6 +56,7 @@ class SmqSmaqParams(ctypes.Structure):
         ("bn_channels", ctypes.c_int64),
         ("bn_inner", ctypes.c_int64),
         ("sample_idx", ctypes.c_int64 * SMQ_MAX_SAMPLES),
+        ("offset_counter", ctypes.c_void_p),
     ]
 
 
@@ -68,11 +69,11 @@ class SmqSmaqStats(ctypes.Structure):
         ("min_val", ctypes.c_float),
         ("max_val", ctypes.c_float),
         ("n_used", ctypes.c_uint32),
-        ("reserved0", ctypes.c_uint32),
+        ("quot_check", ctypes.c_uint32),
         ("n_outlier", ctypes.c_ulonglong),
         ("inv_std_clamped", ctypes.c_double),
-        ("quot_check", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 3),
+        ("rng_offset", ctypes.c_ulonglong),
+        ("reserved", ctypes.c_uint32 * 2),
     ]
 
 

@@ -87,7 +87,7 @@ class SmartFPPacked(SmartFP):
             raise RuntimeError("value cannot be converted to type c10::Half without overflow")
         x = data.contiguous()
         lib = N.lib()
-        p = self._params(numel, all_positive, x.dtype)
+        p = self._params(numel, all_positive, x.dtype, x.device)
         bound = lib.smq_smaq_pack_bound(numel, hp.num_bits_main, hp.num_bits_outlier)
         scratch = N.workspace("smaq_pack_out", x.device, bound)
         ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(numel))

@@ -98,10 +98,36 @@ class SmartFP(CompressionAlgorithmBase):
         self.range_normal = main_codes / hp.main_std_dev_threshold
         self.clamped_range = (1e-4, 1e4) if hp.precision == 16 else (1e-38, 1e38)
         self.rng = N.RngState(getattr(hp, "smq_seed", None))
+        self._graph_safe = False
+        self._counters = {}
+
+    # -- graph-safe random stream ----------------------------------------------------------------
+    def graph_safe(self, enable: bool = True, device=None):
+        """Keep the random-stream position in a device counter (``SmqSmaqParams.offset_counter``)
+        instead of advancing ``self.rng.offset`` on the host, so calls captured in a hipGraph
+        (``torch.cuda.graph``) draw fresh, consecutive random streams on every replay. The stream
+        continues from the host position; create the counter before capturing (pass ``device`` or
+        make one eager call first). Values are identical to the host-offset mode for the same
+        sequence of calls."""
+        self._graph_safe = bool(enable)
+        if enable and device is not None:
+            self._rng_counter(torch.device(device))
+        return self
+
+    def _rng_counter(self, device: torch.device) -> torch.Tensor:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        c = self._counters.get(idx)
+        if c is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("SmartFP.graph_safe: create the device counter before capture "
+                                   "(graph_safe(device=...) or one eager call)")
+            c = torch.tensor([self.rng.offset], dtype=torch.int64, device=device)
+            self._counters[idx] = c
+        return c
 
     # -- parameter block -------------------------------------------------------------------------
     def _params(self, numel: int, all_positive: bool,
-                dtype: torch.dtype = torch.float32) -> N.SmqSmaqParams:
+                dtype: torch.dtype = torch.float32, device=None) -> N.SmqSmaqParams:
         hp = self.hparams
         p = N.SmqSmaqParams()
         p.num_bits_main = hp.num_bits_main
@@ -115,7 +141,11 @@ class SmartFP(CompressionAlgorithmBase):
         p.all_positive = 1 if all_positive else 0
         p.use_range_std_dev = 1 if hp.use_range_std_dev else 0
         p.count_outliers = 1 if hp.measure_compression_ratio else 0
-        p.seed, p.offset = self.rng.take(numel)
+        if self._graph_safe and device is not None:
+            p.seed, p.offset = self.rng.seed, 0
+            p.offset_counter = self._rng_counter(device).data_ptr()
+        else:
+            p.seed, p.offset = self.rng.take(numel)
         p.range_std_coef = -1.0  # set below in range mode (0.0 is a valid coefficient)
         if hp.use_sample_stats:
             k = min(numel, hp.num_samples)
@@ -179,10 +209,13 @@ class SmartFP(CompressionAlgorithmBase):
             if data.dtype == torch.float16 and hp.precision != 16:
                 # the reference's std.clamp(1e-38, 1e38) on a half tensor (smart.py:154)
                 raise RuntimeError("value cannot be converted to type c10::Half without overflow")
+            if hp.measure_compression_ratio and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("SmartFP: --measure_compression_ratio reads the outlier count "
+                                   "on the host; it cannot run inside a graph capture")
             x = data.contiguous()
             # half inputs: the bool*float scalars/ranges tensors promote the chain to fp32
             y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
-            p = self._params(numel, all_positive, x.dtype)
+            p = self._params(numel, all_positive, x.dtype, x.device)
             keep = None
             if hp.use_batch_norm and batch_norm_stats is not None:
                 keep = self._bind_batch_norm(p, x, batch_norm_stats)

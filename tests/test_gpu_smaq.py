@@ -382,7 +382,10 @@ def test_subnormal_z_paths(sc):
     stats = g.stats_struct(0.0, sc, hp)
     y, ws = g.smaq_apply(xd, p, stats_in=stats)
     torch.cuda.synchronize()
-    flag = int(ws[48:52].cpu().numpy().view(np.uint32)[0])
+    from smart_compress_amd import _native as N
+
+    o = N.SmqSmaqStats.quot_check.offset
+    flag = int(ws[o:o + 4].cpu().numpy().view(np.uint32)[0])
     assert flag == quot_check_for(sc) == (1 if sc in (6.0, 2.0**25) else 0)
     y_or, _ = osmaq.apply(x, 0.0, sc, osmaq.SmaqConfig(), orng.uniforms(5, 11, x.size))
     assert same_f32(y.cpu().numpy(), y_or), n_diff_f32(y.cpu().numpy(), y_or)
@@ -406,3 +409,43 @@ def test_huge_range_ieee_quotient():
     yh = y.cpu().numpy()
     assert same_f32(yh, y_or), n_diff_f32(yh, y_or)
     assert np.any((np.abs(yh) < np.finfo(np.float32).tiny) & (yh != 0))  # subnormal q / range hit
+
+
+def test_graph_safe_stream_eager_and_captured():
+    """SmartFP.graph_safe(): the stream position lives in a device counter advanced by the first
+    kernel of each call. Eager calls equal the host-offset mode; a captured torch.cuda graph draws
+    fresh, consecutive streams on every replay (each replay equals the next host-mode call)."""
+    from smart_compress_amd.compress.smart import SmartFP
+
+    n = (1 << 20) + 3
+    x = torch.randn(n, device="cuda") * 1.7
+    host = SmartFP(smaq_hparams())
+    host.rng.seed, host.rng.offset = 77, 5
+    dev = SmartFP(smaq_hparams())
+    dev.rng.seed, dev.rng.offset = 77, 5
+    dev.graph_safe(device="cuda")
+    for _ in range(3):  # eager: identical streams
+        assert torch.equal(dev(x).view(torch.int32), host(x).view(torch.int32))
+    torch.cuda.synchronize()
+    # capture one call, replay three times
+    static_x = x.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        dev(static_x)  # warm-up on the capture stream (workspace for this stream)
+        host(static_x)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y_static = dev(static_x)
+    outs = []
+    for _ in range(3):
+        g.replay()
+        outs.append(y_static.clone())
+    torch.cuda.synchronize()
+    refs = [host(static_x) for _ in range(3)]
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert torch.equal(o.view(torch.int32), r.view(torch.int32))
+    assert not torch.equal(outs[0], outs[1])  # fresh randomness per replay
