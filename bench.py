@@ -420,13 +420,114 @@ def run_packed(args, world, rank, device):
                          "traffic": None}}
 
 
+def _vgg_cifar():
+    import torch.nn as nn
+
+    def stage(cin, cout):
+        return [nn.Conv2d(cin, cout, 3, padding=1, bias=False), nn.BatchNorm2d(cout), nn.ReLU(),
+                nn.Conv2d(cout, cout, 3, padding=1, bias=False), nn.BatchNorm2d(cout), nn.ReLU()]
+
+    layers = stage(3, 64) + [nn.MaxPool2d(2)] + stage(64, 128) + [nn.MaxPool2d(2)] + \
+        stage(128, 256) + [nn.MaxPool2d(2)] + stage(256, 512) + \
+        [nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(512, 10)]
+    return nn.Sequential(*layers)
+
+
+def run_autograd(args, world, rank, device):
+    """SURVEY 8f-2 at model scale: a CIFAR-shaped VGG-style CNN (batch 128) trained with SmaQ on
+    every selected layer's activation (forward) and grad-map (backward) through the mirrored
+    register_autograd_module (autograd.py:50-77). Three variants: no compression, codec calls
+    eager, and the whole training step captured in a hipGraph (SmartFP.graph_safe: fresh random
+    streams per replay)."""
+    from argparse import Namespace
+
+    import torch.nn.functional as F
+
+    from smart_compress_amd.compress.smart import SmartFP
+    from smart_compress_amd.util.pytorch.autograd import register_autograd_module
+
+    batch = 128
+    torch.manual_seed(rank)
+    x = torch.randn(batch, 3, 32, 32, device=device)
+    t = torch.randint(0, 10, (batch,), device=device)
+    flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
+    calls = {"n": 0, "elems": 0}
+
+    def build(compress):
+        torch.manual_seed(0)
+        net = _vgg_cifar().to(device)
+        opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9)
+        codec = None
+        if compress:
+            codec = SmartFP(smaq_hparams())
+            codec.rng.seed = 3000 + rank
+
+            def fn(v, tag=None, **kw):
+                calls["n"] += 1
+                calls["elems"] += v.numel()
+                return codec(v, tag=tag, **kw)
+
+            register_autograd_module(net, fn, flags)
+        return net, opt, codec
+
+    def step_fn(net, opt):
+        def step():
+            opt.zero_grad(set_to_none=False)
+            loss = F.cross_entropy(net(x), t)
+            loss.backward()
+            opt.step()
+        return step
+
+    results = {}
+    for name in ("uncompressed", "smaq_eager", "smaq_graph"):
+        net, opt, codec = build(name != "uncompressed")
+        step = step_fn(net, opt)
+        if name == "smaq_graph":
+            codec.graph_safe(device=device)
+            s = torch.cuda.Stream(device)
+            s.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    step()
+            torch.cuda.current_stream(device).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            run = g.replay
+        else:
+            run = step
+        calls["n"] = calls["elems"] = 0
+        run()
+        torch.cuda.synchronize()
+        per_step = (calls["n"], calls["elems"])
+        for _ in range(args.warmup):
+            run()
+        elapsed = time_steps(run, args.steps, 0, world, device)
+        results[name] = {"ms_per_step": round(elapsed / args.steps * 1e3, 4)}
+        if name != "uncompressed" and per_step[0]:
+            results[name].update(codec_calls_per_step=per_step[0],
+                                 compressed_elements_per_step=per_step[1])
+    calls_per, elems = results["smaq_eager"]["codec_calls_per_step"], \
+        results["smaq_eager"]["compressed_elements_per_step"]
+    g_ms = results["smaq_graph"]["ms_per_step"]
+    return {"metric": "Training step with SmaQ on every layer (activations + grad-maps), ms/step",
+            "value": g_ms, "unit": "ms/step", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": g_ms, "higher_is_better": False,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "vgg_cifar_b128_register_autograd_module",
+                       "codec_calls_per_step": calls_per,
+                       "compressed_elements_per_step": elems},
+            "variants": results}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="smaq",
-                    choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi", "packed"])
+                    choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi", "packed",
+                             "autograd"])
     ap.add_argument("--elements", type=int, default=0, help="override elements (smaq configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 22)
@@ -436,7 +537,7 @@ def main():
     world, rank, local = dist_setup()
     device = torch.device("cuda", local)
     runner = {"smaq": run_smaq, "smaq_sampled": run_smaq, "fp8": run_fp8, "s2fp8": run_s2fp8,
-              "multi": run_multi, "packed": run_packed}[args.config]
+              "multi": run_multi, "packed": run_packed, "autograd": run_autograd}[args.config]
     res = runner(args, world, rank, device)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and args.config.startswith("smaq"):

@@ -236,8 +236,8 @@ uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
 /* ---------------------------------------------------------------------------------------------
  * Packed SmaQ container (format version 1)
  *
- * stream = SmqPackedHeader (128 B) | directory: n_blocks x uint64 (word offset of each block in
- *          the data region) | data region (uint32 words)
+ * stream = SmqPackedHeader (128 B) | directory: n_blocks x uint64 (bits 0-37: word offset of the
+ *          block in the data region, 38-50: n_out, 51-63: n_esc) | data region (uint32 words)
  * block  = SMQ_PACK_BLOCK elements (the last one may be shorter); its words:
  *   w[0]                 n_out (bits 0-15) | n_esc (bits 16-31)
  *   w[1 .. 128]          outlier mask: bit (e % 32) of word e / 32 = element e is an outlier

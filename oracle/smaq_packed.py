@@ -130,6 +130,10 @@ def pack(x, mean, std, cfg: osmaq.SmaqConfig, uniforms: Optional[np.ndarray] = N
         off += words.size
         blocks.append(words)
     data = np.concatenate(blocks) if blocks else np.zeros(0, np.uint32)
+    # directory entry: word offset (38 bits) | n_out << 38 | n_esc << 51
+    counts = np.array([(int(w[0]) & 0xFFFF, int(w[0]) >> 16) for w in blocks], np.uint64).reshape(-1, 2)
+    offsets = (np.asarray(offsets, np.uint64) | (counts[:, 0] << np.uint64(38))
+               | (counts[:, 1] << np.uint64(51)))
     r_main, r_out = F32(cfg.range_normal), F32(cfg.range_outlier)
     total = HEADER_BYTES + 8 * nb + 4 * data.size
     hdr = _HDR.pack(MAGIC, VERSION, n, BLOCK, nb, bm, bo, _flags(all_positive, r_main, r_out),
@@ -157,6 +161,7 @@ def unpack(stream: np.ndarray) -> np.ndarray:
     n, nb = h["n"], h["n_blocks"]
     wm, wo = _widths(h["num_bits_main"], h["num_bits_outlier"])
     dirs = np.asarray(stream[HEADER_BYTES: HEADER_BYTES + 8 * nb], np.uint8).view(np.uint64)
+    dirs = dirs & np.uint64((1 << 38) - 1)  # word offsets (n_out / n_esc also live in w[0])
     data = np.asarray(stream[HEADER_BYTES + 8 * nb:], np.uint8).view(np.uint32)
     q = np.zeros(n, F32)
     hi = np.zeros(n, bool)

@@ -380,7 +380,14 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
     const int v = e ? atoi(e) : kStatsGridCap;
     return (v >= 64 && v <= kStatsGridCap) ? v : kStatsGridCap;
   }();
-  const int grid = grid_for(n, kBlock * 4, cap);
+  // >= 16K elements per workgroup: mid-size tensors (activations, 1-30M elements) are bound by
+  // the arrival of their workgroups, not by bandwidth; at 256M the cap decides (2048)
+  static const int per_wg = [] {  // measurement knob SMQ_STATS_PER_WG (elements, >= 1024)
+    const char* e = getenv("SMQ_STATS_PER_WG");
+    const int v = e ? atoi(e) : kBlock * 4 * 16;
+    return v >= kBlock * 4 ? v : kBlock * 4 * 16;
+  }();
+  const int grid = grid_for(n, per_wg, cap);
   FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n),
                    (unsigned long long*)p->offset_counter, n};
 #define SMQ_STATS(RANGE, TIN)                                                                    \

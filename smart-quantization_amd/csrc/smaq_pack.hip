@@ -56,6 +56,7 @@ struct PackArgs {
   uint32_t n_blocks;
   uint32_t flags;
   int place_atomic;          // measurement knob (SMQ_PACK_PLACE=atomic): see smq_smaq_compress
+  uint32_t stage_words;      // LDS stage (w[0], mask, code stream) for these widths; q values follow
   unsigned long long* cursor;
 };
 
@@ -172,7 +173,7 @@ __device__ __forceinline__ void or_bits(uint32_t* base, uint32_t pos, uint32_t c
 // chunk of at most 28 bits written by two LDS ORs.
 template <int RM, int TIN, bool SUB, bool VEC, bool FULL, int WM, int WO>
 __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c, uint32_t b,
-                                          uint32_t* stage) {
+                                          uint32_t* stage, float* qlds) {
   __shared__ uint32_t seg_cnt[2][16];
   __shared__ uint32_t seg_pre[2][17];
   __shared__ uint64_t s_prefix;
@@ -183,7 +184,9 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   const int n_el = FULL ? kPB : (int)(A.n - e0);
   uint32_t* codes_lds = stage + kHdrWords;
 
-  // 1. codes of this lane's 16 elements: local index el = 1024 k + 4 tid + i
+  // 1. codes of this lane's 16 elements: local index el = 1024 k + 4 tid + i. Every q also goes to
+  //    LDS (one 16-B store per float4): the escape list reads it back after the scan (re-deriving
+  //    it cost a reload + the element chain; keeping it in registers cost occupancy)
   uint32_t code[16];
   uint32_t om[4], xm[4];
 #pragma unroll
@@ -211,15 +214,18 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
     }
     om[k] = 0u;
     xm[k] = 0u;
+    float qk[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       bool hi, lo, esc;
       const float q = smaq_quant<RM, false, TIN, SUB>(v[i], u[i], c, hi, lo);
       const bool valid = FULL || el + i < n_el;
       code[4 * k + i] = valid ? classify(q, hi, lo, wm, wo, esc) : 0u;
+      qk[i] = q;
       om[k] |= (uint32_t)((hi | lo) && valid) << i;
       xm[k] |= (uint32_t)(esc && valid) << i;
     }
+    *reinterpret_cast<float4*>(qlds + el) = make_float4(qk[0], qk[1], qk[2], qk[3]);
   }
 
   // 2. outlier / escape ranks: per 256-element segment s = 4 k + wave, lane prefixes by ballots;
@@ -240,7 +246,7 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
       seg_cnt[1][4 * k + w] = tx;
     }
   }
-  const uint32_t code_cap = (uint32_t)(wo * kPB + 31) / 32u + 1u;
+  const uint32_t code_cap = A.stage_words - kHdrWords;
   for (uint32_t i = tid; i < code_cap; i += kBlock) codes_lds[i] = 0u;
   __syncthreads();
   if (tid < 2) {
@@ -290,7 +296,7 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   }
   __syncthreads();
 
-  // 4. the block image at its prefix, its escapes (q recomputed: rare) and directory entry
+  // 4. the block image at its prefix, its escapes and directory entry
   const uint64_t P = s_prefix;
   uint32_t* out = A.data + P;
   for (uint32_t i = tid; i < img_words; i += kBlock)
@@ -299,20 +305,18 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   for (int k = 0; k < 4; ++k) {
     if (!xm[k]) continue;
     const uint32_t base_x = seg_pre[1][4 * k + w] + pre_x[k];
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (!((xm[k] >> i) & 1u)) continue;
-      const uint32_t el = 1024u * k + 4u * tid + i;
-      const float uf =
-          RM == kRoundHash ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)(e0 + el)) : 0.f;
-      bool hi, lo;
-      const float q = smaq_quant<RM, false, TIN, SUB>(load1<TIN>(A.x, e0 + el), uf, c, hi, lo);
       const uint32_t r = base_x + __popc(xm[k] & ((1u << i) - 1u));
-      out[img_words + 2 * r] = el;
-      out[img_words + 2 * r + 1] = __float_as_uint(q);
+      out[img_words + 2 * r] = 1024u * k + 4u * tid + i;
+      out[img_words + 2 * r + 1] = __float_as_uint(qlds[1024u * k + 4u * tid + i]);
     }
   }
   if (tid == 0) {
-    A.dir[b] = P;
+    // directory entry: word offset (38 bits) | n_out << 38 | n_esc << 51 (decoder: no dependent
+    // load of w[0] before the block image)
+    A.dir[b] = P | ((uint64_t)n_out << 38) | ((uint64_t)n_esc << 51);
     if (!A.place_atomic && b == A.n_blocks - 1) {
       A.hdr->data_words = P + size;
       A.hdr->total_bytes = sizeof(SmqPackedHeader) + 8ull * A.n_blocks + 4ull * (P + size);
@@ -340,7 +344,9 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
 
 template <int RM, int TIN, bool VEC>
 __global__ __launch_bounds__(kBlock) void smaq_pack_kernel(PackArgs A) {
-  __shared__ uint32_t stage[kStageWords];
+  extern __shared__ uint32_t pack_lds[];  // [stage_words] stage, then [kPB] q values
+  uint32_t* stage = pack_lds;
+  float* qlds = reinterpret_cast<float*>(pack_lds + A.stage_words);
   __shared__ uint32_t s_b;
   if (threadIdx.x == 0) {
     const uint32_t id = atomicAdd(A.counter, 1u);  // block ids in start order
@@ -356,8 +362,8 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_kernel(PackArgs A) {
   const bool w57 = A.wm == 5 && A.wo == 7;  // the default 6/8-bit budget, widths compiled in
 #define SMQ_PACK_BODY(SUBV, FULLV)                                          \
   do {                                                                      \
-    if (w57) pack_body<RM, TIN, SUBV, VEC, FULLV, 5, 7>(A, c, b, stage);   \
-    else pack_body<RM, TIN, SUBV, VEC, FULLV, 0, 0>(A, c, b, stage);       \
+    if (w57) pack_body<RM, TIN, SUBV, VEC, FULLV, 5, 7>(A, c, b, stage, qlds);   \
+    else pack_body<RM, TIN, SUBV, VEC, FULLV, 0, 0>(A, c, b, stage, qlds);       \
   } while (0)
   if (A.stats->quot_check) {
     if (full) SMQ_PACK_BODY(true, true); else SMQ_PACK_BODY(true, false);
@@ -385,13 +391,14 @@ struct UnpackArgs {
   int vec;
 };
 
-__device__ __forceinline__ float find_escape(const uint32_t* esc, uint32_t n_esc, uint32_t el) {
-  uint32_t lo = 0, hi = n_esc;  // entries sorted by element index
-  while (hi - lo > 1) {
+// Escapes before element el of a block: the list is sorted by element index (lower bound).
+__device__ __forceinline__ uint32_t escapes_below(const uint32_t* esc, uint32_t n_esc, uint32_t el) {
+  uint32_t lo = 0, hi = n_esc;
+  while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (esc[2 * mid] <= el) lo = mid; else hi = mid;
+    if (esc[2 * mid] < el) lo = mid + 1; else hi = mid;
   }
-  return __uint_as_float(esc[2 * lo + 1]);
+  return lo;
 }
 
 // Decode one code (width wm main / wo outlier) to q and the outlier sides.
@@ -410,28 +417,35 @@ template <bool AP, bool SQ, bool FULL, int WM, int WO>
 __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
                                             int wm_rt, int wo_rt, uint32_t* stage) {
   __shared__ uint32_t pc[kMaskWords];
+  __shared__ uint32_t epc[kMaskWords];
   __shared__ uint32_t esc_mask[kMaskWords];
   constexpr bool kWindow = WO > 0 && WO <= 8;  // a lane's 4 codes fit one 32-bit window
   const int wm = WM > 0 ? WM : wm_rt, wo = WO > 0 ? WO : wo_rt;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
-  const uint32_t* blk = A.data + A.dir[b];
-  const uint32_t w0 = blk[0];
-  const uint32_t n_out = w0 & 0xffffu, n_esc = w0 >> 16;
+  const uint64_t dent = A.dir[b];  // offset | n_out << 38 | n_esc << 51
+  const uint32_t* blk = A.data + (dent & ((1ull << 38) - 1ull));
+  const uint32_t n_out = (uint32_t)(dent >> 38) & 0x1fffu, n_esc = (uint32_t)(dent >> 51);
   const uint32_t code_words = ((uint32_t)wm * (uint32_t)n_el + (uint32_t)(wo - wm) * n_out + 31u) / 32u;
   const uint32_t img_words = kHdrWords + code_words;
-  for (uint32_t i = tid; i < img_words; i += kBlock) stage[i] = blk[i];
+  // the image and (when they fit) the escape list in one coalesced copy
+  const bool esc_lds = img_words + 2u * n_esc <= (uint32_t)kStageWords;
+  const uint32_t copy_words = esc_lds ? img_words + 2u * n_esc : img_words;
+  for (uint32_t i = tid; i < copy_words; i += kBlock) stage[i] = blk[i];
   if (tid < kMaskWords) esc_mask[tid] = 0u;
   __syncthreads();
-  if (tid < kWave) {  // exclusive popcount prefix of the 128 mask words
+  const uint32_t* esc = esc_lds ? stage + img_words : blk + img_words;
+  if (tid < kWave) {  // wave 0: exclusive popcount prefix of the 128 outlier-mask words
     const uint32_t a = __popc(stage[1 + 2 * lane]), bb = __popc(stage[2 + 2 * lane]);
     uint32_t tot;
     const uint32_t ex = wave_prefix_small<7>(a + bb, tot);
     pc[2 * lane] = ex;
     pc[2 * lane + 1] = ex + a;
+  } else if (tid < kWave + kMaskWords) {  // waves 1-2: escapes before each mask word
+    const uint32_t wi = (uint32_t)tid - kWave;
+    epc[wi] = n_esc ? escapes_below(esc, n_esc, 32u * wi) : 0u;
   }
-  const uint32_t* esc = blk + img_words;
   for (uint32_t i = tid; i < n_esc; i += kBlock) {
     const uint32_t el = esc[2 * i];
     atomicOr(esc_mask + (el >> 5), 1u << (el & 31));
@@ -443,6 +457,7 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
     const int el0 = 1024 * k + 4 * tid;
     if (!FULL && el0 >= n_el) break;
     const uint32_t mw = stage[1 + (el0 >> 5)], em = esc_mask[el0 >> 5];
+    const uint32_t ebase = epc[el0 >> 5];
     const uint32_t sh0 = (uint32_t)el0 & 31u;
     const uint32_t r0 = pc[el0 >> 5] + __popc(mw & ((1u << sh0) - 1u));
     const uint32_t nib = (mw >> sh0) & 15u, enib = (em >> sh0) & 15u;
@@ -465,7 +480,10 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
       off += is_o ? (uint32_t)wo : (uint32_t)wm;
       bool hi, lo;
       float q = decode_code(v, is_o, wm, wo, hi, lo);
-      if (__builtin_expect((enib >> i) & 1u, 0)) q = find_escape(esc, n_esc, (uint32_t)(el0 + i));
+      if (__builtin_expect((enib >> i) & 1u, 0)) {  // rank among the block's escapes: O(1)
+        const uint32_t sh = (uint32_t)(el0 + i) & 31u;
+        q = __uint_as_float(esc[2u * (ebase + __popc(em & ((1u << sh) - 1u))) + 1u]);
+      }
       o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
     }
     float* y = A.y + e0 + el0;
@@ -629,6 +647,10 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
   A.wo = A.bo - 1;
   A.n_blocks = (uint32_t)nb;
   A.flags = (p->all_positive ? 1u : 0u) | (R.safe_q ? 2u : 0u);
+  // stage: w[0] + mask + the code stream at its widest (every element an outlier) + 1 word of
+  // slack for the two-word ORs, rounded to 4 words so the q values after it are 16-B aligned
+  A.stage_words = (uint32_t)(kHdrWords + (A.wo * kPB + 31) / 32 + 1 + 3) & ~3u;
+  const size_t lds_bytes = 4 * ((size_t)A.stage_words + kPB);
   if (hipMemsetAsync(A.status, 0, 8 * ((size_t)nb + ng) + 64, st) != hipSuccess ||
       hipMemsetAsync(A.hdr, 0, sizeof(SmqPackedHeader), st) != hipSuccess) {
     set_error("compress: hipMemsetAsync failed");
@@ -640,10 +662,10 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
   do {                                                                                         \
     if (vec)                                                                                   \
       hipLaunchKernelGGL((smaq_pack_kernel<RMV, TINV, true>), dim3((unsigned)nb), dim3(kBlock), \
-                         0, st, A);                                                            \
+                         lds_bytes, st, A);                                                    \
     else                                                                                       \
       hipLaunchKernelGGL((smaq_pack_kernel<RMV, TINV, false>), dim3((unsigned)nb),             \
-                         dim3(kBlock), 0, st, A);                                              \
+                         dim3(kBlock), lds_bytes, st, A);                                      \
   } while (0)
 #define SMQ_PACK_T(TINV)                                  \
   do {                                                    \

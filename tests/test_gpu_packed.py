@@ -174,10 +174,13 @@ def test_large_multiblock_lookback():
     h = P.header(raw)
     nb = h["n_blocks"]
     assert nb == n // 4096 and h["error"] == 0 and h["total_bytes"] == raw.size
-    dirs = raw[128: 128 + 8 * nb].view(np.uint64).astype(np.int64)
+    dent = raw[128: 128 + 8 * nb].view(np.uint64)
+    dirs = (dent & np.uint64((1 << 38) - 1)).astype(np.int64)
     data = raw[128 + 8 * nb:].view(np.uint32)
     w0 = data[dirs]
     n_out, n_esc = (w0 & 0xFFFF).astype(np.int64), (w0 >> 16).astype(np.int64)
+    assert np.array_equal((dent >> np.uint64(38)) & np.uint64(0x1FFF), n_out.astype(np.uint64))
+    assert np.array_equal(dent >> np.uint64(51), n_esc.astype(np.uint64))
     size = 129 + (5 * 4096 + 2 * n_out + 31) // 32 + 2 * n_esc
     assert dirs[0] == 0 and np.array_equal(np.diff(dirs), size[:-1])
     assert dirs[-1] + size[-1] == h["data_words"]
