@@ -189,19 +189,26 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   //    it cost a reload + the element chain; keeping it in registers cost occupancy)
   uint32_t code[16];
   uint32_t om[4], xm[4];
+  // all four 16-B loads of the lane in flight before any element is processed
+  float xv[4][4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int el = 1024 * k + 4 * tid;
-    float v[4] = {0.f, 0.f, 0.f, 0.f}, u[4] = {0.f, 0.f, 0.f, 0.f};
-    const bool full4 = FULL || el + 3 < n_el;
-    if (VEC && full4) {
+    if (VEC && (FULL || el + 3 < n_el)) {
       const float4 t = load4<TIN>(A.x, (e0 + el) >> 2);
-      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+      xv[k][0] = t.x; xv[k][1] = t.y; xv[k][2] = t.z; xv[k][3] = t.w;
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (FULL || el + i < n_el) v[i] = load1<TIN>(A.x, e0 + el + i);
+        xv[k][i] = (FULL || el + i < n_el) ? load1<TIN>(A.x, e0 + el + i) : 0.f;
     }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int el = 1024 * k + 4 * tid;
+    float u[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* v = xv[k];
+    const bool full4 = FULL || el + 3 < n_el;
     if (RM == kRoundHash) {
       const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
       if (full4) {
