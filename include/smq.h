@@ -22,6 +22,7 @@
  *                           qtorch 0.2.0 float_quantize it calls (quantization.py:3) —
  *                           used by compress/fp8.py:31, fp16.py:31, bf16.py:31
  *   smq_s2fp8_roundtrip_f32 smart_compress/compress/s2fp8.py:27-48
+ *   smq_s2fp8_roundtrip     the same with quantization.py:187-204's precision-16 branch
  *   smq_smaq_compress /     the packed SmaQ container: the codes smart.py:154-169
  *   smq_smaq_decompress     computes, stored in the [outlier flag][sign][N-2 magnitude] layout
  *                           of README.md:25-28 (6 bits per main element, 8 per outlier by
@@ -228,6 +229,16 @@ int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
                             const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
                             const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
                             void* stream);
+
+/* S2FP8 for an input of element type `dtype` (SMQ_DTYPE_*) at Lightning precision 16 or 32.
+ * precision 32 needs fp32 input (identical to smq_s2fp8_roundtrip_f32). precision 16 follows the
+ * reference's dtypes: statistics and |x|^alpha * 2^beta in the input type, float_quantize returns
+ * half (quantization.py:201-202), the inverse power runs in half; y is fp16 for fp16 inputs and
+ * fp32 for fp32 / bf16 inputs (torch promotion of `... * signs`, s2fp8.py:48). The SmqS2fp8Stats
+ * fields hold the input-type values (exact in fp32). */
+int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precision,
+                        int check_inf, const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
+                        const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- host reference helpers shared with the oracle (pure functions, no GPU) ---- */
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);

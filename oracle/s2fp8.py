@@ -49,3 +49,69 @@ def roundtrip(x, rand_bits, check_inf_flag=True, st=None):
     Y = transform(x, st)
     T = qf.float_quantize(Y, 5, 2, rand_bits, check_inf_flag)
     return inverse(T, x, st), st, Y, T
+
+
+# ---- precision 16 (Lightning half training) --------------------------------------------------------
+# s2fp8.py:27-48 with quantization.py:187-204's `is_16_bit` branch, op for op in the dtypes torch
+# (CPU, 2.10) uses. P = the input's type ('f32' | 'f16' | 'bf16'):
+#   * statistics and forward transform in P: every op is its fp32 value rounded to P (torch CPU
+#     computes reduced-precision ops in fp32 and rounds once; the mean rounds its fp32 quotient);
+#   * float_quantize quantises Y.float() and returns .half() (E5M2 values are exact in half);
+#   * `truncated * beta_pow2.reciprocal_()`: half tensor times a 0-dim P scalar -> half, computed
+#     from the UNROUNDED scalar (torch's opmath path for CPU scalars);
+#   * `** alpha.reciprocal_()`: the exponent is rounded to half first, the power rounded to half;
+#   * `* signs`: half * P -> half for P = f16, fp32 otherwise (type promotion of two tensors).
+# Pinned by tests/golden/s2p16_*.npz (make_golden.py gen_s2fp8_p16). The CUDA reference may differ
+# in the scalar corner above (a GPU 0-dim tensor is cast to half); not measurable here.
+
+def _r(v, dt):
+    from .smaq import round_to
+
+    return round_to(v, dt)
+
+
+def stats_p16(x, dt: str):
+    a = np.abs(np.asarray(x, dtype=F32))
+    with np.errstate(all="ignore"):
+        lg = _r(np.where(a == F32(0), a, np.log2(a)).astype(F32), dt)
+    mu = _r(F32(np.mean(lg.astype(np.float64))), dt)
+    m = F32(np.max(lg))
+    return derive_p16(mu, m, dt)
+
+
+def derive_p16(mu, m, dt: str):
+    mu, m = F32(mu), F32(m)
+    with np.errstate(all="ignore"):
+        t = _r(m - mu, dt)
+        alpha = _r(_r(F32(1) / t, dt) * F32(15.0), dt)  # reciprocal() * 15.0, both in P
+        beta = _r((-alpha) * mu, dt)
+        bp2 = _r(F32(np.exp2(np.float64(beta))), dt)
+        return dict(mu=mu, m=m, alpha=alpha, beta=beta, beta_pow2=bp2,
+                    inv_beta_pow2=_r(F32(1) / bp2, dt), inv_alpha=_r(F32(1) / alpha, dt))
+
+
+def transform_p16(x, st, dt: str):
+    a = np.abs(np.asarray(x, dtype=F32))
+    with np.errstate(all="ignore"):
+        Y = _r(np.power(a.astype(np.float64), np.float64(st["alpha"])).astype(F32), dt)
+        return _r(Y * st["beta_pow2"], dt)
+
+
+def inverse_p16(T, x, st, dt: str):
+    """-> output values (float32 array) and the output type ('f16' for f16 inputs, else 'f32')."""
+    x = np.asarray(x, dtype=F32)
+    sgn = np.where(x > 0, F32(1), np.where(x < 0, F32(-1), F32(0))).astype(F32)
+    th = _r(np.asarray(T, dtype=F32), "f16")  # .half(): exact for E5M2 values, inf, NaN
+    ia = _r(st["inv_alpha"], "f16")
+    with np.errstate(all="ignore"):
+        t1 = _r(th * st["inv_beta_pow2"], "f16")
+        t2 = _r(np.power(t1.astype(np.float64), np.float64(ia)).astype(F32), "f16")
+        return (t2 * sgn).astype(F32), ("f16" if dt == "f16" else "f32")
+
+
+def roundtrip_p16(x, dt: str, rand_bits, check_inf_flag=True, st=None):
+    st = stats_p16(x, dt) if st is None else st
+    Y = transform_p16(x, st, dt)
+    T = qf.float_quantize(Y, 5, 2, rand_bits, check_inf_flag)
+    y, out_dt = inverse_p16(T, x, st, dt)
+    return y, out_dt, st, Y, T

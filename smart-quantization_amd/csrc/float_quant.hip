@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "smaq_elem.h"
 #include "smq_common.h"
 
 namespace smq {
@@ -162,31 +163,55 @@ __device__ __forceinline__ float nan_max(float a, float b) {
   return (b > a || b != b) ? b : a;  // torch.max propagates NaN
 }
 
-__device__ __forceinline__ float s2_log(float x) {
-  const float a = fabsf(x);
-  return (a == 0.0f) ? a : log2f(a);  // torch.where(X_abs == 0.0, X_abs, torch.log2(X_abs))
+// Rounding of one S2FP8 op to its torch dtype. fp16 goes through an opaque v_cvt_f16_f32: left to
+// itself the compiler fuses `fptrunc(a * b)` into v_fma_mixlo_f16(a, b, +0), which rounds the exact
+// product once (torch rounds to fp32 first, then to half) and turns a -0 product into +0.
+template <int T>
+__device__ __forceinline__ float s2_round(float v) {
+  if (T == kF16) {
+    uint32_t h;
+    asm volatile("v_cvt_f16_f32 %0, %1" : "=v"(h) : "v"(v));
+    return __half2float(__builtin_bit_cast(__half, (uint16_t)(h & 0xffffu)));
+  }
+  return round_in<T>(v);
 }
 
-__device__ void s2fp8_finalize(double s, float m, int64_t n, SmqS2fp8Stats* out) {
-  const float mu = (float)(s / (double)n);  // torch.mean(X_abs_log2)
+template <int TIN>
+__device__ __forceinline__ float s2_log(float x) {
+  const float a = fabsf(x);
+  return (a == 0.0f) ? a : s2_round<TIN>(log2f(a));  // torch.where(X_abs == 0.0, X_abs, torch.log2(X_abs))
+}
+
+// s2fp8.py:31-43 from (sum, max) of the log2 values. TIN = the input type: the reference's torch
+// ops run in it (precision 16 with fp16/bf16 tensors), each op = its fp32 value rounded to TIN
+// (round_in, the identity for fp32); torch rounds the mean's fp32 quotient once.
+template <int TIN>
+__device__ void s2fp8_derive(float mu, float m, uint32_t n_used, SmqS2fp8Stats* out) {
   // s2fp8.py:42 `15.0 / (m - mu)`: Python scalar / tensor is Tensor.__rtruediv__ =
-  // reciprocal() * 15.0 — two fp32 roundings, not one division.
-  const float alpha = (1.0f / (m - mu)) * 15.0f;
-  const float beta = (-alpha) * mu;         // s2fp8.py:43
-  const float bp2 = (float)exp2((double)beta);  // 2.0 ** beta, correctly rounded
+  // reciprocal() * 15.0 — two roundings, not one division.
+  const float alpha = s2_round<TIN>(s2_round<TIN>(1.0f / s2_round<TIN>(m - mu)) * 15.0f);
+  const float beta = s2_round<TIN>((-alpha) * mu);                   // s2fp8.py:43
+  const float bp2 = s2_round<TIN>((float)exp2((double)beta));        // 2.0 ** beta, correctly rounded
   out->mu = mu;
   out->m = m;
   out->alpha = alpha;
   out->beta = beta;
   out->beta_pow2 = bp2;
-  out->inv_beta_pow2 = 1.0f / bp2;  // beta_pow2.reciprocal_()
-  out->inv_alpha = 1.0f / alpha;    // alpha.reciprocal_()
-  out->n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
+  out->inv_beta_pow2 = s2_round<TIN>(1.0f / bp2);  // beta_pow2.reciprocal_()
+  out->inv_alpha = s2_round<TIN>(1.0f / alpha);    // alpha.reciprocal_()
+  out->n_used = n_used;
+}
+
+template <int TIN>
+__device__ void s2fp8_finalize(double s, float m, int64_t n, SmqS2fp8Stats* out) {
+  const float mu = s2_round<TIN>((float)(s / (double)n));  // torch.mean(X_abs_log2)
+  s2fp8_derive<TIN>(mu, m, (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n), out);
 }
 
 constexpr int kS2GridCap = 1024;  // one sweep front, <= 1024 partials (smaq.hip)
 
-__global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const float* __restrict__ x, int64_t n,
+template <int TIN>
+__global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const void* __restrict__ x, int64_t n,
                                                              int vec, S2Partial* partials,
                                                              uint32_t* counter,
                                                              SmqS2fp8Stats* out) {
@@ -198,32 +223,32 @@ __global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const float* __rest
   double s = 0.0;
   float m = -INFINITY;
   if (vec) {
-    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
     const int64_t nv = n >> 2;
     for (int64_t t0 = (int64_t)blockIdx.x * (kBlock * 4); t0 < nv; t0 += (int64_t)gridDim.x * kBlock * 4) {
       float4 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t j = t0 + threadIdx.x + u * kBlock;
-        v[u] = j < nv ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[u] = j < nv ? load4<TIN>(x, j) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t j = t0 + threadIdx.x + u * kBlock;
         if (j >= nv) continue;
-        const float l0 = s2_log(v[u].x), l1 = s2_log(v[u].y), l2 = s2_log(v[u].z), l3 = s2_log(v[u].w);
+        const float l0 = s2_log<TIN>(v[u].x), l1 = s2_log<TIN>(v[u].y), l2 = s2_log<TIN>(v[u].z),
+                    l3 = s2_log<TIN>(v[u].w);
         s += ((double)l0 + (double)l1) + ((double)l2 + (double)l3);
         m = nan_max(nan_max(m, l0), nan_max(l1, nan_max(l2, l3)));
       }
     }
     if (blockIdx.x == 0 && threadIdx.x < (int)(n & 3)) {
-      const float l = s2_log(x[(nv << 2) + threadIdx.x]);
+      const float l = s2_log<TIN>(load1<TIN>(x, (nv << 2) + threadIdx.x));
       s += (double)l;
       m = nan_max(m, l);
     }
   } else {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-      const float l = s2_log(x[i]);
+      const float l = s2_log<TIN>(load1<TIN>(x, i));
       s += (double)l;
       m = nan_max(m, l);
     }
@@ -279,32 +304,20 @@ __global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const float* __rest
   if (threadIdx.x == 0) {
     const double S = (shs[0] + shs[1]) + (shs[2] + shs[3]);
     const float M = nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3]));
-    s2fp8_finalize(S, M, n, out);
+    s2fp8_finalize<TIN>(S, M, n, out);
     *counter = 0u;
   }
 }
 
 // Injected (mu, m): derive the rest exactly like the finaliser (parity tests).
+template <int TIN>
 __global__ void s2fp8_derive_kernel(const SmqS2fp8Stats* in, SmqS2fp8Stats* out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    const float mu = in->mu, m = in->m;
-    const float alpha = (1.0f / (m - mu)) * 15.0f;  // see s2fp8_finalize
-    const float beta = (-alpha) * mu;
-    const float bp2 = (float)exp2((double)beta);
-    out->mu = mu;
-    out->m = m;
-    out->alpha = alpha;
-    out->beta = beta;
-    out->beta_pow2 = bp2;
-    out->inv_beta_pow2 = 1.0f / bp2;
-    out->inv_alpha = 1.0f / alpha;
-    out->n_used = in->n_used;
-  }
+  if (threadIdx.x == 0 && blockIdx.x == 0) s2fp8_derive<TIN>(in->mu, in->m, in->n_used, out);
 }
 
 struct S2Args {
-  const float* x;
-  float* y;
+  const void* x;
+  void* y;
   int64_t n;
   const uint32_t* rand_bits;
   const SmqS2fp8Stats* st;
@@ -338,30 +351,83 @@ __device__ __forceinline__ float s2fp8_elem(float xv, uint32_t r, float alpha, f
   return t2 * sgn;                                        // * signs
 }
 
-template <bool RARR, bool VEC, int kFqTileV>
+// The same at precision 16 (quantization.py:190-202: float_quantize quantises Y.float() and returns
+// .half()). Forward transform in the input type TIN (fp32 keeps the fast power; fp16/bf16 use
+// ocml powf before rounding to TIN, so the rounding sees an accurate power). Inverse in half:
+// `truncated * beta_pow2.reciprocal_()` multiplies by the UNROUNDED TIN scalar (torch's opmath path
+// for 0-dim operands), `** alpha.reciprocal_()` uses the exponent rounded to half (ialpha_h);
+// each result rounds to half. E5M2 values (and inf/NaN) are exact in half, so T needs no rounding.
+template <int TIN, bool FAST>
+__device__ __forceinline__ float s2fp8_elem16(float xv, uint32_t r, float alpha, float bp2,
+                                              float ibp2, float ialpha_h, int check_inf,
+                                              float max_value) {
+  const float sgn = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
+  const float a = fabsf(xv);
+  float Y = (FAST && TIN == kF32) ? pow_pos(a, alpha) : powf(a, alpha);
+  Y = s2_round<TIN>(s2_round<TIN>(Y) * bp2);
+  float T = qtorch_quant(Y, r, 5, 2, true);
+  if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
+  const float t1 = s2_round<kF16>(T * ibp2);
+  const float t2 = s2_round<kF16>(powf(t1, ialpha_h));
+  // `* signs` (fp16 output for fp16 inputs, fp32 otherwise). t2 is >= +0 or NaN, so the product is
+  // a sign flip — written as one: `fptrunc(t2 * sgn)` is otherwise emitted as v_fma_mixlo_f16 with
+  // a +0 addend, which turns -1 * +0 = -0 into +0 (measured on gfx950).
+  (void)sgn;
+  if (xv > 0.0f) return t2;
+  if (xv < 0.0f) return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, t2) ^ 0x80000000u);
+  return t2 * 0.0f;  // sign(+-0) = sign(NaN) = +0
+}
+
+// output element type: fp16 for fp16 inputs at precision 16, fp32 otherwise
+template <int TIN, bool P16>
+constexpr bool s2_half_out() { return P16 && TIN == kF16; }
+
+template <bool HOUT>
+__device__ __forceinline__ void s2_store4(void* y, int64_t j, float4 o) {
+  if (!HOUT) {
+    store_nt(static_cast<float4*>(y) + j, o);
+  } else {
+    const uint32_t lo = (uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.x)) |
+                        ((uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.y)) << 16);
+    const uint32_t hi = (uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.z)) |
+                        ((uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.w)) << 16);
+    static_cast<uint2*>(y)[j] = make_uint2(lo, hi);
+  }
+}
+
+template <bool HOUT>
+__device__ __forceinline__ void s2_store1(void* y, int64_t e, float v) {
+  if (!HOUT) static_cast<float*>(y)[e] = v;
+  else static_cast<__half*>(y)[e] = __float2half_rn(v);
+}
+
+template <bool RARR, bool VEC, int kFqTileV, int TIN, bool P16>
 __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   constexpr int kFqTileElems = kBlock * kFqTileV * 4;
+  constexpr bool HOUT = s2_half_out<TIN, P16>();
   const float alpha = A.st->alpha, bp2 = A.st->beta_pow2, ibp2 = A.st->inv_beta_pow2,
               ialpha = A.st->inv_alpha;
+  const float ialpha_e = P16 ? s2_round<kF16>(ialpha) : ialpha;
   const int64_t n = A.n;
   auto rb = [&](int64_t e) -> uint32_t {
     return RARR ? A.rand_bits[e] : rng_u32(A.key, A.offset + (uint64_t)e);
   };
   const bool fast = alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f && ialpha < INFINITY;
   auto q1 = [&](float v, uint32_t r) {
+    if (P16)
+      return fast ? s2fp8_elem16<TIN, true>(v, r, alpha, bp2, ibp2, ialpha_e, A.check_inf, A.max_value)
+                  : s2fp8_elem16<TIN, false>(v, r, alpha, bp2, ibp2, ialpha_e, A.check_inf, A.max_value);
     return fast ? s2fp8_elem<true>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value)
                 : s2fp8_elem<false>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
   };
   if (VEC) {
-    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
-    float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
     const int64_t nv = n >> 2;
     const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kFqTileV) + threadIdx.x;
     float4 v[kFqTileV];
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
       const int64_t j = t0 + u * kBlock;
-      if (j < nv) v[u] = x4[j];
+      if (j < nv) v[u] = load4<TIN>(A.x, j);
     }
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
@@ -372,18 +438,18 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
       o.y = q1(v[u].y, rb(4 * j + 1));
       o.z = q1(v[u].z, rb(4 * j + 2));
       o.w = q1(v[u].w, rb(4 * j + 3));
-      store_nt(y4 + j, o);
+      s2_store4<HOUT>(A.y, j, o);
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
       const int64_t e = (nv << 2) + threadIdx.x;
-      A.y[e] = q1(A.x[e], rb(e));
+      s2_store1<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
     }
   } else {
     const int64_t e0 = (int64_t)blockIdx.x * kFqTileElems + threadIdx.x;
     for (int k = 0; k < kFqTileElems / kBlock; ++k) {
       const int64_t e = e0 + (int64_t)k * kBlock;
       if (e >= n) break;
-      A.y[e] = q1(A.x[e], rb(e));
+      s2_store1<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
     }
   }
 }
@@ -491,12 +557,24 @@ size_t smq_s2fp8_workspace_bytes(int64_t n) {
   return s2_ws_bytes();
 }
 
-int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
-                            const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
-                            const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
-                            void* stream) {
+int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precision,
+                        int check_inf, const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
+                        const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes, void* stream) {
   if (n < 1 || !x || !y) {
     set_error("s2fp8: n >= 1 and non-NULL x, y required");
+    return SMQ_ERR_INVALID;
+  }
+  if (dtype != SMQ_DTYPE_F32 && dtype != SMQ_DTYPE_F16 && dtype != SMQ_DTYPE_BF16) {
+    set_error("s2fp8: dtype must be SMQ_DTYPE_F32, _F16 or _BF16 (got %d)", dtype);
+    return SMQ_ERR_INVALID;
+  }
+  if (precision != 16 && precision != 32) {
+    set_error("s2fp8: precision must be 16 or 32 (got %d)", precision);
+    return SMQ_ERR_INVALID;
+  }
+  if (precision == 32 && dtype != SMQ_DTYPE_F32) {
+    // quantization.py:193 hands the tensor to qtorch's float_quantize as is; its kernels take fp32
+    set_error("s2fp8: precision 32 quantises the tensor as is and needs fp32 input");
     return SMQ_ERR_INVALID;
   }
   if (!ws || ws_bytes < s2_ws_bytes()) {
@@ -508,12 +586,21 @@ int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
   SmqS2fp8Stats* hdr = (SmqS2fp8Stats*)base;
   uint32_t* counter = (uint32_t*)(base + 64);
   S2Partial* partials = (S2Partial*)(base + 128);
+  const uintptr_t align = dtype == SMQ_DTYPE_F32 ? 15u : 7u;  // one 4-element group per lane
+  const bool xal = ((uintptr_t)x & align) == 0;
   if (stats_in) {
-    hipLaunchKernelGGL(s2fp8_derive_kernel, dim3(1), dim3(64), 0, st, stats_in, hdr);
+    if (dtype == SMQ_DTYPE_F32) hipLaunchKernelGGL(s2fp8_derive_kernel<kF32>, dim3(1), dim3(64), 0, st, stats_in, hdr);
+    else if (dtype == SMQ_DTYPE_F16) hipLaunchKernelGGL(s2fp8_derive_kernel<kF16>, dim3(1), dim3(64), 0, st, stats_in, hdr);
+    else hipLaunchKernelGGL(s2fp8_derive_kernel<kBF16>, dim3(1), dim3(64), 0, st, stats_in, hdr);
   } else {
     const int grid = s2_stats_grid(n);
-    hipLaunchKernelGGL(s2fp8_stats_kernel, dim3(grid), dim3(kBlock), 0, st, x, n,
-                       aligned16f(x) ? 1 : 0, partials, counter, hdr);
+    const int vec = xal ? 1 : 0;
+    if (dtype == SMQ_DTYPE_F32)
+      hipLaunchKernelGGL(s2fp8_stats_kernel<kF32>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr);
+    else if (dtype == SMQ_DTYPE_F16)
+      hipLaunchKernelGGL(s2fp8_stats_kernel<kF16>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr);
+    else
+      hipLaunchKernelGGL(s2fp8_stats_kernel<kBF16>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr);
   }
   int rc = check_launch("s2fp8_stats_kernel");
   if (rc) return rc;
@@ -528,22 +615,48 @@ int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
   A.check_inf = check_inf;
   A.max_value = host_max_value(5, 2);
   const bool rarr = rand_bits != nullptr;
-  const bool vec = aligned16f(x) && aligned16f(y);
+  const bool half_out = precision == 16 && dtype == SMQ_DTYPE_F16;
+  const bool vec = xal && ((uintptr_t)y & (half_out ? 7u : 15u)) == 0;
   const int grid = fq_grid(n);
   const int tv = fq_tile_v();
+  if (precision == 32) {
 #define SMQ_S2(R, V)                                                                             \
   do {                                                                                           \
-    if (tv == 1) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 1>), dim3(grid), dim3(kBlock), 0, st, A); \
-    else if (tv == 2) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 2>), dim3(grid), dim3(kBlock), 0, st, A); \
-    else hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 4>), dim3(grid), dim3(kBlock), 0, st, A); \
+    if (tv == 1) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 1, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
+    else if (tv == 2) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 2, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
+    else hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 4, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
   } while (0)
-  if (rarr) {
-    if (vec) SMQ_S2(true, true); else SMQ_S2(true, false);
-  } else {
-    if (vec) SMQ_S2(false, true); else SMQ_S2(false, false);
-  }
+    if (rarr) {
+      if (vec) SMQ_S2(true, true); else SMQ_S2(true, false);
+    } else {
+      if (vec) SMQ_S2(false, true); else SMQ_S2(false, false);
+    }
 #undef SMQ_S2
+  } else {
+    // precision 16: the tile knob is not swept here (fq_grid's tile must match kFqDefaultTileV)
+    const int g16 = (int)((n + (int64_t)kBlock * 4 * kFqDefaultTileV - 1) / ((int64_t)kBlock * 4 * kFqDefaultTileV));
+#define SMQ_S2H(T, R, V) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, kFqDefaultTileV, T, true>), dim3(g16), dim3(kBlock), 0, st, A)
+#define SMQ_S2T(T)                                               \
+  do {                                                           \
+    if (rarr) { if (vec) SMQ_S2H(T, true, true); else SMQ_S2H(T, true, false); } \
+    else { if (vec) SMQ_S2H(T, false, true); else SMQ_S2H(T, false, false); }    \
+  } while (0)
+    if (dtype == SMQ_DTYPE_F32) SMQ_S2T(kF32);
+    else if (dtype == SMQ_DTYPE_F16) SMQ_S2T(kF16);
+    else SMQ_S2T(kBF16);
+#undef SMQ_S2T
+#undef SMQ_S2H
+  }
+  (void)grid;
   return check_launch("s2fp8_apply_kernel");
+}
+
+int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
+                            const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
+                            const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
+                            void* stream) {
+  return smq_s2fp8_roundtrip(x, SMQ_DTYPE_F32, y, n, 32, check_inf, rand_bits, seed, offset,
+                             stats_in, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

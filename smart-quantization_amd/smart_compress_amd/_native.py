@@ -183,6 +183,10 @@ SIGNATURES = {
         _I32,
         [_P, _P, _I64, _I32, _P, _U64, _U64, _P, _P, _SZ, _P],
     ),
+    "smq_s2fp8_roundtrip": (
+        _I32,
+        [_P, _I32, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _SZ, _P],
+    ),
     "smq_rng_u32": (ctypes.c_uint32, [_U64, _U64]),
     "smq_smaq_pack_bound": (_SZ, [_I64, _I32, _I32]),
     "smq_smaq_pack_workspace_bytes": (_SZ, [_I64]),

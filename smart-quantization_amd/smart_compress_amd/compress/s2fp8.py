@@ -5,8 +5,13 @@ alpha = 15 / (m - mu), beta = -alpha * mu; Y = |x|^alpha * 2^beta; T = E5M2 stoc
 float_quantize(Y) (+ check_inf); y = (T * 2^-beta)^(1/alpha) * sign(x). Logged as 8 bits per element
 plus 64 bits of per-tensor overhead (s2fp8.py:29).
 
-On MI355X this is ``smq_s2fp8_roundtrip_f32``: a log2-domain statistics launch (last-arriving
+On MI355X this is ``smq_s2fp8_roundtrip``: a log2-domain statistics launch (last-arriving
 workgroup finalises alpha, beta) and one fused transform/quantise/inverse launch.
+
+Precision 16 (quantization.py:187-204's half branch) keeps the reference's dtypes: fp16 / bf16
+inputs run the statistics and the forward transform in their own type, float_quantize returns half,
+the inverse power runs in half; the result is fp16 for fp16 inputs and fp32 for fp32 / bf16 inputs
+(torch's promotion of ``... * signs``).
 """
 
 from argparse import ArgumentParser
@@ -29,21 +34,28 @@ class S2FP8(CompressionAlgorithmBase):
     @torch.no_grad()
     def __call__(self, tensor: torch.Tensor, tag: str = None, **_):
         self.log_ratio(tag, tensor.numel(), 32, 8, overhead=64)
-        if self.hparams.precision == 16:
-            raise NotImplementedError("S2FP8 with precision=16 (half I/O) is not supported yet")
-        N.require_device_f32(tensor, "S2FP8")
+        precision = 16 if self.hparams.precision == 16 else 32
+        if precision == 32:
+            N.require_device_f32(tensor, "S2FP8")
+            out_dtype = torch.float32
+        else:
+            N.require_device(tensor, "S2FP8")
+            if tensor.dtype not in (torch.float32, torch.float16, torch.bfloat16):
+                raise NotImplementedError(f"S2FP8: dtype {tensor.dtype} is not supported")
+            out_dtype = torch.float16 if tensor.dtype == torch.float16 else torch.float32
         x = tensor.contiguous()
-        y = torch.empty_like(x)
+        y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
         n = x.numel()
         if n == 0:
             return y
         ws = N.workspace("s2fp8", x.device, N.lib().smq_s2fp8_workspace_bytes(n))
         seed, offset = quant_rng().take(n)
         N.check(
-            N.lib().smq_s2fp8_roundtrip_f32(
-                x.data_ptr(), y.data_ptr(), n, 1 if self.hparams.float_quantize_check_inf else 0,
-                None, seed, offset, None, ws.data_ptr(), ws.numel(), N.stream_ptr(x.device),
+            N.lib().smq_s2fp8_roundtrip(
+                x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), n, precision,
+                1 if self.hparams.float_quantize_check_inf else 0, None, seed, offset, None,
+                ws.data_ptr(), ws.numel(), N.stream_ptr(x.device),
             ),
-            "smq_s2fp8_roundtrip_f32",
+            "smq_s2fp8_roundtrip",
         )
         return y

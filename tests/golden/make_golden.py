@@ -54,14 +54,14 @@ def _install_stubs(record):
     from oracle import qtorch_float as qf
 
     qmod = types.ModuleType("qtorch.quant.quant_function")
-    rs = np.random.default_rng(1234)
+    record["_rs"] = np.random.default_rng(1234)
 
     def float_quantize(x, exp, man, rounding="stochastic"):
         xn = x.detach().cpu().numpy().astype(np.float32)
         if rounding == "nearest":
             y = qf.quantize(xn, exp, man, stochastic=False)
         else:
-            r = rs.integers(0, 2**31 - 1, size=xn.shape, dtype=np.uint32)  # randint_like(INT_MAX)
+            r = record["_rs"].integers(0, 2**31 - 1, size=xn.shape, dtype=np.uint32)  # randint_like(INT_MAX)
             record.setdefault("q_in", []).append(xn.copy())
             record.setdefault("q_rand", []).append(r)
             y = qf.quantize(xn, exp, man, r, stochastic=True)
@@ -247,7 +247,7 @@ def gen_float(out_dir, record):
             for iname, x in inputs.items():
                 if cname == "s2fp8" and iname == "specials":
                     continue
-                record.clear()
+                _clear(record)
                 y = codec(x.float(), tag="golden")
                 rec = dict(x=x.float().numpy(), y=y.numpy(),
                            q_in=record["q_in"][0], q_rand=record["q_rand"][0])
@@ -271,6 +271,57 @@ def gen_float(out_dir, record):
                   sort_keys=True)
 
 
+def _clear(record):
+    for k in [k for k in record if not k.startswith("_")]:
+        del record[k]
+
+
+def gen_s2fp8_p16(out_dir, record):
+    """S2FP8 at Lightning precision 16 (s2fp8.py:27-48 with quantization.py:187-204's half branch):
+    fp16 / bf16 inputs run the statistics and the forward transform in their own type, fp32 inputs
+    in fp32; float_quantize returns half, so the inverse transform runs in half; `* signs` gives
+    the output type (fp16 for fp16 inputs, fp32 otherwise). Own random stream and index file."""
+    from smart_compress.compress.s2fp8 import S2FP8
+
+    record["_rs"] = np.random.default_rng(4321)
+    g = torch.Generator().manual_seed(1616)
+    n = 8192
+    base = {
+        "normal": torch.randn(n, generator=g),
+        "relu": torch.relu(torch.randn(n, generator=g)),
+        "wide": torch.randn(n, generator=g) * torch.exp(torch.randn(n, generator=g) * 2),
+        "tiny": torch.randn(n, generator=g) * 1e-3,
+    }
+    dtypes = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32}
+    index = {}
+    for check_inf in (True, False):
+        argv = [] if check_inf else ["--no_float_quantize_check_inf"]
+        hp = S2FP8.add_argparse_args(ArgumentParser()).parse_args(argv)
+        hp.precision = 16
+        codec = S2FP8(hp)
+        for dname, dt in dtypes.items():
+            for iname, x0 in base.items():
+                x = x0.to(dt)
+                _clear(record)
+                y = codec(x.clone(), tag="golden")
+                xa = x.abs()  # the statistics s2fp8.py:31-43 computes, same torch ops and dtype
+                lg = torch.where(xa == 0.0, xa, torch.log2(xa))
+                mu, mx = torch.mean(lg), torch.max(lg)
+                alpha = 15.0 / (mx - mu)
+                beta = -alpha * mu
+                rec = dict(x=x.float().numpy(), y=y.float().numpy(),
+                           q_in=record["q_in"][0], q_rand=record["q_rand"][0],
+                           mu=np.float32(mu.item()), m=np.float32(mx.item()),
+                           alpha=np.float32(alpha.item()), beta=np.float32(beta.item()),
+                           beta_pow2=np.float32((2.0 ** beta).item()))
+                key = f"{dname}_{iname}_{'inf' if check_inf else 'noinf'}"
+                np.savez_compressed(os.path.join(out_dir, f"s2p16_{key}.npz"), **rec)
+                index[key] = dict(dtype=dname, out_dtype={torch.float16: "f16",
+                                  torch.float32: "f32"}[y.dtype], check_inf=check_inf, input=iname)
+    with open(os.path.join(out_dir, "s2fp8_p16_cases.json"), "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; nothing to do")
@@ -278,8 +329,13 @@ def main():
     record = {}
     _install_stubs(record)
     out_dir = HERE
-    gen_smaq(out_dir)
-    gen_float(out_dir, record)
+    only = sys.argv[1] if len(sys.argv) > 1 else None  # e.g. `s2fp8_p16`: one generator
+    if only in (None, "smaq"):
+        gen_smaq(out_dir)
+    if only in (None, "float"):
+        gen_float(out_dir, record)
+    if only in (None, "s2fp8_p16"):
+        gen_s2fp8_p16(out_dir, record)
     print("golden vectors written to", out_dir)
 
 

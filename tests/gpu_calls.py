@@ -84,9 +84,12 @@ def float_quant(x, exp_bits, man_bits, rounding=N.SMQ_ROUND_STOCHASTIC, check_in
     return y
 
 
-def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None):
+def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None, precision=32):
+    """smq_s2fp8_roundtrip on a device tensor of any supported dtype (precision 16: fp16 in ->
+    fp16 out, fp32 / bf16 in -> fp32 out)."""
     n = x.numel()
-    y = torch.empty_like(x)
+    half_out = precision == 16 and x.dtype == torch.float16
+    y = torch.empty(x.shape, dtype=torch.float16 if half_out else torch.float32, device=x.device)
     ws = torch.zeros(N.lib().smq_s2fp8_workspace_bytes(n), dtype=torch.uint8, device=x.device)
     st_in = None
     if mu_m is not None:
@@ -94,8 +97,8 @@ def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None):
         s.mu, s.m, s.n_used = float(mu_m[0]), float(mu_m[1]), n
         raw = np.frombuffer(ctypes.string_at(ctypes.addressof(s), 64), dtype=np.uint8).copy()
         st_in = torch.from_numpy(raw).to(x.device)
-    N.check(N.lib().smq_s2fp8_roundtrip_f32(
-        x.data_ptr(), y.data_ptr(), n, 1 if check_inf else 0,
+    N.check(N.lib().smq_s2fp8_roundtrip(
+        x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), n, precision, 1 if check_inf else 0,
         rand_bits.data_ptr() if rand_bits is not None else None, seed, offset,
         st_in.data_ptr() if st_in is not None else None, ws.data_ptr(), ws.numel(), stream()),
         "s2fp8")

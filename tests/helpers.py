@@ -20,6 +20,15 @@ def float_meta():
         return json.load(f)
 
 
+def s2p16_meta():
+    with open(os.path.join(GOLDEN, "s2fp8_p16_cases.json")) as f:
+        return json.load(f)
+
+
+def load_s2p16(key):
+    return dict(np.load(os.path.join(GOLDEN, f"s2p16_{key}.npz")))
+
+
 def load_smaq(name):
     return dict(np.load(os.path.join(GOLDEN, f"smaq_{name}.npz")))
 

@@ -130,6 +130,13 @@ def test_validation_errors_without_device():
     assert lib.smq_float_quant_f32(None, None, 0, 9, 2, 1, 1, None, 0, 0, None) == -1
     assert b"exp_bits" in lib.smq_last_error()
     assert lib.smq_s2fp8_roundtrip_f32(None, None, 0, 1, None, 0, 0, None, None, 0, None) == -1
+    fake = ctypes.c_void_p(4096)  # never dereferenced: argument checks come first
+    assert lib.smq_s2fp8_roundtrip(fake, N.SMQ_DTYPE_F16, fake, 8, 32, 1, None, 0, 0, None,
+                                   None, 0, None) == -1  # qtorch's kernels take fp32 only
+    assert b"precision 32" in lib.smq_last_error()
+    assert lib.smq_s2fp8_roundtrip(fake, N.SMQ_DTYPE_F32, fake, 8, 8, 1, None, 0, 0, None,
+                                   None, 0, None) == -1
+    assert lib.smq_s2fp8_roundtrip(fake, 7, fake, 8, 16, 1, None, 0, 0, None, None, 0, None) == -1
     assert lib.smq_smaq_params_set(p, 6, 8, 1.0, 1.0, 32) == -1
 
 

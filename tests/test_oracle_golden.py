@@ -15,8 +15,8 @@
 import numpy as np
 import pytest
 
-from helpers import (float_meta, load_float, load_smaq, n_diff_f32, oracle_cfg, same_f32,
-                     smaq_cases, ulp_diff)
+from helpers import (float_meta, load_float, load_s2p16, load_smaq, n_diff_f32, oracle_cfg, same_f32,
+                     s2p16_meta, smaq_cases, ulp_diff)
 
 CASES = smaq_cases()
 FMETA = float_meta()
@@ -122,6 +122,39 @@ def test_s2fp8_oracle(key):
     ok = (np.isnan(y) & np.isnan(d["y"])) | (np.abs(y.astype(np.float64) - d["y"])
                                              <= 4 * np.spacing(np.abs(d["y"])))
     assert ok.all()
+
+
+@pytest.mark.parametrize("key", sorted(s2p16_meta()))
+def test_s2fp8_p16_oracle(key):
+    """S2FP8 at precision 16 (tests/golden/s2p16_*: the reference run with fp16 / bf16 / fp32
+    tensors and hparams.precision = 16): alpha, beta, 2^beta from the reference's (mu, max) and the
+    oracle's own (mu, max) bit-exact; the quantiser input Y bit-exact for fp16 / bf16 (rounded to
+    the input type) and within 2 fp32 ulp for fp32; the half-precision inverse bit-exact."""
+    from oracle import qtorch_float as qf
+    from oracle import s2fp8
+
+    m, d = s2p16_meta()[key], load_s2p16(key)
+    dt = m["dtype"]
+    st = s2fp8.derive_p16(d["mu"], d["m"], dt)
+    for k in ("alpha", "beta", "beta_pow2"):
+        assert same_f32(st[k], d[k]), k
+    own = s2fp8.stats_p16(d["x"], dt)
+    if dt == "f32":
+        assert ulp_diff(own["mu"], d["mu"]) <= 2
+    else:
+        assert same_f32(own["mu"], d["mu"])
+    assert same_f32(own["m"], d["m"])
+    Y = s2fp8.transform_p16(d["x"], st, dt)
+    if dt == "f32":
+        fin = np.isfinite(d["q_in"])
+        assert np.max(np.abs(Y[fin].view(np.int32).astype(np.int64)
+                             - d["q_in"][fin].view(np.int32)), initial=0) <= 2
+    else:
+        assert same_f32(Y, d["q_in"])
+    T_ref = qf.float_quantize(d["q_in"], 5, 2, d["q_rand"], m["check_inf"])
+    y, out_dt = s2fp8.inverse_p16(T_ref, d["x"], st, dt)
+    assert out_dt == m["out_dtype"]
+    assert same_f32(y, d["y"]), n_diff_f32(y, d["y"])
 
 
 def test_qtorch_known_answers():
