@@ -158,7 +158,9 @@ typedef struct SmqS2fp8Stats {
   float inv_beta_pow2;
   float inv_alpha;
   uint32_t n_used;
-  uint32_t reserved[8];
+  uint64_t rng_offset; /* random-stream position of element 0 relative to the call's offset:
+                          the snapshot of *offset_counter (graph-safe mode), else 0 */
+  uint32_t reserved[6];
 } SmqS2fp8Stats;
 
 /* ---- library ---- */
@@ -209,7 +211,8 @@ int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_
 size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count);
 /* Two launches for the whole list. Statistics of tensor t land in ((SmqSmaqStats*)ws)[t]. Only
  * full statistics (SMQ_STATS_WORKSPACE, no range-std) are supported. host_plan is read for its
- * header only. */
+ * header (and, with params.offset_counter, its descriptors: the call advances the counter by
+ * max(rng_offset + n) over the tensors; tensor t draws offset + snapshot + rng_offset + i). */
 int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan, const SmqSmaqParams* p,
                        void* ws, size_t ws_bytes, void* stream);
 
@@ -219,6 +222,14 @@ int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan, const SmqSma
 int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int man_bits,
                         int rounding, int check_inf, const uint32_t* rand_bits, uint64_t seed,
                         uint64_t offset, void* stream);
+/* The same for any element types: x is SMQ_DTYPE_F32 / F16 / BF16 (quantised as its exact fp32
+ * value), y is SMQ_DTYPE_F32 or SMQ_DTYPE_F16 (RN conversion of the fp32 result: the `.half()` of
+ * quantization.py:201-202, fused). offset_counter: optional device uint64 holding the stream
+ * position; when given, element i draws counter offset + *offset_counter + i and the call
+ * advances *offset_counter by n on the stream (graph-safe: nothing is read on the host). */
+int smq_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t n, int exp_bits,
+                    int man_bits, int rounding, int check_inf, const uint32_t* rand_bits,
+                    uint64_t seed, uint64_t offset, uint64_t* offset_counter, void* stream);
 /* fp32 value of qtorch nearest-quantising FLT_MAX (quantization.py:138-150), host only. */
 float smq_float_quant_max_value(int exp_bits, int man_bits);
 
@@ -235,10 +246,12 @@ int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
  * reference's dtypes: statistics and |x|^alpha * 2^beta in the input type, float_quantize returns
  * half (quantization.py:201-202), the inverse power runs in half; y is fp16 for fp16 inputs and
  * fp32 for fp32 / bf16 inputs (torch promotion of `... * signs`, s2fp8.py:48). The SmqS2fp8Stats
- * fields hold the input-type values (exact in fp32). */
+ * fields hold the input-type values (exact in fp32). offset_counter: as for smq_float_quant
+ * (snapshot in SmqS2fp8Stats.rng_offset, taken by the first launch). */
 int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precision,
                         int check_inf, const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
-                        const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes, void* stream);
+                        uint64_t* offset_counter, const SmqS2fp8Stats* stats_in, void* ws,
+                        size_t ws_bytes, void* stream);
 
 /* ---- host reference helpers shared with the oracle (pure functions, no GPU) ---- */
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);

@@ -79,16 +79,39 @@ __host__ __device__ __forceinline__ float qtorch_quant(float a, uint32_t rand_bi
 }
 
 struct FQArgs {
-  const float* x;
-  float* y;
+  const void* x;
+  void* y;
   int64_t n;
   const uint32_t* rand_bits;
+  const uint64_t* ctr;  // graph-safe stream position (read here, advanced by fq_bump_kernel)
   uint32_t key;
   uint64_t offset;
   int exp_bits, man_bits;
   int check_inf;
   float max_value;
 };
+
+// y element stores: fp32, or fp16 (precision 16: float_quantize returns .half(), RN)
+template <bool HOUT>
+__device__ __forceinline__ void store4_out(void* y, int64_t j, float4 o) {
+  if (!HOUT) {
+    store_nt(static_cast<float4*>(y) + j, o);
+  } else {
+    const uint32_t lo = (uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.x)) |
+                        ((uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.y)) << 16);
+    const uint32_t hi = (uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.z)) |
+                        ((uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.w)) << 16);
+    static_cast<uint2*>(y)[j] = make_uint2(lo, hi);
+  }
+}
+
+template <bool HOUT>
+__device__ __forceinline__ void store1_out(void* y, int64_t e, float v) {
+  if (!HOUT) static_cast<float*>(y)[e] = v;
+  else static_cast<__half*>(y)[e] = __float2half_rn(v);
+}
+
+
 
 // abs(y - max) <= FLT_EPSILON -> +inf (quantization.py:195-199)
 __device__ __forceinline__ float check_inf_fn(float y, const FQArgs& A) {
@@ -97,20 +120,21 @@ __device__ __forceinline__ float check_inf_fn(float y, const FQArgs& A) {
 
 constexpr int kFqDefaultTileV = 1;  // float4 per lane per tile (flat tiles; SMQ_FQ_TILE=1|2|4)
 
-template <bool SR, bool RARR, bool VEC, int kFqTileV>
+// TIN: element type of x (quantised as its exact fp32 value); HOUT: fp16 y (the `.half()` of
+// quantization.py:201-202 fused into the store).
+template <bool SR, bool RARR, bool VEC, int kFqTileV, int TIN, bool HOUT>
 __global__ __launch_bounds__(kBlock) void float_quant_kernel(FQArgs A) {
   constexpr int kFqTileElems = kBlock * kFqTileV * 4;
   const int64_t n = A.n;
+  const uint64_t off = A.offset + (A.ctr ? *A.ctr : 0ull);
   auto rb = [&](int64_t e) -> uint32_t {
     if (!SR) return 0u;
-    return RARR ? A.rand_bits[e] : rng_u32(A.key, A.offset + (uint64_t)e);
+    return RARR ? A.rand_bits[e] : rng_u32(A.key, off + (uint64_t)e);
   };
   auto q1 = [&](float v, uint32_t r) {
     return check_inf_fn(qtorch_quant(v, r, A.exp_bits, A.man_bits, SR), A);
   };
   if (VEC) {
-    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(A.x);
-    float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
     const uint4* __restrict__ r4 = reinterpret_cast<const uint4*>(A.rand_bits);
     const int64_t nv = n >> 2;
     const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kFqTileV) + threadIdx.x;
@@ -118,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void float_quant_kernel(FQArgs A) {
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
       const int64_t j = t0 + u * kBlock;
-      if (j < nv) v[u] = x4[j];
+      if (j < nv) v[u] = load4<TIN>(A.x, j);
     }
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
@@ -136,20 +160,25 @@ __global__ __launch_bounds__(kBlock) void float_quant_kernel(FQArgs A) {
       o.y = q1(v[u].y, r1);
       o.z = q1(v[u].z, r2);
       o.w = q1(v[u].w, r3);
-      store_nt(y4 + j, o);
+      store4_out<HOUT>(A.y, j, o);
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
       const int64_t e = (nv << 2) + threadIdx.x;
-      A.y[e] = q1(A.x[e], rb(e));
+      store1_out<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
     }
   } else {
     const int64_t e0 = (int64_t)blockIdx.x * kFqTileElems + threadIdx.x;
     for (int k = 0; k < kFqTileElems / kBlock; ++k) {
       const int64_t e = e0 + (int64_t)k * kBlock;
       if (e >= n) break;
-      A.y[e] = q1(A.x[e], rb(e));
+      store1_out<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
     }
   }
+}
+
+// Graph-safe stream: after the launch that read *ctr, advance it by the elements drawn.
+__global__ void fq_bump_kernel(uint64_t* ctr, uint64_t n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *ctr += n;
 }
 
 // ---- S2FP8 ---------------------------------------------------------------------------------------
@@ -180,6 +209,15 @@ template <int TIN>
 __device__ __forceinline__ float s2_log(float x) {
   const float a = fabsf(x);
   return (a == 0.0f) ? a : s2_round<TIN>(log2f(a));  // torch.where(X_abs == 0.0, X_abs, torch.log2(X_abs))
+}
+
+// Graph-safe stream position: the snapshot of *ctr, advanced by n (0 without a counter). One
+// thread of the call's first launch runs it; later launches read the snapshot.
+__device__ __forceinline__ uint64_t take_offset(uint64_t* ctr, uint64_t n) {
+  if (!ctr) return 0ull;
+  const uint64_t o = *ctr;
+  *ctr = o + n;
+  return o;
 }
 
 // s2fp8.py:31-43 from (sum, max) of the log2 values. TIN = the input type: the reference's torch
@@ -214,7 +252,10 @@ template <int TIN>
 __global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const void* __restrict__ x, int64_t n,
                                                              int vec, S2Partial* partials,
                                                              uint32_t* counter,
-                                                             SmqS2fp8Stats* out) {
+                                                             SmqS2fp8Stats* out,
+                                                             uint64_t* rng_ctr) {
+  // graph-safe random stream: one snapshot + advance per call, read by the apply launch
+  if (blockIdx.x == 0 && threadIdx.x == 0) out->rng_offset = take_offset(rng_ctr, (uint64_t)n);
   __shared__ double shs[kBlock / kWave];
   __shared__ float shm[kBlock / kWave];
   __shared__ uint32_t slot;
@@ -311,8 +352,12 @@ __global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const void* __restr
 
 // Injected (mu, m): derive the rest exactly like the finaliser (parity tests).
 template <int TIN>
-__global__ void s2fp8_derive_kernel(const SmqS2fp8Stats* in, SmqS2fp8Stats* out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) s2fp8_derive<TIN>(in->mu, in->m, in->n_used, out);
+__global__ void s2fp8_derive_kernel(const SmqS2fp8Stats* in, SmqS2fp8Stats* out, uint64_t* rng_ctr,
+                                    uint64_t n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    s2fp8_derive<TIN>(in->mu, in->m, in->n_used, out);
+    out->rng_offset = take_offset(rng_ctr, n);
+  }
 }
 
 struct S2Args {
@@ -382,25 +427,6 @@ __device__ __forceinline__ float s2fp8_elem16(float xv, uint32_t r, float alpha,
 template <int TIN, bool P16>
 constexpr bool s2_half_out() { return P16 && TIN == kF16; }
 
-template <bool HOUT>
-__device__ __forceinline__ void s2_store4(void* y, int64_t j, float4 o) {
-  if (!HOUT) {
-    store_nt(static_cast<float4*>(y) + j, o);
-  } else {
-    const uint32_t lo = (uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.x)) |
-                        ((uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.y)) << 16);
-    const uint32_t hi = (uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.z)) |
-                        ((uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.w)) << 16);
-    static_cast<uint2*>(y)[j] = make_uint2(lo, hi);
-  }
-}
-
-template <bool HOUT>
-__device__ __forceinline__ void s2_store1(void* y, int64_t e, float v) {
-  if (!HOUT) static_cast<float*>(y)[e] = v;
-  else static_cast<__half*>(y)[e] = __float2half_rn(v);
-}
-
 template <bool RARR, bool VEC, int kFqTileV, int TIN, bool P16>
 __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   constexpr int kFqTileElems = kBlock * kFqTileV * 4;
@@ -409,8 +435,9 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
               ialpha = A.st->inv_alpha;
   const float ialpha_e = P16 ? s2_round<kF16>(ialpha) : ialpha;
   const int64_t n = A.n;
+  const uint64_t off = A.offset + A.st->rng_offset;
   auto rb = [&](int64_t e) -> uint32_t {
-    return RARR ? A.rand_bits[e] : rng_u32(A.key, A.offset + (uint64_t)e);
+    return RARR ? A.rand_bits[e] : rng_u32(A.key, off + (uint64_t)e);
   };
   const bool fast = alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f && ialpha < INFINITY;
   auto q1 = [&](float v, uint32_t r) {
@@ -438,18 +465,18 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
       o.y = q1(v[u].y, rb(4 * j + 1));
       o.z = q1(v[u].z, rb(4 * j + 2));
       o.w = q1(v[u].w, rb(4 * j + 3));
-      s2_store4<HOUT>(A.y, j, o);
+      store4_out<HOUT>(A.y, j, o);
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
       const int64_t e = (nv << 2) + threadIdx.x;
-      s2_store1<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
+      store1_out<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
     }
   } else {
     const int64_t e0 = (int64_t)blockIdx.x * kFqTileElems + threadIdx.x;
     for (int k = 0; k < kFqTileElems / kBlock; ++k) {
       const int64_t e = e0 + (int64_t)k * kBlock;
       if (e >= n) break;
-      s2_store1<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
+      store1_out<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
     }
   }
 }
@@ -501,11 +528,19 @@ float smq_float_quant_max_value(int exp_bits, int man_bits) {
   return host_max_value(exp_bits, man_bits);
 }
 
-int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int man_bits,
-                        int rounding, int check_inf, const uint32_t* rand_bits, uint64_t seed,
-                        uint64_t offset, void* stream) {
+int smq_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t n, int exp_bits,
+                    int man_bits, int rounding, int check_inf, const uint32_t* rand_bits,
+                    uint64_t seed, uint64_t offset, uint64_t* offset_counter, void* stream) {
   if (n < 0 || (n > 0 && (!x || !y))) {
     set_error("float_quant: bad tensor arguments");
+    return SMQ_ERR_INVALID;
+  }
+  if (dtype_in != SMQ_DTYPE_F32 && dtype_in != SMQ_DTYPE_F16 && dtype_in != SMQ_DTYPE_BF16) {
+    set_error("float_quant: dtype_in must be SMQ_DTYPE_F32, _F16 or _BF16 (got %d)", dtype_in);
+    return SMQ_ERR_INVALID;
+  }
+  if (dtype_out != SMQ_DTYPE_F32 && dtype_out != SMQ_DTYPE_F16) {
+    set_error("float_quant: dtype_out must be SMQ_DTYPE_F32 or _F16 (got %d)", dtype_out);
     return SMQ_ERR_INVALID;
   }
   if (exp_bits < 2 || exp_bits > 8 || man_bits < 0 || man_bits > 22) {
@@ -523,6 +558,7 @@ int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int m
   A.y = y;
   A.n = n;
   A.rand_bits = rand_bits;
+  A.ctr = offset_counter;
   A.key = rng_key(seed);
   A.offset = offset;
   A.exp_bits = exp_bits;
@@ -531,25 +567,56 @@ int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int m
   A.max_value = host_max_value(exp_bits, man_bits);
   const bool sr = rounding == SMQ_ROUND_STOCHASTIC;
   const bool rarr = sr && rand_bits != nullptr;
-  const bool vec = aligned16f(x) && aligned16f(y) && (!rarr || aligned16f(rand_bits));
+  const bool hout = dtype_out == SMQ_DTYPE_F16;
+  // one 4-element group per lane: 16 B of fp32 or 8 B of fp16 / bf16
+  const uintptr_t xa = dtype_in == SMQ_DTYPE_F32 ? 15u : 7u, ya = hout ? 7u : 15u;
+  const bool vec = ((uintptr_t)x & xa) == 0 && ((uintptr_t)y & ya) == 0 &&
+                   (!rarr || aligned16f(rand_bits));
   const int grid = fq_grid(n);
   hipStream_t st = (hipStream_t)stream;
-  const int tv = fq_tile_v();
+  if (dtype_in == SMQ_DTYPE_F32 && !hout) {
+    const int tv = fq_tile_v();
 #define SMQ_FQ(S, R, V)                                                                          \
   do {                                                                                           \
-    if (tv == 1) hipLaunchKernelGGL((float_quant_kernel<S, R, V, 1>), dim3(grid), dim3(kBlock), 0, st, A); \
-    else if (tv == 2) hipLaunchKernelGGL((float_quant_kernel<S, R, V, 2>), dim3(grid), dim3(kBlock), 0, st, A); \
-    else hipLaunchKernelGGL((float_quant_kernel<S, R, V, 4>), dim3(grid), dim3(kBlock), 0, st, A); \
+    if (tv == 1) hipLaunchKernelGGL((float_quant_kernel<S, R, V, 1, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
+    else if (tv == 2) hipLaunchKernelGGL((float_quant_kernel<S, R, V, 2, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
+    else hipLaunchKernelGGL((float_quant_kernel<S, R, V, 4, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
   } while (0)
-  if (!sr) {
-    if (vec) SMQ_FQ(false, false, true); else SMQ_FQ(false, false, false);
-  } else if (rarr) {
-    if (vec) SMQ_FQ(true, true, true); else SMQ_FQ(true, true, false);
-  } else {
-    if (vec) SMQ_FQ(true, false, true); else SMQ_FQ(true, false, false);
-  }
+    if (!sr) {
+      if (vec) SMQ_FQ(false, false, true); else SMQ_FQ(false, false, false);
+    } else if (rarr) {
+      if (vec) SMQ_FQ(true, true, true); else SMQ_FQ(true, true, false);
+    } else {
+      if (vec) SMQ_FQ(true, false, true); else SMQ_FQ(true, false, false);
+    }
 #undef SMQ_FQ
-  return check_launch("float_quant_kernel");
+  } else {
+    // mixed-type variants: default tile only (the tile knob is an fp32 measurement aid)
+    const int g = (int)((n + (int64_t)kBlock * 4 * kFqDefaultTileV - 1) / ((int64_t)kBlock * 4 * kFqDefaultTileV));
+#define SMQ_FQ2(S, R, V, T, H) hipLaunchKernelGGL((float_quant_kernel<S, R, V, kFqDefaultTileV, T, H>), dim3(g), dim3(kBlock), 0, st, A)
+#define SMQ_FQT(T, H)                                                                   \
+  do {                                                                                  \
+    if (!sr) { if (vec) SMQ_FQ2(false, false, true, T, H); else SMQ_FQ2(false, false, false, T, H); } \
+    else if (rarr) { if (vec) SMQ_FQ2(true, true, true, T, H); else SMQ_FQ2(true, true, false, T, H); } \
+    else { if (vec) SMQ_FQ2(true, false, true, T, H); else SMQ_FQ2(true, false, false, T, H); } \
+  } while (0)
+    if (dtype_in == SMQ_DTYPE_F32) SMQ_FQT(kF32, true);
+    else if (dtype_in == SMQ_DTYPE_F16) { if (hout) SMQ_FQT(kF16, true); else SMQ_FQT(kF16, false); }
+    else { if (hout) SMQ_FQT(kBF16, true); else SMQ_FQT(kBF16, false); }
+#undef SMQ_FQT
+#undef SMQ_FQ2
+  }
+  int rc = check_launch("float_quant_kernel");
+  if (rc || !offset_counter) return rc;
+  hipLaunchKernelGGL(fq_bump_kernel, dim3(1), dim3(64), 0, st, offset_counter, (uint64_t)n);
+  return check_launch("fq_bump_kernel");
+}
+
+int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int man_bits,
+                        int rounding, int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                        uint64_t offset, void* stream) {
+  return smq_float_quant(x, SMQ_DTYPE_F32, y, SMQ_DTYPE_F32, n, exp_bits, man_bits, rounding,
+                         check_inf, rand_bits, seed, offset, nullptr, stream);
 }
 
 size_t smq_s2fp8_workspace_bytes(int64_t n) {
@@ -559,7 +626,8 @@ size_t smq_s2fp8_workspace_bytes(int64_t n) {
 
 int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precision,
                         int check_inf, const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
-                        const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes, void* stream) {
+                        uint64_t* offset_counter, const SmqS2fp8Stats* stats_in, void* ws,
+                        size_t ws_bytes, void* stream) {
   if (n < 1 || !x || !y) {
     set_error("s2fp8: n >= 1 and non-NULL x, y required");
     return SMQ_ERR_INVALID;
@@ -589,18 +657,18 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
   const uintptr_t align = dtype == SMQ_DTYPE_F32 ? 15u : 7u;  // one 4-element group per lane
   const bool xal = ((uintptr_t)x & align) == 0;
   if (stats_in) {
-    if (dtype == SMQ_DTYPE_F32) hipLaunchKernelGGL(s2fp8_derive_kernel<kF32>, dim3(1), dim3(64), 0, st, stats_in, hdr);
-    else if (dtype == SMQ_DTYPE_F16) hipLaunchKernelGGL(s2fp8_derive_kernel<kF16>, dim3(1), dim3(64), 0, st, stats_in, hdr);
-    else hipLaunchKernelGGL(s2fp8_derive_kernel<kBF16>, dim3(1), dim3(64), 0, st, stats_in, hdr);
+    if (dtype == SMQ_DTYPE_F32) hipLaunchKernelGGL(s2fp8_derive_kernel<kF32>, dim3(1), dim3(64), 0, st, stats_in, hdr, offset_counter, (uint64_t)n);
+    else if (dtype == SMQ_DTYPE_F16) hipLaunchKernelGGL(s2fp8_derive_kernel<kF16>, dim3(1), dim3(64), 0, st, stats_in, hdr, offset_counter, (uint64_t)n);
+    else hipLaunchKernelGGL(s2fp8_derive_kernel<kBF16>, dim3(1), dim3(64), 0, st, stats_in, hdr, offset_counter, (uint64_t)n);
   } else {
     const int grid = s2_stats_grid(n);
     const int vec = xal ? 1 : 0;
     if (dtype == SMQ_DTYPE_F32)
-      hipLaunchKernelGGL(s2fp8_stats_kernel<kF32>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr);
+      hipLaunchKernelGGL(s2fp8_stats_kernel<kF32>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr, offset_counter);
     else if (dtype == SMQ_DTYPE_F16)
-      hipLaunchKernelGGL(s2fp8_stats_kernel<kF16>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr);
+      hipLaunchKernelGGL(s2fp8_stats_kernel<kF16>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr, offset_counter);
     else
-      hipLaunchKernelGGL(s2fp8_stats_kernel<kBF16>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr);
+      hipLaunchKernelGGL(s2fp8_stats_kernel<kBF16>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr, offset_counter);
   }
   int rc = check_launch("s2fp8_stats_kernel");
   if (rc) return rc;
@@ -656,7 +724,7 @@ int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,
                             const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
                             void* stream) {
   return smq_s2fp8_roundtrip(x, SMQ_DTYPE_F32, y, n, 32, check_inf, rand_bits, seed, offset,
-                             stats_in, ws, ws_bytes, stream);
+                             nullptr, stats_in, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

@@ -26,6 +26,7 @@ namespace smq {
 // 32K 80 us).
 constexpr int64_t kDefaultChunk = 8192;
 constexpr int64_t kDefaultStatsChunk = 32768;
+constexpr size_t kSnapBytes = 64;  // workspace slot: the call's random-stream snapshot
 
 struct MultiHeader {
   int32_t count;
@@ -60,6 +61,9 @@ struct MultiArgs {
   const ChunkDesc* stat_chunks;  // statistics chunks
   SmqSmaqStats* stats;       // [count]
   uint32_t* counters;        // [count]
+  uint64_t* rng_snap;        // stream position of this call relative to offset (graph-safe mode)
+  uint64_t* rng_ctr;         // params.offset_counter (NULL: host-managed offsets)
+  uint64_t rng_span;         // elements this call draws: max(desc.rng_offset + n)
   StatPartial* partials;     // [n_chunks]
   float thr, r_main, r_out, clamp_lo, clamp_hi;
   double inv_r_main, inv_r_out;
@@ -72,6 +76,14 @@ struct MultiArgs {
 
 __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   __shared__ uint32_t slot;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // one snapshot + advance per call
+    uint64_t o = 0;
+    if (A.rng_ctr) {
+      o = *A.rng_ctr;
+      *A.rng_ctr = o + A.rng_span;
+    }
+    *A.rng_snap = o;
+  }
   const ChunkDesc ch = A.stat_chunks[blockIdx.x];
   const float* __restrict__ x = ch.x;
   const int64_t n = ch.n;
@@ -159,7 +171,8 @@ __device__ __forceinline__ float elem_ap(float v, float u, const ElemConsts& c, 
 template <bool SR, bool SUB, bool SQ>
 __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, const ChunkDesc& ch,
                                                           const ElemConsts& c, bool all_pos,
-                                                          bool vec, const float4 (&pre)[4]) {
+                                                          bool vec, const float4 (&pre)[4],
+                                                          uint64_t off) {
   const float* __restrict__ x = ch.x;
   float* y = ch.y;  // may alias x
   unsigned long long n_out = 0;
@@ -180,7 +193,7 @@ __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, co
     for (int u = 0; u < 4; ++u) {
       const int64_t j = t0 + threadIdx.x + u * kBlock;
       if (j >= e4) continue;
-      const uint64_t ctr = A.offset + ch.rng_offset + ((uint64_t)j << 2);
+      const uint64_t ctr = off + ch.rng_offset + ((uint64_t)j << 2);
       float u0 = 0.f, u1 = 0.f, u2 = 0.f, u3 = 0.f;
       if (SR) rng_hu4(A.key, ctr, u0, u1, u2, u3);
       bool b0, b1, b2, b3;
@@ -195,14 +208,14 @@ __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, co
     }
     if (threadIdx.x < (int)(ch.end - (e4 << 2))) {
       const int64_t e = (e4 << 2) + threadIdx.x;
-      const float u = SR ? rng_hu(A.key, A.offset + ch.rng_offset + (uint64_t)e) : 0.f;
+      const float u = SR ? rng_hu(A.key, off + ch.rng_offset + (uint64_t)e) : 0.f;
       bool b;
       y[e] = elem_ap<RM, SUB, SQ>(x[e], u, c, all_pos, b);
       n_out += (unsigned)b;
     }
   } else {
     for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) {
-      const float u = SR ? rng_hu(A.key, A.offset + ch.rng_offset + (uint64_t)j) : 0.f;
+      const float u = SR ? rng_hu(A.key, off + ch.rng_offset + (uint64_t)j) : 0.f;
       bool b;
       y[j] = elem_ap<RM, SUB, SQ>(x[j], u, c, all_pos, b);
       n_out += (unsigned)b;
@@ -231,9 +244,10 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
   ElemConsts c;
   init_consts(c, st, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, A.thr);
   const bool all_pos = ch.all_positive != 0;
+  const uint64_t off = A.offset + *A.rng_snap;  // + the call's snapshot (0 unless graph-safe)
   const unsigned long long n_out =
-      st->quot_check ? multi_chunk<SR, true, SQ>(A, ch, c, all_pos, vec, pre)
-                     : multi_chunk<SR, false, SQ>(A, ch, c, all_pos, vec, pre);
+      st->quot_check ? multi_chunk<SR, true, SQ>(A, ch, c, all_pos, vec, pre, off)
+                     : multi_chunk<SR, false, SQ>(A, ch, c, all_pos, vec, pre, off);
   if (A.count_outliers) {
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
     const double t = wave_sum((double)n_out);
@@ -366,7 +380,7 @@ size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count) {
   if (!sizes || count < 1 || !plan_sizes(sizes, count, &ps)) return 0;
   const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
   const size_t counters = ((sizeof(uint32_t) * (size_t)count) + 63) & ~(size_t)63;
-  return stats + counters + sizeof(StatPartial) * (size_t)ps.n_stat_chunks;
+  return stats + counters + kSnapBytes + sizeof(StatPartial) * (size_t)ps.n_stat_chunks;
 }
 
 }  // extern "C"
@@ -392,7 +406,7 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   }
   const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
   const size_t counters = ((sizeof(uint32_t) * (size_t)count) + 63) & ~(size_t)63;
-  const size_t need = stats + counters + sizeof(StatPartial) * (size_t)n_stat_chunks;
+  const size_t need = stats + counters + kSnapBytes + sizeof(StatPartial) * (size_t)n_stat_chunks;
   if (ws_bytes < need) {
     set_error("multi: workspace too small: need %zu bytes, got %zu", need, ws_bytes);
     return SMQ_ERR_WORKSPACE;
@@ -407,7 +421,18 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   char* wb = (char*)ws;
   A.stats = (SmqSmaqStats*)wb;
   A.counters = (uint32_t*)(wb + stats);
-  A.partials = (StatPartial*)(wb + stats + counters);
+  A.rng_snap = (uint64_t*)(wb + stats + counters);
+  A.partials = (StatPartial*)(wb + stats + counters + kSnapBytes);
+  A.rng_ctr = p->offset_counter;
+  uint64_t span = 0;  // the stream span of the call, from the host copy of the descriptors
+  if (A.rng_ctr) {
+    const SmqTensorDesc* hd = (const SmqTensorDesc*)((const char*)host_plan + sizeof(MultiHeader));
+    for (int t = 0; t < count; ++t) {
+      const uint64_t e = hd[t].rng_offset + (uint64_t)hd[t].n;
+      span = e > span ? e : span;
+    }
+  }
+  A.rng_span = span;
   A.thr = p->main_std_dev_threshold;
   A.r_main = p->range_main;
   A.r_out = p->range_outlier;

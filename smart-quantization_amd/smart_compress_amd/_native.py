@@ -126,7 +126,8 @@ class SmqS2fp8Stats(ctypes.Structure):
         ("inv_beta_pow2", ctypes.c_float),
         ("inv_alpha", ctypes.c_float),
         ("n_used", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 8),
+        ("rng_offset", ctypes.c_uint64),
+        ("reserved", ctypes.c_uint32 * 6),
     ]
 
 
@@ -185,7 +186,11 @@ SIGNATURES = {
     ),
     "smq_s2fp8_roundtrip": (
         _I32,
-        [_P, _I32, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _SZ, _P],
+        [_P, _I32, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _P, _SZ, _P],
+    ),
+    "smq_float_quant": (
+        _I32,
+        [_P, _I32, _P, _I32, _I64, _I32, _I32, _I32, _I32, _P, _U64, _U64, _P, _P],
     ),
     "smq_rng_u32": (ctypes.c_uint32, [_U64, _U64]),
     "smq_smaq_pack_bound": (_SZ, [_I64, _I32, _I32]),
@@ -273,7 +278,11 @@ def workspace(kind: str, device: torch.device, nbytes: int) -> torch.Tensor:
 
 
 class RngState:
-    """(seed, offset) of a counter-based RNG stream; offset advances by the elements consumed."""
+    """(seed, offset) of a counter-based RNG stream; offset advances by the elements consumed.
+
+    Graph-safe mode keeps the position in a device uint64 per GPU (``counter(device)``, created
+    from ``offset``); the kernels read and advance it, so hipGraph replays draw fresh streams.
+    ``release_counters`` returns to host offsets, continuing from the device position."""
 
     def __init__(self, seed: int | None = None):
         if seed is None:
@@ -281,6 +290,7 @@ class RngState:
         self.seed = int(seed) & (2**64 - 1)
         self.offset = 0
         self._lock = threading.Lock()
+        self._counters = {}
 
     def take(self, n: int) -> Tuple[int, int]:
         with self._lock:
@@ -288,9 +298,36 @@ class RngState:
             self.offset = (self.offset + int(n)) & (2**64 - 1)
         return self.seed, off
 
+    def counter(self, device) -> torch.Tensor:
+        device = torch.device(device)
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        c = self._counters.get(idx)
+        if c is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("graph-safe random stream: create the device counter before "
+                                   "capture (graph_safe(device=...) or one eager call)")
+            v = self.offset - 2**64 if self.offset >= 2**63 else self.offset  # int64 bit pattern
+            c = torch.tensor([v], dtype=torch.int64, device=torch.device("cuda", idx))
+            self._counters[idx] = c
+        return c
+
+    def position(self) -> int:
+        """The stream position: the host offset, or the furthest device counter (a host sync)."""
+        pos = self.offset
+        for c in self._counters.values():
+            pos = max(pos, int(c.item()) & (2**64 - 1))
+        return pos
+
+    def release_counters(self) -> None:
+        self.offset = self.position()
+        self._counters.clear()
+
     def state_dict(self):
-        return {"seed": self.seed, "offset": self.offset}
+        return {"seed": self.seed, "offset": self.position()}
 
     def load_state_dict(self, d):
         self.seed = int(d["seed"])
         self.offset = int(d["offset"])
+        v = self.offset - 2**64 if self.offset >= 2**63 else self.offset
+        for c in self._counters.values():
+            c.fill_(v)

@@ -8,6 +8,7 @@ from argparse import ArgumentParser
 
 import torch
 
+from ..util.pytorch import quantization as _q
 from ..util.pytorch.quantization import add_float_quantize_args, float_quantize
 from .base import CompressionAlgorithmBase
 
@@ -23,6 +24,11 @@ class FloatFormatCodec(CompressionAlgorithmBase):
             parents=[add_float_quantize_args(CompressionAlgorithmBase.add_argparse_args(parent_parser))],
             add_help=False,
         )
+
+    def graph_safe(self, enable: bool = True, device=None):
+        """hipGraph-capturable random stream (process-wide, see quantization.graph_safe)."""
+        _q.graph_safe(enable, device)
+        return self
 
     @torch.no_grad()
     def __call__(self, tensor: torch.Tensor, tag: str = None, **_):

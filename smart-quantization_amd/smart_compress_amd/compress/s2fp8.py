@@ -19,7 +19,8 @@ from argparse import ArgumentParser
 import torch
 
 from .. import _native as N
-from ..util.pytorch.quantization import add_float_quantize_args, quant_rng
+from ..util.pytorch import quantization as _q
+from ..util.pytorch.quantization import add_float_quantize_args
 from .base import CompressionAlgorithmBase
 
 
@@ -30,6 +31,11 @@ class S2FP8(CompressionAlgorithmBase):
             parents=[add_float_quantize_args(CompressionAlgorithmBase.add_argparse_args(parent_parser))],
             add_help=False,
         )
+
+    def graph_safe(self, enable: bool = True, device=None):
+        """hipGraph-capturable random stream (process-wide, see quantization.graph_safe)."""
+        _q.graph_safe(enable, device)
+        return self
 
     @torch.no_grad()
     def __call__(self, tensor: torch.Tensor, tag: str = None, **_):
@@ -49,11 +55,11 @@ class S2FP8(CompressionAlgorithmBase):
         if n == 0:
             return y
         ws = N.workspace("s2fp8", x.device, N.lib().smq_s2fp8_workspace_bytes(n))
-        seed, offset = quant_rng().take(n)
+        seed, offset, ctr = _q.rng_stream(n, x.device)
         N.check(
             N.lib().smq_s2fp8_roundtrip(
                 x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), n, precision,
-                1 if self.hparams.float_quantize_check_inf else 0, None, seed, offset, None,
+                1 if self.hparams.float_quantize_check_inf else 0, None, seed, offset, ctr, None,
                 ws.data_ptr(), ws.numel(), N.stream_ptr(x.device),
             ),
             "smq_s2fp8_roundtrip",

@@ -99,31 +99,22 @@ class SmartFP(CompressionAlgorithmBase):
         self.clamped_range = (1e-4, 1e4) if hp.precision == 16 else (1e-38, 1e38)
         self.rng = N.RngState(getattr(hp, "smq_seed", None))
         self._graph_safe = False
-        self._counters = {}
 
     # -- graph-safe random stream ----------------------------------------------------------------
     def graph_safe(self, enable: bool = True, device=None):
-        """Keep the random-stream position in a device counter (``SmqSmaqParams.offset_counter``)
-        instead of advancing ``self.rng.offset`` on the host, so calls captured in a hipGraph
-        (``torch.cuda.graph``) draw fresh, consecutive random streams on every replay. The stream
-        continues from the host position; create the counter before capturing (pass ``device`` or
-        make one eager call first). Values are identical to the host-offset mode for the same
-        sequence of calls."""
+        """Keep the random-stream position in a device counter (``SmqSmaqParams.offset_counter``,
+        ``self.rng.counter``) instead of advancing ``self.rng.offset`` on the host, so calls
+        captured in a hipGraph (``torch.cuda.graph``) draw fresh, consecutive random streams on
+        every replay. The stream continues from the host position; create the counter before
+        capturing (pass ``device`` or make one eager call first). Values are identical to the
+        host-offset mode for the same sequence of calls. ``graph_safe(False)`` continues on the
+        host from the device position (one host synchronisation)."""
         self._graph_safe = bool(enable)
         if enable and device is not None:
-            self._rng_counter(torch.device(device))
+            self.rng.counter(device)
+        if not enable:
+            self.rng.release_counters()
         return self
-
-    def _rng_counter(self, device: torch.device) -> torch.Tensor:
-        idx = device.index if device.index is not None else torch.cuda.current_device()
-        c = self._counters.get(idx)
-        if c is None:
-            if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("SmartFP.graph_safe: create the device counter before capture "
-                                   "(graph_safe(device=...) or one eager call)")
-            c = torch.tensor([self.rng.offset], dtype=torch.int64, device=device)
-            self._counters[idx] = c
-        return c
 
     # -- parameter block -------------------------------------------------------------------------
     def _params(self, numel: int, all_positive: bool,
@@ -143,7 +134,7 @@ class SmartFP(CompressionAlgorithmBase):
         p.count_outliers = 1 if hp.measure_compression_ratio else 0
         if self._graph_safe and device is not None:
             p.seed, p.offset = self.rng.seed, 0
-            p.offset_counter = self._rng_counter(device).data_ptr()
+            p.offset_counter = self.rng.counter(device).data_ptr()
         else:
             p.seed, p.offset = self.rng.take(numel)
         p.range_std_coef = -1.0  # set below in range mode (0.0 is a valid coefficient)

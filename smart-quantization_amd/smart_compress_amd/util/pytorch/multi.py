@@ -35,6 +35,7 @@ class SmaqMulti:
         self._plans = {}
         self._last = None
         self._p = None
+        self._graph_safe = False
 
     def _plan(self, xs, ys, allpos, device):
         key = tuple((x.data_ptr(), y.data_ptr(), x.numel(), a) for x, y, a in zip(xs, ys, allpos))
@@ -94,11 +95,16 @@ class SmaqMulti:
             p = self._p = self._codec._params(1, False)
             p.stats_source = N.SMQ_STATS_WORKSPACE
             p.count_outliers = 1 if self.hparams.measure_compression_ratio else 0
-        p.seed, p.offset = self.rng.take(plan["total"])
+        if self._graph_safe:
+            p.seed, p.offset = self.rng.seed, 0
+            p.offset_counter = self.rng.counter(device).data_ptr()
+        else:
+            p.seed, p.offset = self.rng.take(plan["total"])
+            p.offset_counter = None
         N.check(N.lib().smq_smaq_multi_f32(
             plan["dev"].data_ptr(), ctypes.addressof(plan["host"]), p, plan["ws"].data_ptr(),
             plan["ws"].numel(), N.stream_ptr(device)), "smq_smaq_multi_f32")
-        self._last = dict(plan=plan, sel=sel, base=p.offset)
+        self._last = dict(plan=plan, sel=sel, base=None if self._graph_safe else p.offset)
 
     @torch.no_grad()
     def __call__(self, xs: Sequence[torch.Tensor], ys: Optional[Sequence[torch.Tensor]] = None,
@@ -138,8 +144,21 @@ class SmaqMulti:
     def index_of(self, t: int) -> int:
         return self._last["sel"].index(t)
 
+    def graph_safe(self, enable: bool = True, device=None):
+        """Device-counter random stream (``SmqSmaqParams.offset_counter``): bound calls captured
+        in a hipGraph draw fresh streams on every replay. Shares ``self.rng`` (and so its counter)
+        with the SmartFP codec it was built from. ``offset_of`` is unavailable in this mode."""
+        self._graph_safe = bool(enable)
+        if enable and device is not None:
+            self.rng.counter(device)
+        if not enable:
+            self.rng.release_counters()
+        return self
+
     def offset_of(self, t: int) -> int:
         last = self._last
+        if last["base"] is None:
+            raise RuntimeError("offset_of: the stream position is on the device (graph-safe mode)")
         return last["base"] + last["plan"]["offsets"][last["sel"].index(t)]
 
     def read_stats(self):

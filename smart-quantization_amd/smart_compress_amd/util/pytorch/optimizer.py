@@ -98,6 +98,7 @@ class OptimLP(Optimizer):
             multi = self._multi.get(id(fn))
             if multi is None:
                 multi = self._multi[id(fn)] = SmaqMulti(codec.hparams, rng=codec.rng)
+            multi._graph_safe = codec._graph_safe  # same stream, same mode (device counter or host)
             xs = [tensors[i] for i in fused]
             multi(xs, xs, all_positive=[all_pos[i] for i in fused])
             self._log_fused(codec, fn.tag, multi, xs)

@@ -4,8 +4,13 @@ smart_compress/util/pytorch/quantization.py:131-204 (``float_quantize``, ``_get_
 
 The reference calls the un-vendored qtorch 0.2.0 ``float_quantize(x, exp, man, rounding)`` and then
 turns elements equal to the format's largest finite value into +inf (``check_inf``,
-quantization.py:195-199). Here both are one ``smq_float_quant_f32`` launch (8 B/elem, random word
-from the counter-based RNG in registers instead of a materialised ``randint_like`` tensor).
+quantization.py:195-199). Here both are one ``smq_float_quant`` launch (8 B/elem for fp32, random
+word from the counter-based RNG in registers instead of a materialised ``randint_like`` tensor). At
+precision 16 the reference's ``x.float()`` and ``.half()`` passes are fused into that launch (the
+kernel reads fp16 / bf16 and writes fp16: 4 B/elem instead of five passes).
+
+``graph_safe(True, device)`` moves the stream position of ``float_quantize`` and S2FP8 (the
+process-wide ``quant_rng()``) to a device counter so that captured hipGraphs draw fresh streams.
 """
 
 from argparse import ArgumentParser
@@ -23,6 +28,7 @@ TORCH_FLOAT_EPS = torch.tensor(torch.finfo(torch.float32).eps, dtype=torch.float
 MAX_VALUES = dict()
 
 _rng = None
+_graph_safe = False
 
 
 def quant_rng() -> N.RngState:
@@ -50,20 +56,51 @@ def add_float_quantize_args(parent_parser: ArgumentParser) -> ArgumentParser:
     return parser
 
 
+def graph_safe(enable: bool = True, device=None) -> None:
+    """Process-wide switch for the float codecs' random stream (``quant_rng()``): device-counter
+    positions (hipGraph-capturable) when enabled; back to host offsets, continuing from the device
+    position, when disabled. Create the counter before capture (``device=`` or one eager call)."""
+    global _graph_safe
+    _graph_safe = bool(enable)
+    if enable and device is not None:
+        quant_rng().counter(device)
+    if not enable:
+        quant_rng().release_counters()
+
+
+def rng_stream(n: int, device):
+    """(seed, offset, offset_counter pointer or None) for a call drawing ``n`` words."""
+    r = quant_rng()
+    if _graph_safe:
+        return r.seed, 0, r.counter(device).data_ptr()
+    seed, offset = r.take(n)
+    return seed, offset, None
+
+
 def float_quantize(x: torch.Tensor, exp: int, man: int, hparams) -> torch.Tensor:
-    """Stochastic (exp, man) round trip of ``x`` (quantization.py:187-204)."""
+    """Stochastic (exp, man) round trip of ``x`` (quantization.py:187-204). Precision 16: ``x``
+    (fp32 / fp16 / bf16) is quantised as ``x.float()`` and returned as fp16."""
     half_io = hparams.precision == 16
-    src = x.float() if half_io else x
-    N.require_device_f32(src, "float_quantize")
-    src = src.contiguous()
-    out = torch.empty_like(src)
-    seed, offset = quant_rng().take(src.numel())
+    if half_io:
+        N.require_device(x, "float_quantize")
+        if x.dtype not in N.DTYPE_CODES:
+            raise NotImplementedError(f"float_quantize: dtype {x.dtype} is not supported")
+    else:
+        N.require_device_f32(x, "float_quantize")
+    src = x.contiguous()
+    out = torch.empty(src.shape, dtype=torch.float16 if half_io else torch.float32,
+                      device=src.device)
+    n = src.numel()
+    if n == 0:
+        return out
+    seed, offset, ctr = rng_stream(n, src.device)
     N.check(
-        N.lib().smq_float_quant_f32(
-            src.data_ptr(), out.data_ptr(), src.numel(), exp, man, N.SMQ_ROUND_STOCHASTIC,
-            1 if hparams.float_quantize_check_inf else 0, None, seed, offset,
+        N.lib().smq_float_quant(
+            src.data_ptr(), N.DTYPE_CODES[src.dtype], out.data_ptr(),
+            N.SMQ_DTYPE_F16 if half_io else N.SMQ_DTYPE_F32, n, exp, man, N.SMQ_ROUND_STOCHASTIC,
+            1 if hparams.float_quantize_check_inf else 0, None, seed, offset, ctr,
             N.stream_ptr(src.device),
         ),
-        "smq_float_quant_f32",
+        "smq_float_quant",
     )
-    return out.half() if half_io else out
+    return out

@@ -74,6 +74,18 @@ def smaq_roundtrip(x, p, uniforms=None, y=None):
     return y, ws
 
 
+def float_quant_any(x, exp_bits, man_bits, out_dtype=torch.float32, rounding=N.SMQ_ROUND_STOCHASTIC,
+                    check_inf=True, rand_bits=None, seed=0, offset=0, counter=None):
+    """smq_float_quant: any input dtype, fp32 or fp16 output, optional device offset counter."""
+    y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+    N.check(N.lib().smq_float_quant(
+        x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), N.DTYPE_CODES[out_dtype], x.numel(),
+        exp_bits, man_bits, rounding, 1 if check_inf else 0,
+        rand_bits.data_ptr() if rand_bits is not None else None, seed, offset,
+        counter.data_ptr() if counter is not None else None, stream()), "float_quant")
+    return y
+
+
 def float_quant(x, exp_bits, man_bits, rounding=N.SMQ_ROUND_STOCHASTIC, check_inf=True,
                 rand_bits=None, seed=0, offset=0):
     y = torch.empty_like(x)
@@ -84,7 +96,8 @@ def float_quant(x, exp_bits, man_bits, rounding=N.SMQ_ROUND_STOCHASTIC, check_in
     return y
 
 
-def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None, precision=32):
+def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None, precision=32,
+          counter=None):
     """smq_s2fp8_roundtrip on a device tensor of any supported dtype (precision 16: fp16 in ->
     fp16 out, fp32 / bf16 in -> fp32 out)."""
     n = x.numel()
@@ -100,6 +113,7 @@ def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None, precis
     N.check(N.lib().smq_s2fp8_roundtrip(
         x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), n, precision, 1 if check_inf else 0,
         rand_bits.data_ptr() if rand_bits is not None else None, seed, offset,
+        counter.data_ptr() if counter is not None else None,
         st_in.data_ptr() if st_in is not None else None, ws.data_ptr(), ws.numel(), stream()),
         "s2fp8")
     hdr = ws[:32].cpu().numpy().view(np.float32)

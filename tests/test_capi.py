@@ -44,12 +44,13 @@ def test_struct_layouts_match_header():
 #include <stddef.h>
 #include "smq.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(SmqSmaqParams),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(SmqSmaqParams),
          sizeof(SmqSmaqStats), sizeof(SmqTensorDesc), sizeof(SmqS2fp8Stats),
          offsetof(SmqSmaqParams, seed), offsetof(SmqSmaqParams, bn_gamma),
          offsetof(SmqSmaqParams, sample_idx), offsetof(SmqSmaqStats, inv_std_clamped),
          offsetof(SmqSmaqStats, quot_check), sizeof(SmqPackedHeader),
-         offsetof(SmqPackedHeader, inv_range_main), offsetof(SmqPackedHeader, error));
+         offsetof(SmqPackedHeader, inv_range_main), offsetof(SmqPackedHeader, error),
+         offsetof(SmqS2fp8Stats, rng_offset));
   return 0;
 }
 """
@@ -64,7 +65,8 @@ int main(void) {
             N.SmqSmaqParams.seed.offset, N.SmqSmaqParams.bn_gamma.offset,
             N.SmqSmaqParams.sample_idx.offset, N.SmqSmaqStats.inv_std_clamped.offset,
             N.SmqSmaqStats.quot_check.offset, ctypes.sizeof(N.SmqPackedHeader),
-            N.SmqPackedHeader.inv_range_main.offset, N.SmqPackedHeader.error.offset]
+            N.SmqPackedHeader.inv_range_main.offset, N.SmqPackedHeader.error.offset,
+            N.SmqS2fp8Stats.rng_offset.offset]
     assert got == want
     from oracle import smaq_packed as P  # the oracle's header struct matches the C layout
 
@@ -131,12 +133,16 @@ def test_validation_errors_without_device():
     assert b"exp_bits" in lib.smq_last_error()
     assert lib.smq_s2fp8_roundtrip_f32(None, None, 0, 1, None, 0, 0, None, None, 0, None) == -1
     fake = ctypes.c_void_p(4096)  # never dereferenced: argument checks come first
-    assert lib.smq_s2fp8_roundtrip(fake, N.SMQ_DTYPE_F16, fake, 8, 32, 1, None, 0, 0, None,
+    assert lib.smq_s2fp8_roundtrip(fake, N.SMQ_DTYPE_F16, fake, 8, 32, 1, None, 0, 0, None, None,
                                    None, 0, None) == -1  # qtorch's kernels take fp32 only
     assert b"precision 32" in lib.smq_last_error()
-    assert lib.smq_s2fp8_roundtrip(fake, N.SMQ_DTYPE_F32, fake, 8, 8, 1, None, 0, 0, None,
+    assert lib.smq_s2fp8_roundtrip(fake, N.SMQ_DTYPE_F32, fake, 8, 8, 1, None, 0, 0, None, None,
                                    None, 0, None) == -1
-    assert lib.smq_s2fp8_roundtrip(fake, 7, fake, 8, 16, 1, None, 0, 0, None, None, 0, None) == -1
+    assert lib.smq_s2fp8_roundtrip(fake, 7, fake, 8, 16, 1, None, 0, 0, None, None, None, 0,
+                                   None) == -1
+    assert lib.smq_float_quant(fake, 5, fake, 0, 8, 5, 2, 1, 1, None, 0, 0, None, None) == -1
+    assert lib.smq_float_quant(fake, 0, fake, 2, 8, 5, 2, 1, 1, None, 0, 0, None, None) == -1
+    assert b"dtype_out" in lib.smq_last_error()
     assert lib.smq_smaq_params_set(p, 6, 8, 1.0, 1.0, 32) == -1
 
 
