@@ -310,6 +310,16 @@ size_t smq_smaq_pack_workspace_bytes(int64_t n);
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
                       void* packed, size_t packed_bytes, void* workspace, size_t workspace_bytes,
                       void* stream);
+/* Packing-launch flags of smq_smaq_compress_ex. Block b of the stream is placed after blocks
+ * 0..b-1 (decoupled look-back). By default workgroup b packs block b: no global atomic per
+ * workgroup (a ticket on one address serialises at ~11 ns each: 0.75 ms for 2^16 blocks), which
+ * relies on every XCD starting its workgroups in index order. If that ever fails, the bounded
+ * look-back spin gives up and sets header.error; SMQ_PACK_TICKETED then re-packs with block ids
+ * from an atomic ticket (start order: no assumption). Both give the same bytes. */
+#define SMQ_PACK_TICKETED 1u
+int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
+                         void* packed, size_t packed_bytes, void* workspace,
+                         size_t workspace_bytes, uint32_t flags, void* stream);
 /* Decode a stream of n elements into y (fp32). n must equal the header's n (a stream with another
  * n or a bad magic leaves y untouched). */
 int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream);

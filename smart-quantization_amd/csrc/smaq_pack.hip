@@ -5,9 +5,9 @@
 //     quantises them with the same element code as the simulated round trip (smaq_quant), and
 //     builds the block image in LDS: outlier mask, main plane, outlier plane (LDS atomics for the
 //     bit-packed codes; ranks from wave ballots + a 16-segment scan);
-//   * blocks are compacted into one dense stream by a decoupled look-back scan: a workgroup takes
-//     its block id from an atomic ticket (so every predecessor is already resident), publishes its
-//     size, and wave 0 reads up to 64 predecessors' status words per step until it meets an
+//   * blocks are compacted into one dense stream by a decoupled look-back scan: workgroup b packs
+//     block b (index order; SMQ_PACK_TICKETED takes ids from an atomic ticket instead), publishes
+//     its size, and wave 0 reads up to 64 predecessors' status words per step until it meets an
 //     inclusive prefix. Status words are single 64-bit relaxed agent-scope atomics carrying their
 //     value, so no fences are needed; a bounded spin turns a would-be hang into header.error;
 //   * the block image is written with coalesced stores at its prefix, escapes directly, and the
@@ -54,6 +54,8 @@ struct PackArgs {
   uint64_t offset;
   int wm, wo, bm, bo;
   uint32_t n_blocks;
+  uint32_t n_full;           // blocks of SMQ_PACK_BLOCK elements (the main launch)
+  int ticketed;              // SMQ_PACK_TICKETED: block ids from an atomic ticket
   uint32_t flags;
   int place_atomic;          // measurement knob (SMQ_PACK_PLACE=atomic): see smq_smaq_compress
   uint32_t stage_words;      // LDS stage (w[0], mask, code stream) for these widths; q values follow
@@ -349,35 +351,57 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   }
 }
 
-template <int RM, int TIN, bool VEC>
+// One kernel per (widths, full/ragged), chosen on the host, each with ONE body: with the eight
+// (quot_check x full x widths) bodies in one kernel the uniform constants spilled 568 SGPRs
+// (v_writelane / v_readlane traffic on the VALU) and took 104 VGPRs.
+// FULL: the main launch, blocks of SMQ_PACK_BLOCK elements. !FULL: the ragged last
+// block, launched as one workgroup after the main launch (its look-back finds every predecessor
+// published).
+template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO>
 __global__ __launch_bounds__(kBlock) void smaq_pack_kernel(PackArgs A) {
   extern __shared__ uint32_t pack_lds[];  // [stage_words] stage, then [kPB] q values
   uint32_t* stage = pack_lds;
   float* qlds = reinterpret_cast<float*>(pack_lds + A.stage_words);
-  __shared__ uint32_t s_b;
-  if (threadIdx.x == 0) {
-    const uint32_t id = atomicAdd(A.counter, 1u);  // block ids in start order
-    if (id == A.n_blocks - 1) atomicExch(A.counter, 0u);  // every id is taken: reset for reuse
-    s_b = id;
+  uint32_t b;
+  if (FULL) {
+    if (A.ticketed) {  // block ids in start order: predecessors are resident by construction
+      __shared__ uint32_t s_b;
+      if (threadIdx.x == 0) {
+        const uint32_t id = atomicAdd(A.counter, 1u);
+        if (id == A.n_full - 1) atomicExch(A.counter, 0u);  // every id is taken: reset for reuse
+        s_b = id;
+      }
+      __syncthreads();
+      b = s_b;
+    } else {  // index order (see SMQ_PACK_TICKETED in smq.h)
+      b = blockIdx.x;
+    }
+  } else {
+    b = A.n_blocks - 1;
   }
-  __syncthreads();
-  const uint32_t b = s_b;
   ElemConsts c;
   const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);  // z is compared in its type
   init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
-  const bool full = (int64_t)(b + 1) * kPB <= A.n;
+  // SUB = true regardless of stats->quot_check: the IEEE re-division of a subnormal quotient is
+  // exact either way, and one body (no device-side dispatch) keeps the constants in registers
+  pack_body<RM, TIN, true, VEC, FULL, WM, WO>(A, c, b, stage, qlds);
+}
+
+template <int RM, int TIN>
+void launch_pack(const PackArgs& A, bool vec, size_t lds, hipStream_t st) {
   const bool w57 = A.wm == 5 && A.wo == 7;  // the default 6/8-bit budget, widths compiled in
-#define SMQ_PACK_BODY(SUBV, FULLV)                                          \
-  do {                                                                      \
-    if (w57) pack_body<RM, TIN, SUBV, VEC, FULLV, 5, 7>(A, c, b, stage, qlds);   \
-    else pack_body<RM, TIN, SUBV, VEC, FULLV, 0, 0>(A, c, b, stage, qlds);       \
-  } while (0)
-  if (A.stats->quot_check) {
-    if (full) SMQ_PACK_BODY(true, true); else SMQ_PACK_BODY(true, false);
-  } else {
-    if (full) SMQ_PACK_BODY(false, true); else SMQ_PACK_BODY(false, false);
+  const dim3 grid(A.n_full), block(kBlock);
+  if (A.n_full > 0) {
+    if (vec) {
+      if (w57) hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, true, true, 5, 7>), grid, block, lds, st, A);
+      else hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, true, true, 0, 0>), grid, block, lds, st, A);
+    } else {
+      if (w57) hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, false, true, 5, 7>), grid, block, lds, st, A);
+      else hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, false, true, 0, 0>), grid, block, lds, st, A);
+    }
   }
-#undef SMQ_PACK_BODY
+  if (A.n_full < A.n_blocks)
+    hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, false, false, 0, 0>), dim3(1), block, lds, st, A);
 }
 
 // SMQ_PACK_PLACE=atomic: the stream size is the cursor (written after the packing launch).
@@ -575,6 +599,12 @@ size_t smq_smaq_pack_workspace_bytes(int64_t n) {
 
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* packed,
                       size_t packed_bytes, void* ws, size_t ws_bytes, void* stream) {
+  return smq_smaq_compress_ex(x, dtype, n, p, packed, packed_bytes, ws, ws_bytes, 0u, stream);
+}
+
+int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParams* p,
+                         void* packed, size_t packed_bytes, void* ws, size_t ws_bytes,
+                         uint32_t flags, void* stream) {
   int rc = smaq_validate(p, dtype);
   if (rc) return rc;
   if (n < 1 || !x || !packed) {
@@ -653,6 +683,8 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
   A.wm = A.bm - 1;
   A.wo = A.bo - 1;
   A.n_blocks = (uint32_t)nb;
+  A.n_full = (uint32_t)(n / kPB);
+  A.ticketed = (flags & SMQ_PACK_TICKETED) ? 1 : 0;
   A.flags = (p->all_positive ? 1u : 0u) | (R.safe_q ? 2u : 0u);
   // stage: w[0] + mask + the code stream at its widest (every element an outlier) + 1 word of
   // slack for the two-word ORs, rounded to 4 words so the q values after it are 16-B aligned
@@ -665,24 +697,16 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
   }
   const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
   const bool sr = p->stochastic_rounding != 0;
-#define SMQ_PACK(RMV, TINV)                                                                   \
-  do {                                                                                         \
-    if (vec)                                                                                   \
-      hipLaunchKernelGGL((smaq_pack_kernel<RMV, TINV, true>), dim3((unsigned)nb), dim3(kBlock), \
-                         lds_bytes, st, A);                                                    \
-    else                                                                                       \
-      hipLaunchKernelGGL((smaq_pack_kernel<RMV, TINV, false>), dim3((unsigned)nb),             \
-                         dim3(kBlock), lds_bytes, st, A);                                      \
-  } while (0)
-#define SMQ_PACK_T(TINV)                                  \
-  do {                                                    \
-    if (sr) SMQ_PACK(kRoundHash, TINV); else SMQ_PACK(kRoundTrunc, TINV); \
-  } while (0)
-  if (dtype == SMQ_DTYPE_F32) SMQ_PACK_T(kF32);
-  else if (dtype == SMQ_DTYPE_F16) SMQ_PACK_T(kF16);
-  else SMQ_PACK_T(kBF16);
-#undef SMQ_PACK_T
-#undef SMQ_PACK
+  if (dtype == SMQ_DTYPE_F32) {
+    if (sr) launch_pack<kRoundHash, kF32>(A, vec, lds_bytes, st);
+    else launch_pack<kRoundTrunc, kF32>(A, vec, lds_bytes, st);
+  } else if (dtype == SMQ_DTYPE_F16) {
+    if (sr) launch_pack<kRoundHash, kF16>(A, vec, lds_bytes, st);
+    else launch_pack<kRoundTrunc, kF16>(A, vec, lds_bytes, st);
+  } else {
+    if (sr) launch_pack<kRoundHash, kBF16>(A, vec, lds_bytes, st);
+    else launch_pack<kRoundTrunc, kBF16>(A, vec, lds_bytes, st);
+  }
   if (A.place_atomic)
     hipLaunchKernelGGL(smaq_pack_total_kernel, dim3(1), dim3(kWave), 0, st, A.hdr, A.cursor,
                        A.n_blocks);

@@ -26,6 +26,7 @@ SMQ_WS_OUTLIER_SLOTS = 64
 SMQ_STATS_WORKSPACE = 0
 SMQ_STATS_SAMPLED = 1
 SMQ_STATS_INJECTED = 2
+SMQ_PACK_TICKETED = 1
 SMQ_DTYPE_F32 = 0
 SMQ_DTYPE_F16 = 1
 SMQ_DTYPE_BF16 = 2
@@ -139,6 +140,7 @@ _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 _I32 = ctypes.c_int
 _U64 = ctypes.c_uint64
+_U32 = ctypes.c_uint32
 _SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); every function declared in include/smq.h
@@ -197,6 +199,8 @@ SIGNATURES = {
     "smq_smaq_pack_workspace_bytes": (_SZ, [_I64]),
     "smq_smaq_compress": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams),
                                          _P, _SZ, _P, _SZ, _P]),
+    "smq_smaq_compress_ex": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams),
+                                     _P, _SZ, _P, _SZ, _U32, _P]),
     "smq_smaq_decompress": (_I32, [_P, _P, _I64, _P]),
 }
 

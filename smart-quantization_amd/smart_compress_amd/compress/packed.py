@@ -91,13 +91,18 @@ class SmartFPPacked(SmartFP):
         bound = lib.smq_smaq_pack_bound(numel, hp.num_bits_main, hp.num_bits_outlier)
         scratch = N.workspace("smaq_pack_out", x.device, bound)
         ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(numel))
-        N.check(lib.smq_smaq_compress(x.data_ptr(), code, numel, p, scratch.data_ptr(),
-                                      scratch.numel(), ws.data_ptr(), ws.numel(),
-                                      N.stream_ptr(x.device)), "smq_smaq_compress")
-        tail = scratch[_TOTAL_OFF:_ERROR_OFF + 4].cpu().numpy()  # host sync: the stream size
-        total = int(tail[:8].view(np.uint64)[0])
-        if int(tail[_ERROR_OFF - _TOTAL_OFF:].view(np.uint32)[0]) != 0:
+        # index-ordered packing; if the block scan ever gives up (it assumes each XCD starts its
+        # workgroups in index order), re-pack with ticketed block ids (same bytes, no assumption)
+        for flags in (0, N.SMQ_PACK_TICKETED):
+            N.check(lib.smq_smaq_compress_ex(x.data_ptr(), code, numel, p, scratch.data_ptr(),
+                                             scratch.numel(), ws.data_ptr(), ws.numel(), flags,
+                                             N.stream_ptr(x.device)), "smq_smaq_compress_ex")
+            tail = scratch[_TOTAL_OFF:_ERROR_OFF + 4].cpu().numpy()  # host sync: the stream size
+            if int(tail[_ERROR_OFF - _TOTAL_OFF:].view(np.uint32)[0]) == 0:
+                break
+        else:
             raise RuntimeError("smq_smaq_compress: block scan gave up (stream marked broken)")
+        total = int(tail[:8].view(np.uint64)[0])
         return SmaqPacked(scratch[:total].clone(), data.shape, numel)
 
     def decompress(self, packed: SmaqPacked) -> torch.Tensor:

@@ -203,3 +203,34 @@ def test_compress_is_repeatable():
     pk.rng.offset = 0
     b = pk.compress(x).data
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [4096, 3 * 4096 + 77, (1 << 22) + 5])
+def test_ticketed_and_index_order_give_the_same_bytes(n):
+    """smq_smaq_compress_ex: index-ordered block ids (default) and SMQ_PACK_TICKETED ids place
+    block b after blocks 0..b-1 either way: byte-identical streams (twice each: the ticket counter
+    resets itself)."""
+    from smart_compress_amd import _native as N
+
+    hp, pk, _ = _codecs(seed=9, offset=5)
+    gen = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(n, generator=gen, device="cuda")
+    x[::501] *= 30.0
+    lib = N.lib()
+    p = pk._params(n, False, x.dtype, x.device)
+    bound = lib.smq_smaq_pack_bound(n, hp.num_bits_main, hp.num_bits_outlier)
+    ws = torch.zeros(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    outs = []
+    for flags in (0, N.SMQ_PACK_TICKETED, N.SMQ_PACK_TICKETED, 0):
+        out = torch.zeros(bound, dtype=torch.uint8, device="cuda")
+        N.check(lib.smq_smaq_compress_ex(x.data_ptr(), N.SMQ_DTYPE_F32, n, p, out.data_ptr(),
+                                         out.numel(), ws.data_ptr(), ws.numel(), flags,
+                                         N.stream_ptr(x.device)), "compress_ex")
+        outs.append(out)
+    torch.cuda.synchronize()
+    to, eo = N.SmqPackedHeader.total_bytes.offset, N.SmqPackedHeader.error.offset
+    total = int(outs[0][to:to + 8].cpu().numpy().view(np.uint64)[0])
+    assert int(outs[0][eo:eo + 4].cpu().numpy().view(np.uint32)[0]) == 0
+    assert total > 128
+    for o in outs[1:]:
+        assert torch.equal(o[:total], outs[0][:total])
