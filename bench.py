@@ -298,7 +298,7 @@ def run_s2fp8(args, world, rank, device):
 
     shape = (32, 128, 768)
     n = int(np.prod(shape))
-    nbuf = 48
+    nbuf = int(os.environ.get("SMQ_BENCH_NBUF", "48"))  # measurement knob: 1 = MALL/TLB-warm
     hp = S2FP8.add_argparse_args(ArgumentParser()).parse_args([])
     hp.precision = 32
     codec = S2FP8(hp)

@@ -246,55 +246,80 @@ __device__ void s2fp8_finalize(double s, float m, int64_t n, SmqS2fp8Stats* out)
   s2fp8_derive<TIN>(mu, m, (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n), out);
 }
 
-constexpr int kS2GridCap = 1024;  // one sweep front, <= 1024 partials (smaq.hip)
+// Statistics partials. The old shape (last-arriving workgroup reduces, one counter) paid ~12 ns of
+// serialised atomic per arriving workgroup plus the tail workgroup's reduction round trip, and
+// its tile-stride loop one HBM round trip per 16 KiB tile: 11.6 us at C4 for 12.6 MB. Here every
+// workgroup issues all loads of a round (kS2Loads dwordx4 per lane) before consuming any, stores
+// one plain partial and exits; the apply launch (after the kernel boundary, which makes the
+// partials visible) reduces the <= kS2Partials partials in every workgroup, in one fixed order.
+// Measured at C4 (rocprofv3, 48 rotating buffers): partials 7.7 us + apply 10.3 us, step 17.4 us
+// (was 19.1); the same partials with a last-arriver derive instead: 10.8 + 7.4, step 18.4 us.
+// 128 / 64 partials: 9.7 / 14.9 us (per-CU bandwidth: one workgroup per CU).
+constexpr int kS2Partials = kBlock;  // one partial per lane of an apply workgroup
+constexpr int kS2Loads = 16;         // dwordx4 per lane in flight per round
+
+// float4 groups per partial workgroup (>= 1 round of one load per lane); depends on n only, so
+// the summation order — and the statistics — are a function of n
+static inline int64_t s2_groups_per_wg(int64_t ng) {
+  static const int np = [] {  // measurement knob SMQ_S2_PARTIALS (<= kS2Partials)
+    const char* e = getenv("SMQ_S2_PARTIALS");
+    const int v = e ? atoi(e) : kS2Partials;
+    return (v >= 1 && v <= kS2Partials) ? v : kS2Partials;
+  }();
+  int64_t per = (ng + np - 1) / np;
+  const int64_t q = kBlock;  // whole lanes
+  per = (per + q - 1) / q * q;
+  return per < q ? q : per;
+}
 
 template <int TIN>
-__global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const void* __restrict__ x, int64_t n,
-                                                             int vec, S2Partial* partials,
-                                                             uint32_t* counter,
-                                                             SmqS2fp8Stats* out,
-                                                             uint64_t* rng_ctr) {
+__global__ __launch_bounds__(kBlock) void s2fp8_partial_kernel(const void* __restrict__ x, int64_t n,
+                                                               int vec, int64_t per,
+                                                               S2Partial* __restrict__ partials,
+                                                               SmqS2fp8Stats* out,
+                                                               uint64_t* rng_ctr) {
   // graph-safe random stream: one snapshot + advance per call, read by the apply launch
   if (blockIdx.x == 0 && threadIdx.x == 0) out->rng_offset = take_offset(rng_ctr, (uint64_t)n);
   __shared__ double shs[kBlock / kWave];
   __shared__ float shm[kBlock / kWave];
-  __shared__ uint32_t slot;
-  // tile-stride: each step a workgroup consumes a 16 KiB tile with 4 dwordx4 per lane in flight
-  // (S2FP8 tensors are MB-sized: latency, not sweep fronts, is what bounds them)
   double s = 0.0;
   float m = -INFINITY;
   if (vec) {
+    // groups [g0, g1) of this workgroup; lane t takes g0 + t + k * kBlock
     const int64_t nv = n >> 2;
-    for (int64_t t0 = (int64_t)blockIdx.x * (kBlock * 4); t0 < nv; t0 += (int64_t)gridDim.x * kBlock * 4) {
-      float4 v[4];
+    const int64_t g0 = (int64_t)blockIdx.x * per;
+    const int64_t g1 = (g0 + per < nv) ? g0 + per : nv;
+    for (int64_t r0 = g0 + threadIdx.x; r0 < g1; r0 += (int64_t)kS2Loads * kBlock) {
+      float4 v[kS2Loads];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t j = t0 + threadIdx.x + u * kBlock;
-        v[u] = j < nv ? load4<TIN>(x, j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < kS2Loads; ++u) {
+        const int64_t j = r0 + (int64_t)u * kBlock;
+        if (j < g1) v[u] = load4<TIN>(x, j);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t j = t0 + threadIdx.x + u * kBlock;
-        if (j >= nv) continue;
+      for (int u = 0; u < kS2Loads; ++u) {
+        const int64_t j = r0 + (int64_t)u * kBlock;
+        if (j >= g1) continue;
         const float l0 = s2_log<TIN>(v[u].x), l1 = s2_log<TIN>(v[u].y), l2 = s2_log<TIN>(v[u].z),
                     l3 = s2_log<TIN>(v[u].w);
         s += ((double)l0 + (double)l1) + ((double)l2 + (double)l3);
         m = nan_max(nan_max(m, l0), nan_max(l1, nan_max(l2, l3)));
       }
     }
-    if (blockIdx.x == 0 && threadIdx.x < (int)(n & 3)) {
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
       const float l = s2_log<TIN>(load1<TIN>(x, (nv << 2) + threadIdx.x));
       s += (double)l;
       m = nan_max(m, l);
     }
   } else {
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t e0 = (int64_t)blockIdx.x * per * 4;
+    const int64_t e1 = (e0 + per * 4 < n) ? e0 + per * 4 : n;
+    for (int64_t i = e0 + threadIdx.x; i < e1; i += kBlock) {
       const float l = s2_log<TIN>(load1<TIN>(x, i));
       s += (double)l;
       m = nan_max(m, l);
     }
   }
-  // workgroup reduce
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   s = wave_sum(s);
 #pragma unroll
@@ -305,49 +330,56 @@ __global__ __launch_bounds__(kBlock) void s2fp8_stats_kernel(const void* __restr
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    S2Partial* p = partials + blockIdx.x;
-    st_sc1_f64(&p->s, (shs[0] + shs[1]) + (shs[2] + shs[3]));
-    st_sc1_f32x2(&p->m, nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3])), 0.0f);
+    S2Partial p;
+    p.s = (shs[0] + shs[1]) + (shs[2] + shs[3]);
+    p.m = nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3]));
+    p.pad = 0.0f;
+    partials[blockIdx.x] = p;
   }
-  const uint32_t prev = block_arrive(counter, &slot);
-  if (prev != gridDim.x - 1) return;
-  // every load of a lane issued before any is consumed (one round trip, not one per partial)
-  constexpr int K = kS2GridCap / kBlock;
-  double sv[K];
-  float mv[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    const int b = threadIdx.x + i * kBlock;
-    if (b < (int)gridDim.x) {
-      float pad;
-      sv[i] = ld_sc1_f64(&partials[b].s);
-      ld_sc1_f32x2(&partials[b].m, mv[i], pad);
-    }
+}
+
+// Every apply workgroup: reduce the P partials (lane t holds partial t) in one fixed order and
+// derive alpha, beta, ... into *st (LDS). Block 0 also publishes them in the workspace header.
+template <int TIN>
+__device__ __forceinline__ void s2_reduce_partials(const S2Partial* __restrict__ partials, int P,
+                                                   int64_t n, SmqS2fp8Stats* hdr,
+                                                   SmqS2fp8Stats* st) {
+  __shared__ double shs[kBlock / kWave];
+  __shared__ float shm[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  double s = 0.0;
+  float m = -INFINITY;
+  if ((int)threadIdx.x < P) {
+    const S2Partial p = partials[threadIdx.x];
+    s = p.s;
+    m = p.m;
   }
-  double ts = 0.0;
-  float tm = -INFINITY;
+  s = wave_sum(s);
 #pragma unroll
-  for (int i = 0; i < K; ++i) {
-    if (threadIdx.x + i * kBlock < (int)gridDim.x) {
-      ts += sv[i];
-      tm = nan_max(tm, mv[i]);
-    }
-  }
-  ts = wave_sum(ts);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) tm = nan_max(tm, __shfl_xor(tm, o, kWave));
-  __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o, kWave));
   if (lane == 0) {
-    shs[wave] = ts;
-    shm[wave] = tm;
+    shs[wave] = s;
+    shm[wave] = m;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     const double S = (shs[0] + shs[1]) + (shs[2] + shs[3]);
     const float M = nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3]));
-    s2fp8_finalize<TIN>(S, M, n, out);
-    *counter = 0u;
+    SmqS2fp8Stats d;
+    s2fp8_finalize<TIN>(S, M, n, &d);
+    *st = d;
+    if (blockIdx.x == 0) {  // the header (all fields but rng_offset, owned by the partial launch)
+      hdr->mu = d.mu;
+      hdr->m = d.m;
+      hdr->alpha = d.alpha;
+      hdr->beta = d.beta;
+      hdr->beta_pow2 = d.beta_pow2;
+      hdr->inv_beta_pow2 = d.inv_beta_pow2;
+      hdr->inv_alpha = d.inv_alpha;
+      hdr->n_used = d.n_used;
+    }
   }
+  __syncthreads();
 }
 
 // Injected (mu, m): derive the rest exactly like the finaliser (parity tests).
@@ -365,7 +397,9 @@ struct S2Args {
   void* y;
   int64_t n;
   const uint32_t* rand_bits;
-  const SmqS2fp8Stats* st;
+  SmqS2fp8Stats* st;            // workspace header (derived stats, or the rng snapshot only)
+  const S2Partial* partials;    // PART: the partial launch's output
+  int n_partials;
   uint32_t key;
   uint64_t offset;
   int check_inf;
@@ -427,14 +461,33 @@ __device__ __forceinline__ float s2fp8_elem16(float xv, uint32_t r, float alpha,
 template <int TIN, bool P16>
 constexpr bool s2_half_out() { return P16 && TIN == kF16; }
 
-template <bool RARR, bool VEC, int kFqTileV, int TIN, bool P16>
+// PART: reduce the partial launch's output first (s2_reduce_partials), else read the header that
+// s2fp8_derive_kernel wrote (injected mu, m).
+template <bool RARR, bool VEC, int kFqTileV, int TIN, bool P16, bool PART>
 __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   constexpr int kFqTileElems = kBlock * kFqTileV * 4;
   constexpr bool HOUT = s2_half_out<TIN, P16>();
-  const float alpha = A.st->alpha, bp2 = A.st->beta_pow2, ibp2 = A.st->inv_beta_pow2,
-              ialpha = A.st->inv_alpha;
-  const float ialpha_e = P16 ? s2_round<kF16>(ialpha) : ialpha;
+  __shared__ SmqS2fp8Stats sst;
   const int64_t n = A.n;
+  // the tile's loads go out before the statistics are reduced
+  const int64_t nv = n >> 2;
+  const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kFqTileV) + threadIdx.x;
+  float4 v[kFqTileV];
+  if (VEC) {
+#pragma unroll
+    for (int u = 0; u < kFqTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j < nv) v[u] = load4<TIN>(A.x, j);
+    }
+  }
+  const SmqS2fp8Stats* st = A.st;
+  if (PART) {
+    s2_reduce_partials<TIN>(A.partials, A.n_partials, n, A.st, &sst);
+    st = &sst;
+  }
+  const float alpha = st->alpha, bp2 = st->beta_pow2, ibp2 = st->inv_beta_pow2,
+              ialpha = st->inv_alpha;
+  const float ialpha_e = P16 ? s2_round<kF16>(ialpha) : ialpha;
   const uint64_t off = A.offset + A.st->rng_offset;
   auto rb = [&](int64_t e) -> uint32_t {
     return RARR ? A.rand_bits[e] : rng_u32(A.key, off + (uint64_t)e);
@@ -448,14 +501,6 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
                 : s2fp8_elem<false>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
   };
   if (VEC) {
-    const int64_t nv = n >> 2;
-    const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kFqTileV) + threadIdx.x;
-    float4 v[kFqTileV];
-#pragma unroll
-    for (int u = 0; u < kFqTileV; ++u) {
-      const int64_t j = t0 + u * kBlock;
-      if (j < nv) v[u] = load4<TIN>(A.x, j);
-    }
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
       const int64_t j = t0 + u * kBlock;
@@ -498,25 +543,25 @@ static int fq_grid(int64_t n) {  // flat tiles
   return (int)(g < 1 ? 1 : g);
 }
 
-static int s2_stats_grid(int64_t n) {  // 16 KiB tiles, at most kS2GridCap workgroups
-  static const int cap = [] {  // measurement knob SMQ_S2_STATS_GRID
-    const char* e = getenv("SMQ_S2_STATS_GRID");
-    const int v = e ? atoi(e) : kS2GridCap;
-    return (v >= 1 && v <= kS2GridCap) ? v : kS2GridCap;
-  }();
-  // four 16 KiB tiles per workgroup: fewer arrivals to wait for (3.1M elements: 192 workgroups
-  // 11.6 us vs 768 workgroups 15.2 us, rocprofv3 r03)
-  int64_t g = (n + kBlock * 64 - 1) / (kBlock * 64);
-  if (g < 1) g = 1;
-  if (g > cap) g = cap;
-  return (int)g;
+template <int TV, int TIN, bool P16>
+static void s2_launch(const S2Args& A, bool rarr, bool vec, bool part, int grid, hipStream_t st) {
+#define SMQ_S2(R, V, P) \
+  hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, TV, TIN, P16, P>), dim3(grid), dim3(kBlock), 0, st, A)
+  if (part) {
+    if (rarr) { if (vec) SMQ_S2(true, true, true); else SMQ_S2(true, false, true); }
+    else { if (vec) SMQ_S2(false, true, true); else SMQ_S2(false, false, true); }
+  } else {
+    if (rarr) { if (vec) SMQ_S2(true, true, false); else SMQ_S2(true, false, false); }
+    else { if (vec) SMQ_S2(false, true, false); else SMQ_S2(false, false, false); }
+  }
+#undef SMQ_S2
 }
 
 static float host_max_value(int exp_bits, int man_bits) {
   return qtorch_quant(FLT_MAX, 0u, exp_bits, man_bits, false);
 }
 
-static size_t s2_ws_bytes() { return 128 + sizeof(S2Partial) * (size_t)kS2GridCap; }
+static size_t s2_ws_bytes() { return 128 + sizeof(S2Partial) * (size_t)kS2Partials; }
 
 }  // namespace smq
 
@@ -652,25 +697,29 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
   hipStream_t st = (hipStream_t)stream;
   char* base = (char*)ws;
   SmqS2fp8Stats* hdr = (SmqS2fp8Stats*)base;
-  uint32_t* counter = (uint32_t*)(base + 64);
   S2Partial* partials = (S2Partial*)(base + 128);
   const uintptr_t align = dtype == SMQ_DTYPE_F32 ? 15u : 7u;  // one 4-element group per lane
   const bool xal = ((uintptr_t)x & align) == 0;
-  if (stats_in) {
+  const bool part = stats_in == nullptr;
+  int n_partials = 0;
+  if (!part) {
     if (dtype == SMQ_DTYPE_F32) hipLaunchKernelGGL(s2fp8_derive_kernel<kF32>, dim3(1), dim3(64), 0, st, stats_in, hdr, offset_counter, (uint64_t)n);
     else if (dtype == SMQ_DTYPE_F16) hipLaunchKernelGGL(s2fp8_derive_kernel<kF16>, dim3(1), dim3(64), 0, st, stats_in, hdr, offset_counter, (uint64_t)n);
     else hipLaunchKernelGGL(s2fp8_derive_kernel<kBF16>, dim3(1), dim3(64), 0, st, stats_in, hdr, offset_counter, (uint64_t)n);
   } else {
-    const int grid = s2_stats_grid(n);
     const int vec = xal ? 1 : 0;
-    if (dtype == SMQ_DTYPE_F32)
-      hipLaunchKernelGGL(s2fp8_stats_kernel<kF32>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr, offset_counter);
-    else if (dtype == SMQ_DTYPE_F16)
-      hipLaunchKernelGGL(s2fp8_stats_kernel<kF16>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr, offset_counter);
-    else
-      hipLaunchKernelGGL(s2fp8_stats_kernel<kBF16>, dim3(grid), dim3(kBlock), 0, st, x, n, vec, partials, counter, hdr, offset_counter);
+    const int64_t ng = vec ? (n >> 2) : (n + 3) / 4;
+    const int64_t per = s2_groups_per_wg(ng);
+    int64_t g = (ng + per - 1) / per;
+    if (g < 1) g = 1;  // n < 4: the tail alone
+    n_partials = (int)g;
+#define SMQ_S2P(T) hipLaunchKernelGGL((s2fp8_partial_kernel<T>), dim3(n_partials), dim3(kBlock), 0, st, x, n, vec, per, partials, hdr, offset_counter)
+    if (dtype == SMQ_DTYPE_F32) SMQ_S2P(kF32);
+    else if (dtype == SMQ_DTYPE_F16) SMQ_S2P(kF16);
+    else SMQ_S2P(kBF16);
+#undef SMQ_S2P
   }
-  int rc = check_launch("s2fp8_stats_kernel");
+  int rc = check_launch(stats_in ? "s2fp8_derive_kernel" : "s2fp8_partial_kernel");
   if (rc) return rc;
   S2Args A;
   A.x = x;
@@ -678,6 +727,8 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
   A.n = n;
   A.rand_bits = rand_bits;
   A.st = hdr;
+  A.partials = partials;
+  A.n_partials = n_partials;
   A.key = rng_key(seed);
   A.offset = offset;
   A.check_inf = check_inf;
@@ -685,37 +736,18 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
   const bool rarr = rand_bits != nullptr;
   const bool half_out = precision == 16 && dtype == SMQ_DTYPE_F16;
   const bool vec = xal && ((uintptr_t)y & (half_out ? 7u : 15u)) == 0;
-  const int grid = fq_grid(n);
-  const int tv = fq_tile_v();
+  const int tv = precision == 32 ? fq_tile_v() : kFqDefaultTileV;
+  const int grid = (int)((n + (int64_t)kBlock * 4 * tv - 1) / ((int64_t)kBlock * 4 * tv));
   if (precision == 32) {
-#define SMQ_S2(R, V)                                                                             \
-  do {                                                                                           \
-    if (tv == 1) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 1, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
-    else if (tv == 2) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 2, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
-    else hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, 4, kF32, false>), dim3(grid), dim3(kBlock), 0, st, A); \
-  } while (0)
-    if (rarr) {
-      if (vec) SMQ_S2(true, true); else SMQ_S2(true, false);
-    } else {
-      if (vec) SMQ_S2(false, true); else SMQ_S2(false, false);
-    }
-#undef SMQ_S2
+    if (tv == 1) s2_launch<1, kF32, false>(A, rarr, vec, part, grid, st);
+    else if (tv == 2) s2_launch<2, kF32, false>(A, rarr, vec, part, grid, st);
+    else s2_launch<4, kF32, false>(A, rarr, vec, part, grid, st);
   } else {
-    // precision 16: the tile knob is not swept here (fq_grid's tile must match kFqDefaultTileV)
-    const int g16 = (int)((n + (int64_t)kBlock * 4 * kFqDefaultTileV - 1) / ((int64_t)kBlock * 4 * kFqDefaultTileV));
-#define SMQ_S2H(T, R, V) hipLaunchKernelGGL((s2fp8_apply_kernel<R, V, kFqDefaultTileV, T, true>), dim3(g16), dim3(kBlock), 0, st, A)
-#define SMQ_S2T(T)                                               \
-  do {                                                           \
-    if (rarr) { if (vec) SMQ_S2H(T, true, true); else SMQ_S2H(T, true, false); } \
-    else { if (vec) SMQ_S2H(T, false, true); else SMQ_S2H(T, false, false); }    \
-  } while (0)
-    if (dtype == SMQ_DTYPE_F32) SMQ_S2T(kF32);
-    else if (dtype == SMQ_DTYPE_F16) SMQ_S2T(kF16);
-    else SMQ_S2T(kBF16);
-#undef SMQ_S2T
-#undef SMQ_S2H
+    // precision 16: the tile knob is not swept here
+    if (dtype == SMQ_DTYPE_F32) s2_launch<kFqDefaultTileV, kF32, true>(A, rarr, vec, part, grid, st);
+    else if (dtype == SMQ_DTYPE_F16) s2_launch<kFqDefaultTileV, kF16, true>(A, rarr, vec, part, grid, st);
+    else s2_launch<kFqDefaultTileV, kBF16, true>(A, rarr, vec, part, grid, st);
   }
-  (void)grid;
   return check_launch("s2fp8_apply_kernel");
 }
 

@@ -245,17 +245,21 @@ def test_s2fp8_edge_cases():
     assert np.isfinite(yh).all()
 
 
-@pytest.mark.parametrize("n", [3 * 2**20 + 3, 12 * 2**20 + 1])
-def test_s2fp8_single_launch_and_two_launch_paths(n):
-    """n that fits in registers across the grid (one cooperative launch) and n that does not (stats
-    + apply launches): both match the oracle with the device's own statistics and counter RNG."""
+@pytest.mark.parametrize("n,shift", [(1, 0), (3, 0), (5, 1), (1027, 1), (3 * 2**20 + 3, 0),
+                                     (3 * 2**20 + 3, 1), (12 * 2**20 + 1, 0), (40 * 2**20 + 2, 0)])
+def test_s2fp8_partials_vs_oracle(n, shift):
+    """Statistics partials (one per workgroup, several load rounds per workgroup at 40M) reduced by
+    every apply workgroup; aligned and unaligned (x[1:], element path) inputs, tails of 1-3
+    elements: match the oracle with the device's own statistics and counter RNG."""
     from oracle import rng as orng
     from oracle import s2fp8 as os2
 
     g = _g()
     gen = torch.Generator(device="cuda").manual_seed(n)
-    x = torch.randn(n, generator=gen, device="cuda")
+    x = torch.randn(n + shift, generator=gen, device="cuda")[shift:]
     x[::7] = 0.0
+    if n == 1:
+        x[0] = 0.75
     y, st = g.s2fp8(x, check_inf=True, seed=11, offset=5)
     xh = x.cpu().numpy()
     own = os2.stats(xh)
@@ -263,4 +267,7 @@ def test_s2fp8_single_launch_and_two_launch_paths(n):
     assert ulp_diff(st["m"], own["m"]) <= 1
     words = orng.rng_u32(11, 5, n)
     ref = os2.roundtrip(xh, words, True, st=os2.derive(st["mu"], st["m"]))
-    _assert_code_domain(y.cpu().numpy(), ref[0])
+    if np.isnan(ref[0]).all():  # one element: m == mu, alpha = inf -> NaN like the reference
+        assert np.isnan(y.cpu().numpy()).all()
+    else:
+        _assert_code_domain(y.cpu().numpy(), ref[0])

@@ -26,7 +26,7 @@ SHORT = {
     "smaq_multi_stats_kernel": "smaq_multi_stats_kernel",
     "smaq_multi_apply_kernel": "smaq_multi_apply_kernel",
     "float_quant_kernel": "float_quant_kernel",
-    "s2fp8_stats_kernel": "s2fp8_stats_kernel",
+    "s2fp8_partial_kernel": "s2fp8_partial_kernel",
     "s2fp8_apply_kernel": "s2fp8_apply_kernel",
     "smaq_pack_kernel": "smaq_pack_kernel",
     "smaq_unpack_kernel": "smaq_unpack_kernel",
