@@ -444,12 +444,13 @@ __device__ __forceinline__ float decode_code(uint32_t v, bool is_o, int wm, int 
   return is_o ? (float)(lo ? -mag : mag) : qm;
 }
 
+// pc / epc / esc_mask: kMaskWords LDS words each, declared once by the kernel (a __shared__ array
+// inside this template is one allocation PER INSTANTIATION: 16 bodies took 37 KB of LDS per
+// workgroup, 4 workgroups per CU)
 template <bool AP, bool SQ, bool FULL, int WM, int WO>
 __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
-                                            int wm_rt, int wo_rt, uint32_t* stage) {
-  __shared__ uint32_t pc[kMaskWords];
-  __shared__ uint32_t epc[kMaskWords];
-  __shared__ uint32_t esc_mask[kMaskWords];
+                                            int wm_rt, int wo_rt, uint32_t* stage, uint32_t* pc,
+                                            uint32_t* epc, uint32_t* esc_mask) {
   constexpr bool kWindow = WO > 0 && WO <= 8;  // a lane's 4 codes fit one 32-bit window
   const int wm = WM > 0 ? WM : wm_rt, wo = WO > 0 ? WO : wo_rt;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
@@ -530,6 +531,7 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
 
 __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   __shared__ uint32_t stage[kStageWords];
+  __shared__ uint32_t pc[kMaskWords], epc[kMaskWords], esc_mask[kMaskWords];
   const SmqPackedHeader* h = A.hdr;
   if (h->magic != SMQ_PACK_MAGIC || h->version != SMQ_PACK_VERSION || h->n != A.n) return;
   const int wm = h->num_bits_main - 1, wo = h->num_bits_outlier - 1;
@@ -551,8 +553,8 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   const bool w57 = wm == 5 && wo == 7;
 #define SMQ_UNPACK_W(APV, SQV, FULLV)                                                 \
   do {                                                                                \
-    if (w57) unpack_body<APV, SQV, FULLV, 5, 7>(A, c, b, wm, wo, stage);             \
-    else unpack_body<APV, SQV, FULLV, 0, 0>(A, c, b, wm, wo, stage);                 \
+    if (w57) unpack_body<APV, SQV, FULLV, 5, 7>(A, c, b, wm, wo, stage, pc, epc, esc_mask);             \
+    else unpack_body<APV, SQV, FULLV, 0, 0>(A, c, b, wm, wo, stage, pc, epc, esc_mask);                 \
   } while (0)
 #define SMQ_UNPACK(APV, SQV)                                  \
   do {                                                        \
