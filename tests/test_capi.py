@@ -194,3 +194,22 @@ def test_multi_plan_layout():
     assert lib.smq_smaq_multi_workspace_bytes(arr, count) >= 64 * count + 32 * sum(schunks)
     descs[1].n = 0
     assert lib.smq_smaq_multi_plan_build(descs, count, host, nbytes) == -1
+
+
+def test_integration_doc_binding_matches_the_library_struct():
+    """INTEGRATION.md's ctypes mirror of SmqSmaqParams (the binding a maintainer copies into
+    smart.py) has the library's field names, offsets and size: a short mirror would let the library
+    read offset_counter from past the end of the caller's struct."""
+    import ctypes as C
+
+    from smart_compress_amd import _native as N
+
+    doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = re.search(r"class SmqSmaqParams\(ctypes.Structure\):.*?\)\][^\n]*\n", doc, flags=re.S).group(0)
+    ns = {"ctypes": C}
+    exec(block, ns)
+    mirror = ns["SmqSmaqParams"]
+    assert C.sizeof(mirror) == C.sizeof(N.SmqSmaqParams)
+    lib_fields = [(f[0], getattr(N.SmqSmaqParams, f[0]).offset) for f in N.SmqSmaqParams._fields_]
+    doc_fields = [(f[0], getattr(mirror, f[0]).offset) for f in mirror._fields_]
+    assert doc_fields == lib_fields
