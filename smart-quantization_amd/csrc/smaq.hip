@@ -54,16 +54,19 @@ static int grid_for(int64_t work_items, int per_block_items, int cap) {
 }
 
 // Memory shapes measured on MI355X (tools/membench.hip, tools/statsbench.hip, profiles/): a read
-// stream peaks with ONE 16-B load per lane in flight and the whole grid sweeping the buffer in
-// address order (grid-stride over ~1-2k workgroups); several loads per lane at grid-stride
-// distance open several sweep fronts (-20 %). A read+write stream is fastest as flat contiguous
-// tiles, one per workgroup; with the stochastic-rounding ALU chain 2 vector slots per lane beat 1
-// and 4 (cold-cache sweep, profiles/r02_kbench_cold_tile*.json), truncation prefers 1.
+// stream wants the whole grid sweeping the buffer in address order with ONE front: grid-stride
+// single loads over ~2k workgroups, or (better, r04) tile-stride over 512 workgroups where each
+// step of a workgroup is one contiguous 16 KiB tile and the next tile's loads are in flight while
+// the current one is summed; several loads per lane at grid-stride distance open several sweep
+// fronts (-20 %). A read+write stream is fastest as flat contiguous tiles, one per workgroup; with
+// the stochastic-rounding ALU chain 2 vector slots per lane beat 1 and 4 (cold-cache sweep,
+// profiles/r02_kbench_cold_tile*.json), truncation prefers 1.
 constexpr int kStatsGridCap = 2048;  // also the number of fp64 partials the last workgroup sums
+constexpr int kStatsTileGrid = 512;  // tile-stride sweep: 2 workgroups per CU (launch_stats)
 
 static inline bool aligned(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
-template <bool RANGE, int TIN>
+template <bool RANGE, int TIN, bool TILE = false>
 __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restrict__ x, int64_t n,
                                                             int vec, FinalizeArgs fin,
                                                             StatPartial* __restrict__ partials,
@@ -81,7 +84,36 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
   StatAcc acc, ay, az, aw;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (vec) {
+  if (vec && TILE) {
+    // tile-stride: workgroup w sweeps tiles w, w + G, ... of kBlock * 4 float4 (16 KiB, one
+    // contiguous piece per workgroup and step, one front across the grid); the next tile's four
+    // loads are issued before the current tile is consumed (8 loads per lane in flight at most)
+    const int64_t nv = n >> 2;
+    constexpr int64_t kT = (int64_t)kBlock * 4;
+    const int64_t tstride = (int64_t)gridDim.x * kT;
+    int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x;
+    float4 cur[4], nxt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (t + u * kBlock < nv) cur[u] = load4<TIN>(x, t + u * kBlock);
+    for (; t < nv; t += tstride) {
+      const int64_t tn = t + tstride;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (tn + u * kBlock < nv) nxt[u] = load4<TIN>(x, tn + u * kBlock);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (t + u * kBlock < nv) {
+          acc.add<RANGE>(cur[u].x, shift);
+          ay.add<RANGE>(cur[u].y, shift);
+          az.add<RANGE>(cur[u].z, shift);
+          aw.add<RANGE>(cur[u].w, shift);
+        }
+        cur[u] = nxt[u];
+      }
+    }
+    i = (nv << 2) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  } else if (vec) {
     const int64_t nv = n >> 2;
     for (; i < nv; i += stride) {  // one load in flight per lane: a single sweep front
       const float4 v = load4<TIN>(x, i);
@@ -375,13 +407,25 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   uint32_t* counter = (uint32_t*)(base + SmaqWsLayout::kHeader);
   StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
   const int vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) ? 1 : 0;
-  static const int cap = [] {  // measurement knob SMQ_STATS_GRID (<= kStatsGridCap)
-    const char* e = getenv("SMQ_STATS_GRID");
-    const int v = e ? atoi(e) : kStatsGridCap;
-    return (v >= 64 && v <= kStatsGridCap) ? v : kStatsGridCap;
+  // fp32 sweeps tile-stride (smaq_stats_kernel<.., TILE>) on at most kStatsTileGrid workgroups;
+  // measured on the 256M headline (bench, 3 interleaved rounds): grid-stride at 2048 workgroups
+  // 0.542 ms/step; tile-stride at 1024 / 768 / 640 / 512 / 384 / 256 workgroups 0.529 / 0.528 /
+  // 0.528 / 0.515 / 0.522 / 0.589 — at 512 (2 per CU, 8 dwordx4 per lane in flight) the sweep
+  // takes 169 us instead of 184, and the apply launch after it 335 us instead of 352. fp16 / bf16
+  // inputs (8-B loads) keep the grid-stride sweep (not measured in tile form).
+  static const int tile_env = [] {  // measurement knob SMQ_STATS_TILE=0: grid-stride sweep
+    const char* e = getenv("SMQ_STATS_TILE");
+    return e ? atoi(e) : 1;
   }();
+  const bool tile = tile_env != 0 && dtype == SMQ_DTYPE_F32;
+  static const int grid_env = [] {  // measurement knob SMQ_STATS_GRID (64 .. kStatsGridCap)
+    const char* e = getenv("SMQ_STATS_GRID");
+    const int v = e ? atoi(e) : 0;
+    return (v >= 64 && v <= kStatsGridCap) ? v : 0;
+  }();
+  const int cap = grid_env ? grid_env : (tile ? kStatsTileGrid : kStatsGridCap);
   // >= 16K elements per workgroup: mid-size tensors (activations, 1-30M elements) are bound by
-  // the arrival of their workgroups, not by bandwidth; at 256M the cap decides (2048)
+  // the arrival of their workgroups, not by bandwidth; at 256M the cap decides
   static const int per_wg = [] {  // measurement knob SMQ_STATS_PER_WG (elements, >= 1024)
     const char* e = getenv("SMQ_STATS_PER_WG");
     const int v = e ? atoi(e) : kBlock * 4 * 16;
@@ -390,9 +434,15 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   const int grid = grid_for(n, per_wg, cap);
   FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n),
                    (unsigned long long*)p->offset_counter, n};
-#define SMQ_STATS(RANGE, TIN)                                                                    \
-  hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n, vec, \
-                     fin, partials, counter, hdr)
+#define SMQ_STATS(RANGE, TIN)                                                                       \
+  do {                                                                                              \
+    if (tile)                                                                                       \
+      hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true>), dim3(grid), dim3(kBlock), 0, st, x, \
+                         n, vec, fin, partials, counter, hdr);                                      \
+    else                                                                                            \
+      hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n,    \
+                         vec, fin, partials, counter, hdr);                                         \
+  } while (0)
   if (dtype == SMQ_DTYPE_F32) {
     if (p->use_range_std_dev) SMQ_STATS(true, kF32); else SMQ_STATS(false, kF32);
   } else if (dtype == SMQ_DTYPE_F16) {
