@@ -378,14 +378,17 @@ def run_packed(args, world, rank, device):
     st = torch.cuda.current_stream(device).cuda_stream
     trace = EventTrace()
     it = [0]
+    # SMQ_BENCH_PACK_FLAGS: smq_smaq_compress_ex flags (2 = SMQ_PACK_SINGLE, the one-launch packer)
+    pack_flags = int(os.environ.get("SMQ_BENCH_PACK_FLAGS", "0"))
 
     def step():
         x = xs[it[0] & 1]
         it[0] += 1
         p = codec._params(n, False)
         trace.begin("compress")
-        N.check(lib.smq_smaq_compress(x.data_ptr(), N.SMQ_DTYPE_F32, n, p, packed.data_ptr(),
-                                      bound, ws.data_ptr(), ws.numel(), st), "compress")
+        N.check(lib.smq_smaq_compress_ex(x.data_ptr(), N.SMQ_DTYPE_F32, n, p, packed.data_ptr(),
+                                         bound, ws.data_ptr(), ws.numel(), pack_flags, st),
+                "compress")
         trace.end("compress")
         trace.begin("unpack")
         N.check(lib.smq_smaq_decompress(packed.data_ptr(), y.data_ptr(), n, st), "decompress")
@@ -411,7 +414,8 @@ def run_packed(args, world, rank, device):
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": "smaq_6_8_packed_256M_fp32", "elements_per_gpu": n,
                        "stream_bytes": sbytes, "bits_per_element": round(8.0 * sbytes / n, 3),
-                       "compression_ratio_vs_fp32": round(32.0 * n / (8.0 * sbytes), 3)},
+                       "compression_ratio_vs_fp32": round(32.0 * n / (8.0 * sbytes), 3),
+                       "pack_flags": pack_flags},
             "compress_ms": round(c_ms, 4), "decompress_ms": round(u_ms, 4),
             "roofline": {"bound": "hbm", "kernel": "smaq_unpack_kernel",
                          "achieved": round(u_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -302,7 +302,8 @@ typedef struct SmqPackedHeader {
 
 /* Worst-case stream size (every element an outlier and escaped) for n elements. */
 size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier);
-/* Workspace of smq_smaq_compress (statistics + look-back status words). */
+/* Workspace of smq_smaq_compress (statistics, look-back status words, streaming-packer records
+ * of 2 B per element); zero-filled once at allocation, left reusable by every call. */
 size_t smq_smaq_pack_workspace_bytes(int64_t n);
 /* Statistics (full / sampled / range, params as smq_smaq_stats) then one packing launch. Writes the
  * whole stream incl. header.total_bytes on the device; packed_bytes >= smq_smaq_pack_bound. The BN
@@ -310,13 +311,18 @@ size_t smq_smaq_pack_workspace_bytes(int64_t n);
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
                       void* packed, size_t packed_bytes, void* workspace, size_t workspace_bytes,
                       void* stream);
-/* Packing-launch flags of smq_smaq_compress_ex. Block b of the stream is placed after blocks
- * 0..b-1 (decoupled look-back). By default workgroup b packs block b: no global atomic per
+/* Packing flags of smq_smaq_compress_ex; every choice gives the same bytes.
+ * Default (flags 0) with both code widths <= 14 bits: the streaming packer, three launches none
+ * of which waits on another workgroup (records of 2 B per element in the workspace, a scan of the
+ * per-group image sizes, then the block images); never sets header.error.
+ * SMQ_PACK_SINGLE (and any code width > 14 bits): ONE packing launch in which block b is placed
+ * after blocks 0..b-1 by a decoupled look-back. Workgroup b packs block b: no global atomic per
  * workgroup (a ticket on one address serialises at ~11 ns each: 0.75 ms for 2^16 blocks), which
  * relies on every XCD starting its workgroups in index order. If that ever fails, the bounded
- * look-back spin gives up and sets header.error; SMQ_PACK_TICKETED then re-packs with block ids
- * from an atomic ticket (start order: no assumption). Both give the same bytes. */
+ * look-back spin gives up and sets header.error; SMQ_PACK_TICKETED (implies the single launch)
+ * then re-packs with block ids from an atomic ticket (start order: no assumption). */
 #define SMQ_PACK_TICKETED 1u
+#define SMQ_PACK_SINGLE 2u
 int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
                          void* packed, size_t packed_bytes, void* workspace,
                          size_t workspace_bytes, uint32_t flags, void* stream);

@@ -60,6 +60,14 @@ struct PackArgs {
   int place_atomic;          // measurement knob (SMQ_PACK_PLACE=atomic): see smq_smaq_compress
   uint32_t stage_words;      // LDS stage (w[0], mask, code stream) for these widths; q values follow
   unsigned long long* cursor;
+  // streaming packer (smaq_code_kernel / smaq_pack_scan_kernel / smaq_emit_kernel)
+  uint16_t* rec;             // [n_blocks * SMQ_PACK_BLOCK] element records
+  uint64_t* meta;            // [n_blocks] n_out | n_esc << 16 (| arrivals << 32)
+  uint32_t* gsum;            // [n_groups] image words of each group of kGroup blocks
+  uint64_t* gpre;            // [n_groups] exclusive prefix of gsum
+  uint32_t n_groups;
+  int code_ks;               // smaq_code_kernel: float4 groups per workgroup (4 or 2)
+  int code_rev;              // smaq_code_kernel: blocks in reverse address order
 };
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
@@ -404,6 +412,383 @@ void launch_pack(const PackArgs& A, bool vec, size_t lds, hipStream_t st) {
     hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, false, false, 0, 0>), dim3(1), block, lds, st, A);
 }
 
+// ---- streaming packer (the default when both code widths are <= kRecCodeBits) ----------------
+// The single packing launch above chains load -> quantise -> rank scan -> look-back -> image per
+// block in one workgroup; PMC showed it latency-bound (57 % of wave time in s_waitcnt / barriers,
+// VALU ~50 % busy). Here the same bytes come from three plain streaming launches, none of which
+// waits on another workgroup:
+//   1. smaq_code_kernel — one workgroup per block quantises its elements with pack_body's element
+//      code (same smaq_quant / classify) and writes one 16-bit record per element: bit 15 outlier,
+//      bit 14 escape; a plane code in bits 0-13, or for an escape the side (z < -T) in bit 13 and q
+//      in bits 0-12 (two's complement; kRecBig = q outside [-4095, 4095] or not finite: the emitter
+//      re-derives q from x). It adds the block's image size to its group sum (one atomic per
+//      workgroup, 64 blocks per group) and stores n_out | n_esc.
+//   2. smaq_pack_scan_kernel — one workgroup: exclusive scan of the group sums (zeroed by a
+//      memset before phase 1), writes the header.
+//   3. smaq_emit_kernel — one workgroup per block: prefix = its group's prefix + the sizes of its
+//      group predecessors (one load per lane), records -> ranks -> LDS code stream -> block image.
+// Traffic: 4 B/elem read + 2 B/elem records written, 2 B/elem records read + the stream written.
+constexpr int kRecCodeBits = 14;
+constexpr int kRecBig = -4096;
+
+__device__ __forceinline__ uint32_t block_image_words(int wm, int wo, uint32_t n_el, uint32_t n_out) {
+  return (uint32_t)kHdrWords + ((uint32_t)wm * n_el + (uint32_t)(wo - wm) * n_out + 31u) / 32u;
+}
+
+// Record of one element: classify()'s plane code / escape decision in integer ops (fewer selects).
+// v = q + 2^(wm-1) for a main (fits: v < 2^wm), |q| on the element's side for an outlier (fits:
+// v < 2^(wo-1)); |q| > 2^24, inf and NaN always escape (widths are at most 14 bits here). An
+// escape record carries q when |q| <= 4095, else kRecBig (the emitter re-derives q).
+__device__ __forceinline__ uint32_t record_of(float q, bool hi, bool lo, int wm, int wo, bool& esc) {
+  const bool o = hi | lo;
+  const int qi = (__builtin_fabsf(q) <= 0x1p24f) ? (int)q : -(1 << 30);
+  const uint32_t half_m = 1u << (wm - 1), side = 1u << (wo - 1);
+  const uint32_t v = (uint32_t)(lo ? -qi : (o ? qi : qi + (int)half_m));
+  const uint32_t lim = o ? side : 2u * half_m;
+  esc = !(v < lim);
+  const uint32_t code = o ? ((lo ? side : 0u) | v) : (v ^ half_m);
+  const int qe = ((uint32_t)(qi + 4095) <= 8190u) ? qi : kRecBig;
+  return esc ? (0x4000u | ((uint32_t)o << 15) | ((uint32_t)lo << 13) | ((uint32_t)qe & 0x1fffu))
+             : (((uint32_t)o << 15) | code);
+}
+
+// KS = element groups (float4 per lane, 1024 elements each) per workgroup: 4 = the whole block,
+// 2 = half a block (two workgroups per block; the second to finish adds the block's size).
+template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO, int KS>
+__global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
+  static_assert(KS == 4 || (KS == 2 && FULL), "half-block workgroups only for full blocks");
+  __shared__ uint32_t s_cnt[kBlock / kWave];
+  const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
+  // blocks in reverse address order: the statistics sweep just read x front to back, so its tail
+  // is still in the Infinity Cache; the emitter then walks forward over the fresh records
+  const uint32_t wg = FULL ? (A.code_rev ? A.n_full * (4 / KS) - 1 - blockIdx.x : blockIdx.x) : 0u;
+  const uint32_t b = FULL ? wg / (4 / KS) : A.n_blocks - 1;
+  const int k0 = FULL ? (int)(wg % (4 / KS)) * KS : 0;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  const int64_t e0 = (int64_t)b * kPB;
+  const int n_el = FULL ? kPB : (int)(A.n - e0);
+  ElemConsts c;
+  const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
+  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+  float xv[KS][4];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int el = 1024 * (k0 + k) + 4 * tid;
+    if (VEC && (FULL || el + 3 < n_el)) {
+      const float4 t = load4<TIN>(A.x, (e0 + el) >> 2);
+      xv[k][0] = t.x; xv[k][1] = t.y; xv[k][2] = t.z; xv[k][3] = t.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        xv[k][i] = (FULL || el + i < n_el) ? load1<TIN>(A.x, e0 + el + i) : 0.f;
+    }
+  }
+  uint32_t cnt = 0;  // outliers (bits 0-15) | escapes (bits 16-31) of this lane's elements
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int el = 1024 * (k0 + k) + 4 * tid;
+    const bool full4 = FULL || el + 3 < n_el;
+    float u[4] = {0.f, 0.f, 0.f, 0.f};
+    if (RM == kRoundHash) {
+      const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
+      if (full4) {
+        rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (el + i < n_el) u[i] = rng_hu(A.key, ctr + i);
+      }
+    }
+    uint32_t r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool hi, lo, esc;
+      const float q = smaq_quant<RM, false, TIN, true>(xv[k][i], u[i], c, hi, lo);
+      r[i] = record_of(q, hi, lo, wm, wo, esc);
+      const bool o = hi | lo;
+      const bool valid = FULL || el + i < n_el;
+      cnt += valid ? ((uint32_t)o | ((uint32_t)esc << 16)) : 0u;
+    }
+    uint16_t* dst = A.rec + e0 + el;
+    if (full4) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (el + i < n_el) dst[i] = (uint16_t)r[i];
+    }
+  }
+  cnt = wave_sum_u32(cnt);
+  if (lane == 0) s_cnt[w] = cnt;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t t = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+    bool last = true;
+    if (KS == 4) {
+      A.meta[b] = t;
+    } else {  // meta[b] = counts | arrivals << 32, zeroed before the launch
+      const uint64_t old = atomicAdd(reinterpret_cast<unsigned long long*>(A.meta + b),
+                                     (1ull << 32) | t);
+      last = (old >> 32) == (uint64_t)(4 / KS - 1);
+      t += (uint32_t)old;
+    }
+    if (last)
+      atomicAdd(A.gsum + b / kGroup,
+                block_image_words(wm, wo, (uint32_t)n_el, t & 0xffffu) + 2u * (t >> 16));
+  }
+}
+
+constexpr int kScanThreads = 1024;
+
+__global__ __launch_bounds__(kScanThreads) void smaq_pack_scan_kernel(PackArgs A) {
+  __shared__ uint64_t s_wave[kScanThreads / kWave];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  uint64_t carry = 0;
+  for (uint32_t base = 0; base < A.n_groups; base += 4u * kScanThreads) {
+    uint32_t v[4];
+    uint64_t loc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t g = base + 4u * tid + j;
+      v[j] = g < A.n_groups ? A.gsum[g] : 0u;
+      loc += v[j];
+    }
+    uint64_t inc = loc;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint64_t t = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += t;
+    }
+    if (lane == kWave - 1) s_wave[w] = inc;
+    __syncthreads();
+    uint64_t wpre = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kScanThreads / kWave; ++i) {
+      const uint64_t s = s_wave[i];
+      wpre += i < w ? s : 0ull;
+      total += s;
+    }
+    uint64_t run = carry + wpre + (inc - loc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t g = base + 4u * tid + j;
+      if (g < A.n_groups) A.gpre[g] = run;
+      run += v[j];
+    }
+    carry += total;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    SmqPackedHeader* h = A.hdr;
+    const SmqSmaqStats* st = A.stats;
+    h->magic = SMQ_PACK_MAGIC;
+    h->version = SMQ_PACK_VERSION;
+    h->n = A.n;
+    h->block_elems = kPB;
+    h->n_blocks = A.n_blocks;
+    h->num_bits_main = A.bm;
+    h->num_bits_outlier = A.bo;
+    h->flags = A.flags;
+    h->thr = A.thr;
+    h->range_main = A.r_main;
+    h->range_outlier = A.r_out;
+    h->mean = st->mean;
+    h->std_dev = st->std_dev;
+    h->inv_range_main = A.inv_r_main;
+    h->inv_range_outlier = A.inv_r_out;
+    h->data_words = carry;
+    h->total_bytes = sizeof(SmqPackedHeader) + 8ull * A.n_blocks + 4ull * carry;
+    h->error = 0u;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) h->reserved[i] = 0u;
+  }
+}
+
+// q of one element re-derived from x (an escape whose q does not fit its record: |q| > 4095, inf,
+// NaN), with pack_body's element code.
+template <int RM, int TIN>
+__device__ __forceinline__ float rederive_q(const PackArgs& A, int64_t e) {
+  ElemConsts c;
+  const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
+  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+  const float u = (RM == kRoundHash) ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)e) : 0.0f;
+  bool hi, lo;
+  return smaq_quant<RM, false, TIN, true>(load1<TIN>(A.x, e), u, c, hi, lo);
+}
+
+template <int RM, int TIN, bool FULL, int WM, int WO>
+__global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
+  extern __shared__ uint32_t stage[];  // [stage_words]: w[0], mask, code stream
+  __shared__ uint32_t seg_cnt[2][16];
+  __shared__ uint32_t seg_pre[2][17];
+  __shared__ uint64_t s_prefix;
+  constexpr bool kChunk = WO > 0 && WO <= 8;
+  const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
+  const uint32_t b = FULL ? blockIdx.x : A.n_blocks - 1;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  const int64_t e0 = (int64_t)b * kPB;
+  const int n_el = FULL ? kPB : (int)(A.n - e0);
+  uint32_t* codes_lds = stage + kHdrWords;
+
+  // records of this lane's 16 elements (el = 1024 k + 4 tid + i), two per register
+  uint32_t rw[4][2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int el = 1024 * k + 4 * tid;
+    if (FULL || el + 3 < n_el) {
+      const uint2 t = *reinterpret_cast<const uint2*>(A.rec + e0 + el);
+      rw[k][0] = t.x;
+      rw[k][1] = t.y;
+    } else {
+      uint32_t r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = (el + i < n_el) ? (uint32_t)A.rec[e0 + el + i] : 0u;
+      rw[k][0] = r[0] | (r[1] << 16);
+      rw[k][1] = r[2] | (r[3] << 16);
+    }
+  }
+  // block prefix: the group's prefix + the sizes of the group's earlier (full) blocks
+  if (w == 0) {
+    const uint32_t g = b / kGroup, j = g * kGroup + lane;
+    uint32_t sz = 0u;
+    if (j < b) {
+      const uint32_t t = (uint32_t)A.meta[j];
+      sz = block_image_words(wm, wo, kPB, t & 0xffffu) + 2u * (t >> 16);
+    }
+    sz = wave_sum_u32(sz);
+    if (lane == 0) s_prefix = A.gpre[g] + sz;
+  }
+
+  // outlier / escape bits per float4 group (the codes themselves are decoded when placed)
+  uint32_t om[4], xm[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    om[k] = 0u;
+    xm[k] = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t r = (rw[k][i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      om[k] |= (r >> 15) << i;
+      xm[k] |= ((r >> 14) & 1u) << i;
+    }
+  }
+  auto code_of = [&](int k, int i) -> uint32_t {
+    const uint32_t r = (rw[k][i >> 1] >> (16 * (i & 1))) & 0xffffu;
+    const uint32_t side_code = ((r >> 13) & (r >> 15) & 1u) << (wo - 1);
+    return ((r >> 14) & 1u) ? side_code : (r & 0x3fffu);
+  };
+
+  // ranks, mask words and the LDS code stream: pack_body steps 2-3
+  uint32_t pre_o[4], pre_x[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t to, tx;
+    pre_o[k] = wave_prefix_small<3>(__popc(om[k]), to);
+    pre_x[k] = wave_prefix_small<3>(__popc(xm[k]), tx);
+    uint32_t mw = om[k] << (4 * (lane & 7));
+    mw |= __shfl_xor(mw, 1, kWave);
+    mw |= __shfl_xor(mw, 2, kWave);
+    mw |= __shfl_xor(mw, 4, kWave);
+    if ((lane & 7) == 0) stage[1 + ((1024 * k + 4 * tid) >> 5)] = mw;
+    if (lane == 0) {
+      seg_cnt[0][4 * k + w] = to;
+      seg_cnt[1][4 * k + w] = tx;
+    }
+  }
+  const uint32_t code_cap = A.stage_words - kHdrWords;
+  for (uint32_t i = tid; i < code_cap; i += kBlock) codes_lds[i] = 0u;
+  __syncthreads();
+  if (tid < 2) {
+    uint32_t run = 0;
+    for (int s = 0; s < 16; ++s) {
+      seg_pre[tid][s] = run;
+      run += seg_cnt[tid][s];
+    }
+    seg_pre[tid][16] = run;
+  }
+  __syncthreads();
+  const uint32_t n_out = seg_pre[0][16], n_esc = seg_pre[1][16];
+  const uint32_t img_words = block_image_words(wm, wo, (uint32_t)n_el, n_out);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t el0 = 1024u * k + 4u * tid;
+    if (!FULL && (int)el0 >= n_el) continue;
+    const uint32_t r0 = seg_pre[0][4 * k + w] + pre_o[k];
+    const uint32_t pos0 = (uint32_t)wm * el0 + (uint32_t)(wo - wm) * r0;
+    if (kChunk) {
+      uint32_t chunk = 0u, off = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        chunk |= code_of(k, i) << off;
+        off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
+      }
+      or_bits(codes_lds, pos0, chunk);
+    } else {
+      uint32_t off = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        or_bits(codes_lds, pos0 + off, code_of(k, i));
+        off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
+      }
+    }
+  }
+  __syncthreads();
+
+  // the block image at its prefix, its escapes and directory entry
+  const uint64_t P = s_prefix;
+  uint32_t* out = A.data + P;
+  for (uint32_t i = tid; i < img_words; i += kBlock)
+    out[i] = i == 0 ? (n_out | (n_esc << 16)) : stage[i];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (!xm[k]) continue;
+    const uint32_t base_x = seg_pre[1][4 * k + w] + pre_x[k];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!((xm[k] >> i) & 1u)) continue;
+      const uint32_t el = 1024u * k + 4u * tid + i;
+      const uint32_t r = base_x + __popc(xm[k] & ((1u << i) - 1u));
+      const int qi = (int)(((rw[k][i >> 1] >> (16 * (i & 1))) & 0x1fffu) << 19) >> 19;
+      const float q = qi == kRecBig ? rederive_q<RM, TIN>(A, e0 + el) : (float)qi;
+      out[img_words + 2 * r] = el;
+      out[img_words + 2 * r + 1] = __float_as_uint(q);
+    }
+  }
+  if (tid == 0) A.dir[b] = P | ((uint64_t)n_out << 38) | ((uint64_t)n_esc << 51);
+}
+
+template <int RM, int TIN, int KS>
+void launch_code(const PackArgs& A, bool vec, hipStream_t st) {
+  const bool w57 = A.wm == 5 && A.wo == 7;
+  const dim3 grid(A.n_full * (4 / KS)), block(kBlock);
+  if (vec) {
+    if (w57) hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, true, true, 5, 7, KS>), grid, block, 0, st, A);
+    else hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, true, true, 0, 0, KS>), grid, block, 0, st, A);
+  } else {
+    if (w57) hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, true, 5, 7, KS>), grid, block, 0, st, A);
+    else hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, true, 0, 0, KS>), grid, block, 0, st, A);
+  }
+}
+
+template <int RM, int TIN>
+void launch_streaming_pack(const PackArgs& A, bool vec, size_t stage_lds, hipStream_t st) {
+  const bool w57 = A.wm == 5 && A.wo == 7;
+  const dim3 grid(A.n_full), block(kBlock);
+  if (A.n_full > 0) {
+    if (A.code_ks == 4) launch_code<RM, TIN, 4>(A, vec, st);
+    else launch_code<RM, TIN, 2>(A, vec, st);
+  }
+  if (A.n_full < A.n_blocks)
+    hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, false, 0, 0, 4>), dim3(1), block, 0, st, A);
+  hipLaunchKernelGGL(smaq_pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, A);
+  if (A.n_full > 0) {
+    if (w57) hipLaunchKernelGGL((smaq_emit_kernel<RM, TIN, true, 5, 7>), grid, block, stage_lds, st, A);
+    else hipLaunchKernelGGL((smaq_emit_kernel<RM, TIN, true, 0, 0>), grid, block, stage_lds, st, A);
+  }
+  if (A.n_full < A.n_blocks)
+    hipLaunchKernelGGL((smaq_emit_kernel<RM, TIN, false, 0, 0>), dim3(1), block, stage_lds, st, A);
+}
+
 // SMQ_PACK_PLACE=atomic: the stream size is the cursor (written after the packing launch).
 __global__ void smaq_pack_total_kernel(SmqPackedHeader* h, const unsigned long long* cursor,
                                        uint32_t n_blocks) {
@@ -578,6 +963,14 @@ size_t pack_ws_status_offset(int64_t n) {
   return (smaq_stats_ws_bytes(n) + 63) & ~(size_t)63;
 }
 
+// workspace: statistics | counter (64 B) | look-back status words | cursor (64 B) | streaming
+// packer: records (2 B/elem) | meta [nb] | group sums [ng] | prefixes [ng]
+size_t pack_ws_stream_offset(int64_t n) {
+  const size_t nb = (size_t)n_blocks_of(n < 1 ? 1 : n);
+  const size_t ng = (nb + kGroup - 1) / kGroup;
+  return (pack_ws_status_offset(n) + 64 + 8 * nb + 8 * ng + 64 + 255) & ~(size_t)255;
+}
+
 }  // namespace
 }  // namespace smq
 
@@ -596,7 +989,7 @@ size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier) {
 size_t smq_smaq_pack_workspace_bytes(int64_t n) {
   const size_t nb = (size_t)n_blocks_of(n < 1 ? 1 : n);
   const size_t ng = (nb + kGroup - 1) / kGroup;
-  return pack_ws_status_offset(n) + 64 + 8 * nb + 8 * ng + 64;
+  return pack_ws_stream_offset(n) + 2 * nb * kPB + 8 * nb + 4 * (ng + 1) + 8 * ng;
 }
 
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* packed,
@@ -665,6 +1058,11 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.gstatus = A.status + nb;
   const size_t ng = ((size_t)nb + kGroup - 1) / kGroup;
   A.cursor = (unsigned long long*)(A.gstatus + ng);
+  A.n_groups = (uint32_t)ng;
+  A.rec = (uint16_t*)(wb + pack_ws_stream_offset(n));
+  A.meta = (uint64_t*)(A.rec + (size_t)nb * kPB);
+  A.gsum = (uint32_t*)(A.meta + nb);
+  A.gpre = (uint64_t*)(A.gsum + ng + (ng & 1));  // 8-B aligned
   // measurement knob: place blocks by one atomicAdd (valid, decodable stream; block ORDER then
   // depends on timing, so the bytes are not reproducible) instead of the ordered look-back
   static const int place_env = [] {
@@ -692,13 +1090,46 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   // slack for the two-word ORs, rounded to 4 words so the q values after it are 16-B aligned
   A.stage_words = (uint32_t)(kHdrWords + (A.wo * kPB + 31) / 32 + 1 + 3) & ~3u;
   const size_t lds_bytes = 4 * ((size_t)A.stage_words + kPB);
+  const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
+  const bool sr = p->stochastic_rounding != 0;
+  const bool streaming = !(flags & (SMQ_PACK_TICKETED | SMQ_PACK_SINGLE)) && !A.place_atomic &&
+                         A.wm <= kRecCodeBits && A.wo <= kRecCodeBits;
+  if (streaming) {
+    // the group sums start at zero: their place in the workspace moves with n, so a previous call
+    // with another n may have left records there
+    static const int code_ks = [] {
+      const char* e = getenv("SMQ_PACK_CODE_KS");  // measurement knob: 4 or 2 groups per workgroup
+      return (e && !strcmp(e, "2")) ? 2 : 4;
+    }();
+    static const int code_rev = [] {
+      const char* e = getenv("SMQ_PACK_CODE_REV");  // measurement knob: 0 = index order
+      return (e && !strcmp(e, "0")) ? 0 : 1;
+    }();
+    A.code_ks = code_ks;
+    A.code_rev = code_rev;
+    // meta (arrival counts) and the group sums are adjacent: one memset
+    if (hipMemsetAsync(A.meta, 0, 8 * (size_t)nb + 4 * (size_t)A.n_groups, st) != hipSuccess) {
+      set_error("compress: hipMemsetAsync failed");
+      return SMQ_ERR_LAUNCH;
+    }
+    const size_t stage_lds = 4 * (size_t)A.stage_words;
+    if (dtype == SMQ_DTYPE_F32) {
+      if (sr) launch_streaming_pack<kRoundHash, kF32>(A, vec, stage_lds, st);
+      else launch_streaming_pack<kRoundTrunc, kF32>(A, vec, stage_lds, st);
+    } else if (dtype == SMQ_DTYPE_F16) {
+      if (sr) launch_streaming_pack<kRoundHash, kF16>(A, vec, stage_lds, st);
+      else launch_streaming_pack<kRoundTrunc, kF16>(A, vec, stage_lds, st);
+    } else {
+      if (sr) launch_streaming_pack<kRoundHash, kBF16>(A, vec, stage_lds, st);
+      else launch_streaming_pack<kRoundTrunc, kBF16>(A, vec, stage_lds, st);
+    }
+    return check_launch("smaq_code_kernel / smaq_emit_kernel");
+  }
   if (hipMemsetAsync(A.status, 0, 8 * ((size_t)nb + ng) + 64, st) != hipSuccess ||
       hipMemsetAsync(A.hdr, 0, sizeof(SmqPackedHeader), st) != hipSuccess) {
     set_error("compress: hipMemsetAsync failed");
     return SMQ_ERR_LAUNCH;
   }
-  const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
-  const bool sr = p->stochastic_rounding != 0;
   if (dtype == SMQ_DTYPE_F32) {
     if (sr) launch_pack<kRoundHash, kF32>(A, vec, lds_bytes, st);
     else launch_pack<kRoundTrunc, kF32>(A, vec, lds_bytes, st);

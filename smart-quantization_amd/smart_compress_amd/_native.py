@@ -27,6 +27,7 @@ SMQ_STATS_WORKSPACE = 0
 SMQ_STATS_SAMPLED = 1
 SMQ_STATS_INJECTED = 2
 SMQ_PACK_TICKETED = 1
+SMQ_PACK_SINGLE = 2
 SMQ_DTYPE_F32 = 0
 SMQ_DTYPE_F16 = 1
 SMQ_DTYPE_BF16 = 2

@@ -221,7 +221,7 @@ def test_ticketed_and_index_order_give_the_same_bytes(n):
     bound = lib.smq_smaq_pack_bound(n, hp.num_bits_main, hp.num_bits_outlier)
     ws = torch.zeros(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8, device="cuda")
     outs = []
-    for flags in (0, N.SMQ_PACK_TICKETED, N.SMQ_PACK_TICKETED, 0):
+    for flags in (0, N.SMQ_PACK_TICKETED, N.SMQ_PACK_TICKETED, 0, N.SMQ_PACK_SINGLE):
         out = torch.zeros(bound, dtype=torch.uint8, device="cuda")
         N.check(lib.smq_smaq_compress_ex(x.data_ptr(), N.SMQ_DTYPE_F32, n, p, out.data_ptr(),
                                          out.numel(), ws.data_ptr(), ws.numel(), flags,
@@ -234,3 +234,66 @@ def test_ticketed_and_index_order_give_the_same_bytes(n):
     assert total > 128
     for o in outs[1:]:
         assert torch.equal(o[:total], outs[0][:total])
+
+
+def _compress_raw(x, pk, flags, p):
+    """smq_smaq_compress_ex with explicit flags and params into a fresh buffer; returns the
+    stream bytes."""
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    n = x.numel()
+    code = N.DTYPE_CODES[x.dtype]
+    bound = lib.smq_smaq_pack_bound(n, pk.hparams.num_bits_main, pk.hparams.num_bits_outlier)
+    ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(n))
+    out = torch.zeros(bound, dtype=torch.uint8, device=x.device)
+    N.check(lib.smq_smaq_compress_ex(x.data_ptr(), code, n, p, out.data_ptr(), out.numel(),
+                                     ws.data_ptr(), ws.numel(), flags, N.stream_ptr(x.device)),
+            "compress_ex")
+    torch.cuda.synchronize()
+    raw = out.cpu().numpy()
+    to = N.SmqPackedHeader.total_bytes.offset
+    eo = N.SmqPackedHeader.error.offset
+    assert int(raw[eo:eo + 4].view(np.uint32)[0]) == 0
+    return raw[:int(raw[to:to + 8].view(np.uint64)[0])]
+
+
+@pytest.mark.parametrize("n", [8, 4095, 4096, 4097, 3 * 4096 + 77, (1 << 20) + 5])
+@pytest.mark.parametrize("bits", [(6, 8), (4, 6), (9, 12), (15, 15), (16, 18)])
+def test_streaming_packer_equals_single_launch(n, bits):
+    """Default (streaming: code records -> group scan -> block images) and SMQ_PACK_SINGLE (one
+    look-back launch) give the same bytes, incl. escapes whose q does not fit a record (|q| > 4095,
+    inf, NaN: re-derived from x), widths beyond the 14-bit records (both take the single launch),
+    and repeated calls on one workspace."""
+    from smart_compress_amd import _native as N
+
+    hp, pk, _ = _codecs(seed=3, offset=11, num_bits_main=bits[0], num_bits_outlier=bits[1])
+    x_np = _heavy(n, n % 97)
+    rs = np.random.default_rng(n)
+    x_np[rs.random(n) < 0.002] *= 1e6  # |q| far beyond 4095
+    x = torch.from_numpy(x_np).cuda()
+    p = pk._params(n, False, x.dtype, x.device)
+    a = _compress_raw(x, pk, 0, p)
+    b = _compress_raw(x, pk, N.SMQ_PACK_SINGLE, p)
+    c = _compress_raw(x, pk, 0, p)
+    m = min(a.size, b.size)
+    assert a.size == b.size and np.array_equal(a, b), (a.size, b.size, int(np.argmax(a[:m] != b[:m])))
+    assert np.array_equal(a, c)
+
+
+@pytest.mark.parametrize("dt", ["f32", "f16", "bf16"])
+def test_streaming_packer_unaligned_and_half(dt):
+    """Element-path (misaligned x) and half inputs through the streaming packer == the oracle."""
+    tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[dt]
+    hp, pk, _ = _codecs(seed=8, offset=0, precision=16 if dt != "f32" else 32)
+    gen = torch.Generator(device="cuda").manual_seed(2)
+    base = (torch.randn(3 * 4096 + 1000, generator=gen, device="cuda") * 2).to(tdt)
+    x = base[1:]  # misaligned by one element
+    assert x.data_ptr() % 16 != 0
+    got = _compress_raw(x, pk, 0, pk._params(x.numel(), False, x.dtype, x.device))
+    from oracle import smaq_packed as P
+
+    h = P.header(got)
+    packed = type("P", (), {"header": lambda self: h})()
+    stream, _, _ = _oracle_stream(x.float().cpu().numpy(), packed, hp, 8, 0, dtype=dt)
+    assert np.array_equal(got, stream)

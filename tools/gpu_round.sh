@@ -32,6 +32,8 @@ for s in "$@"; do
     profile) step profile 1500 bash tools/profile_round.sh ${ROUND:-r03} smaq ;;
     profile_*) c=${s#profile_}; step profile_$c 1500 bash tools/profile_round.sh ${ROUND:-r03}_$c $c 50 10 ;;
     bench_packed) step bench_packed 600 python bench.py --config packed --steps 20 --warmup 3 ;;
+    bench_packed_single) SMQ_BENCH_PACK_FLAGS=2 step bench_packed_single 600 python bench.py --config packed --steps 20 --warmup 3 ;;
+    tests_packed) step pytest_packed 600 python -u -m pytest tests/test_gpu_packed.py -x -q --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 --cpu-budget 8 ;;
     bench_all) step bench_fp8 300 python bench.py --config fp8 --steps 50 --warmup 5 &&
