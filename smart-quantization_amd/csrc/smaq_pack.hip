@@ -62,12 +62,10 @@ struct PackArgs {
   unsigned long long* cursor;
   // streaming packer (smaq_code_kernel / smaq_pack_scan_kernel / smaq_emit_kernel)
   uint16_t* rec;             // [n_blocks * SMQ_PACK_BLOCK] element records
-  uint64_t* meta;            // [n_blocks] n_out | n_esc << 16 (| arrivals << 32)
+  uint32_t* meta;            // [n_blocks] n_out | n_esc << 16
   uint32_t* gsum;            // [n_groups] image words of each group of kGroup blocks
   uint64_t* gpre;            // [n_groups] exclusive prefix of gsum
   uint32_t n_groups;
-  int code_ks;               // smaq_code_kernel: float4 groups per workgroup (4 or 2)
-  int code_rev;              // smaq_code_kernel: blocks in reverse address order
 };
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
@@ -452,28 +450,25 @@ __device__ __forceinline__ uint32_t record_of(float q, bool hi, bool lo, int wm,
              : (((uint32_t)o << 15) | code);
 }
 
-// KS = element groups (float4 per lane, 1024 elements each) per workgroup: 4 = the whole block,
-// 2 = half a block (two workgroups per block; the second to finish adds the block's size).
-template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO, int KS>
+// One workgroup per block (half-block workgroups, the second to finish adding the block's size,
+// measured 357 vs 338 us at 256M).
+template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO>
 __global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
-  static_assert(KS == 4 || (KS == 2 && FULL), "half-block workgroups only for full blocks");
   __shared__ uint32_t s_cnt[kBlock / kWave];
   const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
   // blocks in reverse address order: the statistics sweep just read x front to back, so its tail
-  // is still in the Infinity Cache; the emitter then walks forward over the fresh records
-  const uint32_t wg = FULL ? (A.code_rev ? A.n_full * (4 / KS) - 1 - blockIdx.x : blockIdx.x) : 0u;
-  const uint32_t b = FULL ? wg / (4 / KS) : A.n_blocks - 1;
-  const int k0 = FULL ? (int)(wg % (4 / KS)) * KS : 0;
+  // is still in the Infinity Cache (331 vs 335 us); the emitter then walks forward
+  const uint32_t b = FULL ? A.n_full - 1 - blockIdx.x : A.n_blocks - 1;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
   ElemConsts c;
   const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
   init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
-  float xv[KS][4];
+  float xv[4][4];
 #pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    const int el = 1024 * (k0 + k) + 4 * tid;
+  for (int k = 0; k < 4; ++k) {
+    const int el = 1024 * k + 4 * tid;
     if (VEC && (FULL || el + 3 < n_el)) {
       const float4 t = load4<TIN>(A.x, (e0 + el) >> 2);
       xv[k][0] = t.x; xv[k][1] = t.y; xv[k][2] = t.z; xv[k][3] = t.w;
@@ -485,8 +480,8 @@ __global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
   }
   uint32_t cnt = 0;  // outliers (bits 0-15) | escapes (bits 16-31) of this lane's elements
 #pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    const int el = 1024 * (k0 + k) + 4 * tid;
+  for (int k = 0; k < 4; ++k) {
+    const int el = 1024 * k + 4 * tid;
     const bool full4 = FULL || el + 3 < n_el;
     float u[4] = {0.f, 0.f, 0.f, 0.f};
     if (RM == kRoundHash) {
@@ -522,19 +517,10 @@ __global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
   if (lane == 0) s_cnt[w] = cnt;
   __syncthreads();
   if (tid == 0) {
-    uint32_t t = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
-    bool last = true;
-    if (KS == 4) {
-      A.meta[b] = t;
-    } else {  // meta[b] = counts | arrivals << 32, zeroed before the launch
-      const uint64_t old = atomicAdd(reinterpret_cast<unsigned long long*>(A.meta + b),
-                                     (1ull << 32) | t);
-      last = (old >> 32) == (uint64_t)(4 / KS - 1);
-      t += (uint32_t)old;
-    }
-    if (last)
-      atomicAdd(A.gsum + b / kGroup,
-                block_image_words(wm, wo, (uint32_t)n_el, t & 0xffffu) + 2u * (t >> 16));
+    const uint32_t t = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+    A.meta[b] = t;
+    atomicAdd(A.gsum + b / kGroup,
+              block_image_words(wm, wo, (uint32_t)n_el, t & 0xffffu) + 2u * (t >> 16));
   }
 }
 
@@ -620,7 +606,6 @@ template <int RM, int TIN, bool FULL, int WM, int WO>
 __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
   extern __shared__ uint32_t stage[];  // [stage_words]: w[0], mask, code stream
   __shared__ uint32_t seg_cnt[2][16];
-  __shared__ uint32_t seg_pre[2][17];
   __shared__ uint64_t s_prefix;
   constexpr bool kChunk = WO > 0 && WO <= 8;
   const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
@@ -652,7 +637,7 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
     const uint32_t g = b / kGroup, j = g * kGroup + lane;
     uint32_t sz = 0u;
     if (j < b) {
-      const uint32_t t = (uint32_t)A.meta[j];
+      const uint32_t t = A.meta[j];
       sz = block_image_words(wm, wo, kPB, t & 0xffffu) + 2u * (t >> 16);
     }
     sz = wave_sum_u32(sz);
@@ -698,22 +683,31 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
   const uint32_t code_cap = A.stage_words - kHdrWords;
   for (uint32_t i = tid; i < code_cap; i += kBlock) codes_lds[i] = 0u;
   __syncthreads();
-  if (tid < 2) {
-    uint32_t run = 0;
-    for (int s = 0; s < 16; ++s) {
-      seg_pre[tid][s] = run;
-      run += seg_cnt[tid][s];
-    }
-    seg_pre[tid][16] = run;
+  // every wave derives its segment prefixes from the 16 + 16 counts itself (no serial scan and
+  // no second barrier): segment 4 k + w starts after segments 0 .. 4 k + w - 1
+  // (lane s < 16 holds segment s's counts packed as outliers | escapes << 16, each <= 4096)
+  uint32_t incl = lane < 16 ? (seg_cnt[0][lane] | (seg_cnt[1][lane] << 16)) : 0u;
+  const uint32_t own = incl;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += t;
   }
-  __syncthreads();
-  const uint32_t n_out = seg_pre[0][16], n_esc = seg_pre[1][16];
+  const uint32_t excl = incl - own, tot = __shfl(incl, 15, kWave);
+  const uint32_t n_out = tot & 0xffffu, n_esc = tot >> 16;
+  uint32_t base_o[4], base_x[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t b4 = __shfl(excl, 4 * k + w, kWave);
+    base_o[k] = b4 & 0xffffu;
+    base_x[k] = b4 >> 16;
+  }
   const uint32_t img_words = block_image_words(wm, wo, (uint32_t)n_el, n_out);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t el0 = 1024u * k + 4u * tid;
     if (!FULL && (int)el0 >= n_el) continue;
-    const uint32_t r0 = seg_pre[0][4 * k + w] + pre_o[k];
+    const uint32_t r0 = base_o[k] + pre_o[k];
     const uint32_t pos0 = (uint32_t)wm * el0 + (uint32_t)(wo - wm) * r0;
     if (kChunk) {
       uint32_t chunk = 0u, off = 0u;
@@ -742,12 +736,12 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (!xm[k]) continue;
-    const uint32_t base_x = seg_pre[1][4 * k + w] + pre_x[k];
+    const uint32_t bx = base_x[k] + pre_x[k];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (!((xm[k] >> i) & 1u)) continue;
       const uint32_t el = 1024u * k + 4u * tid + i;
-      const uint32_t r = base_x + __popc(xm[k] & ((1u << i) - 1u));
+      const uint32_t r = bx + __popc(xm[k] & ((1u << i) - 1u));
       const int qi = (int)(((rw[k][i >> 1] >> (16 * (i & 1))) & 0x1fffu) << 19) >> 19;
       const float q = qi == kRecBig ? rederive_q<RM, TIN>(A, e0 + el) : (float)qi;
       out[img_words + 2 * r] = el;
@@ -757,29 +751,21 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
   if (tid == 0) A.dir[b] = P | ((uint64_t)n_out << 38) | ((uint64_t)n_esc << 51);
 }
 
-template <int RM, int TIN, int KS>
-void launch_code(const PackArgs& A, bool vec, hipStream_t st) {
-  const bool w57 = A.wm == 5 && A.wo == 7;
-  const dim3 grid(A.n_full * (4 / KS)), block(kBlock);
-  if (vec) {
-    if (w57) hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, true, true, 5, 7, KS>), grid, block, 0, st, A);
-    else hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, true, true, 0, 0, KS>), grid, block, 0, st, A);
-  } else {
-    if (w57) hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, true, 5, 7, KS>), grid, block, 0, st, A);
-    else hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, true, 0, 0, KS>), grid, block, 0, st, A);
-  }
-}
-
 template <int RM, int TIN>
 void launch_streaming_pack(const PackArgs& A, bool vec, size_t stage_lds, hipStream_t st) {
   const bool w57 = A.wm == 5 && A.wo == 7;
   const dim3 grid(A.n_full), block(kBlock);
   if (A.n_full > 0) {
-    if (A.code_ks == 4) launch_code<RM, TIN, 4>(A, vec, st);
-    else launch_code<RM, TIN, 2>(A, vec, st);
+    if (vec) {
+      if (w57) hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, true, true, 5, 7>), grid, block, 0, st, A);
+      else hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, true, true, 0, 0>), grid, block, 0, st, A);
+    } else {
+      if (w57) hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, true, 5, 7>), grid, block, 0, st, A);
+      else hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, true, 0, 0>), grid, block, 0, st, A);
+    }
   }
   if (A.n_full < A.n_blocks)
-    hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, false, 0, 0, 4>), dim3(1), block, 0, st, A);
+    hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, false, 0, 0>), dim3(1), block, 0, st, A);
   hipLaunchKernelGGL(smaq_pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, A);
   if (A.n_full > 0) {
     if (w57) hipLaunchKernelGGL((smaq_emit_kernel<RM, TIN, true, 5, 7>), grid, block, stage_lds, st, A);
@@ -989,7 +975,7 @@ size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier) {
 size_t smq_smaq_pack_workspace_bytes(int64_t n) {
   const size_t nb = (size_t)n_blocks_of(n < 1 ? 1 : n);
   const size_t ng = (nb + kGroup - 1) / kGroup;
-  return pack_ws_stream_offset(n) + 2 * nb * kPB + 8 * nb + 4 * (ng + 1) + 8 * ng;
+  return pack_ws_stream_offset(n) + 2 * nb * kPB + 4 * nb + 4 * (ng + 1) + 8 * ng;
 }
 
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* packed,
@@ -1060,9 +1046,9 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.cursor = (unsigned long long*)(A.gstatus + ng);
   A.n_groups = (uint32_t)ng;
   A.rec = (uint16_t*)(wb + pack_ws_stream_offset(n));
-  A.meta = (uint64_t*)(A.rec + (size_t)nb * kPB);
-  A.gsum = (uint32_t*)(A.meta + nb);
-  A.gpre = (uint64_t*)(A.gsum + ng + (ng & 1));  // 8-B aligned
+  A.meta = (uint32_t*)(A.rec + (size_t)nb * kPB);
+  A.gsum = A.meta + nb;
+  A.gpre = (uint64_t*)(((uintptr_t)(A.gsum + ng) + 7) & ~(uintptr_t)7);
   // measurement knob: place blocks by one atomicAdd (valid, decodable stream; block ORDER then
   // depends on timing, so the bytes are not reproducible) instead of the ordered look-back
   static const int place_env = [] {
@@ -1097,18 +1083,7 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   if (streaming) {
     // the group sums start at zero: their place in the workspace moves with n, so a previous call
     // with another n may have left records there
-    static const int code_ks = [] {
-      const char* e = getenv("SMQ_PACK_CODE_KS");  // measurement knob: 4 or 2 groups per workgroup
-      return (e && !strcmp(e, "2")) ? 2 : 4;
-    }();
-    static const int code_rev = [] {
-      const char* e = getenv("SMQ_PACK_CODE_REV");  // measurement knob: 0 = index order
-      return (e && !strcmp(e, "0")) ? 0 : 1;
-    }();
-    A.code_ks = code_ks;
-    A.code_rev = code_rev;
-    // meta (arrival counts) and the group sums are adjacent: one memset
-    if (hipMemsetAsync(A.meta, 0, 8 * (size_t)nb + 4 * (size_t)A.n_groups, st) != hipSuccess) {
+    if (hipMemsetAsync(A.gsum, 0, 4 * (size_t)A.n_groups, st) != hipSuccess) {
       set_error("compress: hipMemsetAsync failed");
       return SMQ_ERR_LAUNCH;
     }

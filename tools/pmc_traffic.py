@@ -30,6 +30,9 @@ SHORT = {
     "s2fp8_apply_kernel": "s2fp8_apply_kernel",
     "smaq_pack_kernel": "smaq_pack_kernel",
     "smaq_unpack_kernel": "smaq_unpack_kernel",
+    "smaq_code_kernel": "smaq_code_kernel",
+    "smaq_emit_kernel": "smaq_emit_kernel",
+    "smaq_pack_scan_kernel": "smaq_pack_scan_kernel",
 }
 
 
