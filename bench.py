@@ -170,24 +170,32 @@ def time_steps(step, steps, warmup, world, device, region=None):
 
 
 def cpu_baseline_smaq(sample_elems, budget_s):
-    """Oracle (numpy, 1 thread) SmaQ 6/8 round trip incl. RNG on a bounded sample."""
-    from oracle import rng as orng
-    from oracle import smaq as osmaq
+    """The reference's algorithm on the host cores: oracle/smaq_torch.py, smart.py's own torch-CPU
+    op sequence (full stats, torch.rand_like SR; bit-exact with the reference's outputs on the
+    golden fixtures), on a bounded sample, with as many intra-op threads as this job's CPU share
+    (OMP_NUM_THREADS, 16 on the GPU box; os.cpu_count() counts the whole machine there)."""
+    from oracle import smaq_torch
 
-    rs = np.random.default_rng(0)
-    x = rs.standard_normal(sample_elems).astype(np.float32)
-    cfg = osmaq.SmaqConfig()
-    reps, t_tot = 0, 0.0
-    while t_tot < budget_s or reps < 2:
-        t0 = time.perf_counter()
-        u = orng.uniforms(1, reps * sample_elems, sample_elems)
-        osmaq.roundtrip(x, cfg, uniforms=u)
-        t_tot += time.perf_counter() - t0
-        reps += 1
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        g = torch.Generator().manual_seed(0)
+        x = torch.randn(sample_elems, generator=g)
+        smaq_torch.roundtrip(x)  # warm-up (allocator, thread pool)
+        reps, t_tot = 0, 0.0
+        while t_tot < budget_s or reps < 2:
+            t0 = time.perf_counter()
+            smaq_torch.roundtrip(x)
+            t_tot += time.perf_counter() - t0
+            reps += 1
+    finally:
+        torch.set_num_threads(prev)
     gbps = 12.0 * sample_elems * reps / t_tot / 1e9
-    return {"value": round(gbps, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} x {sample_elems} fp32 N(0,1), numpy oracle/smaq.py (full stats + "
-                      f"SR incl. counter RNG), single thread, {t_tot:.1f} s"}
+    return {"value": round(gbps, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x {sample_elems} fp32 N(0,1) round trips, oracle/smaq_torch.py "
+                      f"(smart.py's torch-CPU op sequence, full stats + rand_like SR), "
+                      f"{threads} threads, {t_tot:.1f} s"}
 
 
 def traffic_from_profile(config):
@@ -540,8 +548,8 @@ def main():
                              "autograd"])
     ap.add_argument("--elements", type=int, default=0, help="override elements (smaq configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 22)
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 24)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
 
     world, rank, local = dist_setup()

@@ -192,3 +192,31 @@ def test_rng_uniform_properties():
     a = rng.rng_u32(1, 2**32 - 2, 4)
     b = np.concatenate([rng.rng_u32(1, 2**32 - 2, 2), rng.rng_u32(1, 2**32, 2)])
     assert np.array_equal(a, b)  # counter crosses the 32-bit boundary consistently
+
+
+@pytest.mark.parametrize("name", ["normal", "laplace", "small_scale", "relu_allpos", "grad_like"])
+def test_smaq_torch_restatement_bitexact(name):
+    """oracle/smaq_torch.py (the torch-CPU op sequence bench.py times as the CPU baseline) equals the
+    reference's outputs bit for bit with its recorded uniforms and statistics, and its own
+    statistics are within 1 ulp of the reference's."""
+    import torch
+
+    from oracle import smaq_torch
+
+    from helpers import smaq_cases
+
+    meta = smaq_cases()[name]
+    if (meta["use_sample_stats"] or meta["use_range_std_dev"] or meta["use_batch_norm"]
+            or not meta["stochastic_rounding"] or meta["dtype"] != "f32"):
+        pytest.skip("default-flag fp32 cases only")
+    d = load_smaq(name)
+    x = torch.from_numpy(d["x"])
+    kw = dict(num_bits_main=meta["num_bits_main"], num_bits_outlier=meta["num_bits_outlier"],
+              thr=meta["main_std_dev_threshold"], thr_outlier=meta["outlier_std_dev_threshold"],
+              all_positive=meta["all_positive"], uniforms=torch.from_numpy(d["uniforms"]))
+    y = smaq_torch.roundtrip(x, stats=(float(d["mean"]), float(d["std"])), **kw).numpy()
+    assert np.array_equal(y.view(np.uint32), d["y"].astype(np.float32).view(np.uint32))
+    m, s = x.mean().item(), x.std().item()
+    for a, b in ((m, d["mean"]), (s, d["std"])):
+        assert abs(int(np.float32(a).view(np.int32)) - int(np.float32(b).view(np.int32))) <= 1
+
