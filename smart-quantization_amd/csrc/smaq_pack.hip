@@ -68,25 +68,6 @@ struct PackArgs {
   uint32_t n_groups;
 };
 
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// Exclusive wave prefix of small per-lane counts (< 2^BITS) and the wave total, by bit-sliced
-// ballots.
-template <int BITS>
-__device__ __forceinline__ uint32_t wave_prefix_small(uint32_t v, uint32_t& total) {
-  uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int j = 0; j < BITS; ++j) {
-    const uint64_t bal = __ballot((v >> j) & 1u);
-    pre += mbcnt64(bal) << j;
-    tot += (uint32_t)__popcll(bal) << j;
-  }
-  total = tot;
-  return pre;
-}
-
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
@@ -248,17 +229,16 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   uint32_t pre_o[4], pre_x[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    uint32_t to, tx;
-    pre_o[k] = wave_prefix_small<3>(__popc(om[k]), to);
-    pre_x[k] = wave_prefix_small<3>(__popc(xm[k]), tx);
-    uint32_t mw = om[k] << (4 * (lane & 7));
-    mw |= __shfl_xor(mw, 1, kWave);
-    mw |= __shfl_xor(mw, 2, kWave);
-    mw |= __shfl_xor(mw, 4, kWave);
-    if ((lane & 7) == 0) stage[1 + ((1024 * k + 4 * tid) >> 5)] = mw;
-    if (lane == 0) {
-      seg_cnt[0][4 * k + w] = to;
-      seg_cnt[1][4 * k + w] = tx;
+    const uint32_t cnt = (uint32_t)__popc(om[k]) | ((uint32_t)__popc(xm[k]) << 16);
+    const uint32_t incl = wave_incl_scan_u32(cnt);
+    const uint32_t ex = incl - cnt;
+    pre_o[k] = ex & 0xffffu;
+    pre_x[k] = ex >> 16;
+    const uint32_t mw = group8_or_to_last(om[k] << (4 * (lane & 7)));
+    if ((lane & 7) == 7) stage[1 + ((1024 * k + 4 * (tid - 7)) >> 5)] = mw;
+    if (lane == kWave - 1) {
+      seg_cnt[0][4 * k + w] = incl & 0xffffu;
+      seg_cnt[1][4 * k + w] = incl >> 16;
     }
   }
   const uint32_t code_cap = A.stage_words - kHdrWords;
@@ -513,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
         if (el + i < n_el) dst[i] = (uint16_t)r[i];
     }
   }
-  cnt = wave_sum_u32(cnt);
+  cnt = wave_total_u32(cnt);
   if (lane == 0) s_cnt[w] = cnt;
   __syncthreads();
   if (tid == 0) {
@@ -640,7 +620,7 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
       const uint32_t t = A.meta[j];
       sz = block_image_words(wm, wo, kPB, t & 0xffffu) + 2u * (t >> 16);
     }
-    sz = wave_sum_u32(sz);
+    sz = wave_total_u32(sz);
     if (lane == 0) s_prefix = A.gpre[g] + sz;
   }
 
@@ -664,20 +644,21 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
   };
 
   // ranks, mask words and the LDS code stream: pack_body steps 2-3
+  // outlier and escape counts packed in one word (each <= 256 per wave) and scanned together by
+  // DPP; mask words: OR of 8 lanes' nibbles, written by each group's last lane
   uint32_t pre_o[4], pre_x[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    uint32_t to, tx;
-    pre_o[k] = wave_prefix_small<3>(__popc(om[k]), to);
-    pre_x[k] = wave_prefix_small<3>(__popc(xm[k]), tx);
-    uint32_t mw = om[k] << (4 * (lane & 7));
-    mw |= __shfl_xor(mw, 1, kWave);
-    mw |= __shfl_xor(mw, 2, kWave);
-    mw |= __shfl_xor(mw, 4, kWave);
-    if ((lane & 7) == 0) stage[1 + ((1024 * k + 4 * tid) >> 5)] = mw;
-    if (lane == 0) {
-      seg_cnt[0][4 * k + w] = to;
-      seg_cnt[1][4 * k + w] = tx;
+    const uint32_t cnt = (uint32_t)__popc(om[k]) | ((uint32_t)__popc(xm[k]) << 16);
+    const uint32_t incl = wave_incl_scan_u32(cnt);
+    const uint32_t ex = incl - cnt;
+    pre_o[k] = ex & 0xffffu;
+    pre_x[k] = ex >> 16;
+    const uint32_t mw = group8_or_to_last(om[k] << (4 * (lane & 7)));
+    if ((lane & 7) == 7) stage[1 + ((1024 * k + 4 * (tid - 7)) >> 5)] = mw;
+    if (lane == kWave - 1) {
+      seg_cnt[0][4 * k + w] = incl & 0xffffu;
+      seg_cnt[1][4 * k + w] = incl >> 16;
     }
   }
   const uint32_t code_cap = A.stage_words - kHdrWords;
@@ -686,19 +667,19 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
   // every wave derives its segment prefixes from the 16 + 16 counts itself (no serial scan and
   // no second barrier): segment 4 k + w starts after segments 0 .. 4 k + w - 1
   // (lane s < 16 holds segment s's counts packed as outliers | escapes << 16, each <= 4096)
-  uint32_t incl = lane < 16 ? (seg_cnt[0][lane] | (seg_cnt[1][lane] << 16)) : 0u;
-  const uint32_t own = incl;
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
-    const uint32_t t = __shfl_up(incl, o, kWave);
-    if (lane >= o) incl += t;
-  }
-  const uint32_t excl = incl - own, tot = __shfl(incl, 15, kWave);
+  const uint32_t own = lane < 16 ? (seg_cnt[0][lane] | (seg_cnt[1][lane] << 16)) : 0u;
+  uint32_t incl = own;  // row 0 (lanes 0-15) scanned by DPP row shifts
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xf, 0xf, false);
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xf, 0xf, false);
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xf, 0xf, false);
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x118, 0xf, 0xf, false);
+  const uint32_t excl = incl - own;
+  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 15);
   const uint32_t n_out = tot & 0xffffu, n_esc = tot >> 16;
   uint32_t base_o[4], base_x[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint32_t b4 = __shfl(excl, 4 * k + w, kWave);
+    const uint32_t b4 = (uint32_t)__builtin_amdgcn_readlane((int)excl, 4 * k + w);
     base_o[k] = b4 & 0xffffu;
     base_x[k] = b4 >> 16;
   }
@@ -841,8 +822,7 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
   const uint32_t* esc = esc_lds ? stage + img_words : blk + img_words;
   if (tid < kWave) {  // wave 0: exclusive popcount prefix of the 128 outlier-mask words
     const uint32_t a = __popc(stage[1 + 2 * lane]), bb = __popc(stage[2 + 2 * lane]);
-    uint32_t tot;
-    const uint32_t ex = wave_prefix_small<7>(a + bb, tot);
+    const uint32_t ex = wave_incl_scan_u32(a + bb) - (a + bb);
     pc[2 * lane] = ex;
     pc[2 * lane + 1] = ex + a;
   } else if (tid < kWave + kMaskWords) {  // waves 1-2: escapes before each mask word

@@ -143,6 +143,33 @@ struct SmaqWsLayout {
   static constexpr size_t kPartials = kSlots + 8 * SMQ_WS_OUTLIER_SLOTS;  // StatPartial[grid]
 };
 
+// Inclusive wave64 prefix sum by DPP row shifts and row broadcasts (GFX9 rows of 16 lanes; the
+// classic AMDGPU scan: row_shr 1, 2, 4, 8, then row_bcast:15 into rows 1 and 3 and row_bcast:31
+// into rows 2 and 3). Six VALU ops; lanes without a source read 0.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
+// OR of each aligned group of 8 lanes, complete in the group's last lane (lane & 7 == 7): three
+// DPP row shifts (a group never crosses a 16-lane row).
+__device__ __forceinline__ uint32_t group8_or_to_last(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  return v;
+}
+
+// Wave64 sum in every lane: the DPP scan, then lane 63's total.
+__device__ __forceinline__ uint32_t wave_total_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(v), 63);
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
