@@ -95,7 +95,7 @@ struct FQArgs {
 template <bool HOUT>
 __device__ __forceinline__ void store4_out(void* y, int64_t j, float4 o) {
   if (!HOUT) {
-    store_nt(static_cast<float4*>(y) + j, o);
+    store_stream(static_cast<float4*>(y) + j, o);
   } else {
     const uint32_t lo = (uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.x)) |
                         ((uint32_t)__builtin_bit_cast(uint16_t, __float2half_rn(o.y)) << 16);

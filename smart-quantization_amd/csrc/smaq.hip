@@ -295,7 +295,7 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemCon
       o.z = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].z, u2, c, b2, bn_term<BN>(A, 4 * j + 2));
       o.w = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].w, u3, c, b3, bn_term<BN>(A, 4 * j + 3));
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
-      store_nt(y4 + j, o);
+      store_stream(y4 + j, o);
     }
     // ragged tail (n % 4 elements): the workgroup owning the last tile
     if (tile == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {

@@ -210,7 +210,7 @@ __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, co
       o.z = elem_ap<RM, SUB, SQ>(v[u].z, u2, c, all_pos, b2);
       o.w = elem_ap<RM, SUB, SQ>(v[u].w, u3, c, all_pos, b3);
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
-      y4[j] = o;
+      store_stream(y4 + j, o);
     }
     }
     if (threadIdx.x < (int)(ch.end - (e4 << 2))) {

@@ -871,7 +871,7 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
     }
     float* y = A.y + e0 + el0;
     if (A.vec && (FULL || el0 + 3 < n_el)) {
-      store_nt(reinterpret_cast<float4*>(y), make_float4(o[0], o[1], o[2], o[3]));
+      store_stream(reinterpret_cast<float4*>(y), make_float4(o[0], o[1], o[2], o[3]));
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
