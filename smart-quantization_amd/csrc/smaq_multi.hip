@@ -4,7 +4,7 @@
 // (grads, weights, momenta), each of which runs smart.py:110-190 separately (~24 ATen launches
 // + 1 host sync per tensor; a ResNet-34 step has 148 such tensors, median 256 elements).
 //
-// Design: the tensors are cut into fixed chunks (8192 elements by default); one workgroup per chunk.
+// Design: the tensors are cut into fixed chunks (4096 elements by default); one workgroup per chunk.
 //   launch 1 (stats): per-chunk shifted fp64 sums; a tensor with one chunk finalises in place,
 //            a larger tensor's last-arriving chunk reduces that tensor's partials in chunk order.
 //   launch 2 (apply): per chunk, the tensor's SmqSmaqStats + the element transform of smaq.hip,
@@ -23,8 +23,9 @@ namespace smq {
 // multiples of 4096). Measured on the ResNet-34 set (42.5M elements, 148 tensors): the statistics
 // launch wants few, long chunks (each chunk's partial hand-off is a store-drain + atomic round
 // trip: 8K chunks 62 us, 32K chunks 34 us; with the next 16 KiB step prefetched, r04: 32K 32.6 us,
-// 64K 30.7 us, 128K 38.3 us), the apply launch wants many short ones (8K 60 us, 32K 80 us).
-constexpr int64_t kDefaultChunk = 8192;
+// 64K 30.7 us, 128K 38.3 us), the apply launch wants many short ones (8K 60 us, 32K 80 us; with
+// sc0 sc1 nt output stores the whole step: 4K 79.9 us, 8K 82.3 us).
+constexpr int64_t kDefaultChunk = 4096;
 constexpr int64_t kDefaultStatsChunk = 65536;
 constexpr size_t kSnapBytes = 64;  // workspace slot: the call's random-stream snapshot
 

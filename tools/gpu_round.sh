@@ -23,6 +23,7 @@ for s in "$@"; do
     fqtiles) for v in 1 2; do SMQ_FQ_TILE=$v step bench_fp8_t$v 300 python bench.py --config fp8 --steps 50 --warmup 5; SMQ_FQ_TILE=$v step bench_s2fp8_t$v 300 python bench.py --config s2fp8 --steps 200 --warmup 20; done ;;
     cold) for v in 1 2; do SMQ_APPLY_TILE=$v step kbench_cold_t$v 300 python tools/kbench.py --quick --cold; done ;;
     chunks) for c in 4096 8192 16384 32768; do SMQ_MULTI_CHUNK=$c step bench_multi_c$c 300 python bench.py --config multi --steps 100 --warmup 10; done ;;
+    statchunks) for c in 32768 65536 131072; do SMQ_MULTI_STATS_CHUNK=$c step bench_multi_s$c 300 python bench.py --config multi --steps 100 --warmup 10; done ;;
     diag) step bench_diag 300 python tools/bench_diag.py ;;
     warm) step bench_w3 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline &&
           step bench_w20 300 python bench.py --steps 50 --warmup 20 --no-cpu-baseline &&
