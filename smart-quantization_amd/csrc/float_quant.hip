@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void float_quant_kernel(FQArgs A) {
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
       const int64_t j = t0 + u * kBlock;
-      if (j < nv) v[u] = load4<TIN>(A.x, j);
+      if (j < nv) v[u] = load4_stream<TIN>(A.x, j);
     }
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {

@@ -95,12 +95,12 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
     float4 cur[4], nxt[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (t + u * kBlock < nv) cur[u] = load4<TIN>(x, t + u * kBlock);
+      if (t + u * kBlock < nv) cur[u] = load4_stream<TIN>(x, t + u * kBlock);
     for (; t < nv; t += tstride) {
       const int64_t tn = t + tstride;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (tn + u * kBlock < nv) nxt[u] = load4<TIN>(x, tn + u * kBlock);
+        if (tn + u * kBlock < nv) nxt[u] = load4_stream<TIN>(x, tn + u * kBlock);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (t + u * kBlock < nv) {
@@ -274,7 +274,7 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemCon
     for (int u = 0; u < TV; ++u) {
       const int64_t j = t0 + u * kBlock;
       if (j < nv) {
-        v[u] = load4<TIN>(A.x, j);
+        v[u] = load4_stream<TIN>(A.x, j);
         if (RM == kRoundUniform) uu[u] = u4[j];
       }
     }

@@ -59,6 +59,15 @@ __device__ __forceinline__ float4 load4(const void* p, int64_t j) {
   return o;
 }
 
+// Streaming read of a tensor no later kernel of the call reads again (nt: bypasses L1, measured
+// faster for the statistics sweep, the SmaQ apply and the float quantiser; NOT for kernels whose
+// input the next launch re-reads, e.g. the S2FP8 partials -3 %, nor the multi-tensor chunks -0.8 %).
+template <int T>
+__device__ __forceinline__ float4 load4_stream(const void* p, int64_t j) {
+  if (T == kF32) return load_nt(static_cast<const float4*>(p) + j);
+  return load4<T>(p, j);
+}
+
 template <int T>
 constexpr int in_bytes() { return T == kF32 ? 4 : 2; }
 

@@ -150,12 +150,13 @@ def test_multi_plan_layout():
     from smart_compress_amd import _native as N
 
     lib = N.lib()
-    C, S = 8192, 65536  # default apply / statistics chunks (csrc/smaq_multi.hip)
+    C, S = 4096, 65536  # default apply / statistics chunks (csrc/smaq_multi.hip)
     sizes = [10, C, C + 1, 3 * C + 5, S + 1]
     count = len(sizes)
     arr = (ctypes.c_int64 * count)(*sizes)
     nbytes = lib.smq_smaq_multi_plan_bytes(arr, count)
-    chunks = [1, 1, 2, 4, 9]
+    nl = -(-(S + 1) // C)  # chunks of the last tensor
+    chunks = [1, 1, 2, 4, nl]
     schunks = [1, 1, 1, 1, 2]
     dbytes = ((40 * count + 31) // 32) * 32
     assert nbytes == 32 + dbytes + 64 * (sum(chunks) + sum(schunks))
@@ -179,10 +180,10 @@ def test_multi_plan_layout():
     q = rec[:, :48].copy().view(np.int64)  # x, y, n, begin, end, rng_offset
     i32 = rec[:, 48:].copy().view(np.int32)  # tensor, first_chunk, n_chunks, all_positive
     a = slice(0, sum(chunks))
-    assert list(i32[a, 0]) == [0, 1, 2, 2, 3, 3, 3, 3] + [4] * 9
-    assert list(i32[a, 1]) == [0, 1, 2, 2, 4, 4, 4, 4] + [8] * 9
-    assert list(i32[a, 2]) == [1, 1, 2, 2, 4, 4, 4, 4] + [9] * 9
-    assert list(i32[a, 3]) == [0, 1, 0, 0, 1, 1, 1, 1] + [0] * 9
+    assert list(i32[a, 0]) == [0, 1, 2, 2, 3, 3, 3, 3] + [4] * nl
+    assert list(i32[a, 1]) == [0, 1, 2, 2, 4, 4, 4, 4] + [8] * nl
+    assert list(i32[a, 2]) == [1, 1, 2, 2, 4, 4, 4, 4] + [nl] * nl
+    assert list(i32[a, 3]) == [0, 1, 0, 0, 1, 1, 1, 1] + [0] * nl
     assert list(q[a, 3])[:8] == [0, 0, 0, C, 0, C, 2 * C, 3 * C]
     assert list(q[a, 4])[:8] == [10, C, C, C + 1, C, 2 * C, 3 * C, 3 * C + 5]
     assert list(q[a, 5])[:5] == [0, 10, 10 + C, 10 + C, 10 + 2 * C + 1]
