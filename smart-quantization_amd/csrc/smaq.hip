@@ -63,10 +63,11 @@ static int grid_for(int64_t work_items, int per_block_items, int cap) {
 // profiles/r02_kbench_cold_tile*.json), truncation prefers 1.
 constexpr int kStatsGridCap = 2048;  // also the number of fp64 partials the last workgroup sums
 constexpr int kStatsTileGrid = 512;  // tile-stride sweep: 2 workgroups per CU (launch_stats)
+constexpr int64_t kStatsNtMinMB = 512;  // non-temporal statistics loads from this tensor size on
 
 static inline bool aligned(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
-template <bool RANGE, int TIN, bool TILE = false>
+template <bool RANGE, int TIN, bool TILE = false, bool NT = false>
 __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restrict__ x, int64_t n,
                                                             int vec, FinalizeArgs fin,
                                                             StatPartial* __restrict__ partials,
@@ -95,12 +96,12 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
     float4 cur[4], nxt[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (t + u * kBlock < nv) cur[u] = load4_stream<TIN>(x, t + u * kBlock);
+      if (t + u * kBlock < nv) cur[u] = NT ? load4_stream<TIN>(x, t + u * kBlock) : load4<TIN>(x, t + u * kBlock);
     for (; t < nv; t += tstride) {
       const int64_t tn = t + tstride;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (tn + u * kBlock < nv) nxt[u] = load4_stream<TIN>(x, tn + u * kBlock);
+        if (tn + u * kBlock < nv) nxt[u] = NT ? load4_stream<TIN>(x, tn + u * kBlock) : load4<TIN>(x, tn + u * kBlock);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (t + u * kBlock < nv) {
@@ -434,9 +435,21 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   const int grid = grid_for(n, per_wg, cap);
   FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n),
                    (unsigned long long*)p->offset_counter, n};
+  // non-temporal loads only for tensors well beyond the Infinity Cache: there they keep the
+  // sweep from thrashing it (1 GiB: 0.506-0.508 -> 0.499-0.502 ms/step); up to 256 MiB the apply
+  // launch re-reads x from the cache the plain loads filled (64 / 128 / 256 MiB tensors: 0.047 /
+  // 0.075 / 0.131 ms/step plain against 0.051 / 0.080 / 0.138 nt; tools/ntsize_exp.sh)
+  static const int64_t nt_min_bytes = [] {  // measurement knob SMQ_STATS_NT_MIN_MB
+    const char* e = getenv("SMQ_STATS_NT_MIN_MB");
+    return (int64_t)(e ? atoll(e) : kStatsNtMinMB) << 20;
+  }();
+  const bool nt = tile && 4 * n >= nt_min_bytes;
 #define SMQ_STATS(RANGE, TIN)                                                                       \
   do {                                                                                              \
-    if (tile)                                                                                       \
+    if (tile && nt)                                                                                 \
+      hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true, true>), dim3(grid), dim3(kBlock), 0,  \
+                         st, x, n, vec, fin, partials, counter, hdr);                               \
+    else if (tile)                                                                                  \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true>), dim3(grid), dim3(kBlock), 0, st, x, \
                          n, vec, fin, partials, counter, hdr);                                      \
     else                                                                                            \

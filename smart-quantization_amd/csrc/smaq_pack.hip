@@ -184,7 +184,7 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
   for (int k = 0; k < 4; ++k) {
     const int el = 1024 * k + 4 * tid;
     if (VEC && (FULL || el + 3 < n_el)) {
-      const float4 t = load4<TIN>(A.x, (e0 + el) >> 2);
+      const float4 t = load4_stream<TIN>(A.x, (e0 + el) >> 2);
       xv[k][0] = t.x; xv[k][1] = t.y; xv[k][2] = t.z; xv[k][3] = t.w;
     } else {
 #pragma unroll
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
   for (int k = 0; k < 4; ++k) {
     const int el = 1024 * k + 4 * tid;
     if (VEC && (FULL || el + 3 < n_el)) {
-      const float4 t = load4<TIN>(A.x, (e0 + el) >> 2);
+      const float4 t = load4_stream<TIN>(A.x, (e0 + el) >> 2);
       xv[k][0] = t.x; xv[k][1] = t.y; xv[k][2] = t.z; xv[k][3] = t.w;
     } else {
 #pragma unroll
