@@ -430,6 +430,50 @@ __device__ __forceinline__ uint32_t record_of(float q, bool hi, bool lo, int wm,
              : (((uint32_t)o << 15) | code);
 }
 
+// Records of one lane's 16 elements (smaq_code_kernel); returns its outliers | escapes << 16.
+template <int RM, int TIN, bool FULL, bool SUB>
+__device__ __forceinline__ uint32_t code_records(const PackArgs& A, const ElemConsts& c,
+                                                 const float (&xv)[4][4], int64_t e0, int n_el,
+                                                 int wm, int wo) {
+  const int tid = threadIdx.x;
+  uint32_t cnt = 0;  // outliers (bits 0-15) | escapes (bits 16-31) of this lane's elements
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int el = 1024 * k + 4 * tid;
+    const bool full4 = FULL || el + 3 < n_el;
+    float u[4] = {0.f, 0.f, 0.f, 0.f};
+    if (RM == kRoundHash) {
+      const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
+      if (full4) {
+        rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (el + i < n_el) u[i] = rng_hu(A.key, ctr + i);
+      }
+    }
+    uint32_t r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool hi, lo, esc;
+      const float q = smaq_quant<RM, false, TIN, SUB>(xv[k][i], u[i], c, hi, lo);
+      r[i] = record_of(q, hi, lo, wm, wo, esc);
+      const bool o = hi | lo;
+      const bool valid = FULL || el + i < n_el;
+      cnt += valid ? ((uint32_t)o | ((uint32_t)esc << 16)) : 0u;
+    }
+    uint16_t* dst = A.rec + e0 + el;
+    if (full4) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (el + i < n_el) dst[i] = (uint16_t)r[i];
+    }
+  }
+  return cnt;
+}
+
 // One workgroup per block (half-block workgroups, the second to finish adding the block's size,
 // measured 357 vs 338 us at 256M).
 template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO>
@@ -458,43 +502,13 @@ __global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
         xv[k][i] = (FULL || el + i < n_el) ? load1<TIN>(A.x, e0 + el + i) : 0.f;
     }
   }
-  uint32_t cnt = 0;  // outliers (bits 0-15) | escapes (bits 16-31) of this lane's elements
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int el = 1024 * k + 4 * tid;
-    const bool full4 = FULL || el + 3 < n_el;
-    float u[4] = {0.f, 0.f, 0.f, 0.f};
-    if (RM == kRoundHash) {
-      const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
-      if (full4) {
-        rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (el + i < n_el) u[i] = rng_hu(A.key, ctr + i);
-      }
-    }
-    uint32_t r[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bool hi, lo, esc;
-      const float q = smaq_quant<RM, false, TIN, true>(xv[k][i], u[i], c, hi, lo);
-      r[i] = record_of(q, hi, lo, wm, wo, esc);
-      const bool o = hi | lo;
-      const bool valid = FULL || el + i < n_el;
-      cnt += valid ? ((uint32_t)o | ((uint32_t)esc << 16)) : 0u;
-    }
-    uint16_t* dst = A.rec + e0 + el;
-    if (full4) {
-      *reinterpret_cast<uint2*>(dst) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (el + i < n_el) dst[i] = (uint16_t)r[i];
-    }
-  }
-  cnt = wave_total_u32(cnt);
-  if (lane == 0) s_cnt[w] = cnt;
+  // the subnormal-quotient check only where quot_check_for() asks for it (one uniform branch
+  // per workgroup; the x loads above are already in flight)
+  const uint32_t cnt = A.stats->quot_check
+      ? code_records<RM, TIN, FULL, true>(A, c, xv, e0, n_el, wm, wo)
+      : code_records<RM, TIN, FULL, false>(A, c, xv, e0, n_el, wm, wo);
+  const uint32_t tot = wave_total_u32(cnt);
+  if (lane == 0) s_cnt[w] = tot;
   __syncthreads();
   if (tid == 0) {
     const uint32_t t = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
