@@ -297,3 +297,26 @@ def test_streaming_packer_unaligned_and_half(dt):
     packed = type("P", (), {"header": lambda self: h})()
     stream, _, _ = _oracle_stream(x.float().cpu().numpy(), packed, hp, 8, 0, dtype=dt)
     assert np.array_equal(got, stream)
+
+
+@pytest.mark.parametrize("scale", [1e8, 3.0e-3])
+def test_streaming_packer_quot_check_paths(scale):
+    """std >= 2^24 makes the statistics ask for the per-element subnormal-quotient check
+    (quot_check_for): the streaming packer's checked body gives the oracle's bytes and the same
+    bytes as the single launch; a small scale exercises the unchecked body."""
+    from smart_compress_amd import _native as N
+
+    hp, pk, _ = _codecs(seed=6, offset=2)
+    n = 5 * 4096 + 123
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(n, generator=gen, device="cuda") * scale
+    p = pk._params(n, False, x.dtype, x.device)
+    a = _compress_raw(x, pk, 0, p)
+    b = _compress_raw(x, pk, N.SMQ_PACK_SINGLE, p)
+    assert np.array_equal(a, b)
+    from oracle import smaq_packed as P
+
+    h = P.header(a)
+    packed = type("P", (), {"header": lambda self: h})()
+    stream, _, _ = _oracle_stream(x.cpu().numpy(), packed, hp, 6, 2)
+    assert np.array_equal(a, stream)
