@@ -218,6 +218,13 @@ def run_smaq(args, world, rank, device):
     # two input tensors, alternated per step, so a step never finds the previous step's input in
     # the 256 MB Infinity Cache (in training every call sees a different tensor)
     xs = [torch.randn(n, generator=gen, device=device) for _ in range(2)]
+    # measurement knob SMQ_BENCH_DTYPE=f16|bf16: half-precision inputs (statistics and apply read
+    # 2 B/elem, the output stays fp32: 8 B/elem of algorithmic traffic)
+    in_dt = {"f16": torch.float16, "bf16": torch.bfloat16}.get(os.environ.get("SMQ_BENCH_DTYPE", ""))
+    if in_dt is not None:
+        xs = [x.to(in_dt) for x in xs]
+        if in_dt == torch.float16:
+            codec.hparams.precision = 16
     trace = EventTrace()
     codec._trace = trace
     out = {"i": 0}
@@ -232,16 +239,19 @@ def run_smaq(args, world, rank, device):
         step()
     trace.enabled = True
     elapsed = time_steps(step, args.steps, 0, world, device)
-    alg_per_elem = 8 if sampled else 12
+    in_bytes = 4 if in_dt is None else 2
+    alg_per_elem = (in_bytes + 4) if sampled else (2 * in_bytes + 4)
     total_bytes = sum_over_ranks(alg_per_elem * n * args.steps, world, device)
     value = total_bytes / elapsed / 1e9
     apply_ms = trace.mean_ms("apply")
-    apply_gbps = 8.0 * n / (apply_ms * 1e-3) / 1e9
+    apply_gbps = (in_bytes + 4.0) * n / (apply_ms * 1e-3) / 1e9
     res = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32" if in_dt is None else f"{os.environ['SMQ_BENCH_DTYPE']} in, fp32 out",
+        "data": "synthetic",
         "config": {"workload": "smaq_6_8_roundtrip_256M_fp32" if not sampled else
                    "smaq_6_8_roundtrip_sampled_stats", "elements_per_gpu": n,
                    "stats": "sampled(16)" if sampled else "full", "rounding": "stochastic",
@@ -251,7 +261,7 @@ def run_smaq(args, world, rank, device):
         "roofline": {"bound": "hbm", "kernel": "smaq_apply_kernel",
                      "achieved": round(apply_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(apply_gbps / HBM_PEAK_GBPS, 4),
-                     "alg_bytes_per_launch": 8 * n,
+                     "alg_bytes_per_launch": int((in_bytes + 4) * n),
                      "avg_launch_ms": round(apply_ms, 5),
                      "traffic": traffic_from_profile(args.config)},
         # the statistics launch is not bracketed by events (an event between the two launches
