@@ -3,6 +3,7 @@
 // Reference: smart_compress/compress/smart.py:100-108, 130-134, 151-182.
 #pragma once
 
+#include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include <math.h>
 
@@ -22,11 +23,11 @@ enum InType { kF32 = SMQ_DTYPE_F32, kF16 = SMQ_DTYPE_F16, kBF16 = SMQ_DTYPE_BF16
 template <int T>
 __device__ __forceinline__ float round_in(float v) {
   if (T == kF16) return __half2float(__float2half_rn(v));
-  if (T == kBF16) {  // round to nearest even, NaN stays NaN
-    uint32_t u = __builtin_bit_cast(uint32_t, v);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return v;
-    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
-    return __builtin_bit_cast(float, u);
+  if (T == kBF16) {
+    // round to nearest even in hardware (v_cvt_pk_bf16_f32, then a 16-bit shift back): two VALU
+    // ops instead of the five of the integer form (u + 0x7fff + lsb) & 0xffff0000 with its NaN
+    // test; NaN stays NaN (its payload's top bits kept, as torch's bf16 rounding keeps them)
+    return __bfloat162float(__float2bfloat16(v));
   }
   return v;
 }
