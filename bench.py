@@ -237,8 +237,18 @@ def run_smaq(args, world, rank, device):
     prewarm(step, device)
     for _ in range(args.warmup):
         step()
-    trace.enabled = True
+    # the K timed steps carry no per-launch event markers (an event pair between two launches
+    # costs a few us per step); the apply launch duration for `roofline` is then measured with an
+    # event pair around each apply launch over K more steps of the same workload, on the codec's
+    # stream (SMQ_BENCH_EVENTS_IN_TIMED=1: events inside the timed steps instead)
+    in_timed = os.environ.get("SMQ_BENCH_EVENTS_IN_TIMED") == "1"
+    trace.enabled = in_timed
     elapsed = time_steps(step, args.steps, 0, world, device)
+    if not in_timed:
+        trace.enabled = True
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
     in_bytes = 4 if in_dt is None else 2
     alg_per_elem = (in_bytes + 4) if sampled else (2 * in_bytes + 4)
     total_bytes = sum_over_ranks(alg_per_elem * n * args.steps, world, device)
