@@ -1,10 +1,14 @@
 // Packed SmaQ container (include/smq.h "Packed SmaQ container") on gfx950.
 //
-// compress = statistics (smaq.hip, full or sampled) + ONE packing launch:
+// compress = statistics (smaq.hip, full or sampled) + the streaming packer (default, code widths
+// <= 14 bits; see "streaming packer" below): smaq_code_kernel (one 16-bit record per element and
+// the block's image size into its group sum) -> smaq_pack_scan_kernel (group prefixes, header) ->
+// smaq_emit_kernel (each block's image at its prefix). No workgroup waits on another.
+// SMQ_PACK_SINGLE (and wider codes) take ONE packing launch instead:
 //   * each workgroup owns a block of SMQ_PACK_BLOCK = 4096 elements (16 per lane, 4 x dwordx4),
 //     quantises them with the same element code as the simulated round trip (smaq_quant), and
-//     builds the block image in LDS: outlier mask, main plane, outlier plane (LDS atomics for the
-//     bit-packed codes; ranks from wave ballots + a 16-segment scan);
+//     builds the block image in LDS: outlier mask and the element-order code stream (LDS ORs;
+//     ranks from DPP wave scans + per-wave segment prefixes);
 //   * blocks are compacted into one dense stream by a decoupled look-back scan: workgroup b packs
 //     block b (index order; SMQ_PACK_TICKETED takes ids from an atomic ticket instead), publishes
 //     its size, and wave 0 reads up to 64 predecessors' status words per step until it meets an
@@ -12,8 +16,9 @@
 //     value, so no fences are needed; a bounded spin turns a would-be hang into header.error;
 //   * the block image is written with coalesced stores at its prefix, escapes directly, and the
 //     block's word offset into the directory (random-access decode).
+// Both give the same bytes.
 // decompress = one launch, one workgroup per block: block image -> LDS, mask prefix popcounts,
-//   per-element plane reads, escapes via an LDS bitmask + binary search of the block's sorted list,
+//   per-element plane reads, escapes via an LDS bitmask + O(1) rank in the block's sorted list,
 //   then smaq_dequant — the same arithmetic as the simulated round trip, so the result is
 //   bit-identical to smq_smaq_apply for the same statistics and random stream.
 #include <hip/hip_runtime.h>
