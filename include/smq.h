@@ -306,8 +306,9 @@ size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier);
  * of 2 B per element); zero-filled once at allocation, left reusable by every call. */
 size_t smq_smaq_pack_workspace_bytes(int64_t n);
 /* Statistics (full / sampled / range, params as smq_smaq_stats) then the packing launches (see
- * smq_smaq_compress_ex). Writes the whole stream incl. header.total_bytes on the device; packed_bytes >= smq_smaq_pack_bound. The BN
- * variant and injected uniforms are not supported (SMQ_ERR_INVALID). */
+ * smq_smaq_compress_ex). Writes the whole stream incl. header.total_bytes on the device;
+ * packed_bytes >= smq_smaq_pack_bound. The BN variant and injected uniforms are not supported
+ * (SMQ_ERR_INVALID). */
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
                       void* packed, size_t packed_bytes, void* workspace, size_t workspace_bytes,
                       void* stream);
