@@ -478,8 +478,13 @@ def run_packed(args, world, rank, device):
     prewarm(step, device)
     for _ in range(args.warmup):
         step()
-    trace.enabled = True
+    # timed steps without event markers; compress / decompress durations from K more steps with an
+    # event pair around each call (as for the headline)
     elapsed = time_steps(step, args.steps, 0, world, device)
+    trace.enabled = True
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
     hdr = N.SmqPackedHeader.from_buffer_copy(bytes(packed[:128].cpu().numpy()))
     sbytes = int(hdr.total_bytes)
     # algorithmic bytes: stats read 4n, pack read 4n + stream write, unpack stream read + 4n write
