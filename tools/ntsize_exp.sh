@@ -1,7 +1,7 @@
 #!/bin/bash
 # Statistics-load policy vs tensor size: SMQ_STATS_NT_MIN_MB=0 (always nt) vs 100000 (never).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-for e in 4194304 16777216 33554432 67108864 268435456; do for r in 1 2; do for m in 0 100000; do
+for e in 16777216 67108864 268435456; do for r in 1 2; do for m in 0 100000; do
   SMQ_STATS_NT_MIN_MB=$m timeout -k 10 200 python bench.py --elements $e --steps 100 --warmup 10 --no-cpu-baseline > gpurun_out/nts_${e}_${m}_$r.log 2>&1 || exit 1
   python -c "import json;d=json.loads(open('gpurun_out/nts_${e}_${m}_$r.log').read().strip().splitlines()[-1]);print('n=$e nt_min=$m run $r', d['value'], d['ms_per_step'])"
 done; done; done
