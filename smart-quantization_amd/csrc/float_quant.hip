@@ -89,6 +89,7 @@ struct FQArgs {
   int exp_bits, man_bits;
   int check_inf;
   float max_value;
+  int nt_loads;  // non-temporal x loads: inputs of >= kFqNtMinMB only (see smq_float_quant)
 };
 
 // y element stores: fp32, or fp16 (precision 16: float_quantize returns .half(), RN)
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void float_quant_kernel(FQArgs A) {
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
       const int64_t j = t0 + u * kBlock;
-      if (j < nv) v[u] = load4_stream<TIN>(A.x, j);
+      if (j < nv) v[u] = A.nt_loads ? load4_stream<TIN>(A.x, j) : load4<TIN>(A.x, j);
     }
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
@@ -610,6 +611,13 @@ int smq_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t
   A.man_bits = man_bits;
   A.check_inf = check_inf;
   A.max_value = host_max_value(exp_bits, man_bits);
+  // non-temporal loads only for inputs beyond the Infinity Cache, the SmaQ policy (smaq.hip):
+  // nt loads of cache-resident data lose its hits (C3 with 8 rotating buffers, cold: nt +2 %)
+  static const int64_t nt_min = [] {
+    const char* e = getenv("SMQ_STATS_NT_MIN_MB");
+    return (int64_t)(e ? atoll(e) : 512) << 20;
+  }();
+  A.nt_loads = (int64_t)(dtype_in == SMQ_DTYPE_F32 ? 4 : 2) * n >= nt_min ? 1 : 0;
   const bool sr = rounding == SMQ_ROUND_STOCHASTIC;
   const bool rarr = sr && rand_bits != nullptr;
   const bool hout = dtype_out == SMQ_DTYPE_F16;
