@@ -7,16 +7,21 @@ A "step" = one round trip of that tensor (stats launch + apply launch, output te
 the codec like the reference). value = algorithmic bytes (12 B/elem: stats read + apply read +
 write) over all ranks / max-over-ranks wall time of the K timed steps.
 
-Multi-GPU: one process per GPU (torchrun), each rank owns its own 256M tensor (independent
-units, "weak" scaling, no data-path collective; the only collectives are the timing barrier and
-the max-over-ranks reduction of the elapsed time).
+Multi-GPU (independent units, no data-path collective): one process per GPU, each with
+its own tensors and seed ("weak" scaling). `bench.py --gpus N` launches the N rank processes itself
+(before any GPU call) when no launcher did; under torchrun (RANK / WORLD_SIZE set) each process is
+one rank. Ranks meet in a CPU (gloo) process group that only carries the start/stop barriers and
+the reduction of the timings: no RCCL. Rank 0 prints the one JSON line with every rank's time.
 
-Other configs (--config fp8 | s2fp8 | multi | smaq_sampled) are measurement aids, not the line
-the driver records.
+Other configs (--config smaq_sampled | fp8 | s2fp8 | multi | packed | autograd) are measurement
+aids (BASELINE configs 3-5 and SURVEY 8f), not the line the driver records; each carries its own
+`roofline` and, at N=1, a `cpu_baseline`.
 
 roofline: the dominant kernel is smaq_apply_kernel (8 B/elem algorithmic); its average duration is
-measured with events on the codec's stream around every launch inside the timed region.
-cpu_baseline: the oracle (numpy restatement of smart.py, single thread) on a bounded sample.
+measured with events on the codec's stream around each launch (over K steps after the timed ones).
+cpu_baseline: the CPU restatement in oracle/ (kind "port"): smart.py's own torch-CPU op sequence
+(oracle/smaq_torch.py, 16 intra-op threads) for SmaQ, the numpy qtorch / s2fp8 restatements (one
+thread) for FP8 / S2FP8, on a bounded sample.
 """
 
 import argparse
@@ -114,21 +119,22 @@ class EventTrace:
 
 
 def dist_setup():
+    """This process's rank. World > 1: a CPU (gloo) process group over 127.0.0.1 — it carries the
+    start/stop barriers and the timing reductions only; the codecs never communicate."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if os.environ.get("SMQ_BENCH_SHARE_DEVICE") == "1":
-        local = 0  # rehearsal of the N>1 flow on a 1-GPU box (gloo collectives, shared card)
+        local = 0  # rehearsal of the N>1 flow on a 1-GPU box (shared card)
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
 
-        backend = os.environ.get("SMQ_BENCH_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    elif torch.cuda.is_available():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=300))
+    if torch.cuda.is_available():
         torch.cuda.set_device(local)
     return world, rank, local
 
@@ -140,30 +146,83 @@ def barrier(world):
         dist.barrier()
 
 
-def _coll_device(device):
-    import torch.distributed as dist
-
-    return device if dist.get_backend() == "nccl" else torch.device("cpu")
-
-
-def max_over_ranks(value, world, device):
+def max_over_ranks(value, world, device=None):
     if world == 1:
         return value
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
+    t = torch.tensor([value], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def sum_over_ranks(value, world, device):
+def sum_over_ranks(value, world, device=None):
     if world == 1:
         return value
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
+    t = torch.tensor([value], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def gather_over_ranks(value, world):
+    """Every rank's value, in rank order (on every rank)."""
+    if world == 1:
+        return [value]
+    import torch.distributed as dist
+
+    t = torch.zeros(world, dtype=torch.float64)
+    t[dist.get_rank()] = value
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK,
+    LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1) and wait for them. This process never
+    touches the GPU (the children are started before anything initialises HIP). Rank 0's stdout —
+    the one JSON line — is relayed; if a rank fails, the others are stopped. Returns the exit code."""
+    import subprocess
+
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        pending = set(range(n))
+        while pending:
+            for r in sorted(pending):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                pending.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:  # a rank died: the others would wait at a barrier
+                        procs[q].terminate()
+            time.sleep(0.05)
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    out = procs[0].stdout.read().decode()
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return rc
 
 
 def smaq_hparams(**over):
@@ -180,6 +239,11 @@ def smaq_hparams(**over):
 
 HOST = {}
 PREWARM_S = 0.5
+
+
+def _sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
 
 
 def prewarm(step, device):
@@ -199,9 +263,9 @@ def time_steps(step, steps, warmup, world, device, region=None):
     of the timed region (no event between the steps)."""
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    _sync()
     barrier(world)
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     if region is not None:
         region.begin("region")
@@ -210,47 +274,137 @@ def time_steps(step, steps, warmup, world, device, region=None):
     if region is not None:
         region.end("region")
     HOST["enqueue_ms_per_step"] = (time.perf_counter() - t0) / steps * 1e3
-    torch.cuda.synchronize()
+    _sync()
+    own = time.perf_counter() - t0  # this rank's own work, before it waits for the others
     barrier(world)
     elapsed = time.perf_counter() - t0
+    HOST["rank_ms_per_step"] = [round(v / steps * 1e3, 4) for v in gather_over_ranks(own, world)]
     return max_over_ranks(elapsed, world, device)
 
 
-def cpu_baseline_smaq(sample_elems, budget_s):
+def _cpu_threads():
+    """Intra-op threads of this job's CPU share (OMP_NUM_THREADS, 16 on the GPU box; os.cpu_count()
+    counts the whole machine there)."""
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+
+def _time_reps(fn, budget_s, min_reps=2):
+    fn()  # warm-up (allocator, thread pool)
+    reps, t_tot, ts = 0, 0.0, []
+    while t_tot < budget_s or reps < min_reps:
+        t0 = time.perf_counter()
+        fn()
+        dt = time.perf_counter() - t0
+        ts.append(dt)
+        t_tot += dt
+        reps += 1
+    return reps, t_tot, ts
+
+
+def cpu_baseline_smaq(args, sampled=False):
     """The reference's algorithm on the host cores: oracle/smaq_torch.py, smart.py's own torch-CPU
-    op sequence (full stats, torch.rand_like SR; bit-exact with the reference's outputs on the
-    golden fixtures), on a bounded sample, with as many intra-op threads as this job's CPU share
-    (OMP_NUM_THREADS, 16 on the GPU box; os.cpu_count() counts the whole machine there)."""
+    op sequence (full stats — or randperm-sampled ones —, torch.rand_like SR; bit-exact with the
+    reference's outputs on the golden fixtures), on a bounded sample of the workload, plus the
+    reference's own CPU config C1 (1M elements, median of >= 30 calls) for BASELINE.md."""
     from oracle import smaq_torch
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = _cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    ns = 16 if sampled else 0
+    try:
+        x = torch.randn(args.cpu_sample, generator=torch.Generator().manual_seed(0))
+        reps, t_tot, _ = _time_reps(lambda: smaq_torch.roundtrip(x, num_samples=ns),
+                                    args.cpu_budget)
+        torch.manual_seed(0)
+        x1 = torch.randn(1 << 20)
+        _, _, t1 = _time_reps(lambda: smaq_torch.roundtrip(x1, num_samples=ns), 0.0, min_reps=30)
+    finally:
+        torch.set_num_threads(prev)
+    per = 8.0 if sampled else 12.0
+    gbps = per * args.cpu_sample * reps / t_tot / 1e9
+    c1_ms = float(np.median(t1)) * 1e3
+    return {"value": round(gbps, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x {args.cpu_sample} fp32 N(0,1) round trips, oracle/smaq_torch.py "
+                      f"(smart.py's torch-CPU op sequence, {'sampled(16)' if sampled else 'full'} "
+                      f"stats + rand_like SR), {threads} threads, {t_tot:.1f} s",
+            "c1_1M": {"ms_median": round(c1_ms, 3),
+                      "gbps": round(per * (1 << 20) / (c1_ms * 1e-3) / 1e9, 4), "reps": len(t1)}}
+
+
+def cpu_baseline_float(args, codec):
+    """FP8 / S2FP8 on the host: the numpy restatements (oracle/qtorch_float.py with check_inf,
+    oracle/s2fp8.py) — the reference's CPU path would be qtorch's single-thread C++ loop, absent
+    here — one thread, on a bounded sample."""
+    from oracle import qtorch_float as qf
+    from oracle import rng as orng
+    from oracle import s2fp8 as os2
+
+    n = min(args.cpu_sample, 1 << 22)
+    x = np.random.default_rng(0).standard_normal(n).astype(np.float32)
+    if codec == "fp8":
+        x = np.maximum(x, 0)
+        r = orng.rng_u32(7, 0, n)
+        fn, per = (lambda: qf.float_quantize(x, 5, 2, r, True)), 8.0
+    else:
+        r = orng.rng_u32(7, 0, n)
+        fn, per = (lambda: os2.roundtrip(x, r, True)), 12.0
+    reps, t_tot, _ = _time_reps(fn, args.cpu_budget)
+    return {"value": round(per * n * reps / t_tot / 1e9, 4), "unit": "GB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{reps} x {n} fp32 elements, numpy restatement "
+                      f"({'oracle/qtorch_float.py E5M2 SR + check_inf' if codec == 'fp8' else 'oracle/s2fp8.py'}),"
+                      f" 1 thread, {t_tot:.1f} s"}
+
+
+def cpu_baseline_multi(args):
+    """C5 on the host: the reference's per-tensor calls (optimizer.py:79-127 -> smart.py) as
+    oracle/smaq_torch.py over the same 148 ResNet-34 tensors, all host threads."""
+    from oracle import smaq_torch
+
+    threads = _cpu_threads()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
         g = torch.Generator().manual_seed(0)
-        x = torch.randn(sample_elems, generator=g)
-        smaq_torch.roundtrip(x)  # warm-up (allocator, thread pool)
-        reps, t_tot = 0, 0.0
-        while t_tot < budget_s or reps < 2:
-            t0 = time.perf_counter()
-            smaq_torch.roundtrip(x)
-            t_tot += time.perf_counter() - t0
-            reps += 1
+        ts = [torch.randn(s, generator=g) * 1e-3 for s in resnet34_c5_shapes()]
+        n = sum(t.numel() for t in ts)
+
+        def step():
+            for t in ts:
+                if t.numel() >= 8:
+                    smaq_torch.roundtrip(t)
+
+        reps, t_tot, _ = _time_reps(step, args.cpu_budget)
     finally:
         torch.set_num_threads(prev)
-    gbps = 12.0 * sample_elems * reps / t_tot / 1e9
-    return {"value": round(gbps, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} x {sample_elems} fp32 N(0,1) round trips, oracle/smaq_torch.py "
-                      f"(smart.py's torch-CPU op sequence, full stats + rand_like SR), "
-                      f"{threads} threads, {t_tot:.1f} s"}
+    return {"value": round(12.0 * n * reps / t_tot / 1e9, 4), "unit": "GB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{reps} steps x 148 tensors ({n} elements), oracle/smaq_torch.py per tensor "
+                      f"(the reference's per-parameter SmartFP calls), {threads} threads, "
+                      f"{t_tot:.1f} s"}
 
 
-def traffic_from_profile(config):
+CPU_BASELINES = {
+    "smaq": lambda a: cpu_baseline_smaq(a),
+    "smaq_sampled": lambda a: cpu_baseline_smaq(a, sampled=True),
+    "fp8": lambda a: cpu_baseline_float(a, "fp8"),
+    "s2fp8": lambda a: cpu_baseline_float(a, "s2fp8"),
+    "multi": lambda a: cpu_baseline_multi(a),
+}
+
+
+def traffic_from_profile(config, whole_call=False):
+    """HBM bytes per launch from the committed PMC passes (profiles/traffic_<config>.json): the
+    dominant kernel's, or (whole_call) the sum over the call's kernels."""
     path = os.path.join(REPO, "profiles", f"traffic_{config}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f).get("apply_bytes_per_launch")
+        d = json.load(f)
+    if whole_call:
+        return float(sum(d.get("kernels", {}).values())) or None
+    return d.get("apply_bytes_per_launch")
 
 
 def run_smaq(args, world, rank, device):
@@ -315,6 +469,10 @@ def run_smaq(args, world, rank, device):
                    "bits": "6/8", "alg_bytes_per_elem": alg_per_elem,
                    "parallelism": f"replicas{world}"},
         "pct_hbm_peak": round(100.0 * value / world / HBM_PEAK_GBPS, 2),
+        # the same time read as tensor GB/s (in_bytes * n per step) and as HBM-read
+        # GB/s (statistics read + apply read: the north star's "HBM-read roofline" reading)
+        "tensor_gbps": round(value * in_bytes / alg_per_elem, 2),
+        "read_gbps": round(value * (alg_per_elem - 4) / alg_per_elem, 2),
         "roofline": {"bound": "hbm", "kernel": "smaq_apply_kernel",
                      "achieved": round(apply_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(apply_gbps / HBM_PEAK_GBPS, 4),
@@ -370,7 +528,10 @@ def run_fp8(args, world, rank, device):
 
 
 def run_s2fp8(args, world, rank, device):
-    """Config 4: S2FP8 on [32,128,768], rotating 48 buffers (> MALL)."""
+    """Config 4: S2FP8 on [32,128,768], rotating 48 buffers (> MALL). Two variants of the same
+    calls: eager S2FP8.__call__ (the reference's usage; `value`), and the 48 calls of one rotation
+    captured in a hipGraph and replayed (graph_safe random stream), which removes the host path
+    and shows the device time per call."""
     from smart_compress_amd.compress.s2fp8 import S2FP8
     from argparse import ArgumentParser
 
@@ -388,46 +549,119 @@ def run_s2fp8(args, world, rank, device):
         codec(xs[it[0] % nbuf])
         it[0] += 1
 
+    trace = EventTrace()
     prewarm(step, device)
-    elapsed = time_steps(step, args.steps, args.warmup, world, device)
+    elapsed = time_steps(step, args.steps, args.warmup, world, device, region=trace)
+    enqueue = HOST.get("enqueue_ms_per_step", 0.0)
+    eager_dev_ms = trace.mean_ms("region") / args.steps
+    # hipGraph variant: one graph = one rotation of nbuf calls
+    codec.graph_safe(True, device=device)
+    try:
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            for x in xs:
+                codec(x)
+        torch.cuda.current_stream(device).wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for x in xs:
+                codec(x)
+        reps = max(1, -(-args.steps // nbuf))
+        gtrace = EventTrace()
+        g_elapsed = time_steps(g.replay, reps, max(1, args.warmup // nbuf), world, device,
+                               region=gtrace)
+        g_ms = g_elapsed / (reps * nbuf) * 1e3
+        g_dev_ms = gtrace.mean_ms("region") / (reps * nbuf)
+    finally:
+        codec.graph_safe(False)
     total = sum_over_ranks(12.0 * n * args.steps, world, device)
+    gbps = 12.0 * n / (g_dev_ms * 1e-3) / 1e9
     return {"metric": "S2FP8 round-trip GB/s, [32,128,768] fp32", "value": round(total / elapsed / 1e9, 2),
             "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "host_enqueue_ms_per_step": round(HOST.get("enqueue_ms_per_step", 0.0), 4),
+            "host_enqueue_ms_per_step": round(enqueue, 4),
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": "s2fp8_roundtrip_bert_hidden", "shape": list(shape),
-                       "rotating_buffers": nbuf}}
+                       "rotating_buffers": nbuf, "alg_bytes_per_elem": 12,
+                       "parallelism": f"replicas{world}"},
+            "variants": {"eager": {"ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                                   "device_ms_per_step": round(eager_dev_ms, 5)},
+                         "graph": {"ms_per_step": round(g_ms, 5),
+                                   "device_ms_per_step": round(g_dev_ms, 5)}},
+            # one call = the partials + apply launches, timed together (graph replay: no host gaps)
+            "roofline": {"bound": "hbm", "kernel": "s2fp8_partial_kernel+s2fp8_apply_kernel",
+                         "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(gbps / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": int(12 * n),
+                         "avg_launch_ms": round(g_dev_ms, 5), "traffic": traffic_from_profile("s2fp8", True)}}
 
 
-RESNET34_PARAMS = (
-    [(512, 512, 3, 3)] * 5 + [(512, 256, 3, 3)] + [(256, 256, 3, 3)] * 11 + [(256, 128, 3, 3)]
-    + [(128, 128, 3, 3)] * 7 + [(512, 256, 1, 1), (128, 64, 3, 3)] + [(64, 64, 3, 3)] * 6
-    + [(256, 128, 1, 1), (128, 64, 1, 1), (10, 512), (64, 3, 3, 3)] + [(512,)] * 14
-    + [(256,)] * 26 + [(128,)] * 18 + [(64,)] * 14 + [(10,)]
-)
+def resnet34_cifar_params():
+    """(shape, in the BN group) of every parameter of the reference's CIFAR ResNet-34, in module
+    order (models/pytorch/resnet.py:133-260: 3x3 stem, BasicBlock layers [3, 4, 6, 3] with 1x1
+    downsample shortcuts, fc 512 -> 10): 110 tensors, 21,282,122 elements."""
+    out = [((64, 3, 3, 3), False), ((64,), True), ((64,), True)]
+    cin = 64
+    for planes, blocks, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+        for b in range(blocks):
+            s = stride if b == 0 else 1
+            out += [((planes, cin, 3, 3), False), ((planes,), True), ((planes,), True),
+                    ((planes, planes, 3, 3), False), ((planes,), True), ((planes,), True)]
+            if b == 0 and (s != 1 or cin != planes):
+                out += [((planes, cin, 1, 1), False), ((planes,), True), ((planes,), True)]
+            cin = planes
+    out += [((10, 512), False), ((10,), False)]
+    return out
+
+
+def resnet34_c5_shapes():
+    """BASELINE config 5, one optimizer step's SmaQ tensors: the 110 gradients (every parameter)
+    then the 38 weights of the non-BN group (models/base.py:139-150 puts BatchNorm2d parameters in
+    a no_weight_compression group; the fc bias stays): 148 tensors, 42,547,220 elements."""
+    ps = resnet34_cifar_params()
+    return [s for s, _ in ps] + [s for s, bn in ps if not bn]
+
+
+def resnet34_c5_tensors(device, seed):
+    """C5 values: gradients ~ N(0, 1e-3); conv weights Kaiming-normal fan_out (resnet.py:186-188),
+    fc weight / bias U(-1/sqrt(512), 1/sqrt(512)) (nn.Linear's default)."""
+    gen = torch.Generator(device=device).manual_seed(seed)
+    ps = resnet34_cifar_params()
+    grads = [torch.randn(s, generator=gen, device=device) * 1e-3 for s, _ in ps]
+    weights = []
+    for s, bn in ps:
+        if bn:
+            continue
+        if len(s) == 4:
+            std = (2.0 / (s[0] * s[2] * s[3])) ** 0.5
+            weights.append(torch.randn(s, generator=gen, device=device) * std)
+        else:
+            b = 1.0 / 512 ** 0.5
+            weights.append((torch.rand(s, generator=gen, device=device) * 2 - 1) * b)
+    return grads + weights
 
 
 def run_multi(args, world, rank, device):
-    """Config 5: fused multi-tensor SmaQ over ResNet-34 (CIFAR) grads (110) + non-BN weights (38)."""
+    """Config 5: fused multi-tensor SmaQ over ResNet-34 (CIFAR) grads (110) + non-BN weights (38),
+    one bound SmaqMulti call (two launches) per step."""
     from smart_compress_amd.util.pytorch.multi import SmaqMulti
 
-    gen = torch.Generator(device=device).manual_seed(rank)
-    grads = [torch.randn(s, generator=gen, device=device) * 1e-3 for s in RESNET34_PARAMS]
-    weights = [torch.randn(s, generator=gen, device=device) * 0.05 for s in RESNET34_PARAMS
-               if len(s) != 1]
-    tensors = grads + weights
+    tensors = resnet34_c5_tensors(device, rank)
     n = sum(t.numel() for t in tensors)
     outs = [torch.empty_like(t) for t in tensors]
     m = SmaqMulti(smaq_hparams(), seed=rank)
     bound = m.bind(tensors, outs)  # fixed buffers: validated once, one call = two launches
+    trace = EventTrace()
 
     def step():
         bound()
 
     prewarm(step, device)
-    elapsed = time_steps(step, args.steps, args.warmup, world, device)
+    elapsed = time_steps(step, args.steps, args.warmup, world, device, region=trace)
     total = sum_over_ranks(12.0 * n * args.steps, world, device)
+    k_ms = trace.mean_ms("region") / args.steps
+    gbps = 12.0 * n / (k_ms * 1e-3) / 1e9
     return {"metric": "Fused multi-tensor SmaQ GB/s, ResNet-34 weights+grads per step",
             "value": round(total / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -435,7 +669,14 @@ def run_multi(args, world, rank, device):
             "host_enqueue_ms_per_step": round(HOST.get("enqueue_ms_per_step", 0.0), 4),
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": "smaq_multi_resnet34_weights_grads", "tensors": len(tensors),
-                       "elements_per_gpu": n}}
+                       "elements_per_gpu": n, "alg_bytes_per_elem": 12,
+                       "parallelism": f"replicas{world}"},
+            # one call = the statistics + apply launches: timed together by events at the two ends
+            # of the timed region (the per-kernel split is in profiles/*_multi_summary.json)
+            "roofline": {"bound": "hbm", "kernel": "smaq_multi_stats_kernel+smaq_multi_apply_kernel",
+                         "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(gbps / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": int(12 * n),
+                         "avg_launch_ms": round(k_ms, 5), "traffic": traffic_from_profile("multi", True)}}
 
 
 def run_packed(args, world, rank, device):
@@ -610,6 +851,30 @@ def run_autograd(args, world, rank, device):
             "variants": results}
 
 
+def run_mock(args, world, rank, device):
+    """Device-free step (CPU tests of the N-rank launcher, tests/test_dist_gloo.py): a fixed amount
+    of numpy work per step on each rank's own seeded data; reports what each rank saw."""
+    if os.environ.get("SMQ_BENCH_MOCK_FAIL_RANK") == str(rank):
+        raise RuntimeError(f"rank {rank}: injected failure (SMQ_BENCH_MOCK_FAIL_RANK)")
+    rng = np.random.default_rng(1000 + rank)
+    a = rng.standard_normal(1 << 16).astype(np.float32)
+
+    def step():
+        np.sort(a)
+
+    elapsed = time_steps(step, args.steps, args.warmup, world, device)
+    seeds = gather_over_ranks(1000 + rank, world)
+    pids = gather_over_ranks(os.getpid(), world)
+    ranks = gather_over_ranks(rank, world)
+    return {"metric": "mock", "value": round(world * args.steps / elapsed, 2), "unit": "steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "mock"}, "ranks": [int(r) for r in ranks],
+            "seeds": [int(v) for v in seeds], "pids": [int(v) for v in pids],
+            "rank_ms_per_step": HOST.get("rank_ms_per_step")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -617,21 +882,28 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="smaq",
                     choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi", "packed",
-                             "autograd"])
+                             "autograd", "mock"])
     ap.add_argument("--elements", type=int, default=0, help="override elements (smaq configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: this process starts the ranks and relays rank 0's line
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = dist_setup()
-    device = torch.device("cuda", local)
+    device = torch.device("cuda", local) if args.config != "mock" else torch.device("cpu")
     runner = {"smaq": run_smaq, "smaq_sampled": run_smaq, "fp8": run_fp8, "s2fp8": run_s2fp8,
-              "multi": run_multi, "packed": run_packed, "autograd": run_autograd}[args.config]
+              "multi": run_multi, "packed": run_packed, "autograd": run_autograd,
+              "mock": run_mock}[args.config]
     res = runner(args, world, rank, device)
+    if world > 1:
+        res.setdefault("rank_ms_per_step", HOST.get("rank_ms_per_step"))
+        res["launcher"] = "self" if os.environ.get("TORCHELASTIC_RUN_ID") is None else "torchrun"
     if rank == 0:
-        if world == 1 and not args.no_cpu_baseline and args.config.startswith("smaq"):
-            res["cpu_baseline"] = cpu_baseline_smaq(args.cpu_sample, args.cpu_budget)
+        if world == 1 and not args.no_cpu_baseline and args.config in CPU_BASELINES:
+            res["cpu_baseline"] = CPU_BASELINES[args.config](args)
         print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -32,9 +32,11 @@
  * Errors: every function returns SMQ_OK (0) or a negative SMQ_ERR_* code; the message of the
  * last failure on the calling thread is returned by smq_last_error(). Nothing aborts.
  *
- * Workspaces are caller-allocated device memory. A workspace must be zero-filled ONCE when it is
- * allocated (the library leaves its arrival counters at zero after every call) and must not be
- * used by two streams at the same time.
+ * Workspaces are caller-allocated device memory and must not be used by two streams at the same
+ * time. They need no initialisation: every cross-workgroup arrival counter is a 64-bit word tagged
+ * with a per-call value (high half) and a count (low half). A call whose tag does not match the
+ * word it finds (an unzeroed buffer, a call that never finished) re-installs its own tag with one
+ * compare-and-swap instead of miscounting, so one bad call cannot poison later statistics.
  */
 #ifndef SMQ_H_
 #define SMQ_H_
@@ -46,26 +48,35 @@
 extern "C" {
 #endif
 
-#define SMQ_ABI_VERSION 2
+#define SMQ_ABI_VERSION 3
 
 #define SMQ_OK 0
 #define SMQ_ERR_INVALID -1  /* bad argument */
 #define SMQ_ERR_WORKSPACE -2 /* workspace missing or too small */
 #define SMQ_ERR_LAUNCH -3   /* HIP reported an error on launch */
 
-#define SMQ_MAX_SAMPLES 64
+#define SMQ_MAX_SAMPLES 64            /* host-given indices (SMQ_STATS_SAMPLED) */
+#define SMQ_MAX_DEVICE_SAMPLES 4096   /* device-drawn indices (SMQ_STATS_SAMPLED_DEVICE) */
 
-/* Single-tensor SmaQ workspace layout (bytes): [0, 64) SmqSmaqStats header, [64, 128) arrival
- * counter, [128, 640) SMQ_WS_OUTLIER_SLOTS uint64 outlier-count slots (params.count_outliers:
- * the count is their sum; spread so 10^5 workgroups do not serialise on one address), then the
- * statistics partials. */
+/* Single-tensor SmaQ workspace layout (bytes): [0, 64) SmqSmaqStats header, [64, 128) tagged
+ * arrival counter, [128, 640) SMQ_WS_OUTLIER_SLOTS uint64 outlier-count slots
+ * (params.count_outliers: the count is their sum; spread so 10^5 workgroups do not serialise on
+ * one address), [640, SMQ_WS_SAMPLES_OFFSET) the statistics partials, then the
+ * SMQ_MAX_DEVICE_SAMPLES int64 indices the last SMQ_STATS_SAMPLED_DEVICE call drew (in draw
+ * order; read them after the stream has reached the call). */
 #define SMQ_WS_OUTLIER_SLOTS_OFFSET 128
 #define SMQ_WS_OUTLIER_SLOTS 64
+#define SMQ_WS_SAMPLES_OFFSET 66176
 
 /* Where smq_smaq_apply_f32 takes (mean, std) from. */
 #define SMQ_STATS_WORKSPACE 0 /* written by smq_smaq_stats_f32 into the workspace header */
 #define SMQ_STATS_SAMPLED 1   /* computed in-kernel from params.sample_idx (smart.py:86-91) */
 #define SMQ_STATS_INJECTED 2  /* read from the stats_in device pointer (parity tests) */
+/* k = min(n, num_samples) <= SMQ_MAX_DEVICE_SAMPLES distinct indices drawn ON THE DEVICE by
+ * Floyd's algorithm from (seed, offset + graph-safe stream position), a fresh set per call and per
+ * hipGraph replay, replacing torch.randperm(n)[:k] (smart.py:88); mean / biased std of the gathered
+ * elements as smart.py:86-91. smq_smaq_draw_samples is the host mirror of the draw. */
+#define SMQ_STATS_SAMPLED_DEVICE 3
 
 /* Input element types of the SmaQ entry points with a dtype argument. fp16 / bf16 inputs follow
  * the reference's dtype flow: statistics and z-score in the input type, the rest of the chain
@@ -97,7 +108,8 @@ typedef struct SmqSmaqParams {
   int32_t use_range_std_dev;    /* --use_range_std_dev */
   int32_t stats_source;         /* SMQ_STATS_* */
   int32_t count_outliers;       /* accumulate the outlier count into the workspace header */
-  int32_t num_samples;          /* k = min(n, --num_samples) entries of sample_idx are used */
+  int32_t num_samples;          /* k = min(n, --num_samples): entries of sample_idx used
+                                   (SMQ_STATS_SAMPLED) or indices drawn (SMQ_STATS_SAMPLED_DEVICE) */
   uint64_t seed;                /* counter-based RNG key (stochastic rounding) */
   uint64_t offset;              /* RNG counter of element 0; element i uses offset + i */
   /* --use_batch_norm (smart.py:136-149, 174-179): per-channel (x - beta[c]) / gamma[c] before the
@@ -173,8 +185,9 @@ void smq_smaq_params_init(SmqSmaqParams* p);
 int smq_smaq_params_set(SmqSmaqParams* p, int num_bits_main, int num_bits_outlier,
                         double main_std_dev_threshold, double outlier_std_dev_threshold,
                         int precision);
-/* Draw k = min(n, num_samples) distinct indices in [0, n) into p->sample_idx (host only; a
- * deterministic function of (seed, offset)). Replaces torch.randperm(n)[:k] at smart.py:88. */
+/* Draw k = min(n, num_samples) <= SMQ_MAX_SAMPLES distinct indices in [0, n) into p->sample_idx
+ * (host; a deterministic function of (seed, offset)): the same Floyd draw the device performs for
+ * SMQ_STATS_SAMPLED_DEVICE at stream position offset. Replaces torch.randperm(n)[:k], smart.py:88. */
 int smq_smaq_draw_samples(SmqSmaqParams* p, int64_t n, int num_samples);
 
 /* ---- SmaQ single tensor ---- */
@@ -252,6 +265,21 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
                         int check_inf, const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
                         uint64_t* offset_counter, const SmqS2fp8Stats* stats_in, void* ws,
                         size_t ws_bytes, void* stream);
+
+/* Flags of smq_s2fp8_roundtrip_ex. OUT_Y / OUT_T (test aids, precision 32 only) write the
+ * quantiser's input Y = |x|^alpha * 2^beta or its E5M2 quantisation T (after check_inf) instead of
+ * the round-trip output: the S2FP8 parity contract is the E5M2 code of Y (s2fp8.py:45-47).
+ * EXACT_POW computes both powers with the accurate (<= 1 ulp) library powf, as the reference's
+ * torch.pow does, instead of the hardware exp2(p * log2 x) form (a few ulp; slower ALU, same
+ * memory traffic). */
+#define SMQ_S2FP8_OUT_Y 1u
+#define SMQ_S2FP8_OUT_T 2u
+#define SMQ_S2FP8_EXACT_POW 4u
+int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int precision,
+                           int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                           uint64_t offset, uint64_t* offset_counter,
+                           const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
+                           uint32_t flags, void* stream);
 
 /* ---- host reference helpers shared with the oracle (pure functions, no GPU) ---- */
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);

@@ -41,3 +41,32 @@ def u32_to_unit(h: np.ndarray) -> np.ndarray:
 
 def uniforms(seed: int, offset: int, n: int, start: int = 0) -> np.ndarray:
     return u32_to_unit(rng_u32(seed, offset, n, start))
+
+
+DRAW_SALT = 0xD1B54A32D192ED03
+
+
+def floyd_indices(seed: int, position: int, n: int, k: int) -> np.ndarray:
+    """The k = min(n, num_samples) distinct sample indices libsmq draws for SMQ_STATS_SAMPLED_DEVICE
+    at stream position ``position`` (smaq.hip smaq_draw_stats_kernel / smq_smaq_draw_samples), in
+    draw order — the stand-in for the reference's ``torch.randperm(n)[:k]`` (smart.py:88).
+    Floyd's algorithm: step i (j = n - k + i) takes t = h_i mod (j + 1), or j if t was taken, with
+    h_i = (u32(2P + 2i) << 32) | u32(2P + 2i + 1) under the key rng_key(seed ^ DRAW_SALT)."""
+    k = min(int(n), int(k))
+    salted = (int(seed) ^ DRAW_SALT) & ((1 << 64) - 1)
+    key = rng_key(salted)
+    ctr = (2 * int(position) + np.arange(2 * k, dtype=np.uint64)) & np.uint64((1 << 64) - 1)
+    lo = (ctr & np.uint64(_M32)).astype(np.uint32)
+    hi = (ctr >> np.uint64(32)).astype(np.uint32)
+    rot = (hi << np.uint32(16)) | (hi >> np.uint32(16))
+    w = mix32(lo ^ rot ^ np.uint32(key)).astype(np.uint64)
+    h = (w[0::2] << np.uint64(32)) | w[1::2]
+    out, taken = [], set()
+    for i in range(k):
+        j = n - k + i
+        t = int(h[i] % np.uint64(j + 1))
+        if t in taken:
+            t = j
+        taken.add(t)
+        out.append(t)
+    return np.array(out, dtype=np.int64)

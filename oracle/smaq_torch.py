@@ -20,10 +20,15 @@ import torch
 def roundtrip(x: torch.Tensor, num_bits_main: int = 6, num_bits_outlier: int = 8,
               thr: float = 1.0, thr_outlier: float = 2.5, all_positive: bool = False,
               uniforms: Optional[torch.Tensor] = None,
-              stats: Optional[Tuple[float, float]] = None) -> torch.Tensor:
+              stats: Optional[Tuple[float, float]] = None, num_samples: int = 0) -> torch.Tensor:
+    """num_samples > 0: --use_sample_stats (smart.py:86-91: randperm(n)[:k], mean, biased std)."""
     r_out = ((2 ** (num_bits_outlier - 2)) - 1) / (thr_outlier - thr)  # Python doubles
     r_main = ((2 ** (num_bits_main - 2)) - 1) / thr
-    if stats is None:
+    if stats is None and num_samples > 0:
+        k = min(x.numel(), num_samples)
+        sample = x.view(-1)[torch.randperm(x.numel())[:k]]
+        m, s = sample.mean(), sample.std(unbiased=False)
+    elif stats is None:
         m, s = x.mean(), x.std()  # unbiased
     else:
         m, s = (torch.tensor(v, dtype=torch.float32) for v in stats)

@@ -405,6 +405,8 @@ struct S2Args {
   uint64_t offset;
   int check_inf;
   float max_value;
+  int out_mode;   // 0: y, 1: Y, 2: T (SMQ_S2FP8_OUT_*)
+  int exact_pow;  // SMQ_S2FP8_EXACT_POW: library powf for both powers
 };
 
 // x^p for x >= 0 (or NaN) as exp2(p * log2(x)) on the hardware v_log_f32 / v_exp_f32 (ocml's
@@ -415,17 +417,20 @@ __device__ __forceinline__ float pow_pos(float x, float p) { return exp2f(p * lo
 
 // s2fp8.py:45-48 for one element. FAST = alpha is finite and > 0 (else the exact powf path keeps
 // the reference's degenerate-case semantics, e.g. all-zero input -> NaN).
+// out_mode (SMQ_S2FP8_OUT_Y / _T test aids, uniform per launch): return Y or T instead of y.
 template <bool FAST>
 __device__ __forceinline__ float s2fp8_elem(float xv, uint32_t r, float alpha, float bp2,
                                             float ibp2, float ialpha, int check_inf,
-                                            float max_value) {
+                                            float max_value, int out_mode) {
   // torch.sign: +1 / -1, and +0.0 for +-0 and NaN (measured on torch 2.10 CPU)
   const float sgn = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
   const float a = fabsf(xv);
   float Y = FAST ? pow_pos(a, alpha) : powf(a, alpha);  // X_abs.pow_(alpha)
   Y = Y * bp2;                                            // .mul_(beta_pow2)
+  if (out_mode == 1) return Y;
   float T = qtorch_quant(Y, r, 5, 2, true);
   if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
+  if (out_mode == 2) return T;
   const float t1 = T * ibp2;                              // truncated * beta_pow2.reciprocal_()
   const float t2 = FAST ? pow_pos(t1, ialpha) : powf(t1, ialpha);  // ** alpha.reciprocal_()
   return t2 * sgn;                                        // * signs
@@ -493,13 +498,16 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   auto rb = [&](int64_t e) -> uint32_t {
     return RARR ? A.rand_bits[e] : rng_u32(A.key, off + (uint64_t)e);
   };
-  const bool fast = alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f && ialpha < INFINITY;
+  const bool fast = !A.exact_pow && alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f &&
+                    ialpha < INFINITY;
   auto q1 = [&](float v, uint32_t r) {
     if (P16)
       return fast ? s2fp8_elem16<TIN, true>(v, r, alpha, bp2, ibp2, ialpha_e, A.check_inf, A.max_value)
                   : s2fp8_elem16<TIN, false>(v, r, alpha, bp2, ibp2, ialpha_e, A.check_inf, A.max_value);
-    return fast ? s2fp8_elem<true>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value)
-                : s2fp8_elem<false>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value);
+    return fast ? s2fp8_elem<true>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value,
+                                   A.out_mode)
+                : s2fp8_elem<false>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value,
+                                    A.out_mode);
   };
   if (VEC) {
 #pragma unroll
@@ -677,10 +685,11 @@ size_t smq_s2fp8_workspace_bytes(int64_t n) {
   return s2_ws_bytes();
 }
 
-int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precision,
-                        int check_inf, const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
-                        uint64_t* offset_counter, const SmqS2fp8Stats* stats_in, void* ws,
-                        size_t ws_bytes, void* stream) {
+int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int precision,
+                           int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                           uint64_t offset, uint64_t* offset_counter,
+                           const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
+                           uint32_t flags, void* stream) {
   if (n < 1 || !x || !y) {
     set_error("s2fp8: n >= 1 and non-NULL x, y required");
     return SMQ_ERR_INVALID;
@@ -696,6 +705,19 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
   if (precision == 32 && dtype != SMQ_DTYPE_F32) {
     // quantization.py:193 hands the tensor to qtorch's float_quantize as is; its kernels take fp32
     set_error("s2fp8: precision 32 quantises the tensor as is and needs fp32 input");
+    return SMQ_ERR_INVALID;
+  }
+  if (flags & ~(SMQ_S2FP8_OUT_Y | SMQ_S2FP8_OUT_T | SMQ_S2FP8_EXACT_POW)) {
+    set_error("s2fp8: unknown flags 0x%x", flags);
+    return SMQ_ERR_INVALID;
+  }
+  const int out_mode = (flags & SMQ_S2FP8_OUT_Y) ? 1 : ((flags & SMQ_S2FP8_OUT_T) ? 2 : 0);
+  if ((flags & SMQ_S2FP8_OUT_Y) && (flags & SMQ_S2FP8_OUT_T)) {
+    set_error("s2fp8: SMQ_S2FP8_OUT_Y and SMQ_S2FP8_OUT_T are exclusive");
+    return SMQ_ERR_INVALID;
+  }
+  if (out_mode && precision != 32) {
+    set_error("s2fp8: SMQ_S2FP8_OUT_* need precision 32");
     return SMQ_ERR_INVALID;
   }
   if (!ws || ws_bytes < s2_ws_bytes()) {
@@ -741,6 +763,8 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
   A.offset = offset;
   A.check_inf = check_inf;
   A.max_value = host_max_value(5, 2);
+  A.out_mode = out_mode;
+  A.exact_pow = (flags & SMQ_S2FP8_EXACT_POW) ? 1 : 0;
   const bool rarr = rand_bits != nullptr;
   const bool half_out = precision == 16 && dtype == SMQ_DTYPE_F16;
   const bool vec = xal && ((uintptr_t)y & (half_out ? 7u : 15u)) == 0;
@@ -757,6 +781,14 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
     else s2_launch<kFqDefaultTileV, kBF16, true>(A, rarr, vec, part, grid, st);
   }
   return check_launch("s2fp8_apply_kernel");
+}
+
+int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precision,
+                        int check_inf, const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
+                        uint64_t* offset_counter, const SmqS2fp8Stats* stats_in, void* ws,
+                        size_t ws_bytes, void* stream) {
+  return smq_s2fp8_roundtrip_ex(x, dtype, y, n, precision, check_inf, rand_bits, seed, offset,
+                                offset_counter, stats_in, ws, ws_bytes, 0u, stream);
 }
 
 int smq_s2fp8_roundtrip_f32(const float* x, float* y, int64_t n, int check_inf,

@@ -16,6 +16,8 @@
 // them in the same fixed order, so the whole call is ONE launch of 8 B/elem.
 #include <math.h>
 #include <stdarg.h>
+
+#include <atomic>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -46,6 +48,20 @@ int check_launch(const char* what) {
   return SMQ_OK;
 }
 
+ArriveTag arrive_tag(const void* ws, hipStream_t st) {
+  // one running tag per slot; workspaces hashing to the same slot only mispredict (one CAS)
+  static std::atomic<uint32_t> slots[256];
+  const uint64_t h = ((uint64_t)(uintptr_t)ws >> 6) * 0x9e3779b97f4a7c15ull;
+  const uint32_t v = slots[h >> 56].fetch_add(1u, std::memory_order_relaxed);
+  ArriveTag t;
+  t.tag = (v % 0x7fffffffu) + 1u;  // [1, 2^31 - 1]: never the 0 of a zeroed workspace
+  t.next = (t.tag % 0x7fffffffu) + 1u;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive)
+    t.next = t.tag;  // replays of the captured call reuse this tag
+  return t;
+}
+
 static int grid_for(int64_t work_items, int per_block_items, int cap) {
   int64_t g = (work_items + per_block_items - 1) / per_block_items;
   if (g < 1) g = 1;
@@ -71,8 +87,8 @@ template <bool RANGE, int TIN, bool TILE = false, bool NT = false>
 __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restrict__ x, int64_t n,
                                                             int vec, FinalizeArgs fin,
                                                             StatPartial* __restrict__ partials,
-                                                            uint32_t* counter,
-                                                            SmqSmaqStats* out) {
+                                                            unsigned long long* counter,
+                                                            ArriveTag tag, SmqSmaqStats* out) {
   __shared__ uint32_t arrive_slot;
   // Shift = median of three fixed elements: keeps sum(x-K)^2 - (sum(x-K))^2/n well conditioned
   // unless the mean is > 2^14 standard deviations away from all three.
@@ -134,13 +150,18 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
   }
 
   block_reduce_stats<RANGE>(acc);
+  if (gridDim.x == 1) {  // a single workgroup finalises without a hand-off
+    if (threadIdx.x == 0)
+      finalize_stats<RANGE, TIN>(acc.s1, acc.s2, acc.mn, acc.mx, n, shift, false, fin, out);
+    return;
+  }
   if (threadIdx.x == 0) {
     StatPartial* p = partials + blockIdx.x;
     st_sc1_f64(&p->s1, acc.s1);
     st_sc1_f64(&p->s2, acc.s2);
     if (RANGE) st_sc1_f32x2(&p->mn, acc.mn, acc.mx);
   }
-  const uint32_t prev = block_arrive(counter, &arrive_slot);
+  const uint32_t prev = block_arrive_tagged(counter, tag.tag, &arrive_slot);
   if (prev != gridDim.x - 1) return;
 
   // Last workgroup: ordered reduction of all partials (deterministic for a given n). Every load
@@ -174,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
   block_reduce_stats<RANGE>(tot);
   if (threadIdx.x == 0) {
     finalize_stats<RANGE, TIN>(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, fin, out);
-    *counter = 0u;  // leave the workspace ready for the next call
+    arrive_reset(counter, tag.next);  // the next call's tag, count 0
   }
 }
 
@@ -232,6 +253,148 @@ __global__ __launch_bounds__(kWave) void smaq_sample_stats_kernel(ApplyArgs A) {
       finalize_stats<true, TIN>(0.0, m2, mn, mx, A.k, mean, true, f, &st);
     else
       finalize_stats<false, TIN>(0.0, m2, mn, mx, A.k, mean, true, f, &st);
+    *A.ws_stats = st;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Device-drawn sampled statistics (SMQ_STATS_SAMPLED_DEVICE): smart.py:86-91 with the randperm
+// of line 88 replaced by Floyd's algorithm on the device, so every call — and every replay of a
+// captured graph — draws a fresh index set from the call's stream position.
+//
+// Floyd: for i = 0 .. k-1, j = n - k + i: t = h_i mod (j + 1); pick t unless an earlier pick
+// equals it, then pick j (never picked before: every earlier pick is < j). h_i is the 64-bit word
+// (rng_u32(key', 2P + 2i) << 32) | rng_u32(key', 2P + 2i + 1), key' = rng_key(seed ^ kDrawSalt),
+// P = offset + stream position: a function of the call alone (smq_smaq_draw_samples and
+// oracle/rng.py floyd_indices restate it). The candidates t are independent and computed in
+// parallel; only the duplicate test is sequential: a register/ballot scan by one wave for k <= 64,
+// an LDS open-addressing set walked by one lane for larger k.
+// ------------------------------------------------------------------------------------------------
+constexpr uint64_t kDrawSalt = 0xd1b54a32d192ed03ull;
+
+struct DrawArgs {
+  const void* x;
+  int64_t n;
+  int k;
+  int use_range;
+  uint32_t key;                   // rng_key(seed ^ kDrawSalt)
+  uint64_t offset;                // params.offset
+  unsigned long long* rng_ctr;    // params.offset_counter or NULL
+  float clamp_lo, clamp_hi, range_coef;
+  SmqSmaqStats* ws_stats;
+  int64_t* idx_out;               // workspace, SMQ_MAX_DEVICE_SAMPLES entries
+};
+
+__host__ __device__ __forceinline__ int64_t floyd_candidate(uint32_t key, uint64_t pos, int64_t n,
+                                                            int k, int i) {
+  const uint64_t c = 2ull * pos + 2ull * (uint64_t)i;
+  const uint64_t h = ((uint64_t)rng_u32(key, c) << 32) | rng_u32(key, c + 1);
+  return (int64_t)(h % (uint64_t)(n - k + i + 1));
+}
+
+__device__ __forceinline__ uint32_t pick_hash(int64_t t, int bits) {
+  const uint32_t v = (uint32_t)t ^ (uint32_t)((uint64_t)t >> 32);
+  return (v * 0x9e3779b1u) >> (32 - bits);
+}
+
+template <int TIN>
+__global__ __launch_bounds__(kBlock) void smaq_draw_stats_kernel(DrawArgs A) {
+  __shared__ int64_t pick[SMQ_MAX_DEVICE_SAMPLES];          // 32 KiB
+  __shared__ uint16_t table[2 * SMQ_MAX_DEVICE_SAMPLES];    // 16 KiB: pick index + 1, 0 = empty
+  __shared__ unsigned long long pos_s;
+  __shared__ double shs[kBlock / kWave];
+  const int k = A.k;
+  const int64_t n = A.n;
+  if (threadIdx.x == 0) pos_s = A.offset + (A.rng_ctr ? *A.rng_ctr : 0ull);
+  __syncthreads();
+  const uint64_t pos = pos_s;
+  for (int i = threadIdx.x; i < k; i += kBlock) pick[i] = floyd_candidate(A.key, pos, n, k, i);
+  int bits = 1;
+  while ((1 << bits) < 2 * k) ++bits;
+  if (k > kWave)
+    for (int i = threadIdx.x; i < (1 << bits); i += kBlock) table[i] = 0;
+  __syncthreads();
+  if (k <= kWave) {
+    if (threadIdx.x < kWave) {  // lane i holds pick i; lanes < i are final at step i
+      const int lane = threadIdx.x;
+      int64_t p = lane < k ? pick[lane] : -1;
+      for (int i = 1; i < k; ++i) {
+        const int32_t lo = __builtin_amdgcn_readlane((int32_t)p, i);
+        const int32_t hi = __builtin_amdgcn_readlane((int32_t)((uint64_t)p >> 32), i);
+        const int64_t t = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+        const bool dup = __ballot(lane < i && p == t) != 0ull;
+        if (dup && lane == i) p = n - k + i;
+      }
+      if (lane < k) pick[lane] = p;
+    }
+  } else if (threadIdx.x == 0) {
+    const uint32_t mask = (1u << bits) - 1u;
+    for (int i = 0; i < k; ++i) {
+      int64_t t = pick[i];
+      uint32_t s = pick_hash(t, bits);
+      bool dup = false;
+      for (uint16_t e; (e = table[s]) != 0; s = (s + 1) & mask)
+        if (pick[e - 1] == t) {
+          dup = true;
+          break;
+        }
+      if (dup) {  // j = n - k + i is new: probe for its own empty slot
+        t = n - k + i;
+        s = pick_hash(t, bits);
+        while (table[s] != 0) s = (s + 1) & mask;
+      }
+      pick[i] = t;
+      table[s] = (uint16_t)(i + 1);
+    }
+  }
+  __syncthreads();
+  // gather: thread t owns samples t, t + kBlock, ... (<= 16); fp64 sums in one fixed order
+  constexpr int kPer = SMQ_MAX_DEVICE_SAMPLES / kBlock;
+  float v[kPer];
+  double s = 0.0;
+  float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = threadIdx.x + u * kBlock;
+    v[u] = 0.0f;
+    if (i < k) {
+      const int64_t e = pick[i];
+      A.idx_out[i] = e;
+      v[u] = load1<TIN>(A.x, e);
+      s += (double)v[u];
+      mn = fminf(mn, v[u]);
+      mx = fmaxf(mx, v[u]);
+    }
+  }
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  s = wave_sum(s);
+  if (lane == 0) shs[wave] = s;
+  __syncthreads();
+  const double mean = ((shs[0] + shs[1]) + (shs[2] + shs[3])) / (double)k;
+  __syncthreads();
+  double m2 = 0.0;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = threadIdx.x + u * kBlock;
+    if (i < k) {
+      const double d = (double)v[u] - mean;
+      m2 = fma(d, d, m2);
+    }
+  }
+  StatAcc acc;
+  acc.s1 = 0.0;
+  acc.s2 = m2;
+  acc.mn = mn;
+  acc.mx = mx;
+  block_reduce_stats<true>(acc);
+  if (threadIdx.x == 0) {
+    SmqSmaqStats st;
+    FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, A.rng_ctr, n};
+    // shifted sums with shift = mean: s1 = 0, s2 = the biased second moment's numerator
+    if (A.use_range)
+      finalize_stats<true, TIN>(0.0, acc.s2, acc.mn, acc.mx, k, mean, true, f, &st);
+    else
+      finalize_stats<false, TIN>(0.0, acc.s2, acc.mn, acc.mx, k, mean, true, f, &st);
     *A.ws_stats = st;
   }
 }
@@ -369,7 +532,7 @@ static int validate_params(const SmqSmaqParams* p) {
     set_error("params is NULL");
     return SMQ_ERR_INVALID;
   }
-  if (p->stats_source < 0 || p->stats_source > 2) {
+  if (p->stats_source < 0 || p->stats_source > 3) {
     set_error("stats_source %d invalid", p->stats_source);
     return SMQ_ERR_INVALID;
   }
@@ -387,7 +550,9 @@ static float range_coef_for(const SmqSmaqParams* p, int64_t n) {
 
 static size_t stats_ws_bytes(int64_t n) {
   (void)n;
-  return SmaqWsLayout::kPartials + sizeof(StatPartial) * (size_t)kStatsGridCap;
+  static_assert(SmaqWsLayout::kPartials + sizeof(StatPartial) * (size_t)kStatsGridCap ==
+                    SMQ_WS_SAMPLES_OFFSET, "smq.h SMQ_WS_SAMPLES_OFFSET");
+  return SMQ_WS_SAMPLES_OFFSET + 8 * (size_t)SMQ_MAX_DEVICE_SAMPLES;
 }
 
 static int check_dtype(int dtype) {
@@ -406,7 +571,8 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   }
   char* base = (char*)ws;
   SmqSmaqStats* hdr = (SmqSmaqStats*)base;
-  uint32_t* counter = (uint32_t*)(base + SmaqWsLayout::kHeader);
+  unsigned long long* counter = (unsigned long long*)(base + SmaqWsLayout::kHeader);
+  const ArriveTag tag = arrive_tag(ws, st);
   StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
   const int vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) ? 1 : 0;
   // fp32 sweeps tile-stride (smaq_stats_kernel<.., TILE>) on at most kStatsTileGrid workgroups;
@@ -449,13 +615,13 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   do {                                                                                              \
     if (tile && nt)                                                                                 \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true, true>), dim3(grid), dim3(kBlock), 0,  \
-                         st, x, n, vec, fin, partials, counter, hdr);                               \
+                         st, x, n, vec, fin, partials, counter, tag, hdr);                               \
     else if (tile)                                                                                  \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true>), dim3(grid), dim3(kBlock), 0, st, x, \
-                         n, vec, fin, partials, counter, hdr);                                      \
+                         n, vec, fin, partials, counter, tag, hdr);                                      \
     else                                                                                            \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n,    \
-                         vec, fin, partials, counter, hdr);                                         \
+                         vec, fin, partials, counter, tag, hdr);                                         \
   } while (0)
   if (dtype == SMQ_DTYPE_F32) {
     if (p->use_range_std_dev) SMQ_STATS(true, kF32); else SMQ_STATS(false, kF32);
@@ -528,6 +694,42 @@ static void launch_sample_stats(const ApplyArgs& A, int dtype, hipStream_t st) {
     hipLaunchKernelGGL(smaq_sample_stats_kernel<kF16>, dim3(1), dim3(kWave), 0, st, A);
   else
     hipLaunchKernelGGL(smaq_sample_stats_kernel<kBF16>, dim3(1), dim3(kWave), 0, st, A);
+}
+
+static int launch_draw_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p,
+                             void* ws, size_t ws_bytes, hipStream_t st) {
+  const size_t need = SMQ_WS_SAMPLES_OFFSET + 8 * (size_t)SMQ_MAX_DEVICE_SAMPLES;
+  if (!ws || ws_bytes < need) {
+    set_error("workspace too small for device-drawn samples: need %zu bytes, got %zu", need,
+              ws_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  const int64_t k = p->num_samples < n ? p->num_samples : n;
+  if (k < 1 || k > SMQ_MAX_DEVICE_SAMPLES) {
+    set_error("device-drawn sampled stats need 1 <= k <= %d, got %lld", SMQ_MAX_DEVICE_SAMPLES,
+              (long long)k);
+    return SMQ_ERR_INVALID;
+  }
+  DrawArgs D;
+  D.x = x;
+  D.n = n;
+  D.k = (int)k;
+  D.use_range = p->use_range_std_dev;
+  D.key = rng_key(p->seed ^ kDrawSalt);
+  D.offset = p->offset;
+  D.rng_ctr = (unsigned long long*)p->offset_counter;
+  D.clamp_lo = p->clamp_lo;
+  D.clamp_hi = p->clamp_hi;
+  D.range_coef = range_coef_for(p, k);
+  D.ws_stats = (SmqSmaqStats*)ws;
+  D.idx_out = (int64_t*)((char*)ws + SMQ_WS_SAMPLES_OFFSET);
+  if (dtype == SMQ_DTYPE_F32)
+    hipLaunchKernelGGL(smaq_draw_stats_kernel<kF32>, dim3(1), dim3(kBlock), 0, st, D);
+  else if (dtype == SMQ_DTYPE_F16)
+    hipLaunchKernelGGL(smaq_draw_stats_kernel<kF16>, dim3(1), dim3(kBlock), 0, st, D);
+  else
+    hipLaunchKernelGGL(smaq_draw_stats_kernel<kBF16>, dim3(1), dim3(kBlock), 0, st, D);
+  return check_launch("smaq_draw_stats_kernel");
 }
 
 static int launch_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
@@ -618,6 +820,11 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
     launch_sample_stats(A, dtype, st);
     A.stats = A.ws_stats;
   }
+  if (p->stats_source == SMQ_STATS_SAMPLED_DEVICE) {
+    const int rc = launch_draw_stats(x, dtype, n, p, ws, ws_bytes, st);
+    if (rc) return rc;
+    A.stats = A.ws_stats;
+  }
   const bool bn = A.bn_gamma != nullptr;
   if (dtype == SMQ_DTYPE_F32) launch_apply_t<kF32>(A, rm, vec, bn, tv, grid, st);
   else if (dtype == SMQ_DTYPE_F16) launch_apply_t<kF16>(A, rm, vec, bn, tv, grid, st);
@@ -642,8 +849,10 @@ static int check_tensor_args(const void* x, const float* y, int64_t n) {
 int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
                   size_t ws_bytes, hipStream_t st) {
   if (p->stats_source == SMQ_STATS_WORKSPACE) return launch_stats(x, dtype, n, p, ws, ws_bytes, st);
+  if (p->stats_source == SMQ_STATS_SAMPLED_DEVICE)
+    return launch_draw_stats(x, dtype, n, p, ws, ws_bytes, st);
   if (p->stats_source != SMQ_STATS_SAMPLED) {
-    set_error("this entry point computes its statistics (SMQ_STATS_WORKSPACE or _SAMPLED)");
+    set_error("this entry point computes its statistics (SMQ_STATS_WORKSPACE or _SAMPLED*)");
     return SMQ_ERR_INVALID;
   }
   if (!ws || ws_bytes < SmaqWsLayout::kPartials) {
@@ -723,20 +932,16 @@ int smq_smaq_draw_samples(SmqSmaqParams* p, int64_t n, int num_samples) {
     set_error("num_samples %d exceeds SMQ_MAX_SAMPLES", num_samples);
     return SMQ_ERR_INVALID;
   }
-  // Floyd's algorithm: k distinct indices, O(k^2), keyed off a stream separate from rounding.
-  const uint32_t key = rng_key(p->seed ^ 0xd1b54a32d192ed03ull);
-  uint64_t ctr = p->offset * 2;
-  int m = 0;
-  for (int64_t j = n - k; j < n; ++j) {
-    const uint64_t h = ((uint64_t)rng_u32(key, ctr) << 32) | rng_u32(key, ctr + 1);
-    ctr += 2;
-    int64_t t = (int64_t)(h % (uint64_t)(j + 1));
-    for (int q = 0; q < m; ++q)
+  // Floyd's algorithm, the draw smaq_draw_stats_kernel performs at stream position p->offset
+  const uint32_t key = rng_key(p->seed ^ kDrawSalt);
+  for (int i = 0; i < (int)k; ++i) {
+    int64_t t = floyd_candidate(key, p->offset, n, (int)k, i);
+    for (int q = 0; q < i; ++q)
       if (p->sample_idx[q] == t) {
-        t = j;
+        t = n - k + i;
         break;
       }
-    p->sample_idx[m++] = t;
+    p->sample_idx[i] = t;
   }
   p->num_samples = (int32_t)k;
   return SMQ_OK;

@@ -61,7 +61,8 @@ struct MultiArgs {
   const ChunkDesc* chunks;       // apply chunks
   const ChunkDesc* stat_chunks;  // statistics chunks
   SmqSmaqStats* stats;       // [count]
-  uint32_t* counters;        // [count]
+  unsigned long long* counters;  // [count] tagged arrival counters (block_arrive_tagged)
+  ArriveTag tag;
   uint64_t* rng_snap;        // stream position of this call relative to offset (graph-safe mode)
   uint64_t* rng_ctr;         // params.offset_counter (NULL: host-managed offsets)
   uint64_t rng_span;         // elements this call draws: max(desc.rng_offset + n)
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
     st_sc1_f64(&p->s1, acc.s1);
     st_sc1_f64(&p->s2, acc.s2);
   }
-  const uint32_t prev = block_arrive(&A.counters[ch.tensor], &slot);
+  const uint32_t prev = block_arrive_tagged(&A.counters[ch.tensor], A.tag.tag, &slot);
   if (prev != (uint32_t)ch.n_chunks - 1) return;
   // batches of loads issued before they are consumed (one round trip per batch, not per partial)
   constexpr int K = 8;
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   block_reduce_stats<false>(tot);
   if (threadIdx.x == 0) {
     finalize_stats<false>(tot.s1, tot.s2, 0.f, 0.f, n, shift, false, fin, &A.stats[ch.tensor]);
-    A.counters[ch.tensor] = 0u;
+    arrive_reset(&A.counters[ch.tensor], A.tag.next);
   }
 }
 
@@ -387,7 +388,7 @@ size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count) {
   PlanSizes ps;
   if (!sizes || count < 1 || !plan_sizes(sizes, count, &ps)) return 0;
   const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
-  const size_t counters = ((sizeof(uint32_t) * (size_t)count) + 63) & ~(size_t)63;
+  const size_t counters = ((sizeof(uint64_t) * (size_t)count) + 63) & ~(size_t)63;
   return stats + counters + kSnapBytes + sizeof(StatPartial) * (size_t)ps.n_stat_chunks;
 }
 
@@ -413,7 +414,7 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
     return SMQ_ERR_INVALID;
   }
   const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
-  const size_t counters = ((sizeof(uint32_t) * (size_t)count) + 63) & ~(size_t)63;
+  const size_t counters = ((sizeof(uint64_t) * (size_t)count) + 63) & ~(size_t)63;
   const size_t need = stats + counters + kSnapBytes + sizeof(StatPartial) * (size_t)n_stat_chunks;
   if (ws_bytes < need) {
     set_error("multi: workspace too small: need %zu bytes, got %zu", need, ws_bytes);
@@ -428,7 +429,8 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   A.stat_chunks = A.chunks + n_chunks;
   char* wb = (char*)ws;
   A.stats = (SmqSmaqStats*)wb;
-  A.counters = (uint32_t*)(wb + stats);
+  A.counters = (unsigned long long*)(wb + stats);
+  A.tag = arrive_tag(ws, (hipStream_t)stream);
   A.rng_snap = (uint64_t*)(wb + stats + counters);
   A.partials = (StatPartial*)(wb + stats + counters + kSnapBytes);
   A.rng_ctr = p->offset_counter;

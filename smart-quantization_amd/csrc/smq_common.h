@@ -143,6 +143,46 @@ __device__ __forceinline__ uint32_t block_arrive(uint32_t* counter, uint32_t* ld
   return *lds_slot;
 }
 
+// Tagged arrival counter: one 64-bit word, call tag in the high half, arrivals in the low half.
+// The finalising workgroup leaves (next_tag, 0) behind, so the next call on the workspace (whose
+// tag the host predicted, arrive_tag() in smaq.hip) finds its own tag and takes the single atomic
+// add. A word with another tag (an unzeroed workspace, a call that never finished, another
+// workspace sharing the host's tag slot) is stale: the arrival that meets it installs
+// (tag, 1) — or joins a tag another stale arrival installed first — by compare-and-swap. The add
+// that met the stale word only changed the stale word, which the install overwrites. Returns the
+// number of earlier arrivals of this call in every thread (== expected - 1 in the last one).
+__device__ __forceinline__ uint32_t block_arrive_tagged(unsigned long long* ctr, uint32_t tag,
+                                                        uint32_t* lds_slot) {
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 partial stores have landed
+    unsigned long long old =
+        __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t before;
+    if ((uint32_t)(old >> 32) == tag) {
+      before = (uint32_t)old;
+    } else {
+      old = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (;;) {
+        const bool mine = (uint32_t)(old >> 32) == tag;
+        const unsigned long long want = mine ? old + 1ull : (((unsigned long long)tag << 32) | 1ull);
+        if (__hip_atomic_compare_exchange_strong(ctr, &old, want, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          before = (uint32_t)want - 1u;
+          break;
+        }
+      }
+    }
+    *lds_slot = before;
+  }
+  __syncthreads();
+  return *lds_slot;
+}
+
+// What the finalising workgroup leaves in a tagged counter for the next call.
+__device__ __forceinline__ void arrive_reset(unsigned long long* ctr, uint32_t next_tag) {
+  *ctr = (unsigned long long)next_tag << 32;
+}
+
 // Stats partial of one workgroup: shifted fp64 sums plus fp32 extrema.
 struct alignas(32) StatPartial {
   double s1;  // sum (x - shift)
@@ -198,4 +238,13 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 namespace smq {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+
+// Host: the tag a call uses for the tagged arrival counters of workspace `ws` and the tag it leaves
+// behind for the next call (block_arrive_tagged). Tags come from a small per-workspace-slot table;
+// a wrong prediction costs one compare-and-swap, never a miscount. While `st` is being captured
+// into a graph, next == tag, so every replay finds its own tag.
+struct ArriveTag {
+  uint32_t tag, next;
+};
+ArriveTag arrive_tag(const void* ws, hipStream_t st);
 }  // namespace smq

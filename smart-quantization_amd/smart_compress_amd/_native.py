@@ -19,13 +19,19 @@ LIB_PATH = os.environ.get(
     "SMQ_LIB", os.path.join(os.path.dirname(_PKG_DIR), "lib", "libsmq.so")
 )
 
-SMQ_ABI_VERSION = 2
+SMQ_ABI_VERSION = 3
 SMQ_MAX_SAMPLES = 64
+SMQ_MAX_DEVICE_SAMPLES = 4096
 SMQ_WS_OUTLIER_SLOTS_OFFSET = 128
 SMQ_WS_OUTLIER_SLOTS = 64
+SMQ_WS_SAMPLES_OFFSET = 66176
 SMQ_STATS_WORKSPACE = 0
 SMQ_STATS_SAMPLED = 1
 SMQ_STATS_INJECTED = 2
+SMQ_STATS_SAMPLED_DEVICE = 3
+SMQ_S2FP8_OUT_Y = 1
+SMQ_S2FP8_OUT_T = 2
+SMQ_S2FP8_EXACT_POW = 4
 SMQ_PACK_TICKETED = 1
 SMQ_PACK_SINGLE = 2
 SMQ_DTYPE_F32 = 0
@@ -190,6 +196,10 @@ SIGNATURES = {
     "smq_s2fp8_roundtrip": (
         _I32,
         [_P, _I32, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _P, _SZ, _P],
+    ),
+    "smq_s2fp8_roundtrip_ex": (
+        _I32,
+        [_P, _I32, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _P, _SZ, _U32, _P],
     ),
     "smq_float_quant": (
         _I32,

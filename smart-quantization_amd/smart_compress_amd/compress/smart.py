@@ -9,10 +9,13 @@ Below the boundary, the reference's ~24 ATen launches + one host sync (smart.py:
 two launches of libsmq (include/smq.h):
 
 * full statistics (default): ``smq_smaq_stats_f32`` + ``smq_smaq_apply_f32`` (12 B/elem);
-* ``--use_sample_stats``: one ``smq_smaq_apply_f32`` that gathers the k samples in-kernel (8 B/elem).
+* ``--use_sample_stats``: ``smq_smaq_apply`` with ``SMQ_STATS_SAMPLED_DEVICE``: a one-workgroup
+  launch draws k distinct indices (Floyd, on the device, from the call's stream position),
+  gathers them and writes mean / biased std, then the apply launch (8 B/elem).
 
 Randomness: the reference draws ``torch.rand_like`` (smart.py:94) and ``torch.randperm`` (88); here a
-counter-based RNG keyed by ``(seed, offset)`` held on the codec (``self.rng``) — the seed comes from
+counter-based RNG keyed by ``(seed, offset)`` held on the codec (``self.rng``), for the rounding
+draws and the sample indices alike — the seed comes from
 torch's default generator at construction (so ``torch.manual_seed`` makes runs repeatable) or from
 ``hparams.smq_seed``; the offset advances by the elements consumed per call.
 """
@@ -139,13 +142,15 @@ class SmartFP(CompressionAlgorithmBase):
             p.seed, p.offset = self.rng.take(numel)
         p.range_std_coef = -1.0  # set below in range mode (0.0 is a valid coefficient)
         if hp.use_sample_stats:
+            # smart.py:86-91: k indices drawn on the device (Floyd) from this call's stream
+            # position, so eager calls and graph replays alike see a fresh set (smart.py:88)
             k = min(numel, hp.num_samples)
-            if k > N.SMQ_MAX_SAMPLES:
+            if k > N.SMQ_MAX_DEVICE_SAMPLES:
                 raise NotImplementedError(
-                    f"--num_samples {hp.num_samples} > {N.SMQ_MAX_SAMPLES} is not supported"
+                    f"--num_samples {hp.num_samples} > {N.SMQ_MAX_DEVICE_SAMPLES} is not supported"
                 )
-            p.stats_source = N.SMQ_STATS_SAMPLED
-            N.check(N.lib().smq_smaq_draw_samples(p, numel, hp.num_samples), "draw_samples")
+            p.stats_source = N.SMQ_STATS_SAMPLED_DEVICE
+            p.num_samples = k
             if hp.use_range_std_dev:
                 p.range_std_coef = range_std_coef(k, dtype)
         else:

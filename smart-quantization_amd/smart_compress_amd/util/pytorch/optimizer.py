@@ -89,8 +89,9 @@ class OptimLP(Optimizer):
 
     # -- helpers -----------------------------------------------------------------------------------
     def _apply(self, fn, tensors: Sequence[torch.Tensor], all_pos: Sequence[bool],
-               assign: Callable[[int, torch.Tensor], None]):
-        """Quantise ``tensors`` with ``fn``: one fused in-place launch pair when possible, else the
+               assign: Callable[[int, torch.Tensor], None], inplace: bool = True):
+        """Quantise ``tensors`` with ``fn``: one fused launch pair when possible (in place, or into
+        new tensors handed to ``assign`` when the inputs' storage must survive), else the
         reference's per-tensor calls with their results handed to ``assign``."""
         codec = _fusable(fn)
         fused = [i for i, t in enumerate(tensors) if codec is not None and _fusable_tensor(t)]
@@ -100,8 +101,12 @@ class OptimLP(Optimizer):
                 multi = self._multi[id(fn)] = SmaqMulti(codec.hparams, rng=codec.rng)
             multi._graph_safe = codec._graph_safe  # same stream, same mode (device counter or host)
             xs = [tensors[i] for i in fused]
-            multi(xs, xs, all_positive=[all_pos[i] for i in fused])
+            ys = multi(xs, xs if inplace else None, all_positive=[all_pos[i] for i in fused])
             self._log_fused(codec, fn.tag, multi, xs)
+            if not inplace:
+                for i, y in zip(fused, ys):
+                    if y is not tensors[i]:  # below min_size the reference returns the input
+                        assign(i, y)
         done = set(fused)
         for i, t in enumerate(tensors):
             if i not in done:
@@ -159,7 +164,11 @@ class OptimLP(Optimizer):
             def assign_w(i, q):
                 ps[i].data = q.data
 
-            self._apply(self.weight_quant, [p.data for p in ps], [False] * len(ps), assign_w)
+            # with an accumulator, p.data IS weight_acc[p] (swapped in by _pre_closure): the
+            # reference's `p.data = weight_quant(p.data).data` leaves the full-precision
+            # accumulator intact, so the fused launch must not write in place then
+            self._apply(self.weight_quant, [p.data for p in ps], [False] * len(ps), assign_w,
+                        inplace=self.acc_quant is None)
         if self.momentum_quant is not None:
             slots = []
             for g in self.param_groups:

@@ -97,9 +97,9 @@ def float_quant(x, exp_bits, man_bits, rounding=N.SMQ_ROUND_STOCHASTIC, check_in
 
 
 def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None, precision=32,
-          counter=None):
-    """smq_s2fp8_roundtrip on a device tensor of any supported dtype (precision 16: fp16 in ->
-    fp16 out, fp32 / bf16 in -> fp32 out)."""
+          counter=None, flags=0):
+    """smq_s2fp8_roundtrip_ex on a device tensor of any supported dtype (precision 16: fp16 in ->
+    fp16 out, fp32 / bf16 in -> fp32 out); flags = SMQ_S2FP8_* (OUT_Y / OUT_T: y holds Y or T)."""
     n = x.numel()
     half_out = precision == 16 and x.dtype == torch.float16
     y = torch.empty(x.shape, dtype=torch.float16 if half_out else torch.float32, device=x.device)
@@ -110,12 +110,12 @@ def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None, precis
         s.mu, s.m, s.n_used = float(mu_m[0]), float(mu_m[1]), n
         raw = np.frombuffer(ctypes.string_at(ctypes.addressof(s), 64), dtype=np.uint8).copy()
         st_in = torch.from_numpy(raw).to(x.device)
-    N.check(N.lib().smq_s2fp8_roundtrip(
+    N.check(N.lib().smq_s2fp8_roundtrip_ex(
         x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), n, precision, 1 if check_inf else 0,
         rand_bits.data_ptr() if rand_bits is not None else None, seed, offset,
         counter.data_ptr() if counter is not None else None,
-        st_in.data_ptr() if st_in is not None else None, ws.data_ptr(), ws.numel(), stream()),
-        "s2fp8")
+        st_in.data_ptr() if st_in is not None else None, ws.data_ptr(), ws.numel(), flags,
+        stream()), "s2fp8")
     hdr = ws[:32].cpu().numpy().view(np.float32)
     stats = dict(mu=hdr[0], m=hdr[1], alpha=hdr[2], beta=hdr[3], beta_pow2=hdr[4],
                  inv_beta_pow2=hdr[5], inv_alpha=hdr[6])

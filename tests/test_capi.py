@@ -119,6 +119,40 @@ def test_draw_samples():
     assert b"SMQ_MAX_SAMPLES" in lib.smq_last_error()
 
 
+@pytest.mark.parametrize("n,k", [(1000, 16), (10, 16), (64, 64), (2**40, 64), (17, 17), (5, 1)])
+def test_draw_samples_equals_oracle_floyd(n, k):
+    """The host mirror of the device draw (smq_smaq_draw_samples) and oracle/rng.py floyd_indices
+    give the same indices in the same order, for positions beyond 2^32 too."""
+    from oracle import rng
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    for seed, pos in ((9, 0), (2**63 + 5, 2**33 + 7), (1, 123456789)):
+        p = N.SmqSmaqParams()
+        lib.smq_smaq_params_init(p)
+        p.seed, p.offset = seed, pos
+        assert lib.smq_smaq_draw_samples(p, n, k) == 0
+        got = list(p.sample_idx[: p.num_samples])
+        want = rng.floyd_indices(seed, pos, n, k)
+        assert got == want.tolist()
+        assert len(set(got)) == min(n, k) and all(0 <= i < n for i in got)
+
+
+def test_oracle_floyd_large_k_distinct_and_uniform():
+    """k up to SMQ_MAX_DEVICE_SAMPLES: distinct, in range, k == n is a permutation, and each
+    index is drawn with probability ~k/n."""
+    from oracle import rng
+
+    idx = rng.floyd_indices(3, 0, 4096, 4096)
+    assert sorted(idx.tolist()) == list(range(4096))
+    counts = np.zeros(1000)
+    for pos in range(400):
+        i = rng.floyd_indices(11, pos * 1000, 1000, 100)
+        assert len(set(i.tolist())) == 100
+        counts[i] += 1
+    assert abs(counts.mean() - 40.0) < 1e-9 and counts.std() < 10  # binomial sd ~6
+
+
 def test_validation_errors_without_device():
     from smart_compress_amd import _native as N
 

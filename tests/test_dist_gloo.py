@@ -1,13 +1,21 @@
-"""N>1 path of bench.py on CPU: world_size-2 gloo process group, the same helpers the GPU bench
-uses for its barrier, max-over-ranks elapsed time and sum-over-ranks bytes ("weak" scaling: each
-rank processes its own units; no data-path collective)."""
+"""N>1 path of bench.py on CPU (no GPU needed):
 
+* the launcher itself: `python bench.py --gpus N --config mock` starts N rank processes (no
+  torchrun), the ranks meet in a gloo group, and rank 0's one JSON line says n_gpus = N with one
+  time per rank, distinct ranks, pids and seeds (each rank owns its own units: "weak" scaling);
+* the same flow under torch.distributed.run (the driver's declared launcher);
+* the timing helpers (barrier, max / sum / gather over ranks) on a world_size-2 gloo group.
+No data-path collective exists: the group carries barriers and timing reductions only.
+"""
+
+import json
 import os
 import socket
+import subprocess
 import sys
 
+import pytest
 import torch
-import torch.distributed as dist
 import torch.multiprocessing as mp
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,23 +29,74 @@ def _free_port():
     return port
 
 
+def _clean_env():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+              "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def _last_json(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launch_n_ranks(n):
+    res = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n),
+                          "--config", "mock", "--steps", "4", "--warmup", "1"],
+                         env=_clean_env(), cwd=REPO, capture_output=True, timeout=240)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    line = _last_json(res.stdout.decode())
+    assert line["n_gpus"] == n and line["launcher"] == "self"
+    assert line["ranks"] == list(range(n))
+    assert len(set(line["pids"])) == n and os.getpid() not in line["pids"]
+    assert len(set(line["seeds"])) == n
+    assert len(line["rank_ms_per_step"]) == n and all(t > 0 for t in line["rank_ms_per_step"])
+    assert line["scaling"] == "weak"
+
+
+def test_bench_self_launch_failing_rank_propagates():
+    """A rank that fails makes the launcher fail: the rank waiting at the start barrier is stopped
+    instead of being left there."""
+    env = _clean_env()
+    env["SMQ_BENCH_MOCK_FAIL_RANK"] = "1"
+    res = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                          "--config", "mock", "--steps", "3"],
+                         env=env, cwd=REPO, capture_output=True, timeout=120)
+    assert res.returncode != 0
+    assert b"injected failure" in res.stderr
+
+
+def test_bench_under_torchrun():
+    res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                          str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
+                          "--config", "mock", "--steps", "3", "--warmup", "1"],
+                         env=_clean_env(), cwd=REPO, capture_output=True, timeout=240)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    line = _last_json(res.stdout.decode())
+    assert line["n_gpus"] == 2 and line["launcher"] == "torchrun" and line["ranks"] == [0, 1]
+
+
 def _worker(rank, world, port, q):
     sys.path[:0] = [REPO, os.path.join(REPO, "smart-quantization_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), SMQ_BENCH_BACKEND="gloo")
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
     import bench
 
     w, r, _ = bench.dist_setup()
-    assert (w, r) == (world, rank)
-    dev = torch.device("cpu")
+    assert (w, r) == (world, rank) and dist.get_backend() == "gloo"
     bench.barrier(w)
-    elapsed = bench.max_over_ranks(0.5 + rank, w, dev)
-    total = bench.sum_over_ranks(12.0 * (1000 + rank), w, dev)
-    # each rank draws its own units (seed = rank), so the data differs across ranks
-    x = torch.randn(4, generator=torch.Generator().manual_seed(rank))
-    gathered = [torch.zeros(4) for _ in range(world)]
-    dist.all_gather(gathered, x)
-    q.put((rank, elapsed, total, [g.tolist() for g in gathered]))
+    elapsed = bench.max_over_ranks(0.5 + rank, w)
+    total = bench.sum_over_ranks(12.0 * (1000 + rank), w)
+    each = bench.gather_over_ranks(10.0 * rank, w)
+    q.put((rank, elapsed, total, each))
     dist.destroy_process_group()
 
 
@@ -53,7 +112,7 @@ def test_bench_rank_aggregation_gloo():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, elapsed, total, gathered in res:
+    for rank, elapsed, total, each in res:
         assert elapsed == 1.5  # max over ranks
         assert total == 12.0 * (1000 + 1001)  # sum of both ranks' bytes
-        assert gathered[0] != gathered[1]  # independent units per rank
+        assert each == [0.0, 10.0]  # per-rank values in rank order

@@ -78,3 +78,39 @@ def test_bound_multi_equals_per_call():
         torch.cuda.synchronize()
         for u, v in zip(ys1, ys2):
             assert torch.equal(u.view(torch.int32), v.view(torch.int32))
+
+
+def test_multi_c5_full_resnet34_set():
+    """BASELINE config 5 exactly as bench.py --config multi runs it: the 110 ResNet-34 (CIFAR)
+    gradients + the 38 non-BN weights (fc bias included) = 148 tensors, 42,547,220 elements, in one
+    bound SmaqMulti call. Every tensor equals the oracle fed its device statistics and counter
+    stream bit for bit, statistics within 1 ulp of fp64, and the fused call equals the per-tensor
+    SmartFP calls at the same stream offsets."""
+    import bench
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import SmartFP
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    xs = bench.resnet34_c5_tensors(torch.device("cuda"), 0)
+    assert len(xs) == 148 and sum(x.numel() for x in xs) == 42547220
+    assert [tuple(x.shape) for x in xs] == bench.resnet34_c5_shapes()
+    hp = smaq_hparams()
+    ys = [torch.empty_like(x) for x in xs]
+    m = SmaqMulti(hp, seed=21)
+    m.bind(xs, ys)()
+    torch.cuda.synchronize()
+    stats = m.read_stats()
+    single = SmartFP(hp)
+    single.rng.seed = 21
+    for t, (x, y) in enumerate(zip(xs, ys)):
+        xn = x.cpu().numpy().ravel()
+        st = stats[m.index_of(t)]
+        mo, so = osmaq.full_stats(xn, osmaq.SmaqConfig())
+        assert ulp_diff(st["mean"], mo) <= 1 and ulp_diff(st["raw_std"], so) <= 1, t
+        y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], osmaq.SmaqConfig(),
+                              orng.uniforms(21, m.offset_of(t), xn.size))
+        assert same_f32(y.cpu().numpy().ravel(), y_or), t
+        if t % 7 == 0:  # the per-tensor path at the same offset
+            single.rng.offset = m.offset_of(t)
+            assert torch.equal(single(x).view(torch.int32), y.view(torch.int32)), t

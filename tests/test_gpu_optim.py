@@ -191,3 +191,38 @@ def test_register_autograd_module_every_call_bitexact():
     l1, g1, _ = run(SmartFP, False)
     l2, g2, _ = run(SmartFPPacked, False)
     assert torch.equal(l1, l2) and torch.equal(g1.view(torch.int32), g2.view(torch.int32))
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_acc_quant_keeps_full_precision_accumulator(fused):
+    """optimizer.py:63-67, 83-86, 101-107: with acc_quant the inner step updates weight_acc (swapped
+    in as p.data) and the weights are quantised into NEW tensors — the accumulator keeps the full
+    precision update. The fused weight launch must not write through p.data in that case."""
+    from smart_compress_amd.compress.smart import SmartFP
+    from smart_compress_amd.util.pytorch.optimizer import OptimLP, TaggedQuant
+
+    model = _model()
+    base = torch.optim.SGD(_groups(model), lr=0.1, momentum=0.9)
+    codec = SmartFP(smaq_hparams(smq_seed=3))
+    if fused:
+        wq = TaggedQuant(codec, "optimizer_weight")
+    else:
+        def wq(t, **kw):
+            return codec(t, tag="optimizer_weight", **kw)
+    opt = OptimLP(base, weight_quant=wq, acc_quant=lambda t, **kw: t)
+    params = [p for g in opt.param_groups for p in g["params"]]
+    _train(model, opt, steps=2)
+    torch.cuda.synchronize()
+    quantised = [g for g in opt.param_groups if not g.get("no_weight_compression", False)]
+    for g in quantised:
+        for p in g["params"]:
+            acc = opt.weight_acc[p]
+            assert p.data.data_ptr() != acc.data_ptr()  # p now holds a new, quantised tensor
+            if p.numel() >= 8:
+                # the accumulator is not on the SmaQ grid of its own statistics: quantising it
+                # again changes it; the weights are already quantised values
+                assert not torch.equal(acc, p.data)
+    # BN group (no_weight_compression): p.data stays the accumulator itself
+    for p in opt.param_groups[0]["params"]:
+        assert p.data.data_ptr() == opt.weight_acc[p].data_ptr()
+    assert len(params) == len(opt.weight_acc)

@@ -230,8 +230,9 @@ def test_sampled_mode_end_to_end():
     codec = SmartFP(hp)
     codec.rng.seed, codec.rng.offset = 99, 0
     x = torch.randn(1 << 18, device="cuda")
-    p = g.smaq_params(hp, x.numel(), seed=99, offset=0)  # same draws the codec will make
-    idx = np.array(list(p.sample_idx)[: p.num_samples])
+    from oracle import rng as orng0
+
+    idx = orng0.floyd_indices(99, 0, x.numel(), 16)  # the draw the device makes at offset 0
     y = codec(x)
     torch.cuda.synchronize()
     xn = x.cpu().numpy()
