@@ -220,7 +220,8 @@ def launch_ranks(n, argv):
             if pr.poll() is None:
                 pr.kill()
     out = procs[0].stdout.read().decode()
-    sys.stdout.write(out)
+    for line in out.splitlines():  # the JSON line to stdout, anything else (gloo chatter) to stderr
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line + "\n")
     sys.stdout.flush()
     return rc
 

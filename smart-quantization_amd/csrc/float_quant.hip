@@ -407,7 +407,23 @@ struct S2Args {
   float max_value;
   int out_mode;   // 0: y, 1: Y, 2: T (SMQ_S2FP8_OUT_*)
   int exact_pow;  // SMQ_S2FP8_EXACT_POW: library powf for both powers
+  // XCD-aware tile order (vector path): tiles_per_chunk tiles make up partial workgroup w's chunk;
+  // apply block b takes a tile of a chunk w with w % 8 == b % 8 (0: block b takes tile b)
+  int tiles_per_chunk;
+  int n_chunks;
 };
+
+// Apply block -> tile. Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
+// §Workgroup dispatch: blocks b and b + 8 share an XCD; observed, speed only): the partial launch
+// read chunk w on the XCD of its block w, so apply blocks b = c + 8k (one XCD) take the tiles of
+// chunks c, c + 8, ... and find them in that XCD's L2 (C4: 1.6 MB of the 12.6 MB per XCD, well
+// inside its 4 MiB). Any placement gives the same result; only the hit rate depends on it.
+__device__ __forceinline__ int64_t s2_tile_of(int b, int tpc, int n_chunks) {
+  if (tpc == 0) return b;
+  const int c = b & 7, k = b >> 3;
+  const int w = c + 8 * (k / tpc);
+  return w < n_chunks ? (int64_t)w * tpc + (k % tpc) : -1;
+}
 
 // x^p for x >= 0 (or NaN) as exp2(p * log2(x)) on the hardware v_log_f32 / v_exp_f32 (ocml's
 // log2f / exp2f, ~1 ulp each). Valid for finite p > 0 (the caller checks once per launch):
@@ -477,7 +493,12 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   const int64_t n = A.n;
   // the tile's loads go out before the statistics are reduced
   const int64_t nv = n >> 2;
-  const int64_t t0 = (int64_t)blockIdx.x * (kBlock * kFqTileV) + threadIdx.x;
+  const int64_t tile = VEC ? s2_tile_of(blockIdx.x, A.tiles_per_chunk, A.n_chunks)
+                           : (int64_t)blockIdx.x;
+  const int64_t t0 = tile * (kBlock * kFqTileV) + threadIdx.x;
+  const int64_t tiles = (nv + kBlock * kFqTileV - 1) / (kBlock * kFqTileV);
+  const int64_t last_tile = tiles > 0 ? tiles - 1 : 0;  // owns the n % 4 tail
+  if (VEC && (tile < 0 || (tile > last_tile && blockIdx.x != 0))) return;  // no tile
   float4 v[kFqTileV];
   if (VEC) {
 #pragma unroll
@@ -521,7 +542,7 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
       o.w = q1(v[u].w, rb(4 * j + 3));
       store4_out<HOUT>(A.y, j, o);
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < (int)(n & 3)) {
+    if (tile == last_tile && threadIdx.x < (int)(n & 3)) {
       const int64_t e = (nv << 2) + threadIdx.x;
       store1_out<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
     }
@@ -769,7 +790,22 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
   const bool half_out = precision == 16 && dtype == SMQ_DTYPE_F16;
   const bool vec = xal && ((uintptr_t)y & (half_out ? 7u : 15u)) == 0;
   const int tv = precision == 32 ? fq_tile_v() : kFqDefaultTileV;
-  const int grid = (int)((n + (int64_t)kBlock * 4 * tv - 1) / ((int64_t)kBlock * 4 * tv));
+  int grid = (int)((n + (int64_t)kBlock * 4 * tv - 1) / ((int64_t)kBlock * 4 * tv));
+  A.tiles_per_chunk = 0;
+  A.n_chunks = 0;
+  static const int xcd_env = [] {  // measurement knob SMQ_S2_XCD=0: tiles in index order
+    const char* e = getenv("SMQ_S2_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  if (xcd_env && part && vec && xal) {
+    const int64_t per = s2_groups_per_wg(n >> 2);  // float4 groups of one partial chunk
+    const int64_t tile_g = (int64_t)kBlock * tv;
+    if (per % tile_g == 0 && n_partials > 1) {
+      A.tiles_per_chunk = (int)(per / tile_g);
+      A.n_chunks = n_partials;
+      grid = 8 * ((n_partials + 7) / 8) * A.tiles_per_chunk;
+    }
+  }
   if (precision == 32) {
     if (tv == 1) s2_launch<1, kF32, false>(A, rarr, vec, part, grid, st);
     else if (tv == 2) s2_launch<2, kF32, false>(A, rarr, vec, part, grid, st);

@@ -1005,8 +1005,9 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
     set_error("compress: the BatchNorm variant is not supported by the packed container");
     return SMQ_ERR_INVALID;
   }
-  if (p->stats_source != SMQ_STATS_WORKSPACE && p->stats_source != SMQ_STATS_SAMPLED) {
-    set_error("compress: statistics must be SMQ_STATS_WORKSPACE or SMQ_STATS_SAMPLED");
+  if (p->stats_source != SMQ_STATS_WORKSPACE && p->stats_source != SMQ_STATS_SAMPLED &&
+      p->stats_source != SMQ_STATS_SAMPLED_DEVICE) {
+    set_error("compress: statistics must be SMQ_STATS_WORKSPACE or SMQ_STATS_SAMPLED(_DEVICE)");
     return SMQ_ERR_INVALID;
   }
   const int64_t nb = n_blocks_of(n);

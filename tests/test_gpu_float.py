@@ -11,7 +11,7 @@
   * S2FP8 with the reference's (mu, max): alpha, beta, 2^beta bit-exact; outputs y within 2e-5
     relative (the fast pow's error, ~170 fp32 ulp, grows with |p * log2 x|) for >= 99.95 % of the
     elements, the rest an adjacent-code flip seen through the inverse power (<= 0.3 relative);
-    EXACT_POW outputs within 8 fp32 ulp where the codes agree;
+    EXACT_POW outputs within 2 fp32 ulp of the reference's where the codes agree (measured 1);
   * S2FP8 end to end: device mu within 2^-20 relative, m within 1 ulp; outputs as above.
 """
 
@@ -318,8 +318,12 @@ def _ulps(a, b):
     return np.abs(a - b)
 
 
-Y_ULP_FAST = 64   # exp2(p * log2 x): error ~ |p * log2 x| * 2^-23 relative (p <= ~15 / spread)
-Y_ULP_EXACT = 2   # ocml powf vs the reference's pow, both <= 1 ulp
+# measured on MI355X (tools/s2fp8_codes.py, profiles/r2_s2fp8_codes.json): the hardware
+# exp2(p * log2 x) form is off by up to 92 fp32 ulp at C4 (error ~ |p * log2 x| * 2^-23 relative),
+# which flips 2 of 3.1M E5M2 codes to the adjacent one; library powf (EXACT_POW) is within 3 ulp of
+# numpy's / the reference's pow and flipped none
+Y_ULP_FAST = 128
+Y_ULP_EXACT = 4
 
 
 @pytest.mark.parametrize("exact", [False, True])
@@ -349,7 +353,7 @@ def test_s2fp8_code_domain_golden(key, exact):
         y = y.cpu().numpy()
         same = _codes(T) == _codes(T_ref)
         okk = same & ~np.isnan(d["y"])
-        assert _ulps(y[okk], d["y"][okk]).max() <= 8
+        assert _ulps(y[okk], d["y"][okk]).max() <= 2  # measured 1
         assert np.array_equal(np.isnan(y), np.isnan(d["y"]))
 
 

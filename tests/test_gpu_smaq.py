@@ -76,6 +76,7 @@ def test_golden_sampled_indices(name):
     hp = smaq_hparams(meta)
     x = g.golden_x(d, meta)
     p = g.smaq_params(hp, x.numel(), dtype=x.dtype)
+    p.stats_source = g.N.SMQ_STATS_SAMPLED  # host-given indices: the reference's own draw
     idx = d["sample_idx"]
     for j, v in enumerate(idx):
         p.sample_idx[j] = int(v)
