@@ -259,7 +259,19 @@ __device__ void s2fp8_finalize(double s, float m, int64_t n, SmqS2fp8Stats* out)
 constexpr int kS2Partials = kBlock;  // one partial per lane of an apply workgroup
 constexpr int kS2Loads = 16;         // dwordx4 per lane in flight per round
 
-// float4 groups per partial workgroup (>= 1 round of one load per lane); depends on n only, so
+// Threads per partial workgroup (SMQ_S2_PTHREADS = 256 | 1024, measurement knob). One workgroup
+// per CU either way (256 partials); 1024 threads put 4 waves on each SIMD instead of one, so the
+// loads and the log2 chains of one wave hide behind the others'.
+static inline int s2_partial_threads() {
+  static const int v = [] {
+    const char* e = getenv("SMQ_S2_PTHREADS");
+    const int t = e ? atoi(e) : 1024;
+    return (t == 256 || t == 1024) ? t : 1024;
+  }();
+  return v;
+}
+
+// float4 groups per partial workgroup (whole rounds of one load per lane); depends on n only, so
 // the summation order — and the statistics — are a function of n
 static inline int64_t s2_groups_per_wg(int64_t ng) {
   static const int np = [] {  // measurement knob SMQ_S2_PARTIALS (<= kS2Partials)
@@ -268,38 +280,39 @@ static inline int64_t s2_groups_per_wg(int64_t ng) {
     return (v >= 1 && v <= kS2Partials) ? v : kS2Partials;
   }();
   int64_t per = (ng + np - 1) / np;
-  const int64_t q = kBlock;  // whole lanes
+  const int64_t q = s2_partial_threads();  // whole lanes
   per = (per + q - 1) / q * q;
   return per < q ? q : per;
 }
 
-template <int TIN>
-__global__ __launch_bounds__(kBlock) void s2fp8_partial_kernel(const void* __restrict__ x, int64_t n,
-                                                               int vec, int64_t per,
-                                                               S2Partial* __restrict__ partials,
-                                                               SmqS2fp8Stats* out,
-                                                               uint64_t* rng_ctr) {
+template <int TIN, int PT>
+__global__ __launch_bounds__(PT) void s2fp8_partial_kernel(const void* __restrict__ x, int64_t n,
+                                                           int vec, int64_t per,
+                                                           S2Partial* __restrict__ partials,
+                                                           SmqS2fp8Stats* out,
+                                                           uint64_t* rng_ctr) {
+  constexpr int W = PT / kWave;
   // graph-safe random stream: one snapshot + advance per call, read by the apply launch
   if (blockIdx.x == 0 && threadIdx.x == 0) out->rng_offset = take_offset(rng_ctr, (uint64_t)n);
-  __shared__ double shs[kBlock / kWave];
-  __shared__ float shm[kBlock / kWave];
+  __shared__ double shs[W];
+  __shared__ float shm[W];
   double s = 0.0;
   float m = -INFINITY;
   if (vec) {
-    // groups [g0, g1) of this workgroup; lane t takes g0 + t + k * kBlock
+    // groups [g0, g1) of this workgroup; lane t takes g0 + t + k * PT
     const int64_t nv = n >> 2;
     const int64_t g0 = (int64_t)blockIdx.x * per;
     const int64_t g1 = (g0 + per < nv) ? g0 + per : nv;
-    for (int64_t r0 = g0 + threadIdx.x; r0 < g1; r0 += (int64_t)kS2Loads * kBlock) {
+    for (int64_t r0 = g0 + threadIdx.x; r0 < g1; r0 += (int64_t)kS2Loads * PT) {
       float4 v[kS2Loads];
 #pragma unroll
       for (int u = 0; u < kS2Loads; ++u) {
-        const int64_t j = r0 + (int64_t)u * kBlock;
+        const int64_t j = r0 + (int64_t)u * PT;
         if (j < g1) v[u] = load4<TIN>(x, j);
       }
 #pragma unroll
       for (int u = 0; u < kS2Loads; ++u) {
-        const int64_t j = r0 + (int64_t)u * kBlock;
+        const int64_t j = r0 + (int64_t)u * PT;
         if (j >= g1) continue;
         const float l0 = s2_log<TIN>(v[u].x), l1 = s2_log<TIN>(v[u].y), l2 = s2_log<TIN>(v[u].z),
                     l3 = s2_log<TIN>(v[u].w);
@@ -315,7 +328,7 @@ __global__ __launch_bounds__(kBlock) void s2fp8_partial_kernel(const void* __res
   } else {
     const int64_t e0 = (int64_t)blockIdx.x * per * 4;
     const int64_t e1 = (e0 + per * 4 < n) ? e0 + per * 4 : n;
-    for (int64_t i = e0 + threadIdx.x; i < e1; i += kBlock) {
+    for (int64_t i = e0 + threadIdx.x; i < e1; i += PT) {
       const float l = s2_log<TIN>(load1<TIN>(x, i));
       s += (double)l;
       m = nan_max(m, l);
@@ -331,9 +344,16 @@ __global__ __launch_bounds__(kBlock) void s2fp8_partial_kernel(const void* __res
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    double S = 0.0;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < W; w += 4) {  // fixed order: groups of four waves
+      S += (shs[w] + shs[w + 1]) + (shs[w + 2] + shs[w + 3]);
+      M = nan_max(M, nan_max(nan_max(shm[w], shm[w + 1]), nan_max(shm[w + 2], shm[w + 3])));
+    }
     S2Partial p;
-    p.s = (shs[0] + shs[1]) + (shs[2] + shs[3]);
-    p.m = nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3]));
+    p.s = S;
+    p.m = M;
     p.pad = 0.0f;
     partials[blockIdx.x] = p;
   }
@@ -452,6 +472,71 @@ __device__ __forceinline__ float s2fp8_elem(float xv, uint32_t r, float alpha, f
   return t2 * sgn;                                        // * signs
 }
 
+// Inverse of precision 32 by table (s2fp8.py:48: (T * 2^-beta) ** (1/alpha)). T is an E5M2 value
+// (Y >= 0; a NaN Y saturates to +-57344 in the quantiser, +57344 -> +inf under check_inf), so the
+// inverse power has at most 131 distinct arguments per call: each apply workgroup evaluates them
+// once with the accurate library powf into LDS, and an element costs a shift and a table read
+// instead of two transcendental-unit powers. Index = fp32 bits >> 21 (sign, exponent, the two
+// E5M2 mantissa bits; subnormal E5M2 values are normal fp32 numbers of that form): +0 -> 0,
+// 2^-16 .. 57344 -> 444 .. 571, +inf -> 1020, -57344 -> 1595. Other entries hold NaN.
+constexpr int kS2LutSize = 2048;
+constexpr int kS2LutArgs = 131;
+
+__device__ __forceinline__ float s2_lut_arg(int i) {
+  if (i < 128) return __builtin_bit_cast(float, (uint32_t)((111 << 2) + i) << 21);
+  return i == 128 ? 0.0f : (i == 129 ? INFINITY : -57344.0f);
+}
+
+// every thread of the workgroup; ends with a barrier
+__device__ __forceinline__ void s2_build_lut(float* lut, float ibp2, float ialpha) {
+  for (int i = threadIdx.x; i < kS2LutSize; i += blockDim.x) lut[i] = __builtin_nanf("");
+  __syncthreads();
+  if (threadIdx.x < kS2LutArgs) {
+    const float T = s2_lut_arg(threadIdx.x);
+    lut[__builtin_bit_cast(uint32_t, T) >> 21] = powf(T * ibp2, ialpha);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float s2_inverse_lut(float T, const float* lut) {
+  if (T != T) return T;  // (unreachable: the quantiser saturates NaN)
+  return lut[__builtin_bit_cast(uint32_t, T) >> 21];
+}
+
+// The forward of the hot path, branch-free: Y = exp2(alpha * log2|x|) * beta_pow2 (log2f keeps
+// subnormal |x|; the raw v_exp_f32 flushes a subnormal Y, which the quantiser maps to 0 either
+// way: any Y < 2^-37 rounds to 0 in its subnormal path), then qtorch's E5M2 stochastic rounding
+// (qtorch_quant(Y, r, 5, 2, true) with its normal and subnormal paths both computed and one
+// selected) and check_inf (+57344 -> +inf; an E5M2 value within FLT_EPSILON of 57344 is 57344).
+// Returns T's bits.
+__device__ __forceinline__ uint32_t s2_fwd_fast(float xv, uint32_t r, float alpha, float bp2,
+                                                int check_inf) {
+  const float Y = __builtin_amdgcn_exp2f(alpha * log2f(fabsf(xv))) * bp2;
+  const uint32_t t = __builtin_bit_cast(uint32_t, Y);
+  const uint32_t rm = r & 0x1fffffu;            // (1 << (23 - man)) - 1
+  uint32_t qn = (t + rm) & 0xffe00000u;          // round_bitwise
+  qn = ((qn >> 23) & 0xffu) > 142u ? ((t & 0x80000000u) | 0x47600000u) : qn;  // clip_exponent
+  const float sh = __builtin_bit_cast(float, 0x38800000u | (t & 0x80000000u));  // 2^-14
+  const float vs = Y + sh;
+  const float qs = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, vs) + rm) & 0xffe00000u) - sh;
+  uint32_t T = ((t & 0x7f800000u) < 0x38800000u) ? __builtin_bit_cast(uint32_t, qs) : qn;
+  if (check_inf) T = (T == 0x47600000u) ? 0x7f800000u : T;
+  return T;
+}
+
+// Forward half of s2fp8_elem for the LUT inverse: T (after check_inf), or Y / T per out_mode.
+template <bool FAST>
+__device__ __forceinline__ float s2fp8_fwd(float xv, uint32_t r, float alpha, float bp2,
+                                           int check_inf, float max_value, int out_mode) {
+  const float a = fabsf(xv);
+  float Y = FAST ? pow_pos(a, alpha) : powf(a, alpha);  // X_abs.pow_(alpha)
+  Y = Y * bp2;                                            // .mul_(beta_pow2)
+  if (out_mode == 1) return Y;
+  float T = qtorch_quant(Y, r, 5, 2, true);
+  if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
+  return T;
+}
+
 // The same at precision 16 (quantization.py:190-202: float_quantize quantises Y.float() and returns
 // .half()). Forward transform in the input type TIN (fp32 keeps the fast power; fp16/bf16 use
 // ocml powf before rounding to TIN, so the rounding sees an accurate power). Inverse in half:
@@ -490,6 +575,7 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   constexpr int kFqTileElems = kBlock * kFqTileV * 4;
   constexpr bool HOUT = s2_half_out<TIN, P16>();
   __shared__ SmqS2fp8Stats sst;
+  __shared__ float lut[kS2LutSize];
   const int64_t n = A.n;
   // the tile's loads go out before the statistics are reduced
   const int64_t nv = n >> 2;
@@ -521,16 +607,64 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   };
   const bool fast = !A.exact_pow && alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f &&
                     ialpha < INFINITY;
+  if (!P16) s2_build_lut(lut, ibp2, ialpha);  // this call's inverse-power table
   auto q1 = [&](float v, uint32_t r) {
     if (P16)
       return fast ? s2fp8_elem16<TIN, true>(v, r, alpha, bp2, ibp2, ialpha_e, A.check_inf, A.max_value)
                   : s2fp8_elem16<TIN, false>(v, r, alpha, bp2, ibp2, ialpha_e, A.check_inf, A.max_value);
-    return fast ? s2fp8_elem<true>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value,
-                                   A.out_mode)
-                : s2fp8_elem<false>(v, r, alpha, bp2, ibp2, ialpha, A.check_inf, A.max_value,
-                                    A.out_mode);
+    const float T = fast ? s2fp8_fwd<true>(v, r, alpha, bp2, A.check_inf, A.max_value, A.out_mode)
+                         : s2fp8_fwd<false>(v, r, alpha, bp2, A.check_inf, A.max_value, A.out_mode);
+    if (A.out_mode) return T;
+    // `* signs`: torch.sign is +1 / -1, +0 for +-0 and NaN (measured on torch 2.10 CPU)
+    const float sgn = (v > 0.0f) ? 1.0f : ((v < 0.0f) ? -1.0f : 0.0f);
+    return s2_inverse_lut(T, lut) * sgn;
   };
-  if (VEC) {
+  if (VEC && !P16 && !RARR && fast && A.out_mode == 0) {
+    // hot path: all forwards of the tile, then the table reads, then the stores
+    uint32_t T[kFqTileV][4];
+#pragma unroll
+    for (int u = 0; u < kFqTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j >= nv) continue;
+      const uint64_t c = off + ((uint64_t)j << 2);
+      uint32_t r[4];
+      const uint32_t lo = (uint32_t)c;
+      if (__builtin_expect(lo <= 0xfffffffcu, 1)) {  // one rotation of the high word per float4
+        const uint32_t hi = (uint32_t)(c >> 32);
+        const uint32_t kk = ((hi << 16) | (hi >> 16)) ^ A.key;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = mix32((lo + (uint32_t)k) ^ kk);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = rng_u32(A.key, c + (uint64_t)k);
+      }
+      T[u][0] = s2_fwd_fast(v[u].x, r[0], alpha, bp2, A.check_inf);
+      T[u][1] = s2_fwd_fast(v[u].y, r[1], alpha, bp2, A.check_inf);
+      T[u][2] = s2_fwd_fast(v[u].z, r[2], alpha, bp2, A.check_inf);
+      T[u][3] = s2_fwd_fast(v[u].w, r[3], alpha, bp2, A.check_inf);
+    }
+    float t2[kFqTileV][4];
+#pragma unroll
+    for (int u = 0; u < kFqTileV; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t2[u][k] = lut[T[u][k] >> 21];
+    auto sgn = [](float xv) { return (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f); };
+#pragma unroll
+    for (int u = 0; u < kFqTileV; ++u) {
+      const int64_t j = t0 + u * kBlock;
+      if (j >= nv) continue;
+      float4 o;
+      o.x = t2[u][0] * sgn(v[u].x);
+      o.y = t2[u][1] * sgn(v[u].y);
+      o.z = t2[u][2] * sgn(v[u].z);
+      o.w = t2[u][3] * sgn(v[u].w);
+      store4_out<HOUT>(A.y, j, o);
+    }
+    if (tile == last_tile && threadIdx.x < (int)(n & 3)) {
+      const int64_t e = (nv << 2) + threadIdx.x;
+      store1_out<HOUT>(A.y, e, q1(load1<TIN>(A.x, e), rb(e)));
+    }
+  } else if (VEC) {
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
       const int64_t j = t0 + u * kBlock;
@@ -563,6 +697,17 @@ static int fq_tile_v() {
     const char* e = getenv("SMQ_FQ_TILE");
     const int t = e ? atoi(e) : kFqDefaultTileV;
     return (t == 1 || t == 2 || t == 4) ? t : kFqDefaultTileV;
+  }();
+  return v;
+}
+
+// float4 per lane per S2FP8 apply tile (SMQ_S2_TILE = 1 | 2 | 4, measurement knob): a workgroup
+// pays the partial reduction and the inverse-power table once per tile
+static int s2_tile_v() {
+  static const int v = [] {
+    const char* e = getenv("SMQ_S2_TILE");
+    const int t = e ? atoi(e) : 4;  // C4 (bench, 48 buffers): 1 / 2 / 4 -> 18.9 / 15.4 / 14.8 us
+    return (t == 1 || t == 2 || t == 4) ? t : 4;
   }();
   return v;
 }
@@ -764,7 +909,15 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
     int64_t g = (ng + per - 1) / per;
     if (g < 1) g = 1;  // n < 4: the tail alone
     n_partials = (int)g;
-#define SMQ_S2P(T) hipLaunchKernelGGL((s2fp8_partial_kernel<T>), dim3(n_partials), dim3(kBlock), 0, st, x, n, vec, per, partials, hdr, offset_counter)
+#define SMQ_S2P(T)                                                                            \
+  do {                                                                                        \
+    if (s2_partial_threads() == 1024)                                                         \
+      hipLaunchKernelGGL((s2fp8_partial_kernel<T, 1024>), dim3(n_partials), dim3(1024), 0, st, \
+                         x, n, vec, per, partials, hdr, offset_counter);                      \
+    else                                                                                      \
+      hipLaunchKernelGGL((s2fp8_partial_kernel<T, kBlock>), dim3(n_partials), dim3(kBlock), 0, \
+                         st, x, n, vec, per, partials, hdr, offset_counter);                  \
+  } while (0)
     if (dtype == SMQ_DTYPE_F32) SMQ_S2P(kF32);
     else if (dtype == SMQ_DTYPE_F16) SMQ_S2P(kF16);
     else SMQ_S2P(kBF16);
@@ -789,7 +942,7 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
   const bool rarr = rand_bits != nullptr;
   const bool half_out = precision == 16 && dtype == SMQ_DTYPE_F16;
   const bool vec = xal && ((uintptr_t)y & (half_out ? 7u : 15u)) == 0;
-  const int tv = precision == 32 ? fq_tile_v() : kFqDefaultTileV;
+  const int tv = precision == 32 ? s2_tile_v() : kFqDefaultTileV;
   int grid = (int)((n + (int64_t)kBlock * 4 * tv - 1) / ((int64_t)kBlock * 4 * tv));
   A.tiles_per_chunk = 0;
   A.n_chunks = 0;

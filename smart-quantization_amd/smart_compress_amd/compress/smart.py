@@ -215,8 +215,9 @@ class SmartFP(CompressionAlgorithmBase):
             keep = None
             if hp.use_batch_norm and batch_norm_stats is not None:
                 keep = self._bind_batch_norm(p, x, batch_norm_stats)
-            ws = N.workspace("smaq", x.device, N.lib().smq_smaq_workspace_bytes(numel))
-            self._launch(x, y, numel, p, ws, code)
+            st = N.stream_ptr(x.device)
+            ws = N.workspace("smaq", x.device, N.lib().smq_smaq_workspace_bytes(numel), st)
+            self._launch(x, y, numel, p, ws, code, st)
             del keep
 
             def new_size():
@@ -230,9 +231,9 @@ class SmartFP(CompressionAlgorithmBase):
     _trace = None
 
     def _launch(self, x: torch.Tensor, y: torch.Tensor, numel: int, p, ws: torch.Tensor,
-                code: int = N.SMQ_DTYPE_F32):
+                code: int = N.SMQ_DTYPE_F32, st: int = None):
         lib = N.lib()
-        st = N.stream_ptr(x.device)
+        st = N.stream_ptr(x.device) if st is None else st
         tr = self._trace
         if p.stats_source == N.SMQ_STATS_WORKSPACE:
             N.check(lib.smq_smaq_stats(x.data_ptr(), code, numel, p, ws.data_ptr(), ws.numel(), st),

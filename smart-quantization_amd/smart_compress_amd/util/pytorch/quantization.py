@@ -88,19 +88,21 @@ def float_quantize(x: torch.Tensor, exp: int, man: int, hparams) -> torch.Tensor
     else:
         N.require_device_f32(x, "float_quantize")
     src = x.contiguous()
-    out = torch.empty(src.shape, dtype=torch.float16 if half_io else torch.float32,
-                      device=src.device)
+    out = torch.empty_like(src, dtype=torch.float16 if half_io else torch.float32)
     n = src.numel()
     if n == 0:
         return out
+    global _fq
+    if _fq is None:
+        _fq = N.lib().smq_float_quant
     seed, offset, ctr = rng_stream(n, src.device)
-    N.check(
-        N.lib().smq_float_quant(
-            src.data_ptr(), N.DTYPE_CODES[src.dtype], out.data_ptr(),
-            N.SMQ_DTYPE_F16 if half_io else N.SMQ_DTYPE_F32, n, exp, man, N.SMQ_ROUND_STOCHASTIC,
-            1 if hparams.float_quantize_check_inf else 0, None, seed, offset, ctr,
-            N.stream_ptr(src.device),
-        ),
-        "smq_float_quant",
-    )
+    rc = _fq(src.data_ptr(), N.DTYPE_CODES[src.dtype], out.data_ptr(),
+             N.SMQ_DTYPE_F16 if half_io else N.SMQ_DTYPE_F32, n, exp, man, N.SMQ_ROUND_STOCHASTIC,
+             1 if hparams.float_quantize_check_inf else 0, None, seed, offset, ctr,
+             N.stream_ptr(src.device))
+    if rc:
+        N.check(rc, "smq_float_quant")
     return out
+
+
+_fq = None  # the bound C entry point, resolved on first use

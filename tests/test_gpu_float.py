@@ -406,3 +406,27 @@ def test_fp8_c3_full_size_vs_oracle():
     y_or = qf.float_quantize(xn, 5, 2, orng.rng_u32(7, 12345, xn.size), True)
     yh = y.cpu().numpy().ravel()
     assert same_f32(yh, y_or), n_diff_f32(yh, y_or)
+
+
+@pytest.mark.parametrize("n,shift", [(3 * 2**20 + 3, 0), (3 * 2**20 + 3, 1), (4096 * 7, 0), (5, 0)])
+@pytest.mark.parametrize("check_inf", [True, False])
+def test_s2fp8_hot_path_equals_generic(n, shift, check_inf):
+    """The counter-RNG hot path of the apply (branch-free forward, batched table reads) gives the
+    same bits as the generic element path fed the same random words as an array (rand_bits), on
+    data with zeros, subnormals, huge values (saturation, check_inf) and a ragged tail."""
+    from oracle import rng as orng
+
+    g = _g()
+    gen = torch.Generator(device="cuda").manual_seed(n)
+    base = torch.randn(n + shift, generator=gen, device="cuda") * torch.exp(
+        torch.randn(n + shift, generator=gen, device="cuda") * 3)
+    base[::11] = 0.0
+    base[5::13] = 1e-40
+    base[7::17] = -3e38
+    x = base[shift:]
+    y_hot, st = g.s2fp8(x, check_inf=check_inf, seed=9, offset=2**32 - 77)
+    words = g.to_dev(orng.rng_u32(9, 2**32 - 77, n).view(np.int32))
+    y_gen, st2 = g.s2fp8(x, check_inf=check_inf, rand_bits=words)
+    assert st["alpha"] == st2["alpha"] and st["beta_pow2"] == st2["beta_pow2"]
+    assert same_f32(y_hot.cpu().numpy(), y_gen.cpu().numpy()), n_diff_f32(y_hot.cpu().numpy(),
+                                                                        y_gen.cpu().numpy())
