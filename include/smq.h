@@ -150,13 +150,16 @@ typedef struct SmqSmaqStats {
   uint32_t reserved[2];
 } SmqSmaqStats;
 
-/* One tensor of a multi-tensor call. y may alias x (in-place, the optimizer path). */
+/* One tensor of a multi-tensor call. x holds n elements of the call's dtype; y (fp32) may alias x
+ * for fp32 inputs (in-place, the optimizer path). */
 typedef struct SmqTensorDesc {
-  const float* x;
+  const void* x;
   float* y;
   int64_t n;
   int32_t all_positive;
-  int32_t reserved;
+  float range_std_coef; /* --use_range_std_dev: C for this tensor (n, or k samples, in its dtype,
+                           as the reference's torch ops give it: see SmqSmaqParams.range_std_coef);
+                           negative: the library's fp32 1 / sqrt(2 ln n). Unused otherwise. */
   uint64_t rng_offset; /* RNG counter of element 0, relative to params.offset */
 } SmqTensorDesc;
 
@@ -222,10 +225,18 @@ size_t smq_smaq_multi_plan_bytes(const int64_t* sizes, int count);
 int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_plan,
                               size_t plan_bytes);
 size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count);
-/* Two launches for the whole list. Statistics of tensor t land in ((SmqSmaqStats*)ws)[t]. Only
- * full statistics (SMQ_STATS_WORKSPACE, no range-std) are supported. host_plan is read for its
- * header (and, with params.offset_counter, its descriptors: the call advances the counter by
- * max(rng_offset + n) over the tensors; tensor t draws offset + snapshot + rng_offset + i). */
+/* Two launches for the whole list. Statistics of tensor t land in ((SmqSmaqStats*)ws)[t]:
+ * SMQ_STATS_WORKSPACE (full statistics, with --use_range_std_dev the range form), or
+ * SMQ_STATS_SAMPLED_DEVICE (k = min(n, num_samples) indices per tensor drawn on the device at
+ * position offset + snapshot + rng_offset: the draw of a single-tensor call at that offset). The
+ * inputs are all of element type `dtype` (SMQ_DTYPE_*), outputs fp32; fp16 / bf16 inputs cannot be
+ * updated in place. No BN variant. host_plan is read for its header and descriptors (with
+ * params.offset_counter the call advances the counter by max(rng_offset + n) over the tensors;
+ * tensor t draws offset + snapshot + rng_offset + i). A multi call equals the sequence of
+ * single-tensor calls at those offsets, bit for bit. */
+int smq_smaq_multi(const void* dev_plan, const void* host_plan, int dtype, const SmqSmaqParams* p,
+                   void* ws, size_t ws_bytes, void* stream);
+/* smq_smaq_multi with dtype SMQ_DTYPE_F32. */
 int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan, const SmqSmaqParams* p,
                        void* ws, size_t ws_bytes, void* stream);
 

@@ -257,21 +257,8 @@ __global__ __launch_bounds__(kWave) void smaq_sample_stats_kernel(ApplyArgs A) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Device-drawn sampled statistics (SMQ_STATS_SAMPLED_DEVICE): smart.py:86-91 with the randperm
-// of line 88 replaced by Floyd's algorithm on the device, so every call — and every replay of a
-// captured graph — draws a fresh index set from the call's stream position.
-//
-// Floyd: for i = 0 .. k-1, j = n - k + i: t = h_i mod (j + 1); pick t unless an earlier pick
-// equals it, then pick j (never picked before: every earlier pick is < j). h_i is the 64-bit word
-// (rng_u32(key', 2P + 2i) << 32) | rng_u32(key', 2P + 2i + 1), key' = rng_key(seed ^ kDrawSalt),
-// P = offset + stream position: a function of the call alone (smq_smaq_draw_samples and
-// oracle/rng.py floyd_indices restate it). The candidates t are independent and computed in
-// parallel; only the duplicate test is sequential: a register/ballot scan by one wave for k <= 64,
-// an LDS open-addressing set walked by one lane for larger k.
-// ------------------------------------------------------------------------------------------------
-constexpr uint64_t kDrawSalt = 0xd1b54a32d192ed03ull;
-
+// Device-drawn sampled statistics (SMQ_STATS_SAMPLED_DEVICE): one workgroup draws k indices
+// (Floyd, smaq_elem.h draw_sample_stats) from the call's stream position and writes the statistics.
 struct DrawArgs {
   const void* x;
   int64_t n;
@@ -285,118 +272,15 @@ struct DrawArgs {
   int64_t* idx_out;               // workspace, SMQ_MAX_DEVICE_SAMPLES entries
 };
 
-__host__ __device__ __forceinline__ int64_t floyd_candidate(uint32_t key, uint64_t pos, int64_t n,
-                                                            int k, int i) {
-  const uint64_t c = 2ull * pos + 2ull * (uint64_t)i;
-  const uint64_t h = ((uint64_t)rng_u32(key, c) << 32) | rng_u32(key, c + 1);
-  return (int64_t)(h % (uint64_t)(n - k + i + 1));
-}
-
-__device__ __forceinline__ uint32_t pick_hash(int64_t t, int bits) {
-  const uint32_t v = (uint32_t)t ^ (uint32_t)((uint64_t)t >> 32);
-  return (v * 0x9e3779b1u) >> (32 - bits);
-}
-
 template <int TIN>
 __global__ __launch_bounds__(kBlock) void smaq_draw_stats_kernel(DrawArgs A) {
-  __shared__ int64_t pick[SMQ_MAX_DEVICE_SAMPLES];          // 32 KiB
-  __shared__ uint16_t table[2 * SMQ_MAX_DEVICE_SAMPLES];    // 16 KiB: pick index + 1, 0 = empty
+  __shared__ DrawLds L;
   __shared__ unsigned long long pos_s;
-  __shared__ double shs[kBlock / kWave];
-  const int k = A.k;
-  const int64_t n = A.n;
   if (threadIdx.x == 0) pos_s = A.offset + (A.rng_ctr ? *A.rng_ctr : 0ull);
   __syncthreads();
-  const uint64_t pos = pos_s;
-  for (int i = threadIdx.x; i < k; i += kBlock) pick[i] = floyd_candidate(A.key, pos, n, k, i);
-  int bits = 1;
-  while ((1 << bits) < 2 * k) ++bits;
-  if (k > kWave)
-    for (int i = threadIdx.x; i < (1 << bits); i += kBlock) table[i] = 0;
-  __syncthreads();
-  if (k <= kWave) {
-    if (threadIdx.x < kWave) {  // lane i holds pick i; lanes < i are final at step i
-      const int lane = threadIdx.x;
-      int64_t p = lane < k ? pick[lane] : -1;
-      for (int i = 1; i < k; ++i) {
-        const int32_t lo = __builtin_amdgcn_readlane((int32_t)p, i);
-        const int32_t hi = __builtin_amdgcn_readlane((int32_t)((uint64_t)p >> 32), i);
-        const int64_t t = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-        const bool dup = __ballot(lane < i && p == t) != 0ull;
-        if (dup && lane == i) p = n - k + i;
-      }
-      if (lane < k) pick[lane] = p;
-    }
-  } else if (threadIdx.x == 0) {
-    const uint32_t mask = (1u << bits) - 1u;
-    for (int i = 0; i < k; ++i) {
-      int64_t t = pick[i];
-      uint32_t s = pick_hash(t, bits);
-      bool dup = false;
-      for (uint16_t e; (e = table[s]) != 0; s = (s + 1) & mask)
-        if (pick[e - 1] == t) {
-          dup = true;
-          break;
-        }
-      if (dup) {  // j = n - k + i is new: probe for its own empty slot
-        t = n - k + i;
-        s = pick_hash(t, bits);
-        while (table[s] != 0) s = (s + 1) & mask;
-      }
-      pick[i] = t;
-      table[s] = (uint16_t)(i + 1);
-    }
-  }
-  __syncthreads();
-  // gather: thread t owns samples t, t + kBlock, ... (<= 16); fp64 sums in one fixed order
-  constexpr int kPer = SMQ_MAX_DEVICE_SAMPLES / kBlock;
-  float v[kPer];
-  double s = 0.0;
-  float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int i = threadIdx.x + u * kBlock;
-    v[u] = 0.0f;
-    if (i < k) {
-      const int64_t e = pick[i];
-      A.idx_out[i] = e;
-      v[u] = load1<TIN>(A.x, e);
-      s += (double)v[u];
-      mn = fminf(mn, v[u]);
-      mx = fmaxf(mx, v[u]);
-    }
-  }
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  s = wave_sum(s);
-  if (lane == 0) shs[wave] = s;
-  __syncthreads();
-  const double mean = ((shs[0] + shs[1]) + (shs[2] + shs[3])) / (double)k;
-  __syncthreads();
-  double m2 = 0.0;
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int i = threadIdx.x + u * kBlock;
-    if (i < k) {
-      const double d = (double)v[u] - mean;
-      m2 = fma(d, d, m2);
-    }
-  }
-  StatAcc acc;
-  acc.s1 = 0.0;
-  acc.s2 = m2;
-  acc.mn = mn;
-  acc.mx = mx;
-  block_reduce_stats<true>(acc);
-  if (threadIdx.x == 0) {
-    SmqSmaqStats st;
-    FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, A.rng_ctr, n};
-    // shifted sums with shift = mean: s1 = 0, s2 = the biased second moment's numerator
-    if (A.use_range)
-      finalize_stats<true, TIN>(0.0, acc.s2, acc.mn, acc.mx, k, mean, true, f, &st);
-    else
-      finalize_stats<false, TIN>(0.0, acc.s2, acc.mn, acc.mx, k, mean, true, f, &st);
-    *A.ws_stats = st;
-  }
+  // the finaliser snapshots the graph-safe position and advances it by n
+  const FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, A.rng_ctr, A.n};
+  draw_sample_stats<TIN>(A.x, A.n, A.k, A.key, pos_s, A.use_range, f, A.ws_stats, A.idx_out, L);
 }
 
 // Injected statistics (parity tests, callers with their own mean/std): copy the record into the

@@ -11,6 +11,13 @@
 //            RNG counter = params.offset + desc.rng_offset + element index (so a multi call equals
 //            the sequence of single-tensor calls at those offsets, and a plan is reusable).
 // y may alias x: every element is read once by the apply launch before it is written.
+//
+// Statistics variants (params): full (the statistics launch above; with --use_range_std_dev it also
+// carries min / max), or SMQ_STATS_SAMPLED_DEVICE: one workgroup per tensor draws its k indices
+// (Floyd, smaq_elem.h draw_sample_stats) at position offset + snapshot + desc.rng_offset — the
+// draw a single-tensor call at that offset makes — instead of the sweep. Input element types:
+// fp32, fp16, bf16 (one per call; outputs fp32 like the single-tensor path, so y may alias x only
+// for fp32).
 #include <stdlib.h>
 #include <string.h>
 
@@ -41,7 +48,7 @@ struct MultiHeader {
 // Everything one workgroup needs, in ONE 64-B record (uniform per workgroup -> two s_load_dwordx8):
 // no dependent descriptor loads stand between the launch and the first data load.
 struct ChunkDesc {
-  const float* x;       // tensor base
+  const void* x;        // tensor base (element type: the call's dtype)
   float* y;
   int64_t n;            // tensor elements
   int64_t begin, end;   // element range of this chunk within the tensor
@@ -68,6 +75,10 @@ struct MultiArgs {
   uint64_t rng_span;         // elements this call draws: max(desc.rng_offset + n)
   StatPartial* partials;     // [n_chunks]
   float thr, r_main, r_out, clamp_lo, clamp_hi;
+  int k;                     // SMQ_STATS_SAMPLED_DEVICE: samples per tensor (min(n, k) used)
+  uint32_t draw_key;         // rng_key(seed ^ kDrawSalt)
+  int advance_in_apply;      // sampled: the apply launch advances *rng_ctr (see the draw kernel)
+  int use_range;             // --use_range_std_dev
   double inv_r_main, inv_r_out;
   int safe_q;
   uint32_t key;
@@ -76,6 +87,13 @@ struct MultiArgs {
   int count_outliers;
 };
 
+// range-std coefficient of tensor t (desc.range_std_coef; negative: the fp32 1 / sqrt(2 ln n))
+__device__ __forceinline__ float multi_range_coef(const MultiArgs& A, int t, int64_t n) {
+  const float c = A.descs[t].range_std_coef;
+  return c >= 0.0f ? c : 1.0f / sqrtf(2.0f * logf((float)n));
+}
+
+template <int TIN, bool RANGE>
 __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   __shared__ uint32_t slot;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // one snapshot + advance per call
@@ -87,54 +105,55 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
     *A.rng_snap = o;
   }
   const ChunkDesc ch = A.stat_chunks[blockIdx.x];
-  const float* __restrict__ x = ch.x;
+  const void* __restrict__ x = ch.x;
   const int64_t n = ch.n;
-  const float k0 = x[0], k1 = x[n >> 1], k2 = x[n - 1];
+  const float k0 = load1<TIN>(x, 0), k1 = load1<TIN>(x, n >> 1), k2 = load1<TIN>(x, n - 1);
   const double shift = (double)fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));
   StatAcc acc;
-  if (((uintptr_t)x & 15u) == 0) {
-    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+  if (((uintptr_t)x & (TIN == kF32 ? 15u : 7u)) == 0) {
     const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;  // begin is a multiple of the chunk
     // 16 KiB steps; the next step's four loads are in flight while the current one is summed
     float4 cur[4], nxt[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t j = b4 + threadIdx.x + u * kBlock;
-      cur[u] = j < e4 ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      cur[u] = j < e4 ? load4<TIN>(x, j) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     for (int64_t t0 = b4; t0 < e4; t0 += 4 * kBlock) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t j = t0 + 4 * kBlock + threadIdx.x + u * kBlock;
-        nxt[u] = j < e4 ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        nxt[u] = j < e4 ? load4<TIN>(x, j) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t j = t0 + threadIdx.x + u * kBlock;
         if (j < e4) {
-          acc.add<false>(cur[u].x, shift);
-          acc.add<false>(cur[u].y, shift);
-          acc.add<false>(cur[u].z, shift);
-          acc.add<false>(cur[u].w, shift);
+          acc.add<RANGE>(cur[u].x, shift);
+          acc.add<RANGE>(cur[u].y, shift);
+          acc.add<RANGE>(cur[u].z, shift);
+          acc.add<RANGE>(cur[u].w, shift);
         }
         cur[u] = nxt[u];
       }
     }
-    if (threadIdx.x < (int)(ch.end - (e4 << 2))) acc.add<false>(x[(e4 << 2) + threadIdx.x], shift);
+    if (threadIdx.x < (int)(ch.end - (e4 << 2))) acc.add<RANGE>(load1<TIN>(x, (e4 << 2) + threadIdx.x), shift);
   } else {
-    for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) acc.add<false>(x[j], shift);
+    for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) acc.add<RANGE>(load1<TIN>(x, j), shift);
   }
-  block_reduce_stats<false>(acc);
-  const FinalizeArgs fin{A.clamp_lo, A.clamp_hi, 0.0f};
+  block_reduce_stats<RANGE>(acc);
+  const FinalizeArgs fin{A.clamp_lo, A.clamp_hi, RANGE ? multi_range_coef(A, ch.tensor, n) : 0.0f};
   if (ch.n_chunks == 1) {
     if (threadIdx.x == 0)
-      finalize_stats<false>(acc.s1, acc.s2, 0.f, 0.f, n, shift, false, fin, &A.stats[ch.tensor]);
+      finalize_stats<RANGE, TIN>(acc.s1, acc.s2, acc.mn, acc.mx, n, shift, false, fin,
+                                 &A.stats[ch.tensor]);
     return;
   }
   if (threadIdx.x == 0) {
     StatPartial* p = A.partials + blockIdx.x;
     st_sc1_f64(&p->s1, acc.s1);
     st_sc1_f64(&p->s2, acc.s2);
+    if (RANGE) st_sc1_f32x2(&p->mn, acc.mn, acc.mx);
   }
   const uint32_t prev = block_arrive_tagged(&A.counters[ch.tensor], A.tag.tag, &slot);
   if (prev != (uint32_t)ch.n_chunks - 1) return;
@@ -143,6 +162,7 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   StatAcc tot;
   for (int b0 = 0; b0 < ch.n_chunks; b0 += K * kBlock) {
     double s1v[K], s2v[K];
+    float mnv[K], mxv[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       const int b = b0 + threadIdx.x + i * kBlock;
@@ -150,6 +170,7 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
         const StatPartial* p = A.partials + ch.first_chunk + b;
         s1v[i] = ld_sc1_f64(&p->s1);
         s2v[i] = ld_sc1_f64(&p->s2);
+        if (RANGE) ld_sc1_f32x2(&p->mn, mnv[i], mxv[i]);
       }
     }
 #pragma unroll
@@ -157,37 +178,59 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
       if (b0 + threadIdx.x + i * kBlock < ch.n_chunks) {
         tot.s1 += s1v[i];
         tot.s2 += s2v[i];
+        if (RANGE) {
+          tot.mn = fminf(tot.mn, mnv[i]);
+          tot.mx = fmaxf(tot.mx, mxv[i]);
+        }
       }
     }
   }
-  block_reduce_stats<false>(tot);
+  block_reduce_stats<RANGE>(tot);
   if (threadIdx.x == 0) {
-    finalize_stats<false>(tot.s1, tot.s2, 0.f, 0.f, n, shift, false, fin, &A.stats[ch.tensor]);
+    finalize_stats<RANGE, TIN>(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, fin,
+                               &A.stats[ch.tensor]);
     arrive_reset(&A.counters[ch.tensor], A.tag.next);
   }
 }
 
+// SMQ_STATS_SAMPLED_DEVICE: one workgroup per tensor. Every workgroup reads the graph-safe position
+// (nobody writes it during this launch); workgroup 0 records it for the apply launch, whose
+// workgroup 0 then advances it (apply workgroups read only the record).
+template <int TIN>
+__global__ __launch_bounds__(kBlock) void smaq_multi_draw_kernel(MultiArgs A) {
+  __shared__ DrawLds L;
+  const int t = blockIdx.x;
+  const SmqTensorDesc d = A.descs[t];
+  const uint64_t snap = A.rng_ctr ? *A.rng_ctr : 0ull;
+  if (t == 0 && threadIdx.x == 0) *A.rng_snap = snap;
+  const int k = (int64_t)A.k < d.n ? A.k : (int)d.n;
+  const FinalizeArgs f{A.clamp_lo, A.clamp_hi,
+                       A.descs[t].range_std_coef >= 0.0f ? A.descs[t].range_std_coef
+                                                         : 1.0f / sqrtf(2.0f * logf((float)k))};
+  draw_sample_stats<TIN>(d.x, d.n, k, A.draw_key, A.offset + snap + d.rng_offset,
+                         A.use_range, f, &A.stats[t], nullptr, L);
+}
+
 // all_positive varies per tensor here (one chunk = one tensor): a per-element select.
-template <int RM, bool SUB, bool SQ>
+template <int RM, int TIN, bool SUB, bool SQ>
 __device__ __forceinline__ float elem_ap(float v, float u, const ElemConsts& c, bool all_pos,
                                          bool& b) {
-  const float o = smaq_elem<RM, false, kF32, false, SUB, SQ>(v, u, c, b);
+  const float o = smaq_elem<RM, false, TIN, false, SUB, SQ>(v, u, c, b);
   return (all_pos && o < 0.0f) ? 0.0f : o;  // clamp_min(0.0)
 }
 
 // One chunk. SUB: subnormal-quotient check (per tensor, quot_check_for); SQ: RangeRecips::safe_q.
 // pre: the first step's data, loaded by the caller before the tensor's statistics arrive.
-template <bool SR, bool SUB, bool SQ>
+template <bool SR, int TIN, bool SUB, bool SQ>
 __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, const ChunkDesc& ch,
                                                           const ElemConsts& c, bool all_pos,
                                                           bool vec, const float4 (&pre)[4],
                                                           uint64_t off) {
-  const float* __restrict__ x = ch.x;
-  float* y = ch.y;  // may alias x
+  const void* __restrict__ x = ch.x;
+  float* y = ch.y;  // may alias x (fp32)
   unsigned long long n_out = 0;
   constexpr int RM = SR ? kRoundHash : kRoundTrunc;
   if (vec) {
-    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
     float4* y4 = reinterpret_cast<float4*>(y);
     const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;
     for (int64_t t0 = b4; t0 < e4; t0 += 4 * kBlock) {  // 16 KiB per step, 4 dwordx4 per lane
@@ -196,7 +239,7 @@ __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, co
     for (int u = 0; u < 4; ++u) {
       const int64_t j = t0 + threadIdx.x + u * kBlock;
       if (t0 == b4) v[u] = pre[u];
-      else if (j < e4) v[u] = x4[j];
+      else if (j < e4) v[u] = load4<TIN>(x, j);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -207,10 +250,10 @@ __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, co
       if (SR) rng_hu4(A.key, ctr, u0, u1, u2, u3);
       bool b0, b1, b2, b3;
       float4 o;
-      o.x = elem_ap<RM, SUB, SQ>(v[u].x, u0, c, all_pos, b0);
-      o.y = elem_ap<RM, SUB, SQ>(v[u].y, u1, c, all_pos, b1);
-      o.z = elem_ap<RM, SUB, SQ>(v[u].z, u2, c, all_pos, b2);
-      o.w = elem_ap<RM, SUB, SQ>(v[u].w, u3, c, all_pos, b3);
+      o.x = elem_ap<RM, TIN, SUB, SQ>(v[u].x, u0, c, all_pos, b0);
+      o.y = elem_ap<RM, TIN, SUB, SQ>(v[u].y, u1, c, all_pos, b1);
+      o.z = elem_ap<RM, TIN, SUB, SQ>(v[u].z, u2, c, all_pos, b2);
+      o.w = elem_ap<RM, TIN, SUB, SQ>(v[u].w, u3, c, all_pos, b3);
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
       store_stream(y4 + j, o);
     }
@@ -219,44 +262,46 @@ __device__ __forceinline__ unsigned long long multi_chunk(const MultiArgs& A, co
       const int64_t e = (e4 << 2) + threadIdx.x;
       const float u = SR ? rng_hu(A.key, off + ch.rng_offset + (uint64_t)e) : 0.f;
       bool b;
-      y[e] = elem_ap<RM, SUB, SQ>(x[e], u, c, all_pos, b);
+      y[e] = elem_ap<RM, TIN, SUB, SQ>(load1<TIN>(x, e), u, c, all_pos, b);
       n_out += (unsigned)b;
     }
   } else {
     for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) {
       const float u = SR ? rng_hu(A.key, off + ch.rng_offset + (uint64_t)j) : 0.f;
       bool b;
-      y[j] = elem_ap<RM, SUB, SQ>(x[j], u, c, all_pos, b);
+      y[j] = elem_ap<RM, TIN, SUB, SQ>(load1<TIN>(x, j), u, c, all_pos, b);
       n_out += (unsigned)b;
     }
   }
   return n_out;
 }
 
-template <bool SR, bool SQ>
+template <bool SR, bool SQ, int TIN>
 __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
   __shared__ unsigned long long sh_cnt[kBlock / kWave];
   const ChunkDesc ch = A.chunks[blockIdx.x];
   // the first 16 KiB of the chunk is requested before the statistics (they do not depend on them)
-  const bool vec = (((uintptr_t)ch.x | (uintptr_t)ch.y) & 15u) == 0;
+  const bool vec = (((uintptr_t)ch.x & (TIN == kF32 ? 15u : 7u)) | ((uintptr_t)ch.y & 15u)) == 0;
   float4 pre[4];
   if (vec) {
-    const float4* __restrict__ x4 = reinterpret_cast<const float4*>(ch.x);
     const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t j = b4 + threadIdx.x + u * kBlock;
-      pre[u] = j < e4 ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      pre[u] = j < e4 ? load4<TIN>(ch.x, j) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  if (A.advance_in_apply && blockIdx.x == 0 && threadIdx.x == 0 && A.rng_ctr)
+    *A.rng_ctr = *A.rng_snap + A.rng_span;  // sampled: the draw launch only recorded the position
   const SmqSmaqStats* st = &A.stats[ch.tensor];
   ElemConsts c;
-  init_consts(c, st, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, A.thr);
+  const float cthr = TIN == kF32 ? A.thr : round_in<TIN>(A.thr);
+  init_consts(c, st, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
   const bool all_pos = ch.all_positive != 0;
   const uint64_t off = A.offset + *A.rng_snap;  // + the call's snapshot (0 unless graph-safe)
   const unsigned long long n_out =
-      st->quot_check ? multi_chunk<SR, true, SQ>(A, ch, c, all_pos, vec, pre, off)
-                     : multi_chunk<SR, false, SQ>(A, ch, c, all_pos, vec, pre, off);
+      st->quot_check ? multi_chunk<SR, TIN, true, SQ>(A, ch, c, all_pos, vec, pre, off)
+                     : multi_chunk<SR, TIN, false, SQ>(A, ch, c, all_pos, vec, pre, off);
   if (A.count_outliers) {
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
     const double t = wave_sum((double)n_out);
@@ -394,9 +439,33 @@ size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count) {
 
 }  // extern "C"
 
-extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
-                                  const SmqSmaqParams* p, void* ws, size_t ws_bytes,
-                                  void* stream) {
+template <int TIN>
+static int launch_multi(const MultiArgs& A, bool sampled, bool range, int n_stat_chunks,
+                        int count, int n_chunks, hipStream_t st) {
+  if (sampled) {
+    hipLaunchKernelGGL((smaq_multi_draw_kernel<TIN>), dim3(count), dim3(kBlock), 0, st, A);
+  } else if (range) {
+    hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kBlock), 0,
+                       st, A);
+  } else {
+    hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, false>), dim3(n_stat_chunks), dim3(kBlock),
+                       0, st, A);
+  }
+  int rc = check_launch(sampled ? "smaq_multi_draw_kernel" : "smaq_multi_stats_kernel");
+  if (rc) return rc;
+#define SMQ_MULTI_APPLY(SRV, SQV) \
+  hipLaunchKernelGGL((smaq_multi_apply_kernel<SRV, SQV, TIN>), dim3(n_chunks), dim3(kBlock), 0, st, A)
+  if (A.sr) {
+    if (A.safe_q) SMQ_MULTI_APPLY(true, true); else SMQ_MULTI_APPLY(true, false);
+  } else {
+    if (A.safe_q) SMQ_MULTI_APPLY(false, true); else SMQ_MULTI_APPLY(false, false);
+  }
+#undef SMQ_MULTI_APPLY
+  return check_launch("smaq_multi_apply_kernel");
+}
+
+extern "C" int smq_smaq_multi(const void* dev_plan, const void* host_plan, int dtype,
+                              const SmqSmaqParams* p, void* ws, size_t ws_bytes, void* stream) {
   if (!dev_plan || !host_plan) {
     set_error("multi: dev_plan and host_plan are required");
     return SMQ_ERR_INVALID;
@@ -409,8 +478,22 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
     set_error("multi: bad arguments");
     return SMQ_ERR_INVALID;
   }
-  if (p->stats_source != SMQ_STATS_WORKSPACE || p->use_range_std_dev) {
-    set_error("multi: only full statistics (no sampled / range-std) are supported");
+  if (dtype != SMQ_DTYPE_F32 && dtype != SMQ_DTYPE_F16 && dtype != SMQ_DTYPE_BF16) {
+    set_error("multi: dtype %d is not one of SMQ_DTYPE_F32/F16/BF16", dtype);
+    return SMQ_ERR_INVALID;
+  }
+  const bool sampled = p->stats_source == SMQ_STATS_SAMPLED_DEVICE;
+  if (p->stats_source != SMQ_STATS_WORKSPACE && !sampled) {
+    set_error("multi: statistics must be SMQ_STATS_WORKSPACE or SMQ_STATS_SAMPLED_DEVICE");
+    return SMQ_ERR_INVALID;
+  }
+  if (sampled && (p->num_samples < 1 || p->num_samples > SMQ_MAX_DEVICE_SAMPLES)) {
+    set_error("multi: device-drawn sampled stats need 1 <= num_samples <= %d",
+              SMQ_MAX_DEVICE_SAMPLES);
+    return SMQ_ERR_INVALID;
+  }
+  if (p->bn_gamma) {
+    set_error("multi: the BN variant is per activation tensor (smq_smaq_apply)");
     return SMQ_ERR_INVALID;
   }
   const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
@@ -420,9 +503,18 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
     set_error("multi: workspace too small: need %zu bytes, got %zu", need, ws_bytes);
     return SMQ_ERR_WORKSPACE;
   }
+  if (dtype != SMQ_DTYPE_F32) {  // fp32 outputs: an in-place half tensor cannot hold them
+    const SmqTensorDesc* hd = (const SmqTensorDesc*)((const char*)host_plan + sizeof(MultiHeader));
+    for (int t = 0; t < count; ++t)
+      if ((const void*)hd[t].x == (const void*)hd[t].y) {
+        set_error("multi: tensor %d: fp16 / bf16 inputs write fp32 outputs, y cannot alias x", t);
+        return SMQ_ERR_INVALID;
+      }
+  }
   const char* pb = (const char*)dev_plan;
   const size_t descs_bytes = ((sizeof(SmqTensorDesc) * (size_t)count) + 31) & ~(size_t)31;
   MultiArgs A;
+  memset(&A, 0, sizeof(A));
   A.hdr = (const MultiHeader*)pb;
   A.descs = (const SmqTensorDesc*)(pb + sizeof(MultiHeader));
   A.chunks = (const ChunkDesc*)(pb + sizeof(MultiHeader) + descs_bytes);
@@ -456,17 +548,21 @@ extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
   A.offset = p->offset;
   A.sr = p->stochastic_rounding;
   A.count_outliers = p->count_outliers;
+  A.use_range = p->use_range_std_dev;
+  A.k = sampled ? p->num_samples : 0;
+  A.draw_key = rng_key(p->seed ^ kDrawSalt);
+  A.advance_in_apply = sampled ? 1 : 0;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(smaq_multi_stats_kernel, dim3(n_stat_chunks), dim3(kBlock), 0, st, A);
-  int rc = check_launch("smaq_multi_stats_kernel");
-  if (rc) return rc;
-#define SMQ_MULTI_APPLY(SRV, SQV) \
-  hipLaunchKernelGGL((smaq_multi_apply_kernel<SRV, SQV>), dim3(n_chunks), dim3(kBlock), 0, st, A)
-  if (A.sr) {
-    if (A.safe_q) SMQ_MULTI_APPLY(true, true); else SMQ_MULTI_APPLY(true, false);
-  } else {
-    if (A.safe_q) SMQ_MULTI_APPLY(false, true); else SMQ_MULTI_APPLY(false, false);
-  }
-#undef SMQ_MULTI_APPLY
-  return check_launch("smaq_multi_apply_kernel");
+  const bool range = p->use_range_std_dev != 0;
+  if (dtype == SMQ_DTYPE_F32)
+    return launch_multi<kF32>(A, sampled, range, n_stat_chunks, count, n_chunks, st);
+  if (dtype == SMQ_DTYPE_F16)
+    return launch_multi<kF16>(A, sampled, range, n_stat_chunks, count, n_chunks, st);
+  return launch_multi<kBF16>(A, sampled, range, n_stat_chunks, count, n_chunks, st);
+}
+
+extern "C" int smq_smaq_multi_f32(const void* dev_plan, const void* host_plan,
+                                  const SmqSmaqParams* p, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  return smq_smaq_multi(dev_plan, host_plan, SMQ_DTYPE_F32, p, ws, ws_bytes, stream);
 }

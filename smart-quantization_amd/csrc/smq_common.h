@@ -67,10 +67,16 @@ __device__ __forceinline__ void store_nt(float4* p, const float4& v) {
 #ifndef SMQ_STORE_SC
 #define SMQ_STORE_SC 1
 #endif
+//
+// The store is inline asm, which the compiler's hazard recognizer cannot see as a VMEM store of
+// 16 bytes: a VALU write of the data VGPRs right behind it would race the store's read of them
+// (a wave64 store reads its data 16 lanes per cycle; measured on gfx950: the first element of 16
+// lanes of some tiles came out as the next value written to that register). The trailing
+// `s_nop 1` gives the two wait states the hazard needs, inside the asm statement.
 __device__ __forceinline__ void store_stream(float4* p, const float4& v) {
 #if SMQ_STORE_SC
   const f32x4 w = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(w) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
 #else
   store_nt(p, v);
 #endif

@@ -119,7 +119,7 @@ class SmqTensorDesc(ctypes.Structure):
         ("y", ctypes.c_void_p),
         ("n", ctypes.c_int64),
         ("all_positive", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("range_std_coef", ctypes.c_float),
         ("rng_offset", ctypes.c_uint64),
     ]
 
@@ -183,6 +183,7 @@ SIGNATURES = {
     "smq_smaq_multi_plan_build": (_I32, [ctypes.POINTER(SmqTensorDesc), _I32, _P, _SZ]),
     "smq_smaq_multi_workspace_bytes": (_SZ, [ctypes.POINTER(_I64), _I32]),
     "smq_smaq_multi_f32": (_I32, [_P, _P, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P]),
+    "smq_smaq_multi": (_I32, [_P, _P, _I32, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P]),
     "smq_float_quant_f32": (
         _I32,
         [_P, _P, _I64, _I32, _I32, _I32, _I32, _P, _U64, _U64, _P],

@@ -3,8 +3,9 @@
 Reference: util/pytorch/optimizer.py:69-127 runs ``SmartFP.__call__`` once per parameter tensor
 (a ResNet-34 step: 148 tensors, median 256 elements, each call ~24 ATen launches + 1 host sync).
 ``SmaqMulti`` computes exactly what those per-tensor calls compute — each tensor keeps its own
-mean/std (full statistics), its own ``all_positive`` flag and passthrough below ``min_size`` — in
-two launches of libsmq (``smq_smaq_multi_f32``) for the whole list.
+statistics (full, range-std or device-drawn samples: smart.py:86-108), its own ``all_positive``
+flag and passthrough below ``min_size`` — in two launches of libsmq (``smq_smaq_multi``) per input
+dtype of the list (fp32 / fp16 / bf16; outputs fp32 like the single-tensor path).
 
 The plan (descriptor table + chunk map) is cached by the list's pointers and sizes, so a training
 loop whose parameter and gradient buffers stay put uploads it once.
@@ -18,13 +19,14 @@ import numpy as np
 import torch
 
 from ... import _native as N
-from ...compress.smart import SmartFP
+from ...compress.smart import SmartFP, range_std_coef
 
 
 class SmaqMulti:
     def __init__(self, hparams, seed: Optional[int] = None, rng: Optional[N.RngState] = None):
-        if hparams.use_sample_stats or hparams.use_range_std_dev:
-            raise NotImplementedError("SmaqMulti supports full statistics only")
+        if hparams.use_sample_stats and min(hparams.num_samples, 1 << 30) > N.SMQ_MAX_DEVICE_SAMPLES:
+            raise NotImplementedError(
+                f"--num_samples {hparams.num_samples} > {N.SMQ_MAX_DEVICE_SAMPLES} is not supported")
         self.hparams = hparams
         internal = copy.copy(hparams)
         internal.smq_seed = 0  # the internal codec only builds parameter blocks: no torch RNG draw
@@ -37,21 +39,24 @@ class SmaqMulti:
         self._p = None
         self._graph_safe = False
 
-    def _plan(self, xs, ys, allpos, device):
-        key = tuple((x.data_ptr(), y.data_ptr(), x.numel(), a) for x, y, a in zip(xs, ys, allpos))
+    def _plan(self, xs, ys, allpos, rels, device):
+        """Plan of one dtype group; rels = each tensor's stream offset within the whole call."""
+        key = tuple((x.data_ptr(), y.data_ptr(), x.numel(), a, r, x.dtype)
+                    for x, y, a, r in zip(xs, ys, allpos, rels))
         hit = self._plans.get(key)
         if hit is not None:
             return hit
+        hp = self.hparams
         count = len(xs)
         descs = (N.SmqTensorDesc * count)()
-        rel = 0
-        offsets = []
-        for i, (x, y, a) in enumerate(zip(xs, ys, allpos)):
+        for i, (x, y, a, r) in enumerate(zip(xs, ys, allpos, rels)):
             descs[i].x, descs[i].y, descs[i].n = x.data_ptr(), y.data_ptr(), x.numel()
             descs[i].all_positive = 1 if a else 0
-            descs[i].rng_offset = rel
-            offsets.append(rel)
-            rel += x.numel()
+            descs[i].rng_offset = r
+            descs[i].range_std_coef = -1.0
+            if hp.use_range_std_dev:  # C of the n (or k sampled) elements, in the tensor's dtype
+                m = min(x.numel(), hp.num_samples) if hp.use_sample_stats else x.numel()
+                descs[i].range_std_coef = range_std_coef(m, x.dtype)
         sizes = (ctypes.c_int64 * count)(*[x.numel() for x in xs])
         lib = N.lib()
         nbytes = lib.smq_smaq_multi_plan_bytes(sizes, count)
@@ -61,7 +66,7 @@ class SmaqMulti:
         dev_t = host_t.to(device)
         ws_bytes = lib.smq_smaq_multi_workspace_bytes(sizes, count)
         ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=device)
-        plan = dict(host=host, dev=dev_t, ws=ws, offsets=offsets, total=rel, count=count)
+        plan = dict(host=host, dev=dev_t, ws=ws, count=count, dtype=N.DTYPE_CODES[xs[0].dtype])
         if len(self._plans) > 16:
             self._plans.clear()
         self._plans[key] = plan
@@ -79,47 +84,87 @@ class SmaqMulti:
                 if y is not x:
                     y.copy_(x)
                 continue
-            N.require_device_f32(x, "SmaqMulti")
+            N.require_device(x, "SmaqMulti")
+            if x.dtype not in N.DTYPE_CODES:
+                raise NotImplementedError(f"SmaqMulti: dtype {x.dtype} is not supported")
+            if x.dtype == torch.float16 and hp.precision != 16:
+                # the reference's std.clamp(1e-38, 1e38) on a half tensor (smart.py:154)
+                raise RuntimeError("value cannot be converted to type c10::Half without overflow")
             if not (x.is_contiguous() and y.is_contiguous() and y.dtype == torch.float32
                     and y.numel() == x.numel()):
-                raise RuntimeError("SmaqMulti needs contiguous float32 tensors of equal size")
+                raise RuntimeError("SmaqMulti needs contiguous inputs and float32 outputs of equal "
+                                   "size")
+            if x.dtype != torch.float32 and y.data_ptr() == x.data_ptr():
+                raise RuntimeError("SmaqMulti: fp16 / bf16 inputs give fp32 outputs; y cannot "
+                                   "alias x")
             sel.append(i)
             sx.append(x)
             sy.append(y)
             sa.append(bool(all_positive[i]))
         return sel, sx, sy, sa
 
-    def _launch(self, plan, sel, device):
+    def _groups(self, sx, sy, sa, device):
+        """One plan per input dtype (list order kept inside each); rels over the whole list."""
+        rels, rel = [], 0
+        for x in sx:
+            rels.append(rel)
+            rel += x.numel()
+        by = {}
+        for j, x in enumerate(sx):
+            by.setdefault(x.dtype, []).append(j)
+        if len(by) > 1 and self._graph_safe:
+            raise NotImplementedError("SmaqMulti: a graph-safe call takes one input dtype")
+        plans = [self._plan([sx[j] for j in js], [sy[j] for j in js], [sa[j] for j in js],
+                            [rels[j] for j in js], device) for js in by.values()]
+        return plans, rels, rel
+
+    def _params(self):
         p = self._p
         if p is None:  # built once: the C call reads it synchronously, only seed/offset change
+            hp = self.hparams
             p = self._p = self._codec._params(1, False)
-            p.stats_source = N.SMQ_STATS_WORKSPACE
-            p.count_outliers = 1 if self.hparams.measure_compression_ratio else 0
+            if hp.use_sample_stats:
+                p.stats_source = N.SMQ_STATS_SAMPLED_DEVICE
+                p.num_samples = hp.num_samples
+            else:
+                p.stats_source = N.SMQ_STATS_WORKSPACE
+            p.count_outliers = 1 if hp.measure_compression_ratio else 0
+        return p
+
+    def _launch(self, plans, rels, total, sel, device):
+        p = self._params()
         if self._graph_safe:
             p.seed, p.offset = self.rng.seed, 0
             p.offset_counter = self.rng.counter(device).data_ptr()
         else:
-            p.seed, p.offset = self.rng.take(plan["total"])
+            p.seed, p.offset = self.rng.take(total)
             p.offset_counter = None
-        N.check(N.lib().smq_smaq_multi_f32(
-            plan["dev"].data_ptr(), ctypes.addressof(plan["host"]), p, plan["ws"].data_ptr(),
-            plan["ws"].numel(), N.stream_ptr(device)), "smq_smaq_multi_f32")
-        self._last = dict(plan=plan, sel=sel, base=None if self._graph_safe else p.offset)
+        st = N.stream_ptr(device)
+        fn = N.lib().smq_smaq_multi
+        for plan in plans:
+            rc = fn(plan["dev"].data_ptr(), ctypes.addressof(plan["host"]), plan["dtype"], p,
+                    plan["ws"].data_ptr(), plan["ws"].numel(), st)
+            if rc:
+                N.check(rc, "smq_smaq_multi")
+        self._last = dict(plans=plans, rels=rels, sel=sel,
+                          base=None if self._graph_safe else p.offset)
 
     @torch.no_grad()
     def __call__(self, xs: Sequence[torch.Tensor], ys: Optional[Sequence[torch.Tensor]] = None,
                  all_positive=None) -> List[torch.Tensor]:
-        """Quantise-dequantise every ``xs[i]`` into ``ys[i]`` (new tensors if ``ys`` is None; may
-        alias ``xs`` for in-place). Tensors below ``min_size`` are passed through."""
+        """Quantise-dequantise every ``xs[i]`` into ``ys[i]`` (new fp32 tensors if ``ys`` is None;
+        may alias fp32 ``xs`` for in-place). Tensors below ``min_size`` are passed through."""
         hp = self.hparams
         if ys is None:
-            ys = [torch.empty_like(x) if x.numel() >= hp.min_size else x for x in xs]
+            ys = [torch.empty(x.shape, dtype=torch.float32, device=x.device)
+                  if x.numel() >= hp.min_size else x for x in xs]
         sel, sx, sy, sa = self._select(xs, ys, all_positive)
         self._last = None
         if not sel:
             return list(ys)
         device = sx[0].device
-        self._launch(self._plan(sx, sy, sa, device), sel, device)
+        plans, rels, total = self._groups(sx, sy, sa, device)
+        self._launch(plans, rels, total, sel, device)
         return list(ys)
 
     def bind(self, xs: Sequence[torch.Tensor], ys: Sequence[torch.Tensor],
@@ -132,8 +177,8 @@ class SmaqMulti:
             if i not in sel and y is not x:
                 raise RuntimeError("bind: tensors below min_size must be passed as ys[i] = xs[i]")
         device = sx[0].device if sx else None
-        plan = self._plan(sx, sy, sa, device) if sel else None
-        return BoundSmaqMulti(self, plan, sel, device, list(ys))
+        groups = self._groups(sx, sy, sa, device) if sel else None
+        return BoundSmaqMulti(self, groups, sel, device, list(ys))
 
     # -- inspection (tests, logging) ---------------------------------------------------------------
     @property
@@ -159,28 +204,36 @@ class SmaqMulti:
         last = self._last
         if last["base"] is None:
             raise RuntimeError("offset_of: the stream position is on the device (graph-safe mode)")
-        return last["base"] + last["plan"]["offsets"][last["sel"].index(t)]
+        return last["base"] + last["rels"][last["sel"].index(t)]
 
     def read_stats(self):
-        plan = self._last["plan"]
-        raw = plan["ws"][: 64 * plan["count"]].cpu().numpy()
-        out = []
-        for t in range(plan["count"]):
-            r = raw[64 * t: 64 * (t + 1)]
-            f = r[:24].view(np.float32)
-            out.append(dict(mean=float(f[0]), std_dev=float(f[1]), std_clamped=float(f[2]),
-                            raw_std=float(f[3]), n_outlier=int(r[32:40].view(np.uint64)[0])))
+        """Statistics of the last call's selected tensors, in list order."""
+        last = self._last
+        out = [None] * len(last["sel"])
+        # tensors of each plan in list order: map back through the rels (unique per tensor)
+        pos = {r: j for j, r in enumerate(last["rels"])}
+        for plan in last["plans"]:
+            raw = plan["ws"][: 64 * plan["count"]].cpu().numpy()
+            descs = np.frombuffer(bytes(plan["host"])[32: 32 + 40 * plan["count"]], dtype=np.uint8)
+            for t in range(plan["count"]):
+                r = raw[64 * t: 64 * (t + 1)]
+                f = r[:24].view(np.float32)
+                rel = int(descs[40 * t + 32: 40 * t + 40].view(np.uint64)[0])
+                out[pos[rel]] = dict(mean=float(f[0]), std_dev=float(f[1]),
+                                     std_clamped=float(f[2]), raw_std=float(f[3]),
+                                     n_outlier=int(r[32:40].view(np.uint64)[0]))
         return out
 
 
 class BoundSmaqMulti:
-    """``SmaqMulti.bind`` result: one call = the two launches of the bound list."""
+    """``SmaqMulti.bind`` result: one call = the two launches per dtype group of the bound list."""
 
-    def __init__(self, multi: SmaqMulti, plan, sel, device, ys):
-        self.multi, self.plan, self.sel, self.device, self.ys = multi, plan, sel, device, ys
+    def __init__(self, multi: SmaqMulti, groups, sel, device, ys):
+        self.multi, self.groups, self.sel, self.device, self.ys = multi, groups, sel, device, ys
 
     @torch.no_grad()
     def __call__(self) -> List[torch.Tensor]:
-        if self.plan is not None:
-            self.multi._launch(self.plan, self.sel, self.device)
+        if self.groups is not None:
+            plans, rels, total = self.groups
+            self.multi._launch(plans, rels, total, self.sel, self.device)
         return self.ys

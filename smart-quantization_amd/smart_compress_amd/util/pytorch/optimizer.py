@@ -11,8 +11,8 @@ util/pytorch/hooks.py:22-34 (``wrap_optimizer``). Same constructor, same order o
   unless ``momentum == 0``; Adam/AdamW ``exp_avg`` and ``exp_avg_sq`` with ``all_positive=True``),
   skipping ``no_momentum_compression`` groups.
 
-Fusion: when a quantiser is this package's ``SmartFP`` (wrapped by ``wrap_optimizer`` below) and
-uses full statistics, each of those loops becomes ONE ``SmaqMulti`` call (two launches) that
+Fusion: when a quantiser is this package's ``SmartFP`` (wrapped by ``wrap_optimizer`` below), each
+of those loops becomes ONE ``SmaqMulti`` call (two launches) that
 rewrites the tensors in place, instead of one ``SmartFP.__call__`` (two launches + allocation) per
 tensor. Per tensor the arithmetic is identical: own mean/std, own ``all_positive``, ``min_size``
 passthrough, and the same ``optimizer_*`` compression-ratio logs when measuring. Any other
@@ -53,10 +53,10 @@ def wrap_optimizer(optimizer: Optimizer, compress_fn, hparams):
 
 
 def _fusable(fn) -> Optional[SmartFP]:
+    """The SmartFP behind a wrap_optimizer quantiser (any statistics mode: full, range-std or
+    sampled — SmaqMulti computes each exactly as the per-tensor call would)."""
     if isinstance(fn, TaggedQuant) and isinstance(fn.codec, SmartFP):
-        hp = fn.codec.hparams
-        if not hp.use_sample_stats and not hp.use_range_std_dev:
-            return fn.codec
+        return fn.codec
     return None
 
 

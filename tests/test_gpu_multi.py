@@ -114,3 +114,100 @@ def test_multi_c5_full_resnet34_set():
         if t % 7 == 0:  # the per-tensor path at the same offset
             single.rng.offset = m.offset_of(t)
             assert torch.equal(single(x).view(torch.int32), y.view(torch.int32)), t
+
+
+MODES = [dict(use_sample_stats=True), dict(use_sample_stats=True, num_samples=300),
+         dict(use_sample_stats=True, use_range_std_dev=True), dict(use_range_std_dev=True),
+         dict(stochastic_rounding=False, use_sample_stats=True)]
+
+
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "-".join(f"{k}={v}" for k, v in m.items()))
+@pytest.mark.parametrize("dt", ["f32", "f16", "bf16"])
+def test_multi_modes_equal_single_calls(mode, dt):
+    """Sampled (device-drawn, any k), range-std and half-input lists in one SmaqMulti call equal
+    the per-tensor SmartFP calls at the same stream offsets bit for bit (statistics included)."""
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.smart import SmartFP
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[dt]
+    hp = smaq_hparams(precision=16 if dt == "f16" else 32, **mode)
+    xs = [x.to(tdt) for x in _make(4)]
+    m = SmaqMulti(hp, seed=8)
+    ys = m(xs)
+    torch.cuda.synchronize()
+    stats = m.read_stats()
+    single = SmartFP(hp)
+    single.rng.seed = 8
+    for t, (x, y) in enumerate(zip(xs, ys)):
+        if x.numel() < hp.min_size:
+            assert y is x
+            continue
+        assert y.dtype == torch.float32
+        single.rng.offset = m.offset_of(t)
+        ref = single(x)
+        torch.cuda.synchronize()
+        st = SmartFP.read_stats(N.workspace("smaq", x.device, 0))
+        assert torch.equal(ref.view(torch.int32), y.view(torch.int32)), t
+        assert stats[m.index_of(t)]["mean"] == st["mean"], t
+        assert stats[m.index_of(t)]["raw_std"] == st["raw_std"], t
+
+
+def test_multi_mixed_dtypes_one_call_per_group():
+    """A list mixing fp32 / bf16 tensors: one launch pair per dtype, each tensor as its single
+    call at its offset in the whole list."""
+    from smart_compress_amd.compress.smart import SmartFP
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    hp = smaq_hparams(use_sample_stats=True)
+    base = _make(5)
+    xs = [x if i % 2 else x.to(torch.bfloat16) for i, x in enumerate(base)]
+    m = SmaqMulti(hp, seed=3)
+    ys = m(xs)
+    single = SmartFP(hp)
+    single.rng.seed = 3
+    for t, (x, y) in enumerate(zip(xs, ys)):
+        if x.numel() < hp.min_size:
+            continue
+        single.rng.offset = m.offset_of(t)
+        assert torch.equal(single(x).view(torch.int32), y.view(torch.int32)), t
+
+
+def test_multi_sampled_graph_replays():
+    """Graph-safe bound sampled multi call: eager calls and replays equal the host-offset calls
+    (fresh index sets per replay, the draw at each tensor's offset)."""
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    hp = smaq_hparams(use_sample_stats=True, num_samples=50)
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    sizes = [4099, 1 << 16, 3, (1 << 18) + 1, 777]
+    xs = [torch.randn(s, generator=gen, device="cuda") for s in sizes]
+    ys_h = [torch.empty_like(x) if x.numel() >= hp.min_size else x for x in xs]
+    ys_d = [torch.empty_like(x) if x.numel() >= hp.min_size else x for x in xs]
+    host = SmaqMulti(hp, seed=11)
+    dev = SmaqMulti(hp, seed=11).graph_safe(True, device="cuda")
+    bh, bd = host.bind(xs, ys_h), dev.bind(xs, ys_d)
+    bh()
+    bd()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        bd()
+    outs = []
+    for _ in range(3):
+        graph.replay()
+        bh()
+        torch.cuda.synchronize()
+        for a, b in zip(ys_h, ys_d):
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+        outs.append(ys_d[1].clone())
+    assert not torch.equal(outs[0], outs[1])
+    assert dev.rng.position() == host.rng.offset
+
+
+def test_multi_half_in_place_rejected():
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    x = torch.randn(1000, device="cuda").half()
+    with pytest.raises(RuntimeError):
+        SmaqMulti(smaq_hparams(precision=16))([x], [x])
