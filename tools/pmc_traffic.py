@@ -33,6 +33,8 @@ SHORT = {
     "smaq_code_kernel": "smaq_code_kernel",
     "smaq_emit_kernel": "smaq_emit_kernel",
     "smaq_pack_scan_kernel": "smaq_pack_scan_kernel",
+    "smaq_draw_stats_kernel": "smaq_draw_stats_kernel",
+    "smaq_multi_draw_kernel": "smaq_multi_draw_kernel",
 }
 
 
