@@ -218,7 +218,7 @@ __device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c
     float qk[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      bool hi, lo, esc;
+      bool hi, lo, esc = false;
       const float q = smaq_quant<RM, false, TIN, SUB>(v[i], u[i], c, hi, lo);
       const bool valid = FULL || el + i < n_el;
       code[4 * k + i] = valid ? classify(q, hi, lo, wm, wo, esc) : 0u;
@@ -818,24 +818,80 @@ __device__ __forceinline__ float decode_code(uint32_t v, bool is_o, int wm, int 
 // pc / epc / esc_mask: kMaskWords LDS words each, declared once by the kernel (a __shared__ array
 // inside this template is one allocation PER INSTANTIATION: 16 bodies took 37 KB of LDS per
 // workgroup, 4 workgroups per CU)
+// Decode table of narrow codes (both widths <= 8 bits: the 6/8-bit default): every main code
+// (2^wm) and outlier code (2^wo) de-quantised once per block by smaq_dequant into LDS, so an
+// element costs a table read instead of decode + fp64 reciprocal product + de-normalisation
+// (the PMC count of the decoder was 37 VALU per element, VALU-bound). Same arithmetic, same bits.
+constexpr int kLutMax = 512;
+
 template <bool AP, bool SQ, bool FULL, int WM, int WO>
 __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
-                                            int wm_rt, int wo_rt, uint32_t* stage, uint32_t* pc,
-                                            uint32_t* epc, uint32_t* esc_mask) {
+                                            uint64_t dent, int wm_rt, int wo_rt, uint32_t* stage,
+                                            uint32_t* pc, uint32_t* epc, uint32_t* esc_mask,
+                                            float* lut) {
   constexpr bool kWindow = WO > 0 && WO <= 8;  // a lane's 4 codes fit one 32-bit window
+  constexpr bool kLut = kWindow && WM > 0 && WM <= 8;
   const int wm = WM > 0 ? WM : wm_rt, wo = WO > 0 ? WO : wo_rt;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
-  const uint64_t dent = A.dir[b];  // offset | n_out << 38 | n_esc << 51
+  // dent = the block's directory entry: offset | n_out << 38 | n_esc << 51
   const uint32_t* blk = A.data + (dent & ((1ull << 38) - 1ull));
   const uint32_t n_out = (uint32_t)(dent >> 38) & 0x1fffu, n_esc = (uint32_t)(dent >> 51);
   const uint32_t code_words = ((uint32_t)wm * (uint32_t)n_el + (uint32_t)(wo - wm) * n_out + 31u) / 32u;
   const uint32_t img_words = kHdrWords + code_words;
-  // the image and (when they fit) the escape list in one coalesced copy
+  // the image and (when they fit) the escape list in one coalesced copy: 16-B windows
+  // (dwordx4 loads from the image's 16-B line on, every load of a lane issued before its LDS
+  // stores; the last window is clipped to the block with dword loads, so nothing past the stream
+  // is read); word i of the block lands in stage[sh + i]
   const bool esc_lds = img_words + 2u * n_esc <= (uint32_t)kStageWords;
   const uint32_t copy_words = esc_lds ? img_words + 2u * n_esc : img_words;
-  for (uint32_t i = tid; i < copy_words; i += kBlock) stage[i] = blk[i];
+  {
+    const uintptr_t a = (uintptr_t)blk;
+    const uint32_t sh = (uint32_t)((a >> 2) & 3u);
+    const uint4* src = reinterpret_cast<const uint4*>(a - 4u * sh);
+    const uint32_t nvec = (sh + copy_words + 3u) >> 2;
+    constexpr int kR = (kStageWords + 3 + 4 * kBlock - 1) / (4 * kBlock);
+    uint4 w[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const uint32_t v = (uint32_t)tid + (uint32_t)r * kBlock;
+      if (v >= nvec) continue;
+      if (4u * v + 4u <= sh + copy_words) {
+        w[r] = src[v];
+      } else {  // the clipped last window
+        uint32_t q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int idx = (int)(4u * v) + k - (int)sh;
+          q[k] = (idx >= 0 && idx < (int)copy_words) ? blk[idx] : 0u;
+        }
+        w[r] = make_uint4(q[0], q[1], q[2], q[3]);
+      }
+    }
+    if (kLut) {  // while the image is in flight: the block's decode table
+      for (int i = tid; i < (1 << WM) + (1 << WO); i += kBlock) {
+        bool hi = false, lo = false;
+        float q;
+        if (i < (1 << WM)) {
+          q = (float)(((int32_t)((uint32_t)i << (32 - WM))) >> (32 - WM));  // sign-extend
+        } else {
+          const uint32_t v = (uint32_t)(i - (1 << WM));
+          lo = (v >> (WO - 1)) & 1u;
+          hi = !lo;
+          const int mag = (int)(v & ((1u << (WO - 1)) - 1u));
+          q = (float)(lo ? -mag : mag);
+        }
+        lut[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const uint32_t v = (uint32_t)tid + (uint32_t)r * kBlock;
+      if (v < nvec) reinterpret_cast<uint4*>(stage)[v] = w[r];
+    }
+    stage += sh;
+  }
   if (tid < kMaskWords) esc_mask[tid] = 0u;
   __syncthreads();
   const uint32_t* esc = esc_lds ? stage + img_words : blk + img_words;
@@ -880,6 +936,17 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
         v = __builtin_amdgcn_alignbit(bits[(pos >> 5) + 1], bits[pos >> 5], pos & 31u);
       }
       off += is_o ? (uint32_t)wo : (uint32_t)wm;
+      if (kLut) {
+        o[i] = lut[is_o ? (1u << WM) + (v & ((1u << WO) - 1u)) : (v & ((1u << WM) - 1u))];
+        if (__builtin_expect((enib >> i) & 1u, 0)) {  // an escape: its q from the list
+          bool hi, lo;
+          decode_code(v, is_o, wm, wo, hi, lo);
+          const uint32_t sh = (uint32_t)(el0 + i) & 31u;
+          const float q = __uint_as_float(esc[2u * (ebase + __popc(em & ((1u << sh) - 1u))) + 1u]);
+          o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
+        }
+        continue;
+      }
       bool hi, lo;
       float q = decode_code(v, is_o, wm, wo, hi, lo);
       if (__builtin_expect((enib >> i) & 1u, 0)) {  // rank among the block's escapes: O(1)
@@ -900,8 +967,12 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
 }
 
 __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
-  __shared__ uint32_t stage[kStageWords];
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kStageWords + 4];  // + the 16-B shift
   __shared__ uint32_t pc[kMaskWords], epc[kMaskWords], esc_mask[kMaskWords];
+  __shared__ float lut[kLutMax];
+  // the directory entry is requested together with the header (not behind its checks): the
+  // header -> directory -> image chain becomes two round trips
+  const uint64_t dent = A.dir[blockIdx.x];
   const SmqPackedHeader* h = A.hdr;
   if (h->magic != SMQ_PACK_MAGIC || h->version != SMQ_PACK_VERSION || h->n != A.n) return;
   const int wm = h->num_bits_main - 1, wo = h->num_bits_outlier - 1;
@@ -923,8 +994,8 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   const bool w57 = wm == 5 && wo == 7;
 #define SMQ_UNPACK_W(APV, SQV, FULLV)                                                 \
   do {                                                                                \
-    if (w57) unpack_body<APV, SQV, FULLV, 5, 7>(A, c, b, wm, wo, stage, pc, epc, esc_mask);             \
-    else unpack_body<APV, SQV, FULLV, 0, 0>(A, c, b, wm, wo, stage, pc, epc, esc_mask);                 \
+    if (w57) unpack_body<APV, SQV, FULLV, 5, 7>(A, c, b, dent, wm, wo, stage, pc, epc, esc_mask, lut); \
+    else unpack_body<APV, SQV, FULLV, 0, 0>(A, c, b, dent, wm, wo, stage, pc, epc, esc_mask, lut);     \
   } while (0)
 #define SMQ_UNPACK(APV, SQV)                                  \
   do {                                                        \
