@@ -24,10 +24,14 @@ template <int T>
 __device__ __forceinline__ float round_in(float v) {
   if (T == kF16) return __half2float(__float2half_rn(v));
   if (T == kBF16) {
-    // round to nearest even in hardware (v_cvt_pk_bf16_f32, then a 16-bit shift back): two VALU
-    // ops instead of the five of the integer form (u + 0x7fff + lsb) & 0xffff0000 with its NaN
-    // test; NaN stays NaN (its payload's top bits kept, as torch's bf16 rounding keeps them)
-    return __bfloat162float(__float2bfloat16(v));
+    // round to nearest even in hardware, ONE op: v_cvt_pk_bf16_f32 with the value as the HIGH
+    // half and +0 as the low half leaves exactly the rounded fp32 bit pattern (the compiler's
+    // own lowering of __float2bfloat16 adds a shift or permute back; the integer form
+    // (u + 0x7fff + lsb) & 0xffff0000 with its NaN test is five). NaN stays NaN (its payload's top
+    // bits kept, as torch's bf16 rounding keeps them)
+    float r;
+    asm("v_cvt_pk_bf16_f32 %0, 0, %1" : "=v"(r) : "v"(v));
+    return r;
   }
   return v;
 }
