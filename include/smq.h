@@ -282,10 +282,20 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
  * the round-trip output: the S2FP8 parity contract is the E5M2 code of Y (s2fp8.py:45-47).
  * EXACT_POW computes both powers with the accurate (<= 1 ulp) library powf, as the reference's
  * torch.pow does, instead of the hardware exp2(p * log2 x) form (a few ulp; slower ALU, same
- * memory traffic). */
+ * memory traffic).
+ * fp32 precision-32 calls on 16-B-aligned x / y with the statistics computed (stats_in NULL) and no
+ * rand_bits run as ONE launch when the tensor fits a resident grid's registers (n <= 4,194,304:
+ * 256 chunks of <= 4 float4 per lane of 1024 threads); otherwise, or with SPLIT, as two (statistics
+ * partials, then transform). Both give the same bytes: the same chunks and summation order.
+ * TEST_LATE (test aid, single launch only): the upper half of the workgroups start ~500 us late
+ * and the others take their unclaimed chunks after 20 us, exercising the path that keeps the
+ * single launch free of any co-residency assumption. The single launch sets
+ * SmqS2fp8Stats.reserved[0] = 1 if a wait gave up (a poisoned workspace; never in a healthy run). */
 #define SMQ_S2FP8_OUT_Y 1u
 #define SMQ_S2FP8_OUT_T 2u
 #define SMQ_S2FP8_EXACT_POW 4u
+#define SMQ_S2FP8_SPLIT 8u
+#define SMQ_S2FP8_TEST_LATE 16u
 int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int precision,
                            int check_inf, const uint32_t* rand_bits, uint64_t seed,
                            uint64_t offset, uint64_t* offset_counter,

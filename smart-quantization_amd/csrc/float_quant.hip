@@ -14,6 +14,7 @@
 // tensor (+8 B/elem), runs the quantiser and then 3-4 more passes for check_inf; here the random
 // word comes from the counter-based RNG in registers and check_inf is fused.
 #include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -690,6 +691,417 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
   }
 }
 
+// ---- S2FP8 in ONE launch (fp32, precision 32, tensors a resident grid holds in registers) -------
+// The two-launch shape pays a kernel boundary, the apply's launch ramp and its re-read of x between
+// the statistics and the transform; at C4 (12.6 MB) those are most of the call. Here workgroup b
+// loads chunk b (V float4 per lane of 1024 threads) into registers ONCE, publishes the chunk's
+// (sum, max) partial, waits until every chunk's partial is there, reduces them in the two-launch
+// path's fixed order, derives alpha / beta and the inverse-power table, and transforms the
+// registers.
+//
+// Hand-off: cdna_hip_programming.md Guideline 16 R2 — the data is the flag. A partial is three
+// aligned 8-byte granules {epoch, 32-bit word} (low and high half of the fp64 sum, the max), each
+// ONE relaxed agent-scope (sc1) store; one wave of every workgroup re-reads the granules it still
+// misses with sc1 loads until every tag is this call's epoch. epoch = f(generation word, host tag),
+// never 0: the generation is read by every workgroup at its start and advanced by the last
+// workgroup past the wait (an arrival counter tagged with the generation, so the next call finds
+// its own tag, eager or replayed; the add is issued early and looked at only at the end), so graph
+// replays get fresh epochs; the host tag makes an eager call on a workspace some earlier call left
+// mid-way distinct as well.
+//
+// No co-residency assumption: a workgroup that has waited kS2StealTicks computes the partials it
+// still misses itself, from memory (every partial is a pure function of its chunk, so duplicates
+// write the same bytes). So if only some workgroups are resident (another kernel holding CUs, a
+// shared device) they finish the statistics, transform their own chunks and exit, and the rest
+// start later, find the statistics complete and transform theirs. A wait that sees no completion
+// for kS2GiveUpTicks (impossible unless the workspace is corrupted mid-call) stops and flags
+// hdr->reserved[0].
+constexpr int kS2FT = 1024;       // threads per workgroup
+constexpr int kS2FMaxV = 4;       // float4 per lane held in registers (4.2M elements)
+constexpr int kS2FMaxG = 256;     // chunks (= partials; four per lane of the polling wave)
+constexpr int kS2FLds = 88 * 1024;  // dynamic LDS request: one workgroup per CU
+constexpr int kS2FRep = 8;          // granule replicas: replica r is read by the blocks b % 8 == r
+constexpr uint64_t kS2StealTicks = 20000;       // s_memrealtime runs at 100 MHz: 200 us
+constexpr uint64_t kS2GiveUpTicks = 200000000;  // 2 s
+
+struct S2FArgs {
+  const float* x;
+  float* y;
+  int64_t n, nv;
+  int V, G;
+  uint32_t key;
+  uint64_t offset;
+  uint64_t* ctr;  // graph-safe stream position (nullable)
+  SmqS2fp8Stats* hdr;
+  uint32_t* gen;               // generation word
+  unsigned long long* left;    // count of workgroups past the wait, tagged with the generation
+  unsigned long long* gran;    // [kS2FRep][3][kS2FMaxG] granules: sum low word, sum high word, max
+  uint32_t tag;                // host tag of the call (mixed into the epoch)
+  int check_inf;
+  float max_value;
+  int out_mode;
+  int exact_pow;
+  int test_late;     // SMQ_S2FP8_TEST_LATE
+  uint64_t* trace;   // measurement aid (SMQ_S2_TRACE=1 and a workspace with room): 16 words per workgroup
+};
+
+__device__ __forceinline__ void s2f_stamp(const S2FArgs& A, int i) {
+  if (A.trace && threadIdx.x == 0)
+    A.trace[(size_t)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memrealtime();
+}
+
+// (sum, max) of log2|x| over chunk k (lane t: float4 j = k*V*kS2FT + t + u*kS2FT), the two-launch
+// partial kernel's per-lane order; the last chunk adds the n % 4 tail. From the registers v, or
+// (v == nullptr: a missing partial computed by another workgroup) from memory one float4 at a time.
+__device__ __forceinline__ void s2f_lane_sums(const float4* v, const S2FArgs& A, int k, double& s,
+                                              float& m) {
+  const int64_t base = (int64_t)k * A.V * kS2FT + threadIdx.x;
+  s = 0.0;
+  m = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < kS2FMaxV; ++u) {
+    if (u >= A.V) break;
+    const int64_t j = base + (int64_t)u * kS2FT;
+    if (j >= A.nv) continue;
+    const float4 xv = v ? v[u] : reinterpret_cast<const float4*>(A.x)[j];
+    const float l0 = s2_log<kF32>(xv.x), l1 = s2_log<kF32>(xv.y), l2 = s2_log<kF32>(xv.z),
+                l3 = s2_log<kF32>(xv.w);
+    s += ((double)l0 + (double)l1) + ((double)l2 + (double)l3);
+    m = nan_max(nan_max(m, l0), nan_max(l1, nan_max(l2, l3)));
+  }
+  if (k == A.G - 1 && threadIdx.x < (int)(A.n & 3)) {
+    const float l = s2_log<kF32>(A.x[(A.nv << 2) + threadIdx.x]);
+    s += (double)l;
+    m = nan_max(m, l);
+  }
+}
+
+// Workgroup reduce of the lane sums in the partial kernel's order; lanes 0-23 of wave 0 store
+// partial k as three granules in each of the kS2FRep replicas (one sc1 store each; nobody waits for
+// them here). Barriers are LDS-only (lds_barrier) throughout the kernel: no workgroup-internal
+// hand-off goes through global memory, and a __syncthreads would drain the granule stores and the
+// `left` atomic on the critical path. Replicas: every workgroup polls all partials, and 256
+// workgroups sweeping the same 6 KB queue on the few memory channels that hold it (first poll pass
+// 2.1 us); replica b % 8 spreads the readers over 8x the channels.
+__device__ void s2f_publish(double s, float m, const S2FArgs& A, int k, uint32_t epoch,
+                            double* shs, float* shm) {
+  constexpr int W = kS2FT / kWave;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  s = wave_sum(s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o, kWave));
+  if (lane == 0) {
+    shs[wave] = s;
+    shm[wave] = m;
+  }
+  lds_barrier();
+  if (wave == 0 && lane < 3 * kS2FRep) {
+    double S = 0.0;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < W; w += 4) {
+      S += (shs[w] + shs[w + 1]) + (shs[w + 2] + shs[w + 3]);
+      M = nan_max(M, nan_max(nan_max(shm[w], shm[w + 1]), nan_max(shm[w + 2], shm[w + 3])));
+    }
+    const uint64_t sb = __builtin_bit_cast(uint64_t, S);
+    const int r = lane / 3, c = lane - 3 * r;
+    const uint32_t word = c == 0 ? (uint32_t)sb
+                                 : (c == 1 ? (uint32_t)(sb >> 32) : __builtin_bit_cast(uint32_t, M));
+    st_sc1_u64(&A.gran[(r * 3 + c) * kS2FMaxG + k], ((unsigned long long)epoch << 32) | word);
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
+  __shared__ float lut[kS2LutSize];
+  __shared__ double shs[kS2FT / kWave];
+  __shared__ float shm[kS2FT / kWave];
+  __shared__ SmqS2fp8Stats sst;
+  __shared__ int sflag;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t base = (int64_t)b * A.V * kS2FT + threadIdx.x;
+  const uint64_t steal_ticks = A.test_late ? 2000 : kS2StealTicks;
+  s2f_stamp(A, 0);
+  if (A.test_late && 2 * b >= A.G && A.G > 1) {  // test aid: start ~500 us late
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 50000) __builtin_amdgcn_s_sleep(127);
+  }
+  // (then the call's generation and stream snapshot, read before this workgroup can be counted past
+  // the wait)
+  // this chunk into registers (nt: read once): branch-free (indices past the end re-read the last
+  // float4 and are ignored), so every load is in flight before the first wait
+  float4 v[kS2FMaxV];
+  if (A.nv > 0) {
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int64_t j = base + (int64_t)u * kS2FT;
+      v[u] = load_nt(reinterpret_cast<const float4*>(A.x) + (j < A.nv ? j : A.nv - 1));
+    }
+  }
+  const uint32_t gen = ld_sc1_u32(A.gen);
+  const uint64_t ctr_word = ld_sc1_u64(A.ctr ? A.ctr : reinterpret_cast<uint64_t*>(A.left));
+  const uint64_t off0 = A.ctr ? ctr_word : 0ull;  // a select, not a branch: no wait here
+  const uint32_t epoch = mix32(gen ^ mix32(A.tag)) | 1u;
+  const uint64_t off = A.offset + off0;
+  asm volatile("" ::"v"(off));  // materialised here: no later wait on it waits for the `left` atomic
+  // the table's unreachable entries (NaN) need no statistics
+  for (int i = threadIdx.x; i < kS2LutSize; i += kS2FT) lut[i] = __builtin_nanf("");
+  {
+    double s;
+    float m;
+    s2f_lane_sums(v, A, b, s, m);
+    s2f_stamp(A, 1);
+    s2f_publish(s, m, A, b, epoch, shs, shm);
+  }
+  s2f_stamp(A, 2);
+  // wave 0 gathers the G partials (lane l: partials l + 64q) from replica b % 8 until every granule
+  // carries the epoch
+  const unsigned long long* rep = A.gran + (size_t)(b % kS2FRep) * 3 * kS2FMaxG;
+  double ps[4] = {0.0, 0.0, 0.0, 0.0};
+  float pm[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int n_stolen = 0;
+  if (wave == 0) {
+    uint32_t lo[4], hi[4], mx[4];
+    uint32_t have = 0;  // bit 3q + c: granule c of partial l + 64q holds the epoch
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (lane + 64 * q >= A.G) have |= 7u << (3 * q);
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    bool gave_up = false;
+    uint32_t polls = 0;
+    for (;;) {
+      // every granule load of the pass in flight at once, one wait
+      unsigned long long g[4][3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          g[q][c] = lane + 64 * q < A.G ? ld_sc1_u64(&rep[c * kS2FMaxG + lane + 64 * q]) : 0ull;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if ((uint32_t)(g[q][c] >> 32) != epoch || (have & (1u << (3 * q + c)))) continue;
+          have |= 1u << (3 * q + c);
+          const uint32_t w = (uint32_t)g[q][c];
+          if (c == 0) lo[q] = w;
+          else if (c == 1) hi[q] = w;
+          else mx[q] = w;
+        }
+      }
+      const bool all = __all(have == 0xfffu);
+      if (polls == 0) s2f_stamp(A, 11);
+      if (all) break;
+      if ((++polls & 7) != 0) {
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (now - t_start > kS2GiveUpTicks) {
+        if (lane == 0) A.hdr->reserved[0] = 1u;
+        gave_up = true;
+        break;
+      }
+      if (now - t_start > steal_ticks) break;  // compute the missing partials below
+      __builtin_amdgcn_s_sleep(2);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (lane + 64 * q < A.G && (have & (7u << (3 * q))) == (7u << (3 * q))) {
+        ps[q] = __builtin_bit_cast(double, ((uint64_t)hi[q] << 32) | lo[q]);
+        pm[q] = __builtin_bit_cast(float, mx[q]);
+      }
+    }
+    // first missing partial after b (cyclically), or -1 when complete
+    int miss = INT_MAX;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if ((have & (7u << (3 * q))) != (7u << (3 * q))) miss = min(miss, (lane + 64 * q - b + A.G) % A.G);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, kWave));
+    if (lane == 0) sflag = (miss == INT_MAX || gave_up) ? -1 : (miss + b) % A.G;
+  }
+  lds_barrier();
+  // missing partials after the patience ran out: the whole workgroup computes them one by one from
+  // memory; after each, wave 0 re-reads every granule and names the next missing one
+  while (sflag >= 0) {
+    const int k = sflag;
+    lds_barrier();
+    double s;
+    float m;
+    s2f_lane_sums(nullptr, A, k, s, m);
+    s2f_publish(s, m, A, k, epoch, shs, shm);
+    ++n_stolen;
+    if (wave == 0) {  // next missing partial, or -1 when all are present
+      int miss = INT_MAX;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kk = lane + 64 * q;
+        if (kk >= A.G) continue;
+        bool ok = true;
+        uint32_t wd[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const unsigned long long g = ld_sc1_u64(&rep[c * kS2FMaxG + kk]);
+          ok &= (uint32_t)(g >> 32) == epoch;
+          wd[c] = (uint32_t)g;
+        }
+        if (ok) {
+          ps[q] = __builtin_bit_cast(double, ((uint64_t)wd[1] << 32) | wd[0]);
+          pm[q] = __builtin_bit_cast(float, wd[2]);
+        } else {
+          miss = min(miss, (kk - b + A.G) % A.G);
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, kWave));
+      if (lane == 0) sflag = miss == INT_MAX ? -1 : (miss + b) % A.G;
+    }
+    lds_barrier();
+  }
+  s2f_stamp(A, 3);
+  // count this workgroup past the wait now; the returned word is looked at only at the end
+  unsigned long long left_old = 0;
+  if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.left);
+  // wave 0: reduce the partials in the two-launch apply's order (a wave sum over partial indices
+  // l + 64q for each q, the four butterflies interleaved, then (q0 + q1) + (q2 + q3)) and derive;
+  // then threads 0-130 tabulate the inverse powers
+  if (wave == 0) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      double ts[4];
+      float tm[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ts[q] = __shfl_xor(ps[q], o, kWave);
+        tm[q] = __shfl_xor(pm[q], o, kWave);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ps[q] += ts[q];
+        pm[q] = nan_max(pm[q], tm[q]);
+      }
+    }
+    s2f_stamp(A, 8);
+    if (lane == 0) {
+      const double S = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+      const float M = nan_max(nan_max(pm[0], pm[1]), nan_max(pm[2], pm[3]));
+      SmqS2fp8Stats d;
+      s2fp8_finalize<kF32>(S, M, A.n, &d);
+      sst = d;
+      if (b == 0) {
+        SmqS2fp8Stats* h = A.hdr;
+        h->mu = d.mu;
+        h->m = d.m;
+        h->alpha = d.alpha;
+        h->beta = d.beta;
+        h->beta_pow2 = d.beta_pow2;
+        h->inv_beta_pow2 = d.inv_beta_pow2;
+        h->inv_alpha = d.inv_alpha;
+        h->n_used = d.n_used;
+        h->rng_offset = off0;
+      }
+    }
+    s2f_stamp(A, 9);
+  }
+  lds_barrier();
+  if (threadIdx.x < kS2LutArgs) {
+    const float T = s2_lut_arg(threadIdx.x);
+    lut[__builtin_bit_cast(uint32_t, T) >> 21] = powf(T * sst.inv_beta_pow2, sst.inv_alpha);
+  }
+  s2f_stamp(A, 10);
+  lds_barrier();
+  s2f_stamp(A, 4);
+  // the last workgroup past the wait (its `left` add, issued after the gather, has long returned)
+  // advances the generation and the stream and re-arms `left`, before its own stores
+  if (threadIdx.x == 0 && arrive_tagged_finish(A.left, gen, left_old) == (uint32_t)A.G - 1) {
+    st_sc1_u32(A.gen, gen + 1u);
+    if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
+    st_sc1_u64(A.left, (unsigned long long)(gen + 1u) << 32);
+  }
+  const float alpha = sst.alpha, bp2 = sst.beta_pow2, ialpha = sst.inv_alpha;
+  const bool fast = !A.exact_pow && alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f &&
+                    ialpha < INFINITY;
+  const bool last_chunk = b == A.G - 1;
+  if (fast && A.out_mode == 0) {
+    uint32_t T[kS2FMaxV][4];
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int64_t j = base + (int64_t)u * kS2FT;
+      if (j >= A.nv) continue;
+      const uint64_t c = off + ((uint64_t)j << 2);
+      uint32_t r[4];
+      const uint32_t lo = (uint32_t)c;
+      if (__builtin_expect(lo <= 0xfffffffcu, 1)) {
+        const uint32_t hi = (uint32_t)(c >> 32);
+        const uint32_t kk = ((hi << 16) | (hi >> 16)) ^ A.key;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = mix32((lo + (uint32_t)q) ^ kk);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = rng_u32(A.key, c + (uint64_t)q);
+      }
+      T[u][0] = s2_fwd_fast(v[u].x, r[0], alpha, bp2, A.check_inf);
+      T[u][1] = s2_fwd_fast(v[u].y, r[1], alpha, bp2, A.check_inf);
+      T[u][2] = s2_fwd_fast(v[u].z, r[2], alpha, bp2, A.check_inf);
+      T[u][3] = s2_fwd_fast(v[u].w, r[3], alpha, bp2, A.check_inf);
+    }
+    auto sgn = [](float xv) { return (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f); };
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int64_t j = base + (int64_t)u * kS2FT;
+      if (j >= A.nv) continue;
+      float4 o;
+      o.x = lut[T[u][0] >> 21] * sgn(v[u].x);
+      o.y = lut[T[u][1] >> 21] * sgn(v[u].y);
+      o.z = lut[T[u][2] >> 21] * sgn(v[u].z);
+      o.w = lut[T[u][3] >> 21] * sgn(v[u].w);
+      store_stream(reinterpret_cast<float4*>(A.y) + j, o);
+    }
+  } else {
+    auto q1 = [&](float xv, uint64_t e) {
+      const uint32_t r = rng_u32(A.key, off + e);
+      const float T = fast ? s2fp8_fwd<true>(xv, r, alpha, bp2, A.check_inf, A.max_value, A.out_mode)
+                           : s2fp8_fwd<false>(xv, r, alpha, bp2, A.check_inf, A.max_value, A.out_mode);
+      if (A.out_mode) return T;
+      const float sg = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
+      return s2_inverse_lut(T, lut) * sg;
+    };
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int64_t j = base + (int64_t)u * kS2FT;
+      if (j >= A.nv) continue;
+      const uint64_t e = (uint64_t)j << 2;
+      float4 o;
+      o.x = q1(v[u].x, e);
+      o.y = q1(v[u].y, e + 1);
+      o.z = q1(v[u].z, e + 2);
+      o.w = q1(v[u].w, e + 3);
+      store_stream(reinterpret_cast<float4*>(A.y) + j, o);
+    }
+  }
+  if (last_chunk && threadIdx.x < (int)(A.n & 3)) {
+    const int64_t e = (A.nv << 2) + threadIdx.x;
+    const float xv = A.x[e];
+    const uint32_t r = rng_u32(A.key, off + (uint64_t)e);
+    const float T = fast ? s2fp8_fwd<true>(xv, r, alpha, bp2, A.check_inf, A.max_value, A.out_mode)
+                         : s2fp8_fwd<false>(xv, r, alpha, bp2, A.check_inf, A.max_value, A.out_mode);
+    const float sg = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
+    A.y[e] = A.out_mode ? T : s2_inverse_lut(T, lut) * sg;
+  }
+  if (A.trace && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    A.trace[(size_t)blockIdx.x * 16 + 5] = __builtin_amdgcn_s_memrealtime();
+    uint32_t xcc, hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    A.trace[(size_t)blockIdx.x * 16 + 6] = (uint64_t)n_stolen;
+    A.trace[(size_t)blockIdx.x * 16 + 12] = (uint64_t)epoch | ((uint64_t)gen << 32);
+    A.trace[(size_t)blockIdx.x * 16 + 7] = (uint64_t)xcc | ((uint64_t)hwid << 32);
+  }
+}
+
 static inline bool aligned16f(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 static int fq_tile_v() {
@@ -736,7 +1148,20 @@ static float host_max_value(int exp_bits, int man_bits) {
   return qtorch_quant(FLT_MAX, 0u, exp_bits, man_bits, false);
 }
 
-static size_t s2_ws_bytes() { return 128 + sizeof(S2Partial) * (size_t)kS2Partials; }
+// workspace: header, partials, then the single-launch words (own 64-B lines) and granules
+constexpr size_t kS2WsGen = 128 + sizeof(S2Partial) * (size_t)kS2Partials;
+constexpr size_t kS2WsLeft = kS2WsGen + 64;
+constexpr size_t kS2WsGran = kS2WsLeft + 64;
+static size_t s2_ws_bytes() { return kS2WsGran + (size_t)kS2FRep * 3 * 8 * kS2FMaxG; }
+
+// single-launch path (SMQ_S2_FUSED=0 keeps the two launches: measurement knob)
+static bool s2_fused_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("SMQ_S2_FUSED");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
 
 }  // namespace smq
 
@@ -873,7 +1298,8 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
     set_error("s2fp8: precision 32 quantises the tensor as is and needs fp32 input");
     return SMQ_ERR_INVALID;
   }
-  if (flags & ~(SMQ_S2FP8_OUT_Y | SMQ_S2FP8_OUT_T | SMQ_S2FP8_EXACT_POW)) {
+  if (flags & ~(SMQ_S2FP8_OUT_Y | SMQ_S2FP8_OUT_T | SMQ_S2FP8_EXACT_POW | SMQ_S2FP8_SPLIT |
+                SMQ_S2FP8_TEST_LATE)) {
     set_error("s2fp8: unknown flags 0x%x", flags);
     return SMQ_ERR_INVALID;
   }
@@ -897,6 +1323,74 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
   const uintptr_t align = dtype == SMQ_DTYPE_F32 ? 15u : 7u;  // one 4-element group per lane
   const bool xal = ((uintptr_t)x & align) == 0;
   const bool part = stats_in == nullptr;
+  if (part && precision == 32 && !rand_bits && xal && aligned16f(y) && s2_fused_enabled() &&
+      !(flags & SMQ_S2FP8_SPLIT)) {
+    // one launch when a resident grid holds the tensor: <= kS2FMaxG chunks of <= kS2FMaxV float4
+    // per lane (4.2M elements)
+    const int64_t nv = n >> 2;
+    const int64_t per_v = (int64_t)kS2FMaxG * kS2FT;
+    int64_t V = (nv + per_v - 1) / per_v;
+    if (V < 1) V = 1;
+    if (V <= kS2FMaxV) {
+      const int64_t G = nv > 0 ? (nv + V * kS2FT - 1) / (V * kS2FT) : 1;
+      const ArriveTag tg = arrive_tag(ws, st);
+      S2FArgs F;
+      F.x = static_cast<const float*>(x);
+      F.y = static_cast<float*>(y);
+      F.n = n;
+      F.nv = nv;
+      F.V = (int)V;
+      F.G = (int)G;
+      F.key = rng_key(seed);
+      F.offset = offset;
+      F.ctr = offset_counter;
+      F.hdr = hdr;
+      F.gen = reinterpret_cast<uint32_t*>(base + kS2WsGen);
+      F.left = reinterpret_cast<unsigned long long*>(base + kS2WsLeft);
+      F.gran = reinterpret_cast<unsigned long long*>(base + kS2WsGran);
+      F.tag = tg.tag;
+      F.check_inf = check_inf;
+      F.max_value = host_max_value(5, 2);
+      F.out_mode = out_mode;
+      F.exact_pow = (flags & SMQ_S2FP8_EXACT_POW) ? 1 : 0;
+      F.test_late = (flags & SMQ_S2FP8_TEST_LATE) ? 1 : 0;
+      static const bool trace_env = [] {
+        const char* e = getenv("SMQ_S2_TRACE");
+        return e && atoi(e) != 0;
+      }();
+      F.trace = (trace_env && ws_bytes >= s2_ws_bytes() + 128 * (size_t)kS2FMaxG)
+                    ? reinterpret_cast<uint64_t*>(base + s2_ws_bytes())
+                    : nullptr;
+      static const hipError_t lds_attr = hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&s2fp8_fused_kernel<1>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, kS2FLds) != hipSuccess
+          ? hipErrorInvalidValue
+          : (hipFuncSetAttribute(reinterpret_cast<const void*>(&s2fp8_fused_kernel<2>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, kS2FLds) != hipSuccess ||
+             hipFuncSetAttribute(reinterpret_cast<const void*>(&s2fp8_fused_kernel<3>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, kS2FLds) != hipSuccess ||
+             hipFuncSetAttribute(reinterpret_cast<const void*>(&s2fp8_fused_kernel<4>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, kS2FLds) != hipSuccess)
+                ? hipErrorInvalidValue
+                : hipSuccess;
+      if (lds_attr != hipSuccess) {
+        set_error("s2fp8: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed: %s",
+                  hipGetErrorString(lds_attr));
+        return SMQ_ERR_LAUNCH;
+      }
+      static const int lds_bytes = [] {  // measurement knob SMQ_S2_LDS_KB (default: 1 per CU)
+        const char* e = getenv("SMQ_S2_LDS_KB");
+        const int v = e ? atoi(e) * 1024 : kS2FLds;
+        return (v >= 0 && v <= kS2FLds) ? v : kS2FLds;
+      }();
+      const dim3 grid((unsigned)G), block(kS2FT);
+      if (V == 1) hipLaunchKernelGGL(s2fp8_fused_kernel<1>, grid, block, lds_bytes, st, F);
+      else if (V == 2) hipLaunchKernelGGL(s2fp8_fused_kernel<2>, grid, block, lds_bytes, st, F);
+      else if (V == 3) hipLaunchKernelGGL(s2fp8_fused_kernel<3>, grid, block, lds_bytes, st, F);
+      else hipLaunchKernelGGL(s2fp8_fused_kernel<4>, grid, block, lds_bytes, st, F);
+      return check_launch("s2fp8_fused_kernel");
+    }
+  }
   int n_partials = 0;
   if (!part) {
     if (dtype == SMQ_DTYPE_F32) hipLaunchKernelGGL(s2fp8_derive_kernel<kF32>, dim3(1), dim3(64), 0, st, stats_in, hdr, offset_counter, (uint64_t)n);

@@ -138,6 +138,12 @@ __device__ __forceinline__ uint32_t ld_sc1_u32(const void* p) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global loads, stores and atomics (__syncthreads' workgroup fence also drains those).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Thread 0 has stored this workgroup's partial with st_sc1_*; count the arrival. Returns the
 // pre-increment value in every thread (== expected - 1 in the last workgroup).
 __device__ __forceinline__ uint32_t block_arrive(uint32_t* counter, uint32_t* lds_slot) {
@@ -149,7 +155,7 @@ __device__ __forceinline__ uint32_t block_arrive(uint32_t* counter, uint32_t* ld
   return *lds_slot;
 }
 
-// Tagged arrival counter: one 64-bit word, call tag in the high half, arrivals in the low half.
+// Tagged arrival counter (one lane): one 64-bit word, call tag in the high half, arrivals in the low half.
 // The finalising workgroup leaves (next_tag, 0) behind, so the next call on the workspace (whose
 // tag the host predicted, arrive_tag() in smaq.hip) finds its own tag and takes the single atomic
 // add. A word with another tag (an unzeroed workspace, a call that never finished, another
@@ -157,28 +163,43 @@ __device__ __forceinline__ uint32_t block_arrive(uint32_t* counter, uint32_t* ld
 // (tag, 1) — or joins a tag another stale arrival installed first — by compare-and-swap. The add
 // that met the stale word only changed the stale word, which the install overwrites. Returns the
 // number of earlier arrivals of this call in every thread (== expected - 1 in the last one).
+__device__ __forceinline__ uint32_t arrive_tagged_finish(unsigned long long* ctr, uint32_t tag,
+                                                         unsigned long long old) {
+  if ((uint32_t)(old >> 32) == tag) return (uint32_t)old;
+  // The add met a stale word. One arrival installs (tag, 1); the others then add to the installed
+  // word (a bounded number of atomics each: a CAS loop per arrival would cost O(arrivals^2) when
+  // every add of a call met the stale word, e.g. adds issued long before they are looked at).
+  for (;;) {
+    unsigned long long cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(cur >> 32) != tag) {
+      if (__hip_atomic_compare_exchange_strong(ctr, &cur, ((unsigned long long)tag << 32) | 1ull,
+                                               __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        return 0u;
+      if ((uint32_t)(cur >> 32) != tag) continue;  // another stale value: look again
+    }
+    old = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(old >> 32) == tag) return (uint32_t)old;
+  }
+}
+
+// arrive_tagged in two halves: the add (issue it early) and, where the count is needed, the check
+// of the word it returned (arrive_tagged_finish).
+__device__ __forceinline__ unsigned long long arrive_tagged_issue(unsigned long long* ctr) {
+  return __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t arrive_tagged(unsigned long long* ctr, uint32_t tag) {
+  return arrive_tagged_finish(ctr, tag, arrive_tagged_issue(ctr));
+}
+
+// The same for a workgroup whose thread 0 stored a partial with st_sc1_*: drain, arrive, and hand
+// the count to every thread.
 __device__ __forceinline__ uint32_t block_arrive_tagged(unsigned long long* ctr, uint32_t tag,
                                                         uint32_t* lds_slot) {
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 partial stores have landed
-    unsigned long long old =
-        __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t before;
-    if ((uint32_t)(old >> 32) == tag) {
-      before = (uint32_t)old;
-    } else {
-      old = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (;;) {
-        const bool mine = (uint32_t)(old >> 32) == tag;
-        const unsigned long long want = mine ? old + 1ull : (((unsigned long long)tag << 32) | 1ull);
-        if (__hip_atomic_compare_exchange_strong(ctr, &old, want, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-          before = (uint32_t)want - 1u;
-          break;
-        }
-      }
-    }
-    *lds_slot = before;
+    *lds_slot = arrive_tagged(ctr, tag);
   }
   __syncthreads();
   return *lds_slot;

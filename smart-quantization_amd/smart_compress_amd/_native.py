@@ -32,6 +32,8 @@ SMQ_STATS_SAMPLED_DEVICE = 3
 SMQ_S2FP8_OUT_Y = 1
 SMQ_S2FP8_OUT_T = 2
 SMQ_S2FP8_EXACT_POW = 4
+SMQ_S2FP8_SPLIT = 8
+SMQ_S2FP8_TEST_LATE = 16
 SMQ_PACK_TICKETED = 1
 SMQ_PACK_SINGLE = 2
 SMQ_DTYPE_F32 = 0

@@ -97,13 +97,14 @@ def float_quant(x, exp_bits, man_bits, rounding=N.SMQ_ROUND_STOCHASTIC, check_in
 
 
 def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None, precision=32,
-          counter=None, flags=0):
+          counter=None, flags=0, ws=None):
     """smq_s2fp8_roundtrip_ex on a device tensor of any supported dtype (precision 16: fp16 in ->
     fp16 out, fp32 / bf16 in -> fp32 out); flags = SMQ_S2FP8_* (OUT_Y / OUT_T: y holds Y or T)."""
     n = x.numel()
     half_out = precision == 16 and x.dtype == torch.float16
     y = torch.empty(x.shape, dtype=torch.float16 if half_out else torch.float32, device=x.device)
-    ws = torch.zeros(N.lib().smq_s2fp8_workspace_bytes(n), dtype=torch.uint8, device=x.device)
+    if ws is None:
+        ws = torch.zeros(N.lib().smq_s2fp8_workspace_bytes(n), dtype=torch.uint8, device=x.device)
     st_in = None
     if mu_m is not None:
         s = N.SmqS2fp8Stats()
@@ -118,7 +119,8 @@ def s2fp8(x, check_inf=True, rand_bits=None, seed=0, offset=0, mu_m=None, precis
         stream()), "s2fp8")
     hdr = ws[:32].cpu().numpy().view(np.float32)
     stats = dict(mu=hdr[0], m=hdr[1], alpha=hdr[2], beta=hdr[3], beta_pow2=hdr[4],
-                 inv_beta_pow2=hdr[5], inv_alpha=hdr[6])
+                 inv_beta_pow2=hdr[5], inv_alpha=hdr[6],
+                 gave_up=int(ws[40:44].cpu().numpy().view(np.uint32)[0]))
     return y, stats
 
 

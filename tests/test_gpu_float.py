@@ -430,3 +430,68 @@ def test_s2fp8_hot_path_equals_generic(n, shift, check_inf):
     assert st["alpha"] == st2["alpha"] and st["beta_pow2"] == st2["beta_pow2"]
     assert same_f32(y_hot.cpu().numpy(), y_gen.cpu().numpy()), n_diff_f32(y_hot.cpu().numpy(),
                                                                         y_gen.cpu().numpy())
+
+
+# ---- S2FP8 in one launch (fp32, precision 32, n <= 4,194,304) -----------------------------------
+def _s2_data(n, seed):
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(n, generator=gen, device="cuda") * torch.exp(
+        torch.randn(n, generator=gen, device="cuda"))
+    x[::11] = 0.0
+    x[5::13] = 1e-40
+    return x
+
+
+@pytest.mark.parametrize("n", [1, 5, 4096 * 7 + 2, 3 * 2**20, 3 * 2**20 + 3, 4 * 2**20,
+                               4 * 2**20 + 4])
+@pytest.mark.parametrize("mode", ["fast", "exact", "out_t"])
+def test_s2fp8_single_launch_equals_split(n, mode):
+    """The single launch (statistics partials handed over inside the launch, transform from
+    registers) and the two-launch path (SMQ_S2FP8_SPLIT) use the same chunks and summation order:
+    the same statistics and the same bytes, up to the largest single-launch size (4M) and past it."""
+    g = _g()
+    x = _s2_data(n, n)
+    f = {"fast": 0, "exact": g.N.SMQ_S2FP8_EXACT_POW, "out_t": g.N.SMQ_S2FP8_OUT_T}[mode]
+    y1, st1 = g.s2fp8(x, seed=5, offset=9, flags=f)
+    y2, st2 = g.s2fp8(x, seed=5, offset=9, flags=f | g.N.SMQ_S2FP8_SPLIT)
+    for k in ("mu", "m", "alpha", "beta", "beta_pow2"):
+        assert st1[k].tobytes() == st2[k].tobytes(), k
+    assert st1["gave_up"] == 0
+    a, b = y1.cpu().numpy(), y2.cpu().numpy()
+    assert same_f32(a, b), n_diff_f32(a, b)
+
+
+@pytest.mark.parametrize("n", [3 * 2**20, 1000003, 64 * 1024 + 1])
+def test_s2fp8_single_launch_late_workgroups(n):
+    """SMQ_S2FP8_TEST_LATE: the upper half of the workgroups start ~500 us late, the others take
+    their chunks' partials after 20 us, transform their own chunks and exit; the late ones find
+    the statistics complete. Same bytes as the normal launch, no wait gave up, and the call words
+    are re-armed for the next call (a normal call on the same workspace right after agrees too)."""
+    g = _g()
+    x = _s2_data(n, 7 + n)
+    ws = torch.zeros(g.N.lib().smq_s2fp8_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    ref, st_ref = g.s2fp8(x, seed=2, offset=4)
+    for flags in (g.N.SMQ_S2FP8_TEST_LATE, 0, g.N.SMQ_S2FP8_TEST_LATE):
+        y, st = g.s2fp8(x, seed=2, offset=4, flags=flags, ws=ws)
+        assert st["gave_up"] == 0 and st["alpha"] == st_ref["alpha"]
+        assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), flags
+
+
+def test_s2fp8_single_launch_poisoned_workspace():
+    """A workspace of random bytes, and call words overwritten with stale values between calls
+    (a call that never finished): every call still equals the clean one."""
+    g = _g()
+    n = 3 * 2**20 + 1
+    x = _s2_data(n, 99)
+    ref, _ = g.s2fp8(x, seed=6, offset=1)
+    nb = g.N.lib().smq_s2fp8_workspace_bytes(n)
+    ws = torch.randint(0, 256, (nb,), dtype=torch.uint8, device="cuda")
+    ws[:64] = 0  # the header (its reserved[0] is the sticky gave-up flag read below)
+    done = 128 + 16 * 256
+    for i in range(4):
+        if i:
+            junk = torch.randint(0, 256, (nb - done,), dtype=torch.uint8, device="cuda")
+            ws[done:] = junk
+        y, st = g.s2fp8(x, seed=6, offset=1, ws=ws)
+        assert st["gave_up"] == 0
+        assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), i

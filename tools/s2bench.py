@@ -1,5 +1,6 @@
 """Measurement aid for C4 (S2FP8 [32,128,768], 48 rotating buffers): device time per call of
-  full      smq_s2fp8_roundtrip (partials + apply)
+  full      smq_s2fp8_roundtrip (the single launch for fp32 up to 8M elements)
+  split     the same forced to two launches (SMQ_S2FP8_SPLIT: partials + apply)
   injected  the same with (mu, m) given: a 1-thread derive launch + the apply without the reduce
   fp8       smq_float_quant E5M2 (one read+write launch over the same bytes: the pass floor)
   copy      torch copy_ of the same bytes
@@ -21,8 +22,8 @@ from smart_compress_amd import _native as N  # noqa: E402
 
 def main():
     lib = N.lib()
-    nbuf = 48
-    shape = (32, 128, 768)
+    nbuf = int(os.environ.get("S2B_NBUF", "48"))
+    shape = (int(os.environ.get("S2B_N", str(32 * 128 * 768))),)
     n = int(np.prod(shape))
     xs = [torch.randn(shape, device="cuda") for _ in range(nbuf)]
     ys = [torch.empty_like(x) for x in xs]
@@ -39,6 +40,11 @@ def main():
                                            1, i * n, None, None, ws.data_ptr(), ws.numel(), flags,
                                            st), "s2")
 
+    def split(i):
+        N.check(lib.smq_s2fp8_roundtrip_ex(xs[i].data_ptr(), 0, ys[i].data_ptr(), n, 32, 1, None,
+                                           1, i * n, None, None, ws.data_ptr(), ws.numel(),
+                                           flags | N.SMQ_S2FP8_SPLIT, st), "s2s")
+
     def injected(i):
         N.check(lib.smq_s2fp8_roundtrip_ex(xs[i].data_ptr(), 0, ys[i].data_ptr(), n, 32, 1, None,
                                            1, i * n, None, st_in.data_ptr(), ws.data_ptr(),
@@ -51,7 +57,7 @@ def main():
     def copy(i):
         ys[i].copy_(xs[i])
 
-    variants = dict(full=full, injected=injected, fp8=fp8, copy=copy)
+    variants = dict(full=full, split=split, injected=injected, fp8=fp8, copy=copy)
     res = {k: [] for k in variants}
     for _ in range(3):
         for fn in variants.values():
