@@ -27,6 +27,7 @@ SHORT = {
     "smaq_multi_apply_kernel": "smaq_multi_apply_kernel",
     "float_quant_kernel": "float_quant_kernel",
     "s2fp8_partial_kernel": "s2fp8_partial_kernel",
+    "s2fp8_fused_kernel": "s2fp8_fused_kernel",
     "s2fp8_apply_kernel": "s2fp8_apply_kernel",
     "smaq_pack_kernel": "smaq_pack_kernel",
     "smaq_unpack_kernel": "smaq_unpack_kernel",
@@ -89,7 +90,7 @@ def main():
     with open(os.path.join(REPO, "profiles", f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     main_k = {"smaq": "smaq_apply_kernel", "smaq_sampled": "smaq_apply_kernel",
-              "fp8": "float_quant_kernel", "s2fp8": "s2fp8_apply_kernel",
+              "fp8": "float_quant_kernel", "s2fp8": "s2fp8_fused_kernel",
               "multi": "smaq_multi_apply_kernel", "packed": "smaq_unpack_kernel"}[config]
     if main_k in kernels and "hbm_bytes_per_launch" in kernels[main_k]:
         with open(os.path.join(REPO, "profiles", f"traffic_{config}.json"), "w") as f:
