@@ -5,10 +5,13 @@ alpha = 15 / (m - mu), beta = -alpha * mu; Y = |x|^alpha * 2^beta; T = E5M2 stoc
 float_quantize(Y) (+ check_inf); y = (T * 2^-beta)^(1/alpha) * sign(x). Logged as 8 bits per element
 plus 64 bits of per-tensor overhead (s2fp8.py:29).
 
-On MI355X this is ``smq_s2fp8_roundtrip``: a log2-domain statistics launch (one (sum, max) partial
-per workgroup) and one fused launch in which every workgroup reduces the partials in a fixed order,
-derives alpha, beta, evaluates the 131 possible inverse powers into an LDS table, and transforms,
-quantises and inverts its tile.
+On MI355X this is ``smq_s2fp8_roundtrip``. fp32 tensors up to 4M elements run as ONE launch: every
+workgroup holds its chunk in registers, publishes the chunk's log2-domain (sum, max) partial,
+gathers all partials, reduces them in a fixed order, derives alpha, beta, evaluates the 131
+possible inverse powers into an LDS table, and transforms, quantises and inverts its registers.
+Larger tensors (and precision 16) take a statistics launch (one partial per workgroup) and an
+apply launch that does the same reduce / derive / table per workgroup; both shapes give the same
+bytes.
 
 Precision 16 (quantization.py:187-204's half branch) keeps the reference's dtypes: fp16 / bf16
 inputs run the statistics and the forward transform in their own type, float_quantize returns half,
