@@ -578,9 +578,19 @@ def run_s2fp8(args, world, rank, device):
     finally:
         codec.graph_safe(False)
     total = sum_over_ranks(12.0 * n * args.steps, world, device)
-    # roofline of the single launch (s2fp8_fused_kernel): it reads x once and writes y once, 8 B/elem
-    # of algorithmic traffic (the metric's 12 B/elem convention counts the statistics read too)
-    gbps = 8.0 * n / (g_dev_ms * 1e-3) / 1e9
+    # S2FP8 algorithmic bytes are 12 B/elem (log2 statistics read + read + write) over
+    # all launches of the call; the single launch (s2fp8_fused_kernel) moves 8 of them (x is read
+    # once into registers), so HBM traffic / alg bytes = 0.68
+    gbps = 12.0 * n / (g_dev_ms * 1e-3) / 1e9
+    # in-MALL variant ("in-MALL vs rotated"): one input buffer, eager calls
+    xs1 = xs[:1]
+    it1 = [0]
+
+    def step1():
+        codec(xs1[0])
+        it1[0] += 1
+
+    t1 = time_steps(step1, args.steps, args.warmup, world, device)
     return {"metric": "S2FP8 round-trip GB/s, [32,128,768] fp32", "value": round(total / elapsed / 1e9, 2),
             "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
@@ -592,11 +602,12 @@ def run_s2fp8(args, world, rank, device):
             "variants": {"eager": {"ms_per_step": round(elapsed / args.steps * 1e3, 4),
                                    "device_ms_per_step": round(eager_dev_ms, 5)},
                          "graph": {"ms_per_step": round(g_ms, 5),
-                                   "device_ms_per_step": round(g_dev_ms, 5)}},
+                                   "device_ms_per_step": round(g_dev_ms, 5)},
+                         "in_mall_1buf": {"ms_per_step": round(t1 / args.steps * 1e3, 5)}},
             # one call = one launch, timed over graph replays (no host gaps)
             "roofline": {"bound": "hbm", "kernel": "s2fp8_fused_kernel",
                          "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(gbps / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": int(8 * n),
+                         "frac": round(gbps / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": int(12 * n),
                          "avg_launch_ms": round(g_dev_ms, 5), "traffic": traffic_from_profile("s2fp8", True)}}
 
 
