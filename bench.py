@@ -13,8 +13,8 @@ its own tensors and seed ("weak" scaling). `bench.py --gpus N` launches the N ra
 one rank. Ranks meet in a CPU (gloo) process group that only carries the start/stop barriers and
 the reduction of the timings: no RCCL. Rank 0 prints the one JSON line with every rank's time.
 
-Other configs (--config smaq_sampled | fp8 | s2fp8 | multi | packed | autograd) are measurement
-aids (BASELINE configs 3-5 and SURVEY 8f), not the line the driver records; each carries its own
+Other configs (--config smaq_sampled | fp8 | s2fp8 | multi | packed | autograd | smaq_cpu) are measurement
+aids (BASELINE configs 1 and 3-5), not the line the driver records; each carries its own
 `roofline` and, at N=1, a `cpu_baseline`.
 
 roofline: the dominant kernel is smaq_apply_kernel (8 B/elem algorithmic); its average duration is
@@ -388,6 +388,7 @@ def cpu_baseline_multi(args):
 
 CPU_BASELINES = {
     "smaq": lambda a: cpu_baseline_smaq(a),
+    "smaq_cpu": lambda a: cpu_baseline_smaq(a),
     "smaq_sampled": lambda a: cpu_baseline_smaq(a, sampled=True),
     "fp8": lambda a: cpu_baseline_float(a, "fp8"),
     "s2fp8": lambda a: cpu_baseline_float(a, "s2fp8"),
@@ -865,6 +866,41 @@ def run_autograd(args, world, rank, device):
             "variants": results}
 
 
+def run_smaq_cpu(args, world, rank, device):
+    """BASELINE config 1 on the library's own CPU path: SmartFP.__call__ on a 1,048,576-element fp32
+    CPU tensor (defaults: 6/8 bits, full statistics, stochastic rounding) -> smq_cpu_smaq_roundtrip,
+    median of >= 30 calls after warm-up, on this job's CPU share (torch intra-op threads). Also a
+    16M-element tensor for throughput. The reference on the container's 8 cores: 6.56 ms = 1.92 GB/s
+    at 1M; its torch op sequence is timed in the same run as cpu_baseline."""
+    from smart_compress_amd.compress.smart import SmartFP
+
+    threads = _cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        codec = SmartFP(smaq_hparams())
+        torch.manual_seed(0)
+        x1 = torch.randn(1 << 20)
+        _, _, t1 = _time_reps(lambda: codec(x1), 0.0, min_reps=max(30, args.steps))
+        n16 = args.elements or (1 << 24)
+        x16 = torch.randn(n16, generator=torch.Generator().manual_seed(1))
+        reps, t_tot, _ = _time_reps(lambda: codec(x16), min(args.cpu_budget, 5.0))
+    finally:
+        torch.set_num_threads(prev)
+    ms = float(np.median(t1)) * 1e3
+    gbps = 12.0 * (1 << 20) / (ms * 1e-3) / 1e9
+    return {"metric": "SmaQ 6/8-bit quant+dequant round-trip GB/s on CPU, 1M fp32 (BASELINE config 1)",
+            "value": round(gbps, 3), "unit": "GB/s", "n_gpus": 0, "steps": len(t1), "warmup": 1,
+            "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "none",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "smaq_6_8_roundtrip_1M_fp32_cpu", "elements": 1 << 20,
+                       "threads": threads, "path": "smq_cpu_smaq_roundtrip (libsmq host code)"},
+            "vs_reference_in_container": {"reference_ms": 6.56, "reference_threads": 8,
+                                          "speedup": round(6.56 / ms, 2)},
+            "large": {"elements": n16, "gbps": round(12.0 * n16 * reps / t_tot / 1e9, 3),
+                      "reps": reps}}
+
+
 def run_mock(args, world, rank, device):
     """Device-free step (CPU tests of the N-rank launcher, tests/test_dist_gloo.py): a fixed amount
     of numpy work per step on each rank's own seeded data; reports what each rank saw."""
@@ -896,7 +932,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="smaq",
                     choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi", "packed",
-                             "autograd", "mock"])
+                             "autograd", "smaq_cpu", "mock"])
     ap.add_argument("--elements", type=int, default=0, help="override elements (smaq configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
@@ -907,10 +943,11 @@ def main():
         # no launcher: this process starts the ranks and relays rank 0's line
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = dist_setup()
-    device = torch.device("cuda", local) if args.config != "mock" else torch.device("cpu")
+    on_host = args.config in ("mock", "smaq_cpu")
+    device = torch.device("cuda", local) if not on_host else torch.device("cpu")
     runner = {"smaq": run_smaq, "smaq_sampled": run_smaq, "fp8": run_fp8, "s2fp8": run_s2fp8,
               "multi": run_multi, "packed": run_packed, "autograd": run_autograd,
-              "mock": run_mock}[args.config]
+              "smaq_cpu": run_smaq_cpu, "mock": run_mock}[args.config]
     res = runner(args, world, rank, device)
     if world > 1:
         res.setdefault("rank_ms_per_step", HOST.get("rank_ms_per_step"))

@@ -302,6 +302,35 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
                            const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
                            uint32_t flags, void* stream);
 
+/* ---- CPU tensors ----
+ * The codecs on host pointers, for tensors that live on the CPU (the reference's plugins run on
+ * any device; BASELINE config 1 is a CPU run). Same argument meaning as the device entry points,
+ * minus the stream; n_threads <= 0 uses the library's pool (SMQ_CPU_THREADS, else
+ * OMP_NUM_THREADS, else all hardware threads). Each element uses the device path's arithmetic, so
+ * for the same statistics and random stream the SmaQ and float_quant outputs are the device's
+ * bytes; statistics are fp64 sums in a fixed order independent of the thread count. S2FP8 uses the
+ * C library's powf / log2f (the device's SMQ_S2FP8_EXACT_POW semantics). */
+/* Number of threads of the library's CPU pool. */
+int smq_cpu_threads(void);
+/* SmaQ round trip; ws: host buffer of smq_smaq_workspace_bytes(n) bytes that receives the
+ * SmqSmaqStats header, the outlier count (slot 0 of SMQ_WS_OUTLIER_SLOTS, when
+ * params.count_outliers) and the drawn indices (SMQ_STATS_SAMPLED_DEVICE: the same Floyd draw as the
+ * device, any k <= SMQ_MAX_DEVICE_SAMPLES). params.bn_gamma / bn_beta / offset_counter and
+ * uniforms / stats_in are host pointers here. */
+int smq_cpu_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                           const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
+                           size_t ws_bytes, int n_threads);
+/* smq_float_quant on host pointers (no offset_counter). */
+int smq_cpu_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t n,
+                        int exp_bits, int man_bits, int rounding, int check_inf,
+                        const uint32_t* rand_bits, uint64_t seed, uint64_t offset, int n_threads);
+/* smq_s2fp8_roundtrip_ex on host pointers; ws (optional, >= 64 bytes) receives SmqS2fp8Stats.
+ * flags: OUT_Y / OUT_T as on the device; EXACT_POW and SPLIT are accepted and change nothing. */
+int smq_cpu_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precision,
+                            int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                            uint64_t offset, const SmqS2fp8Stats* stats_in, void* ws,
+                            size_t ws_bytes, uint32_t flags, int n_threads);
+
 /* ---- host reference helpers shared with the oracle (pure functions, no GPU) ---- */
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
 

@@ -1,0 +1,742 @@
+// cpu_codecs.hip — the same codecs on CPU tensors (host pointers), for callers whose tensors live on
+// the host: the reference's plugins run on whatever device the tensor is on (smart.py:110-190,
+// quantization.py:187-204, s2fp8.py:27-48 are plain torch ops), and BASELINE config 1 is a CPU
+// run. Host code only (this translation unit has no kernels); it is built with the rest of
+// libsmq.so so that it shares the element arithmetic's helpers (counter RNG, Floyd draw, qtorch
+// bit code) with the device path.
+//
+// Every element is computed with the device path's arithmetic in the same order, so for the same
+// statistics and random stream the bytes are the same as the GPU's (SmaQ, float_quantize):
+//   * z = (x - mean) / std_clamped and q / range as IEEE fp32 divisions — the device's
+//     RN32(RN64(a * RN64(1/b))) equals them (smaq_elem.h div_by_const, proven exact);
+//   * SR draws u = rng_u32(key, offset + i) >> 8, t = fma(u, -2^-24, fr) + 0.5 (one rounding);
+//   * fp16 / bf16 inputs follow the torch type flow with the same round-to-nearest-even steps.
+// Statistics are fp64 sums in a fixed order (per 64K-element task, combined in task order: the
+// result does not depend on the thread count); the device sums in another fixed order, so mean /
+// std can differ from the GPU's in the last fp32 bit in rare cases (both are within 1 ulp of the
+// exact value, tests/test_cpu_codecs.py).
+// S2FP8 powers use the C library's powf / log2f (the device's SMQ_S2FP8_EXACT_POW semantics).
+//
+// Parallelism: a process-wide pool of std::threads (no OpenMP runtime next to torch's); the
+// calling thread takes part. Work is split into fixed 64K-element tasks.
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "qtorch.h"
+#include "smaq_elem.h"
+#include "smaq_host.h"
+#include "smq_common.h"
+
+namespace smq {
+namespace cpu {
+
+constexpr int64_t kTask = 1 << 16;  // elements per task
+
+// ---- thread pool ----------------------------------------------------------------------------------
+class Pool {
+ public:
+  explicit Pool(int n_workers) {
+    for (int i = 0; i < n_workers; ++i) workers_.emplace_back([this, i] { loop(i); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+  int size() const { return (int)workers_.size() + 1; }
+
+  // fn(task) for task in [0, n_tasks) on up to n_threads threads (the caller included)
+  void run(int64_t n_tasks, int n_threads, const std::function<void(int64_t)>& fn) {
+    std::lock_guard<std::mutex> one_job(job_mu_);
+    int helpers = std::min<int64_t>((int64_t)std::max(n_threads, 1) - 1, n_tasks - 1);
+    helpers = std::max(0, std::min(helpers, (int)workers_.size()));
+    if (helpers == 0) {
+      for (int64_t t = 0; t < n_tasks; ++t) fn(t);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_tasks_ = n_tasks;
+      next_.store(0, std::memory_order_relaxed);
+      active_ = helpers;
+      pending_ = helpers;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const int64_t t = next_.fetch_add(1, std::memory_order_relaxed);
+      if (t >= n_tasks_) return;
+      (*fn_)(t);
+    }
+  }
+  void loop(int idx) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        if (idx >= active_) continue;
+      }
+      work();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+
+  std::vector<std::thread> workers_;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int64_t)>* fn_ = nullptr;
+  int64_t n_tasks_ = 0;
+  std::atomic<int64_t> next_{0};
+  int active_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+static int default_threads() {
+  for (const char* name : {"SMQ_CPU_THREADS", "OMP_NUM_THREADS"}) {
+    const char* e = getenv(name);
+    if (e && atoi(e) > 0) return std::min(atoi(e), 256);
+  }
+  const unsigned hc = std::thread::hardware_concurrency();
+  return hc ? (int)std::min(hc, 256u) : 1;
+}
+
+static Pool& pool() {
+  static Pool* p = new Pool(default_threads() - 1);  // never destroyed: no join at exit
+  return *p;
+}
+
+static int threads_for(int n_threads) { return n_threads > 0 ? n_threads : pool().size(); }
+
+template <class F>
+static void parallel_tasks(int64_t n, int n_threads, F&& f) {
+  const int64_t tasks = (n + kTask - 1) / kTask;
+  const std::function<void(int64_t)> fn = [&](int64_t t) {
+    const int64_t i0 = t * kTask;
+    f(t, i0, std::min(n, i0 + kTask));
+  };
+  pool().run(tasks, threads_for(n_threads), fn);
+}
+
+// ---- element types ------------------------------------------------------------------------------
+static inline float h2f(uint16_t h) {  // fp16 -> fp32 (exact)
+  const uint32_t s = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  if (e == 0x1fu) return u2f(s | 0x7f800000u | (m << 13));
+  if (e == 0) return m ? (s ? -1.0f : 1.0f) * (float)m * 0x1p-24f : u2f(s);
+  return u2f(s | ((e + 112u) << 23) | (m << 13));
+}
+
+static inline uint16_t f2h(float f) {  // fp32 -> fp16, round to nearest even
+  const uint32_t x = f2u(f), s = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(s | 0x7c00u | (ax > 0x7f800000u ? (0x200u | ((ax >> 13) & 0x3ffu)) : 0u));
+  if (ax >= 0x477ff000u) return (uint16_t)(s | 0x7c00u);  // rounds to inf
+  if (ax < 0x38800000u) {                                   // fp16 subnormal (or zero)
+    const float t = u2f(ax) * 0x1p24f;                      // exact; < 2^10
+    return (uint16_t)(s | (uint32_t)rintf(t));              // RN-even (0x400 = smallest normal)
+  }
+  const uint32_t r = ax - 0x38000000u;  // rebias 127 -> 15
+  return (uint16_t)(s | ((r + 0x0fffu + ((r >> 13) & 1u)) >> 13));
+}
+
+static inline float bf2f(uint16_t h) { return u2f((uint32_t)h << 16); }
+
+static inline float round_bf16(float v) {  // RN-even to bf16, as an fp32 value
+  const uint32_t u = f2u(v);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return u2f((u | 0x00400000u) & 0xffff0000u);
+  return u2f((u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u);
+}
+
+template <int T>
+static inline float rin(float v) {  // round_in<T> on the host
+  if (T == kF16) return h2f(f2h(v));
+  if (T == kBF16) return round_bf16(v);
+  return v;
+}
+
+template <int T>
+static inline float ld(const void* p, int64_t i) {
+  if (T == kF32) return static_cast<const float*>(p)[i];
+  const uint16_t h = static_cast<const uint16_t*>(p)[i];
+  return T == kF16 ? h2f(h) : bf2f(h);
+}
+
+static inline float hash_u24(uint32_t key, uint64_t ctr) {  // rng_hu: h >> 8 as a float
+  return (float)(rng_u32(key, ctr) >> 8);
+}
+
+// ---- SmaQ statistics ----------------------------------------------------------------------------
+struct Moments {
+  double s1 = 0.0, s2 = 0.0;
+  float mn = INFINITY, mx = -INFINITY;
+};
+
+// Shifted fp64 sums of one task: 8 interleaved chains (element i of the task in chain i % 8),
+// combined in a fixed order.
+template <int T>
+static Moments task_moments(const void* x, int64_t i0, int64_t i1, double shift) {
+  double a1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mn[8], mx[8];
+  for (int j = 0; j < 8; ++j) {
+    mn[j] = INFINITY;
+    mx[j] = -INFINITY;
+  }
+  int64_t i = i0;
+  for (; i + 8 <= i1; i += 8) {
+    for (int j = 0; j < 8; ++j) {
+      const float v = ld<T>(x, i + j);
+      const double d = (double)v - shift;
+      a1[j] += d;
+      a2[j] = fma(d, d, a2[j]);
+      mn[j] = fminf(mn[j], v);
+      mx[j] = fmaxf(mx[j], v);
+    }
+  }
+  for (int j = 0; i < i1; ++i, ++j) {
+    const float v = ld<T>(x, i);
+    const double d = (double)v - shift;
+    a1[j] += d;
+    a2[j] = fma(d, d, a2[j]);
+    mn[j] = fminf(mn[j], v);
+    mx[j] = fmaxf(mx[j], v);
+  }
+  Moments m;
+  m.s1 = ((a1[0] + a1[1]) + (a1[2] + a1[3])) + ((a1[4] + a1[5]) + (a1[6] + a1[7]));
+  m.s2 = ((a2[0] + a2[1]) + (a2[2] + a2[3])) + ((a2[4] + a2[5]) + (a2[6] + a2[7]));
+  for (int j = 0; j < 8; ++j) {
+    m.mn = fminf(m.mn, mn[j]);
+    m.mx = fmaxf(m.mx, mx[j]);
+  }
+  return m;
+}
+
+// smaq_elem.h finalize_stats on the host (the same formulas).
+template <int T>
+static void finalize(double s1, double s2, float mn, float mx, int64_t n, double shift, bool biased,
+                     bool range, float clamp_lo, float clamp_hi, float range_coef,
+                     SmqSmaqStats* out) {
+  const double nd = (double)n;
+  const double mean = shift + s1 / nd;
+  float sd;
+  if (range) {
+    sd = rin<T>(rin<T>(mx - mn) * range_coef);
+  } else {
+    double var = (s2 - s1 * (s1 / nd)) / (biased ? nd : (nd - 1.0));
+    if (var < 0.0) var = 0.0;
+    sd = rin<T>((float)sqrt(var));
+  }
+  const float std_dev = (sd == 0.0f) ? 1.0f : sd;
+  const float lo = rin<T>(clamp_lo), hi = rin<T>(clamp_hi);
+  float sc = std_dev < lo ? lo : std_dev;
+  sc = sc > hi ? hi : sc;
+  memset(out, 0, sizeof(*out));
+  out->mean = rin<T>((float)mean);
+  out->std_dev = std_dev;
+  out->std_clamped = sc;
+  out->raw_std = sd;
+  out->min_val = mn;
+  out->max_val = mx;
+  out->n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
+  out->inv_std_clamped = 1.0 / (double)sc;
+  out->quot_check = quot_check_for(sc);
+}
+
+template <int T>
+static void full_stats(const void* x, int64_t n, const SmqSmaqParams* p, float range_coef,
+                       int n_threads, SmqSmaqStats* out) {
+  const float k0 = ld<T>(x, 0), k1 = ld<T>(x, n >> 1), k2 = ld<T>(x, n - 1);
+  const double shift = (double)fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));  // as the device
+  std::vector<Moments> part((size_t)((n + kTask - 1) / kTask));
+  parallel_tasks(n, n_threads, [&](int64_t t, int64_t i0, int64_t i1) {
+    part[(size_t)t] = task_moments<T>(x, i0, i1, shift);
+  });
+  Moments tot;
+  for (const Moments& m : part) {
+    tot.s1 += m.s1;
+    tot.s2 += m.s2;
+    tot.mn = fminf(tot.mn, m.mn);
+    tot.mx = fmaxf(tot.mx, m.mx);
+  }
+  finalize<T>(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, p->use_range_std_dev != 0,
+              p->clamp_lo, p->clamp_hi, range_coef, out);
+}
+
+// smart.py:86-91 over k given indices: mean, biased std (shift = mean, as the device)
+template <int T>
+static void sampled_stats(const void* x, const int64_t* idx, int64_t k, const SmqSmaqParams* p,
+                          float range_coef, SmqSmaqStats* out) {
+  double s = 0.0;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int64_t i = 0; i < k; ++i) {
+    const float v = ld<T>(x, idx[i]);
+    s += (double)v;
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  const double mean = s / (double)k;
+  double m2 = 0.0;
+  for (int64_t i = 0; i < k; ++i) {
+    const double d = (double)ld<T>(x, idx[i]) - mean;
+    m2 = fma(d, d, m2);
+  }
+  finalize<T>(0.0, m2, mn, mx, k, mean, true, p->use_range_std_dev != 0, p->clamp_lo, p->clamp_hi,
+              range_coef, out);
+}
+
+// The device draw (smaq_elem.h Floyd, smq_smaq_draw_samples) for any k <= SMQ_MAX_DEVICE_SAMPLES.
+static void floyd_draw(uint64_t seed, uint64_t pos, int64_t n, int64_t k, int64_t* out) {
+  const uint32_t key = rng_key(seed ^ kDrawSalt);
+  std::vector<int64_t> seen;
+  seen.reserve((size_t)k);
+  for (int i = 0; i < (int)k; ++i) {
+    int64_t t = floyd_candidate(key, pos, n, (int)k, i);
+    if (std::find(seen.begin(), seen.end(), t) != seen.end()) t = n - k + i;
+    seen.push_back(t);
+    out[i] = t;
+  }
+}
+
+// ---- SmaQ element pass --------------------------------------------------------------------------
+struct SmaqCtx {
+  const void* x;
+  float* y;
+  const float* uniforms;
+  const float* bn_gamma;
+  const float* bn_beta;
+  int64_t bn_channels, bn_inner;
+  float mean, sd, sc, thr, nthr, cthr, cnthr, zh, zl, r_main, r_out;
+  uint32_t key;
+  uint64_t off;  // params.offset + stream snapshot
+};
+
+// smart.py:144-182 for elements [i0, i1): smaq_quant + smaq_dequant with the device's arithmetic.
+// RM: kRoundHash / kRoundUniform / kRoundTrunc. Returns the outliers among them.
+template <int T, int RM, bool BN, bool AP>
+static uint64_t smaq_task(const SmaqCtx& c, int64_t i0, int64_t i1) {
+  constexpr int TZ = BN ? kF32 : T;
+  uint64_t n_out = 0;
+  for (int64_t i = i0; i < i1; ++i) {
+    float v = ld<T>(c.x, i);
+    float g = 1.0f, bb = 0.0f;
+    if (BN) {
+      const int64_t ch = (i / c.bn_inner) % c.bn_channels;
+      g = c.bn_gamma[ch];
+      bb = c.bn_beta[ch];
+      v = (v - bb) / g;
+    }
+    const float dm = rin<TZ>(v - c.mean);
+    const float z = rin<TZ>(dm / c.sc);
+    const bool hi = z > c.cthr, lo = z < c.cnthr, o = hi || lo;
+    const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);
+    const float r = o ? c.r_out : c.r_main;
+    const float d = (z + a) * r;
+    float q;
+    if (RM == kRoundTrunc) {
+      q = truncf(d);
+    } else {
+      const float f = floorf(d);
+      const float fr = d - f;
+      float t;
+      if (RM == kRoundHash)
+        t = fmaf(hash_u24(c.key, c.off + (uint64_t)i), -0x1p-24f, fr) + 0.5f;
+      else
+        t = (fr - c.uniforms[i]) + 0.5f;
+      t = (t < 0.0f) ? 0.0f : t;
+      q = f + rintf(t);
+    }
+    float out = q / r - a;
+    out = out * c.sd;
+    out = out + c.mean;
+    if (BN) {
+      out = out * g;
+      out = out + bb;
+    }
+    if (AP) out = (out < 0.0f) ? 0.0f : out;
+    c.y[i] = out;
+    n_out += o ? 1u : 0u;
+  }
+  return n_out;
+}
+
+template <int T>
+static uint64_t smaq_pass(const SmaqCtx& c, int64_t n, int rm, bool bn, bool ap, int n_threads) {
+  std::vector<uint64_t> part((size_t)((n + kTask - 1) / kTask));
+  auto go = [&](auto rm_c, auto bn_c, auto ap_c) {
+    parallel_tasks(n, n_threads, [&](int64_t t, int64_t i0, int64_t i1) {
+      part[(size_t)t] = smaq_task<T, decltype(rm_c)::value, decltype(bn_c)::value,
+                                  decltype(ap_c)::value>(c, i0, i1);
+    });
+  };
+  using H = std::integral_constant<int, kRoundHash>;
+  using U = std::integral_constant<int, kRoundUniform>;
+  using R = std::integral_constant<int, kRoundTrunc>;
+  using Y = std::true_type;
+  using N = std::false_type;
+  if (rm == kRoundHash) {
+    if (bn) { if (ap) go(H(), Y(), Y()); else go(H(), Y(), N()); }
+    else { if (ap) go(H(), N(), Y()); else go(H(), N(), N()); }
+  } else if (rm == kRoundUniform) {
+    if (bn) { if (ap) go(U(), Y(), Y()); else go(U(), Y(), N()); }
+    else { if (ap) go(U(), N(), Y()); else go(U(), N(), N()); }
+  } else {
+    if (bn) { if (ap) go(R(), Y(), Y()); else go(R(), Y(), N()); }
+    else { if (ap) go(R(), N(), Y()); else go(R(), N(), N()); }
+  }
+  uint64_t tot = 0;
+  for (uint64_t v : part) tot += v;
+  return tot;
+}
+
+static float range_coef_host(const SmqSmaqParams* p, int64_t n) {
+  if (p->range_std_coef >= 0.0f) return p->range_std_coef;
+  const float lg = logf((float)n);
+  return 1.0f / sqrtf(2.0f * lg);
+}
+
+template <int T>
+static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParams* p,
+                          const float* uniforms, const SmqSmaqStats* stats_in, char* ws,
+                          int n_threads) {
+  SmqSmaqStats st;
+  uint64_t base = 0;
+  if (p->offset_counter) {  // a host uint64 stream position, advanced by n (graph-safe mirror)
+    base = *p->offset_counter;
+    *p->offset_counter = base + (uint64_t)n;
+  }
+  switch (p->stats_source) {
+    case SMQ_STATS_WORKSPACE:
+      full_stats<T>(x, n, p, range_coef_host(p, n), n_threads, &st);
+      break;
+    case SMQ_STATS_SAMPLED: {
+      const int64_t k = std::min<int64_t>(p->num_samples, n);
+      if (k < 1 || k > SMQ_MAX_SAMPLES) {
+        set_error("cpu smaq: num_samples must be in [1, %d] for SMQ_STATS_SAMPLED", SMQ_MAX_SAMPLES);
+        return SMQ_ERR_INVALID;
+      }
+      for (int64_t i = 0; i < k; ++i)
+        if (p->sample_idx[i] < 0 || p->sample_idx[i] >= n) {
+          set_error("cpu smaq: sample index %lld out of range", (long long)p->sample_idx[i]);
+          return SMQ_ERR_INVALID;
+        }
+      sampled_stats<T>(x, p->sample_idx, k, p, range_coef_host(p, k), &st);
+      break;
+    }
+    case SMQ_STATS_SAMPLED_DEVICE: {
+      const int64_t k = std::min<int64_t>(p->num_samples, n);
+      if (k < 1 || k > SMQ_MAX_DEVICE_SAMPLES) {
+        set_error("cpu smaq: num_samples must be in [1, %d]", SMQ_MAX_DEVICE_SAMPLES);
+        return SMQ_ERR_INVALID;
+      }
+      int64_t* idx = reinterpret_cast<int64_t*>(ws + SMQ_WS_SAMPLES_OFFSET);
+      floyd_draw(p->seed, p->offset + base, n, k, idx);
+      sampled_stats<T>(x, idx, k, p, range_coef_host(p, k), &st);
+      break;
+    }
+    default: {  // SMQ_STATS_INJECTED: mean / std from stats_in, the rest derived
+      if (!stats_in) {
+        set_error("cpu smaq: SMQ_STATS_INJECTED needs stats_in");
+        return SMQ_ERR_INVALID;
+      }
+      st = *stats_in;
+      st.inv_std_clamped = 1.0 / (double)st.std_clamped;
+      st.quot_check = quot_check_for(st.std_clamped);
+    }
+  }
+  st.rng_offset = base;
+  SmaqCtx c;
+  c.x = x;
+  c.y = y;
+  c.uniforms = uniforms;
+  c.bn_gamma = p->bn_gamma;
+  c.bn_beta = p->bn_beta;
+  c.bn_channels = p->bn_channels;
+  c.bn_inner = p->bn_inner;
+  c.mean = st.mean;
+  c.sd = st.std_dev;
+  c.sc = st.std_clamped;
+  c.thr = p->main_std_dev_threshold;
+  c.nthr = -c.thr;
+  const bool bn = p->bn_gamma != nullptr;
+  c.cthr = bn ? c.thr : rin<T>(c.thr);
+  c.cnthr = -c.cthr;
+  c.zh = 0.0f * c.nthr;
+  c.zl = 0.0f * c.thr;
+  c.r_main = p->range_main;
+  c.r_out = p->range_outlier;
+  c.key = rng_key(p->seed);
+  c.off = p->offset + base;
+  const int rm = !p->stochastic_rounding ? kRoundTrunc : (uniforms ? kRoundUniform : kRoundHash);
+  const uint64_t n_out = smaq_pass<T>(c, n, rm, bn, p->all_positive != 0, n_threads);
+  if (p->count_outliers) st.n_outlier = n_out;
+  memcpy(ws, &st, sizeof(st));
+  uint64_t* slots = reinterpret_cast<uint64_t*>(ws + SMQ_WS_OUTLIER_SLOTS_OFFSET);
+  for (int i = 0; i < SMQ_WS_OUTLIER_SLOTS; ++i) slots[i] = 0;
+  if (p->count_outliers) slots[0] = n_out;
+  return SMQ_OK;
+}
+
+// ---- float_quantize -----------------------------------------------------------------------------
+template <int TIN, bool HOUT>
+static void float_quant_pass(const void* x, void* y, int64_t n, int eb, int mb, bool sr,
+                             int check_inf, const uint32_t* rand_bits, uint32_t key,
+                             uint64_t offset, float max_value, int n_threads) {
+  parallel_tasks(n, n_threads, [&](int64_t, int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      const uint32_t r = !sr ? 0u : (rand_bits ? rand_bits[i] : rng_u32(key, offset + (uint64_t)i));
+      float q = qtorch_quant(ld<TIN>(x, i), r, eb, mb, sr);
+      if (check_inf && fabsf(q - max_value) <= FLT_EPSILON) q = INFINITY;
+      if (HOUT) static_cast<uint16_t*>(y)[i] = f2h(q);
+      else static_cast<float*>(y)[i] = q;
+    }
+  });
+}
+
+// ---- S2FP8 ----------------------------------------------------------------------------------------
+static inline float nan_max_h(float a, float b) { return (b > a || b != b) ? b : a; }
+
+template <int TIN>
+static void s2_derive(float mu, float m, uint32_t n_used, SmqS2fp8Stats* o) {
+  const float alpha = rin<TIN>(rin<TIN>(1.0f / rin<TIN>(m - mu)) * 15.0f);
+  const float beta = rin<TIN>((-alpha) * mu);
+  const float bp2 = rin<TIN>((float)exp2((double)beta));
+  o->mu = mu;
+  o->m = m;
+  o->alpha = alpha;
+  o->beta = beta;
+  o->beta_pow2 = bp2;
+  o->inv_beta_pow2 = rin<TIN>(1.0f / bp2);
+  o->inv_alpha = rin<TIN>(1.0f / alpha);
+  o->n_used = n_used;
+}
+
+template <int TIN>
+static inline float s2_log_h(float v) {
+  const float a = fabsf(v);
+  return a == 0.0f ? a : rin<TIN>(log2f(a));
+}
+
+template <int TIN>
+static void s2_stats(const void* x, int64_t n, int n_threads, SmqS2fp8Stats* o) {
+  struct P {
+    double s;
+    float m;
+  };
+  std::vector<P> part((size_t)((n + kTask - 1) / kTask));
+  parallel_tasks(n, n_threads, [&](int64_t t, int64_t i0, int64_t i1) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float mx = -INFINITY;
+    for (int64_t i = i0; i < i1; ++i) {
+      const float l = s2_log_h<TIN>(ld<TIN>(x, i));
+      a[(i - i0) & 7] += (double)l;
+      mx = nan_max_h(mx, l);
+    }
+    part[(size_t)t] = P{((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])), mx};
+  });
+  double s = 0.0;
+  float m = -INFINITY;
+  for (const P& q : part) {
+    s += q.s;
+    m = nan_max_h(m, q.m);
+  }
+  const float mu = rin<TIN>((float)(s / (double)n));
+  s2_derive<TIN>(mu, m, (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n), o);
+}
+
+// s2fp8.py:45-48 (precision 32; out_mode 1 / 2: Y / T as the device's OUT_Y / OUT_T)
+static inline float s2_elem32(float xv, uint32_t r, const SmqS2fp8Stats& s, int check_inf,
+                              float max_value, int out_mode) {
+  const float sgn = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
+  float Y = powf(fabsf(xv), s.alpha);
+  Y = Y * s.beta_pow2;
+  if (out_mode == 1) return Y;
+  float T = qtorch_quant(Y, r, 5, 2, true);
+  if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
+  if (out_mode == 2) return T;
+  return powf(T * s.inv_beta_pow2, s.inv_alpha) * sgn;
+}
+
+// precision 16 (quantization.py:187-204 half branch): forward in TIN, inverse in half
+template <int TIN>
+static inline float s2_elem16(float xv, uint32_t r, const SmqS2fp8Stats& s, int check_inf,
+                              float max_value) {
+  float Y = powf(fabsf(xv), s.alpha);
+  Y = rin<TIN>(rin<TIN>(Y) * s.beta_pow2);
+  float T = qtorch_quant(Y, r, 5, 2, true);
+  if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
+  const float t1 = rin<kF16>(T * s.inv_beta_pow2);
+  const float t2 = rin<kF16>(powf(t1, rin<kF16>(s.inv_alpha)));
+  if (xv > 0.0f) return t2;
+  if (xv < 0.0f) return u2f(f2u(t2) ^ 0x80000000u);
+  return t2 * 0.0f;
+}
+
+template <int TIN>
+static void s2_pass(const void* x, void* y, int64_t n, bool p16, bool hout, int check_inf,
+                    const uint32_t* rand_bits, uint32_t key, uint64_t off, const SmqS2fp8Stats& s,
+                    int out_mode, int n_threads) {
+  const float max_value = qtorch_quant(FLT_MAX, 0u, 5, 2, false);
+  parallel_tasks(n, n_threads, [&](int64_t, int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      const uint32_t r = rand_bits ? rand_bits[i] : rng_u32(key, off + (uint64_t)i);
+      const float xv = ld<TIN>(x, i);
+      const float v = p16 ? s2_elem16<TIN>(xv, r, s, check_inf, max_value)
+                          : s2_elem32(xv, r, s, check_inf, max_value, out_mode);
+      if (hout) static_cast<uint16_t*>(y)[i] = f2h(v);
+      else static_cast<float*>(y)[i] = v;
+    }
+  });
+}
+
+}  // namespace cpu
+}  // namespace smq
+
+using namespace smq;
+
+extern "C" {
+
+int smq_cpu_threads(void) { return cpu::pool().size(); }
+
+int smq_cpu_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                           const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
+                           size_t ws_bytes, int n_threads) {
+  int rc = smaq_validate(p, dtype);
+  if (rc) return rc;
+  if (n < 1 || !x || !y) {
+    set_error("cpu smaq: n >= 1 and non-NULL x, y required");
+    return SMQ_ERR_INVALID;
+  }
+  if (!ws || ws_bytes < smq_smaq_workspace_bytes(n)) {
+    set_error("cpu smaq: workspace too small: need %zu bytes", smq_smaq_workspace_bytes(n));
+    return SMQ_ERR_WORKSPACE;
+  }
+  if (p->bn_gamma && (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1)) {
+    set_error("cpu smaq: batch-norm parameters incomplete");
+    return SMQ_ERR_INVALID;
+  }
+  char* w = static_cast<char*>(ws);
+  if (dtype == SMQ_DTYPE_F32) return cpu::smaq_roundtrip<kF32>(x, y, n, p, uniforms, stats_in, w, n_threads);
+  if (dtype == SMQ_DTYPE_F16) return cpu::smaq_roundtrip<kF16>(x, y, n, p, uniforms, stats_in, w, n_threads);
+  return cpu::smaq_roundtrip<kBF16>(x, y, n, p, uniforms, stats_in, w, n_threads);
+}
+
+int smq_cpu_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t n,
+                        int exp_bits, int man_bits, int rounding, int check_inf,
+                        const uint32_t* rand_bits, uint64_t seed, uint64_t offset, int n_threads) {
+  if (n < 0 || (n > 0 && (!x || !y))) {
+    set_error("cpu float_quant: bad tensor arguments");
+    return SMQ_ERR_INVALID;
+  }
+  if (dtype_in != SMQ_DTYPE_F32 && dtype_in != SMQ_DTYPE_F16 && dtype_in != SMQ_DTYPE_BF16) {
+    set_error("cpu float_quant: dtype_in must be SMQ_DTYPE_F32, _F16 or _BF16 (got %d)", dtype_in);
+    return SMQ_ERR_INVALID;
+  }
+  if (dtype_out != SMQ_DTYPE_F32 && dtype_out != SMQ_DTYPE_F16) {
+    set_error("cpu float_quant: dtype_out must be SMQ_DTYPE_F32 or _F16 (got %d)", dtype_out);
+    return SMQ_ERR_INVALID;
+  }
+  if (exp_bits < 2 || exp_bits > 8 || man_bits < 0 || man_bits > 22) {
+    set_error("cpu float_quant: exp_bits in [2,8] and man_bits in [0,22] required (got %d,%d)",
+              exp_bits, man_bits);
+    return SMQ_ERR_INVALID;
+  }
+  if (rounding != SMQ_ROUND_NEAREST && rounding != SMQ_ROUND_STOCHASTIC) {
+    set_error("cpu float_quant: rounding must be SMQ_ROUND_NEAREST or SMQ_ROUND_STOCHASTIC");
+    return SMQ_ERR_INVALID;
+  }
+  if (n == 0) return SMQ_OK;
+  const bool sr = rounding == SMQ_ROUND_STOCHASTIC, hout = dtype_out == SMQ_DTYPE_F16;
+  const float mv = qtorch_quant(FLT_MAX, 0u, exp_bits, man_bits, false);
+  const uint32_t key = rng_key(seed);
+#define SMQ_CFQ(T, H) \
+  cpu::float_quant_pass<T, H>(x, y, n, exp_bits, man_bits, sr, check_inf, rand_bits, key, offset, mv, n_threads)
+  if (dtype_in == SMQ_DTYPE_F32) { if (hout) SMQ_CFQ(kF32, true); else SMQ_CFQ(kF32, false); }
+  else if (dtype_in == SMQ_DTYPE_F16) { if (hout) SMQ_CFQ(kF16, true); else SMQ_CFQ(kF16, false); }
+  else { if (hout) SMQ_CFQ(kBF16, true); else SMQ_CFQ(kBF16, false); }
+#undef SMQ_CFQ
+  return SMQ_OK;
+}
+
+int smq_cpu_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precision,
+                            int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                            uint64_t offset, const SmqS2fp8Stats* stats_in, void* ws,
+                            size_t ws_bytes, uint32_t flags, int n_threads) {
+  if (n < 1 || !x || !y) {
+    set_error("cpu s2fp8: n >= 1 and non-NULL x, y required");
+    return SMQ_ERR_INVALID;
+  }
+  if (dtype != SMQ_DTYPE_F32 && dtype != SMQ_DTYPE_F16 && dtype != SMQ_DTYPE_BF16) {
+    set_error("cpu s2fp8: dtype must be SMQ_DTYPE_F32, _F16 or _BF16 (got %d)", dtype);
+    return SMQ_ERR_INVALID;
+  }
+  if (precision != 16 && precision != 32) {
+    set_error("cpu s2fp8: precision must be 16 or 32 (got %d)", precision);
+    return SMQ_ERR_INVALID;
+  }
+  if (precision == 32 && dtype != SMQ_DTYPE_F32) {
+    set_error("cpu s2fp8: precision 32 quantises the tensor as is and needs fp32 input");
+    return SMQ_ERR_INVALID;
+  }
+  if (flags & ~(SMQ_S2FP8_OUT_Y | SMQ_S2FP8_OUT_T | SMQ_S2FP8_EXACT_POW | SMQ_S2FP8_SPLIT)) {
+    set_error("cpu s2fp8: unsupported flags 0x%x", flags);
+    return SMQ_ERR_INVALID;
+  }
+  const int out_mode = (flags & SMQ_S2FP8_OUT_Y) ? 1 : ((flags & SMQ_S2FP8_OUT_T) ? 2 : 0);
+  if ((flags & SMQ_S2FP8_OUT_Y) && (flags & SMQ_S2FP8_OUT_T)) {
+    set_error("cpu s2fp8: SMQ_S2FP8_OUT_Y and SMQ_S2FP8_OUT_T are exclusive");
+    return SMQ_ERR_INVALID;
+  }
+  if (out_mode && precision != 32) {
+    set_error("cpu s2fp8: SMQ_S2FP8_OUT_* need precision 32");
+    return SMQ_ERR_INVALID;
+  }
+  SmqS2fp8Stats s;
+  memset(&s, 0, sizeof(s));
+  const uint32_t n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
+  if (dtype == SMQ_DTYPE_F32) {
+    if (stats_in) cpu::s2_derive<kF32>(stats_in->mu, stats_in->m, n_used, &s);
+    else cpu::s2_stats<kF32>(x, n, n_threads, &s);
+  } else if (dtype == SMQ_DTYPE_F16) {
+    if (stats_in) cpu::s2_derive<kF16>(stats_in->mu, stats_in->m, n_used, &s);
+    else cpu::s2_stats<kF16>(x, n, n_threads, &s);
+  } else {
+    if (stats_in) cpu::s2_derive<kBF16>(stats_in->mu, stats_in->m, n_used, &s);
+    else cpu::s2_stats<kBF16>(x, n, n_threads, &s);
+  }
+  const bool p16 = precision == 16, hout = p16 && dtype == SMQ_DTYPE_F16;
+  const uint32_t key = rng_key(seed);
+  if (dtype == SMQ_DTYPE_F32)
+    cpu::s2_pass<kF32>(x, y, n, p16, hout, check_inf, rand_bits, key, offset, s, out_mode, n_threads);
+  else if (dtype == SMQ_DTYPE_F16)
+    cpu::s2_pass<kF16>(x, y, n, p16, hout, check_inf, rand_bits, key, offset, s, out_mode, n_threads);
+  else
+    cpu::s2_pass<kBF16>(x, y, n, p16, hout, check_inf, rand_bits, key, offset, s, out_mode, n_threads);
+  if (ws && ws_bytes >= sizeof(s)) memcpy(ws, &s, sizeof(s));
+  return SMQ_OK;
+}
+
+}  // extern "C"

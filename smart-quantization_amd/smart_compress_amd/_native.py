@@ -216,6 +216,19 @@ SIGNATURES = {
     "smq_smaq_compress_ex": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams),
                                      _P, _SZ, _P, _SZ, _U32, _P]),
     "smq_smaq_decompress": (_I32, [_P, _P, _I64, _P]),
+    "smq_cpu_threads": (_I32, []),
+    "smq_cpu_smaq_roundtrip": (
+        _I32,
+        [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _P, _SZ, _I32],
+    ),
+    "smq_cpu_float_quant": (
+        _I32,
+        [_P, _I32, _P, _I32, _I64, _I32, _I32, _I32, _I32, _P, _U64, _U64, _I32],
+    ),
+    "smq_cpu_s2fp8_roundtrip": (
+        _I32,
+        [_P, _I32, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _SZ, _U32, _I32],
+    ),
 }
 
 _lib = None
@@ -265,6 +278,36 @@ def require_device(t: torch.Tensor, who: str) -> None:
             f"{who}: smart_compress_amd runs on ROCm device tensors only (got device={t.device}); "
             "move the tensor to the GPU"
         )
+
+
+def on_cpu(t: torch.Tensor) -> bool:
+    """CPU tensors run on the library's host path (smq_cpu_*), ROCm tensors on the kernels."""
+    return t.device.type == "cpu"
+
+
+def require_supported(t: torch.Tensor, who: str) -> None:
+    """A ROCm device tensor or a CPU tensor (the reference's plugins run on either)."""
+    if not (t.is_cuda or on_cpu(t)):
+        raise RuntimeError(f"{who}: tensors on {t.device} are not supported (ROCm device or CPU)")
+
+
+def cpu_threads() -> int:
+    """Threads a host-path call uses: torch's intra-op setting, like the reference's CPU ops."""
+    return max(1, torch.get_num_threads())
+
+
+_cpu_ws = threading.local()
+
+
+def cpu_workspace(kind: str, nbytes: int) -> torch.Tensor:
+    """A host workspace of at least nbytes for the calling thread (host calls are synchronous)."""
+    cache = getattr(_cpu_ws, "bufs", None)
+    if cache is None:
+        cache = _cpu_ws.bufs = {}
+    buf = cache.get(kind)
+    if buf is None or buf.numel() < nbytes:
+        buf = cache[kind] = torch.zeros(max(nbytes, 256), dtype=torch.uint8)
+    return buf
 
 
 def require_device_f32(t: torch.Tensor, who: str) -> None:

@@ -50,11 +50,13 @@ class S2FP8(CompressionAlgorithmBase):
         hp = self.hparams
         self.log_ratio(tag, tensor.numel(), 32, 8, overhead=64)
         precision = 16 if hp.precision == 16 else 32
+        N.require_supported(tensor, "S2FP8")
         if precision == 32:
-            N.require_device_f32(tensor, "S2FP8")
+            if tensor.dtype != torch.float32:
+                raise NotImplementedError(
+                    f"S2FP8: dtype {tensor.dtype} at precision 32 is not supported (float32 only)")
             out_dtype = torch.float32
         else:
-            N.require_device(tensor, "S2FP8")
             if tensor.dtype not in (torch.float32, torch.float16, torch.bfloat16):
                 raise NotImplementedError(f"S2FP8: dtype {tensor.dtype} is not supported")
             out_dtype = torch.float16 if tensor.dtype == torch.float16 else torch.float32
@@ -62,6 +64,13 @@ class S2FP8(CompressionAlgorithmBase):
         y = torch.empty_like(x, dtype=out_dtype)
         n = x.numel()
         if n == 0:
+            return y
+        if N.on_cpu(x):  # the library's host path, host RNG offsets
+            seed, offset = _q.quant_rng().take(n)
+            N.check(N.lib().smq_cpu_s2fp8_roundtrip(
+                x.data_ptr(), N.DTYPE_CODES[x.dtype], y.data_ptr(), n, precision,
+                1 if hp.float_quantize_check_inf else 0, None, seed, offset, None, None, 0, 0,
+                N.cpu_threads()), "smq_cpu_s2fp8_roundtrip")
             return y
         fn = S2FP8._fn
         if fn is None:

@@ -197,7 +197,7 @@ class SmartFP(CompressionAlgorithmBase):
                 self.log_ratio(tag, numel * 32, 32, 32)
                 return data
 
-            N.require_device(data, "SmartFP")
+            N.require_supported(data, "SmartFP")
             code = N.DTYPE_CODES.get(data.dtype)
             if code is None:
                 raise NotImplementedError(
@@ -205,6 +205,8 @@ class SmartFP(CompressionAlgorithmBase):
             if data.dtype == torch.float16 and hp.precision != 16:
                 # the reference's std.clamp(1e-38, 1e38) on a half tensor (smart.py:154)
                 raise RuntimeError("value cannot be converted to type c10::Half without overflow")
+            if N.on_cpu(data):
+                return self._call_cpu(data, tag, numel, code, all_positive, batch_norm_stats)
             if hp.measure_compression_ratio and torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("SmartFP: --measure_compression_ratio reads the outlier count "
                                    "on the host; it cannot run inside a graph capture")
@@ -226,6 +228,30 @@ class SmartFP(CompressionAlgorithmBase):
 
             self.log_size(tag, numel * 32, new_size)
             return y
+
+    def _call_cpu(self, data, tag, numel, code, all_positive, batch_norm_stats):
+        """CPU tensors: the library's host path (smq_cpu_smaq_roundtrip), one synchronous call on
+        torch's intra-op thread count; host RNG offsets (there is no graph to replay)."""
+        hp = self.hparams
+        x = data.contiguous()
+        y = torch.empty(x.shape, dtype=torch.float32)
+        p = self._params(numel, all_positive, x.dtype, None)
+        keep = None
+        if hp.use_batch_norm and batch_norm_stats is not None:
+            keep = self._bind_batch_norm(p, x, batch_norm_stats)
+        lib = N.lib()
+        ws = N.cpu_workspace("smaq", lib.smq_smaq_workspace_bytes(numel))
+        N.check(lib.smq_cpu_smaq_roundtrip(x.data_ptr(), code, y.data_ptr(), numel, p, None, None,
+                                           ws.data_ptr(), ws.numel(), N.cpu_threads()),
+                "smq_cpu_smaq_roundtrip")
+        del keep
+        if hp.measure_compression_ratio:
+            n_out = self.outlier_count(ws)
+            self.log_size(tag, numel * 32,
+                          n_out * hp.num_bits_outlier + (numel - n_out) * hp.num_bits_main)
+        else:
+            self.log_size(tag, numel * 32, None)
+        return y
 
     # bench.py sets an event recorder here to time the apply launch on the codec's stream
     _trace = None

@@ -81,16 +81,25 @@ def float_quantize(x: torch.Tensor, exp: int, man: int, hparams) -> torch.Tensor
     """Stochastic (exp, man) round trip of ``x`` (quantization.py:187-204). Precision 16: ``x``
     (fp32 / fp16 / bf16) is quantised as ``x.float()`` and returned as fp16."""
     half_io = hparams.precision == 16
+    N.require_supported(x, "float_quantize")
     if half_io:
-        N.require_device(x, "float_quantize")
         if x.dtype not in N.DTYPE_CODES:
             raise NotImplementedError(f"float_quantize: dtype {x.dtype} is not supported")
-    else:
-        N.require_device_f32(x, "float_quantize")
+    elif x.dtype != torch.float32:
+        raise NotImplementedError(
+            f"float_quantize: dtype {x.dtype} at precision 32 is not supported (float32 only)")
     src = x.contiguous()
     out = torch.empty_like(src, dtype=torch.float16 if half_io else torch.float32)
     n = src.numel()
     if n == 0:
+        return out
+    if N.on_cpu(src):  # the library's host path, host RNG offsets
+        seed, offset = quant_rng().take(n)
+        N.check(N.lib().smq_cpu_float_quant(
+            src.data_ptr(), N.DTYPE_CODES[src.dtype], out.data_ptr(),
+            N.SMQ_DTYPE_F16 if half_io else N.SMQ_DTYPE_F32, n, exp, man, N.SMQ_ROUND_STOCHASTIC,
+            1 if hparams.float_quantize_check_inf else 0, None, seed, offset, N.cpu_threads()),
+            "smq_cpu_float_quant")
         return out
     global _fq
     if _fq is None:

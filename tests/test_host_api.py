@@ -89,14 +89,20 @@ def test_range_coef_matches_torch():
         assert np.float32(osmaq.range_coef(n)) == np.float32(ref)
 
 
-def test_passthrough_and_cpu_rejection():
+def test_passthrough_cpu_path_and_rejections():
+    """n < min_size passes the same object through; CPU tensors take the library's host path;
+    fp64 and meta tensors are rejected with a clear error."""
     from smart_compress_amd.compress.smart import SmartFP
 
     c = SmartFP(smaq_hparams())
     x = torch.randn(7)
     assert c(x) is x  # smart.py:123-128, no device needed
-    with pytest.raises(RuntimeError, match="ROCm device tensors only"):
-        c(torch.randn(100))
+    y = c(torch.randn(100))
+    assert y.shape == (100,) and y.device.type == "cpu"
+    with pytest.raises(NotImplementedError, match="float64"):
+        c(torch.randn(100, dtype=torch.float64))
+    with pytest.raises(RuntimeError, match="not supported"):
+        c(torch.randn(100, device="meta"))
 
 
 def test_log_size_routing():
