@@ -37,6 +37,7 @@ for s in "$@"; do
     tests_packed) step pytest_packed 600 python -u -m pytest tests/test_gpu_packed.py -x -q --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 --cpu-budget 8 ;;
+    bench_cpu) step bench_cpu 300 python bench.py --config smaq_cpu --cpu-budget 5 ;;
     bench_all) step bench_fp8 300 python bench.py --config fp8 --steps 50 --warmup 5 &&
                step bench_s2fp8 300 python bench.py --config s2fp8 --steps 200 --warmup 20 &&
                step bench_multi 300 python bench.py --config multi --steps 100 --warmup 10 &&
