@@ -282,9 +282,8 @@ __global__ __launch_bounds__(PT) void s2fp8_partial_kernel(const void* __restric
     }
   }
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  s = wave_sum(s);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o, kWave));
+  s = wave_sum_asc(s);
+  m = wave_nanmax_asc(m);
   if (lane == 0) {
     shs[wave] = s;
     shm[wave] = m;
@@ -322,9 +321,8 @@ __device__ __forceinline__ void s2_reduce_partials(const S2Partial* __restrict__
     s = p.s;
     m = p.m;
   }
-  s = wave_sum(s);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o, kWave));
+  s = wave_sum_asc(s);
+  m = wave_nanmax_asc(m);
   if (lane == 0) {
     shs[wave] = s;
     shm[wave] = m;
@@ -733,9 +731,8 @@ __device__ void s2f_publish(double s, float m, const S2FArgs& A, int k, uint32_t
                             double* shs, float* shm) {
   constexpr int W = kS2FT / kWave;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  s = wave_sum(s);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o, kWave));
+  s = wave_sum_asc(s);
+  m = wave_nanmax_asc(m);
   if (lane == 0) {
     shs[wave] = s;
     shm[wave] = m;
@@ -911,23 +908,13 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
   unsigned long long left_old = 0;
   if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.left);
   // wave 0: reduce the partials in the two-launch apply's order (a wave sum over partial indices
-  // l + 64q for each q, the four butterflies interleaved, then (q0 + q1) + (q2 + q3)) and derive;
+  // l + 64q for each q in the ascending butterfly order, then (q0 + q1) + (q2 + q3)) and derive;
   // then threads 0-130 tabulate the inverse powers
   if (wave == 0) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      double ts[4];
-      float tm[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ts[q] = __shfl_xor(ps[q], o, kWave);
-        tm[q] = __shfl_xor(pm[q], o, kWave);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ps[q] += ts[q];
-        pm[q] = nan_max(pm[q], tm[q]);
-      }
+    for (int q = 0; q < 4; ++q) {
+      ps[q] = wave_sum_asc(ps[q]);
+      pm[q] = wave_nanmax_asc(pm[q]);
     }
     s2f_stamp(A, 8);
     if (lane == 0) {

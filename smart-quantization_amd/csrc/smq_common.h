@@ -90,6 +90,57 @@ __device__ __forceinline__ double wave_sum(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   return v;
 }
+// DPP lane permutations (GFX9 encodings): quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror,
+// row_mirror.
+constexpr int kDppXor1 = 0xb1, kDppXor2 = 0x4e, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xf, 0xf, false));
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// Wave64 sum in the ASCENDING xor-butterfly order (partners at distance 1, 2, 4, 8, 16, 32), the
+// same value in every lane (a wave-uniform result). After the step at distance o the value is
+// uniform over each aligned group of 2o lanes, so any lane of the partner group serves as lane
+// l ^ o: quad permutes for 1 and 2, the half-row / row mirrors for 4 and 8 (VALU DPP moves, no
+// LDS round trip), and the four row totals by readlane: (r0 + r1) + (r2 + r3), which is what the
+// last two butterfly steps compute in every lane (fp add is commutative). All 64 lanes active.
+__device__ __forceinline__ double wave_sum_asc(double v) {
+  v += dpp_f64<kDppXor1>(v);
+  v += dpp_f64<kDppXor2>(v);
+  v += dpp_f64<kDppHalfMirror>(v);
+  v += dpp_f64<kDppMirror>(v);
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+
+// The same butterfly for a NaN-propagating max (torch.max): max is order-free up to NaN payloads.
+__device__ __forceinline__ float nan_max2(float a, float b) { return (b > a || b != b) ? b : a; }
+__device__ __forceinline__ float wave_nanmax_asc(float v) {
+  v = nan_max2(v, dpp_f32<kDppXor1>(v));
+  v = nan_max2(v, dpp_f32<kDppXor2>(v));
+  v = nan_max2(v, dpp_f32<kDppHalfMirror>(v));
+  v = nan_max2(v, dpp_f32<kDppMirror>(v));
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return nan_max2(nan_max2(r0, r1), nan_max2(r2, r3));
+}
+
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
