@@ -763,7 +763,7 @@ def run_packed(args, world, rank, device):
                          "achieved": round(u_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(u_gbps / HBM_PEAK_GBPS, 4),
                          "alg_bytes_per_launch": sbytes + 4 * n, "avg_launch_ms": round(u_ms, 5),
-                         "traffic": None}}
+                         "traffic": traffic_from_profile("packed")}}
 
 
 def _vgg_cifar():

@@ -601,10 +601,34 @@ __device__ __forceinline__ float rederive_q(const PackArgs& A, int64_t e) {
   return smaq_quant<RM, false, TIN, true>(load1<TIN>(A.x, e), u, c, hi, lo);
 }
 
+// OR a code chunk of up to 64 bits at bit pos of an LDS bit stream (two or three words; the third
+// only when bits land there, so it never passes the image; ORing 0 into the second is harmless).
+__device__ __forceinline__ void or_bits64(uint32_t* base, uint32_t pos, uint64_t chunk) {
+  const uint32_t sft = pos & 31u, w0 = pos >> 5;
+  const uint64_t lo = chunk << sft;
+  const uint32_t hi = sft ? (uint32_t)(chunk >> (64u - sft)) : 0u;
+  atomicOr(base + w0, (uint32_t)lo);
+  atomicOr(base + w0 + 1, (uint32_t)(lo >> 32));
+  if (hi) atomicOr(base + w0 + 2, hi);
+}
+
+// OR of each aligned group of 4 lanes, complete in the group's last lane (lane & 3 == 3).
+__device__ __forceinline__ uint32_t group4_or_to_last(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  return v;
+}
+
+// Emitter lane layout: lane t of the workgroup owns elements 2048 k + 8 t + i (k = 0, 1; i < 8), so
+// its 8 records per k are one 16-B load (8-B loads of 4 records ran at ~0.6x the 16-B rate) and one
+// 64-bit code chunk; segment 4 k + w (wave w) covers 512 consecutive elements.
+constexpr int kEmitK = 2;
+constexpr int kEmitE = 8;
+
 template <int RM, int TIN, bool FULL, int WM, int WO>
 __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
   extern __shared__ uint32_t stage[];  // [stage_words]: w[0], mask, code stream
-  __shared__ uint32_t seg_cnt[2][16];
+  __shared__ uint32_t seg_cnt[kEmitK * kBlock / kWave];
   __shared__ uint64_t s_prefix;
   constexpr bool kChunk = WO > 0 && WO <= 8;
   const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
@@ -614,21 +638,23 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
   const int n_el = FULL ? kPB : (int)(A.n - e0);
   uint32_t* codes_lds = stage + kHdrWords;
 
-  // records of this lane's 16 elements (el = 1024 k + 4 tid + i), two per register
-  uint32_t rw[4][2];
+  // records of this lane's 16 elements, two per register
+  uint32_t rw[kEmitK][4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int el = 1024 * k + 4 * tid;
-    if (FULL || el + 3 < n_el) {
-      const uint2 t = *reinterpret_cast<const uint2*>(A.rec + e0 + el);
+  for (int k = 0; k < kEmitK; ++k) {
+    const int el = 2048 * k + kEmitE * tid;
+    if (FULL || el + kEmitE <= n_el) {
+      const uint4 t = *reinterpret_cast<const uint4*>(A.rec + e0 + el);
       rw[k][0] = t.x;
       rw[k][1] = t.y;
+      rw[k][2] = t.z;
+      rw[k][3] = t.w;
     } else {
-      uint32_t r[4];
+      uint32_t r[kEmitE];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = (el + i < n_el) ? (uint32_t)A.rec[e0 + el + i] : 0u;
-      rw[k][0] = r[0] | (r[1] << 16);
-      rw[k][1] = r[2] | (r[3] << 16);
+      for (int i = 0; i < kEmitE; ++i) r[i] = (el + i < n_el) ? (uint32_t)A.rec[e0 + el + i] : 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rw[k][j] = r[2 * j] | (r[2 * j + 1] << 16);
     }
   }
   // block prefix: the group's prefix + the sizes of the group's earlier (full) blocks
@@ -643,84 +669,82 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
     if (lane == 0) s_prefix = A.gpre[g] + sz;
   }
 
-  // outlier / escape bits per float4 group (the codes themselves are decoded when placed)
-  uint32_t om[4], xm[4];
+  auto rec = [&](int k, int i) -> uint32_t { return (rw[k][i >> 1] >> (16 * (i & 1))) & 0xffffu; };
+  // outlier / escape bits per 8-element group (the codes themselves are decoded when placed)
+  uint32_t om[kEmitK], xm[kEmitK];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < kEmitK; ++k) {
     om[k] = 0u;
     xm[k] = 0u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t r = (rw[k][i >> 1] >> (16 * (i & 1))) & 0xffffu;
+    for (int i = 0; i < kEmitE; ++i) {
+      const uint32_t r = rec(k, i);
       om[k] |= (r >> 15) << i;
       xm[k] |= ((r >> 14) & 1u) << i;
     }
   }
   auto code_of = [&](int k, int i) -> uint32_t {
-    const uint32_t r = (rw[k][i >> 1] >> (16 * (i & 1))) & 0xffffu;
+    const uint32_t r = rec(k, i);
     const uint32_t side_code = ((r >> 13) & (r >> 15) & 1u) << (wo - 1);
     return ((r >> 14) & 1u) ? side_code : (r & 0x3fffu);
   };
 
-  // ranks, mask words and the LDS code stream: pack_body steps 2-3
-  // outlier and escape counts packed in one word (each <= 256 per wave) and scanned together by
-  // DPP; mask words: OR of 8 lanes' nibbles, written by each group's last lane
-  uint32_t pre_o[4], pre_x[4];
+  // ranks, mask words and the LDS code stream: outlier and escape counts packed in one word (each
+  // <= 512 per wave) and scanned together by DPP; a mask word is the OR of 4 lanes' bytes, written
+  // by each group's last lane
+  uint32_t pre_o[kEmitK], pre_x[kEmitK];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < kEmitK; ++k) {
     const uint32_t cnt = (uint32_t)__popc(om[k]) | ((uint32_t)__popc(xm[k]) << 16);
     const uint32_t incl = wave_incl_scan_u32(cnt);
     const uint32_t ex = incl - cnt;
     pre_o[k] = ex & 0xffffu;
     pre_x[k] = ex >> 16;
-    const uint32_t mw = group8_or_to_last(om[k] << (4 * (lane & 7)));
-    if ((lane & 7) == 7) stage[1 + ((1024 * k + 4 * (tid - 7)) >> 5)] = mw;
-    if (lane == kWave - 1) {
-      seg_cnt[0][4 * k + w] = incl & 0xffffu;
-      seg_cnt[1][4 * k + w] = incl >> 16;
-    }
+    const uint32_t mw = group4_or_to_last(om[k] << (8 * (lane & 3)));
+    if ((lane & 3) == 3) stage[1 + ((2048 * k + kEmitE * (tid - 3)) >> 5)] = mw;
+    if (lane == kWave - 1) seg_cnt[4 * k + w] = incl;
   }
   const uint32_t code_cap = A.stage_words - kHdrWords;
   for (uint32_t i = tid; i < code_cap; i += kBlock) codes_lds[i] = 0u;
   __syncthreads();
-  // every wave derives its segment prefixes from the 16 + 16 counts itself (no serial scan and
-  // no second barrier): segment 4 k + w starts after segments 0 .. 4 k + w - 1
-  // (lane s < 16 holds segment s's counts packed as outliers | escapes << 16, each <= 4096)
-  const uint32_t own = lane < 16 ? (seg_cnt[0][lane] | (seg_cnt[1][lane] << 16)) : 0u;
-  uint32_t incl = own;  // row 0 (lanes 0-15) scanned by DPP row shifts
+  // every wave derives its segment prefixes from the 8 counts itself (no serial scan and no
+  // second barrier): segment 4 k + w starts after segments 0 .. 4 k + w - 1 (lane s < 8 holds
+  // segment s's counts packed as outliers | escapes << 16, each <= 2048)
+  const uint32_t own = lane < kEmitK * 4 ? seg_cnt[lane] : 0u;
+  uint32_t incl = own;  // lanes 0-7 scanned by DPP row shifts
   incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xf, 0xf, false);
   incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xf, 0xf, false);
   incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xf, 0xf, false);
-  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x118, 0xf, 0xf, false);
   const uint32_t excl = incl - own;
-  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 15);
+  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kEmitK * 4 - 1);
   const uint32_t n_out = tot & 0xffffu, n_esc = tot >> 16;
-  uint32_t base_o[4], base_x[4];
+  uint32_t base_o[kEmitK], base_x[kEmitK];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < kEmitK; ++k) {
     const uint32_t b4 = (uint32_t)__builtin_amdgcn_readlane((int)excl, 4 * k + w);
     base_o[k] = b4 & 0xffffu;
     base_x[k] = b4 >> 16;
   }
   const uint32_t img_words = block_image_words(wm, wo, (uint32_t)n_el, n_out);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t el0 = 1024u * k + 4u * tid;
+  for (int k = 0; k < kEmitK; ++k) {
+    const uint32_t el0 = 2048u * k + kEmitE * tid;
     if (!FULL && (int)el0 >= n_el) continue;
     const uint32_t r0 = base_o[k] + pre_o[k];
     const uint32_t pos0 = (uint32_t)wm * el0 + (uint32_t)(wo - wm) * r0;
     if (kChunk) {
-      uint32_t chunk = 0u, off = 0u;
+      uint64_t chunk = 0u;
+      uint32_t off = 0u;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        chunk |= code_of(k, i) << off;
+      for (int i = 0; i < kEmitE; ++i) {
+        chunk |= (uint64_t)code_of(k, i) << off;
         off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
       }
-      or_bits(codes_lds, pos0, chunk);
+      or_bits64(codes_lds, pos0, chunk);
     } else {
       uint32_t off = 0u;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < kEmitE; ++i) {
         or_bits(codes_lds, pos0 + off, code_of(k, i));
         off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
       }
@@ -734,15 +758,15 @@ __global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
   for (uint32_t i = tid; i < img_words; i += kBlock)
     out[i] = i == 0 ? (n_out | (n_esc << 16)) : stage[i];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < kEmitK; ++k) {
     if (!xm[k]) continue;
     const uint32_t bx = base_x[k] + pre_x[k];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kEmitE; ++i) {
       if (!((xm[k] >> i) & 1u)) continue;
-      const uint32_t el = 1024u * k + 4u * tid + i;
+      const uint32_t el = 2048u * k + kEmitE * tid + i;
       const uint32_t r = bx + __popc(xm[k] & ((1u << i) - 1u));
-      const int qi = (int)(((rw[k][i >> 1] >> (16 * (i & 1))) & 0x1fffu) << 19) >> 19;
+      const int qi = (int)((rec(k, i) & 0x1fffu) << 19) >> 19;
       const float q = qi == kRecBig ? rederive_q<RM, TIN>(A, e0 + el) : (float)qi;
       out[img_words + 2 * r] = el;
       out[img_words + 2 * r + 1] = __float_as_uint(q);
