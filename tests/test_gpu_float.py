@@ -495,3 +495,28 @@ def test_s2fp8_single_launch_poisoned_workspace():
         y, st = g.s2fp8(x, seed=6, offset=1, ws=ws)
         assert st["gave_up"] == 0
         assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), i
+
+
+def test_s2fp8_single_launch_under_contention():
+    """The single launch beside GEMMs on another stream (CUs held by another kernel, so its
+    workgroups may not all be resident at once: the resident ones take the missing partials after
+    their patience runs out): every call still equals the uncontended one, and none gives up."""
+    g = _g()
+    n = 3 * 2**20
+    x = _s2_data(n, 123)
+    ref, _ = g.s2fp8(x, seed=3, offset=0)
+    a = torch.randn(4096, 4096, device="cuda") / 64.0
+    busy, work = torch.cuda.Stream(), torch.cuda.Stream()
+    busy.wait_stream(torch.cuda.current_stream())
+    work.wait_stream(torch.cuda.current_stream())
+    outs = []
+    with torch.cuda.stream(busy):
+        for _ in range(40):
+            a = torch.tanh(a @ a)
+    with torch.cuda.stream(work):
+        for _ in range(40):
+            outs.append(g.s2fp8(x, seed=3, offset=0))
+    torch.cuda.synchronize()
+    for y, st in outs:
+        assert st["gave_up"] == 0
+        assert torch.equal(y.view(torch.int32), ref.view(torch.int32))
