@@ -79,6 +79,10 @@ static int grid_for(int64_t work_items, int per_block_items, int cap) {
 // profiles/r02_kbench_cold_tile*.json), truncation prefers 1.
 constexpr int kStatsGridCap = 2048;  // also the number of fp64 partials the last workgroup sums
 constexpr int kStatsTileGrid = 512;  // tile-stride sweep: 2 workgroups per CU (launch_stats)
+// plain-load tail of an nt sweep (launch_stats): the Infinity Cache's size. 256M headline, two
+// interleaved rounds, ms/step: tail 0: 0.497 / 0.497; 128: 0.495 / 0.491; 160: 0.488 / 0.486;
+// 192: 0.484-0.490; 224: 0.488 / 0.489; 256: 0.488-0.492; 320: 0.484 / 0.488 (tools/tail_exp.sh)
+constexpr int64_t kStatsPlainTailMB = 256;
 constexpr int64_t kStatsNtMinMB = 512;  // non-temporal statistics loads from this tensor size on
 
 static inline bool aligned(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
@@ -88,7 +92,8 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
                                                             int vec, FinalizeArgs fin,
                                                             StatPartial* __restrict__ partials,
                                                             unsigned long long* counter,
-                                                            ArriveTag tag, SmqSmaqStats* out) {
+                                                            ArriveTag tag, SmqSmaqStats* out,
+                                                            int64_t nt_end) {
   __shared__ uint32_t arrive_slot;
   // Shift = median of three fixed elements: keeps sum(x-K)^2 - (sum(x-K))^2/n well conditioned
   // unless the mean is > 2^14 standard deviations away from all three.
@@ -112,12 +117,16 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
     float4 cur[4], nxt[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (t + u * kBlock < nv) cur[u] = NT ? load4_stream<TIN>(x, t + u * kBlock) : load4<TIN>(x, t + u * kBlock);
+      if (t + u * kBlock < nv)
+        cur[u] = (NT && t + u * kBlock < nt_end) ? load4_stream<TIN>(x, t + u * kBlock)
+                                                 : load4<TIN>(x, t + u * kBlock);
     for (; t < nv; t += tstride) {
       const int64_t tn = t + tstride;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (tn + u * kBlock < nv) nxt[u] = NT ? load4_stream<TIN>(x, tn + u * kBlock) : load4<TIN>(x, tn + u * kBlock);
+        if (tn + u * kBlock < nv)
+          nxt[u] = (NT && tn + u * kBlock < nt_end) ? load4_stream<TIN>(x, tn + u * kBlock)
+                                                    : load4<TIN>(x, tn + u * kBlock);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (t + u * kBlock < nv) {
@@ -495,17 +504,25 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
     return (int64_t)(e ? atoll(e) : kStatsNtMinMB) << 20;
   }();
   const bool nt = tile && 4 * n >= nt_min_bytes;
+  // with nt loads, the last plain_tail bytes of the sweep still load plain, so they stay in the
+  // Infinity Cache for the apply launch, which walks its tiles from the end (measurement knob
+  // SMQ_STATS_PLAIN_TAIL_MB)
+  static const int64_t plain_tail = [] {
+    const char* e = getenv("SMQ_STATS_PLAIN_TAIL_MB");
+    return (int64_t)(e ? atoll(e) : kStatsPlainTailMB) << 20;
+  }();
+  const int64_t nt_end = (n >> 2) - plain_tail / 16;
 #define SMQ_STATS(RANGE, TIN)                                                                       \
   do {                                                                                              \
     if (tile && nt)                                                                                 \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true, true>), dim3(grid), dim3(kBlock), 0,  \
-                         st, x, n, vec, fin, partials, counter, tag, hdr);                               \
+                         st, x, n, vec, fin, partials, counter, tag, hdr, nt_end);                     \
     else if (tile)                                                                                  \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true>), dim3(grid), dim3(kBlock), 0, st, x, \
-                         n, vec, fin, partials, counter, tag, hdr);                                      \
+                         n, vec, fin, partials, counter, tag, hdr, nt_end);                            \
     else                                                                                            \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n,    \
-                         vec, fin, partials, counter, tag, hdr);                                         \
+                         vec, fin, partials, counter, tag, hdr, nt_end);                               \
   } while (0)
   if (dtype == SMQ_DTYPE_F32) {
     if (p->use_range_std_dev) SMQ_STATS(true, kF32); else SMQ_STATS(false, kF32);
