@@ -79,6 +79,14 @@ static int grid_for(int64_t work_items, int per_block_items, int cap) {
 // profiles/r02_kbench_cold_tile*.json), truncation prefers 1.
 constexpr int kStatsGridCap = 2048;  // also the number of fp64 partials the last workgroup sums
 constexpr int kStatsTileGrid = 512;  // tile-stride sweep: 2 workgroups per CU (launch_stats)
+// Deferred statistics (defer_consts): at most kDeferMaxG statistics workgroups, whose partials
+// every apply workgroup loads (4 per lane of wave 0), on tensors of at most kDeferMaxN elements.
+// Back-to-back smq_smaq_roundtrip calls, fp32, us per call, off -> on (tools/defer_exp.sh, two
+// interleaved rounds): 64K 9.1 -> 8.0; 256K 9.4 -> 8.4; 1M 11.5 -> 10.2; 2M 13.2 -> 11.7; 4M 16.9 ->
+// 15.1; 8M 26.0 -> 23.6; 16M 40.1 -> 44.0; 32M 66.5 -> 79.6 (there the apply grid's partial
+// loads and the 256-workgroup sweep cost more than the hand-off they replace).
+constexpr int kDeferMaxG = 256;
+constexpr int64_t kDeferMaxN = 12ll << 20;
 // plain-load tail of an nt sweep (launch_stats): the Infinity Cache's size. 256M headline, two
 // interleaved rounds, ms/step: tail 0: 0.497 / 0.497; 128: 0.495 / 0.491; 160: 0.488 / 0.486;
 // 192: 0.484-0.490; 224: 0.488 / 0.489; 256: 0.488-0.492; 320: 0.484 / 0.488 (tools/tail_exp.sh)
@@ -93,7 +101,7 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
                                                             StatPartial* __restrict__ partials,
                                                             unsigned long long* counter,
                                                             ArriveTag tag, SmqSmaqStats* out,
-                                                            int64_t nt_end) {
+                                                            int64_t nt_end, double* def_rec) {
   __shared__ uint32_t arrive_slot;
   // Shift = median of three fixed elements: keeps sum(x-K)^2 - (sum(x-K))^2/n well conditioned
   // unless the mean is > 2^14 standard deviations away from all three.
@@ -164,13 +172,35 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
       finalize_stats<RANGE, TIN>(acc.s1, acc.s2, acc.mn, acc.mx, n, shift, false, fin, out);
     return;
   }
+  if (def_rec) {  // deferred statistics: the apply launch reduces the partials (defer_consts)
+    if (threadIdx.x == 0) {
+      StatPartial* p = partials + blockIdx.x;
+      p->s1 = acc.s1;
+      p->s2 = acc.s2;
+      if (RANGE) {
+        p->mn = acc.mn;
+        p->mx = acc.mx;
+      }
+      if (blockIdx.x == 0) {  // the shift, and the call's graph-safe stream position
+        unsigned long long base = 0ull;
+        if (fin.rng_ctr) {
+          base = *fin.rng_ctr;
+          *fin.rng_ctr = base + (unsigned long long)fin.rng_n;
+        }
+        def_rec[0] = shift;
+        def_rec[1] = __builtin_bit_cast(double, base);
+      }
+    }
+    return;
+  }
   if (threadIdx.x == 0) {
     StatPartial* p = partials + blockIdx.x;
     st_sc1_f64(&p->s1, acc.s1);
     st_sc1_f64(&p->s2, acc.s2);
     if (RANGE) st_sc1_f32x2(&p->mn, acc.mn, acc.mx);
   }
-  const uint32_t prev = block_arrive_tagged(counter, tag.tag, &arrive_slot);
+  const uint32_t prev = block_arrive_tagged(counter + (tag.tag & (SmaqWsLayout::kTagWords - 1)),
+                                            tag.tag, &arrive_slot);
   if (prev != gridDim.x - 1) return;
 
   // Last workgroup: ordered reduction of all partials (deterministic for a given n). Every load
@@ -204,7 +234,8 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
   block_reduce_stats<RANGE>(tot);
   if (threadIdx.x == 0) {
     finalize_stats<RANGE, TIN>(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, fin, out);
-    arrive_reset(counter, tag.next);  // the next call's tag, count 0
+    // the next call's tag, count 0, in the word that call will use
+    arrive_reset(counter + (tag.next & (SmaqWsLayout::kTagWords - 1)), tag.next);
   }
 }
 
@@ -231,8 +262,71 @@ struct ApplyArgs {
   const float* bn_gamma;         // BN variant
   const float* bn_beta;
   int64_t bn_channels, bn_inner;
+  const StatPartial* def_parts;  // deferred statistics (defer_consts): the statistics launch's
+  const double* def_rec;         // partials and {shift, stream position}; def_g partials, 0 = off
+  int def_g;
   int64_t sample_idx[SMQ_MAX_SAMPLES];
 };
+
+// Deferred statistics (smq_smaq_roundtrip on tensors up to kDeferMaxN elements): the statistics
+// launch leaves only its workgroup partials, and every apply workgroup reduces them itself — in
+// one fixed order, so every workgroup (and every call on the same n) gets the same totals — and
+// finalises. This replaces the hand-off in which the last statistics workgroup to arrive reduces
+// and finalises (partial store, arrival atomic, partial loads, header store: ~5 us of dependent
+// round trips, the larger part of a statistics launch on an activation-sized tensor). Wave 0
+// loads the partials after the workgroup's x loads are in flight and finalises in lane 0; the
+// other waves wait at an LDS-only barrier, their loads still outstanding. Workgroup 0 also
+// writes the header (log_size, read_stats).
+template <int TIN>
+__device__ __forceinline__ void defer_consts(const ApplyArgs& A, ElemConsts& c, uint64_t& off,
+                                          float cthr) {
+  __shared__ SmqSmaqStats sh;
+  if (threadIdx.x < kWave) {
+    constexpr int K = kDeferMaxG / kWave;
+    const int l = threadIdx.x;
+    double2 sv[K];
+    float2 mv[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int b = l + i * kWave;
+      if (b < A.def_g) {
+        sv[i] = *reinterpret_cast<const double2*>(&A.def_parts[b].s1);
+        if (A.use_range) mv[i] = *reinterpret_cast<const float2*>(&A.def_parts[b].mn);
+      }
+    }
+    double s1 = 0.0, s2 = 0.0;
+    float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      if (l + i * kWave < A.def_g) {
+        s1 += sv[i].x;
+        s2 += sv[i].y;
+        if (A.use_range) {
+          mn = fminf(mn, mv[i].x);
+          mx = fmaxf(mx, mv[i].y);
+        }
+      }
+    }
+    s1 = wave_sum_asc(s1);
+    s2 = wave_sum_asc(s2);
+    if (A.use_range) {
+      mn = wave_min(mn);
+      mx = wave_max(mx);
+    }
+    if (l == 0) {
+      const FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, nullptr, 0};
+      SmqSmaqStats st;
+      if (A.use_range) finalize_stats<true, TIN>(s1, s2, mn, mx, A.n, A.def_rec[0], false, f, &st);
+      else finalize_stats<false, TIN>(s1, s2, mn, mx, A.n, A.def_rec[0], false, f, &st);
+      st.rng_offset = __builtin_bit_cast(uint64_t, A.def_rec[1]);
+      sh = st;
+      if (blockIdx.x == 0) *A.ws_stats = st;
+    }
+  }
+  lds_barrier();
+  init_consts(c, &sh, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+  off = A.offset + sh.rng_offset;
+}
 
 template <bool BN>
 __device__ __forceinline__ BnTerm bn_term(const ApplyArgs& A, int64_t e) {
@@ -313,9 +407,9 @@ __global__ void smaq_prep_injected_kernel(const SmqSmaqStats* in, SmqSmaqStats* 
 // kBlock * TV float4 dispatched in (reverse) address order, one front across the grid.
 // SUB: see quot_check_for. The unaligned (!VEC) variant always keeps the subnormal check and
 // divides q / range by IEEE division (the launcher routes safe_q calls to it).
-template <int RM, bool VEC, bool BN, int TIN, int TV, bool AP, bool SUB>
-__device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemConsts& c,
-                                               uint64_t off) {
+template <int RM, bool VEC, bool BN, int TIN, int TV, bool AP, bool SUB, bool DEF = false>
+__device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, ElemConsts& c, uint64_t off,
+                                               float cthr) {
   constexpr int kTileElems = kBlock * TV * 4;
   uint32_t n_out = 0;
   const int64_t n = A.n;
@@ -336,6 +430,7 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, const ElemCon
         if (RM == kRoundUniform) uu[u] = u4[j];
       }
     }
+    if (DEF) defer_consts<TIN>(A, c, off, cthr);  // with this tile's loads in flight
 #pragma unroll
     for (int u = 0; u < TV; ++u) {
       const int64_t j = t0 + u * kBlock;
@@ -389,19 +484,25 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
   __shared__ uint32_t sh_cnt[kBlock / kWave];
   ElemConsts c;
   const float cthr = (BN || TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
-  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
-  const uint64_t off = A.offset + A.stats->rng_offset;  // + graph-safe stream position
   // uniform per launch: pick the body once (all_positive, subnormal-quotient check)
   uint32_t n_out;
-  if (!VEC) {
-    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c, off)
-                      : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c, off);
-  } else if (A.stats->quot_check) {
-    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c, off)
-                      : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c, off);
+  if (VEC && !BN && A.def_g) {
+    // deferred statistics: quot_check is not known before the loads, keep the check
+    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true, VEC && !BN>(A, c, 0, cthr)
+                      : apply_body<RM, VEC, BN, TIN, TV, false, true, VEC && !BN>(A, c, 0, cthr);
   } else {
-    n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, false>(A, c, off)
-                      : apply_body<RM, VEC, BN, TIN, TV, false, false>(A, c, off);
+    init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+    const uint64_t off = A.offset + A.stats->rng_offset;  // + graph-safe stream position
+    if (!VEC) {
+      n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c, off, cthr)
+                        : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c, off, cthr);
+    } else if (A.stats->quot_check) {
+      n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c, off, cthr)
+                        : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c, off, cthr);
+    } else {
+      n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, false>(A, c, off, cthr)
+                        : apply_body<RM, VEC, BN, TIN, TV, false, false>(A, c, off, cthr);
+    }
   }
 
   if (A.count) {  // outlier count for log_size (smart.py:184-188): one atomic per workgroup,
@@ -445,7 +546,7 @@ static size_t stats_ws_bytes(int64_t n) {
   (void)n;
   static_assert(SmaqWsLayout::kPartials + sizeof(StatPartial) * (size_t)kStatsGridCap ==
                     SMQ_WS_SAMPLES_OFFSET, "smq.h SMQ_WS_SAMPLES_OFFSET");
-  return SMQ_WS_SAMPLES_OFFSET + 8 * (size_t)SMQ_MAX_DEVICE_SAMPLES;
+  return SmaqWsLayout::kTagCounters + 8 * (size_t)SmaqWsLayout::kTagWords;
 }
 
 static int check_dtype(int dtype) {
@@ -456,16 +557,17 @@ static int check_dtype(int dtype) {
   return SMQ_OK;
 }
 
+// def_g != NULL: deferred statistics (defer_consts) — *def_g = the number of partials left for the
+// apply launch, or 0 when a single workgroup finalised the header itself.
 static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
-                        size_t ws_bytes, hipStream_t st) {
+                        size_t ws_bytes, hipStream_t st, int* def_g = nullptr) {
   if (!ws || ws_bytes < stats_ws_bytes(n)) {
     set_error("workspace too small: need %zu bytes, got %zu", stats_ws_bytes(n), ws_bytes);
     return SMQ_ERR_WORKSPACE;
   }
   char* base = (char*)ws;
   SmqSmaqStats* hdr = (SmqSmaqStats*)base;
-  unsigned long long* counter = (unsigned long long*)(base + SmaqWsLayout::kHeader);
-  const ArriveTag tag = arrive_tag(ws, st);
+  unsigned long long* counter = (unsigned long long*)(base + SmaqWsLayout::kTagCounters);
   StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
   const int vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) ? 1 : 0;
   // fp32 sweeps tile-stride (smaq_stats_kernel<.., TILE>) on at most kStatsTileGrid workgroups;
@@ -492,7 +594,15 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
     const int v = e ? atoi(e) : kBlock * 4 * 16;
     return v >= kBlock * 4 ? v : kBlock * 4 * 16;
   }();
-  const int grid = grid_for(n, per_wg, cap);
+  const int grid = grid_for(n, per_wg, def_g && cap > kDeferMaxG ? kDeferMaxG : cap);
+  double* def_rec = nullptr;
+  ArriveTag tag{};
+  if (def_g) {
+    *def_g = grid > 1 ? grid : 0;
+    if (grid > 1) def_rec = (double*)(base + SmaqWsLayout::kDeferRec);
+  }
+  // the host's tag prediction follows the calls that use the arrival counter
+  if (!def_rec) tag = arrive_tag(ws, st);
   FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n),
                    (unsigned long long*)p->offset_counter, n};
   // non-temporal loads only for tensors well beyond the Infinity Cache: there they keep the
@@ -516,13 +626,13 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   do {                                                                                              \
     if (tile && nt)                                                                                 \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true, true>), dim3(grid), dim3(kBlock), 0,  \
-                         st, x, n, vec, fin, partials, counter, tag, hdr, nt_end);                     \
+                         st, x, n, vec, fin, partials, counter, tag, hdr, nt_end, def_rec);         \
     else if (tile)                                                                                  \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true>), dim3(grid), dim3(kBlock), 0, st, x, \
-                         n, vec, fin, partials, counter, tag, hdr, nt_end);                            \
+                         n, vec, fin, partials, counter, tag, hdr, nt_end, def_rec);                \
     else                                                                                            \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n,    \
-                         vec, fin, partials, counter, tag, hdr, nt_end);                               \
+                         vec, fin, partials, counter, tag, hdr, nt_end, def_rec);                   \
   } while (0)
   if (dtype == SMQ_DTYPE_F32) {
     if (p->use_range_std_dev) SMQ_STATS(true, kF32); else SMQ_STATS(false, kF32);
@@ -635,7 +745,7 @@ static int launch_draw_stats(const void* x, int dtype, int64_t n, const SmqSmaqP
 
 static int launch_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                         const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
-                        size_t ws_bytes, hipStream_t st) {
+                        size_t ws_bytes, hipStream_t st, int def_g = 0) {
   if (!ws || ws_bytes < SmaqWsLayout::kPartials) {
     set_error("workspace too small: need >= %zu bytes", (size_t)SmaqWsLayout::kPartials);
     return SMQ_ERR_WORKSPACE;
@@ -663,6 +773,12 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   A.all_pos = p->all_positive;
   A.count = p->count_outliers;
   A.use_range = p->use_range_std_dev;
+  if (def_g) {  // the statistics launch left def_g partials (launch_stats)
+    A.def_parts = (const StatPartial*)((const char*)ws + SmaqWsLayout::kPartials);
+    A.def_rec = (const double*)((const char*)ws + SmaqWsLayout::kDeferRec);
+    A.def_g = def_g;
+    A.range_coef = range_coef_for(p, n);
+  }
   if (p->bn_gamma) {
     if (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1) {
       set_error("BN variant needs bn_beta, bn_channels >= 1 and bn_inner >= 1");
@@ -872,20 +988,36 @@ int smq_smaq_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqP
   return launch_apply(x, dtype, y, n, p, uniforms, stats_in, ws, ws_bytes, (hipStream_t)stream);
 }
 
+// Deferred statistics need the vector apply body without the BN term (defer_consts).
+static bool defer_eligible(const void* x, int dtype, const float* y, int64_t n,
+                           const SmqSmaqParams* p, const float* uniforms) {
+  static const int64_t max_n = [] {  // measurement knob SMQ_DEFER_MAX_N (elements; 0 = off)
+    const char* e = getenv("SMQ_DEFER_MAX_N");
+    return e ? (int64_t)atoll(e) : kDeferMaxN;
+  }();
+  if (n > max_n || p->bn_gamma) return false;
+  if (!aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) || !aligned(y, 16)) return false;
+  if (p->stochastic_rounding && uniforms && !aligned(uniforms, 16)) return false;
+  return !range_recips(p->range_main, p->range_outlier).safe_q;
+}
+
 int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                        const float* uniforms, void* ws, size_t ws_bytes, void* stream) {
   int rc = validate_params(p);
   if (!rc) rc = check_dtype(dtype);
   if (!rc) rc = check_tensor_args(x, y, n);
   if (rc) return rc;
+  int def_g = 0;
   if (p->stats_source == SMQ_STATS_WORKSPACE) {
-    rc = launch_stats(x, dtype, n, p, ws, ws_bytes, (hipStream_t)stream);
+    rc = launch_stats(x, dtype, n, p, ws, ws_bytes, (hipStream_t)stream,
+                      defer_eligible(x, dtype, y, n, p, uniforms) ? &def_g : nullptr);
     if (rc) return rc;
   } else if (p->stats_source == SMQ_STATS_INJECTED) {
     set_error("roundtrip: use smq_smaq_apply for injected statistics");
     return SMQ_ERR_INVALID;
   }
-  return launch_apply(x, dtype, y, n, p, uniforms, nullptr, ws, ws_bytes, (hipStream_t)stream);
+  return launch_apply(x, dtype, y, n, p, uniforms, nullptr, ws, ws_bytes, (hipStream_t)stream,
+                      def_g);
 }
 
 int smq_smaq_stats_f32(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,

@@ -272,9 +272,15 @@ struct alignas(32) StatPartial {
 // Workspace layout of a single-tensor SmaQ call.
 struct SmaqWsLayout {
   static constexpr size_t kHeader = 64;     // SmqSmaqStats
-  static constexpr size_t kCounter = 64;    // arrival counter (own 64-B line)
+  static constexpr size_t kDeferRec = kHeader;  // {shift, stream position} (deferred statistics)
   static constexpr size_t kSlots = SMQ_WS_OUTLIER_SLOTS_OFFSET;  // uint64[SMQ_WS_OUTLIER_SLOTS]
   static constexpr size_t kPartials = kSlots + 8 * SMQ_WS_OUTLIER_SLOTS;  // StatPartial[grid]
+  // tagged arrival counters, one per tag residue: a call with tag t arrives on word t % kTagWords
+  // and leaves (next, 0) in word next % kTagWords. Eager calls take consecutive tags (next = t + 1);
+  // a call captured into a graph keeps its tag (next = t), so up to kTagWords calls on one
+  // workspace captured into one graph each find their own word on every replay.
+  static constexpr size_t kTagCounters = SMQ_WS_SAMPLES_OFFSET + 8 * SMQ_MAX_DEVICE_SAMPLES;
+  static constexpr int kTagWords = 64;
 };
 
 // Inclusive wave64 prefix sum by DPP row shifts and row broadcasts (GFX9 rows of 16 lanes; the

@@ -347,7 +347,17 @@ def workspace(kind: str, device: torch.device, nbytes: int, stream: int = None) 
     with _ws_lock:
         buf = _ws.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
+            # Allocated while a graph is being captured, a zero-fill would become a graph node
+            # that clears the buffer on every replay: each replay's calls would then find their
+            # arrival counters cleared and take the slow re-tagging path (include/smq.h: the
+            # SmaQ and S2FP8 workspaces need no initialisation). The packed codec's look-back
+            # status words do need it; for them a per-replay clear is only a redundant memset.
+            capturing = (torch.device(device).type == "cuda"
+                         and torch.cuda.is_current_stream_capturing())
+            if capturing and kind in ("smaq", "s2fp8"):
+                buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+            else:
+                buf = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
             _ws[key] = buf
     return buf
 

@@ -261,6 +261,12 @@ class SmartFP(CompressionAlgorithmBase):
         lib = N.lib()
         st = N.stream_ptr(x.device) if st is None else st
         tr = self._trace
+        if tr is None and p.stats_source == N.SMQ_STATS_WORKSPACE:
+            # one entry point for both launches: it may defer the statistics' final reduction
+            # into the apply launch (smaq.hip defer_consts)
+            N.check(lib.smq_smaq_roundtrip(x.data_ptr(), code, y.data_ptr(), numel, p, None,
+                                           ws.data_ptr(), ws.numel(), st), "smq_smaq_roundtrip")
+            return
         if p.stats_source == N.SMQ_STATS_WORKSPACE:
             N.check(lib.smq_smaq_stats(x.data_ptr(), code, numel, p, ws.data_ptr(), ws.numel(), st),
                     "smq_smaq_stats")

@@ -192,3 +192,42 @@ def test_optimizer_step_graph_safe_matches_host():
     assert oh == od
     for a, b in zip(ph, pd):
         assert torch.equal(_bits(a), _bits(b))
+
+
+def test_workspace_created_in_capture_keeps_counters_across_replays():
+    """A SmaQ workspace first requested while a graph is being captured (torch.cuda.graph's own
+    capture stream) is allocated without a zero-fill node: replays leave its arrival counters as
+    the last replay set them, so every call finds its own tag (a cleared word sent all 60 calls of
+    the VGG autograd graph down the re-tagging path: 14 -> 53 us per 512-workgroup statistics
+    launch). Outputs still equal the host-offset calls."""
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.smart import SmartFP
+
+    n = 13 << 20  # above the deferred-statistics limit: the statistics launch counts arrivals
+    x1 = torch.randn(n, device="cuda")
+    x2 = torch.randn(n, device="cuda") * 3
+    dev = SmartFP(smaq_hparams())
+    dev.rng.seed, dev.rng.offset = 5, 0
+    dev.graph_safe(device="cuda")
+    host = SmartFP(smaq_hparams())
+    host.rng.seed, host.rng.offset = 5, 0
+    before = {k for k in N._ws if k[0] == "smaq"}
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y1 = dev(x1)
+        y2 = dev(x2)
+    new = [N._ws[k] for k in N._ws if k[0] == "smaq" and k not in before]
+    assert len(new) == 1
+    ws = new[0]
+    sentinel = N.SMQ_WS_SAMPLES_OFFSET + 8 * N.SMQ_MAX_DEVICE_SAMPLES - 1  # only device draws write it
+    ws[sentinel] = 0xA5
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(ws[sentinel]) == 0xA5  # no captured clear of the workspace
+    refs = []
+    for _ in range(2):
+        refs += [host(x1), host(x2)]
+    torch.cuda.synchronize()
+    # replay 2 equals the host's 3rd and 4th calls
+    assert torch.equal(_bits(y1), _bits(refs[2])) and torch.equal(_bits(y2), _bits(refs[3]))

@@ -451,3 +451,52 @@ def test_graph_safe_stream_eager_and_captured():
     for o, r in zip(outs, refs):
         assert torch.equal(o.view(torch.int32), r.view(torch.int32))
     assert not torch.equal(outs[0], outs[1])  # fresh randomness per replay
+
+
+@pytest.mark.parametrize("n", [65536 + 5, 1 << 20, 5 * (1 << 20) + 3, 9 * (1 << 20), 40 << 20])
+@pytest.mark.parametrize("mode", ["sr", "trunc", "range", "f16", "bf16", "allpos", "counter"])
+def test_deferred_statistics_equal_two_call_path(n, mode):
+    """smq_smaq_roundtrip on tensors up to kDeferMaxN (12M) reduces the statistics partials in
+    every apply workgroup (smaq.hip defer_consts) instead of in the last statistics workgroup.
+    Outputs, header and graph-safe stream position equal the separate smq_smaq_stats +
+    smq_smaq_apply calls bit for bit (the two reductions differ only in fp64 summation order);
+    40M runs the non-deferred path through the same entry point."""
+    from smart_compress_amd import _native as N
+
+    g = _gpu()
+    gen = torch.Generator(device="cuda").manual_seed(n % 1000 + len(mode))
+    dt = {"f16": torch.float16, "bf16": torch.bfloat16}.get(mode, torch.float32)
+    x = (torch.randn(n, generator=gen, device="cuda") * 1.3 - 0.2)
+    if mode == "allpos":
+        x = x.abs()
+    x = x.to(dt)
+    hp = smaq_hparams(stochastic_rounding=mode != "trunc", use_range_std_dev=mode == "range")
+    outs, hdrs, ctrs = [], [], []
+    for split in (False, True):
+        p = g.smaq_params(hp, n, all_positive=mode == "allpos", seed=99, offset=12345, dtype=dt)
+        ctr = None
+        if mode == "counter":
+            ctr = torch.tensor([1 << 33], dtype=torch.int64, device="cuda")
+            p.offset_counter = ctr.data_ptr()
+        y = torch.empty(n, dtype=torch.float32, device="cuda")
+        ws = torch.zeros(N.lib().smq_smaq_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+        args = (x.data_ptr(), N.DTYPE_CODES[dt])
+        if split:
+            N.check(N.lib().smq_smaq_stats(*args, n, p, ws.data_ptr(), ws.numel(), g.stream()),
+                    "stats")
+            N.check(N.lib().smq_smaq_apply(*args, y.data_ptr(), n, p, None, None, ws.data_ptr(),
+                                           ws.numel(), g.stream()), "apply")
+        else:
+            N.check(N.lib().smq_smaq_roundtrip(*args, y.data_ptr(), n, p, None, ws.data_ptr(),
+                                               ws.numel(), g.stream()), "roundtrip")
+        torch.cuda.synchronize()
+        outs.append(y)
+        hdrs.append(g.read_stats(ws))
+        ctrs.append(None if ctr is None else int(ctr.item()))
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    for k in ("mean", "std_dev", "std_clamped", "raw_std", "n_used"):
+        assert hdrs[0][k] == hdrs[1][k], k
+    if mode == "range":
+        assert hdrs[0]["min"] == hdrs[1]["min"] and hdrs[0]["max"] == hdrs[1]["max"]
+    if mode == "counter":
+        assert ctrs[0] == ctrs[1] == (1 << 33) + n

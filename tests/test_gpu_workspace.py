@@ -16,13 +16,25 @@ pytestmark = pytest.mark.gpu
 POISON = [0xFFFFFFFFFFFFFFF0, (0x7FFFFFF0 << 32) | 5, 3, 0x7FFFFFFF00000000 | 12345, 1 << 63]
 
 
+def _counter_words(ws):
+    """The 64 tagged arrival counters at the end of the single-tensor workspace (smq.h layout)."""
+    from smart_compress_amd import _native as N
+
+    off = N.SMQ_WS_SAMPLES_OFFSET + 8 * N.SMQ_MAX_DEVICE_SAMPLES
+    return off, off + 8 * 64
+
+
 def _poison_counter(ws, value):
-    v = np.array([value], dtype=np.uint64).view(np.uint8)
-    ws[64:72] = torch.from_numpy(v.copy()).to(ws.device)
+    lo, hi = _counter_words(ws)
+    v = np.full(64, value, dtype=np.uint64).view(np.uint8)
+    ws[lo:hi] = torch.from_numpy(v.copy()).to(ws.device)
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("n", [(1 << 22) + 1, 1 << 24, 5000])
-def test_stats_after_poisoned_counter(n):
+def test_stats_after_poisoned_counter(n, split):
+    """split: smq_smaq_stats + smq_smaq_apply (the statistics launch always hands off through a
+    counter); else smq_smaq_roundtrip, which defers the reduction below 12M elements."""
     import gpu_calls as g
     from oracle import rng as orng
     from oracle import smaq as osmaq
@@ -39,17 +51,26 @@ def test_stats_after_poisoned_counter(n):
         if poison is not None:
             _poison_counter(ws, poison)
         p = g.smaq_params(hp, n, seed=4, offset=i * n)
-        N.check(N.lib().smq_smaq_roundtrip(x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p,
-                                           None, ws.data_ptr(), ws.numel(), g.stream()), "rt")
+        if split:
+            N.check(N.lib().smq_smaq_stats(x.data_ptr(), N.SMQ_DTYPE_F32, n, p, ws.data_ptr(),
+                                           ws.numel(), g.stream()), "stats")
+            N.check(N.lib().smq_smaq_apply(x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p,
+                                           None, None, ws.data_ptr(), ws.numel(), g.stream()),
+                    "apply")
+        else:
+            N.check(N.lib().smq_smaq_roundtrip(x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p,
+                                               None, ws.data_ptr(), ws.numel(), g.stream()), "rt")
         torch.cuda.synchronize()
         st = g.read_stats(ws)
         assert ulp_diff(st["mean"], mo) <= 1 and ulp_diff(st["raw_std"], so) <= 1, (i, st)
         y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], osmaq.SmaqConfig(),
                               orng.uniforms(4, i * n, n))
         assert same_f32(y.cpu().numpy(), y_or), i
-    # the counter is left tagged with a zero count
-    word = int(ws[64:72].cpu().numpy().view(np.uint64)[0])
-    assert word & 0xFFFFFFFF == 0 and word >> 32 != 0
+    # a call that counted arrivals leaves the next call's word tagged with a zero count
+    lo, hi = _counter_words(ws)
+    words = [int(w) for w in ws[lo:hi].cpu().numpy().view(np.uint64)]
+    if split and n > 5000:
+        assert any(w & 0xFFFFFFFF == 0 and w >> 32 != 0 for w in words)
 
 
 def test_multi_after_poisoned_workspace():

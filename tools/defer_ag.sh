@@ -1,0 +1,10 @@
+#!/bin/bash
+# Autograd config (VGG b128, SmaQ on every activation and gradient) with deferred statistics
+# off (SMQ_DEFER_MAX_N=0) and on, interleaved.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+for r in 1 2; do for m in 0 default; do
+  if [ $m = 0 ]; then export SMQ_DEFER_MAX_N=0; else unset SMQ_DEFER_MAX_N; fi
+  timeout -k 10 240 python bench.py --config autograd > gpurun_out/dag_${m}_$r.log 2>&1 || exit 1
+  python -c "import json;d=json.loads(open('gpurun_out/dag_${m}_$r.log').read().strip().splitlines()[-1]);print('defer=$m run $r', d['value'], d['ms_per_step'], {k: v for k, v in d.items() if 'ms' in k})"
+done; done
