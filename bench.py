@@ -420,7 +420,16 @@ def run_smaq(args, world, rank, device):
     gen = torch.Generator(device=device).manual_seed(rank)
     # two input tensors, alternated per step, so a step never finds the previous step's input in
     # the 256 MB Infinity Cache (in training every call sees a different tensor)
-    xs = [torch.randn(n, generator=gen, device=device) for _ in range(2)]
+    # SMQ_BENCH_DIST=laplace: C2's heavy-tailed variant, Laplace(0, 1) as the
+    # difference of two Exp(1) draws
+    dist = os.environ.get("SMQ_BENCH_DIST", "normal")
+    if dist == "laplace":
+        xs = []
+        for _ in range(2):
+            x = -torch.log1p(-torch.rand(n, generator=gen, device=device))
+            xs.append(x.sub_(-torch.log1p(-torch.rand(n, generator=gen, device=device))))
+    else:
+        xs = [torch.randn(n, generator=gen, device=device) for _ in range(2)]
     # measurement knob SMQ_BENCH_DTYPE=f16|bf16: half-precision inputs (statistics and apply read
     # 2 B/elem, the output stays fp32: 8 B/elem of algorithmic traffic)
     in_dt = {"f16": torch.float16, "bf16": torch.bfloat16}.get(os.environ.get("SMQ_BENCH_DTYPE", ""))
@@ -469,7 +478,8 @@ def run_smaq(args, world, rank, device):
                    "smaq_6_8_roundtrip_sampled_stats", "elements_per_gpu": n,
                    "stats": "sampled(16)" if sampled else "full", "rounding": "stochastic",
                    "bits": "6/8", "alg_bytes_per_elem": alg_per_elem,
-                   "parallelism": f"replicas{world}"},
+                   "parallelism": f"replicas{world}",
+                   **({"dist": dist} if dist != "normal" else {})},
         "pct_hbm_peak": round(100.0 * value / world / HBM_PEAK_GBPS, 2),
         # the same time read as tensor GB/s (in_bytes * n per step) and as HBM-read
         # GB/s (statistics read + apply read: the north star's "HBM-read roofline" reading)

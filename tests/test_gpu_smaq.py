@@ -307,6 +307,40 @@ def test_full_size_256m_windows():
     assert abs((y - x).double().mean().item()) < 1e-4  # unbiased SR
 
 
+def _laplace(n, seed, device="cuda"):
+    """Laplace(0, 1) as the difference of two Exp(1) draws -log1p(-U), U in [0, 1) (SURVEY 8d
+    C2's heavy-tailed variant; finite for every U)."""
+    gen = torch.Generator(device=device).manual_seed(seed)
+    x = -torch.log1p(-torch.rand(n, generator=gen, device=device))
+    return x.sub_(-torch.log1p(-torch.rand(n, generator=gen, device=device)))
+
+
+def test_full_size_256m_laplace_windows():
+    """C2's heavy-tailed variant at full size: Laplace(0, 1) puts ~24 % of the elements beyond
+    1 std and a long tail beyond T_o = 2.5 std (outliers the 8-bit range clips). Statistics vs
+    fp64, windows incl. the ragged tail vs the oracle, outlier fraction vs the Laplace law."""
+    from smart_compress_amd.compress.smart import SmartFP
+
+    n = 1 << 28
+    x = _laplace(n, 7)
+    hp = smaq_hparams()
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = 5, 0
+    y = codec(x)
+    torch.cuda.synchronize()
+    st = _gpu().read_stats(_smaq_ws())
+    xd = x.double()
+    assert ulp_diff(st["mean"], np.float32(xd.mean().item())) <= 1
+    assert ulp_diff(st["raw_std"], np.float32(xd.std().item())) <= 1
+    del xd
+    for lo, hi in [(0, 1 << 16), (n // 3, n // 3 + 77777), (n - (1 << 16) - 1, n)]:
+        _oracle_window(x[lo:hi].cpu().numpy(), y, st, hp, lo, hi)
+    # P(|x| > sqrt(2)) = exp(-sqrt(2)) for Laplace(0, 1) (std sqrt(2))
+    frac_out = ((x - st["mean"]).abs() / st["std_clamped"] > 1.0).float().mean().item()
+    assert abs(frac_out - float(np.exp(-np.sqrt(2.0)))) < 0.002
+    assert abs((y - x).double().mean().item()) < 1e-4
+
+
 def _oracle_window(xw, y, st, hp, lo, hi):
     from oracle import rng as orng
     from oracle import smaq as osmaq
