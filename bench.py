@@ -711,7 +711,8 @@ def run_packed(args, world, rank, device):
     from smart_compress_amd.compress.packed import SmartFPPacked
 
     n = args.elements or (1 << 28)
-    hp = smaq_hparams()
+    # measurement knob SMQ_BENCH_SR=0: truncation instead of stochastic rounding
+    hp = smaq_hparams(stochastic_rounding=os.environ.get("SMQ_BENCH_SR", "1") != "0")
     codec = SmartFPPacked(hp)
     codec.rng.seed = 2000 + rank
     gen = torch.Generator(device=device).manual_seed(rank)

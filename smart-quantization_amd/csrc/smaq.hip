@@ -62,6 +62,16 @@ ArriveTag arrive_tag(const void* ws, hipStream_t st) {
   return t;
 }
 
+// measurement knob SMQ_HALF_TILE=0: fp16 / bf16 inputs keep 8-B loads (grid-stride statistics
+// sweep, one float4 of elements per apply slot)
+static bool half_tile_env() {
+  static const bool v = [] {
+    const char* e = getenv("SMQ_HALF_TILE");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 static int grid_for(int64_t work_items, int per_block_items, int cap) {
   int64_t g = (work_items + per_block_items - 1) / per_block_items;
   if (g < 1) g = 1;
@@ -114,7 +124,43 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
   StatAcc acc, ay, az, aw;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (vec && TILE) {
+  if (TIN != kF32 && vec == 2 && TILE) {
+    // fp16 / bf16 on a 16-B aligned pointer: the same tile-stride sweep with one 16-B load of 8
+    // elements per lane and slot (tiles of kBlock * 4 such loads, the next tile's in flight)
+    const int64_t n8 = n >> 3;
+    constexpr int64_t kT = (int64_t)kBlock * 4;
+    const int64_t tstride = (int64_t)gridDim.x * kT;
+    int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x;
+    uint4 cur[4], nxt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (t + u * kBlock < n8) cur[u] = static_cast<const uint4*>(x)[t + u * kBlock];
+    for (; t < n8; t += tstride) {
+      const int64_t tn = t + tstride;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (tn + u * kBlock < n8) nxt[u] = static_cast<const uint4*>(x)[tn + u * kBlock];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (t + u * kBlock < n8) {
+          float4 a, b;
+          const uint2 lo = make_uint2(cur[u].x, cur[u].y), hi = make_uint2(cur[u].z, cur[u].w);
+          a = load4<TIN>(&lo, 0);
+          b = load4<TIN>(&hi, 0);
+          acc.add<RANGE>(a.x, shift);
+          ay.add<RANGE>(a.y, shift);
+          az.add<RANGE>(a.z, shift);
+          aw.add<RANGE>(a.w, shift);
+          acc.add<RANGE>(b.x, shift);
+          ay.add<RANGE>(b.y, shift);
+          az.add<RANGE>(b.z, shift);
+          aw.add<RANGE>(b.w, shift);
+        }
+        cur[u] = nxt[u];
+      }
+    }
+    i = (n8 << 3) + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  } else if (vec && TILE) {
     // tile-stride: workgroup w sweeps tiles w, w + G, ... of kBlock * 4 float4 (16 KiB, one
     // contiguous piece per workgroup and step, one front across the grid); the next tile's four
     // loads are issued before the current tile is consumed (8 loads per lane in flight at most)
@@ -575,12 +621,17 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   // 0.542 ms/step; tile-stride at 1024 / 768 / 640 / 512 / 384 / 256 workgroups 0.529 / 0.528 /
   // 0.528 / 0.515 / 0.522 / 0.589 — at 512 (2 per CU, 8 dwordx4 per lane in flight) the sweep
   // takes 169 us instead of 184, and the apply launch after it 335 us instead of 352. fp16 / bf16
-  // inputs (8-B loads) keep the grid-stride sweep (not measured in tile form).
+  // inputs on a 16-B aligned x sweep tile-stride too, with one 16-B load of 8 elements per lane and
+  // slot (256M: 112 -> 90 us, 0.422-0.431 -> 0.407-0.408 ms/step fp16, tools/half_tile.sh; with
+  // 8-B loads the tile form had lost, 0.636 vs 0.463); an 8-B aligned x keeps the grid-stride sweep.
   static const int tile_env = [] {  // measurement knob SMQ_STATS_TILE=0: grid-stride sweep
     const char* e = getenv("SMQ_STATS_TILE");
     return e ? atoi(e) : 1;
   }();
-  const bool tile = tile_env != 0 && dtype == SMQ_DTYPE_F32;
+  // half inputs take the tile sweep with 16-B loads when x is 16-B aligned (vec = 2)
+  const bool x16 = dtype != SMQ_DTYPE_F32 && aligned(x, 16) && half_tile_env();
+  const bool tile = tile_env != 0 && (dtype == SMQ_DTYPE_F32 || x16);
+  const int vec_arg = x16 ? 2 : vec;
   static const int grid_env = [] {  // measurement knob SMQ_STATS_GRID (64 .. kStatsGridCap)
     const char* e = getenv("SMQ_STATS_GRID");
     const int v = e ? atoi(e) : 0;
@@ -626,13 +677,13 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   do {                                                                                              \
     if (tile && nt)                                                                                 \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true, true>), dim3(grid), dim3(kBlock), 0,  \
-                         st, x, n, vec, fin, partials, counter, tag, hdr, nt_end, def_rec);         \
+                         st, x, n, vec_arg, fin, partials, counter, tag, hdr, nt_end, def_rec);         \
     else if (tile)                                                                                  \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN, true>), dim3(grid), dim3(kBlock), 0, st, x, \
-                         n, vec, fin, partials, counter, tag, hdr, nt_end, def_rec);                \
+                         n, vec_arg, fin, partials, counter, tag, hdr, nt_end, def_rec);                \
     else                                                                                            \
       hipLaunchKernelGGL((smaq_stats_kernel<RANGE, TIN>), dim3(grid), dim3(kBlock), 0, st, x, n,    \
-                         vec, fin, partials, counter, tag, hdr, nt_end, def_rec);                   \
+                         vec_arg, fin, partials, counter, tag, hdr, nt_end, def_rec);                   \
   } while (0)
   if (dtype == SMQ_DTYPE_F32) {
     if (p->use_range_std_dev) SMQ_STATS(true, kF32); else SMQ_STATS(false, kF32);
@@ -670,6 +721,8 @@ static void launch_apply_t(const ApplyArgs& A, int rm, bool vec, bool bn, int tv
   } while (0)
   if (vec && !bn && rm == kRoundHash && tv == 2) {
     SMQ_APPLY(kRoundHash, true, false, 2);
+  } else if (TIN != kF32 && vec && !bn && rm == kRoundHash && tv == 4) {
+    SMQ_APPLY(kRoundHash, true, false, 4);
   } else if (vec) {
     if (bn) SMQ_APPLY_RM(true, true); else SMQ_APPLY_RM(true, false);
   } else {
@@ -820,7 +873,16 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
     return (int64_t)(e ? atoll(e) : kStatsNtMinMB) << 20;
   }();
   A.nt_loads = (int64_t)(dtype == SMQ_DTYPE_F32 ? 4 : 2) * n >= apply_nt_min ? 1 : 0;
-  const int tv = (rm == kRoundHash && vec && !A.bn_gamma) ? sr_tile_v() : 1;
+  int tv = (rm == kRoundHash && vec && !A.bn_gamma) ? sr_tile_v() : 1;
+  // bf16 inputs: 8-B loads, so twice the slots for the bytes in flight per lane of fp32. 256M, two
+  // interleaved rounds, ms/step (tools/half_tv.sh): bf16 2 slots 0.401-0.404, 4 slots 0.384-0.390;
+  // fp16 0.4016 / 0.4016 vs 0.403 / 0.407 (its cvt-based element chain gains nothing), so 2
+  static const int half_tv = [] {  // measurement knob SMQ_HALF_TV (2 | 4): both half types
+    const char* e = getenv("SMQ_HALF_TV");
+    return e ? (atoi(e) == 4 ? 4 : 2) : 0;
+  }();
+  if (tv == 2 && dtype != SMQ_DTYPE_F32)
+    tv = half_tv ? half_tv : (dtype == SMQ_DTYPE_BF16 ? 4 : 2);
   const int64_t tile_elems = (int64_t)kBlock * 4 * tv;
   const int64_t tiles = (n + tile_elems - 1) / tile_elems;
   if (tiles > 0x7fffffffLL) {
