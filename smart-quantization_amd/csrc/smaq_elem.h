@@ -64,15 +64,6 @@ __device__ __forceinline__ float4 load4(const void* p, int64_t j) {
   return o;
 }
 
-// fp16 / bf16 elements 8j .. 8j+7 with one 16-B load, as two float4 (4j' = 8j and 8j + 4)
-template <int T>
-__device__ __forceinline__ void load8(const void* p, int64_t j, float4& a, float4& b) {
-  const uint4 w = static_cast<const uint4*>(p)[j];
-  const uint2 lo = make_uint2(w.x, w.y), hi = make_uint2(w.z, w.w);
-  a = load4<T>(&lo, 0);
-  b = load4<T>(&hi, 0);
-}
-
 // Streaming read of a tensor no later kernel of the call reads again (nt: bypasses L1, measured
 // faster for the statistics sweep, the SmaQ apply and the float quantiser; NOT for kernels whose
 // input the next launch re-reads, e.g. the S2FP8 partials -3 %, nor the multi-tensor chunks -0.8 %).
