@@ -311,9 +311,11 @@ template <int TIN>
 __device__ __forceinline__ void s2_reduce_partials(const S2Partial* __restrict__ partials, int P,
                                                    int64_t n, SmqS2fp8Stats* hdr,
                                                    SmqS2fp8Stats* st) {
-  __shared__ double shs[kBlock / kWave];
-  __shared__ float shm[kBlock / kWave];
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  // order (shared with s2fp8_fused_kernel): lane l of one wave adds partials l, l + 64, l + 128,
+  // l + 192 as (p0 + p1) + (p2 + p3), then one ascending butterfly over the 64 lanes
+  static_assert(kBlock == 4 * kWave, "one partial per thread, four per lane of wave 0");
+  __shared__ double shs[kBlock];
+  __shared__ float shm[kBlock];
   double s = 0.0;
   float m = -INFINITY;
   if ((int)threadIdx.x < P) {
@@ -321,16 +323,19 @@ __device__ __forceinline__ void s2_reduce_partials(const S2Partial* __restrict__
     s = p.s;
     m = p.m;
   }
-  s = wave_sum_asc(s);
-  m = wave_nanmax_asc(m);
-  if (lane == 0) {
-    shs[wave] = s;
-    shm[wave] = m;
-  }
+  shs[threadIdx.x] = s;
+  shm[threadIdx.x] = m;
   __syncthreads();
+  if (threadIdx.x < kWave) {
+    const int l = threadIdx.x;
+    s = (shs[l] + shs[l + 64]) + (shs[l + 128] + shs[l + 192]);
+    m = nan_max(nan_max(shm[l], shm[l + 64]), nan_max(shm[l + 128], shm[l + 192]));
+    s = wave_sum_asc(s);
+    m = wave_nanmax_asc(m);
+  }
   if (threadIdx.x == 0) {
-    const double S = (shs[0] + shs[1]) + (shs[2] + shs[3]);
-    const float M = nan_max(nan_max(shm[0], shm[1]), nan_max(shm[2], shm[3]));
+    const double S = s;
+    const float M = m;
     SmqS2fp8Stats d;
     s2fp8_finalize<TIN>(S, M, n, &d);
     *st = d;
@@ -907,19 +912,15 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
   // count this workgroup past the wait now; the returned word is looked at only at the end
   unsigned long long left_old = 0;
   if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.left);
-  // wave 0: reduce the partials in the two-launch apply's order (a wave sum over partial indices
-  // l + 64q for each q in the ascending butterfly order, then (q0 + q1) + (q2 + q3)) and derive;
-  // then threads 0-130 tabulate the inverse powers
+  // wave 0: reduce the partials in the two-launch apply's order (lane l: partials l + 64q summed
+  // as (q0 + q1) + (q2 + q3), then one ascending butterfly — four butterflies before, 0.7 us) and
+  // derive; then threads 0-130 tabulate the inverse powers
   if (wave == 0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      ps[q] = wave_sum_asc(ps[q]);
-      pm[q] = wave_nanmax_asc(pm[q]);
-    }
+    // s2_reduce_partials' order: per lane (p0 + p1) + (p2 + p3), then one butterfly
+    const double S = wave_sum_asc((ps[0] + ps[1]) + (ps[2] + ps[3]));
+    const float M = wave_nanmax_asc(nan_max(nan_max(pm[0], pm[1]), nan_max(pm[2], pm[3])));
     s2f_stamp(A, 8);
     if (lane == 0) {
-      const double S = (ps[0] + ps[1]) + (ps[2] + ps[3]);
-      const float M = nan_max(nan_max(pm[0], pm[1]), nan_max(pm[2], pm[3]));
       SmqS2fp8Stats d;
       s2fp8_finalize<kF32>(S, M, A.n, &d);
       sst = d;
