@@ -167,7 +167,7 @@ def test_register_autograd_module_every_call_bitexact():
             seed, off = codec.rng.seed, codec.rng.offset
             y = codec(x, tag=tag, **kw)
             if record and y is not x:
-                ws = next(v for k, v in N._ws.items() if k[0] == "smaq")
+                ws = N._ws[("smaq", 0, N.stream_ptr(x.device))]  # this stream's workspace
                 calls.append((x.detach().clone(), y.detach().clone(), seed, off,
                               SmartFP.read_stats(ws), kw.get("batch_norm_stats")))
             return y

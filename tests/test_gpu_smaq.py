@@ -149,7 +149,8 @@ def test_golden_full_pipeline(name):
 def _smaq_ws():
     from smart_compress_amd import _native as N
 
-    return next(v for k, v in N._ws.items() if k[0] == "smaq")
+    # the current stream's workspace (earlier tests may have left others, e.g. a capture stream's)
+    return N._ws[("smaq", 0, N.stream_ptr(torch.device("cuda")))]
 
 
 def _oracle_check(x_np, y_dev, ws, hp, seed, offset, all_positive=False, window=None):
