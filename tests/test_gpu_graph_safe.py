@@ -211,14 +211,12 @@ def test_workspace_created_in_capture_keeps_counters_across_replays():
     dev.graph_safe(device="cuda")
     host = SmartFP(smaq_hparams())
     host.rng.seed, host.rng.offset = 5, 0
-    before = {k for k in N._ws if k[0] == "smaq"}
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         y1 = dev(x1)
         y2 = dev(x2)
-    new = [N._ws[k] for k in N._ws if k[0] == "smaq" and k not in before]
-    assert len(new) == 1
-    ws = new[0]
+        key = ("smaq", 0, N.stream_ptr(x1.device))  # the capture stream's workspace
+    ws = N._ws[key]  # created in this capture, or by an earlier test's capture on this stream
     sentinel = N.SMQ_WS_SAMPLES_OFFSET + 8 * N.SMQ_MAX_DEVICE_SAMPLES - 1  # only device draws write it
     ws[sentinel] = 0xA5
     for _ in range(2):
