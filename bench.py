@@ -490,7 +490,9 @@ def run_smaq(args, world, rank, device):
                      "frac": round(apply_gbps / HBM_PEAK_GBPS, 4),
                      "alg_bytes_per_launch": int((in_bytes + 4) * n),
                      "avg_launch_ms": round(apply_ms, 5),
-                     "traffic": traffic_from_profile(args.config)},
+                     "traffic": traffic_from_profile(
+                         args.config if in_dt is None
+                         else f"{args.config}_{os.environ['SMQ_BENCH_DTYPE']}")},
         # the statistics launch is not bracketed by events (an event between the two launches
         # costs ~1 %); its duration is in the committed rocprofv3 summary (profiles/)
         "host_enqueue_ms_per_step": round(HOST.get("enqueue_ms_per_step", 0.0), 4),

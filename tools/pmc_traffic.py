@@ -90,6 +90,7 @@ def main():
     with open(os.path.join(REPO, "profiles", f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     main_k = {"smaq": "smaq_apply_kernel", "smaq_sampled": "smaq_apply_kernel",
+              "smaq_f16": "smaq_apply_kernel", "smaq_bf16": "smaq_apply_kernel",
               "fp8": "float_quant_kernel", "s2fp8": "s2fp8_fused_kernel",
               "multi": "smaq_multi_apply_kernel", "packed": "smaq_unpack_kernel"}[config]
     if main_k in kernels and "hbm_bytes_per_launch" in kernels[main_k]:
