@@ -352,9 +352,13 @@ def _oracle_window(xw, y, st, hp, lo, hi):
 
 
 @pytest.mark.parametrize("dt", ["f16", "bf16"])
-def test_half_inputs_end_to_end(dt):
+@pytest.mark.parametrize("offset_elems,n", [(0, 1 << 18), (4, (1 << 20) + 5), (1, 70001),
+                                            (0, (3 << 22) + 8)])
+def test_half_inputs_end_to_end(dt, offset_elems, n):
     """SmartFP on fp16 / bf16 tensors (Lightning precision=16): fp32 output, stats in the input
-    type, bit-exact vs the oracle fed the device statistics and counter RNG."""
+    type, bit-exact vs the oracle fed the device statistics and counter RNG. Offsets: 0 (16-B
+    aligned: tile sweep with 16-B loads), 4 elements (8-B aligned: grid-stride sweep), 1 (element
+    path); 12M runs the non-deferred round trip and several statistics tiles per workgroup."""
     from oracle import rng as orng
     from oracle import smaq as osmaq
     from smart_compress_amd.compress.smart import SmartFP
@@ -362,7 +366,8 @@ def test_half_inputs_end_to_end(dt):
     g = _gpu()
     tdt = g.TORCH_DT[dt]
     gen = torch.Generator(device="cuda").manual_seed(11)
-    x = (torch.randn(1 << 18, generator=gen, device="cuda") * 1.5 - 0.2).to(tdt)
+    base = (torch.randn(n + offset_elems, generator=gen, device="cuda") * 1.5 - 0.2).to(tdt)
+    x = base[offset_elems:]
     hp = smaq_hparams(precision=16)
     codec = SmartFP(hp)
     codec.rng.seed, codec.rng.offset = 3, 10
