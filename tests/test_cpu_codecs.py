@@ -422,3 +422,27 @@ def test_cpu_smartfp_batch_norm_and_outlier_count():
     assert same_f32(y.numpy(), y_or), n_diff_f32(y.numpy(), y_or)
     n_out = int(np.asarray(o).sum())
     assert logged["new_size"] == n_out * 8 + (x.numel() - n_out) * 6
+
+
+@pytest.mark.parametrize("special", ["nan", "inf", "-inf"])
+def test_cpu_nonfinite_input_propagates_like_reference(special):
+    """One NaN / +-inf element on the host path: statistics NaN / inf as the fp64 oracle's, every
+    output NaN, bit-exact vs the oracle (as tests/test_gpu_smaq.py does on the device)."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import SmartFP
+
+    N = _N()
+    n = 200003
+    x = torch.randn(n, generator=torch.Generator().manual_seed(5))
+    x[n // 3] = float(special)
+    codec = SmartFP(smaq_hparams())
+    codec.rng.seed, codec.rng.offset = 8, 0
+    y = codec(x)
+    st = SmartFP.read_stats(N.cpu_workspace("smaq", 0))
+    xn = x.numpy()
+    with np.errstate(invalid="ignore"):  # inf - inf in the oracle's centred sums
+        mo, so = osmaq.full_stats(xn, osmaq.SmaqConfig())
+    assert same_f32(np.float32(st["mean"]), mo) and same_f32(np.float32(st["raw_std"]), so)
+    y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], osmaq.SmaqConfig(), orng.uniforms(8, 0, n))
+    assert same_f32(y.numpy(), y_or) and np.isnan(y.numpy()).all()
