@@ -540,3 +540,34 @@ def test_deferred_statistics_equal_two_call_path(n, mode):
         assert hdrs[0]["min"] == hdrs[1]["min"] and hdrs[0]["max"] == hdrs[1]["max"]
     if mode == "counter":
         assert ctrs[0] == ctrs[1] == (1 << 33) + n
+
+
+@pytest.mark.parametrize("n", [100003, 5 << 20, 13 << 20])
+@pytest.mark.parametrize("special", ["nan", "inf", "-inf"])
+def test_nonfinite_input_propagates_like_reference(special, n):
+    """One NaN / +-inf element: the reference's data.mean() / data.std() become NaN or inf
+    (inf - inf), the clamp keeps NaN, and every output element is NaN (smart.py:130-182). The
+    device statistics (deferred below 12M, counted hand-off above) equal the fp64 oracle's and
+    the output equals the oracle's bit for bit (every NaN equal to every NaN)."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import SmartFP
+
+    gen = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(n, generator=gen, device="cuda")
+    x[n // 3] = float(special)
+    hp = smaq_hparams()
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = 8, 0
+    y = codec(x)
+    torch.cuda.synchronize()
+    st = _gpu().read_stats(_smaq_ws())
+    xn = x.cpu().numpy()
+    with np.errstate(invalid="ignore"):  # inf - inf in the oracle's centred sums
+        mo, so = osmaq.full_stats(xn, osmaq.SmaqConfig())
+    assert same_f32(np.float32(st["mean"]), mo) and same_f32(np.float32(st["raw_std"]), so)
+    y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], osmaq.SmaqConfig(),
+                          orng.uniforms(8, 0, n))
+    yh = y.cpu().numpy()
+    assert same_f32(yh, y_or)
+    assert np.isnan(yh).all()
