@@ -474,7 +474,7 @@ def run_smaq(args, world, rank, device):
         "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32" if in_dt is None else f"{os.environ['SMQ_BENCH_DTYPE']} in, fp32 out",
         "data": "synthetic",
-        "config": {"workload": "smaq_6_8_roundtrip_256M_fp32" if not sampled else
+        "config": {"workload": f"smaq_6_8_roundtrip_{n >> 20}M_fp32" if not sampled else
                    "smaq_6_8_roundtrip_sampled_stats", "elements_per_gpu": n,
                    "stats": "sampled(16)" if sampled else "full", "rounding": "stochastic",
                    "bits": "6/8", "alg_bytes_per_elem": alg_per_elem,
