@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   const int64_t n = ch.n;
   const float k0 = load1<TIN>(x, 0), k1 = load1<TIN>(x, n >> 1), k2 = load1<TIN>(x, n - 1);
   const double shift = (double)fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));
-  StatAcc acc;
+  StatAcc acc, ay, az, aw;
   if (((uintptr_t)x & (TIN == kF32 ? 15u : 7u)) == 0) {
     const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;  // begin is a multiple of the chunk
     // 16 KiB steps; the next step's four loads are in flight while the current one is summed
@@ -128,16 +128,22 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t j = t0 + threadIdx.x + u * kBlock;
-        if (j < e4) {
+        if (j < e4) {  // four independent fp64 chains (one per component), as the single sweep
           acc.add<RANGE>(cur[u].x, shift);
-          acc.add<RANGE>(cur[u].y, shift);
-          acc.add<RANGE>(cur[u].z, shift);
-          acc.add<RANGE>(cur[u].w, shift);
+          ay.add<RANGE>(cur[u].y, shift);
+          az.add<RANGE>(cur[u].z, shift);
+          aw.add<RANGE>(cur[u].w, shift);
         }
         cur[u] = nxt[u];
       }
     }
     if (threadIdx.x < (int)(ch.end - (e4 << 2))) acc.add<RANGE>(load1<TIN>(x, (e4 << 2) + threadIdx.x), shift);
+    acc.s1 = (acc.s1 + ay.s1) + (az.s1 + aw.s1);
+    acc.s2 = (acc.s2 + ay.s2) + (az.s2 + aw.s2);
+    if (RANGE) {
+      acc.mn = fminf(fminf(acc.mn, ay.mn), fminf(az.mn, aw.mn));
+      acc.mx = fmaxf(fmaxf(acc.mx, ay.mx), fmaxf(az.mx, aw.mx));
+    }
   } else {
     for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) acc.add<RANGE>(load1<TIN>(x, j), shift);
   }
