@@ -11,6 +11,10 @@
 //                      z-score, main/outlier split, N-bit scale, stochastic rounding from the
 //                      counter-based RNG (or trunc), de-quantisation, all_positive.  smart.py:154-182
 //
+// smq_smaq_roundtrip on tensors up to kDeferMaxN elements defers the statistics' final reduction:
+// the statistics launch only stores its partials, and every apply workgroup reduces them itself in
+// one fixed order (defer_consts) — no workgroup of either launch waits on another.
+//
 // Sampled statistics (smart.py:86-91) need no stats launch: every workgroup of the apply kernel
 // gathers the k <= 64 sampled elements itself (L2-resident after the first workgroup) and reduces
 // them in the same fixed order, so the whole call is ONE launch of 8 B/elem.
