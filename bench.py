@@ -386,7 +386,35 @@ def cpu_baseline_multi(args):
                       f"{t_tot:.1f} s"}
 
 
+def cpu_baseline_packed(args):
+    """Packed container on the host: the numpy restatement (oracle/smaq_packed.py: full statistics,
+    counter-RNG codes, block images, then the decoder), one thread, on a bounded sample; the same
+    algorithmic bytes as the GPU line (12 B/elem + the stream written and read)."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from oracle import smaq_packed as opk
+
+    n = min(args.cpu_sample, 1 << 20)
+    x = np.random.default_rng(0).standard_normal(n).astype(np.float32)
+    cfg = osmaq.SmaqConfig()
+    u = orng.uniforms(7, 0, n)
+    box = {}
+
+    def step():
+        mean, std = osmaq.full_stats(x, cfg)
+        box["s"] = opk.pack(x, mean, std, cfg, u)
+        opk.unpack(box["s"])
+
+    reps, t_tot, _ = _time_reps(step, args.cpu_budget)
+    alg = 12.0 * n + 2.0 * box["s"].size
+    return {"value": round(alg * reps / t_tot / 1e9, 4), "unit": "GB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{reps} x {n} fp32 N(0,1) compress + decompress, numpy restatement "
+                      f"(oracle/smaq_packed.py), 1 thread, {t_tot:.1f} s"}
+
+
 CPU_BASELINES = {
+    "packed": lambda a: cpu_baseline_packed(a),
     "smaq": lambda a: cpu_baseline_smaq(a),
     "smaq_cpu": lambda a: cpu_baseline_smaq(a),
     "smaq_sampled": lambda a: cpu_baseline_smaq(a, sampled=True),
