@@ -459,9 +459,10 @@ __device__ __forceinline__ float s2_inverse_lut(float T, const float* lut) {
 // (qtorch_quant(Y, r, 5, 2, true) with its normal and subnormal paths both computed and one
 // selected) and check_inf (+57344 -> +inf; an E5M2 value within FLT_EPSILON of 57344 is 57344).
 // Returns T's bits.
-__device__ __forceinline__ uint32_t s2_fwd_fast(float xv, uint32_t r, float alpha, float bp2,
-                                                int check_inf) {
-  const float Y = __builtin_amdgcn_exp2f(alpha * log2f(fabsf(xv))) * bp2;
+// s2_fwd_fast from lg = log2f(|x|) (the single launch keeps it from its statistics pass).
+__device__ __forceinline__ uint32_t s2_fwd_fast_lg(float lg, uint32_t r, float alpha, float bp2,
+                                                   int check_inf) {
+  const float Y = __builtin_amdgcn_exp2f(alpha * lg) * bp2;
   const uint32_t t = __builtin_bit_cast(uint32_t, Y);
   const uint32_t rm = r & 0x1fffffu;            // (1 << (23 - man)) - 1
   uint32_t qn = (t + rm) & 0xffe00000u;          // round_bitwise
@@ -472,6 +473,11 @@ __device__ __forceinline__ uint32_t s2_fwd_fast(float xv, uint32_t r, float alph
   uint32_t T = ((t & 0x7f800000u) < 0x38800000u) ? __builtin_bit_cast(uint32_t, qs) : qn;
   if (check_inf) T = (T == 0x47600000u) ? 0x7f800000u : T;
   return T;
+}
+
+__device__ __forceinline__ uint32_t s2_fwd_fast(float xv, uint32_t r, float alpha, float bp2,
+                                                int check_inf) {
+  return s2_fwd_fast_lg(log2f(fabsf(xv)), r, alpha, bp2, check_inf);
 }
 
 // Forward half of s2fp8_elem for the LUT inverse: T (after check_inf), or Y / T per out_mode.
@@ -725,6 +731,51 @@ __device__ __forceinline__ void s2f_lane_sums(const float4* v, const S2FArgs& A,
   }
 }
 
+// The same sums over this workgroup's registers, keeping lg = log2f(|x|) of every element for the
+// forward transform (s2_log is lg with zeros as +0: the same partial bit for bit). Computing the
+// logarithms once moves them off the path behind the gather.
+__device__ __forceinline__ void s2f_lane_sums_keep(const float4* v, const S2FArgs& A, int k,
+                                                   double& s, float& m, float (*lg)[4]) {
+  const int64_t base = (int64_t)k * A.V * kS2FT + threadIdx.x;
+  s = 0.0;
+  m = -INFINITY;
+  auto slog = [](float xv, float l) { return fabsf(xv) == 0.0f ? 0.0f : l; };
+#pragma unroll
+  for (int u = 0; u < kS2FMaxV; ++u) {
+    if (u >= A.V) break;
+    const int64_t j = base + (int64_t)u * kS2FT;
+    if (j >= A.nv) continue;
+    const float4 xv = v[u];
+    lg[u][0] = log2f(fabsf(xv.x));
+    lg[u][1] = log2f(fabsf(xv.y));
+    lg[u][2] = log2f(fabsf(xv.z));
+    lg[u][3] = log2f(fabsf(xv.w));
+    const float l0 = slog(xv.x, lg[u][0]), l1 = slog(xv.y, lg[u][1]), l2 = slog(xv.z, lg[u][2]),
+                l3 = slog(xv.w, lg[u][3]);
+    s += ((double)l0 + (double)l1) + ((double)l2 + (double)l3);
+    m = nan_max(nan_max(m, l0), nan_max(l1, nan_max(l2, l3)));
+  }
+  if (k == A.G - 1 && threadIdx.x < (int)(A.n & 3)) {
+    const float l = s2_log<kF32>(A.x[(A.nv << 2) + threadIdx.x]);
+    s += (double)l;
+    m = nan_max(m, l);
+  }
+}
+
+// The four stochastic-rounding words of elements 4j .. 4j+3 (rng_u32(key, c + q), c = off + 4j).
+__device__ __forceinline__ void s2f_hash4(uint32_t key, uint64_t c, uint32_t r[4]) {
+  const uint32_t lo = (uint32_t)c;
+  if (__builtin_expect(lo <= 0xfffffffcu, 1)) {
+    const uint32_t hi = (uint32_t)(c >> 32);
+    const uint32_t kk = ((hi << 16) | (hi >> 16)) ^ key;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = mix32((lo + (uint32_t)q) ^ kk);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = rng_u32(key, c + (uint64_t)q);
+  }
+}
+
 // Workgroup reduce of the lane sums in the partial kernel's order; lanes 0-23 of wave 0 store
 // partial k as three granules in each of the kS2FRep replicas (one sc1 store each; nobody waits for
 // them here). Barriers are LDS-only (lds_barrier) throughout the kernel: no workgroup-internal
@@ -766,6 +817,7 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
   __shared__ float shm[kS2FT / kWave];
   __shared__ SmqS2fp8Stats sst;
   __shared__ int sflag;
+  __shared__ uint4 r0lds[kS2FMaxV][kWave];  // wave 0's rounding words, computed by waves 1..V
   const int b = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int64_t base = (int64_t)b * A.V * kS2FT + threadIdx.x;
@@ -795,14 +847,31 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
   asm volatile("" ::"v"(off));  // materialised here: no later wait on it waits for the `left` atomic
   // the table's unreachable entries (NaN) need no statistics
   for (int i = threadIdx.x; i < kS2LutSize; i += kS2FT) lut[i] = __builtin_nanf("");
+  float lg[kS2FMaxV][4];
   {
     double s;
     float m;
-    s2f_lane_sums(v, A, b, s, m);
+    s2f_lane_sums_keep(v, A, b, s, m, lg);
     s2f_stamp(A, 1);
     s2f_publish(s, m, A, b, epoch, shs, shm);
   }
   s2f_stamp(A, 2);
+  // The stochastic-rounding words depend on the stream position only: waves 1..15, idle while wave
+  // 0 gathers the partials, compute their own now, and waves 1..V also wave 0's slot u = wave - 1
+  // (handed over in LDS behind the gather's barrier), so the transform after the statistics starts
+  // without the counter hashes.
+  uint32_t rw[kS2FMaxV][4];
+  if (wave != 0) {
+#pragma unroll
+    for (int u = 0; u < kS2FMaxV; ++u)
+      if (u < V) s2f_hash4(A.key, off + ((uint64_t)(base + (int64_t)u * kS2FT) << 2), rw[u]);
+    if (wave <= V) {
+      const int u = wave - 1;
+      uint32_t r0[4];
+      s2f_hash4(A.key, off + ((uint64_t)((int64_t)b * A.V * kS2FT + lane + (int64_t)u * kS2FT) << 2), r0);
+      r0lds[u][lane] = make_uint4(r0[0], r0[1], r0[2], r0[3]);
+    }
+  }
   // wave 0 gathers the G partials (lane l: partials l + 64q) from replica b % 8 until every granule
   // carries the epoch
   const unsigned long long* rep = A.gran + (size_t)(b % kS2FRep) * 3 * kS2FMaxG;
@@ -871,6 +940,18 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
     if (lane == 0) sflag = (miss == INT_MAX || gave_up) ? -1 : (miss + b) % A.G;
   }
   lds_barrier();
+  if (wave == 0) {
+#pragma unroll
+    for (int u = 0; u < kS2FMaxV; ++u) {
+      if (u < V) {
+        const uint4 w = r0lds[u][lane];
+        rw[u][0] = w.x;
+        rw[u][1] = w.y;
+        rw[u][2] = w.z;
+        rw[u][3] = w.w;
+      }
+    }
+  }
   // missing partials after the patience ran out: the whole workgroup computes them one by one from
   // memory; after each, wave 0 re-reads every granule and names the next missing one
   while (sflag >= 0) {
@@ -964,22 +1045,8 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
     for (int u = 0; u < V; ++u) {
       const int64_t j = base + (int64_t)u * kS2FT;
       if (j >= A.nv) continue;
-      const uint64_t c = off + ((uint64_t)j << 2);
-      uint32_t r[4];
-      const uint32_t lo = (uint32_t)c;
-      if (__builtin_expect(lo <= 0xfffffffcu, 1)) {
-        const uint32_t hi = (uint32_t)(c >> 32);
-        const uint32_t kk = ((hi << 16) | (hi >> 16)) ^ A.key;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) r[q] = mix32((lo + (uint32_t)q) ^ kk);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) r[q] = rng_u32(A.key, c + (uint64_t)q);
-      }
-      T[u][0] = s2_fwd_fast(v[u].x, r[0], alpha, bp2, A.check_inf);
-      T[u][1] = s2_fwd_fast(v[u].y, r[1], alpha, bp2, A.check_inf);
-      T[u][2] = s2_fwd_fast(v[u].z, r[2], alpha, bp2, A.check_inf);
-      T[u][3] = s2_fwd_fast(v[u].w, r[3], alpha, bp2, A.check_inf);
+      for (int q = 0; q < 4; ++q) T[u][q] = s2_fwd_fast_lg(lg[u][q], rw[u][q], alpha, bp2, A.check_inf);
     }
     auto sgn = [](float xv) { return (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f); };
 #pragma unroll
