@@ -39,7 +39,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-METRIC = "SmaQ 6/8-bit quant+dequant round-trip GB/s (and % HBM peak), 256M fp32"
+METRIC = "SmaQ 6/8-bit quant+dequant round-trip GB/s (and % HBM peak), {size} fp32"
 
 
 def _hip_runtime():
@@ -190,16 +190,20 @@ def launch_ranks(n, argv):
     """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK,
     LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1) and wait for them. This process never
     touches the GPU (the children are started before anything initialises HIP). Rank 0's stdout —
-    the one JSON line — is relayed; if a rank fails, the others are stopped. Returns the exit code."""
+    the one JSON line — goes to a temporary file (never a pipe: a rank writing more than a pipe
+    buffer would block on it while the others wait at a barrier) and is relayed after the ranks
+    exit; if a rank fails, the others are stopped. Returns the exit code."""
     import subprocess
+    import tempfile
 
     port = str(_free_port())
     procs = []
+    out0 = tempfile.TemporaryFile()
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL,
                                       start_new_session=True))
     rc = 0
     try:
@@ -219,7 +223,9 @@ def launch_ranks(n, argv):
         for pr in procs:
             if pr.poll() is None:
                 pr.kill()
-    out = procs[0].stdout.read().decode()
+    out0.seek(0)
+    out = out0.read().decode(errors="replace")
+    out0.close()
     for line in out.splitlines():  # the JSON line to stdout, anything else (gloo chatter) to stderr
         (sys.stdout if line.startswith("{") else sys.stderr).write(line + "\n")
     sys.stdout.flush()
@@ -424,17 +430,26 @@ CPU_BASELINES = {
 }
 
 
-def traffic_from_profile(config, whole_call=False):
-    """HBM bytes per launch from the committed PMC passes (profiles/traffic_<config>.json): the
-    dominant kernel's, or (whole_call) the sum over the call's kernels."""
-    path = os.path.join(REPO, "profiles", f"traffic_{config}.json")
+def traffic_from_profile(config, elements, dtype="f32", whole_call=False, profile=None):
+    """HBM bytes per launch from the committed PMC passes (profiles/traffic_<profile>.json): the
+    dominant kernel's, or (whole_call) the sum over the call's kernels. Reported only when the
+    profiled run was this workload (same config, element count and input dtype); otherwise None —
+    counter bytes of another size say nothing about this run."""
+    path = os.path.join(REPO, "profiles", f"traffic_{profile or config}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
+    if (d.get("config"), d.get("elements"), d.get("dtype", "f32")) != (config, int(elements), dtype):
+        return None
     if whole_call:
         return float(sum(d.get("kernels", {}).values())) or None
     return d.get("apply_bytes_per_launch")
+
+
+def size_label(n):
+    """'256M' for whole multiples of 2^20 elements, else the exact count."""
+    return f"{n >> 20}M" if n % (1 << 20) == 0 else str(n)
 
 
 def run_smaq(args, world, rank, device):
@@ -496,14 +511,14 @@ def run_smaq(args, world, rank, device):
     apply_ms = trace.mean_ms("apply")
     apply_gbps = (in_bytes + 4.0) * n / (apply_ms * 1e-3) / 1e9
     res = {
-        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+        "metric": METRIC.format(size=size_label(n)), "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32" if in_dt is None else f"{os.environ['SMQ_BENCH_DTYPE']} in, fp32 out",
         "data": "synthetic",
-        "config": {"workload": f"smaq_6_8_roundtrip_{n >> 20}M_fp32" if not sampled else
-                   "smaq_6_8_roundtrip_sampled_stats", "elements_per_gpu": n,
+        "config": {"workload": f"smaq_6_8_roundtrip_{size_label(n)}_fp32" if not sampled else
+                   f"smaq_6_8_roundtrip_sampled_stats_{size_label(n)}", "elements_per_gpu": n,
                    "stats": "sampled(16)" if sampled else "full", "rounding": "stochastic",
                    "bits": "6/8", "alg_bytes_per_elem": alg_per_elem,
                    "parallelism": f"replicas{world}",
@@ -519,7 +534,8 @@ def run_smaq(args, world, rank, device):
                      "alg_bytes_per_launch": int((in_bytes + 4) * n),
                      "avg_launch_ms": round(apply_ms, 5),
                      "traffic": traffic_from_profile(
-                         args.config if in_dt is None
+                         args.config, n, "f32" if in_dt is None else os.environ["SMQ_BENCH_DTYPE"],
+                         profile=args.config if in_dt is None
                          else f"{args.config}_{os.environ['SMQ_BENCH_DTYPE']}")},
         # the statistics launch is not bracketed by events (an event between the two launches
         # costs ~1 %); its duration is in the committed rocprofv3 summary (profiles/)
@@ -566,7 +582,7 @@ def run_fp8(args, world, rank, device):
                        "rotating_buffers": nbuf},
             "roofline": {"bound": "hbm", "kernel": "float_quant_kernel", "achieved": round(gbps, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
-                         "avg_launch_ms": round(k_ms, 5), "traffic": traffic_from_profile("fp8")}}
+                         "avg_launch_ms": round(k_ms, 5), "traffic": traffic_from_profile("fp8", n)}}
 
 
 def run_s2fp8(args, world, rank, device):
@@ -649,7 +665,7 @@ def run_s2fp8(args, world, rank, device):
             "roofline": {"bound": "hbm", "kernel": "s2fp8_fused_kernel",
                          "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(gbps / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": int(12 * n),
-                         "avg_launch_ms": round(g_dev_ms, 5), "traffic": traffic_from_profile("s2fp8", True)}}
+                         "avg_launch_ms": round(g_dev_ms, 5), "traffic": traffic_from_profile("s2fp8", n, whole_call=True)}}
 
 
 def resnet34_cifar_params():
@@ -731,7 +747,7 @@ def run_multi(args, world, rank, device):
             "roofline": {"bound": "hbm", "kernel": "smaq_multi_stats_kernel+smaq_multi_apply_kernel",
                          "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(gbps / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": int(12 * n),
-                         "avg_launch_ms": round(k_ms, 5), "traffic": traffic_from_profile("multi", True)}}
+                         "avg_launch_ms": round(k_ms, 5), "traffic": traffic_from_profile("multi", n, whole_call=True)}}
 
 
 def run_packed(args, world, rank, device):
@@ -789,13 +805,13 @@ def run_packed(args, world, rank, device):
     total = sum_over_ranks(alg * args.steps, world, device)
     c_ms, u_ms = trace.mean_ms("compress"), trace.mean_ms("unpack")
     u_gbps = (sbytes + 4.0 * n) / (u_ms * 1e-3) / 1e9
-    return {"metric": "Packed SmaQ 6/8 compress+decompress GB/s, 256M fp32",
+    return {"metric": f"Packed SmaQ 6/8 compress+decompress GB/s, {size_label(n)} fp32",
             "value": round(total / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "host_enqueue_ms_per_step": round(HOST.get("enqueue_ms_per_step", 0.0), 4),
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": "smaq_6_8_packed_256M_fp32", "elements_per_gpu": n,
+            "config": {"workload": f"smaq_6_8_packed_{size_label(n)}_fp32", "elements_per_gpu": n,
                        "stream_bytes": sbytes, "bits_per_element": round(8.0 * sbytes / n, 3),
                        "compression_ratio_vs_fp32": round(32.0 * n / (8.0 * sbytes), 3),
                        "pack_flags": pack_flags},
@@ -804,7 +820,7 @@ def run_packed(args, world, rank, device):
                          "achieved": round(u_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(u_gbps / HBM_PEAK_GBPS, 4),
                          "alg_bytes_per_launch": sbytes + 4 * n, "avg_launch_ms": round(u_ms, 5),
-                         "traffic": traffic_from_profile("packed")}}
+                         "traffic": traffic_from_profile("packed", n)}}
 
 
 def _vgg_cifar():
@@ -947,6 +963,10 @@ def run_mock(args, world, rank, device):
     of numpy work per step on each rank's own seeded data; reports what each rank saw."""
     if os.environ.get("SMQ_BENCH_MOCK_FAIL_RANK") == str(rank):
         raise RuntimeError(f"rank {rank}: injected failure (SMQ_BENCH_MOCK_FAIL_RANK)")
+    chatter = int(os.environ.get("SMQ_BENCH_MOCK_CHATTER", "0"))  # bytes of non-JSON stdout
+    if chatter:
+        sys.stdout.write(("x" * 1023 + "\n") * (chatter // 1024))
+        sys.stdout.flush()
     rng = np.random.default_rng(1000 + rank)
     a = rng.standard_normal(1 << 16).astype(np.float32)
 

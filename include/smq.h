@@ -293,8 +293,9 @@ int smq_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int precis
  * partials, then transform). Both give the same bytes: the same chunks and summation order.
  * TEST_LATE (test aid, single launch only): the upper half of the workgroups start ~500 us late
  * and the others take their unclaimed chunks after 20 us, exercising the path that keeps the
- * single launch free of any co-residency assumption. The single launch sets
- * SmqS2fp8Stats.reserved[0] = 1 if a wait gave up (a poisoned workspace; never in a healthy run). */
+ * single launch free of any co-residency assumption. The single launch leaves
+ * SmqS2fp8Stats.reserved[0] = 0 (it has no give-up path: a workgroup that waited long for a
+ * partial computes it itself). */
 #define SMQ_S2FP8_OUT_Y 1u
 #define SMQ_S2FP8_OUT_T 2u
 #define SMQ_S2FP8_EXACT_POW 4u

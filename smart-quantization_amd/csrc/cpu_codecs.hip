@@ -423,11 +423,9 @@ static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParam
                           const float* uniforms, const SmqSmaqStats* stats_in, char* ws,
                           int n_threads) {
   SmqSmaqStats st;
-  uint64_t base = 0;
-  if (p->offset_counter) {  // a host uint64 stream position, advanced by n (graph-safe mirror)
-    base = *p->offset_counter;
-    *p->offset_counter = base + (uint64_t)n;
-  }
+  // a host uint64 stream position (graph-safe mirror), advanced by n only once the call is
+  // validated: a rejected call consumes no stream positions, like the device entry points
+  const uint64_t base = p->offset_counter ? *p->offset_counter : 0ull;
   switch (p->stats_source) {
     case SMQ_STATS_WORKSPACE:
       full_stats<T>(x, n, p, range_coef_host(p, n), n_threads, &st);
@@ -467,6 +465,7 @@ static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParam
       st.quot_check = quot_check_for(st.std_clamped);
     }
   }
+  if (p->offset_counter) *p->offset_counter = base + (uint64_t)n;
   st.rng_offset = base;
   SmaqCtx c;
   c.x = x;

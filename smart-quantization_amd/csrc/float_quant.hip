@@ -668,16 +668,16 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
 // still misses itself, from memory (every partial is a pure function of its chunk, so duplicates
 // write the same bytes). So if only some workgroups are resident (another kernel holding CUs, a
 // shared device) they finish the statistics, transform their own chunks and exit, and the rest
-// start later, find the statistics complete and transform theirs. A wait that sees no completion
-// for kS2GiveUpTicks (impossible unless the workspace is corrupted mid-call) stops and flags
-// hdr->reserved[0].
+// start later, find the statistics complete and transform theirs. There is no give-up path: a
+// workgroup never proceeds with a partial it has neither read nor computed (a give-up after a
+// fixed time would hand a workgroup descheduled for that long incomplete statistics and corrupt
+// its output silently); workgroup 0 clears hdr->reserved[0] (the former give-up flag) every call.
 constexpr int kS2FT = 1024;       // threads per workgroup
 constexpr int kS2FMaxV = 4;       // float4 per lane held in registers (4.2M elements)
 constexpr int kS2FMaxG = 256;     // chunks (= partials; four per lane of the polling wave)
 constexpr int kS2FLds = 88 * 1024;  // dynamic LDS request: one workgroup per CU
 constexpr int kS2FRep = 8;          // granule replicas: replica r is read by the blocks b % 8 == r
 constexpr uint64_t kS2StealTicks = 20000;       // s_memrealtime runs at 100 MHz: 200 us
-constexpr uint64_t kS2GiveUpTicks = 200000000;  // 2 s
 
 struct S2FArgs {
   const float* x;
@@ -885,7 +885,6 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
     for (int q = 0; q < 4; ++q)
       if (lane + 64 * q >= A.G) have |= 7u << (3 * q);
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    bool gave_up = false;
     uint32_t polls = 0;
     for (;;) {
       // every granule load of the pass in flight at once, one wait
@@ -915,11 +914,6 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
         continue;
       }
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      if (now - t_start > kS2GiveUpTicks) {
-        if (lane == 0) A.hdr->reserved[0] = 1u;
-        gave_up = true;
-        break;
-      }
       if (now - t_start > steal_ticks) break;  // compute the missing partials below
       __builtin_amdgcn_s_sleep(2);
     }
@@ -937,7 +931,7 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
       if ((have & (7u << (3 * q))) != (7u << (3 * q))) miss = min(miss, (lane + 64 * q - b + A.G) % A.G);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, kWave));
-    if (lane == 0) sflag = (miss == INT_MAX || gave_up) ? -1 : (miss + b) % A.G;
+    if (lane == 0) sflag = miss == INT_MAX ? -1 : (miss + b) % A.G;
   }
   lds_barrier();
   if (wave == 0) {
@@ -1016,6 +1010,7 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
         h->inv_alpha = d.inv_alpha;
         h->n_used = d.n_used;
         h->rng_offset = off0;
+        h->reserved[0] = 0u;
       }
     }
     s2f_stamp(A, 9);

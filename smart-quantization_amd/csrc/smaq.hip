@@ -109,6 +109,56 @@ constexpr int64_t kStatsNtMinMB = 512;  // non-temporal statistics loads from th
 
 static inline bool aligned(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
+// Wave-0 reduction of g <= kDeferMaxG statistics partials in ONE fixed order: lane l sums
+// partials l, l + 64, l + 128, l + 192 in that order, then the ascending DPP butterfly. Used by the
+// deferred path (every apply workgroup, plain loads: the partials come from an earlier launch) and by
+// the last statistics workgroup of a grid of <= kDeferMaxG (sc1 loads: same launch), so both give
+// the same fp64 totals bit for bit. Every load is issued before any is consumed. Call from wave 0
+// (all 64 lanes); the result is wave-uniform.
+template <bool SC1>
+__device__ __forceinline__ void reduce_partials_w0(const StatPartial* parts, int g, bool range,
+                                                   double& s1, double& s2, float& mn, float& mx) {
+  constexpr int K = kDeferMaxG / kWave;
+  const int l = threadIdx.x & (kWave - 1);
+  double2 sv[K];
+  float2 mv[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int b = l + i * kWave;
+    if (b < g) {
+      if (SC1) {
+        sv[i].x = ld_sc1_f64(&parts[b].s1);
+        sv[i].y = ld_sc1_f64(&parts[b].s2);
+        if (range) ld_sc1_f32x2(&parts[b].mn, mv[i].x, mv[i].y);
+      } else {
+        sv[i] = *reinterpret_cast<const double2*>(&parts[b].s1);
+        if (range) mv[i] = *reinterpret_cast<const float2*>(&parts[b].mn);
+      }
+    }
+  }
+  s1 = 0.0;
+  s2 = 0.0;
+  mn = INFINITY;
+  mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    if (l + i * kWave < g) {
+      s1 += sv[i].x;
+      s2 += sv[i].y;
+      if (range) {
+        mn = fminf(mn, mv[i].x);
+        mx = fmaxf(mx, mv[i].y);
+      }
+    }
+  }
+  s1 = wave_sum_asc(s1);
+  s2 = wave_sum_asc(s2);
+  if (range) {
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+  }
+}
+
 template <bool RANGE, int TIN, bool TILE = false, bool NT = false>
 __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restrict__ x, int64_t n,
                                                             int vec, FinalizeArgs fin,
@@ -255,7 +305,21 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
 
   // Last workgroup: ordered reduction of all partials (deterministic for a given n). Every load
   // of a lane is issued before any is consumed: a loop that adds as it loads waits out one memory
-  // round trip per partial (8 serial ~1.5 us trips at 2048 partials).
+  // round trip per partial (8 serial ~1.5 us trips at 2048 partials). Grids of <= kDeferMaxG
+  // reduce in the deferred path's order (reduce_partials_w0), so smq_smaq_stats + smq_smaq_apply
+  // and the deferred smq_smaq_roundtrip produce the same statistics bit for bit.
+  if ((int)gridDim.x <= kDeferMaxG) {
+    if (threadIdx.x < kWave) {
+      double t1, t2;
+      float tmn, tmx;
+      reduce_partials_w0<true>(partials, gridDim.x, RANGE, t1, t2, tmn, tmx);
+      if (threadIdx.x == 0) {
+        finalize_stats<RANGE, TIN>(t1, t2, tmn, tmx, n, shift, false, fin, out);
+        arrive_reset(counter + (tag.next & (SmaqWsLayout::kTagWords - 1)), tag.next);
+      }
+    }
+    return;
+  }
   constexpr int K = kStatsGridCap / kBlock;
   double s1v[K], s2v[K];
   float mnv[K], mxv[K];
@@ -332,37 +396,10 @@ __device__ __forceinline__ void defer_consts(const ApplyArgs& A, ElemConsts& c, 
                                           float cthr) {
   __shared__ SmqSmaqStats sh;
   if (threadIdx.x < kWave) {
-    constexpr int K = kDeferMaxG / kWave;
     const int l = threadIdx.x;
-    double2 sv[K];
-    float2 mv[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const int b = l + i * kWave;
-      if (b < A.def_g) {
-        sv[i] = *reinterpret_cast<const double2*>(&A.def_parts[b].s1);
-        if (A.use_range) mv[i] = *reinterpret_cast<const float2*>(&A.def_parts[b].mn);
-      }
-    }
-    double s1 = 0.0, s2 = 0.0;
-    float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      if (l + i * kWave < A.def_g) {
-        s1 += sv[i].x;
-        s2 += sv[i].y;
-        if (A.use_range) {
-          mn = fminf(mn, mv[i].x);
-          mx = fmaxf(mx, mv[i].y);
-        }
-      }
-    }
-    s1 = wave_sum_asc(s1);
-    s2 = wave_sum_asc(s2);
-    if (A.use_range) {
-      mn = wave_min(mn);
-      mx = wave_max(mx);
-    }
+    double s1, s2;
+    float mn, mx;
+    reduce_partials_w0<false>(A.def_parts, A.def_g, A.use_range, s1, s2, mn, mx);
     if (l == 0) {
       const FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, nullptr, 0};
       SmqSmaqStats st;
@@ -649,7 +686,10 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
     const int v = e ? atoi(e) : kBlock * 4 * 16;
     return v >= kBlock * 4 ? v : kBlock * 4 * 16;
   }();
-  const int grid = grid_for(n, per_wg, def_g && cap > kDeferMaxG ? kDeferMaxG : cap);
+  // tensors the deferred path may take use its grid cap in EVERY statistics launch, so the
+  // partials (and, through reduce_partials_w0, the totals) are the same in both paths
+  const bool defer_size = n <= kDeferMaxN || def_g;
+  const int grid = grid_for(n, per_wg, defer_size && cap > kDeferMaxG ? kDeferMaxG : cap);
   double* def_rec = nullptr;
   ArriveTag tag{};
   if (def_g) {

@@ -446,3 +446,27 @@ def test_cpu_nonfinite_input_propagates_like_reference(special):
     assert same_f32(np.float32(st["mean"]), mo) and same_f32(np.float32(st["raw_std"]), so)
     y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], osmaq.SmaqConfig(), orng.uniforms(8, 0, n))
     assert same_f32(y.numpy(), y_or) and np.isnan(y.numpy()).all()
+
+
+def test_cpu_rejected_call_consumes_no_stream_positions():
+    """A call that fails validation (num_samples out of range, missing injected statistics)
+    leaves the graph-safe stream position where it was; a valid call advances it by n."""
+    N = _N()
+    n = 3 * N.SMQ_MAX_DEVICE_SAMPLES
+    x = torch.randn(n)
+    y = torch.empty(n)
+    ws = torch.zeros(N.lib().smq_smaq_workspace_bytes(n), dtype=torch.uint8)
+    ctr = torch.tensor([777], dtype=torch.int64)
+    for src, k in ((N.SMQ_STATS_SAMPLED_DEVICE, N.SMQ_MAX_DEVICE_SAMPLES + 1),
+                   (N.SMQ_STATS_SAMPLED, N.SMQ_MAX_SAMPLES + 1), (N.SMQ_STATS_INJECTED, 16)):
+        p = _params(smaq_hparams(), n)
+        p.offset_counter = ctr.data_ptr()
+        p.stats_source, p.num_samples = src, k
+        rc = N.lib().smq_cpu_smaq_roundtrip(x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p,
+                                            None, None, ws.data_ptr(), ws.numel(), 1)
+        assert rc != 0 and int(ctr.item()) == 777
+    p = _params(smaq_hparams(), n)
+    p.offset_counter = ctr.data_ptr()
+    assert N.lib().smq_cpu_smaq_roundtrip(x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p,
+                                          None, None, ws.data_ptr(), ws.numel(), 1) == 0
+    assert int(ctr.item()) == 777 + n

@@ -71,6 +71,39 @@ def test_bench_self_launch_failing_rank_propagates():
     assert b"injected failure" in res.stderr
 
 
+def test_bench_self_launch_rank0_chatter_does_not_block():
+    """Rank 0 writing more than a pipe buffer (2 MiB of non-JSON stdout) before its barrier: the
+    launcher must not deadlock (rank 0's stdout goes to a file, not a pipe read after exit), and
+    the JSON line is still relayed."""
+    env = _clean_env()
+    env["SMQ_BENCH_MOCK_CHATTER"] = str(2 << 20)
+    res = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                          "--config", "mock", "--steps", "3", "--warmup", "1"],
+                         env=env, cwd=REPO, capture_output=True, timeout=120)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    assert _last_json(res.stdout.decode())["n_gpus"] == 2
+    assert len(res.stderr) >= 2 << 20  # the chatter went to stderr, whole
+
+
+def test_bench_traffic_only_for_the_profiled_workload():
+    """roofline.traffic comes from a committed PMC profile only when that profile measured this
+    workload (config, element count, dtype); any other size reports null, and the metric string
+    names the size actually run."""
+    sys.path[:0] = [REPO]
+    import bench
+
+    full = bench.traffic_from_profile("smaq", 1 << 28)
+    assert full is not None and 2.1e9 < full < 2.2e9
+    assert bench.traffic_from_profile("smaq", 1 << 26) is None
+    assert bench.traffic_from_profile("smaq", 1 << 28, "bf16", profile="smaq_bf16") is not None
+    assert bench.traffic_from_profile("smaq", 1 << 28, "f16", profile="smaq_bf16") is None
+    assert bench.traffic_from_profile("fp8", 25690112) is not None
+    assert bench.traffic_from_profile("s2fp8", 3145728, whole_call=True) is not None
+    assert bench.traffic_from_profile("s2fp8", 1 << 20, whole_call=True) is None
+    assert bench.METRIC.format(size=bench.size_label(1 << 26)).endswith("64M fp32")
+    assert bench.size_label(1000) == "1000"
+
+
 def test_bench_under_torchrun():
     res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                           "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",

@@ -277,9 +277,40 @@ def test_sr_unbiased():
     assert err < 0.05  # step 1/15 std, sd of the mean ~ step/2/sqrt(400)*...
 
 
+def _oracle_every_element(x, y, st, hp, seed, offset, chunk=1 << 24):
+    """Every element of y vs the oracle fed x, the device statistics and the counter RNG, bit for
+    bit: host chunks of 16M elements on a thread pool (numpy releases the GIL). Returns the number
+    of elements compared."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+
+    n = x.numel()
+    xh = x.cpu().numpy()
+    yh = y.cpu().numpy()
+    cfg = osmaq.SmaqConfig(num_bits_main=hp.num_bits_main, num_bits_outlier=hp.num_bits_outlier,
+                           main_std_dev_threshold=hp.main_std_dev_threshold,
+                           outlier_std_dev_threshold=hp.outlier_std_dev_threshold,
+                           stochastic_rounding=hp.stochastic_rounding)
+
+    def one(lo):
+        hi = min(n, lo + chunk)
+        u = orng.uniforms(seed, offset, hi - lo, start=lo) if hp.stochastic_rounding else None
+        y_or, _ = osmaq.apply(xh[lo:hi], st["mean"], st["raw_std"], cfg, u)
+        return n_diff_f32(yh[lo:hi], y_or)
+
+    with ThreadPoolExecutor(max_workers=8) as pool:
+        bad = sum(pool.map(one, range(0, n, chunk)))
+    assert bad == 0, f"{bad} of {n} elements differ from the oracle"
+    return n
+
+
 @pytest.mark.slow
-def test_full_size_256m_windows():
-    """BASELINE config 2 size: stats vs fp64 on device, windows (incl. tail) vs the oracle."""
+def test_full_size_256m_every_element():
+    """BASELINE config 2 (the headline: 268,435,456 fp32 N(0,1) elements): statistics vs fp64
+    within 1 ulp, then EVERY output element vs the oracle (device statistics, same counter RNG),
+    bit for bit; outlier share and SR bias as size-independent properties."""
     from smart_compress_amd.compress.smart import SmartFP
 
     n = 1 << 28
@@ -290,22 +321,15 @@ def test_full_size_256m_windows():
     codec.rng.seed, codec.rng.offset = 5, 0
     y = codec(x)
     torch.cuda.synchronize()
-    ws = _smaq_ws()
-    g = _gpu()
-    st = g.read_stats(ws)
+    st = _gpu().read_stats(_smaq_ws())
     xd = x.double()
-    mean64 = xd.mean().item()
-    std64 = xd.std().item()
-    assert ulp_diff(st["mean"], np.float32(mean64)) <= 1
-    assert ulp_diff(st["raw_std"], np.float32(std64)) <= 1
+    assert ulp_diff(st["mean"], np.float32(xd.mean().item())) <= 1
+    assert ulp_diff(st["raw_std"], np.float32(xd.std().item())) <= 1
     del xd
-    xn_windows = [(0, 1 << 16), (n // 2 - 12345, n // 2 + 54321), (n - (1 << 16) - 3, n)]
-    for lo, hi in xn_windows:
-        xw = x[lo:hi].cpu().numpy()
-        _oracle_window(xw, y, st, hp, lo, hi)
     frac_out = ((x - st["mean"]).abs() / st["std_clamped"] > 1.0).float().mean().item()
     assert abs(frac_out - 0.3173) < 0.002
     assert abs((y - x).double().mean().item()) < 1e-4  # unbiased SR
+    assert _oracle_every_element(x, y, st, hp, 5, 0) == n
 
 
 def _laplace(n, seed, device="cuda"):
@@ -316,10 +340,10 @@ def _laplace(n, seed, device="cuda"):
     return x.sub_(-torch.log1p(-torch.rand(n, generator=gen, device=device)))
 
 
-def test_full_size_256m_laplace_windows():
+def test_full_size_256m_laplace_every_element():
     """C2's heavy-tailed variant at full size: Laplace(0, 1) puts ~24 % of the elements beyond
     1 std and a long tail beyond T_o = 2.5 std (outliers the 8-bit range clips). Statistics vs
-    fp64, windows incl. the ragged tail vs the oracle, outlier fraction vs the Laplace law."""
+    fp64, every element vs the oracle, outlier fraction vs the Laplace law."""
     from smart_compress_amd.compress.smart import SmartFP
 
     n = 1 << 28
@@ -334,21 +358,39 @@ def test_full_size_256m_laplace_windows():
     assert ulp_diff(st["mean"], np.float32(xd.mean().item())) <= 1
     assert ulp_diff(st["raw_std"], np.float32(xd.std().item())) <= 1
     del xd
-    for lo, hi in [(0, 1 << 16), (n // 3, n // 3 + 77777), (n - (1 << 16) - 1, n)]:
-        _oracle_window(x[lo:hi].cpu().numpy(), y, st, hp, lo, hi)
     # P(|x| > sqrt(2)) = exp(-sqrt(2)) for Laplace(0, 1) (std sqrt(2))
     frac_out = ((x - st["mean"]).abs() / st["std_clamped"] > 1.0).float().mean().item()
     assert abs(frac_out - float(np.exp(-np.sqrt(2.0)))) < 0.002
     assert abs((y - x).double().mean().item()) < 1e-4
+    assert _oracle_every_element(x, y, st, hp, 5, 0) == n
 
 
-def _oracle_window(xw, y, st, hp, lo, hi):
+def test_full_size_256m_sampled_every_element():
+    """C2 with --use_sample_stats (smart.py:86-91): the 16 indices the device draws equal
+    oracle/rng.py floyd_indices, the statistics equal the oracle's over them, and every one of the
+    268,435,456 outputs equals the oracle's, bit for bit."""
     from oracle import rng as orng
     from oracle import smaq as osmaq
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.smart import SmartFP
 
-    u = orng.uniforms(5, 0, hi - lo, start=lo)
-    y_or, _ = osmaq.apply(xw, st["mean"], st["raw_std"], osmaq.SmaqConfig(), u)
-    assert same_f32(y[lo:hi].cpu().numpy(), y_or)
+    n = 1 << 28
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(n, generator=gen, device="cuda") * 0.7 + 0.1
+    hp = smaq_hparams(use_sample_stats=True)
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = 21, 1 << 30
+    y = codec(x)
+    torch.cuda.synchronize()
+    ws = _smaq_ws()
+    o = N.SMQ_WS_SAMPLES_OFFSET
+    idx = ws[o: o + 8 * 16].cpu().numpy().view(np.int64).copy()
+    assert idx.tolist() == orng.floyd_indices(21, 1 << 30, n, 16).tolist()
+    st = _gpu().read_stats(ws)
+    mo, so = osmaq.sampled_stats(x[torch.from_numpy(idx).cuda()].cpu().numpy(), np.arange(16),
+                                 osmaq.SmaqConfig())
+    assert ulp_diff(st["mean"], mo) <= 1 and ulp_diff(st["raw_std"], so) <= 1, (st, mo, so)
+    assert _oracle_every_element(x, y, st, hp, 21, 1 << 30) == n
 
 
 @pytest.mark.parametrize("dt", ["f16", "bf16"])
@@ -499,8 +541,9 @@ def test_deferred_statistics_equal_two_call_path(n, mode):
     """smq_smaq_roundtrip on tensors up to kDeferMaxN (12M) reduces the statistics partials in
     every apply workgroup (smaq.hip defer_consts) instead of in the last statistics workgroup.
     Outputs, header and graph-safe stream position equal the separate smq_smaq_stats +
-    smq_smaq_apply calls bit for bit (the two reductions differ only in fp64 summation order);
-    40M runs the non-deferred path through the same entry point."""
+    smq_smaq_apply calls bit for bit BY CONSTRUCTION: both statistics launches use the same grid
+    (<= 256 workgroups up to 12M elements) and both reductions run reduce_partials_w0's one fixed
+    order; 40M runs the non-deferred path through the same entry point."""
     from smart_compress_amd import _native as N
 
     g = _gpu()

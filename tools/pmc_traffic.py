@@ -94,8 +94,14 @@ def main():
               "fp8": "float_quant_kernel", "s2fp8": "s2fp8_fused_kernel",
               "multi": "smaq_multi_apply_kernel", "packed": "smaq_unpack_kernel"}[config]
     if main_k in kernels and "hbm_bytes_per_launch" in kernels[main_k]:
+        # the workload the counters describe: bench.py reports them only for the same one
+        elements = int(os.environ.get("SMQ_PROFILE_ELEMENTS", "0")) or {
+            "fp8": 25690112, "s2fp8": 3145728, "multi": 42547220}.get(config, 1 << 28)
+        dtype = {"smaq_f16": "f16", "smaq_bf16": "bf16"}.get(config, "f32")
         with open(os.path.join(REPO, "profiles", f"traffic_{config}.json"), "w") as f:
-            json.dump(dict(source=f"profiles/{tag}_summary.json", kernel=main_k,
+            json.dump(dict(source=f"profiles/{tag}_summary.json",
+                           config=config.replace("_f16", "").replace("_bf16", ""),
+                           elements=elements, dtype=dtype, kernel=main_k,
                            apply_bytes_per_launch=kernels[main_k]["hbm_bytes_per_launch"],
                            kernels={k: v.get("hbm_bytes_per_launch") for k, v in kernels.items()}),
                       f, indent=1)
