@@ -771,7 +771,7 @@ def run_packed(args, world, rank, device):
     st = torch.cuda.current_stream(device).cuda_stream
     trace = EventTrace()
     it = [0]
-    # SMQ_BENCH_PACK_FLAGS: smq_smaq_compress_ex flags (2 = SMQ_PACK_SINGLE, the one-launch packer)
+    # SMQ_BENCH_PACK_FLAGS: smq_smaq_compress_ex flags (legacy, no effect since format version 2)
     pack_flags = int(os.environ.get("SMQ_BENCH_PACK_FLAGS", "0"))
 
     def step():
@@ -784,7 +784,8 @@ def run_packed(args, world, rank, device):
                 "compress")
         trace.end("compress")
         trace.begin("unpack")
-        N.check(lib.smq_smaq_decompress(packed.data_ptr(), y.data_ptr(), n, st), "decompress")
+        N.check(lib.smq_smaq_decompress_ex(packed.data_ptr(), y.data_ptr(), n, hp.num_bits_main,
+                                           hp.num_bits_outlier, st), "decompress")
         trace.end("unpack")
 
     trace.enabled = False
@@ -804,7 +805,21 @@ def run_packed(args, world, rank, device):
     alg = 12.0 * n + 2.0 * sbytes
     total = sum_over_ranks(alg * args.steps, world, device)
     c_ms, u_ms = trace.mean_ms("compress"), trace.mean_ms("unpack")
+    # compress: statistics read (4n) + the packer's read of x (4n) + the stream written; decompress:
+    # the stream read + 4n written
+    c_alg = 8.0 * n + sbytes
+    c_gbps = c_alg / (c_ms * 1e-3) / 1e9
     u_gbps = (sbytes + 4.0 * n) / (u_ms * 1e-3) / 1e9
+    traffic = None
+    tp = os.path.join(REPO, "profiles", "traffic_packed.json")
+    if os.path.exists(tp):
+        with open(tp) as f:
+            d = json.load(f)
+        if (d.get("config"), d.get("elements")) == ("packed", n):
+            ks = d.get("kernels", {})
+            comp = [v for k, v in ks.items() if k != "smaq_unpack_kernel" and v]
+            traffic = {"compress": float(sum(comp)) if comp else None,
+                       "decompress": ks.get("smaq_unpack_kernel")}
     return {"metric": f"Packed SmaQ 6/8 compress+decompress GB/s, {size_label(n)} fp32",
             "value": round(total / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -814,13 +829,23 @@ def run_packed(args, world, rank, device):
             "config": {"workload": f"smaq_6_8_packed_{size_label(n)}_fp32", "elements_per_gpu": n,
                        "stream_bytes": sbytes, "bits_per_element": round(8.0 * sbytes / n, 3),
                        "compression_ratio_vs_fp32": round(32.0 * n / (8.0 * sbytes), 3),
-                       "pack_flags": pack_flags},
+                       "format_version": int(hdr.version), "pack_flags": pack_flags},
             "compress_ms": round(c_ms, 4), "decompress_ms": round(u_ms, 4),
-            "roofline": {"bound": "hbm", "kernel": "smaq_unpack_kernel",
-                         "achieved": round(u_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(u_gbps / HBM_PEAK_GBPS, 4),
-                         "alg_bytes_per_launch": sbytes + 4 * n, "avg_launch_ms": round(u_ms, 5),
-                         "traffic": traffic_from_profile("packed", n)}}
+            # compress (all its launches: statistics, block codes, scan, variable sections) over
+            # its algorithmic bytes; traffic = the sum of those kernels' PMC bytes per call
+            "roofline": {"bound": "hbm",
+                         "kernel": "smaq_stats_kernel+smaq_pack_block_kernel+smaq_pack_scan_kernel"
+                                   "+smaq_pack_var_kernel",
+                         "achieved": round(c_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(c_gbps / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": int(c_alg),
+                         "avg_launch_ms": round(c_ms, 5),
+                         "traffic": None if traffic is None else traffic["compress"]},
+            "roofline_decompress": {"bound": "hbm", "kernel": "smaq_unpack_kernel",
+                                    "achieved": round(u_gbps, 1), "peak": HBM_PEAK_GBPS,
+                                    "unit": "GB/s", "frac": round(u_gbps / HBM_PEAK_GBPS, 4),
+                                    "alg_bytes_per_launch": int(sbytes + 4 * n),
+                                    "avg_launch_ms": round(u_ms, 5),
+                                    "traffic": None if traffic is None else traffic["decompress"]}}
 
 
 def _vgg_cifar():

@@ -341,28 +341,33 @@ uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
 
 
 /* ---------------------------------------------------------------------------------------------
- * Packed SmaQ container (format version 1)
+ * Packed SmaQ container (format version 2)
  *
- * stream = SmqPackedHeader (128 B) | directory: n_blocks x uint64 (bits 0-37: word offset of the
- *          block in the data region, 38-50: n_out, 51-63: n_esc) | data region (uint32 words)
- * block  = SMQ_PACK_BLOCK elements (the last one may be shorter); its words:
- *   w[0]                 n_out (bits 0-15) | n_esc (bits 16-31)
- *   w[1 .. 128]          outlier mask: bit (e % 32) of word e / 32 = element e is an outlier
- *   codes                one code per element in ELEMENT order, LSB-first across words:
- *                        element e's code starts at bit wm * e + (wo - wm) * (outliers before e),
- *                        wm = num_bits_main - 1, wo = num_bits_outlier - 1;
- *                        main: wm-bit two's-complement q; outlier: top bit = side (1: z < -T,
- *                        the code is -q; 0: z > T, the code is q), the rest = |q|;
- *                        ceil((wm * n + (wo - wm) * n_out) / 32) words
- *   escapes              n_esc x {element index in the block, q as float32 bits}, in element
- *                        order: codes outside the budget (|q| too large, a negative q for z > T,
- *                        a positive q for z < -T, inf / NaN); their codes hold 0 (main) or
- *                        the side bit alone (outlier)
+ * stream = SmqPackedHeader (128 B)
+ *        | directory: n_blocks x uint64 (bits 0-37: word offset of the block's VARIABLE section in
+ *          the variable region, 38-50: n_out, 51-63: n_esc), padded with one zero entry when
+ *          n_blocks is odd
+ *        | fixed region: n_blocks x F words, F = 128 + 128 * wm (block b's at b * F; 16-B aligned)
+ *        | variable region: the blocks' variable sections, in block order
+ * (every region's place but the variable one's depends on n alone; the variable one's on wm too)
+ * block  = SMQ_PACK_BLOCK elements (the last one may be shorter: its absent elements code 0);
+ *   wm = num_bits_main - 1, wo = num_bits_outlier - 1, we = max(0, wo - wm);
+ *   code of an element: main: wm-bit two's-complement q; outlier: wo bits, top bit = side (1: z < -T,
+ *   the code is -q; 0: z > T, the code is q), the rest = |q|; an element whose code does not fit
+ *   the budget (|q| too large, a negative q for z > T, a positive q for z < -T, inf / NaN) is an
+ *   escape: its code is 0 (main) or the side bit alone (outlier), its q is in the escape list.
+ *   fixed section:  w[0 .. 127]  outlier mask: bit (e % 32) of word e / 32 = element e is an outlier
+ *                   w[128 ..]    plane: the low wm bits of element e's code at bit wm * e, LSB-first
+ *   variable section: the outliers' code bits above the plane (we bits each, in element order,
+ *                   LSB-first: ceil(we * n_out / 32) words), then n_esc x {element index in the
+ *                   block, q as float32 bits (any NaN q as 0x7fc00000)} in element order
+ * Size: the same bits as an element-order stream of wm-bit main and wo-bit outlier codes, but the
+ * fixed section can be written the moment its block is coded (no prefix over earlier blocks).
  * Decoding: q -> (q / range) - scalars, * std + mean (smart.py:171-182), bit-identical to
  * smq_smaq_apply for the same statistics, rounding mode and random stream. Needs T_m > 0.
  * ------------------------------------------------------------------------------------------- */
 #define SMQ_PACK_MAGIC 0x50514d53u /* "SMQP" */
-#define SMQ_PACK_VERSION 1u
+#define SMQ_PACK_VERSION 2u
 #define SMQ_PACK_BLOCK 4096
 
 typedef struct SmqPackedHeader {
@@ -379,32 +384,30 @@ typedef struct SmqPackedHeader {
   double inv_range_main, inv_range_outlier;
   uint64_t data_words;        /* size of the data region in uint32 words */
   uint64_t total_bytes;       /* header + directory + data */
-  uint32_t error;             /* nonzero: the packing launch gave up waiting on a predecessor */
+  uint32_t error;             /* 0 (no packing launch waits on another workgroup) */
   uint32_t reserved[9];
 } SmqPackedHeader;
 
-/* Worst-case stream size (every element an outlier and escaped) for n elements. */
+/* Worst-case stream size (every element an outlier and escaped) for n elements; the stream's real
+ * size is header.total_bytes. */
 size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier);
-/* Workspace of smq_smaq_compress (statistics, look-back status words, streaming-packer records
- * of 2 B per element); zero-filled once at allocation, left reusable by every call. */
+/* Workspace of smq_smaq_compress: statistics, per-block sizes, group sums / prefixes and a
+ * 3 KiB scratch slot per block for its variable section (0.75 B per element); needs no
+ * initialisation. */
 size_t smq_smaq_pack_workspace_bytes(int64_t n);
-/* Statistics (full / sampled / range, params as smq_smaq_stats) then the packing launches (see
- * smq_smaq_compress_ex). Writes the whole stream incl. header.total_bytes on the device;
- * packed_bytes >= smq_smaq_pack_bound. The BN variant and injected uniforms are not supported
- * (SMQ_ERR_INVALID). */
+/* Statistics (full / sampled / range, params as smq_smaq_stats) then the packing launches: codes,
+ * fixed sections and variable-section sizes (one workgroup per block), a scan of the group sizes
+ * (header), the variable sections moved to their prefix (one workgroup per 64 blocks; a block
+ * whose section outgrew its scratch slot is re-coded from x there). No launch waits on another
+ * workgroup and the host is never synchronised; the stream incl. header.total_bytes is written on
+ * the device. packed_bytes >= smq_smaq_pack_bound. The BN variant and injected uniforms are not
+ * supported (SMQ_ERR_INVALID). */
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
                       void* packed, size_t packed_bytes, void* workspace, size_t workspace_bytes,
                       void* stream);
-/* Packing flags of smq_smaq_compress_ex; every choice gives the same bytes.
- * Default (flags 0) with both code widths <= 14 bits: the streaming packer, three launches none
- * of which waits on another workgroup (records of 2 B per element in the workspace, a scan of the
- * per-group image sizes, then the block images); never sets header.error.
- * SMQ_PACK_SINGLE (and any code width > 14 bits): ONE packing launch in which block b is placed
- * after blocks 0..b-1 by a decoupled look-back. Workgroup b packs block b: no global atomic per
- * workgroup (a ticket on one address serialises at ~11 ns each: 0.75 ms for 2^16 blocks), which
- * relies on every XCD starting its workgroups in index order. If that ever fails, the bounded
- * look-back spin gives up and sets header.error; SMQ_PACK_TICKETED (implies the single launch)
- * then re-packs with block ids from an atomic ticket (start order: no assumption). */
+/* Packing flags of smq_smaq_compress_ex, kept for ABI compatibility with format version 1 (whose
+ * single-launch look-back packer they selected): accepted and without effect — there is one packer
+ * and it gives the same bytes whatever the flags. */
 #define SMQ_PACK_TICKETED 1u
 #define SMQ_PACK_SINGLE 2u
 int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
@@ -413,6 +416,11 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
 /* Decode a stream of n elements into y (fp32). n must equal the header's n (a stream with another
  * n or a bad magic leaves y untouched). */
 int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream);
+/* The same with the stream's bit widths given by the caller (who compressed it, e.g. with its
+ * hparams): the fixed and variable regions are located without waiting for the header (256M:
+ * ~6 % faster). A stream whose header records other widths leaves y untouched. */
+int smq_smaq_decompress_ex(const void* packed, float* y, int64_t n, int num_bits_main,
+                           int num_bits_outlier, void* stream);
 
 #ifdef __cplusplus
 }

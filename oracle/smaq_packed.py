@@ -1,5 +1,5 @@
 """TEST INFRASTRUCTURE ONLY — numpy restatement of the packed SmaQ container (include/smq.h,
-"Packed SmaQ container", format version 1). The product never imports this module.
+"Packed SmaQ container", format version 2). The product never imports this module.
 
 What it pins: the codes are smart.py's own (oracle.smaq.codes, smart.py:144-169); the container
 stores them losslessly (escape list for anything outside the [outlier flag][sign][N-2 magnitude]
@@ -19,15 +19,21 @@ from . import smaq as osmaq
 
 F32 = np.float32
 MAGIC = 0x50514D53
-VERSION = 1
+VERSION = 2
 BLOCK = 4096
 HEADER_BYTES = 128
+MASK_WORDS = BLOCK // 32
 _HDR = struct.Struct("<IIqIIiiIfffffddQQI36x")
 assert _HDR.size == HEADER_BYTES
 
 
 def _widths(bm: int, bo: int):
     return bm - 1, bo - 1
+
+
+def fixed_words(wm: int) -> int:
+    """Words of a block's fixed section: the outlier mask, then the plane of wm bits per element."""
+    return MASK_WORDS + (wm * BLOCK) // 32
 
 
 def _flags(all_positive: bool, r_main: np.float32, r_out: np.float32) -> int:
@@ -37,7 +43,9 @@ def _flags(all_positive: bool, r_main: np.float32, r_out: np.float32) -> int:
 
 
 def block_codes(q, hi, lo, wm: int, wo: int):
-    """Per element: (plane code, is_outlier, escaped) — smq.h packed format rules."""
+    """Per element: (code, is_outlier, escaped) — smq.h packed format rules. A main code is the
+    wm-bit two's complement q; an outlier code is side << (wo - 1) | |q| (wo bits); a code outside
+    the budget is 0 (main) or the side bit alone (outlier) and the element is escaped."""
     o = hi | lo
     with np.errstate(invalid="ignore"):
         main_lo, main_hi = -(2 ** (wm - 1)), 2 ** (wm - 1) - 1
@@ -58,7 +66,7 @@ def _pack_bits(codes: np.ndarray, width: int) -> np.ndarray:
     """LSB-first concatenation of ``width``-bit codes into uint32 words."""
     n = codes.size
     words = (width * n + 31) // 32
-    if n == 0:
+    if n == 0 or width == 0:
         return np.zeros(0, np.uint32)
     bits = ((codes[:, None] >> np.arange(width, dtype=np.uint64)) & 1).astype(np.uint8).ravel()
     bits = np.concatenate([bits, np.zeros(words * 32 - bits.size, np.uint8)])
@@ -66,55 +74,54 @@ def _pack_bits(codes: np.ndarray, width: int) -> np.ndarray:
 
 
 def _unpack_bits(words: np.ndarray, width: int, n: int) -> np.ndarray:
-    if n == 0:
-        return np.zeros(0, np.uint64)
-    bits = np.unpackbits(words.astype(">u4").view(np.uint8).reshape(-1, 4), axis=1)
+    if n == 0 or width == 0:
+        return np.zeros(n, np.uint64)
+    bits = np.unpackbits(np.asarray(words, np.uint32).astype(">u4").view(np.uint8).reshape(-1, 4),
+                         axis=1)
     bits = bits.reshape(-1, 32)[:, ::-1].ravel()[: width * n].reshape(n, width).astype(np.uint64)
     return (bits << np.arange(width, dtype=np.uint64)).sum(axis=1)
 
 
-def _code_stream(cb, ob, wm: int, wo: int) -> np.ndarray:
-    """Codes concatenated LSB-first in ELEMENT order: element e's code (wm bits if main, wo bits if
-    outlier) starts at bit wm * e + (wo - wm) * (outliers before e)."""
-    widths = np.where(ob, wo, wm).astype(np.int64)
-    n = cb.size
-    total = int(widths.sum())
-    words = (total + 31) // 32
-    if n == 0:
-        return np.zeros(0, np.uint32)
-    wmax = max(wm, wo)
-    bits = ((cb[:, None] >> np.arange(wmax, dtype=np.uint64)) & 1).astype(np.uint8)
-    keep = np.arange(wmax)[None, :] < widths[:, None]
-    flat = bits[keep]  # row-major: element order, LSB first within each code
-    flat = np.concatenate([flat, np.zeros(words * 32 - flat.size, np.uint8)])
-    return np.packbits(flat.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").ravel().astype(np.uint32)
-
-
-def block_words(cb, ob, eb, qb, wm: int, wo: int) -> np.ndarray:
-    """The uint32 image of one block (w[0], mask, code stream, escapes)."""
-    n_out, n_esc = int(ob.sum()), int(eb.sum())
+def block_fixed(cb, ob, wm: int) -> np.ndarray:
+    """The fixed section of one block: 128 mask words (bit e % 32 of word e // 32: element e is an
+    outlier), then the plane: the low wm bits of every element's code at bit wm * e (absent
+    elements of a short last block are zero)."""
+    m = cb.size
     mask = np.zeros(BLOCK, np.uint8)
-    mask[: ob.size] = ob
+    mask[:m] = ob
     mask_words = np.packbits(mask.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").ravel()
+    plane = np.zeros(BLOCK, np.uint64)
+    plane[:m] = cb & np.uint64((1 << wm) - 1)
+    return np.concatenate([mask_words.astype(np.uint32), _pack_bits(plane, wm)])
+
+
+def block_var(cb, ob, eb, qb, wm: int, wo: int) -> np.ndarray:
+    """The variable section of one block: the outliers' code bits above the plane (we = wo - wm
+    bits each, in element order, LSB-first; none when wo <= wm), then the escapes {element index
+    in the block, q as float32 bits} in element order."""
+    we = max(0, wo - wm)
+    ext = _pack_bits(cb[ob] >> np.uint64(wm), we)
     esc_idx = np.nonzero(eb)[0].astype(np.uint32)
-    esc_words = np.stack([esc_idx, qb[esc_idx].view(np.uint32)], axis=1).ravel()
-    return np.concatenate([np.array([n_out | (n_esc << 16)], np.uint32),
-                           mask_words.astype(np.uint32), _code_stream(cb, ob, wm, wo),
-                           esc_words.astype(np.uint32)])
+    qe = np.asarray(qb, F32)[esc_idx]
+    qbits = np.where(np.isnan(qe), np.uint32(0x7FC00000), qe.view(np.uint32))  # one NaN pattern
+    esc_words = np.stack([esc_idx, qbits.astype(np.uint32)], axis=1).ravel()
+    return np.concatenate([ext, esc_words.astype(np.uint32)])
 
 
 def pack_block(xb, mean, std, cfg: osmaq.SmaqConfig, uniforms=None, dtype: str = "f32"):
-    """Image of one block's elements (the GPU stream holds it at its directory offset)."""
+    """(fixed, variable) sections of one block's elements."""
     wm, wo = _widths(cfg.num_bits_main, cfg.num_bits_outlier)
     q, hi, lo, _ = osmaq.codes(np.asarray(xb, F32).ravel(), mean, std, cfg, uniforms, None, dtype)
     code, o, esc = block_codes(q, hi, lo, wm, wo)
-    return block_words(code, o, esc, q, wm, wo)
+    return block_fixed(code, o, wm), block_var(code, o, esc, q, wm, wo)
 
 
 def pack(x, mean, std, cfg: osmaq.SmaqConfig, uniforms: Optional[np.ndarray] = None,
          all_positive: bool = False, dtype: str = "f32") -> np.ndarray:
     """The stream smq_smaq_compress writes, given the device statistics (mean, raw std) and the
-    same uniforms. Returns uint8 bytes."""
+    same uniforms. Returns uint8 bytes: header | directory (padded to an even number of entries)
+    | fixed region | variable region — every region's place but the variable one's depends on n
+    alone, and the fixed region is 16-B aligned."""
     x = np.asarray(x, dtype=F32).ravel()
     n = x.size
     bm, bo = cfg.num_bits_main, cfg.num_bits_outlier
@@ -122,28 +129,28 @@ def pack(x, mean, std, cfg: osmaq.SmaqConfig, uniforms: Optional[np.ndarray] = N
     q, hi, lo, std1 = osmaq.codes(x, mean, std, cfg, uniforms, None, dtype)
     code, o, esc = block_codes(q, hi, lo, wm, wo)
     nb = (n + BLOCK - 1) // BLOCK
-    blocks, offsets, off = [], [], 0
+    fixed, var, dirs, off = [], [], [], 0
     for b in range(nb):
         s = slice(b * BLOCK, min(n, (b + 1) * BLOCK))
-        words = block_words(code[s], o[s], esc[s], q[s], wm, wo)
-        offsets.append(off)
-        off += words.size
-        blocks.append(words)
-    data = np.concatenate(blocks) if blocks else np.zeros(0, np.uint32)
-    # directory entry: word offset (38 bits) | n_out << 38 | n_esc << 51
-    counts = np.array([(int(w[0]) & 0xFFFF, int(w[0]) >> 16) for w in blocks], np.uint64).reshape(-1, 2)
-    offsets = (np.asarray(offsets, np.uint64) | (counts[:, 0] << np.uint64(38))
-               | (counts[:, 1] << np.uint64(51)))
+        fixed.append(block_fixed(code[s], o[s], wm))
+        v = block_var(code[s], o[s], esc[s], q[s], wm, wo)
+        # directory entry: variable-section word offset (38 bits) | n_out << 38 | n_esc << 51
+        dirs.append(off | (int(o[s].sum()) << 38) | (int(esc[s].sum()) << 51))
+        off += v.size
+        var.append(v)
+    fixed_w = np.concatenate(fixed) if fixed else np.zeros(0, np.uint32)
+    var_w = np.concatenate(var) if var else np.zeros(0, np.uint32)
     r_main, r_out = F32(cfg.range_normal), F32(cfg.range_outlier)
-    total = HEADER_BYTES + 8 * nb + 4 * data.size
+    nbp = nb + (nb & 1)
+    total = HEADER_BYTES + 8 * nbp + 4 * (fixed_w.size + var_w.size)
     hdr = _HDR.pack(MAGIC, VERSION, n, BLOCK, nb, bm, bo, _flags(all_positive, r_main, r_out),
                     F32(cfg.main_std_dev_threshold), r_main, r_out, F32(mean), F32(std1),
                     1.0 / float(r_main) if r_main != 0 else float("inf"),
                     1.0 / float(r_out) if r_out != 0 else float("inf"),
-                    data.size, total, 0)
-    return np.concatenate([np.frombuffer(hdr, np.uint8),
-                           np.asarray(offsets, np.uint64).view(np.uint8),
-                           data.view(np.uint8)])
+                    var_w.size, total, 0)
+    dirs += [0] * (nbp - nb)
+    return np.concatenate([np.frombuffer(hdr, np.uint8), np.asarray(dirs, np.uint64).view(np.uint8),
+                           fixed_w.view(np.uint8), var_w.view(np.uint8)])
 
 
 def header(stream: np.ndarray) -> dict:
@@ -154,37 +161,44 @@ def header(stream: np.ndarray) -> dict:
     return dict(zip(keys, f))
 
 
+def regions(stream: np.ndarray):
+    """(header dict, directory uint64[nb], fixed region uint32[nb * F], variable region uint32)."""
+    h = header(stream)
+    nb = h["n_blocks"]
+    wm = h["num_bits_main"] - 1
+    nbp = nb + (nb & 1)
+    dirs = np.asarray(stream[HEADER_BYTES: HEADER_BYTES + 8 * nb], np.uint8).view(np.uint64)
+    f0 = HEADER_BYTES + 8 * nbp
+    fb = 4 * nb * fixed_words(wm)
+    fixed_w = np.asarray(stream[f0: f0 + fb], np.uint8).view(np.uint32)
+    var_w = np.asarray(stream[f0 + fb:], np.uint8).view(np.uint32)
+    return h, dirs, fixed_w, var_w
+
+
 def unpack(stream: np.ndarray) -> np.ndarray:
     """Decode a stream (smq_smaq_decompress): fp32 values in element order."""
-    h = header(stream)
+    h, dirs, fixed_w, var_w = regions(stream)
     assert h["magic"] == MAGIC and h["version"] == VERSION
     n, nb = h["n"], h["n_blocks"]
     wm, wo = _widths(h["num_bits_main"], h["num_bits_outlier"])
-    dirs = np.asarray(stream[HEADER_BYTES: HEADER_BYTES + 8 * nb], np.uint8).view(np.uint64)
-    dirs = dirs & np.uint64((1 << 38) - 1)  # word offsets (n_out / n_esc also live in w[0])
-    data = np.asarray(stream[HEADER_BYTES + 8 * nb:], np.uint8).view(np.uint32)
+    we = max(0, wo - wm)
+    F = fixed_words(wm)
     q = np.zeros(n, F32)
     hi = np.zeros(n, bool)
     lo = np.zeros(n, bool)
     for b in range(nb):
-        base = int(dirs[b])
         m = min(BLOCK, n - b * BLOCK)
-        w0 = int(data[base])
-        n_out, n_esc = w0 & 0xFFFF, w0 >> 16
-        mask_bits = np.unpackbits(data[base + 1: base + 129].astype(">u4").view(np.uint8)
+        d = int(dirs[b])
+        base, n_out, n_esc = d & ((1 << 38) - 1), (d >> 38) & 0x1FFF, d >> 51
+        fx = fixed_w[b * F: (b + 1) * F]
+        mask_bits = np.unpackbits(fx[:MASK_WORDS].astype(">u4").view(np.uint8)
                                   .reshape(-1, 4), axis=1).reshape(-1, 32)[:, ::-1].ravel()
         ob = mask_bits[:m].astype(bool)
-        p = base + 129
-        nw = (wm * m + (wo - wm) * n_out + 31) // 32
-        bits = np.unpackbits(data[p: p + nw].astype(">u4").view(np.uint8).reshape(-1, 4),
-                             axis=1).reshape(-1, 32)[:, ::-1].ravel().astype(np.uint64)
-        r_out = np.concatenate([[0], np.cumsum(ob)[:-1]]).astype(np.int64)
-        pos = wm * np.arange(m, dtype=np.int64) + (wo - wm) * r_out
-        widths = np.where(ob, wo, wm)
-        cd = np.zeros(m, np.uint64)
-        for t in range(max(wm, wo)):
-            sel = t < widths
-            cd[sel] |= bits[pos[sel] + t] << np.uint64(t)
+        assert int(ob.sum()) == n_out
+        cd = _unpack_bits(fx[MASK_WORDS:], wm, m)
+        n_ext = (we * n_out + 31) // 32
+        ext = _unpack_bits(var_w[base: base + n_ext], we, n_out)
+        cd[ob] |= ext << np.uint64(wm)
         cd = cd.astype(np.int64)
         qm = np.where(cd >= 2 ** (wm - 1), cd - 2**wm, cd)
         side = (cd >> (wo - 1)) & 1
@@ -193,7 +207,7 @@ def unpack(stream: np.ndarray) -> np.ndarray:
         qb = np.where(ob, qo, qm).astype(F32)
         hb = ob & (side == 0)
         lb = ob & (side == 1)
-        e = data[p + nw: p + nw + 2 * n_esc].reshape(-1, 2)
+        e = var_w[base + n_ext: base + n_ext + 2 * n_esc].reshape(-1, 2)
         qb[e[:, 0].astype(np.int64)] = e[:, 1].view(F32)
         s = slice(b * BLOCK, b * BLOCK + m)
         q[s], hi[s], lo[s] = qb, hb, lb

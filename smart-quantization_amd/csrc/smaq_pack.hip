@@ -1,26 +1,32 @@
-// Packed SmaQ container (include/smq.h "Packed SmaQ container") on gfx950.
+// Packed SmaQ container, format version 2 (include/smq.h "Packed SmaQ container"),
+// on gfx950.
 //
-// compress = statistics (smaq.hip, full or sampled) + the streaming packer (default, code widths
-// <= 14 bits; see "streaming packer" below): smaq_code_kernel (one 16-bit record per element and
-// the block's image size into its group sum) -> smaq_pack_scan_kernel (group prefixes, header) ->
-// smaq_emit_kernel (each block's image at its prefix). No workgroup waits on another.
-// SMQ_PACK_SINGLE (and wider codes) take ONE packing launch instead:
-//   * each workgroup owns a block of SMQ_PACK_BLOCK = 4096 elements (16 per lane, 4 x dwordx4),
-//     quantises them with the same element code as the simulated round trip (smaq_quant), and
-//     builds the block image in LDS: outlier mask and the element-order code stream (LDS ORs;
-//     ranks from DPP wave scans + per-wave segment prefixes);
-//   * blocks are compacted into one dense stream by a decoupled look-back scan: workgroup b packs
-//     block b (index order; SMQ_PACK_TICKETED takes ids from an atomic ticket instead), publishes
-//     its size, and wave 0 reads up to 64 predecessors' status words per step until it meets an
-//     inclusive prefix. Status words are single 64-bit relaxed agent-scope atomics carrying their
-//     value, so no fences are needed; a bounded spin turns a would-be hang into header.error;
-//   * the block image is written with coalesced stores at its prefix, escapes directly, and the
-//     block's word offset into the directory (random-access decode).
-// Both give the same bytes.
-// decompress = one launch, one workgroup per block: block image -> LDS, mask prefix popcounts,
-//   per-element plane reads, escapes via an LDS bitmask + O(1) rank in the block's sorted list,
-//   then smaq_dequant — the same arithmetic as the simulated round trip, so the result is
-//   bit-identical to smq_smaq_apply for the same statistics and random stream.
+// The codes are smart.py's own (smart.py:144-169, the same smaq_quant as the simulated round trip);
+// the container splits every block of SMQ_PACK_BLOCK = 4096 elements into
+//   * a FIXED section (outlier mask + a plane of wm = num_bits_main - 1 bits per element: the low
+//     wm bits of each code), whose size does not depend on the data, so block b's lands at b * F
+//     words without knowing any other block, and
+//   * a VARIABLE section (the outliers' remaining wo - wm code bits, then the escape list), small
+//     (~0.09 B/element at 6/8 bits), placed by a prefix over the blocks.
+// compress = statistics (smaq.hip) + three launches, none of which waits on another workgroup:
+//   smaq_pack_block_kernel  one workgroup per block: x -> codes (registers) -> mask / plane / outlier
+//                           ranks in LDS -> the fixed section straight into the stream, the variable
+//                           section into a per-block scratch slot (kVarCap words), its size into the
+//                           block's group sum;
+//   smaq_pack_scan_kernel   one workgroup: exclusive prefix of the group sums, the header;
+//   smaq_pack_var_kernel    one workgroup per group of 64 blocks: directory entries, the variable
+//                           sections copied from scratch to their prefix; a block whose section
+//                           outgrew its slot (escape-heavy data) is re-coded from x right there.
+// HBM traffic: x read once (4 B/elem), the stream written once (0.93 B/elem at 6/8 bits on N(0,1)),
+// plus the variable sections through scratch (~0.18 B/elem). The round-1/2 container (version 1)
+// interleaved codes of two widths in element order, so every block needed its prefix before its
+// first code could be placed: 2 B/elem of records went to HBM and back (1.45x the algorithmic
+// bytes).
+// decompress = one launch, one workgroup per block: fixed section + variable section -> LDS, mask
+//   prefix popcounts for the outlier ranks, escapes via an LDS bitmask + O(1) rank, then
+//   smaq_dequant (or a per-block table of it for narrow codes) — the same arithmetic as the
+//   simulated round trip, so the result is bit-identical to smq_smaq_apply for the same
+//   statistics and random stream.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
@@ -33,464 +39,138 @@
 namespace smq {
 namespace {
 
-constexpr int kPB = SMQ_PACK_BLOCK;
-constexpr int kMaskWords = kPB / 32;            // 128
-constexpr int kHdrWords = 1 + kMaskWords;       // w[0] + mask
-constexpr int kMaxWidth = 24;                   // widest code (num_bits - 1)
-constexpr int kStageWords = kHdrWords + (kMaxWidth * kPB) / 32 + 2;
-constexpr uint64_t kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 22;       // ~0.5 s of polling before giving up
+constexpr int kPB = SMQ_PACK_BLOCK;          // 4096 elements per block
+constexpr int kMaskWords = kPB / 32;         // 128
+constexpr int kMaxWidth = 24;                // widest code (num_bits - 1)
+constexpr int kGroup = 64;                   // blocks per group sum (one per lane of a wave)
+constexpr int kVarCap = 768;                 // scratch words per block for its variable section
+constexpr int kSegs = 16;                    // rank segments of a block: 4 slots x 4 waves
 
 static_assert(sizeof(SmqPackedHeader) == 128, "packed header layout");
+
+// directory entries incl. the padding that keeps the fixed region 16-B aligned
+__host__ __device__ inline int64_t dir_entries(int64_t nb) { return (nb + 1) & ~(int64_t)1; }
+__host__ __device__ inline uint32_t fixed_words(int wm) { return kMaskWords + 128u * (uint32_t)wm; }
+__host__ __device__ inline uint32_t ext_words(int we, uint32_t n_out) {
+  return ((uint32_t)we * n_out + 31u) / 32u;
+}
 
 struct PackArgs {
   const void* x;
   int64_t n;
   SmqPackedHeader* hdr;
-  uint64_t* dir;
-  uint32_t* data;
+  uint32_t* fixed;           // n_blocks * F words
+  uint64_t* dir;             // n_blocks entries
+  uint32_t* var;             // variable region
   const SmqSmaqStats* stats;
-  uint64_t* status;          // [n_blocks] block aggregates
-  uint64_t* gstatus;         // [n_groups] group aggregates / inclusive prefixes
-  uint32_t* counter;
+  uint32_t* scratch;         // n_blocks * kVarCap words
+  uint32_t* meta;            // [n_blocks] n_out | n_esc << 16 | kMetaRecode
+  uint32_t* gsum;            // [n_groups] variable words of each group of kGroup blocks
+  uint64_t* gpre;            // [n_groups] exclusive prefix of gsum
   float thr, r_main, r_out;
   double inv_r_main, inv_r_out;
   uint32_t key;
   uint64_t offset;
   int wm, wo, bm, bo;
   uint32_t n_blocks;
-  uint32_t n_full;           // blocks of SMQ_PACK_BLOCK elements (the main launch)
-  int ticketed;              // SMQ_PACK_TICKETED: block ids from an atomic ticket
-  uint32_t flags;
-  int place_atomic;          // measurement knob (SMQ_PACK_PLACE=atomic): see smq_smaq_compress
-  uint32_t stage_words;      // LDS stage (w[0], mask, code stream) for these widths; q values follow
-  unsigned long long* cursor;
-  // streaming packer (smaq_code_kernel / smaq_pack_scan_kernel / smaq_emit_kernel)
-  uint16_t* rec;             // [n_blocks * SMQ_PACK_BLOCK] element records
-  uint32_t* meta;            // [n_blocks] n_out | n_esc << 16
-  uint32_t* gsum;            // [n_groups] image words of each group of kGroup blocks
-  uint64_t* gpre;            // [n_groups] exclusive prefix of gsum
+  uint32_t n_full;           // blocks of SMQ_PACK_BLOCK elements
   uint32_t n_groups;
+  uint32_t flags;
+  uint32_t lds_words;        // dynamic LDS of the packing kernels (PackLds::words)
 };
 
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+// smart.py:151-169 for one element, as smaq_quant computes it (same IEEE ops in the same order, so
+// the same q), in the packer's branch-free form: the scalars term is a select, since with T > 0
+// (a packer precondition) hi and lo exclude each other and (hi ? -T : -0.0) + (lo ? T : +0.0) is
+// -T, T or +0.0 exactly. Returns q; o = outlier, lo = below -T.
+template <int RM, int TIN, bool SUB>
+__device__ __forceinline__ float pack_quant(float v, float u, const ElemConsts& c, bool& o, bool& lo) {
+  const float dm = round_in<TIN>(v - c.mean);           // data - mean
+  float z = div_by_const(dm, c.inv_sc);                 // / std.clamp(...)
+  if (SUB && __builtin_expect(__builtin_amdgcn_classf(z, 0x90), 0)) z = dm / c.sc;
+  z = round_in<TIN>(z);
+  const bool hi = z > c.cthr;
+  lo = z < c.cnthr;
+  o = hi | lo;
+  const float a = hi ? c.nthr : (lo ? c.thr : 0.0f);    // scalars
+  const float r = o ? c.r_out : c.r_main;               // ranges
+  const float d = (z + a) * r;
+  if (RM == kRoundTrunc) return truncf(d);
+  const float f = floorf(d);                            // _round_stochastic
+  const float fr = d - f;
+  float t = __builtin_fmaf(u, -0x1p-24f, fr) + 0.5f;
+  t = (t < 0.0f) ? 0.0f : t;
+  return f + __builtin_rintf(t);
 }
 
-// Plane code of one element (smq.h rules), branch-free; esc = the code does not fit the budget.
-__device__ __forceinline__ uint32_t classify(float q, bool hi, bool lo, int wm, int wo, bool& esc) {
-  const bool o = hi | lo;
-  const float lim = (float)(1 << (wm - 1));
-  const bool ok_m = (q >= -lim) && (q <= lim - 1.0f);          // false for NaN
-  const float mag = hi ? q : -q;                                // hi: q >= 0, lo: q <= 0
-  const bool ok_o = (mag >= 0.0f) && (mag <= (float)((1 << (wo - 1)) - 1));
-  const uint32_t code_m = (uint32_t)(int32_t)q & ((1u << wm) - 1u);
-  const uint32_t code_o = (lo ? (1u << (wo - 1)) : 0u) | (ok_o ? (uint32_t)(int32_t)mag : 0u);
-  const bool ok = o ? ok_o : ok_m;
-  esc = !ok;
-  return o ? code_o : (ok_m ? code_m : 0u);
+// Code of one element (smq.h format rules), branch-free integer form: v = q + 2^(wm-1) for a main
+// (fits: v < 2^wm; the code is v ^ 2^(wm-1) = q's wm-bit two's complement), |q| on the element's
+// side for an outlier (fits: v < 2^(wo-1); the code is side << (wo-1) | v). |q| > 2^24, inf and NaN
+// always escape; an escaped main codes 0, an escaped outlier its side bit alone.
+// hm = 2^(wm-1), side = 2^(wo-1), lim_m = 2^wm
+__device__ __forceinline__ uint32_t code_sel(float q, bool o, bool lo, uint32_t hm, uint32_t side,
+                                             uint32_t lim_m, bool& esc) {
+  const int qi = (int)q;
+  const bool big = !(__builtin_fabsf(q) <= 0x1p24f);     // also NaN
+  const uint32_t hsel = o ? 0u : hm;
+  const uint32_t vv = lo ? (uint32_t)(-qi) : (uint32_t)qi + hsel;
+  const uint32_t lim = o ? side : lim_m;
+  esc = big | !(vv < lim);
+  const uint32_t sb = lo ? side : 0u;
+  return esc ? sb : ((vv ^ hsel) | sb);
 }
 
-constexpr int kGroup = 64;  // blocks per look-back group (one status word per lane)
+// OR a chunk of up to 64 bits at bit pos of an LDS bit stream (two or three words; the third only
+// when bits land there).
+__device__ __forceinline__ void or_bits64(uint32_t* base, uint32_t pos, uint64_t chunk) {
+  const uint32_t sft = pos & 31u, w0 = pos >> 5;
+  const uint64_t lo = chunk << sft;
+  const uint32_t hi = sft ? (uint32_t)(chunk >> (64u - sft)) : 0u;
+  if ((uint32_t)lo) atomicOr(base + w0, (uint32_t)lo);
+  if ((uint32_t)(lo >> 32)) atomicOr(base + w0 + 1, (uint32_t)(lo >> 32));
+  if (hi) atomicOr(base + w0 + 2, hi);
+}
 
-// Poll until lanes [0, count) hold a published status (flag != 0); returns this lane's value.
-__device__ __forceinline__ uint64_t wait_all(const PackArgs& A, const uint64_t* st, int count,
-                                             uint32_t& spins) {
-  const int lane = threadIdx.x & (kWave - 1);
-  for (;;) {
-    const uint64_t v = lane < count ? ld_sc1_u64(st + lane) : kAgg;
-    if (!__ballot((v >> 62) == 0ull)) return v;
-    if (++spins >= kSpinLimit) {
-      if (lane == 0) atomicOr(&A.hdr->error, 1u);  // give up: the stream is marked broken
-      return v;
-    }
-    __builtin_amdgcn_s_sleep(2);
+// OR a chunk of up to 32 bits at bit pos of an LDS bit stream (one or two words).
+__device__ __forceinline__ void or_bits32(uint32_t* base, uint32_t pos, uint32_t chunk) {
+  const uint32_t sft = pos & 31u, w0 = pos >> 5;
+  atomicOr(base + w0, chunk << sft);
+  const uint32_t hi = sft ? (chunk >> (32u - sft)) : 0u;
+  if (hi) atomicOr(base + w0 + 1, hi);
+}
+
+// Escapes of one rank segment (256 elements) a block keeps in LDS before the segment bases are
+// known; a segment with more (an escape-heavy block) makes the var kernel re-code the block.
+constexpr int kSegEsc = 32;
+// meta bit: the block's variable section is not in its scratch slot (re-code it)
+constexpr uint32_t kMetaRecode = 1u << 31;
+
+// Dynamic LDS of the packing kernels (words): the fixed image (mask, plane), the outlier-bit
+// stream, the 16 segments' escape lists {element, q bits}, the 16 segment counts.
+struct PackLds {
+  static uint32_t words(int wm, int we) {
+    return fixed_words(wm) + 128u * (uint32_t)we + 2u * kSegs * kSegEsc + kSegs + 4u;
   }
-}
+};
 
-// Two-level decoupled look-back (wave 0). Returns the exclusive prefix (words) of block b.
-// Level 1: the blocks of b's group of 64 publish their sizes (one window read). Level 2: the
-// group's last block publishes the group aggregate, walks back over group words (64 groups =
-// 4096 blocks per read) to the nearest inclusive prefix and publishes its own; every block of the
-// group walks the same group words. A single-level scan advances one 64-block window per memory
-// round trip (~1 us): 65536 blocks took 1.1 ms; two levels move 4096 blocks per round trip.
-__device__ uint64_t look_back(const PackArgs& A, uint32_t b, uint64_t size) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t g = b / kGroup, i = b % kGroup;
-  const bool last = (i == kGroup - 1) || (b == A.n_blocks - 1);
-  uint32_t spins = 0;
-  if (lane == 0) st_sc1_u64(A.status + b, kAgg | size);
-  // level 1: sizes of the group's earlier blocks
-  uint64_t lp = 0;
-  if (i > 0) {
-    const uint64_t v = wait_all(A, A.status + (uint64_t)g * kGroup, (int)i, spins);
-    lp = wave_sum_u64(lane < (int)i ? (v & kValMask) : 0ull);
-  }
-  if (last && lane == 0) st_sc1_u64(A.gstatus + g, (g == 0 ? kIncl : kAgg) | (lp + size));
-  // level 2: prefix of the groups before g
-  uint64_t gp = 0;
-  if (g > 0) {
-    int64_t j = (int64_t)g - 1;
-    for (;;) {
-      const int64_t idx = j - lane;
-      const uint64_t v = idx >= 0 ? ld_sc1_u64(A.gstatus + idx) : kIncl;  // before group 0: 0
-      const uint32_t flag = (uint32_t)(v >> 62);
-      const uint64_t incl = __ballot(flag == 2u);
-      const uint64_t invalid = __ballot(flag == 0u);
-      const int first = incl ? __builtin_ctzll(incl) : 64;
-      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
-      if ((invalid & need) && ++spins < kSpinLimit) {
-        __builtin_amdgcn_s_sleep(2);
-        continue;
-      }
-      if (spins >= kSpinLimit && lane == 0) atomicOr(&A.hdr->error, 1u);
-      gp += wave_sum_u64(lane <= first ? (v & kValMask) : 0ull);
-      if (first < 64 || spins >= kSpinLimit) break;
-      j -= 64;
-    }
-    if (last && lane == 0) st_sc1_u64(A.gstatus + g, kIncl | (gp + lp + size));
-  }
-  return gp + lp;
-}
-
-// OR a code chunk (< 2^32) at bit pos of an LDS bit stream (two words; ORing 0 is harmless).
-__device__ __forceinline__ void or_bits(uint32_t* base, uint32_t pos, uint32_t chunk) {
-  const uint64_t v = (uint64_t)chunk << (pos & 31u);
-  atomicOr(base + (pos >> 5), (uint32_t)v);
-  atomicOr(base + (pos >> 5) + 1, (uint32_t)(v >> 32));
-}
-
-// FULL: the block holds SMQ_PACK_BLOCK elements (every block but a ragged last one).
-// WM / WO: code widths compiled in (0: runtime widths). With WO <= 8 a lane's four codes form one
-// chunk of at most 28 bits written by two LDS ORs.
-template <int RM, int TIN, bool SUB, bool VEC, bool FULL, int WM, int WO>
-__device__ __forceinline__ void pack_body(const PackArgs& A, const ElemConsts& c, uint32_t b,
-                                          uint32_t* stage, float* qlds) {
-  __shared__ uint32_t seg_cnt[2][16];
-  __shared__ uint32_t seg_pre[2][17];
-  __shared__ uint64_t s_prefix;
-  constexpr bool kChunk = WO > 0 && WO <= 8;
+// One block (smaq_pack_block_kernel): codes of its elements, its fixed image in LDS -> the stream
+// at b * F, outlier ranks and escapes -> the variable section in the block's scratch slot (unless
+// it outgrows kVarCap or a segment's escape list: then the var kernel re-codes the block), the
+// section's size -> meta / the group sum.
+template <int RM, int TIN, bool VEC, bool FULL, bool SUB, int WM, int WO>
+__device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, uint32_t* lds) {
+  constexpr int kWE = (WM > 0 && WO > 0) ? (WO > WM ? WO - WM : 0) : -1;  // -1: runtime
   const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
+  const int we = kWE >= 0 ? kWE : (wo > wm ? wo - wm : 0);
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
-  uint32_t* codes_lds = stage + kHdrWords;
-
-  // 1. codes of this lane's 16 elements: local index el = 1024 k + 4 tid + i. Every q also goes to
-  //    LDS (one 16-B store per float4): the escape list reads it back after the scan (re-deriving
-  //    it cost a reload + the element chain; keeping it in registers cost occupancy)
-  uint32_t code[16];
-  uint32_t om[4], xm[4];
-  // all four 16-B loads of the lane in flight before any element is processed
-  float xv[4][4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int el = 1024 * k + 4 * tid;
-    if (VEC && (FULL || el + 3 < n_el)) {
-      const float4 t = load4_stream<TIN>(A.x, (e0 + el) >> 2);
-      xv[k][0] = t.x; xv[k][1] = t.y; xv[k][2] = t.z; xv[k][3] = t.w;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        xv[k][i] = (FULL || el + i < n_el) ? load1<TIN>(A.x, e0 + el + i) : 0.f;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int el = 1024 * k + 4 * tid;
-    float u[4] = {0.f, 0.f, 0.f, 0.f};
-    const float* v = xv[k];
-    const bool full4 = FULL || el + 3 < n_el;
-    if (RM == kRoundHash) {
-      const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
-      if (full4) {
-        rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (el + i < n_el) u[i] = rng_hu(A.key, ctr + i);
-      }
-    }
-    om[k] = 0u;
-    xm[k] = 0u;
-    float qk[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bool hi, lo, esc = false;
-      const float q = smaq_quant<RM, false, TIN, SUB>(v[i], u[i], c, hi, lo);
-      const bool valid = FULL || el + i < n_el;
-      code[4 * k + i] = valid ? classify(q, hi, lo, wm, wo, esc) : 0u;
-      qk[i] = q;
-      om[k] |= (uint32_t)((hi | lo) && valid) << i;
-      xm[k] |= (uint32_t)(esc && valid) << i;
-    }
-    *reinterpret_cast<float4*>(qlds + el) = make_float4(qk[0], qk[1], qk[2], qk[3]);
-  }
-
-  // 2. outlier / escape ranks: per 256-element segment s = 4 k + wave, lane prefixes by ballots;
-  //    mask words from nibbles (8 lanes per word) by three xor-shuffles
-  uint32_t pre_o[4], pre_x[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t cnt = (uint32_t)__popc(om[k]) | ((uint32_t)__popc(xm[k]) << 16);
-    const uint32_t incl = wave_incl_scan_u32(cnt);
-    const uint32_t ex = incl - cnt;
-    pre_o[k] = ex & 0xffffu;
-    pre_x[k] = ex >> 16;
-    const uint32_t mw = group8_or_to_last(om[k] << (4 * (lane & 7)));
-    if ((lane & 7) == 7) stage[1 + ((1024 * k + 4 * (tid - 7)) >> 5)] = mw;
-    if (lane == kWave - 1) {
-      seg_cnt[0][4 * k + w] = incl & 0xffffu;
-      seg_cnt[1][4 * k + w] = incl >> 16;
-    }
-  }
-  const uint32_t code_cap = A.stage_words - kHdrWords;
-  for (uint32_t i = tid; i < code_cap; i += kBlock) codes_lds[i] = 0u;
-  __syncthreads();
-  if (tid < 2) {
-    uint32_t run = 0;
-    for (int s = 0; s < 16; ++s) {
-      seg_pre[tid][s] = run;
-      run += seg_cnt[tid][s];
-    }
-    seg_pre[tid][16] = run;
-  }
-  __syncthreads();
-  const uint32_t n_out = seg_pre[0][16], n_esc = seg_pre[1][16];
-  const uint32_t code_words = ((uint32_t)wm * (uint32_t)n_el + (uint32_t)(wo - wm) * n_out + 31u) / 32u;
-  const uint32_t img_words = kHdrWords + code_words;
-  const uint64_t size = (uint64_t)img_words + 2ull * n_esc;
-
-  // 3. wave 0 starts the look-back; every lane ORs its codes into the LDS code stream at
-  //    pos(el) = wm * el + (wo - wm) * (outliers before el)
-  if (A.place_atomic) {
-    if (tid == 0) s_prefix = atomicAdd(A.cursor, (unsigned long long)size);
-  } else if (w == 0) {
-    const uint64_t p = look_back(A, b, size);
-    if (lane == 0) s_prefix = p;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t el0 = 1024u * k + 4u * tid;
-    if (!FULL && (int)el0 >= n_el) continue;
-    const uint32_t r0 = seg_pre[0][4 * k + w] + pre_o[k];
-    const uint32_t pos0 = (uint32_t)wm * el0 + (uint32_t)(wo - wm) * r0;
-    if (kChunk) {
-      uint32_t chunk = 0u, off = 0u;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        chunk |= code[4 * k + i] << off;  // invalid tail elements carry code 0, width wm
-        off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
-      }
-      or_bits(codes_lds, pos0, chunk);
-    } else {
-      uint32_t off = 0u;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        or_bits(codes_lds, pos0 + off, code[4 * k + i]);
-        off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
-      }
-    }
-  }
-  __syncthreads();
-
-  // 4. the block image at its prefix, its escapes and directory entry
-  const uint64_t P = s_prefix;
-  uint32_t* out = A.data + P;
-  for (uint32_t i = tid; i < img_words; i += kBlock)
-    out[i] = i == 0 ? (n_out | (n_esc << 16)) : stage[i];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (!xm[k]) continue;
-    const uint32_t base_x = seg_pre[1][4 * k + w] + pre_x[k];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (!((xm[k] >> i) & 1u)) continue;
-      const uint32_t r = base_x + __popc(xm[k] & ((1u << i) - 1u));
-      out[img_words + 2 * r] = 1024u * k + 4u * tid + i;
-      out[img_words + 2 * r + 1] = __float_as_uint(qlds[1024u * k + 4u * tid + i]);
-    }
-  }
-  if (tid == 0) {
-    // directory entry: word offset (38 bits) | n_out << 38 | n_esc << 51 (decoder: no dependent
-    // load of w[0] before the block image)
-    A.dir[b] = P | ((uint64_t)n_out << 38) | ((uint64_t)n_esc << 51);
-    if (!A.place_atomic && b == A.n_blocks - 1) {
-      A.hdr->data_words = P + size;
-      A.hdr->total_bytes = sizeof(SmqPackedHeader) + 8ull * A.n_blocks + 4ull * (P + size);
-    }
-    if (b == 0) {
-      SmqPackedHeader* h = A.hdr;
-      h->magic = SMQ_PACK_MAGIC;
-      h->version = SMQ_PACK_VERSION;
-      h->n = A.n;
-      h->block_elems = kPB;
-      h->n_blocks = A.n_blocks;
-      h->num_bits_main = A.bm;
-      h->num_bits_outlier = A.bo;
-      h->flags = A.flags;
-      h->thr = A.thr;
-      h->range_main = A.r_main;
-      h->range_outlier = A.r_out;
-      h->mean = c.mean;
-      h->std_dev = c.sd;
-      h->inv_range_main = A.inv_r_main;
-      h->inv_range_outlier = A.inv_r_out;
-    }
-  }
-}
-
-// One kernel per (widths, full/ragged), chosen on the host, each with ONE body: with the eight
-// (quot_check x full x widths) bodies in one kernel the uniform constants spilled 568 SGPRs
-// (v_writelane / v_readlane traffic on the VALU) and took 104 VGPRs.
-// FULL: the main launch, blocks of SMQ_PACK_BLOCK elements. !FULL: the ragged last
-// block, launched as one workgroup after the main launch (its look-back finds every predecessor
-// published).
-template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO>
-__global__ __launch_bounds__(kBlock) void smaq_pack_kernel(PackArgs A) {
-  extern __shared__ uint32_t pack_lds[];  // [stage_words] stage, then [kPB] q values
-  uint32_t* stage = pack_lds;
-  float* qlds = reinterpret_cast<float*>(pack_lds + A.stage_words);
-  uint32_t b;
-  if (FULL) {
-    if (A.ticketed) {  // block ids in start order: predecessors are resident by construction
-      __shared__ uint32_t s_b;
-      if (threadIdx.x == 0) {
-        const uint32_t id = atomicAdd(A.counter, 1u);
-        if (id == A.n_full - 1) atomicExch(A.counter, 0u);  // every id is taken: reset for reuse
-        s_b = id;
-      }
-      __syncthreads();
-      b = s_b;
-    } else {  // index order (see SMQ_PACK_TICKETED in smq.h)
-      b = blockIdx.x;
-    }
-  } else {
-    b = A.n_blocks - 1;
-  }
-  ElemConsts c;
-  const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);  // z is compared in its type
-  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
-  // SUB = true regardless of stats->quot_check: the IEEE re-division of a subnormal quotient is
-  // exact either way, and one body (no device-side dispatch) keeps the constants in registers
-  pack_body<RM, TIN, true, VEC, FULL, WM, WO>(A, c, b, stage, qlds);
-}
-
-template <int RM, int TIN>
-void launch_pack(const PackArgs& A, bool vec, size_t lds, hipStream_t st) {
-  const bool w57 = A.wm == 5 && A.wo == 7;  // the default 6/8-bit budget, widths compiled in
-  const dim3 grid(A.n_full), block(kBlock);
-  if (A.n_full > 0) {
-    if (vec) {
-      if (w57) hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, true, true, 5, 7>), grid, block, lds, st, A);
-      else hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, true, true, 0, 0>), grid, block, lds, st, A);
-    } else {
-      if (w57) hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, false, true, 5, 7>), grid, block, lds, st, A);
-      else hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, false, true, 0, 0>), grid, block, lds, st, A);
-    }
-  }
-  if (A.n_full < A.n_blocks)
-    hipLaunchKernelGGL((smaq_pack_kernel<RM, TIN, false, false, 0, 0>), dim3(1), block, lds, st, A);
-}
-
-// ---- streaming packer (the default when both code widths are <= kRecCodeBits) ----------------
-// The single packing launch above chains load -> quantise -> rank scan -> look-back -> image per
-// block in one workgroup; PMC showed it latency-bound (57 % of wave time in s_waitcnt / barriers,
-// VALU ~50 % busy). Here the same bytes come from three plain streaming launches, none of which
-// waits on another workgroup:
-//   1. smaq_code_kernel — one workgroup per block quantises its elements with pack_body's element
-//      code (same smaq_quant / classify) and writes one 16-bit record per element: bit 15 outlier,
-//      bit 14 escape; a plane code in bits 0-13, or for an escape the side (z < -T) in bit 13 and q
-//      in bits 0-12 (two's complement; kRecBig = q outside [-4095, 4095] or not finite: the emitter
-//      re-derives q from x). It adds the block's image size to its group sum (one atomic per
-//      workgroup, 64 blocks per group) and stores n_out | n_esc.
-//   2. smaq_pack_scan_kernel — one workgroup: exclusive scan of the group sums (zeroed by a
-//      memset before phase 1), writes the header.
-//   3. smaq_emit_kernel — one workgroup per block: prefix = its group's prefix + the sizes of its
-//      group predecessors (one load per lane), records -> ranks -> LDS code stream -> block image.
-// Traffic: 4 B/elem read + 2 B/elem records written, 2 B/elem records read + the stream written.
-constexpr int kRecCodeBits = 14;
-constexpr int kRecBig = -4096;
-
-__device__ __forceinline__ uint32_t block_image_words(int wm, int wo, uint32_t n_el, uint32_t n_out) {
-  return (uint32_t)kHdrWords + ((uint32_t)wm * n_el + (uint32_t)(wo - wm) * n_out + 31u) / 32u;
-}
-
-// Record of one element: classify()'s plane code / escape decision in integer ops (fewer selects).
-// v = q + 2^(wm-1) for a main (fits: v < 2^wm), |q| on the element's side for an outlier (fits:
-// v < 2^(wo-1)); |q| > 2^24, inf and NaN always escape (widths are at most 14 bits here). An
-// escape record carries q when |q| <= 4095, else kRecBig (the emitter re-derives q).
-__device__ __forceinline__ uint32_t record_of(float q, bool hi, bool lo, int wm, int wo, bool& esc) {
-  const bool o = hi | lo;
-  const int qi = (__builtin_fabsf(q) <= 0x1p24f) ? (int)q : -(1 << 30);
-  const uint32_t half_m = 1u << (wm - 1), side = 1u << (wo - 1);
-  const uint32_t v = (uint32_t)(lo ? -qi : (o ? qi : qi + (int)half_m));
-  const uint32_t lim = o ? side : 2u * half_m;
-  esc = !(v < lim);
-  const uint32_t code = o ? ((lo ? side : 0u) | v) : (v ^ half_m);
-  const int qe = ((uint32_t)(qi + 4095) <= 8190u) ? qi : kRecBig;
-  return esc ? (0x4000u | ((uint32_t)o << 15) | ((uint32_t)lo << 13) | ((uint32_t)qe & 0x1fffu))
-             : (((uint32_t)o << 15) | code);
-}
-
-// Records of one lane's 16 elements (smaq_code_kernel); returns its outliers | escapes << 16.
-template <int RM, int TIN, bool FULL, bool SUB>
-__device__ __forceinline__ uint32_t code_records(const PackArgs& A, const ElemConsts& c,
-                                                 const float (&xv)[4][4], int64_t e0, int n_el,
-                                                 int wm, int wo) {
-  const int tid = threadIdx.x;
-  uint32_t cnt = 0;  // outliers (bits 0-15) | escapes (bits 16-31) of this lane's elements
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int el = 1024 * k + 4 * tid;
-    const bool full4 = FULL || el + 3 < n_el;
-    float u[4] = {0.f, 0.f, 0.f, 0.f};
-    if (RM == kRoundHash) {
-      const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
-      if (full4) {
-        rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (el + i < n_el) u[i] = rng_hu(A.key, ctr + i);
-      }
-    }
-    uint32_t r[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bool hi, lo, esc;
-      const float q = smaq_quant<RM, false, TIN, SUB>(xv[k][i], u[i], c, hi, lo);
-      r[i] = record_of(q, hi, lo, wm, wo, esc);
-      const bool o = hi | lo;
-      const bool valid = FULL || el + i < n_el;
-      cnt += valid ? ((uint32_t)o | ((uint32_t)esc << 16)) : 0u;
-    }
-    uint16_t* dst = A.rec + e0 + el;
-    if (full4) {
-      *reinterpret_cast<uint2*>(dst) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (el + i < n_el) dst[i] = (uint16_t)r[i];
-    }
-  }
-  return cnt;
-}
-
-// One workgroup per block (half-block workgroups, the second to finish adding the block's size,
-// measured 357 vs 338 us at 256M).
-template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO>
-__global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
-  __shared__ uint32_t s_cnt[kBlock / kWave];
-  const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
-  // blocks in reverse address order: the statistics sweep just read x front to back, so its tail
-  // is still in the Infinity Cache (331 vs 335 us); the emitter then walks forward
-  const uint32_t b = FULL ? A.n_full - 1 - blockIdx.x : A.n_blocks - 1;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-  const int64_t e0 = (int64_t)b * kPB;
-  const int n_el = FULL ? kPB : (int)(A.n - e0);
+  const uint32_t F = fixed_words(wm);
+  uint32_t* mask = lds;
+  uint32_t* plane = lds + kMaskWords;
+  uint32_t* ext = lds + F;
+  uint32_t* elist = ext + 128 * we;                  // [kSegs][kSegEsc][2]
+  uint32_t* seg = elist + 2 * kSegs * kSegEsc;
   ElemConsts c;
   const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
   init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
@@ -507,20 +187,212 @@ __global__ __launch_bounds__(kBlock) void smaq_code_kernel(PackArgs A) {
         xv[k][i] = (FULL || el + i < n_el) ? load1<TIN>(A.x, e0 + el + i) : 0.f;
     }
   }
-  // the subnormal-quotient check only where quot_check_for() asks for it (one uniform branch
-  // per workgroup; the x loads above are already in flight)
-  const uint32_t cnt = A.stats->quot_check
-      ? code_records<RM, TIN, FULL, true>(A, c, xv, e0, n_el, wm, wo)
-      : code_records<RM, TIN, FULL, false>(A, c, xv, e0, n_el, wm, wo);
-  const uint32_t tot = wave_total_u32(cnt);
-  if (lane == 0) s_cnt[w] = tot;
-  __syncthreads();
-  if (tid == 0) {
-    const uint32_t t = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
-    A.meta[b] = t;
-    atomicAdd(A.gsum + b / kGroup,
-              block_image_words(wm, wo, (uint32_t)n_el, t & 0xffffu) + 2u * (t >> 16));
+  // the plane and the outlier-bit stream are built by ORs: clear them while the loads are in flight
+  for (uint32_t i = tid; i < 128u * (uint32_t)(wm + we); i += kBlock) plane[i] = 0u;
+  lds_barrier();
+
+  uint32_t nibs = 0u;      // per slot k: outlier nibble (bits 4k..4k+3)
+  uint32_t pre[4];         // wave-exclusive outliers | escapes << 16 before this lane, per slot
+  uint64_t ech[4];         // this lane's outlier bits above the plane, in element order (we <= 16;
+                           // we == 2: its 8-lane group's run, in the group's last lane)
+  uint32_t gfirst[4];      // we == 2: wave-local rank of the group's first outlier
+  uint32_t ev[4][4];       // the same per element (we > 16 only)
+  const uint32_t pmask = (wm >= 32) ? 0xffffffffu : ((1u << wm) - 1u);
+  const uint32_t hm = 1u << (wm - 1), side = 1u << (wo - 1), lim_m = 2u * hm;
+  // per-thread constants of the slot loop: the mask word this lane's group writes, and where its
+  // 4 * wm plane bits start (the same bit offset in every slot: 1024 * wm is a multiple of 32)
+  const uint32_t msh = 4u * (uint32_t)(lane & 7);
+  const bool mwriter = (lane & 7) == 7;
+  const uint32_t ppos0 = 4u * (uint32_t)wm * (uint32_t)tid;
+  const uint32_t pw0 = ppos0 >> 5, psft = ppos0 & 31u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int el = 1024 * k + 4 * tid;
+    const bool full4 = FULL || el + 3 < n_el;
+    float u[4] = {0.f, 0.f, 0.f, 0.f};
+    if (RM == kRoundHash) {
+      const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
+      if (full4) {
+        rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (el + i < n_el) u[i] = rng_hu(A.key, ctr + i);
+      }
+    }
+    uint32_t code[4], on = 0u, en = 0u;
+    float qv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool o, lo, esc;
+      qv[i] = pack_quant<RM, TIN, SUB>(xv[k][i], u[i], c, o, lo);
+      code[i] = code_sel(qv[i], o, lo, hm, side, lim_m, esc);
+      const bool valid = FULL || el + i < n_el;
+      if (!FULL) code[i] = valid ? code[i] : 0u;
+      on |= ((FULL || valid) && o) ? (1u << i) : 0u;
+      en |= ((FULL || valid) && esc) ? (1u << i) : 0u;
+    }
+    nibs |= on << (4 * k);
+    // mask word of 32 elements = the nibbles of 8 consecutive lanes
+    const uint32_t mw = group8_or_to_last(on << msh);
+    if (mwriter) mask[32 * k + (tid >> 3)] = mw;
+    // plane: the low wm bits of the 4 codes at bit wm * el
+    if (4 * wm <= 32) {
+      uint32_t ch = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ch |= (code[i] & pmask) << (wm * i);
+      uint32_t* pw = plane + pw0 + 32u * (uint32_t)wm * (uint32_t)k;
+      atomicOr(pw, ch << psft);
+      if (psft + 4u * (uint32_t)wm > 32u) atomicOr(pw + 1, ch >> (32u - psft));
+    } else if (wm <= 16) {
+      uint64_t ch = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ch |= (uint64_t)(code[i] & pmask) << (wm * i);
+      if (ch) or_bits64(plane, (uint32_t)wm * (uint32_t)el, ch);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {
+        const uint64_t ch = (uint64_t)(code[i] & pmask) | ((uint64_t)(code[i + 1] & pmask) << wm);
+        if (ch) or_bits64(plane, (uint32_t)wm * (uint32_t)(el + i), ch);
+      }
+    }
+    // outlier bits above the plane, in element order
+    ech[k] = 0u;
+    if (we > 0) {
+      if (4 * we <= 32) {
+        // code >> wm is 0 for a main element (its code has wm bits), so only the shifts depend on
+        // which slots are outliers: slot i's bits start at we * (outliers among slots < i)
+        const uint32_t s1 = (uint32_t)we * (on & 1u);
+        const uint32_t s2 = (uint32_t)we * (uint32_t)__popc(on & 3u);
+        const uint32_t s3 = (uint32_t)we * (uint32_t)__popc(on & 7u);
+        ech[k] = (code[0] >> wm) | ((code[1] >> wm) << s1) | ((code[2] >> wm) << s2) |
+                 ((code[3] >> wm) << s3);
+      } else if (we <= 16) {
+        uint32_t sft = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if ((on >> i) & 1u) {
+            ech[k] |= (uint64_t)(code[i] >> wm) << sft;
+            sft += (uint32_t)we;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ev[k][i] = code[i] >> wm;
+      }
+    }
+    const uint32_t cnt = (uint32_t)__popc(on) | ((uint32_t)__popc(en) << 16);
+    const uint32_t incl = wave_incl_scan_u32(cnt);
+    pre[k] = incl - cnt;
+    if (lane == kWave - 1) seg[4 * k + w] = incl;
+    if (kWE == 2) {
+      // 2-bit outlier codes: the 8 lanes of a group own consecutive ranks, so their bits form one
+      // run of <= 64 bits: assemble it in the group's last lane (DPP ORs), which alone ORs it into
+      // the stream after the barrier — one lane per 8 instead of every lane ORing a few bits into
+      // words its neighbours hit too (the LDS atomics serialised: 60 us of 425 at 256M)
+      const uint32_t po = pre[k] & 0xffffu;
+      const uint32_t first = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (lane & ~7), (int)po);
+      const uint64_t ch = (uint64_t)(uint32_t)ech[k] << (2u * (po - first));
+      const uint32_t glo = group8_or_to_last((uint32_t)ch), ghi = group8_or_to_last((uint32_t)(ch >> 32));
+      ech[k] = ((uint64_t)ghi << 32) | glo;
+      gfirst[k] = first;
+    }
+    // escapes (rare) go to the segment's list at their wave-local rank
+    if (__builtin_expect(en != 0u, 0)) {
+      uint32_t r = pre[k] >> 16;
+      uint32_t* L = elist + 2 * kSegEsc * (4 * k + w);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if ((en >> i) & 1u) {
+          if (r < (uint32_t)kSegEsc) {
+            const float qe = qv[i];
+            L[2 * r] = (uint32_t)(el + i);
+            L[2 * r + 1] = qe == qe ? __float_as_uint(qe) : 0x7fc00000u;  // one NaN pattern
+          }
+          ++r;
+        }
+      }
+    }
   }
+  lds_barrier();
+  // segment 4 k + w covers elements 1024 k + 256 w .. + 255: its base = the counts of the segments
+  // before it (lanes 0-15 scan the 16 counts by DPP row shifts; every wave does it itself)
+  const uint32_t own = lane < kSegs ? seg[lane] : 0u;
+  uint32_t sincl = own;
+  sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x111, 0xf, 0xf, false);
+  sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x112, 0xf, 0xf, false);
+  sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x114, 0xf, 0xf, false);
+  sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x118, 0xf, 0xf, false);
+  const uint32_t sexcl = sincl - own;
+  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)sincl, kSegs - 1);
+  const bool seg_over = __ballot(lane < kSegs && (own >> 16) > (uint32_t)kSegEsc) != 0ull;
+  const uint32_t n_out = tot & 0xffffu, n_esc = tot >> 16;
+  const uint32_t n_ext = ext_words(we, n_out);
+  const uint32_t var_words = n_ext + 2u * n_esc;
+  const bool fits = !seg_over && var_words <= (uint32_t)kVarCap;
+  uint32_t* dst = A.scratch + (size_t)b * kVarCap;
+  if (we > 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t on = (nibs >> (4 * k)) & 15u;
+      if (kWE != 2 && !on) continue;
+      const uint32_t sbase = (uint32_t)__builtin_amdgcn_readlane((int)sexcl, 4 * k + w);
+      if (kWE == 2) {
+        if ((lane & 7) == 7 && ech[k]) or_bits64(ext, 2u * ((sbase & 0xffffu) + gfirst[k]), ech[k]);
+        continue;
+      }
+      const uint32_t r_out = (sbase + pre[k]) & 0xffffu;
+      if (4 * we <= 32) {
+        or_bits32(ext, (uint32_t)we * r_out, (uint32_t)ech[k]);
+      } else if (we <= 16) {
+        or_bits64(ext, (uint32_t)we * r_out, ech[k]);
+      } else {
+        uint32_t r = r_out;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if ((on >> i) & 1u) or_bits64(ext, (uint32_t)we * r++, ev[k][i]);
+      }
+    }
+  }
+  // escapes: thread t copies entries t % 16 and t % 16 + 16 of segment t / 16 to their rank
+  if (fits && n_esc) {
+    const int s = tid >> 4;
+    const uint32_t sb = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * s, (int)sexcl) >> 16;
+    const uint32_t sc = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * s, (int)own) >> 16;
+    const uint32_t* L = elist + 2 * kSegEsc * s;
+#pragma unroll
+    for (int jj = 0; jj < kSegEsc; jj += 16) {
+      const uint32_t j = (uint32_t)(tid & 15) + (uint32_t)jj;
+      if (j < sc) {
+        dst[n_ext + 2u * (sb + j)] = L[2 * j];
+        dst[n_ext + 2u * (sb + j) + 1u] = L[2 * j + 1];
+      }
+    }
+  }
+  lds_barrier();
+  // the fixed section (mask + plane, F words, a multiple of 4) at b * F, 16-B stores
+  uint4* fdst = reinterpret_cast<uint4*>(A.fixed + (size_t)b * F);
+  const uint4* fsrc = reinterpret_cast<const uint4*>(lds);
+  for (uint32_t i = tid; i < F / 4u; i += kBlock) fdst[i] = fsrc[i];
+  if (tid == 0) {
+    A.meta[b] = n_out | (n_esc << 16) | (fits ? 0u : kMetaRecode);
+    atomicAdd(A.gsum + b / kGroup, var_words);
+  }
+  if (fits)
+    for (uint32_t i = tid; i < n_ext; i += kBlock) dst[i] = ext[i];
+}
+
+// One workgroup per full block, in reverse address order: the statistics sweep just read x front
+// to back, so its tail is still in the Infinity Cache. The short last block has its own launch.
+template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO>
+__global__ __launch_bounds__(kBlock) void smaq_pack_block_kernel(PackArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t b = FULL ? A.n_full - 1 - blockIdx.x : A.n_blocks - 1;
+  // the subnormal-quotient check only where quot_check_for() asks for it (one uniform branch)
+  if (A.stats->quot_check)
+    pack_block_body<RM, TIN, VEC, FULL, true, WM, WO>(A, b, lds);
+  else
+    pack_block_body<RM, TIN, VEC, FULL, false, WM, WO>(A, b, lds);
 }
 
 constexpr int kScanThreads = 1024;
@@ -582,253 +454,212 @@ __global__ __launch_bounds__(kScanThreads) void smaq_pack_scan_kernel(PackArgs A
     h->inv_range_main = A.inv_r_main;
     h->inv_range_outlier = A.inv_r_out;
     h->data_words = carry;
-    h->total_bytes = sizeof(SmqPackedHeader) + 8ull * A.n_blocks + 4ull * carry;
+    h->total_bytes = sizeof(SmqPackedHeader) + 8ull * dir_entries(A.n_blocks) +
+                     4ull * A.n_blocks * fixed_words(A.wm) + 4ull * carry;
     h->error = 0u;
 #pragma unroll
     for (int i = 0; i < 9; ++i) h->reserved[i] = 0u;
+    if (A.n_blocks & 1u) A.dir[A.n_blocks] = 0ull;  // the directory's padding entry
   }
 }
 
-// q of one element re-derived from x (an escape whose q does not fit its record: |q| > 4095, inf,
-// NaN), with pack_body's element code.
+// The variable section of block b re-coded from x straight to the stream at var_dst (a block
+// whose section outgrew its scratch slot: more than ~kVarCap / 2 escapes). A rare path built for a
+// small register footprint, so the common copy path of smaq_pack_var_kernel keeps its occupancy:
+// 16 passes of 256 consecutive elements, one per thread; outlier and escape ranks by wave ballots
+// and the passes' running totals; the outlier bits are ORed into LDS (ext, 128 * we words) and
+// copied out at the end, the escapes are written directly.
 template <int RM, int TIN>
-__device__ __forceinline__ float rederive_q(const PackArgs& A, int64_t e) {
+__device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_dst, uint32_t* ext,
+                                   uint32_t* s_cnt) {
+  const int wm = A.wm, wo = A.wo, we = wo > wm ? wo - wm : 0;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  const int64_t e0 = (int64_t)b * kPB;
+  const int n_el = (int)min((int64_t)kPB, A.n - e0);
   ElemConsts c;
   const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
   init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
-  const float u = (RM == kRoundHash) ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)e) : 0.0f;
-  bool hi, lo;
-  return smaq_quant<RM, false, TIN, true>(load1<TIN>(A.x, e), u, c, hi, lo);
+  const uint32_t hm = 1u << (wm - 1), side = 1u << (wo - 1);
+  for (uint32_t i = tid; i < 128u * (uint32_t)we; i += kBlock) ext[i] = 0u;
+  __syncthreads();
+  // pass 0 counts the block's outliers (its escapes follow the outlier bits: ext_words(we, n_out)
+  // words); pass 1 places the outlier bits and writes the escapes
+  uint32_t n_out = 0u;
+#pragma unroll 1
+  for (int pass = we > 0 ? 0 : 1; pass < 2; ++pass) {
+    uint32_t r_out = 0u, r_esc = 0u;
+    uint32_t* out = A.var + var_dst + ext_words(we, n_out);
+#pragma unroll 1
+    for (int j = 0; j < kPB / kBlock; ++j) {
+      const int el = j * kBlock + tid;
+      bool o = false, lo = false, esc = false;
+      float q = 0.0f;
+      uint32_t code = 0u;
+      if (el < n_el) {
+        const float u = (RM == kRoundHash) ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)(e0 + el)) : 0.0f;
+        q = pack_quant<RM, TIN, true>(load1<TIN>(A.x, e0 + el), u, c, o, lo);
+        code = code_sel(q, o, lo, hm, side, 2u * hm, esc);
+      }
+      const unsigned long long bo = __ballot(o), be = __ballot(esc);
+      const uint32_t ro = __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u));
+      const uint32_t re = __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
+      if (lane == 0) s_cnt[w] = (uint32_t)__popcll(bo) | ((uint32_t)__popcll(be) << 16);
+      __syncthreads();
+      uint32_t before = 0u, tot = 0u;
+#pragma unroll
+      for (int v = 0; v < kBlock / kWave; ++v) {
+        const uint32_t t = s_cnt[v];
+        before += v < w ? t : 0u;
+        tot += t;
+      }
+      __syncthreads();
+      if (pass == 1) {
+        const uint32_t ko = r_out + (before & 0xffffu) + ro, ke = r_esc + (before >> 16) + re;
+        if (o && we > 0) or_bits32(ext, (uint32_t)we * ko, code >> wm);  // we <= 23 bits
+        if (esc) {
+          out[2u * ke] = (uint32_t)el;
+          out[2u * ke + 1u] = q == q ? __float_as_uint(q) : 0x7fc00000u;
+        }
+      }
+      r_out += tot & 0xffffu;
+      r_esc += tot >> 16;
+    }
+    n_out = r_out;
+  }
+  __syncthreads();
+  uint32_t* out = A.var + var_dst;
+  for (uint32_t i = tid; i < ext_words(we, n_out); i += kBlock) out[i] = ext[i];
 }
 
-// OR a code chunk of up to 64 bits at bit pos of an LDS bit stream (two or three words; the third
-// only when bits land there, so it never passes the image; ORing 0 into the second is harmless).
-__device__ __forceinline__ void or_bits64(uint32_t* base, uint32_t pos, uint64_t chunk) {
-  const uint32_t sft = pos & 31u, w0 = pos >> 5;
-  const uint64_t lo = chunk << sft;
-  const uint32_t hi = sft ? (uint32_t)(chunk >> (64u - sft)) : 0u;
-  atomicOr(base + w0, (uint32_t)lo);
-  atomicOr(base + w0 + 1, (uint32_t)(lo >> 32));
-  if (hi) atomicOr(base + w0 + 2, hi);
-}
-
-// OR of each aligned group of 4 lanes, complete in the group's last lane (lane & 3 == 3).
-__device__ __forceinline__ uint32_t group4_or_to_last(uint32_t v) {
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
-  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
-  return v;
-}
-
-// Emitter lane layout: lane t of the workgroup owns elements 2048 k + 8 t + i (k = 0, 1; i < 8), so
-// its 8 records per k are one 16-B load (8-B loads of 4 records ran at ~0.6x the 16-B rate) and one
-// 64-bit code chunk; segment 4 k + w (wave w) covers 512 consecutive elements.
-constexpr int kEmitK = 2;
-constexpr int kEmitE = 8;
-
-template <int RM, int TIN, bool FULL, int WM, int WO>
-__global__ __launch_bounds__(kBlock) void smaq_emit_kernel(PackArgs A) {
-  extern __shared__ uint32_t stage[];  // [stage_words]: w[0], mask, code stream
-  __shared__ uint32_t seg_cnt[kEmitK * kBlock / kWave];
-  __shared__ uint64_t s_prefix;
-  constexpr bool kChunk = WO > 0 && WO <= 8;
-  const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
-  const uint32_t b = FULL ? blockIdx.x : A.n_blocks - 1;
+// One workgroup per group of kGroup blocks: wave 0 turns the blocks' sizes into their offsets
+// (group prefix + DPP scan) and directory entries; each wave then copies the variable sections of
+// every fourth block from its scratch slot to the stream (a lane copies words lane, lane + 64, ...;
+// four blocks' loads in flight before their stores); blocks whose section outgrew the slot are
+// re-coded from x by the whole workgroup (recode_var_section).
+template <int RM, int TIN, int WM, int WO>
+__global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // re-code: 128 * we words
+  __shared__ uint32_t s_off[kGroup + 1];   // group-relative word offsets (s_off[64] = total)
+  __shared__ uint64_t s_base;
+  __shared__ unsigned long long s_over;    // blocks of the group re-coded from x
+  __shared__ uint32_t s_cnt[kBlock / kWave];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-  const int64_t e0 = (int64_t)b * kPB;
-  const int n_el = FULL ? kPB : (int)(A.n - e0);
-  uint32_t* codes_lds = stage + kHdrWords;
-
-  // records of this lane's 16 elements, two per register
-  uint32_t rw[kEmitK][4];
-#pragma unroll
-  for (int k = 0; k < kEmitK; ++k) {
-    const int el = 2048 * k + kEmitE * tid;
-    if (FULL || el + kEmitE <= n_el) {
-      const uint4 t = *reinterpret_cast<const uint4*>(A.rec + e0 + el);
-      rw[k][0] = t.x;
-      rw[k][1] = t.y;
-      rw[k][2] = t.z;
-      rw[k][3] = t.w;
-    } else {
-      uint32_t r[kEmitE];
-#pragma unroll
-      for (int i = 0; i < kEmitE; ++i) r[i] = (el + i < n_el) ? (uint32_t)A.rec[e0 + el + i] : 0u;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) rw[k][j] = r[2 * j] | (r[2 * j + 1] << 16);
+  const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
+  const int we = wo > wm ? wo - wm : 0;
+  const uint32_t g = blockIdx.x;
+  const uint32_t b0 = g * kGroup;
+  const uint32_t nb = min((uint32_t)kGroup, A.n_blocks - b0);
+  if (tid < kWave) {
+    uint32_t sz = 0u, t = 0u;
+    bool rec = false;
+    if ((uint32_t)lane < nb) {
+      const uint32_t m = A.meta[b0 + lane];
+      rec = (m & kMetaRecode) != 0u;
+      t = m & ~kMetaRecode;
+      sz = ext_words(we, t & 0xffffu) + 2u * (t >> 16);
     }
-  }
-  // block prefix: the group's prefix + the sizes of the group's earlier (full) blocks
-  if (w == 0) {
-    const uint32_t g = b / kGroup, j = g * kGroup + lane;
-    uint32_t sz = 0u;
-    if (j < b) {
-      const uint32_t t = A.meta[j];
-      sz = block_image_words(wm, wo, kPB, t & 0xffffu) + 2u * (t >> 16);
-    }
-    sz = wave_total_u32(sz);
-    if (lane == 0) s_prefix = A.gpre[g] + sz;
-  }
-
-  auto rec = [&](int k, int i) -> uint32_t { return (rw[k][i >> 1] >> (16 * (i & 1))) & 0xffffu; };
-  // outlier / escape bits per 8-element group (the codes themselves are decoded when placed)
-  uint32_t om[kEmitK], xm[kEmitK];
-#pragma unroll
-  for (int k = 0; k < kEmitK; ++k) {
-    om[k] = 0u;
-    xm[k] = 0u;
-#pragma unroll
-    for (int i = 0; i < kEmitE; ++i) {
-      const uint32_t r = rec(k, i);
-      om[k] |= (r >> 15) << i;
-      xm[k] |= ((r >> 14) & 1u) << i;
-    }
-  }
-  auto code_of = [&](int k, int i) -> uint32_t {
-    const uint32_t r = rec(k, i);
-    const uint32_t side_code = ((r >> 13) & (r >> 15) & 1u) << (wo - 1);
-    return ((r >> 14) & 1u) ? side_code : (r & 0x3fffu);
-  };
-
-  // ranks, mask words and the LDS code stream: outlier and escape counts packed in one word (each
-  // <= 512 per wave) and scanned together by DPP; a mask word is the OR of 4 lanes' bytes, written
-  // by each group's last lane
-  uint32_t pre_o[kEmitK], pre_x[kEmitK];
-#pragma unroll
-  for (int k = 0; k < kEmitK; ++k) {
-    const uint32_t cnt = (uint32_t)__popc(om[k]) | ((uint32_t)__popc(xm[k]) << 16);
-    const uint32_t incl = wave_incl_scan_u32(cnt);
-    const uint32_t ex = incl - cnt;
-    pre_o[k] = ex & 0xffffu;
-    pre_x[k] = ex >> 16;
-    const uint32_t mw = group4_or_to_last(om[k] << (8 * (lane & 3)));
-    if ((lane & 3) == 3) stage[1 + ((2048 * k + kEmitE * (tid - 3)) >> 5)] = mw;
-    if (lane == kWave - 1) seg_cnt[4 * k + w] = incl;
-  }
-  const uint32_t code_cap = A.stage_words - kHdrWords;
-  for (uint32_t i = tid; i < code_cap; i += kBlock) codes_lds[i] = 0u;
-  __syncthreads();
-  // every wave derives its segment prefixes from the 8 counts itself (no serial scan and no
-  // second barrier): segment 4 k + w starts after segments 0 .. 4 k + w - 1 (lane s < 8 holds
-  // segment s's counts packed as outliers | escapes << 16, each <= 2048)
-  const uint32_t own = lane < kEmitK * 4 ? seg_cnt[lane] : 0u;
-  uint32_t incl = own;  // lanes 0-7 scanned by DPP row shifts
-  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xf, 0xf, false);
-  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xf, 0xf, false);
-  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xf, 0xf, false);
-  const uint32_t excl = incl - own;
-  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kEmitK * 4 - 1);
-  const uint32_t n_out = tot & 0xffffu, n_esc = tot >> 16;
-  uint32_t base_o[kEmitK], base_x[kEmitK];
-#pragma unroll
-  for (int k = 0; k < kEmitK; ++k) {
-    const uint32_t b4 = (uint32_t)__builtin_amdgcn_readlane((int)excl, 4 * k + w);
-    base_o[k] = b4 & 0xffffu;
-    base_x[k] = b4 >> 16;
-  }
-  const uint32_t img_words = block_image_words(wm, wo, (uint32_t)n_el, n_out);
-#pragma unroll
-  for (int k = 0; k < kEmitK; ++k) {
-    const uint32_t el0 = 2048u * k + kEmitE * tid;
-    if (!FULL && (int)el0 >= n_el) continue;
-    const uint32_t r0 = base_o[k] + pre_o[k];
-    const uint32_t pos0 = (uint32_t)wm * el0 + (uint32_t)(wo - wm) * r0;
-    if (kChunk) {
-      uint64_t chunk = 0u;
-      uint32_t off = 0u;
-#pragma unroll
-      for (int i = 0; i < kEmitE; ++i) {
-        chunk |= (uint64_t)code_of(k, i) << off;
-        off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
-      }
-      or_bits64(codes_lds, pos0, chunk);
-    } else {
-      uint32_t off = 0u;
-#pragma unroll
-      for (int i = 0; i < kEmitE; ++i) {
-        or_bits(codes_lds, pos0 + off, code_of(k, i));
-        off += ((om[k] >> i) & 1u) ? (uint32_t)wo : (uint32_t)wm;
-      }
+    const uint32_t incl = wave_incl_scan_u32(sz);
+    const uint32_t ex = incl - sz;
+    const uint64_t base = A.gpre[g];
+    s_off[lane] = ex;
+    if (lane == kWave - 1) s_off[kGroup] = incl;
+    if ((uint32_t)lane < nb)
+      A.dir[b0 + lane] = (base + ex) | ((uint64_t)(t & 0xffffu) << 38) | ((uint64_t)(t >> 16) << 51);
+    const unsigned long long over = __ballot(rec);
+    if (lane == 0) {
+      s_base = base;
+      s_over = over;
     }
   }
   __syncthreads();
-
-  // the block image at its prefix, its escapes and directory entry
-  const uint64_t P = s_prefix;
-  uint32_t* out = A.data + P;
-  for (uint32_t i = tid; i < img_words; i += kBlock)
-    out[i] = i == 0 ? (n_out | (n_esc << 16)) : stage[i];
+  const uint64_t base = s_base;
+  const unsigned long long over = s_over;
+  uint32_t* out = A.var + base;
+  constexpr int kB = 4;  // blocks per step of a wave
+  constexpr int kW = 4;  // words per lane and block per step (256 words: most sections at 6/8 bits)
+  for (uint32_t j0 = (uint32_t)w * kB; j0 < nb; j0 += kB * (kBlock / kWave)) {
+    uint32_t v[kB][kW];
 #pragma unroll
-  for (int k = 0; k < kEmitK; ++k) {
-    if (!xm[k]) continue;
-    const uint32_t bx = base_x[k] + pre_x[k];
+    for (int q = 0; q < kB; ++q) {
+      const uint32_t j = j0 + q;
+      const bool ok = j < nb && !((over >> j) & 1ull);
+      const uint32_t o0 = ok ? s_off[j] : 0u, sz = ok ? s_off[j + 1] - o0 : 0u;
+      const uint32_t* src = A.scratch + (size_t)(b0 + j) * kVarCap;
 #pragma unroll
-    for (int i = 0; i < kEmitE; ++i) {
-      if (!((xm[k] >> i) & 1u)) continue;
-      const uint32_t el = 2048u * k + kEmitE * tid + i;
-      const uint32_t r = bx + __popc(xm[k] & ((1u << i) - 1u));
-      const int qi = (int)((rec(k, i) & 0x1fffu) << 19) >> 19;
-      const float q = qi == kRecBig ? rederive_q<RM, TIN>(A, e0 + el) : (float)qi;
-      out[img_words + 2 * r] = el;
-      out[img_words + 2 * r + 1] = __float_as_uint(q);
+      for (int r = 0; r < kW; ++r) {
+        const uint32_t i = (uint32_t)lane + (uint32_t)r * kWave;
+        if (i < sz) v[q][r] = src[i];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kB; ++q) {
+      const uint32_t j = j0 + q;
+      const bool ok = j < nb && !((over >> j) & 1ull);
+      const uint32_t o0 = ok ? s_off[j] : 0u, sz = ok ? s_off[j + 1] - o0 : 0u;
+      const uint32_t* src = A.scratch + (size_t)(b0 + j) * kVarCap;
+#pragma unroll
+      for (int r = 0; r < kW; ++r) {
+        const uint32_t i = (uint32_t)lane + (uint32_t)r * kWave;
+        if (i < sz) out[o0 + i] = v[q][r];
+      }
+      for (uint32_t i = (uint32_t)lane + kW * kWave; i < sz; i += kWave) out[o0 + i] = src[i];
     }
   }
-  if (tid == 0) A.dir[b] = P | ((uint64_t)n_out << 38) | ((uint64_t)n_esc << 51);
+  // blocks whose variable section outgrew the scratch slot
+  for (unsigned long long m = over; m; m &= m - 1) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(m);
+    __syncthreads();
+    recode_var_section<RM, TIN>(A, b0 + j, base + s_off[j], lds, s_cnt);
+  }
+}
+
+template <int RM, int TIN, int WM, int WO>
+void launch_pack_w(const PackArgs& A, bool vec, hipStream_t st) {
+  const size_t lds = 4 * (size_t)A.lds_words;
+  if (A.n_full > 0) {
+    if (vec)
+      hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, true, true, WM, WO>), dim3(A.n_full),
+                         dim3(kBlock), lds, st, A);
+    else
+      hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, false, true, WM, WO>), dim3(A.n_full),
+                         dim3(kBlock), lds, st, A);
+  }
+  if (A.n_full < A.n_blocks)
+    hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, false, false, WM, WO>), dim3(1),
+                       dim3(kBlock), lds, st, A);
+  hipLaunchKernelGGL(smaq_pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, A);
+  const int we = A.wo > A.wm ? A.wo - A.wm : 0;
+  hipLaunchKernelGGL((smaq_pack_var_kernel<RM, TIN, WM, WO>), dim3(A.n_groups), dim3(kBlock),
+                     4 * 128 * (size_t)(we > 0 ? we : 1), st, A);
 }
 
 template <int RM, int TIN>
-void launch_streaming_pack(const PackArgs& A, bool vec, size_t stage_lds, hipStream_t st) {
-  const bool w57 = A.wm == 5 && A.wo == 7;
-  const dim3 grid(A.n_full), block(kBlock);
-  if (A.n_full > 0) {
-    if (vec) {
-      if (w57) hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, true, true, 5, 7>), grid, block, 0, st, A);
-      else hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, true, true, 0, 0>), grid, block, 0, st, A);
-    } else {
-      if (w57) hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, true, 5, 7>), grid, block, 0, st, A);
-      else hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, true, 0, 0>), grid, block, 0, st, A);
-    }
-  }
-  if (A.n_full < A.n_blocks)
-    hipLaunchKernelGGL((smaq_code_kernel<RM, TIN, false, false, 0, 0>), dim3(1), block, 0, st, A);
-  hipLaunchKernelGGL(smaq_pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, A);
-  if (A.n_full > 0) {
-    if (w57) hipLaunchKernelGGL((smaq_emit_kernel<RM, TIN, true, 5, 7>), grid, block, stage_lds, st, A);
-    else hipLaunchKernelGGL((smaq_emit_kernel<RM, TIN, true, 0, 0>), grid, block, stage_lds, st, A);
-  }
-  if (A.n_full < A.n_blocks)
-    hipLaunchKernelGGL((smaq_emit_kernel<RM, TIN, false, 0, 0>), dim3(1), block, stage_lds, st, A);
+void launch_pack(const PackArgs& A, bool vec, hipStream_t st) {
+  if (A.wm == 5 && A.wo == 7) launch_pack_w<RM, TIN, 5, 7>(A, vec, st);  // the 6/8-bit default
+  else launch_pack_w<RM, TIN, 0, 0>(A, vec, st);
 }
 
-// SMQ_PACK_PLACE=atomic: the stream size is the cursor (written after the packing launch).
-__global__ void smaq_pack_total_kernel(SmqPackedHeader* h, const unsigned long long* cursor,
-                                       uint32_t n_blocks) {
-  if (threadIdx.x == 0) {
-    h->data_words = *cursor;
-    h->total_bytes = sizeof(SmqPackedHeader) + 8ull * n_blocks + 4ull * *cursor;
-  }
-}
-
+// ---- decoder ------------------------------------------------------------------------------------
 struct UnpackArgs {
   const SmqPackedHeader* hdr;
   const uint64_t* dir;
-  const uint32_t* data;
+  const uint32_t* fixed;     // the fixed region (its place depends on n only)
+  const uint32_t* var;       // the variable region: from the caller's widths, or (NULL) from the
+                             // header's (one more dependent load at the start of every workgroup)
   float* y;
   int64_t n;
+  int wm, wo;                // the caller's widths (smq_smaq_decompress_ex), else 0
   int vec;
-  int reverse;  // blocks in reverse order (smq_smaq_decompress)
+  int reverse;  // blocks in reverse order (measurement knob SMQ_UNPACK_REVERSE=1)
 };
 
-// Escapes before element el of a block: the list is sorted by element index (lower bound).
-__device__ __forceinline__ uint32_t escapes_below(const uint32_t* esc, uint32_t n_esc, uint32_t el) {
-  uint32_t lo = 0, hi = n_esc;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (esc[2 * mid] < el) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
+// Decode table of narrow codes (both widths <= 8 bits: the 6/8-bit default): every main code
+// (2^wm) and outlier code (2^wo) de-quantised once per block by smaq_dequant into LDS, so an
+// element costs a table read instead of decode + fp64 reciprocal product + de-normalisation. Same
+// arithmetic, same bits.
+constexpr int kLutMax = 512;
 
-// Decode one code (width wm main / wo outlier) to q and the outlier sides.
+// q and the outlier sides of a full code (plane bits | outlier bits << wm).
 __device__ __forceinline__ float decode_code(uint32_t v, bool is_o, int wm, int wo, bool& hi,
                                              bool& lo) {
   const uint32_t side_bit = 1u << (wo - 1);
@@ -840,144 +671,173 @@ __device__ __forceinline__ float decode_code(uint32_t v, bool is_o, int wm, int 
   return is_o ? (float)(lo ? -mag : mag) : qm;
 }
 
-// pc / epc / esc_mask: kMaskWords LDS words each, declared once by the kernel (a __shared__ array
-// inside this template is one allocation PER INSTANTIATION: 16 bodies took 37 KB of LDS per
-// workgroup, 4 workgroups per CU)
-// Decode table of narrow codes (both widths <= 8 bits: the 6/8-bit default): every main code
-// (2^wm) and outlier code (2^wo) de-quantised once per block by smaq_dequant into LDS, so an
-// element costs a table read instead of decode + fp64 reciprocal product + de-normalisation
-// (the PMC count of the decoder was 37 VALU per element, VALU-bound). Same arithmetic, same bits.
-constexpr int kLutMax = 512;
+// dynamic LDS of the decoder (words): fixed image, variable section (when it fits kVarCap), mask
+// prefix counts, escape bitmask and its prefix counts, decode table
+constexpr uint32_t kUnpackLdsWords = 128u * (kMaxWidth + 1) + kVarCap + 4u + 3u * kMaskWords + kLutMax;
 
 template <bool AP, bool SQ, bool FULL, int WM, int WO>
 __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
-                                            uint64_t dent, int wm_rt, int wo_rt, uint32_t* stage,
-                                            uint32_t* pc, uint32_t* epc, uint32_t* esc_mask,
-                                            float* lut) {
-  constexpr bool kWindow = WO > 0 && WO <= 8;  // a lane's 4 codes fit one 32-bit window
-  constexpr bool kLut = kWindow && WM > 0 && WM <= 8;
+                                            uint64_t dent, int wm_rt, int wo_rt, uint32_t* lds) {
+  constexpr bool kLut = WM > 0 && WM <= 8 && WO > 0 && WO <= 8;
   const int wm = WM > 0 ? WM : wm_rt, wo = WO > 0 ? WO : wo_rt;
+  const int we = wo > wm ? wo - wm : 0;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
-  // dent = the block's directory entry: offset | n_out << 38 | n_esc << 51
-  const uint32_t* blk = A.data + (dent & ((1ull << 38) - 1ull));
+  const uint32_t F = fixed_words(wm);
+  uint32_t* fx = lds;                    // [F]: mask, plane
+  uint32_t* vs = lds + F;                // [kVarCap + 4]: outlier bits, escapes (16-B shifted)
+  uint32_t* pc = vs + kVarCap + 4;       // [128] outliers before each mask word
+  uint32_t* esc_mask = pc + kMaskWords;  // [128]
+  uint32_t* epc = esc_mask + kMaskWords; // [128] escapes before each mask word
+  float* lut = reinterpret_cast<float*>(epc + kMaskWords);
   const uint32_t n_out = (uint32_t)(dent >> 38) & 0x1fffu, n_esc = (uint32_t)(dent >> 51);
-  const uint32_t code_words = ((uint32_t)wm * (uint32_t)n_el + (uint32_t)(wo - wm) * n_out + 31u) / 32u;
-  const uint32_t img_words = kHdrWords + code_words;
-  // the image and (when they fit) the escape list in one coalesced copy: 16-B windows
-  // (dwordx4 loads from the image's 16-B line on, every load of a lane issued before its LDS
-  // stores; the last window is clipped to the block with dword loads, so nothing past the stream
-  // is read); word i of the block lands in stage[sh + i]
-  const bool esc_lds = img_words + 2u * n_esc <= (uint32_t)kStageWords;
-  const uint32_t copy_words = esc_lds ? img_words + 2u * n_esc : img_words;
-  {
-    const uintptr_t a = (uintptr_t)blk;
-    const uint32_t sh = (uint32_t)((a >> 2) & 3u);
-    const uint4* src = reinterpret_cast<const uint4*>(a - 4u * sh);
-    const uint32_t nvec = (sh + copy_words + 3u) >> 2;
-    constexpr int kR = (kStageWords + 3 + 4 * kBlock - 1) / (4 * kBlock);
-    uint4 w[kR];
+  const uint32_t n_ext = ext_words(we, n_out);
+  const uint32_t var_words = n_ext + 2u * n_esc;
+  const uint32_t* vsrc = A.var + (dent & ((1ull << 38) - 1ull));
+  const bool var_lds = var_words <= (uint32_t)kVarCap;
+  // fixed section: F / 4 16-B loads; variable section: 16-B windows from its line on (the last
+  // window clipped with dword loads, so nothing past the stream is read); every load of a lane is
+  // issued before any LDS store
+  const uint4* fsrc = reinterpret_cast<const uint4*>(A.fixed + (size_t)b * F);
+  // (one 16-B load per lane covers F <= 1024 words, i.e. wm <= 7; wider planes copy the rest in a
+  // second loop below)
+  const uint32_t nf4 = F / 4u;
+  uint4 f0 = make_uint4(0u, 0u, 0u, 0u);
+  if ((uint32_t)tid < nf4) f0 = fsrc[tid];
+  const uintptr_t va = (uintptr_t)vsrc;
+  const uint32_t sh = (uint32_t)((va >> 2) & 3u);
+  const uint32_t nvec = var_lds ? (sh + var_words + 3u) >> 2 : 0u;
+  uint4 vv = make_uint4(0u, 0u, 0u, 0u);
+  constexpr int kRV = (kVarCap + 4 + 4 * kBlock - 1) / (4 * kBlock);
+  static_assert(kRV == 1, "one 16-B window per lane covers the variable section");
+  if ((uint32_t)tid < nvec) {
+    const uint4* src = reinterpret_cast<const uint4*>(va - 4u * sh);
+    if (4u * tid + 4u <= sh + var_words) {
+      vv = src[tid];
+    } else {
+      uint32_t q[4];
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
-      const uint32_t v = (uint32_t)tid + (uint32_t)r * kBlock;
-      if (v >= nvec) continue;
-      if (4u * v + 4u <= sh + copy_words) {
-        w[r] = src[v];
-      } else {  // the clipped last window
-        uint32_t q[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int idx = (int)(4u * v) + k - (int)sh;
-          q[k] = (idx >= 0 && idx < (int)copy_words) ? blk[idx] : 0u;
-        }
-        w[r] = make_uint4(q[0], q[1], q[2], q[3]);
+      for (int k = 0; k < 4; ++k) {
+        const int idx = (int)(4u * tid) + k - (int)sh;
+        q[k] = (idx >= 0 && idx < (int)var_words) ? vsrc[idx] : 0u;
       }
+      vv = make_uint4(q[0], q[1], q[2], q[3]);
     }
-    if (kLut) {  // while the image is in flight: the block's decode table
-      for (int i = tid; i < (1 << WM) + (1 << WO); i += kBlock) {
-        bool hi = false, lo = false;
-        float q;
-        if (i < (1 << WM)) {
-          q = (float)(((int32_t)((uint32_t)i << (32 - WM))) >> (32 - WM));  // sign-extend
-        } else {
-          const uint32_t v = (uint32_t)(i - (1 << WM));
-          lo = (v >> (WO - 1)) & 1u;
-          hi = !lo;
-          const int mag = (int)(v & ((1u << (WO - 1)) - 1u));
-          q = (float)(lo ? -mag : mag);
-        }
-        lut[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
+  }
+  if (kLut) {  // while the loads are in flight: the block's decode table
+    for (int i = tid; i < (1 << WM) + (1 << WO); i += kBlock) {
+      bool hi = false, lo = false;
+      float q;
+      if (i < (1 << WM)) {
+        q = (float)(((int32_t)((uint32_t)i << (32 - WM))) >> (32 - WM));  // sign-extend
+      } else {
+        const uint32_t v = (uint32_t)(i - (1 << WM));
+        lo = (v >> (WO - 1)) & 1u;
+        hi = !lo;
+        const int mag = (int)(v & ((1u << (WO - 1)) - 1u));
+        q = (float)(lo ? -mag : mag);
       }
+      lut[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
     }
-#pragma unroll
-    for (int r = 0; r < kR; ++r) {
-      const uint32_t v = (uint32_t)tid + (uint32_t)r * kBlock;
-      if (v < nvec) reinterpret_cast<uint4*>(stage)[v] = w[r];
-    }
-    stage += sh;
   }
   if (tid < kMaskWords) esc_mask[tid] = 0u;
+  if ((uint32_t)tid < nf4) reinterpret_cast<uint4*>(fx)[tid] = f0;
+  for (uint32_t i = tid + kBlock; i < nf4; i += kBlock) reinterpret_cast<uint4*>(fx)[i] = fsrc[i];
+  if ((uint32_t)tid < nvec) reinterpret_cast<uint4*>(vs)[tid] = vv;
   __syncthreads();
-  const uint32_t* esc = esc_lds ? stage + img_words : blk + img_words;
+  const uint32_t* ext = var_lds ? vs + sh : vsrc;
+  const uint32_t* esc = ext + n_ext;
   if (tid < kWave) {  // wave 0: exclusive popcount prefix of the 128 outlier-mask words
-    const uint32_t a = __popc(stage[1 + 2 * lane]), bb = __popc(stage[2 + 2 * lane]);
+    const uint32_t a = __popc(fx[2 * lane]), bb = __popc(fx[2 * lane + 1]);
     const uint32_t ex = wave_incl_scan_u32(a + bb) - (a + bb);
     pc[2 * lane] = ex;
     pc[2 * lane + 1] = ex + a;
-  } else if (tid < kWave + kMaskWords) {  // waves 1-2: escapes before each mask word
-    const uint32_t wi = (uint32_t)tid - kWave;
-    epc[wi] = n_esc ? escapes_below(esc, n_esc, 32u * wi) : 0u;
+  } else if (tid < kWave + kMaskWords) {  // waves 1-2: escapes before each mask word (lower
+    const uint32_t wi = (uint32_t)tid - kWave;  // bound in the list, which is in element order)
+    uint32_t lo = 0u, hi = n_esc;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (esc[2 * mid] < 32u * wi) lo = mid + 1u; else hi = mid;
+    }
+    epc[wi] = lo;
   }
   for (uint32_t i = tid; i < n_esc; i += kBlock) {
     const uint32_t el = esc[2 * i];
     atomicOr(esc_mask + (el >> 5), 1u << (el & 31));
   }
   __syncthreads();
-  const uint32_t* bits = stage + kHdrWords;
+  const uint32_t* plane = fx + kMaskWords;
+  const uint32_t pm = (1u << wm) - 1u;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int el0 = 1024 * k + 4 * tid;
     if (!FULL && el0 >= n_el) break;
-    const uint32_t mw = stage[1 + (el0 >> 5)], em = esc_mask[el0 >> 5];
-    const uint32_t ebase = epc[el0 >> 5];
-    const uint32_t sh0 = (uint32_t)el0 & 31u;
-    const uint32_t r0 = pc[el0 >> 5] + __popc(mw & ((1u << sh0) - 1u));
+    const uint32_t wi = (uint32_t)el0 >> 5, sh0 = (uint32_t)el0 & 31u;
+    const uint32_t mw = fx[wi], em = esc_mask[wi];
     const uint32_t nib = (mw >> sh0) & 15u, enib = (em >> sh0) & 15u;
-    const uint32_t pos0 = (uint32_t)wm * (uint32_t)el0 + (uint32_t)(wo - wm) * r0;
-    uint32_t window = 0u;
-    if (kWindow)
-      window = __builtin_amdgcn_alignbit(bits[(pos0 >> 5) + 1], bits[pos0 >> 5], pos0 & 31u);
+    // plane codes: the lane's 4 * wm bits from bit wm * el0
+    uint32_t cd[4];
+    const uint32_t p0 = (uint32_t)wm * (uint32_t)el0;
+    if (4 * wm <= 32) {
+      const uint32_t win = __builtin_amdgcn_alignbit(plane[(p0 >> 5) + 1], plane[p0 >> 5], p0 & 31u);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cd[i] = (win >> (wm * i)) & pm;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t p = p0 + (uint32_t)(wm * i);
+        cd[i] = __builtin_amdgcn_alignbit(plane[(p >> 5) + 1], plane[p >> 5], p & 31u) & pm;
+      }
+    }
+    // outlier bits above the plane: we bits per outlier from bit we * rank
+    if (we > 0 && nib) {
+      uint32_t r = pc[wi] + __popc(mw & ((1u << sh0) - 1u));
+      const uint32_t emk = (we >= 32) ? 0xffffffffu : ((1u << we) - 1u);
+      // (the word after the last holds no bits of it; not read past the section when it lives
+      // in memory)
+      auto ext_hi = [&](uint32_t wd) -> uint32_t { return wd < n_ext ? ext[wd] : 0u; };
+      if (4 * we <= 32) {
+        const uint32_t p = (uint32_t)we * r;
+        const uint32_t win = __builtin_amdgcn_alignbit(ext_hi((p >> 5) + 1), ext[p >> 5], p & 31u);
+        uint32_t s = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if ((nib >> i) & 1u) {
+            cd[i] |= ((win >> s) & emk) << wm;
+            s += (uint32_t)we;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if ((nib >> i) & 1u) {
+            const uint32_t p = (uint32_t)we * r++;
+            cd[i] |= (__builtin_amdgcn_alignbit(ext_hi((p >> 5) + 1), ext[p >> 5], p & 31u) & emk) << wm;
+          }
+        }
+      }
+    }
     float o[4];
-    uint32_t off = 0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool is_o = (nib >> i) & 1u;
-      uint32_t v;
-      if (kWindow) {
-        v = window >> off;
-      } else {
-        const uint32_t pos = pos0 + off;
-        v = __builtin_amdgcn_alignbit(bits[(pos >> 5) + 1], bits[pos >> 5], pos & 31u);
-      }
-      off += is_o ? (uint32_t)wo : (uint32_t)wm;
-      if (kLut) {
-        o[i] = lut[is_o ? (1u << WM) + (v & ((1u << WO) - 1u)) : (v & ((1u << WM) - 1u))];
-        if (__builtin_expect((enib >> i) & 1u, 0)) {  // an escape: its q from the list
-          bool hi, lo;
-          decode_code(v, is_o, wm, wo, hi, lo);
-          const uint32_t sh = (uint32_t)(el0 + i) & 31u;
-          const float q = __uint_as_float(esc[2u * (ebase + __popc(em & ((1u << sh) - 1u))) + 1u]);
-          o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
-        }
-        continue;
-      }
       bool hi, lo;
-      float q = decode_code(v, is_o, wm, wo, hi, lo);
-      if (__builtin_expect((enib >> i) & 1u, 0)) {  // rank among the block's escapes: O(1)
-        const uint32_t sh = (uint32_t)(el0 + i) & 31u;
-        q = __uint_as_float(esc[2u * (ebase + __popc(em & ((1u << sh) - 1u))) + 1u]);
+      float q;
+      if (kLut) {
+        o[i] = lut[is_o ? (1u << WM) + cd[i] : cd[i]];
+        if (__builtin_expect(!((enib >> i) & 1u), 1)) continue;
+        decode_code(cd[i], is_o, wm, wo, hi, lo);
+      } else {
+        q = decode_code(cd[i], is_o, wm, wo, hi, lo);
+        if (__builtin_expect(!((enib >> i) & 1u), 1)) {
+          o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
+          continue;
+        }
       }
+      // an escape: its q from the list, rank in O(1)
+      const uint32_t s = sh0 + (uint32_t)i;
+      q = __uint_as_float(esc[2u * (epc[wi] + __popc(em & ((1u << s) - 1u))) + 1u]);
       o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
     }
     float* y = A.y + e0 + el0;
@@ -992,17 +852,23 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
 }
 
 __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
-  __shared__ __attribute__((aligned(16))) uint32_t stage[kStageWords + 4];  // + the 16-B shift
-  __shared__ uint32_t pc[kMaskWords], epc[kMaskWords], esc_mask[kMaskWords];
-  __shared__ float lut[kLutMax];
-  // the directory entry is requested together with the header (not behind its checks): the
-  // header -> directory -> image chain becomes two round trips
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kUnpackLdsWords];
   const uint32_t b = A.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
   const uint64_t dent = A.dir[b];
   const SmqPackedHeader* h = A.hdr;
-  if (h->magic != SMQ_PACK_MAGIC || h->version != SMQ_PACK_VERSION || h->n != A.n) return;
-  const int wm = h->num_bits_main - 1, wo = h->num_bits_outlier - 1;
-  if (wm < 1 || wm > kMaxWidth || wo < 2 || wo > kMaxWidth) return;
+  int wm, wo;
+  if (A.var) {  // widths from the caller: the fixed and variable sections' addresses do not wait
+    wm = A.wm;  // for the header; a stream of other widths (or n, magic) is left alone
+    wo = A.wo;
+  } else {
+    wm = h->num_bits_main - 1;
+    wo = h->num_bits_outlier - 1;
+    if (wm < 1 || wm > kMaxWidth || wo < 2 || wo > kMaxWidth) return;
+    A.var = A.fixed + (size_t)gridDim.x * fixed_words(wm);
+  }
+  if (h->magic != SMQ_PACK_MAGIC || h->version != SMQ_PACK_VERSION || h->n != A.n ||
+      h->num_bits_main != wm + 1 || h->num_bits_outlier != wo + 1)
+    return;
   ElemConsts c;
   c.mean = h->mean;
   c.sd = h->std_dev;
@@ -1017,15 +883,15 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   const uint32_t f = h->flags;
   const bool full = (int64_t)(b + 1) * kPB <= A.n;
   const bool w57 = wm == 5 && wo == 7;
-#define SMQ_UNPACK_W(APV, SQV, FULLV)                                                 \
-  do {                                                                                \
-    if (w57) unpack_body<APV, SQV, FULLV, 5, 7>(A, c, b, dent, wm, wo, stage, pc, epc, esc_mask, lut); \
-    else unpack_body<APV, SQV, FULLV, 0, 0>(A, c, b, dent, wm, wo, stage, pc, epc, esc_mask, lut);     \
+#define SMQ_UNPACK_W(APV, SQV, FULLV)                                           \
+  do {                                                                          \
+    if (w57) unpack_body<APV, SQV, FULLV, 5, 7>(A, c, b, dent, wm, wo, lds);   \
+    else unpack_body<APV, SQV, FULLV, 0, 0>(A, c, b, dent, wm, wo, lds);       \
   } while (0)
-#define SMQ_UNPACK(APV, SQV)                                  \
-  do {                                                        \
-    if (full) SMQ_UNPACK_W(APV, SQV, true);                   \
-    else SMQ_UNPACK_W(APV, SQV, false);                       \
+#define SMQ_UNPACK(APV, SQV)                \
+  do {                                      \
+    if (full) SMQ_UNPACK_W(APV, SQV, true); \
+    else SMQ_UNPACK_W(APV, SQV, false);     \
   } while (0)
   if (f & 2u) {
     if (f & 1u) SMQ_UNPACK(true, true); else SMQ_UNPACK(false, true);
@@ -1040,17 +906,19 @@ inline bool aligned_to(const void* p, unsigned a) { return ((uintptr_t)p & (a - 
 
 inline int64_t n_blocks_of(int64_t n) { return (n + kPB - 1) / kPB; }
 
-size_t pack_ws_status_offset(int64_t n) {
-  return (smaq_stats_ws_bytes(n) + 63) & ~(size_t)63;
-}
-
-// workspace: statistics | counter (64 B) | look-back status words | cursor (64 B) | streaming
-// packer: records (2 B/elem) | meta [nb] | group sums [ng] | prefixes [ng]
-size_t pack_ws_stream_offset(int64_t n) {
-  const size_t nb = (size_t)n_blocks_of(n < 1 ? 1 : n);
-  const size_t ng = (nb + kGroup - 1) / kGroup;
-  return (pack_ws_status_offset(n) + 64 + 8 * nb + 8 * ng + 64 + 255) & ~(size_t)255;
-}
+// workspace: statistics | meta [nb] | group sums [ng] | group prefixes [ng] | scratch [nb][kVarCap]
+struct PackWs {
+  size_t meta, gsum, gpre, scratch, total;
+  explicit PackWs(int64_t n) {
+    const size_t nb = (size_t)n_blocks_of(n < 1 ? 1 : n);
+    const size_t ng = (nb + kGroup - 1) / kGroup;
+    meta = (smaq_stats_ws_bytes(n) + 255) & ~(size_t)255;
+    gsum = meta + 4 * nb;
+    gpre = (gsum + 4 * ng + 7) & ~(size_t)7;
+    scratch = (gpre + 8 * ng + 255) & ~(size_t)255;
+    total = scratch + 4 * (size_t)kVarCap * nb;
+  }
+};
 
 }  // namespace
 }  // namespace smq
@@ -1061,17 +929,15 @@ extern "C" {
 
 size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier) {
   if (n < 1) return sizeof(SmqPackedHeader);
-  const int wmax = (num_bits_main > num_bits_outlier ? num_bits_main : num_bits_outlier) - 1;
+  const int wm = num_bits_main - 1, wo = num_bits_outlier - 1;
+  const size_t we = wo > wm ? (size_t)(wo - wm) : 0;
   const size_t nb = (size_t)n_blocks_of(n);
-  const size_t per_block = kHdrWords + ((size_t)wmax * kPB + 31) / 32 + 1 + 2 * (size_t)kPB;
-  return sizeof(SmqPackedHeader) + 8 * nb + 4 * nb * per_block;
+  // every element an outlier and escaped
+  const size_t per_block = fixed_words(wm < 1 ? 1 : wm) + 2 + 128 * we + 2 * (size_t)kPB;
+  return sizeof(SmqPackedHeader) + 8 * (size_t)dir_entries((int64_t)nb) + 4 * nb * per_block;
 }
 
-size_t smq_smaq_pack_workspace_bytes(int64_t n) {
-  const size_t nb = (size_t)n_blocks_of(n < 1 ? 1 : n);
-  const size_t ng = (nb + kGroup - 1) / kGroup;
-  return pack_ws_stream_offset(n) + 2 * nb * kPB + 4 * nb + 4 * (ng + 1) + 8 * ng;
-}
+size_t smq_smaq_pack_workspace_bytes(int64_t n) { return PackWs(n).total; }
 
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* packed,
                       size_t packed_bytes, void* ws, size_t ws_bytes, void* stream) {
@@ -1081,6 +947,7 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
 int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParams* p,
                          void* packed, size_t packed_bytes, void* ws, size_t ws_bytes,
                          uint32_t flags, void* stream) {
+  (void)flags;  // SMQ_PACK_TICKETED / SMQ_PACK_SINGLE: accepted, one packer (see smq.h)
   int rc = smaq_validate(p, dtype);
   if (rc) return rc;
   if (n < 1 || !x || !packed) {
@@ -1107,7 +974,7 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
     return SMQ_ERR_INVALID;
   }
   const int64_t nb = n_blocks_of(n);
-  if (nb > 0xffffffffLL) {
+  if (nb > 0x7fffffffLL) {
     set_error("compress: tensor too large (%lld elements)", (long long)n);
     return SMQ_ERR_INVALID;
   }
@@ -1117,41 +984,34 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
               bound, packed_bytes);
     return SMQ_ERR_WORKSPACE;
   }
-  if (!ws || ws_bytes < smq_smaq_pack_workspace_bytes(n)) {
-    set_error("compress: workspace too small: need %zu bytes, got %zu",
-              smq_smaq_pack_workspace_bytes(n), ws_bytes);
+  const PackWs L(n);
+  if (!ws || ws_bytes < L.total) {
+    set_error("compress: workspace too small: need %zu bytes, got %zu", L.total, ws_bytes);
     return SMQ_ERR_WORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
   rc = prepare_stats(x, dtype, n, p, ws, ws_bytes, st);
   if (rc) return rc;
   char* wb = (char*)ws;
-  const size_t so = pack_ws_status_offset(n);
   PackArgs A;
   memset(&A, 0, sizeof(A));
   A.x = x;
   A.n = n;
+  A.bm = p->num_bits_main;
+  A.bo = p->num_bits_outlier;
+  A.wm = A.bm - 1;
+  A.wo = A.bo - 1;
+  const int we = A.wo > A.wm ? A.wo - A.wm : 0;
   A.hdr = (SmqPackedHeader*)packed;
   A.dir = (uint64_t*)((char*)packed + sizeof(SmqPackedHeader));
-  A.data = (uint32_t*)((char*)packed + sizeof(SmqPackedHeader) + 8 * (size_t)nb);
+  A.fixed = (uint32_t*)(A.dir + dir_entries(nb));
+  A.var = A.fixed + (size_t)nb * fixed_words(A.wm);
   A.stats = (const SmqSmaqStats*)ws;
-  A.counter = (uint32_t*)(wb + so);
-  A.status = (uint64_t*)(wb + so + 64);
-  A.gstatus = A.status + nb;
-  const size_t ng = ((size_t)nb + kGroup - 1) / kGroup;
-  A.cursor = (unsigned long long*)(A.gstatus + ng);
-  A.n_groups = (uint32_t)ng;
-  A.rec = (uint16_t*)(wb + pack_ws_stream_offset(n));
-  A.meta = (uint32_t*)(A.rec + (size_t)nb * kPB);
-  A.gsum = A.meta + nb;
-  A.gpre = (uint64_t*)(((uintptr_t)(A.gsum + ng) + 7) & ~(uintptr_t)7);
-  // measurement knob: place blocks by one atomicAdd (valid, decodable stream; block ORDER then
-  // depends on timing, so the bytes are not reproducible) instead of the ordered look-back
-  static const int place_env = [] {
-    const char* e = getenv("SMQ_PACK_PLACE");
-    return (e && !strcmp(e, "atomic")) ? 1 : 0;
-  }();
-  A.place_atomic = place_env;
+  A.meta = (uint32_t*)(wb + L.meta);
+  A.gsum = (uint32_t*)(wb + L.gsum);
+  A.gpre = (uint64_t*)(wb + L.gpre);
+  A.scratch = (uint32_t*)(wb + L.scratch);
+  A.n_groups = (uint32_t)(((size_t)nb + kGroup - 1) / kGroup);
   A.thr = p->main_std_dev_threshold;
   A.r_main = p->range_main;
   A.r_out = p->range_outlier;
@@ -1160,93 +1020,79 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.inv_r_out = R.inv_out;
   A.key = rng_key(p->seed);
   A.offset = p->offset;
-  A.bm = p->num_bits_main;
-  A.bo = p->num_bits_outlier;
-  A.wm = A.bm - 1;
-  A.wo = A.bo - 1;
   A.n_blocks = (uint32_t)nb;
   A.n_full = (uint32_t)(n / kPB);
-  A.ticketed = (flags & SMQ_PACK_TICKETED) ? 1 : 0;
   A.flags = (p->all_positive ? 1u : 0u) | (R.safe_q ? 2u : 0u);
-  // stage: w[0] + mask + the code stream at its widest (every element an outlier) + 1 word of
-  // slack for the two-word ORs, rounded to 4 words so the q values after it are 16-B aligned
-  A.stage_words = (uint32_t)(kHdrWords + (A.wo * kPB + 31) / 32 + 1 + 3) & ~3u;
-  const size_t lds_bytes = 4 * ((size_t)A.stage_words + kPB);
+  A.lds_words = PackLds::words(A.wm, we);
   const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
   const bool sr = p->stochastic_rounding != 0;
-  const bool streaming = !(flags & (SMQ_PACK_TICKETED | SMQ_PACK_SINGLE)) && !A.place_atomic &&
-                         A.wm <= kRecCodeBits && A.wo <= kRecCodeBits;
-  if (streaming) {
-    // the group sums start at zero: their place in the workspace moves with n, so a previous call
-    // with another n may have left records there
-    if (hipMemsetAsync(A.gsum, 0, 4 * (size_t)A.n_groups, st) != hipSuccess) {
-      set_error("compress: hipMemsetAsync failed");
-      return SMQ_ERR_LAUNCH;
-    }
-    const size_t stage_lds = 4 * (size_t)A.stage_words;
-    if (dtype == SMQ_DTYPE_F32) {
-      if (sr) launch_streaming_pack<kRoundHash, kF32>(A, vec, stage_lds, st);
-      else launch_streaming_pack<kRoundTrunc, kF32>(A, vec, stage_lds, st);
-    } else if (dtype == SMQ_DTYPE_F16) {
-      if (sr) launch_streaming_pack<kRoundHash, kF16>(A, vec, stage_lds, st);
-      else launch_streaming_pack<kRoundTrunc, kF16>(A, vec, stage_lds, st);
-    } else {
-      if (sr) launch_streaming_pack<kRoundHash, kBF16>(A, vec, stage_lds, st);
-      else launch_streaming_pack<kRoundTrunc, kBF16>(A, vec, stage_lds, st);
-    }
-    return check_launch("smaq_code_kernel / smaq_emit_kernel");
-  }
-  if (hipMemsetAsync(A.status, 0, 8 * ((size_t)nb + ng) + 64, st) != hipSuccess ||
-      hipMemsetAsync(A.hdr, 0, sizeof(SmqPackedHeader), st) != hipSuccess) {
+  // the group sums start at zero
+  if (hipMemsetAsync(A.gsum, 0, 4 * (size_t)A.n_groups, st) != hipSuccess) {
     set_error("compress: hipMemsetAsync failed");
     return SMQ_ERR_LAUNCH;
   }
   if (dtype == SMQ_DTYPE_F32) {
-    if (sr) launch_pack<kRoundHash, kF32>(A, vec, lds_bytes, st);
-    else launch_pack<kRoundTrunc, kF32>(A, vec, lds_bytes, st);
+    if (sr) launch_pack<kRoundHash, kF32>(A, vec, st);
+    else launch_pack<kRoundTrunc, kF32>(A, vec, st);
   } else if (dtype == SMQ_DTYPE_F16) {
-    if (sr) launch_pack<kRoundHash, kF16>(A, vec, lds_bytes, st);
-    else launch_pack<kRoundTrunc, kF16>(A, vec, lds_bytes, st);
+    if (sr) launch_pack<kRoundHash, kF16>(A, vec, st);
+    else launch_pack<kRoundTrunc, kF16>(A, vec, st);
   } else {
-    if (sr) launch_pack<kRoundHash, kBF16>(A, vec, lds_bytes, st);
-    else launch_pack<kRoundTrunc, kBF16>(A, vec, lds_bytes, st);
+    if (sr) launch_pack<kRoundHash, kBF16>(A, vec, st);
+    else launch_pack<kRoundTrunc, kBF16>(A, vec, st);
   }
-  if (A.place_atomic)
-    hipLaunchKernelGGL(smaq_pack_total_kernel, dim3(1), dim3(kWave), 0, st, A.hdr, A.cursor,
-                       A.n_blocks);
-  return check_launch("smaq_pack_kernel");
+  return check_launch("smaq_pack_block_kernel / smaq_pack_var_kernel");
 }
 
-int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream) {
+static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int bo, void* stream) {
   if (n < 1 || !packed || !y) {
     set_error("decompress: n must be >= 1, packed and y non-NULL");
     return SMQ_ERR_INVALID;
   }
   const int64_t nb = n_blocks_of(n);
-  if (nb > 0xffffffffLL) {
+  if (nb > 0x7fffffffLL) {
     set_error("decompress: tensor too large (%lld elements)", (long long)n);
     return SMQ_ERR_INVALID;
   }
+  if (bm && (bm < 2 || bm > kMaxWidth + 1 || bo < 3 || bo > kMaxWidth + 1)) {
+    set_error("decompress: needs 2 <= num_bits_main <= %d and 3 <= num_bits_outlier <= %d",
+              kMaxWidth + 1, kMaxWidth + 1);
+    return SMQ_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
   UnpackArgs A;
   A.hdr = (const SmqPackedHeader*)packed;
   A.dir = (const uint64_t*)((const char*)packed + sizeof(SmqPackedHeader));
-  A.data = (const uint32_t*)((const char*)packed + sizeof(SmqPackedHeader) + 8 * (size_t)nb);
+  A.fixed = (const uint32_t*)(A.dir + dir_entries(nb));
+  A.wm = bm ? bm - 1 : 0;
+  A.wo = bo ? bo - 1 : 0;
+  A.var = bm ? A.fixed + (size_t)nb * fixed_words(A.wm) : nullptr;
   A.y = y;
   A.n = n;
   A.vec = aligned_to(y, 16) ? 1 : 0;
-  // blocks in reverse order: the emitter writes the stream front to back, so a decompress soon
-  // after the compress finds the stream's tail (~the Infinity Cache's size) still cached; 256M
-  // back to back: 252 -> 234 us (tools/unpack_rev.sh, two interleaved rounds; the compress after
-  // it then sweeps its statistics 16 us slower, so the bench's round trip is unchanged). A stream
-  // that has left the cache decodes alike in either order. Measurement knob SMQ_UNPACK_REVERSE=0.
+  // blocks in index order: the packer writes the fixed sections in reverse block order, so the
+  // head of the stream is the part still in the Infinity Cache right after a compress (256M: 325 ->
+  // 293 us). Measurement knob SMQ_UNPACK_REVERSE=1.
   static const int rev = [] {
     const char* e = getenv("SMQ_UNPACK_REVERSE");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   A.reverse = rev;
-  hipLaunchKernelGGL(smaq_unpack_kernel, dim3((unsigned)nb), dim3(kBlock), 0,
-                     (hipStream_t)stream, A);
+  hipLaunchKernelGGL(smaq_unpack_kernel, dim3((unsigned)nb), dim3(kBlock), 0, st, A);
   return check_launch("smaq_unpack_kernel");
+}
+
+int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream) {
+  return decompress_impl(packed, y, n, 0, 0, stream);
+}
+
+int smq_smaq_decompress_ex(const void* packed, float* y, int64_t n, int num_bits_main,
+                           int num_bits_outlier, void* stream) {
+  if (num_bits_main == 0) {
+    set_error("decompress_ex: num_bits_main / num_bits_outlier required");
+    return SMQ_ERR_INVALID;
+  }
+  return decompress_impl(packed, y, n, num_bits_main, num_bits_outlier, stream);
 }
 
 }  // extern "C"

@@ -216,6 +216,7 @@ SIGNATURES = {
     "smq_smaq_compress_ex": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams),
                                      _P, _SZ, _P, _SZ, _U32, _P]),
     "smq_smaq_decompress": (_I32, [_P, _P, _I64, _P]),
+    "smq_smaq_decompress_ex": (_I32, [_P, _P, _I64, _I32, _I32, _P]),
     "smq_cpu_threads": (_I32, []),
     "smq_cpu_smaq_roundtrip": (
         _I32,

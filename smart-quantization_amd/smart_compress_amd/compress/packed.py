@@ -6,11 +6,12 @@ memory saving (README.md:25-28: ``[outlier flag][sign][N-2 magnitude bits]``, 6 
 element and 8 per outlier by default) needs the codes to be kept. ``SmartFPPacked`` keeps them in
 the container of include/smq.h ("Packed SmaQ container"):
 
-* ``compress(x)`` -> ``SmaqPacked``: device bytes (header, block directory, bit-packed planes,
-  escape list for codes outside the budget), built by ``smq_smaq_compress`` (statistics + one
-  packing launch);
+* ``compress(x)`` -> ``SmaqPacked``: device bytes (header, block directory, per block a fixed
+  section — outlier mask and a plane of num_bits_main - 1 bits per element — and a variable
+  section — the outliers' remaining code bits and the escape list for codes outside the budget),
+  built by ``smq_smaq_compress`` (statistics + three packing launches);
 * ``decompress(p)`` -> fp32 tensor, bit-identical to what ``SmartFP`` returns for the same input,
-  flags and random stream (``smq_smaq_decompress``, one launch);
+  flags and random stream (``smq_smaq_decompress_ex``, one launch);
 * ``__call__`` = decompress(compress(x)), a drop-in SmaQ codec whose ``new_size`` log is the real
   stream size.
 
@@ -33,18 +34,19 @@ __all__ = ["SmaqPacked", "SmartFPPacked"]
 
 _HDR_BYTES = ctypes.sizeof(N.SmqPackedHeader)
 _TOTAL_OFF = N.SmqPackedHeader.total_bytes.offset
-_ERROR_OFF = N.SmqPackedHeader.error.offset
 
 
 class SmaqPacked:
     """A packed SmaQ tensor: ``data`` (uint8, on the device) plus the original shape.
     ``raw``: a tensor below ``min_size``, kept as its original fp32 bytes (smart.py:123-128)."""
 
-    def __init__(self, data: torch.Tensor, shape: torch.Size, n: int, raw: bool = False):
+    def __init__(self, data: torch.Tensor, shape: torch.Size, n: int, raw: bool = False,
+                 widths=None):
         self.data = data
         self.shape = torch.Size(shape)
         self.n = int(n)
         self.raw = raw
+        self.widths = widths  # (num_bits_main, num_bits_outlier) the stream was written with
 
     @property
     def nbytes(self) -> int:
@@ -91,27 +93,25 @@ class SmartFPPacked(SmartFP):
         bound = lib.smq_smaq_pack_bound(numel, hp.num_bits_main, hp.num_bits_outlier)
         scratch = N.workspace("smaq_pack_out", x.device, bound)
         ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(numel))
-        # index-ordered packing; if the block scan ever gives up (it assumes each XCD starts its
-        # workgroups in index order), re-pack with ticketed block ids (same bytes, no assumption)
-        for flags in (0, N.SMQ_PACK_TICKETED):
-            N.check(lib.smq_smaq_compress_ex(x.data_ptr(), code, numel, p, scratch.data_ptr(),
-                                             scratch.numel(), ws.data_ptr(), ws.numel(), flags,
-                                             N.stream_ptr(x.device)), "smq_smaq_compress_ex")
-            tail = scratch[_TOTAL_OFF:_ERROR_OFF + 4].cpu().numpy()  # host sync: the stream size
-            if int(tail[_ERROR_OFF - _TOTAL_OFF:].view(np.uint32)[0]) == 0:
-                break
-        else:
-            raise RuntimeError("smq_smaq_compress: block scan gave up (stream marked broken)")
-        total = int(tail[:8].view(np.uint64)[0])
-        return SmaqPacked(scratch[:total].clone(), data.shape, numel)
+        N.check(lib.smq_smaq_compress(x.data_ptr(), code, numel, p, scratch.data_ptr(),
+                                      scratch.numel(), ws.data_ptr(), ws.numel(),
+                                      N.stream_ptr(x.device)), "smq_smaq_compress")
+        # host sync: the stream size, for a right-sized buffer
+        total = int(scratch[_TOTAL_OFF:_TOTAL_OFF + 8].cpu().numpy().view(np.uint64)[0])
+        return SmaqPacked(scratch[:total].clone(), data.shape, numel,
+                          widths=(hp.num_bits_main, hp.num_bits_outlier))
 
     def decompress(self, packed: SmaqPacked) -> torch.Tensor:
         if packed.raw:
             return packed.data.view(torch.float32).reshape(packed.shape).clone()
         N.require_device(packed.data, "SmartFPPacked.decompress")
         y = torch.empty(packed.shape, dtype=torch.float32, device=packed.data.device)
-        N.check(N.lib().smq_smaq_decompress(packed.data.data_ptr(), y.data_ptr(), packed.n,
-                                            N.stream_ptr(y.device)), "smq_smaq_decompress")
+        # the widths this codec wrote the stream with (read from its header when the stream came
+        # from elsewhere: the ex entry point then rejects a mismatch by leaving y alone)
+        bm, bo = packed.widths or (self.hparams.num_bits_main, self.hparams.num_bits_outlier)
+        N.check(N.lib().smq_smaq_decompress_ex(packed.data.data_ptr(), y.data_ptr(), packed.n,
+                                               bm, bo, N.stream_ptr(y.device)),
+                "smq_smaq_decompress_ex")
         return y
 
     def __call__(self, data: torch.Tensor, tag: str = None, all_positive=False,

@@ -4,8 +4,10 @@
   statistics and the same counter RNG): header, directory, every block image, escapes.
 * decompress(compress(x)) equals SmartFP(x) bit for bit for the same flags and random stream,
   and equals the oracle's unpack of the same stream.
-* Large tensors (16k+ blocks, the decoupled look-back under load): the round-trip identity, the
-  directory (monotone, consistent with each block's size) and sampled block images vs the oracle.
+* Large tensors (16k+ blocks): the round-trip identity, the directory (monotone, consistent with
+  each block's size) and sampled blocks' fixed and variable sections vs the oracle.
+* Escape-heavy blocks whose variable section outgrows its scratch slot are re-coded by the var
+  kernel: same bytes as the oracle.
 """
 
 import numpy as np
@@ -152,9 +154,9 @@ def test_rejections():
             batch_norm_stats=(torch.ones(3, device="cuda"), torch.zeros(3, device="cuda")))
 
 
-def test_large_multiblock_lookback():
-    """64M elements = 16384 blocks compacted by the look-back scan: round trip == SmartFP, the
-    directory matches each block's size, sampled block images equal the oracle's."""
+def test_large_multiblock():
+    """64M elements = 16384 blocks: round trip == SmartFP, the directory matches each block's
+    variable-section size, sampled blocks' fixed and variable sections equal the oracle's."""
     from oracle import rng as orng
     from oracle import smaq as osmaq
     from oracle import smaq_packed as P
@@ -171,32 +173,32 @@ def test_large_multiblock_lookback():
     assert torch.equal(y.view(torch.int32), y_ref.view(torch.int32))
     del y, y_ref
     raw = packed.data.cpu().numpy()
-    h = P.header(raw)
+    h, dirs, fixed_w, var_w = P.regions(raw)
     nb = h["n_blocks"]
     assert nb == n // 4096 and h["error"] == 0 and h["total_bytes"] == raw.size
-    dent = raw[128: 128 + 8 * nb].view(np.uint64)
-    dirs = (dent & np.uint64((1 << 38) - 1)).astype(np.int64)
-    data = raw[128 + 8 * nb:].view(np.uint32)
-    w0 = data[dirs]
-    n_out, n_esc = (w0 & 0xFFFF).astype(np.int64), (w0 >> 16).astype(np.int64)
-    assert np.array_equal((dent >> np.uint64(38)) & np.uint64(0x1FFF), n_out.astype(np.uint64))
-    assert np.array_equal(dent >> np.uint64(51), n_esc.astype(np.uint64))
-    size = 129 + (5 * 4096 + 2 * n_out + 31) // 32 + 2 * n_esc
-    assert dirs[0] == 0 and np.array_equal(np.diff(dirs), size[:-1])
-    assert dirs[-1] + size[-1] == h["data_words"]
+    assert h["version"] == 2 and var_w.size == h["data_words"]
+    off = (dirs & np.uint64((1 << 38) - 1)).astype(np.int64)
+    n_out = ((dirs >> np.uint64(38)) & np.uint64(0x1FFF)).astype(np.int64)
+    n_esc = (dirs >> np.uint64(51)).astype(np.int64)
+    size = (2 * n_out + 31) // 32 + 2 * n_esc
+    assert off[0] == 0 and np.array_equal(np.diff(off), size[:-1])
+    assert off[-1] + size[-1] == h["data_words"]
     assert n_esc.sum() > nb  # escapes present throughout
+    F = P.fixed_words(5)
+    mask_pop = np.unpackbits(fixed_w.reshape(nb, F)[:, :128].view(np.uint8), axis=1).sum(axis=1)
+    assert np.array_equal(mask_pop, n_out)
     cfg = osmaq.SmaqConfig()
     xh = x.cpu().numpy()
     for b in (0, 1, 2, nb // 2, nb - 2, nb - 1):
         s = slice(b * 4096, (b + 1) * 4096)
         u = orng.uniforms(77, 1000 + b * 4096, 4096)
-        img = P.pack_block(xh[s], h["mean"], h["std_dev"], cfg, u)
-        got = data[dirs[b]: dirs[b] + img.size]
-        assert np.array_equal(got, img), b
+        fx, vr = P.pack_block(xh[s], h["mean"], h["std_dev"], cfg, u)
+        assert np.array_equal(fixed_w[b * F:(b + 1) * F], fx), b
+        assert np.array_equal(var_w[off[b]: off[b] + vr.size], vr), b
 
 
 def test_compress_is_repeatable():
-    """Same seed/offset twice (workspace counters reset by the last block): identical streams."""
+    """Same seed/offset twice on one workspace: identical streams."""
     hp, pk, _ = _codecs(seed=4, offset=0)
     x = torch.randn(3 * 4096 + 77, device="cuda")
     a = pk.compress(x).data.clone()
@@ -205,38 +207,7 @@ def test_compress_is_repeatable():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("n", [4096, 3 * 4096 + 77, (1 << 22) + 5])
-def test_ticketed_and_index_order_give_the_same_bytes(n):
-    """smq_smaq_compress_ex: index-ordered block ids (default) and SMQ_PACK_TICKETED ids place
-    block b after blocks 0..b-1 either way: byte-identical streams (twice each: the ticket counter
-    resets itself)."""
-    from smart_compress_amd import _native as N
-
-    hp, pk, _ = _codecs(seed=9, offset=5)
-    gen = torch.Generator(device="cuda").manual_seed(n)
-    x = torch.randn(n, generator=gen, device="cuda")
-    x[::501] *= 30.0
-    lib = N.lib()
-    p = pk._params(n, False, x.dtype, x.device)
-    bound = lib.smq_smaq_pack_bound(n, hp.num_bits_main, hp.num_bits_outlier)
-    ws = torch.zeros(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8, device="cuda")
-    outs = []
-    for flags in (0, N.SMQ_PACK_TICKETED, N.SMQ_PACK_TICKETED, 0, N.SMQ_PACK_SINGLE):
-        out = torch.zeros(bound, dtype=torch.uint8, device="cuda")
-        N.check(lib.smq_smaq_compress_ex(x.data_ptr(), N.SMQ_DTYPE_F32, n, p, out.data_ptr(),
-                                         out.numel(), ws.data_ptr(), ws.numel(), flags,
-                                         N.stream_ptr(x.device)), "compress_ex")
-        outs.append(out)
-    torch.cuda.synchronize()
-    to, eo = N.SmqPackedHeader.total_bytes.offset, N.SmqPackedHeader.error.offset
-    total = int(outs[0][to:to + 8].cpu().numpy().view(np.uint64)[0])
-    assert int(outs[0][eo:eo + 4].cpu().numpy().view(np.uint32)[0]) == 0
-    assert total > 128
-    for o in outs[1:]:
-        assert torch.equal(o[:total], outs[0][:total])
-
-
-def _compress_raw(x, pk, flags, p):
+def _compress_raw(x, pk, flags, p, ws=None):
     """smq_smaq_compress_ex with explicit flags and params into a fresh buffer; returns the
     stream bytes."""
     from smart_compress_amd import _native as N
@@ -245,7 +216,8 @@ def _compress_raw(x, pk, flags, p):
     n = x.numel()
     code = N.DTYPE_CODES[x.dtype]
     bound = lib.smq_smaq_pack_bound(n, pk.hparams.num_bits_main, pk.hparams.num_bits_outlier)
-    ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(n))
+    if ws is None:
+        ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(n))
     out = torch.zeros(bound, dtype=torch.uint8, device=x.device)
     N.check(lib.smq_smaq_compress_ex(x.data_ptr(), code, n, p, out.data_ptr(), out.numel(),
                                      ws.data_ptr(), ws.numel(), flags, N.stream_ptr(x.device)),
@@ -258,32 +230,63 @@ def _compress_raw(x, pk, flags, p):
     return raw[:int(raw[to:to + 8].view(np.uint64)[0])]
 
 
+def _oracle_of(raw, x, hp, seed, offset, dtype="f32"):
+    from oracle import smaq_packed as P
+
+    h = P.header(raw)
+    packed = type("P", (), {"header": lambda self: h})()
+    stream, _, _ = _oracle_stream(x.float().cpu().numpy(), packed, hp, seed, offset, dtype=dtype)
+    return stream
+
+
 @pytest.mark.parametrize("n", [8, 4095, 4096, 4097, 3 * 4096 + 77, (1 << 20) + 5])
-@pytest.mark.parametrize("bits", [(6, 8), (4, 6), (9, 12), (15, 15), (16, 18)])
-def test_streaming_packer_equals_single_launch(n, bits):
-    """Default (streaming: code records -> group scan -> block images) and SMQ_PACK_SINGLE (one
-    look-back launch) give the same bytes, incl. escapes whose q does not fit a record (|q| > 4095,
-    inf, NaN: re-derived from x), widths beyond the 14-bit records (both take the single launch),
-    and repeated calls on one workspace."""
+@pytest.mark.parametrize("bits", [(6, 8), (4, 6), (9, 12), (15, 15), (16, 18), (3, 21), (10, 5)])
+def test_packer_widths_escapes_and_flags(n, bits):
+    """Heavy-tailed input (NaN, +-inf, |q| far beyond any budget) at widths from 2 to 20 bits
+    (wo - wm from -5 to 18): the stream equals the oracle's byte for byte; the legacy flags
+    (SMQ_PACK_SINGLE / TICKETED) give the same bytes; a second call on the same workspace too."""
     from smart_compress_amd import _native as N
 
     hp, pk, _ = _codecs(seed=3, offset=11, num_bits_main=bits[0], num_bits_outlier=bits[1])
     x_np = _heavy(n, n % 97)
     rs = np.random.default_rng(n)
-    x_np[rs.random(n) < 0.002] *= 1e6  # |q| far beyond 4095
+    x_np[rs.random(n) < 0.002] *= 1e6
     x = torch.from_numpy(x_np).cuda()
     p = pk._params(n, False, x.dtype, x.device)
     a = _compress_raw(x, pk, 0, p)
-    b = _compress_raw(x, pk, N.SMQ_PACK_SINGLE, p)
-    c = _compress_raw(x, pk, 0, p)
-    m = min(a.size, b.size)
-    assert a.size == b.size and np.array_equal(a, b), (a.size, b.size, int(np.argmax(a[:m] != b[:m])))
-    assert np.array_equal(a, c)
+    assert np.array_equal(a, _oracle_of(a, x, hp, 3, 11))
+    for flags in (N.SMQ_PACK_SINGLE, N.SMQ_PACK_TICKETED, 0):
+        assert np.array_equal(a, _compress_raw(x, pk, flags, p))
+
+
+@pytest.mark.parametrize("frac", [0.2, 0.6, 1.0])
+def test_escape_heavy_blocks_recoded(frac):
+    """Blocks with more escapes than their 3 KiB scratch slot holds (> ~380 at 6/8 bits) are
+    re-coded from x by the var kernel: mixed with ordinary blocks, the stream equals the oracle's
+    and decodes to SmartFP's output."""
+    hp, pk, ref = _codecs(seed=12, offset=7)
+    n = 9 * 4096 + 333
+    rs = np.random.default_rng(int(frac * 10))
+    x_np = rs.standard_normal(n).astype(np.float32)
+    for b in (1, 4, 8, 9):  # escape-heavy blocks (incl. the short last one)
+        s = slice(b * 4096, min(n, (b + 1) * 4096))
+        sel = rs.random(x_np[s].size) < frac
+        x_np[s][sel] *= 1e4
+    x = torch.from_numpy(x_np).cuda()
+    p = pk._params(n, False, x.dtype, x.device)
+    a = _compress_raw(x, pk, 0, p)
+    assert np.array_equal(a, _oracle_of(a, x, hp, 12, 7))
+    pk.rng.offset = 7  # (_params advanced it)
+    packed = pk.compress(x)
+    y = pk.decompress(packed)
+    y_ref = ref(x)
+    torch.cuda.synchronize()
+    assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
 
 
 @pytest.mark.parametrize("dt", ["f32", "f16", "bf16"])
-def test_streaming_packer_unaligned_and_half(dt):
-    """Element-path (misaligned x) and half inputs through the streaming packer == the oracle."""
+def test_packer_unaligned_and_half(dt):
+    """Element-path (misaligned x) and half inputs == the oracle."""
     tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[dt]
     hp, pk, _ = _codecs(seed=8, offset=0, precision=16 if dt != "f32" else 32)
     gen = torch.Generator(device="cuda").manual_seed(2)
@@ -291,32 +294,41 @@ def test_streaming_packer_unaligned_and_half(dt):
     x = base[1:]  # misaligned by one element
     assert x.data_ptr() % 16 != 0
     got = _compress_raw(x, pk, 0, pk._params(x.numel(), False, x.dtype, x.device))
-    from oracle import smaq_packed as P
-
-    h = P.header(got)
-    packed = type("P", (), {"header": lambda self: h})()
-    stream, _, _ = _oracle_stream(x.float().cpu().numpy(), packed, hp, 8, 0, dtype=dt)
-    assert np.array_equal(got, stream)
+    assert np.array_equal(got, _oracle_of(got, x, hp, 8, 0, dtype=dt))
 
 
 @pytest.mark.parametrize("scale", [1e8, 3.0e-3])
-def test_streaming_packer_quot_check_paths(scale):
+def test_packer_quot_check_paths(scale):
     """std >= 2^24 makes the statistics ask for the per-element subnormal-quotient check
-    (quot_check_for): the streaming packer's checked body gives the oracle's bytes and the same
-    bytes as the single launch; a small scale exercises the unchecked body."""
-    from smart_compress_amd import _native as N
-
+    (quot_check_for): the checked body gives the oracle's bytes; a small scale exercises the
+    unchecked body."""
     hp, pk, _ = _codecs(seed=6, offset=2)
     n = 5 * 4096 + 123
     gen = torch.Generator(device="cuda").manual_seed(7)
     x = torch.randn(n, generator=gen, device="cuda") * scale
-    p = pk._params(n, False, x.dtype, x.device)
-    a = _compress_raw(x, pk, 0, p)
-    b = _compress_raw(x, pk, N.SMQ_PACK_SINGLE, p)
-    assert np.array_equal(a, b)
-    from oracle import smaq_packed as P
+    a = _compress_raw(x, pk, 0, pk._params(n, False, x.dtype, x.device))
+    assert np.array_equal(a, _oracle_of(a, x, hp, 6, 2))
 
-    h = P.header(a)
-    packed = type("P", (), {"header": lambda self: h})()
-    stream, _, _ = _oracle_stream(x.cpu().numpy(), packed, hp, 6, 2)
-    assert np.array_equal(a, stream)
+
+def test_decompress_with_and_without_caller_widths():
+    """smq_smaq_decompress (widths from the stream header) and smq_smaq_decompress_ex (the
+    caller's widths: no header wait) decode the same bytes; _ex with widths the stream was not
+    written with leaves y untouched."""
+    from smart_compress_amd import _native as N
+
+    hp, pk, _ = _codecs(seed=31, offset=0, num_bits_main=4, num_bits_outlier=6)
+    n = 7 * 4096 + 19
+    x = torch.randn(n, device="cuda") * 2
+    packed = pk.compress(x)
+    lib = N.lib()
+    st = N.stream_ptr(x.device)
+    a = torch.full((n,), 7.0, device="cuda")
+    b = torch.full((n,), 7.0, device="cuda")
+    c = torch.full((n,), 7.0, device="cuda")
+    N.check(lib.smq_smaq_decompress(packed.data.data_ptr(), a.data_ptr(), n, st), "dec")
+    N.check(lib.smq_smaq_decompress_ex(packed.data.data_ptr(), b.data_ptr(), n, 4, 6, st), "dex")
+    N.check(lib.smq_smaq_decompress_ex(packed.data.data_ptr(), c.data_ptr(), n, 6, 8, st), "dex2")
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    assert not torch.equal(a, torch.full_like(a, 7.0))
+    assert torch.equal(c, torch.full_like(c, 7.0))

@@ -56,18 +56,36 @@ def test_packed_escapes_and_sizes(n, bits):
         assert same_f32(P.unpack(st), y_ref)
 
 
-def test_code_stream_layout():
-    """Codes in element order, LSB-first, width wm (main) or wo (outlier): element e at bit
-    wm * e + (wo - wm) * (outliers before e)."""
+def test_fixed_and_variable_layout():
+    """Format v2: a block's fixed section is 128 mask words + the plane (the low wm bits of every
+    code at bit wm * e); its variable section holds the outliers' remaining wo - wm code bits in
+    element order, then the escapes. Each block's fixed section sits at b * F words (no prefix
+    needed to place it), the directory locates the variable sections."""
     from oracle import smaq_packed as P
 
     cb = np.array([1, 0x45, 2, 3], np.uint64)
     ob = np.array([False, True, False, False])
-    w = P._code_stream(cb, ob, 5, 7)
-    assert w.size == 1 and w[0] == (1 | (0x45 << 5) | (2 << 12) | (3 << 17))
+    fx = P.block_fixed(cb, ob, 5)
+    assert fx.size == P.fixed_words(5) == 128 + 5 * 128
+    assert fx[0] == 0b0010 and not fx[1:128].any()
+    assert fx[128] == (1 | ((0x45 & 31) << 5) | (2 << 10) | (3 << 15)) and not fx[129:].any()
+    v = P.block_var(cb, ob, np.zeros(4, bool), np.zeros(4, np.float32), 5, 7)
+    assert v.size == 1 and v[0] == (0x45 >> 5)
     rs = np.random.default_rng(0)
-    for wm, wo in ((5, 7), (1, 2), (13, 24)):
+    for wm, wo in ((5, 7), (1, 2), (13, 24), (6, 4)):
         ob = rs.random(1000) < 0.3
         cb = np.where(ob, rs.integers(0, 2**wo, 1000), rs.integers(0, 2**wm, 1000)).astype(np.uint64)
-        words = P._code_stream(cb, ob, wm, wo)
-        assert words.size == (wm * 1000 + (wo - wm) * int(ob.sum()) + 31) // 32
+        eb = rs.random(1000) < 0.01
+        v = P.block_var(cb, ob, eb, rs.standard_normal(1000).astype(np.float32), wm, wo)
+        assert v.size == (max(0, wo - wm) * int(ob.sum()) + 31) // 32 + 2 * int(eb.sum())
+    x = rs.standard_normal(3 * 4096 + 5).astype(np.float32) * 3
+    from oracle import smaq as osmaq
+
+    st = P.pack(x, np.float32(0.1), np.float32(2.0), osmaq.SmaqConfig(stochastic_rounding=False))
+    h, dirs, fixed_w, var_w = P.regions(st)
+    assert fixed_w.size == 4 * P.fixed_words(5) and h["data_words"] == var_w.size
+    off = (dirs & np.uint64((1 << 38) - 1)).astype(np.int64)
+    n_out = ((dirs >> np.uint64(38)) & np.uint64(0x1FFF)).astype(np.int64)
+    n_esc = (dirs >> np.uint64(51)).astype(np.int64)
+    size = (2 * n_out + 31) // 32 + 2 * n_esc
+    assert off[0] == 0 and np.array_equal(np.diff(off), size[:-1]) and off[-1] + size[-1] == var_w.size

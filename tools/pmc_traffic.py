@@ -31,8 +31,8 @@ SHORT = {
     "s2fp8_apply_kernel": "s2fp8_apply_kernel",
     "smaq_pack_kernel": "smaq_pack_kernel",
     "smaq_unpack_kernel": "smaq_unpack_kernel",
-    "smaq_code_kernel": "smaq_code_kernel",
-    "smaq_emit_kernel": "smaq_emit_kernel",
+    "smaq_pack_block_kernel": "smaq_pack_block_kernel",
+    "smaq_pack_var_kernel": "smaq_pack_var_kernel",
     "smaq_pack_scan_kernel": "smaq_pack_scan_kernel",
     "smaq_draw_stats_kernel": "smaq_draw_stats_kernel",
     "smaq_multi_draw_kernel": "smaq_multi_draw_kernel",
