@@ -395,31 +395,37 @@ __device__ __forceinline__ int64_t s2_tile_of(int b, int tpc, int n_chunks) {
   return w < n_chunks ? (int64_t)w * tpc + (k % tpc) : -1;
 }
 
-// x^p for x >= 0 (or NaN) as exp2(p * log2(x)) on the hardware v_log_f32 / v_exp_f32 (ocml's
-// log2f / exp2f, ~1 ulp each). Valid for finite p > 0 (the caller checks once per launch):
-// 0 -> 0, inf -> inf, NaN -> NaN like powf. Relative error ~ ln2 * |p * log2 x| * 2^-23; the S2FP8
-// parity contract is the E5M2 code of Y (measured: 2 adjacent-code flips per 10^6 elements).
-__device__ __forceinline__ float pow_pos(float x, float p) { return exp2f(p * log2f(x)); }
+// The fast forward power: x^p for x >= 0 (or NaN) as exp2(p * log2(x)) on the hardware v_log_f32 /
+// v_exp_f32 (ocml's log2f / exp2f, ~1 ulp each), valid for finite p > 0 (the caller checks once
+// per launch): 0 -> 0, inf -> inf, NaN -> NaN like powf. Relative error ~ ln2 * |p * log2 x| *
+// 2^-23 (at C4 up to 92 ulp of Y), so on its own it moved 2 of 3.1M E5M2 codes to the adjacent
+// code (round 2); s2_fast_uncertain finds every element where that can happen.
 
-// s2fp8.py:45-48 for one element. FAST = alpha is finite and > 0 (else the exact powf path keeps
-// the reference's degenerate-case semantics, e.g. all-zero input -> NaN).
-// out_mode (SMQ_S2FP8_OUT_Y / _T test aids, uniform per launch): return Y or T instead of y.
-template <bool FAST>
-__device__ __forceinline__ float s2fp8_elem(float xv, uint32_t r, float alpha, float bp2,
-                                            float ibp2, float ialpha, int check_inf,
-                                            float max_value, int out_mode) {
-  // torch.sign: +1 / -1, and +0.0 for +-0 and NaN (measured on torch 2.10 CPU)
-  const float sgn = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
-  const float a = fabsf(xv);
-  float Y = FAST ? pow_pos(a, alpha) : powf(a, alpha);  // X_abs.pow_(alpha)
-  Y = Y * bp2;                                            // .mul_(beta_pow2)
-  if (out_mode == 1) return Y;
-  float T = qtorch_quant(Y, r, 5, 2, true);
-  if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
-  if (out_mode == 2) return T;
-  const float t1 = T * ibp2;                              // truncated * beta_pow2.reciprocal_()
-  const float t2 = FAST ? pow_pos(t1, ialpha) : powf(t1, ialpha);  // ** alpha.reciprocal_()
-  return t2 * sgn;                                        // * signs
+// Could the E5M2 code stochastic rounding gives Y_fast = exp2(alpha * lg) * 2^beta (lg = log2f|x|)
+// differ from the one it gives the accurate Y = powf(|x|, alpha) * 2^beta? The code is
+// (bits(v) + (r & M)) & ~M with v = Y (normal E5M2 range) or Y + 2^-14 (subnormal range),
+// M = 2^21 - 1: it changes only if the two v lie on different sides of a multiple of 2^21 after
+// adding the random bits. Bound on |bits(v_fast) - bits(v_accurate)| (integer bit distance, <=
+// 2^24 x relative error): log2f <= 2^-22 max(|lg|, 1) absolute, the product, v_exp_f32, both
+// multiplies and powf (<= 2 ulp) give relative error <= ln2 (|alpha| 2^-22 max(|lg|,1) +
+// 2^-24 |alpha lg|) + 2^-21 + 2^-23, i.e. <= 3.5 |alpha| max(|lg|, 1) + 10 in bit distance; the
+// test uses 4 |alpha| max(|lg|, 1) + 16. Where the random offset leaves less than that to the
+// boundary the element is recomputed with powf (~2e-4 of N(0,1) elements at C4), so the fast
+// path's codes — and outputs — are the accurate path's, bit for bit (tests/test_gpu_float.py
+// test_s2fp8_fast_equals_exact_pow). |x| = 0 is exact on both paths.
+// The margin: E >= 4 |alpha| max(|lg|, 1) + 16 for every element it is used for (lgmax: the largest
+// such |lg| — one element's, or a lane's to share one margin), saturated at 2^20, where it flags all.
+__device__ __forceinline__ uint32_t s2_fast_margin(float alpha, float lgmax) {
+  const float e = __builtin_fmaf(4.0f * fabsf(alpha), lgmax > 1.0f ? lgmax : 1.0f, 16.0f);
+  return e < 1048576.0f ? (uint32_t)e : 1048576u;  // (inf / NaN alpha: all)
+}
+
+// v: the value whose low 21 bits the rounding adds the random word rm to (Y, or Y + 2^-14 in the
+// subnormal E5M2 range); uncertain iff that sum is within E of a multiple of 2^21. A NaN x (lg NaN)
+// always, x = 0 (lg = -inf, Y = 0 on both paths) never.
+__device__ __forceinline__ bool s2_fast_uncertain(uint32_t vb, uint32_t rm, uint32_t E, float lg) {
+  const uint32_t L = (vb + rm) & 0x1fffffu;
+  return ((L - E >= 0x200000u - 2u * E) && lg != -INFINITY) || lg != lg;
 }
 
 // Inverse of precision 32 by table (s2fp8.py:48: (T * 2^-beta) ** (1/alpha)). T is an E5M2 value
@@ -459,9 +465,15 @@ __device__ __forceinline__ float s2_inverse_lut(float T, const float* lut) {
 // (qtorch_quant(Y, r, 5, 2, true) with its normal and subnormal paths both computed and one
 // selected) and check_inf (+57344 -> +inf; an E5M2 value within FLT_EPSILON of 57344 is 57344).
 // Returns T's bits.
-// s2_fwd_fast from lg = log2f(|x|) (the single launch keeps it from its statistics pass).
-__device__ __forceinline__ uint32_t s2_fwd_fast_lg(float lg, uint32_t r, float alpha, float bp2,
-                                                   int check_inf) {
+template <bool FAST>
+__device__ __forceinline__ float s2fp8_fwd(float xv, uint32_t r, float alpha, float bp2,
+                                           int check_inf, float max_value, int out_mode);
+
+// s2_fwd_fast from lg = log2f(|x|) (the single launch keeps it from its statistics pass); an
+// element whose code the fast power's error could change (s2_fast_uncertain, margin E) takes powf.
+__device__ __forceinline__ uint32_t s2_fwd_fast_lg(float xv, float lg, uint32_t r, float alpha,
+                                                   float bp2, int check_inf, float max_value,
+                                                   uint32_t E) {
   const float Y = __builtin_amdgcn_exp2f(alpha * lg) * bp2;
   const uint32_t t = __builtin_bit_cast(uint32_t, Y);
   const uint32_t rm = r & 0x1fffffu;            // (1 << (23 - man)) - 1
@@ -469,24 +481,49 @@ __device__ __forceinline__ uint32_t s2_fwd_fast_lg(float lg, uint32_t r, float a
   qn = ((qn >> 23) & 0xffu) > 142u ? ((t & 0x80000000u) | 0x47600000u) : qn;  // clip_exponent
   const float sh = __builtin_bit_cast(float, 0x38800000u | (t & 0x80000000u));  // 2^-14
   const float vs = Y + sh;
-  const float qs = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, vs) + rm) & 0xffe00000u) - sh;
-  uint32_t T = ((t & 0x7f800000u) < 0x38800000u) ? __builtin_bit_cast(uint32_t, qs) : qn;
+  const uint32_t vsb = __builtin_bit_cast(uint32_t, vs);
+  const float qs = __builtin_bit_cast(float, (vsb + rm) & 0xffe00000u) - sh;
+  const bool sub = (t & 0x7f800000u) < 0x38800000u;
+  uint32_t T = sub ? __builtin_bit_cast(uint32_t, qs) : qn;
   if (check_inf) T = (T == 0x47600000u) ? 0x7f800000u : T;
+  if (__builtin_expect(s2_fast_uncertain(sub ? vsb : t, rm, E, lg), 0))
+    T = __builtin_bit_cast(uint32_t, s2fp8_fwd<false>(xv, r, alpha, bp2, check_inf, max_value, 0));
   return T;
 }
 
 __device__ __forceinline__ uint32_t s2_fwd_fast(float xv, uint32_t r, float alpha, float bp2,
-                                                int check_inf) {
-  return s2_fwd_fast_lg(log2f(fabsf(xv)), r, alpha, bp2, check_inf);
+                                                int check_inf, float max_value) {
+  const float lg = log2f(fabsf(xv));
+  return s2_fwd_fast_lg(xv, lg, r, alpha, bp2, check_inf, max_value,
+                        s2_fast_margin(alpha, fabsf(lg)));
+}
+
+// T of the fast power for the generic paths (the same codes as s2_fwd_fast_lg: either equals the
+// accurate path's wherever it matters)
+__device__ __forceinline__ bool s2_fast_uncertain_y(float Y, uint32_t r, float alpha, float lg) {
+  const uint32_t t = __builtin_bit_cast(uint32_t, Y);
+  const float sh = __builtin_bit_cast(float, 0x38800000u | (t & 0x80000000u));
+  const uint32_t vb = ((t & 0x7f800000u) < 0x38800000u) ? __builtin_bit_cast(uint32_t, Y + sh) : t;
+  return s2_fast_uncertain(vb, r & 0x1fffffu, s2_fast_margin(alpha, fabsf(lg)), lg);
 }
 
 // Forward half of s2fp8_elem for the LUT inverse: T (after check_inf), or Y / T per out_mode.
+// FAST: the hardware exp2(alpha log2|x|), with powf where the code could differ (s2_fast_uncertain;
+// OUT_Y returns the fast Y itself).
 template <bool FAST>
 __device__ __forceinline__ float s2fp8_fwd(float xv, uint32_t r, float alpha, float bp2,
                                            int check_inf, float max_value, int out_mode) {
   const float a = fabsf(xv);
-  float Y = FAST ? pow_pos(a, alpha) : powf(a, alpha);  // X_abs.pow_(alpha)
-  Y = Y * bp2;                                            // .mul_(beta_pow2)
+  float Y;
+  if (FAST) {
+    const float lg = log2f(a);
+    Y = exp2f(alpha * lg) * bp2;
+    if (out_mode == 1) return Y;
+    if (__builtin_expect(s2_fast_uncertain_y(Y, r, alpha, lg), 0)) Y = powf(a, alpha) * bp2;
+  } else {
+    Y = powf(a, alpha);                                   // X_abs.pow_(alpha)
+    Y = Y * bp2;                                          // .mul_(beta_pow2)
+  }
   if (out_mode == 1) return Y;
   float T = qtorch_quant(Y, r, 5, 2, true);
   if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
@@ -505,8 +542,14 @@ __device__ __forceinline__ float s2fp8_elem16(float xv, uint32_t r, float alpha,
                                               float max_value) {
   const float sgn = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
   const float a = fabsf(xv);
-  float Y = (FAST && TIN == kF32) ? pow_pos(a, alpha) : powf(a, alpha);
-  Y = s2_round<TIN>(s2_round<TIN>(Y) * bp2);
+  float Y;
+  if (FAST && TIN == kF32) {  // fp32 data: Y is fp32, the fast power with the same check
+    const float lg = log2f(a);
+    Y = exp2f(alpha * lg) * bp2;
+    if (__builtin_expect(s2_fast_uncertain_y(Y, r, alpha, lg), 0)) Y = powf(a, alpha) * bp2;
+  } else {
+    Y = s2_round<TIN>(s2_round<TIN>(powf(a, alpha)) * bp2);
+  }
   float T = qtorch_quant(Y, r, 5, 2, true);
   if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
   const float t1 = s2_round<kF16>(T * ibp2);
@@ -594,10 +637,10 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) r[k] = rng_u32(A.key, c + (uint64_t)k);
       }
-      T[u][0] = s2_fwd_fast(v[u].x, r[0], alpha, bp2, A.check_inf);
-      T[u][1] = s2_fwd_fast(v[u].y, r[1], alpha, bp2, A.check_inf);
-      T[u][2] = s2_fwd_fast(v[u].z, r[2], alpha, bp2, A.check_inf);
-      T[u][3] = s2_fwd_fast(v[u].w, r[3], alpha, bp2, A.check_inf);
+      T[u][0] = s2_fwd_fast(v[u].x, r[0], alpha, bp2, A.check_inf, A.max_value);
+      T[u][1] = s2_fwd_fast(v[u].y, r[1], alpha, bp2, A.check_inf, A.max_value);
+      T[u][2] = s2_fwd_fast(v[u].z, r[2], alpha, bp2, A.check_inf, A.max_value);
+      T[u][3] = s2_fwd_fast(v[u].w, r[3], alpha, bp2, A.check_inf, A.max_value);
     }
     float t2[kFqTileV][4];
 #pragma unroll
@@ -1035,13 +1078,26 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
                     ialpha < INFINITY;
   const bool last_chunk = b == A.G - 1;
   if (fast && A.out_mode == 0) {
+    // one margin for the lane's elements: the largest |log2|x|| among them (zeros and NaN aside)
+    float lgmax = 1.0f;
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      if (base + (int64_t)u * kS2FT >= A.nv) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        lgmax = fmaxf(lgmax, lg[u][q] == -INFINITY ? 0.0f : fabsf(lg[u][q]));
+    }
+    const uint32_t E = s2_fast_margin(alpha, lgmax);
     uint32_t T[kS2FMaxV][4];
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       const int64_t j = base + (int64_t)u * kS2FT;
       if (j >= A.nv) continue;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) T[u][q] = s2_fwd_fast_lg(lg[u][q], rw[u][q], alpha, bp2, A.check_inf);
+      for (int q = 0; q < 4; ++q) {
+        const float xq = q == 0 ? v[u].x : (q == 1 ? v[u].y : (q == 2 ? v[u].z : v[u].w));
+        T[u][q] = s2_fwd_fast_lg(xq, lg[u][q], rw[u][q], alpha, bp2, A.check_inf, A.max_value, E);
+      }
     }
     auto sgn = [](float xv) { return (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f); };
 #pragma unroll
