@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SMQ_ABI_VERSION 3
+#define SMQ_ABI_VERSION 4
 
 #define SMQ_OK 0
 #define SMQ_ERR_INVALID -1  /* bad argument */
@@ -68,11 +68,19 @@ extern "C" {
 #define SMQ_WS_OUTLIER_SLOTS 64
 #define SMQ_WS_SAMPLES_OFFSET 66176
 
+/* Device-drawn samples beyond SMQ_MAX_DEVICE_SAMPLES, up to SMQ_MAX_DRAW_SAMPLES: the draw runs
+ * across workgroups (smaq.hip, "multi-workgroup draw") and needs
+ * smq_smaq_workspace_bytes_sampled(n, k) bytes; its k indices land at SMQ_WS_LARGE_SAMPLES_OFFSET
+ * (int64, draw order) instead of SMQ_WS_SAMPLES_OFFSET. The indices are the same Floyd draw either
+ * way (smq_smaq_draw_samples / oracle/rng.py floyd_indices). */
+#define SMQ_MAX_DRAW_SAMPLES (1 << 28)
+#define SMQ_WS_LARGE_SAMPLES_OFFSET 99584
+
 /* Where smq_smaq_apply_f32 takes (mean, std) from. */
 #define SMQ_STATS_WORKSPACE 0 /* written by smq_smaq_stats_f32 into the workspace header */
 #define SMQ_STATS_SAMPLED 1   /* computed in-kernel from params.sample_idx (smart.py:86-91) */
 #define SMQ_STATS_INJECTED 2  /* read from the stats_in device pointer (parity tests) */
-/* k = min(n, num_samples) <= SMQ_MAX_DEVICE_SAMPLES distinct indices drawn ON THE DEVICE by
+/* k = min(n, num_samples) <= SMQ_MAX_DRAW_SAMPLES distinct indices drawn ON THE DEVICE by
  * Floyd's algorithm from (seed, offset + graph-safe stream position), a fresh set per call and per
  * hipGraph replay, replacing torch.randperm(n)[:k] (smart.py:88); mean / biased std of the gathered
  * elements as smart.py:86-91. smq_smaq_draw_samples is the host mirror of the draw. */
@@ -84,6 +92,11 @@ extern "C" {
 #define SMQ_DTYPE_F32 0
 #define SMQ_DTYPE_F16 1
 #define SMQ_DTYPE_BF16 2
+/* fp64 tensors: the _f64 entry points (SmaQ, S2FP8) and smq_float_quant / smq_cpu_float_quant.
+ * The reference computes fp64 data in fp64 (smart.py:130-182 under torch's type flow: statistics,
+ * z-score, rounding and de-quantisation in fp64; the bool*float scalars and ranges tensors hold fp32
+ * values) and returns fp64. */
+#define SMQ_DTYPE_F64 3
 
 /* Rounding modes of smq_float_quant_f32 (qtorch float_quantize rounding=...). */
 #define SMQ_ROUND_NEAREST 0
@@ -125,6 +138,14 @@ typedef struct SmqSmaqParams {
    * it by n; element i then draws counter offset + rng_offset + i. Nothing on the host changes
    * between calls, so a captured hipGraph replays with fresh, consecutive random streams. */
   uint64_t* offset_counter;
+  /* fp64 inputs (smq_smaq_roundtrip_f64, smq_cpu_smaq_roundtrip_f64): the Python doubles the
+   * reference compares and clamps fp64 data with (smart.py:82-84, 154-156); smq_smaq_params_set
+   * fills them. The scalars / ranges tensors stay fp32 values (torch's default dtype). */
+  double main_std_dev_threshold_f64; /* T_m */
+  double clamp_lo_f64;               /* 1e-38 (1e-4 at precision 16) */
+  double clamp_hi_f64;               /* 1e38 (1e4 at precision 16) */
+  double range_std_coef_f64;         /* C = 1/sqrt(2 log n) in fp64 (smart.py:103-105 with
+                                        type_as(range_) = double); < 0: the library computes it */
 } SmqSmaqParams;
 
 /*
@@ -147,8 +168,25 @@ typedef struct SmqSmaqStats {
                                   ignored, the library derives it and quot_check itself) */
   unsigned long long rng_offset; /* the call's stream position when params.offset_counter is set
                                     (else 0), added to params.offset by the element kernels */
-  uint32_t reserved[2];
+  float inv_std_clamped_f32;    /* RN32(1 / std_clamped); written by the library (half inputs:
+                                   the z-score quotient, smaq_elem.h half_quot) */
+  uint32_t reserved;
 } SmqSmaqStats;
+
+/* Header of the workspace of an fp64 SmaQ call ([0, 80) of the single-tensor layout; the outlier
+ * slots stay at SMQ_WS_OUTLIER_SLOTS_OFFSET). Also the record of SMQ_STATS_INJECTED for the _f64
+ * entry points (mean and raw_std read; the rest derived). */
+typedef struct SmqSmaqStatsF64 {
+  double mean;        /* data.mean() */
+  double std_dev;     /* std after the `std == 0 -> 1` rule */
+  double std_clamped; /* std_dev.clamp(clamp_lo_f64, clamp_hi_f64) */
+  double raw_std;     /* std before the `std == 0` rule */
+  double min_val, max_val; /* valid in range-std mode */
+  uint32_t n_used;
+  uint32_t reserved0;
+  unsigned long long rng_offset; /* as SmqSmaqStats.rng_offset */
+  unsigned long long reserved[2];
+} SmqSmaqStatsF64;
 
 /* One tensor of a multi-tensor call. x holds n elements of the call's dtype; y (fp32) may alias x
  * for fp32 inputs (in-place, the optimizer path). */
@@ -178,6 +216,15 @@ typedef struct SmqS2fp8Stats {
   uint32_t reserved[6];
 } SmqS2fp8Stats;
 
+/* Header of an fp64 S2FP8 workspace: the reference's fp64 values (s2fp8.py:35-43). */
+typedef struct SmqS2fp8StatsF64 {
+  double mu, m, alpha, beta, beta_pow2, inv_beta_pow2, inv_alpha;
+  uint32_t n_used;
+  uint32_t reserved0;
+  uint64_t rng_offset;
+  uint64_t reserved[3];
+} SmqS2fp8StatsF64;
+
 /* ---- library ---- */
 int smq_abi_version(void);
 const char* smq_last_error(void);
@@ -195,6 +242,10 @@ int smq_smaq_draw_samples(SmqSmaqParams* p, int64_t n, int num_samples);
 
 /* ---- SmaQ single tensor ---- */
 size_t smq_smaq_workspace_bytes(int64_t n);
+/* Workspace of a call on n elements with k = min(n, num_samples) device-drawn samples
+ * (SMQ_STATS_SAMPLED_DEVICE): smq_smaq_workspace_bytes(n) for k <= SMQ_MAX_DEVICE_SAMPLES, more for
+ * the multi-workgroup draw above it (k <= SMQ_MAX_DRAW_SAMPLES; 0 for larger k). */
+size_t smq_smaq_workspace_bytes_sampled(int64_t n, int64_t num_samples);
 int smq_smaq_stats_f32(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,
                        size_t ws_bytes, void* stream);
 /* uniforms: optional device array of n U[0,1) floats replacing the in-kernel RNG (parity tests
@@ -219,6 +270,15 @@ int smq_smaq_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqP
  * smq_smaq_stats + smq_smaq_apply, ~1.1-2.5 us less per call. Knob: SMQ_DEFER_MAX_N (0 = off). */
 int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                        const float* uniforms, void* ws, size_t ws_bytes, void* stream);
+/* fp64 data (smart.py:130-182 on a float64 tensor): statistics, z-score, stochastic or truncating
+ * rounding and de-quantisation in fp64, output fp64; every stats_source (k of SMQ_STATS_SAMPLED_DEVICE
+ * up to SMQ_MAX_DRAW_SAMPLES with a workspace of smq_smaq_workspace_bytes_sampled), BN
+ * (params.bn_gamma / bn_beta then point at fp64 arrays), all_positive, count_outliers.
+ * uniforms: optional n fp64 U[0,1) values (torch.rand_like of fp64 data); else the counter RNG's
+ * u = (h >> 8) * 2^-24. stats_in: SMQ_STATS_INJECTED only. Header: SmqSmaqStatsF64 at offset 0. */
+int smq_smaq_roundtrip_f64(const double* x, double* y, int64_t n, const SmqSmaqParams* p,
+                           const double* uniforms, const SmqSmaqStatsF64* stats_in, void* ws,
+                           size_t ws_bytes, void* stream);
 
 /* ---- SmaQ multi tensor ---- */
 /* A plan is a descriptor table plus a chunk map. smq_smaq_multi_plan_build writes it into a host
@@ -258,6 +318,10 @@ int smq_float_quant_f32(const float* x, float* y, int64_t n, int exp_bits, int m
 int smq_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t n, int exp_bits,
                     int man_bits, int rounding, int check_inf, const uint32_t* rand_bits,
                     uint64_t seed, uint64_t offset, uint64_t* offset_counter, void* stream);
+/* dtype_in SMQ_DTYPE_F64: each element is quantised as its fp32 rounding (the precision-16 branch's
+ * x.float(), quantization.py:190-191; qtorch 0.2.0's kernel itself reads data_ptr<float>() and
+ * raises on fp64, so at precision 32 this is the dtype-generic extension: zeros_like(x) filled with
+ * the quantised values), written as fp64 (dtype_out SMQ_DTYPE_F64) or fp16 (the `.half()`). */
 /* fp32 value of qtorch nearest-quantising FLT_MAX (quantization.py:138-150), host only. */
 float smq_float_quant_max_value(int exp_bits, int man_bits);
 
@@ -307,6 +371,18 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
                            const SmqS2fp8Stats* stats_in, void* ws, size_t ws_bytes,
                            uint32_t flags, void* stream);
 
+/* S2FP8 of fp64 data (s2fp8.py:27-48 in fp64): log2 statistics, alpha, beta, 2^beta and |x|^alpha *
+ * 2^beta in fp64; float_quantize of that as for smq_float_quant with SMQ_DTYPE_F64 input. Precision
+ * 32 (dtype-generic quantiser): the inverse in fp64. Precision 16: float_quantize returns half and
+ * the inverse runs in half as torch does (the 0-dim fp64 reciprocal of 2^beta enters the product at
+ * fp32, the exponent 1/alpha rounded to half), times the fp64 signs: y is fp64 either way.
+ * flags: SMQ_S2FP8_OUT_Y / OUT_T (precision 32). Three launches (statistics partials, derive,
+ * transform); header SmqS2fp8StatsF64 at offset 0 of ws (smq_s2fp8_workspace_bytes(n) bytes). */
+int smq_s2fp8_roundtrip_f64(const double* x, double* y, int64_t n, int precision, int check_inf,
+                            const uint32_t* rand_bits, uint64_t seed, uint64_t offset,
+                            uint64_t* offset_counter, const SmqS2fp8StatsF64* stats_in, void* ws,
+                            size_t ws_bytes, uint32_t flags, void* stream);
+
 /* ---- CPU tensors ----
  * The codecs on host pointers, for tensors that live on the CPU (the reference's plugins run on
  * any device; BASELINE config 1 is a CPU run). Same argument meaning as the device entry points,
@@ -320,7 +396,9 @@ int smq_cpu_threads(void);
 /* SmaQ round trip; ws: host buffer of smq_smaq_workspace_bytes(n) bytes that receives the
  * SmqSmaqStats header, the outlier count (slot 0 of SMQ_WS_OUTLIER_SLOTS, when
  * params.count_outliers) and the drawn indices (SMQ_STATS_SAMPLED_DEVICE: the same Floyd draw as the
- * device, any k <= SMQ_MAX_DEVICE_SAMPLES). params.bn_gamma / bn_beta / offset_counter and
+ * device, any k <= SMQ_MAX_DRAW_SAMPLES; above SMQ_MAX_DEVICE_SAMPLES the buffer is
+ * smq_smaq_workspace_bytes_sampled(n, k) bytes and the indices land at SMQ_WS_LARGE_SAMPLES_OFFSET).
+ * params.bn_gamma / bn_beta / offset_counter and
  * uniforms / stats_in are host pointers here. */
 int smq_cpu_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                            const float* uniforms, const SmqSmaqStats* stats_in, void* ws,
@@ -335,6 +413,15 @@ int smq_cpu_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int pr
                             int check_inf, const uint32_t* rand_bits, uint64_t seed,
                             uint64_t offset, const SmqS2fp8Stats* stats_in, void* ws,
                             size_t ws_bytes, uint32_t flags, int n_threads);
+
+/* The fp64 codecs on host pointers (see the device entry points). */
+int smq_cpu_smaq_roundtrip_f64(const double* x, double* y, int64_t n, const SmqSmaqParams* p,
+                               const double* uniforms, const SmqSmaqStatsF64* stats_in, void* ws,
+                               size_t ws_bytes, int n_threads);
+int smq_cpu_s2fp8_roundtrip_f64(const double* x, double* y, int64_t n, int precision,
+                                int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                                uint64_t offset, const SmqS2fp8StatsF64* stats_in, void* ws,
+                                size_t ws_bytes, uint32_t flags, int n_threads);
 
 /* ---- host reference helpers shared with the oracle (pure functions, no GPU) ---- */
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);

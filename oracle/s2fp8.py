@@ -115,3 +115,75 @@ def roundtrip_p16(x, dt: str, rand_bits, check_inf_flag=True, st=None):
     T = qf.float_quantize(Y, 5, 2, rand_bits, check_inf_flag)
     y, out_dt = inverse_p16(T, x, st, dt)
     return y, out_dt, st, Y, T
+
+
+# ---- float64 data --------------------------------------------------------------------------------
+# s2fp8.py:27-48 on a float64 tensor: the log2 statistics, alpha, beta, 2^beta and |x|^alpha * 2^beta
+# are fp64 ops; float_quantize quantises the fp32 rounding of Y (qtorch's quantiser works on fp32
+# words: the precision-16 branch's Y.float(); at precision 32 the dtype-generic extension, see
+# include/smq.h SMQ_DTYPE_F64). Precision 32: the inverse in fp64. Precision 16: float_quantize
+# returns half and the inverse runs in half as torch does — the 0-dim fp64 reciprocal of 2^beta
+# enters the product as its fp32 value, the exponent 1/alpha is cast to half — times the fp64 signs.
+# Powers and logarithms are the C library's (math.pow / math.log2, element by element: numpy's
+# vectorised fp64 pow differs from libm in ~4 % of elements); the device's may differ by an ulp.
+F64 = np.float64
+_pow = np.frompyfunc(lambda a, b: _libm_pow(a, b), 2, 1)
+_log2 = np.frompyfunc(lambda a: _libm_log2(a), 1, 1)
+
+
+def _libm_pow(a, b):
+    import math
+
+    try:
+        return math.pow(a, b)
+    except (OverflowError, ValueError):
+        return float(np.power(F64(a), F64(b)))
+
+
+def _libm_log2(a):
+    import math
+
+    if a == 0.0 or a != a or a == float("inf"):
+        return float(np.log2(F64(a))) if a != 0.0 else float("-inf")
+    return math.log2(a)
+
+
+def stats_f64(x):
+    a = np.abs(np.asarray(x, dtype=F64))
+    with np.errstate(all="ignore"):
+        lg = np.where(a == F64(0), a, _log2(a).astype(F64))
+    return derive_f64(float(np.mean(lg)), float(np.max(lg)))
+
+
+def derive_f64(mu, m):
+    mu, m = F64(mu), F64(m)
+    with np.errstate(all="ignore"):
+        alpha = (F64(1) / (m - mu)) * F64(15.0)
+        beta = (-alpha) * mu
+        bp2 = F64(_libm_pow(2.0, float(beta)))
+        return dict(mu=mu, m=m, alpha=alpha, beta=beta, beta_pow2=bp2,
+                    inv_beta_pow2=F64(1) / bp2, inv_alpha=F64(1) / alpha)
+
+
+def transform_f64(x, st):
+    a = np.abs(np.asarray(x, dtype=F64))
+    with np.errstate(all="ignore"):
+        return _pow(a, float(st["alpha"])).astype(F64) * st["beta_pow2"]
+
+
+def roundtrip_f64(x, rand_bits, check_inf_flag=True, precision=32, st=None):
+    """-> (y float64, st, Y float64, T float32 quantised codes' values)."""
+    x = np.asarray(x, dtype=F64)
+    st = stats_f64(x) if st is None else st
+    Y = transform_f64(x, st)
+    with np.errstate(all="ignore"):
+        T = qf.float_quantize(Y.astype(F32), 5, 2, rand_bits, check_inf_flag)
+        sgn = np.where(x > 0, F64(1), np.where(x < 0, F64(-1), F64(0)))
+        if precision == 32:
+            t2 = _pow(T.astype(F64) * st["inv_beta_pow2"], float(st["inv_alpha"])).astype(F64)
+            return t2 * sgn, st, Y, T
+        th = _r(T, "f16")
+        t1 = _r(th * F32(st["inv_beta_pow2"]), "f16")
+        ia = _r(F32(st["inv_alpha"]), "f16")
+        t2 = _r(np.power(t1.astype(F64), F64(ia)).astype(F32), "f16")
+        return t2.astype(F64) * sgn, st, Y, T

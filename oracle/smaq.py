@@ -183,3 +183,92 @@ def roundtrip(x: np.ndarray, cfg: SmaqConfig, uniforms=None, sample_idx=None,
         mean, std = full_stats(x, cfg, dtype)
     y, o = apply(x, mean, std, cfg, uniforms, all_positive, bn, dtype)
     return y, mean, std, int(o.sum())
+
+
+# ---- float64 data (smart.py:130-182 under torch's type flow for a float64 tensor) -------------------
+# Statistics, z-score, rounding and de-quantisation are fp64 ops; the clamp bounds and the
+# threshold the z-score is compared with are the Python doubles; the scalars (bool * float) and
+# ranges (torch.where of two Python floats) are float32 tensors, so their fp32 values enter the
+# fp64 chain. Each line is one IEEE fp64 op in the reference's order (numpy does not contract).
+F64 = np.float64
+
+
+def range_coef_f64(n: int) -> float:
+    """1 / sqrt(2 * log(double(n))) (smart.py:103-105 with type_as(range_) = float64)."""
+    return float(F64(1.0) / np.sqrt(F64(2.0) * np.log(F64(n))))
+
+
+def full_stats_f64(x: np.ndarray, cfg: SmaqConfig) -> Tuple[float, float]:
+    """(data.mean(), std) of float64 data: mean, unbiased std (or range-std), in fp64."""
+    x = np.asarray(x, dtype=F64).ravel()
+    mean = float(np.mean(x))
+    if cfg.use_range_std_dev:
+        return mean, float((F64(x.max()) - F64(x.min())) * F64(range_coef_f64(x.size)))
+    d = x - np.mean(x)
+    var = float(np.dot(d, d)) / (x.size - 1) if x.size > 1 else float("nan")
+    return mean, float(np.sqrt(var))
+
+
+def sampled_stats_f64(x: np.ndarray, idx: np.ndarray, cfg: SmaqConfig) -> Tuple[float, float]:
+    """smart.py:86-91 on float64 data: mean and biased std (or range-std) of the samples."""
+    s = np.asarray(x, dtype=F64).ravel()[np.asarray(idx, dtype=np.int64)]
+    mean = float(np.mean(s))
+    if cfg.use_range_std_dev:
+        return mean, float((F64(s.max()) - F64(s.min())) * F64(range_coef_f64(s.size)))
+    d = s - np.mean(s)
+    return mean, float(np.sqrt(float(np.dot(d, d)) / s.size))
+
+
+def apply_f64(x: np.ndarray, mean: float, std: float, cfg: SmaqConfig,
+              uniforms: Optional[np.ndarray] = None, all_positive: bool = False,
+              bn: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+    """smart.py:144-182 on float64 data given (mean, std); returns (y float64, is_outlier)."""
+    x = np.asarray(x, dtype=F64)
+    shape = x.shape
+    mean, std = F64(mean), F64(std)
+    thr = F64(cfg.main_std_dev_threshold)             # compared in fp64 (a Python double)
+    sthr = F64(F32(cfg.main_std_dev_threshold))       # the fp32 scalars tensor's value
+    r_out, r_main = F64(F32(cfg.range_outlier)), F64(F32(cfg.range_normal))
+    lo_c, hi_c = (F64(v) for v in cfg.clamped_range)
+    data = x
+    if bn is not None:
+        g, b = [np.asarray(t, dtype=F64).reshape((1, -1, 1, 1)) for t in bn]
+        data = (data - b) / g
+    if std == F64(0):
+        std = F64(1)
+    sc = std
+    if sc < lo_c:
+        sc = lo_c
+    if sc > hi_c:
+        sc = hi_c
+    with np.errstate(all="ignore"):
+        z = (data - mean) / sc
+        hi = z > thr
+        lo = z < -thr
+        scal = (np.where(hi, -sthr, F64(F32(0) * -F32(cfg.main_std_dev_threshold)))
+                + np.where(lo, sthr, F64(F32(0) * F32(cfg.main_std_dev_threshold))))
+        ranges = np.where(hi | lo, r_out, r_main)
+        d = (z + scal) * ranges
+        if cfg.stochastic_rounding:
+            u = np.asarray(uniforms, dtype=F64).reshape(shape)
+            f = np.floor(d)
+            t = (d - f) - u
+            t = t + F64(0.5)
+            t = np.where(t < F64(0), F64(0), t)
+            q = f + np.rint(t)
+        else:
+            q = np.trunc(d)
+        y = (q / ranges) - scal
+        y = (y * std) + mean
+        if bn is not None:
+            y = (y * g) + b
+        if all_positive:
+            y = np.where(y < F64(0), F64(0), y)
+    return y.astype(F64).reshape(shape), (hi | lo).reshape(shape)
+
+
+def uniforms_f64(seed: int, offset: int, n: int, start: int = 0) -> np.ndarray:
+    """The counter RNG's fp64 uniforms (the same 24-bit values as the fp32 path)."""
+    from . import rng as _rng
+
+    return (_rng.rng_u32(seed, offset, n, start) >> np.uint32(8)).astype(F64) * F64(2.0**-24)

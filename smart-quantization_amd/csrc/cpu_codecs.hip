@@ -30,10 +30,12 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "qtorch.h"
 #include "smaq_elem.h"
+#include "smaq_f64.h"
 #include "smaq_host.h"
 #include "smq_common.h"
 
@@ -182,6 +184,7 @@ static inline float rin(float v) {  // round_in<T> on the host
 template <int T>
 static inline float ld(const void* p, int64_t i) {
   if (T == kF32) return static_cast<const float*>(p)[i];
+  if (T == SMQ_DTYPE_F64) return (float)static_cast<const double*>(p)[i];  // the x.float() RN
   const uint16_t h = static_cast<const uint16_t*>(p)[i];
   return T == kF16 ? h2f(h) : bf2f(h);
 }
@@ -263,6 +266,7 @@ static void finalize(double s1, double s2, float mn, float mx, int64_t n, double
   out->max_val = mx;
   out->n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
   out->inv_std_clamped = 1.0 / (double)sc;
+  out->inv_std_clamped_f32 = (float)out->inv_std_clamped;
   out->quot_check = quot_check_for(sc);
 }
 
@@ -308,15 +312,17 @@ static void sampled_stats(const void* x, const int64_t* idx, int64_t k, const Sm
               range_coef, out);
 }
 
-// The device draw (smaq_elem.h Floyd, smq_smaq_draw_samples) for any k <= SMQ_MAX_DEVICE_SAMPLES.
+// The device draw (smaq_elem.h Floyd, smq_smaq_draw_samples) for any k <= SMQ_MAX_DRAW_SAMPLES.
 static void floyd_draw(uint64_t seed, uint64_t pos, int64_t n, int64_t k, int64_t* out) {
   const uint32_t key = rng_key(seed ^ kDrawSalt);
-  std::vector<int64_t> seen;
-  seen.reserve((size_t)k);
+  std::unordered_set<int64_t> seen;
+  seen.reserve((size_t)(2 * k));
   for (int i = 0; i < (int)k; ++i) {
     int64_t t = floyd_candidate(key, pos, n, (int)k, i);
-    if (std::find(seen.begin(), seen.end(), t) != seen.end()) t = n - k + i;
-    seen.push_back(t);
+    if (!seen.insert(t).second) {
+      t = n - k + i;
+      seen.insert(t);
+    }
     out[i] = t;
   }
 }
@@ -421,7 +427,7 @@ static float range_coef_host(const SmqSmaqParams* p, int64_t n) {
 template <int T>
 static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParams* p,
                           const float* uniforms, const SmqSmaqStats* stats_in, char* ws,
-                          int n_threads) {
+                          size_t ws_bytes, int n_threads) {
   SmqSmaqStats st;
   // a host uint64 stream position (graph-safe mirror), advanced by n only once the call is
   // validated: a rejected call consumes no stream positions, like the device entry points
@@ -446,11 +452,17 @@ static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParam
     }
     case SMQ_STATS_SAMPLED_DEVICE: {
       const int64_t k = std::min<int64_t>(p->num_samples, n);
-      if (k < 1 || k > SMQ_MAX_DEVICE_SAMPLES) {
-        set_error("cpu smaq: num_samples must be in [1, %d]", SMQ_MAX_DEVICE_SAMPLES);
+      if (k < 1 || k > SMQ_MAX_DRAW_SAMPLES) {
+        set_error("cpu smaq: num_samples must be in [1, %d]", SMQ_MAX_DRAW_SAMPLES);
         return SMQ_ERR_INVALID;
       }
-      int64_t* idx = reinterpret_cast<int64_t*>(ws + SMQ_WS_SAMPLES_OFFSET);
+      if (ws_bytes < smq_smaq_workspace_bytes_sampled(n, k)) {
+        set_error("cpu smaq: workspace too small for %lld samples: need %zu bytes", (long long)k,
+                  smq_smaq_workspace_bytes_sampled(n, k));
+        return SMQ_ERR_WORKSPACE;
+      }
+      int64_t* idx = reinterpret_cast<int64_t*>(
+          ws + (k > SMQ_MAX_DEVICE_SAMPLES ? SMQ_WS_LARGE_SAMPLES_OFFSET : SMQ_WS_SAMPLES_OFFSET));
       floyd_draw(p->seed, p->offset + base, n, k, idx);
       sampled_stats<T>(x, idx, k, p, range_coef_host(p, k), &st);
       break;
@@ -462,6 +474,7 @@ static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParam
       }
       st = *stats_in;
       st.inv_std_clamped = 1.0 / (double)st.std_clamped;
+      st.inv_std_clamped_f32 = (float)st.inv_std_clamped;
       st.quot_check = quot_check_for(st.std_clamped);
     }
   }
@@ -611,6 +624,182 @@ static void s2_pass(const void* x, void* y, int64_t n, bool p16, bool hout, int 
   });
 }
 
+
+// ---- fp64 tensors (smaq_f64.h holds the shared finaliser and element transforms) -----------------
+static int smaq_roundtrip_f64(const double* x, double* y, int64_t n, const SmqSmaqParams* p,
+                              const double* uniforms, const SmqSmaqStatsF64* stats_in, char* ws,
+                              size_t ws_bytes, int n_threads) {
+  SmqSmaqStatsF64 st;
+  memset(&st, 0, sizeof(st));
+  const uint64_t base = p->offset_counter ? *p->offset_counter : 0ull;
+  auto coef = [&](int64_t cnt) {
+    return p->range_std_coef_f64 >= 0.0 ? p->range_std_coef_f64 : 1.0 / sqrt(2.0 * log((double)cnt));
+  };
+  const bool range = p->use_range_std_dev != 0;
+  switch (p->stats_source) {
+    case SMQ_STATS_WORKSPACE: {
+      const double shift = median3_f64(x[0], x[n >> 1], x[n - 1]);
+      struct M { double s1, s2, mn, mx; };
+      std::vector<M> part((size_t)((n + kTask - 1) / kTask));
+      parallel_tasks(n, n_threads, [&](int64_t t, int64_t i0, int64_t i1) {
+        double a1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double mn = INFINITY, mx = -INFINITY;
+        for (int64_t i = i0; i < i1; ++i) {
+          const double d = x[i] - shift;
+          a1[(i - i0) & 7] += d;
+          a2[(i - i0) & 7] = fma(d, d, a2[(i - i0) & 7]);
+          mn = fmin(mn, x[i]);
+          mx = fmax(mx, x[i]);
+        }
+        part[(size_t)t] = M{((a1[0] + a1[1]) + (a1[2] + a1[3])) + ((a1[4] + a1[5]) + (a1[6] + a1[7])),
+                            ((a2[0] + a2[1]) + (a2[2] + a2[3])) + ((a2[4] + a2[5]) + (a2[6] + a2[7])),
+                            mn, mx};
+      });
+      M tot{0.0, 0.0, INFINITY, -INFINITY};
+      for (const M& m : part) {
+        tot.s1 += m.s1;
+        tot.s2 += m.s2;
+        tot.mn = fmin(tot.mn, m.mn);
+        tot.mx = fmax(tot.mx, m.mx);
+      }
+      finalize_f64(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, range, p->clamp_lo_f64,
+                   p->clamp_hi_f64, coef(n), &st);
+      break;
+    }
+    case SMQ_STATS_SAMPLED:
+    case SMQ_STATS_SAMPLED_DEVICE: {
+      const bool draw = p->stats_source == SMQ_STATS_SAMPLED_DEVICE;
+      const int64_t k = std::min<int64_t>(p->num_samples, n);
+      const int64_t cap = draw ? SMQ_MAX_DRAW_SAMPLES : SMQ_MAX_SAMPLES;
+      if (k < 1 || k > cap) {
+        set_error("cpu smaq f64: num_samples must be in [1, %lld]", (long long)cap);
+        return SMQ_ERR_INVALID;
+      }
+      const int64_t* idx = p->sample_idx;
+      if (draw) {
+        if (ws_bytes < smq_smaq_workspace_bytes_sampled(n, k)) {
+          set_error("cpu smaq f64: workspace too small for %lld samples", (long long)k);
+          return SMQ_ERR_WORKSPACE;
+        }
+        int64_t* out = reinterpret_cast<int64_t*>(
+            ws + (k > SMQ_MAX_DEVICE_SAMPLES ? SMQ_WS_LARGE_SAMPLES_OFFSET : SMQ_WS_SAMPLES_OFFSET));
+        floyd_draw(p->seed, p->offset + base, n, k, out);
+        idx = out;
+      } else {
+        for (int64_t i = 0; i < k; ++i)
+          if (idx[i] < 0 || idx[i] >= n) {
+            set_error("cpu smaq f64: sample index %lld out of range", (long long)idx[i]);
+            return SMQ_ERR_INVALID;
+          }
+      }
+      double sum = 0.0, mn = INFINITY, mx = -INFINITY;
+      for (int64_t i = 0; i < k; ++i) {
+        const double v = x[idx[i]];
+        sum += v;
+        mn = fmin(mn, v);
+        mx = fmax(mx, v);
+      }
+      const double mean = sum / (double)k;
+      double m2 = 0.0;
+      for (int64_t i = 0; i < k; ++i) {
+        const double d = x[idx[i]] - mean;
+        m2 = fma(d, d, m2);
+      }
+      finalize_f64(0.0, m2, mn, mx, k, mean, true, range, p->clamp_lo_f64, p->clamp_hi_f64, coef(k),
+                   &st);
+      break;
+    }
+    default: {
+      if (!stats_in) {
+        set_error("cpu smaq f64: SMQ_STATS_INJECTED needs stats_in");
+        return SMQ_ERR_INVALID;
+      }
+      st = *stats_in;
+      const double sd = st.raw_std;
+      const double std_dev = (sd == 0.0) ? 1.0 : sd;
+      double sc = std_dev < p->clamp_lo_f64 ? p->clamp_lo_f64 : std_dev;
+      sc = sc > p->clamp_hi_f64 ? p->clamp_hi_f64 : sc;
+      st.std_dev = std_dev;
+      st.std_clamped = sc;
+    }
+  }
+  if (p->offset_counter) *p->offset_counter = base + (uint64_t)n;
+  st.rng_offset = base;
+  const ElemF64 c = elem_f64_consts(st, *p);
+  const uint32_t key = rng_key(p->seed);
+  const uint64_t off = p->offset + base;
+  const double* gam = reinterpret_cast<const double*>(p->bn_gamma);
+  const double* bet = reinterpret_cast<const double*>(p->bn_beta);
+  const int rm = !p->stochastic_rounding ? kRoundTrunc : (uniforms ? kRoundUniform : kRoundHash);
+  const bool bn = p->bn_gamma != nullptr, ap = p->all_positive != 0;
+  std::vector<uint64_t> part((size_t)((n + kTask - 1) / kTask));
+  auto go = [&](auto rm_c, auto bn_c, auto ap_c) {
+    constexpr int RM = decltype(rm_c)::value;
+    constexpr bool BN = decltype(bn_c)::value, AP = decltype(ap_c)::value;
+    parallel_tasks(n, n_threads, [&](int64_t t, int64_t i0, int64_t i1) {
+      uint64_t cnt = 0;
+      for (int64_t i = i0; i < i1; ++i) {
+        double u = 0.0, g = 1.0, b = 0.0;
+        if (RM == kRoundHash) u = (double)(rng_u32(key, off + (uint64_t)i) >> 8);
+        if (RM == kRoundUniform) u = uniforms[i];
+        if (BN) {
+          const int64_t ch = (i / p->bn_inner) % p->bn_channels;
+          g = gam[ch];
+          b = bet[ch];
+        }
+        bool o;
+        y[i] = smaq_elem_f64<RM, BN, AP>(x[i], u, c, o, g, b);
+        cnt += o ? 1u : 0u;
+      }
+      part[(size_t)t] = cnt;
+    });
+  };
+  using H = std::integral_constant<int, kRoundHash>;
+  using U = std::integral_constant<int, kRoundUniform>;
+  using R = std::integral_constant<int, kRoundTrunc>;
+  using Y = std::true_type;
+  using N = std::false_type;
+  if (rm == kRoundHash) {
+    if (bn) { if (ap) go(H(), Y(), Y()); else go(H(), Y(), N()); }
+    else { if (ap) go(H(), N(), Y()); else go(H(), N(), N()); }
+  } else if (rm == kRoundUniform) {
+    if (bn) { if (ap) go(U(), Y(), Y()); else go(U(), Y(), N()); }
+    else { if (ap) go(U(), N(), Y()); else go(U(), N(), N()); }
+  } else {
+    if (bn) { if (ap) go(R(), Y(), Y()); else go(R(), Y(), N()); }
+    else { if (ap) go(R(), N(), Y()); else go(R(), N(), N()); }
+  }
+  uint64_t n_out = 0;
+  for (uint64_t v : part) n_out += v;
+  memcpy(ws, &st, sizeof(st));
+  uint64_t* slots = reinterpret_cast<uint64_t*>(ws + SMQ_WS_OUTLIER_SLOTS_OFFSET);
+  for (int i = 0; i < SMQ_WS_OUTLIER_SLOTS; ++i) slots[i] = 0;
+  if (p->count_outliers) slots[0] = n_out;
+  return SMQ_OK;
+}
+
+static void s2_stats_f64(const double* x, int64_t n, int n_threads, SmqS2fp8StatsF64* o) {
+  struct P {
+    double s, m;
+  };
+  std::vector<P> part((size_t)((n + kTask - 1) / kTask));
+  parallel_tasks(n, n_threads, [&](int64_t t, int64_t i0, int64_t i1) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double mx = -INFINITY;
+    for (int64_t i = i0; i < i1; ++i) {
+      const double l = s2_log_f64(x[i]);
+      a[(i - i0) & 7] += l;
+      mx = nan_max_f64(mx, l);
+    }
+    part[(size_t)t] = P{((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])), mx};
+  });
+  double s = 0.0, m = -INFINITY;
+  for (const P& q : part) {
+    s += q.s;
+    m = nan_max_f64(m, q.m);
+  }
+  s2_derive_f64(s, m, n, o);
+}
 }  // namespace cpu
 }  // namespace smq
 
@@ -638,9 +827,9 @@ int smq_cpu_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const 
     return SMQ_ERR_INVALID;
   }
   char* w = static_cast<char*>(ws);
-  if (dtype == SMQ_DTYPE_F32) return cpu::smaq_roundtrip<kF32>(x, y, n, p, uniforms, stats_in, w, n_threads);
-  if (dtype == SMQ_DTYPE_F16) return cpu::smaq_roundtrip<kF16>(x, y, n, p, uniforms, stats_in, w, n_threads);
-  return cpu::smaq_roundtrip<kBF16>(x, y, n, p, uniforms, stats_in, w, n_threads);
+  if (dtype == SMQ_DTYPE_F32) return cpu::smaq_roundtrip<kF32>(x, y, n, p, uniforms, stats_in, w, ws_bytes, n_threads);
+  if (dtype == SMQ_DTYPE_F16) return cpu::smaq_roundtrip<kF16>(x, y, n, p, uniforms, stats_in, w, ws_bytes, n_threads);
+  return cpu::smaq_roundtrip<kBF16>(x, y, n, p, uniforms, stats_in, w, ws_bytes, n_threads);
 }
 
 int smq_cpu_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t n,
@@ -650,12 +839,15 @@ int smq_cpu_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int
     set_error("cpu float_quant: bad tensor arguments");
     return SMQ_ERR_INVALID;
   }
-  if (dtype_in != SMQ_DTYPE_F32 && dtype_in != SMQ_DTYPE_F16 && dtype_in != SMQ_DTYPE_BF16) {
-    set_error("cpu float_quant: dtype_in must be SMQ_DTYPE_F32, _F16 or _BF16 (got %d)", dtype_in);
+  if (dtype_in != SMQ_DTYPE_F32 && dtype_in != SMQ_DTYPE_F16 && dtype_in != SMQ_DTYPE_BF16 &&
+      dtype_in != SMQ_DTYPE_F64) {
+    set_error("cpu float_quant: dtype_in must be SMQ_DTYPE_F32, _F16, _BF16 or _F64 (got %d)", dtype_in);
     return SMQ_ERR_INVALID;
   }
-  if (dtype_out != SMQ_DTYPE_F32 && dtype_out != SMQ_DTYPE_F16) {
-    set_error("cpu float_quant: dtype_out must be SMQ_DTYPE_F32 or _F16 (got %d)", dtype_out);
+  const bool dout = dtype_in == SMQ_DTYPE_F64 && dtype_out == SMQ_DTYPE_F64;
+  if (!dout && dtype_out != SMQ_DTYPE_F16 && (dtype_out != SMQ_DTYPE_F32 || dtype_in == SMQ_DTYPE_F64)) {
+    set_error("cpu float_quant: dtype_out must be SMQ_DTYPE_F32 or _F16 (_F64 or _F16 for fp64 "
+              "input; got %d)", dtype_out);
     return SMQ_ERR_INVALID;
   }
   if (exp_bits < 2 || exp_bits > 8 || man_bits < 0 || man_bits > 22) {
@@ -673,7 +865,17 @@ int smq_cpu_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int
   const uint32_t key = rng_key(seed);
 #define SMQ_CFQ(T, H) \
   cpu::float_quant_pass<T, H>(x, y, n, exp_bits, man_bits, sr, check_inf, rand_bits, key, offset, mv, n_threads)
-  if (dtype_in == SMQ_DTYPE_F32) { if (hout) SMQ_CFQ(kF32, true); else SMQ_CFQ(kF32, false); }
+  if (dout) {
+    cpu::parallel_tasks(n, n_threads, [&](int64_t, int64_t i0, int64_t i1) {
+      for (int64_t i = i0; i < i1; ++i) {
+        const uint32_t r = !sr ? 0u : (rand_bits ? rand_bits[i] : rng_u32(key, offset + (uint64_t)i));
+        float q = qtorch_quant((float)static_cast<const double*>(x)[i], r, exp_bits, man_bits, sr);
+        if (check_inf && fabsf(q - mv) <= FLT_EPSILON) q = INFINITY;
+        static_cast<double*>(y)[i] = (double)q;
+      }
+    });
+  } else if (dtype_in == SMQ_DTYPE_F64) SMQ_CFQ(SMQ_DTYPE_F64, true);
+  else if (dtype_in == SMQ_DTYPE_F32) { if (hout) SMQ_CFQ(kF32, true); else SMQ_CFQ(kF32, false); }
   else if (dtype_in == SMQ_DTYPE_F16) { if (hout) SMQ_CFQ(kF16, true); else SMQ_CFQ(kF16, false); }
   else { if (hout) SMQ_CFQ(kBF16, true); else SMQ_CFQ(kBF16, false); }
 #undef SMQ_CFQ
@@ -734,6 +936,88 @@ int smq_cpu_s2fp8_roundtrip(const void* x, int dtype, void* y, int64_t n, int pr
     cpu::s2_pass<kF16>(x, y, n, p16, hout, check_inf, rand_bits, key, offset, s, out_mode, n_threads);
   else
     cpu::s2_pass<kBF16>(x, y, n, p16, hout, check_inf, rand_bits, key, offset, s, out_mode, n_threads);
+  if (ws && ws_bytes >= sizeof(s)) memcpy(ws, &s, sizeof(s));
+  return SMQ_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int smq_cpu_smaq_roundtrip_f64(const double* x, double* y, int64_t n, const SmqSmaqParams* p,
+                               const double* uniforms, const SmqSmaqStatsF64* stats_in, void* ws,
+                               size_t ws_bytes, int n_threads) {
+  int rc = smaq_validate(p, SMQ_DTYPE_F32);
+  if (rc) return rc;
+  if (n < 1 || !x || !y) {
+    set_error("cpu smaq f64: n >= 1 and non-NULL x, y required");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->main_std_dev_threshold_f64 == 0.0 || !(p->clamp_hi_f64 > 0.0)) {
+    set_error("cpu smaq f64: params.main_std_dev_threshold_f64 / clamp_*_f64 unset");
+    return SMQ_ERR_INVALID;
+  }
+  if (!ws || ws_bytes < smq_smaq_workspace_bytes(n)) {
+    set_error("cpu smaq f64: workspace too small: need %zu bytes", smq_smaq_workspace_bytes(n));
+    return SMQ_ERR_WORKSPACE;
+  }
+  if (p->bn_gamma && (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1)) {
+    set_error("cpu smaq f64: batch-norm parameters incomplete");
+    return SMQ_ERR_INVALID;
+  }
+  return cpu::smaq_roundtrip_f64(x, y, n, p, uniforms, stats_in, static_cast<char*>(ws), ws_bytes,
+                                 n_threads);
+}
+
+int smq_cpu_s2fp8_roundtrip_f64(const double* x, double* y, int64_t n, int precision,
+                                int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                                uint64_t offset, const SmqS2fp8StatsF64* stats_in, void* ws,
+                                size_t ws_bytes, uint32_t flags, int n_threads) {
+  if (n < 1 || !x || !y) {
+    set_error("cpu s2fp8 f64: n >= 1 and non-NULL x, y required");
+    return SMQ_ERR_INVALID;
+  }
+  if (precision != 16 && precision != 32) {
+    set_error("cpu s2fp8 f64: precision must be 16 or 32 (got %d)", precision);
+    return SMQ_ERR_INVALID;
+  }
+  if (flags & ~(SMQ_S2FP8_OUT_Y | SMQ_S2FP8_OUT_T | SMQ_S2FP8_EXACT_POW | SMQ_S2FP8_SPLIT)) {
+    set_error("cpu s2fp8 f64: unsupported flags 0x%x", flags);
+    return SMQ_ERR_INVALID;
+  }
+  if ((flags & SMQ_S2FP8_OUT_Y) && (flags & SMQ_S2FP8_OUT_T)) {
+    set_error("cpu s2fp8 f64: SMQ_S2FP8_OUT_Y and SMQ_S2FP8_OUT_T are exclusive");
+    return SMQ_ERR_INVALID;
+  }
+  const int out_mode = (flags & SMQ_S2FP8_OUT_Y) ? 1 : ((flags & SMQ_S2FP8_OUT_T) ? 2 : 0);
+  if (out_mode && precision != 32) {
+    set_error("cpu s2fp8 f64: SMQ_S2FP8_OUT_* need precision 32");
+    return SMQ_ERR_INVALID;
+  }
+  SmqS2fp8StatsF64 s;
+  memset(&s, 0, sizeof(s));
+  if (stats_in) {
+    s2_derive_f64(stats_in->mu * (double)n, stats_in->m, n, &s);
+    s.mu = stats_in->mu;
+    const double alpha = (1.0 / (s.m - s.mu)) * 15.0;
+    s.alpha = alpha;
+    s.beta = (-alpha) * s.mu;
+    s.beta_pow2 = pow(2.0, s.beta);
+    s.inv_beta_pow2 = 1.0 / s.beta_pow2;
+    s.inv_alpha = 1.0 / alpha;
+  } else {
+    cpu::s2_stats_f64(x, n, n_threads, &s);
+  }
+  const float mv = qtorch_quant(FLT_MAX, 0u, 5, 2, false);
+  const uint32_t key = rng_key(seed);
+  const bool p16 = precision == 16;
+  cpu::parallel_tasks(n, n_threads, [&](int64_t, int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      const uint32_t r = rand_bits ? rand_bits[i] : rng_u32(key, offset + (uint64_t)i);
+      y[i] = p16 ? s2_elem_f64<true>(x[i], r, s, check_inf, mv, 0)
+                 : s2_elem_f64<false>(x[i], r, s, check_inf, mv, out_mode);
+    }
+  });
   if (ws && ws_bytes >= sizeof(s)) memcpy(ws, &s, sizeof(s));
   return SMQ_OK;
 }

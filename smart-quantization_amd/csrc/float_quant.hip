@@ -21,6 +21,7 @@
 
 #include "qtorch.h"
 #include "smaq_elem.h"
+#include "smaq_host.h"
 #include "smq_common.h"
 
 namespace smq {
@@ -1232,11 +1233,12 @@ int smq_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t
     set_error("float_quant: bad tensor arguments");
     return SMQ_ERR_INVALID;
   }
-  if (dtype_in != SMQ_DTYPE_F32 && dtype_in != SMQ_DTYPE_F16 && dtype_in != SMQ_DTYPE_BF16) {
-    set_error("float_quant: dtype_in must be SMQ_DTYPE_F32, _F16 or _BF16 (got %d)", dtype_in);
+  if (dtype_in != SMQ_DTYPE_F32 && dtype_in != SMQ_DTYPE_F16 && dtype_in != SMQ_DTYPE_BF16 &&
+      dtype_in != SMQ_DTYPE_F64) {
+    set_error("float_quant: dtype_in must be SMQ_DTYPE_F32, _F16, _BF16 or _F64 (got %d)", dtype_in);
     return SMQ_ERR_INVALID;
   }
-  if (dtype_out != SMQ_DTYPE_F32 && dtype_out != SMQ_DTYPE_F16) {
+  if (dtype_in != SMQ_DTYPE_F64 && dtype_out != SMQ_DTYPE_F32 && dtype_out != SMQ_DTYPE_F16) {
     set_error("float_quant: dtype_out must be SMQ_DTYPE_F32 or _F16 (got %d)", dtype_out);
     return SMQ_ERR_INVALID;
   }
@@ -1249,6 +1251,10 @@ int smq_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t
     set_error("float_quant: rounding must be SMQ_ROUND_NEAREST or SMQ_ROUND_STOCHASTIC");
     return SMQ_ERR_INVALID;
   }
+  if (dtype_in == SMQ_DTYPE_F64)  // fp64.hip
+    return float_quant_f64(static_cast<const double*>(x), y, dtype_out, n, exp_bits, man_bits,
+                           rounding, check_inf, rand_bits, seed, offset, offset_counter,
+                           host_max_value(exp_bits, man_bits), (hipStream_t)stream);
   if (n == 0) return SMQ_OK;
   FQArgs A;
   A.x = x;

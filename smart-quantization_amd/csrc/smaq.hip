@@ -21,6 +21,7 @@
 #include <math.h>
 #include <stdarg.h>
 
+#include <algorithm>
 #include <atomic>
 #include <stdio.h>
 #include <stdlib.h>
@@ -28,6 +29,7 @@
 
 #include "smq_common.h"
 #include "smaq_elem.h"
+#include "smaq_host.h"
 
 namespace smq {
 
@@ -473,6 +475,154 @@ __global__ __launch_bounds__(kBlock) void smaq_draw_stats_kernel(DrawArgs A) {
   draw_sample_stats<TIN>(A.x, A.n, A.k, A.key, pos_s, A.use_range, f, A.ws_stats, A.idx_out, L);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Multi-workgroup draw (k > SMQ_MAX_DEVICE_SAMPLES; smart.py:86-91 takes any k = min(n, num_samples)).
+// The same Floyd picks as draw_picks. A step whose candidate t_i no other candidate equals and that
+// lies below n - k keeps t_i: every earlier pick is another candidate or a substitute j_m >= n - k.
+// Only the other steps — "suspects": a candidate repeated among the candidates, or one in
+// [n - k, n) — can be substituted, and their outcome depends on earlier suspects alone (a
+// non-suspect pick never equals a suspect's candidate or any j). So:
+//   draw_candidates (grid): t_i into pick[], and into a hash set that marks repeated keys;
+//   draw_suspects   (grid): a bitmap of the suspect steps (each 32-step word stored once);
+//   draw_resolve    (one wave): the suspects in draw order, 64 at a time — a lookup of each
+//                   candidate among the earlier chunks' final picks (a second hash set), then
+//                   the in-chunk order by readlane / compare — writing the final picks back;
+//   draw_gather     (grid): shifted fp64 sums / extrema of the gathered samples per workgroup;
+//   draw_finalize   (one workgroup): fixed-order total, finalize_stats (biased), the header.
+// Without repeats (k^2 << n) the resolve pass only walks the bitmap.
+// ------------------------------------------------------------------------------------------------
+constexpr unsigned long long kEmptyKey = ~0ull;
+
+__global__ __launch_bounds__(kBlock) void smaq_draw_candidates_kernel(LargeDrawArgs A) {
+  const uint64_t pos = A.offset + (A.rng_ctr ? *A.rng_ctr : 0ull);
+  const uint32_t mask = (1u << A.bits) - 1u;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.k;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t t = floyd_candidate(A.key, pos, A.n, (int)A.k, (int)i);
+    A.pick[i] = t;
+    for (uint32_t s = pick_hash(t, A.bits);; s = (s + 1) & mask) {
+      const unsigned long long prev = atomicCAS(A.hkey + s, kEmptyKey, (unsigned long long)t);
+      if (prev == kEmptyKey) break;
+      if (prev == (unsigned long long)t) {
+        atomicOr(A.hdup + s, 1u);
+        break;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void smaq_draw_suspects_kernel(LargeDrawArgs A) {
+  const uint32_t mask = (1u << A.bits) - 1u;
+  const int64_t span = (A.k + kWave - 1) / kWave * kWave;  // whole waves: every word stored once
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < span;
+       i += (int64_t)gridDim.x * kBlock) {
+    bool sus = false;
+    if (i < A.k) {
+      const int64_t t = A.pick[i];
+      sus = t >= A.n - A.k;
+      if (!sus) {
+        uint32_t s = pick_hash(t, A.bits);
+        while (A.hkey[s] != (unsigned long long)t) s = (s + 1) & mask;
+        sus = A.hdup[s] != 0u;
+      }
+    }
+    const uint64_t b = __ballot(sus);
+    const int lane = threadIdx.x & (kWave - 1);
+    if ((lane & 31) == 0 && i < A.k) A.susp[i >> 5] = (uint32_t)(b >> lane);
+  }
+}
+
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__global__ __launch_bounds__(kWave) void smaq_draw_resolve_kernel(LargeDrawArgs A) {
+  __shared__ int32_t list[kWave * 32];  // suspect steps of one 64-word window of the bitmap
+  const int lane = threadIdx.x;
+  const uint32_t mask = (1u << A.bits) - 1u;
+  const int64_t words = (A.k + 31) / 32, base_j = A.n - A.k;
+  for (int64_t w0 = 0; w0 < words; w0 += kWave) {
+    const int64_t w = w0 + lane;
+    uint32_t b = w < words ? A.susp[w] : 0u;
+    const uint32_t c = (uint32_t)__builtin_popcount(b);
+    const uint32_t incl = wave_incl_scan_u32(c);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    if (total == 0) continue;
+    for (uint32_t o = incl - c; b; b &= b - 1) list[o++] = (int32_t)(w * 32 + __builtin_ctz(b));
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < total; c0 += kWave) {
+      const uint32_t m = c0 + lane;
+      const bool act = m < total;
+      const int64_t i = act ? list[m] : 0;
+      const int64_t t = act ? A.pick[i] : -1;
+      bool dup = false;
+      if (act) {  // among the final picks of earlier chunks (sc1 loads: the L1 may hold old lines)
+        for (uint32_t s = pick_hash(t, A.bits);; s = (s + 1) & mask) {
+          const unsigned long long e = ld_sc1_u64(A.h2key + s);
+          if (e == kEmptyKey) break;
+          if (e == (unsigned long long)t) {
+            dup = true;
+            break;
+          }
+        }
+      }
+      const int cnt = (int)min((uint32_t)kWave, total - c0);
+      int64_t p = t;
+      for (int l = 0; l < cnt; ++l) {  // step l is final once the earlier lanes' picks are known
+        if (lane == l && dup) p = base_j + i;
+        const int64_t pl = readlane_i64(p, l);
+        if (lane > l && t == pl) dup = true;
+      }
+      if (act) {
+        A.pick[i] = p;
+        for (uint32_t s = pick_hash(p, A.bits);; s = (s + 1) & mask)
+          if (atomicCAS(A.h2key + s, kEmptyKey, (unsigned long long)p) == kEmptyKey) break;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int TIN, bool RANGE>
+__global__ __launch_bounds__(kBlock) void smaq_draw_gather_kernel(LargeDrawArgs A) {
+  const double shift = (double)load1<TIN>(A.x, A.pick[0]);  // step 0 is never substituted
+  StatAcc acc;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.k;
+       i += (int64_t)gridDim.x * kBlock)
+    acc.add<RANGE>(load1<TIN>(A.x, A.pick[i]), shift);
+  block_reduce_stats<RANGE>(acc);
+  if (threadIdx.x == 0) {
+    StatPartial& q = A.parts[blockIdx.x];
+    q.s1 = acc.s1;
+    q.s2 = acc.s2;
+    q.mn = acc.mn;
+    q.mx = acc.mx;
+  }
+}
+
+template <int TIN, bool RANGE>
+__global__ __launch_bounds__(kBlock) void smaq_draw_finalize_kernel(LargeDrawArgs A, int g) {
+  StatAcc acc;
+  for (int b = threadIdx.x; b < g; b += kBlock) {  // per-thread partials in a fixed order
+    const StatPartial& q = A.parts[b];
+    acc.s1 += q.s1;
+    acc.s2 += q.s2;
+    acc.mn = fminf(acc.mn, q.mn);
+    acc.mx = fmaxf(acc.mx, q.mx);
+  }
+  block_reduce_stats<RANGE>(acc);
+  if (threadIdx.x == 0) {
+    const double shift = (double)load1<TIN>(A.x, A.pick[0]);
+    // the finaliser snapshots the graph-safe position and advances it by n
+    const FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, A.rng_ctr, A.n};
+    SmqSmaqStats st;
+    finalize_stats<RANGE, TIN>(acc.s1, acc.s2, acc.mn, acc.mx, A.k, shift, true, f, &st);
+    *A.ws_stats = st;
+  }
+}
+
 // Injected statistics (parity tests, callers with their own mean/std): copy the record into the
 // workspace header with the fp64 reciprocal the element transform reads.
 __global__ void smaq_prep_injected_kernel(const SmqSmaqStats* in, SmqSmaqStats* out,
@@ -480,6 +630,7 @@ __global__ void smaq_prep_injected_kernel(const SmqSmaqStats* in, SmqSmaqStats* 
   if (threadIdx.x == 0) {
     SmqSmaqStats s = *in;
     s.inv_std_clamped = 1.0 / (double)s.std_clamped;
+    s.inv_std_clamped_f32 = (float)s.inv_std_clamped;
     s.quot_check = quot_check_for(s.std_clamped);
     s.rng_offset = 0ull;
     if (rng_ctr) {
@@ -804,19 +955,89 @@ static void launch_sample_stats(const ApplyArgs& A, int dtype, hipStream_t st) {
     hipLaunchKernelGGL(smaq_sample_stats_kernel<kBF16>, dim3(1), dim3(kWave), 0, st, A);
 }
 
+// Host side of the multi-workgroup draw: checks, memsets of the two hash sets, the three draw
+// launches. Fills *A (x, statistics fields and ws_stats are the caller's).
+int launch_large_draw(int64_t n, int64_t k, const SmqSmaqParams* p, void* ws, size_t ws_bytes,
+                      hipStream_t st, LargeDrawArgs* A, int* grid) {
+  const LargeDrawLayout L(k);
+  const size_t need = SMQ_WS_LARGE_SAMPLES_OFFSET + L.total;
+  if (!ws || ws_bytes < need) {
+    set_error("workspace too small for %lld device-drawn samples: need %zu bytes "
+              "(smq_smaq_workspace_bytes_sampled), got %zu", (long long)k, need, ws_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  char* r = (char*)ws + SMQ_WS_LARGE_SAMPLES_OFFSET;
+  memset(A, 0, sizeof(*A));
+  A->n = n;
+  A->k = k;
+  A->key = rng_key(p->seed ^ kDrawSalt);
+  A->offset = p->offset;
+  A->rng_ctr = (unsigned long long*)p->offset_counter;
+  A->bits = L.bits;
+  A->pick = (int64_t*)(r + L.pick);
+  A->hkey = (unsigned long long*)(r + L.hkey);
+  A->hdup = (uint32_t*)(r + L.hdup);
+  A->h2key = (unsigned long long*)(r + L.h2key);
+  A->susp = (uint32_t*)(r + L.susp);
+  A->parts = (StatPartial*)(r + L.parts);
+  const size_t slots = (size_t)1 << L.bits;
+  if (hipMemsetAsync(A->hkey, 0xff, 8 * slots, st) != hipSuccess ||
+      hipMemsetAsync(A->hdup, 0, 4 * slots, st) != hipSuccess ||
+      hipMemsetAsync(A->h2key, 0xff, 8 * slots, st) != hipSuccess) {
+    set_error("hipMemsetAsync of the draw's hash sets failed");
+    return SMQ_ERR_LAUNCH;
+  }
+  const int g = (int)std::min<int64_t>(kDrawGridCap, (k + 4 * kBlock - 1) / (4 * kBlock));
+  hipLaunchKernelGGL(smaq_draw_candidates_kernel, dim3(g), dim3(kBlock), 0, st, *A);
+  hipLaunchKernelGGL(smaq_draw_suspects_kernel, dim3(g), dim3(kBlock), 0, st, *A);
+  hipLaunchKernelGGL(smaq_draw_resolve_kernel, dim3(1), dim3(kWave), 0, st, *A);
+  *grid = g;
+  return check_launch("smaq_draw_resolve_kernel");
+}
+
+size_t large_draw_ws_bytes(int64_t k) {
+  return SMQ_WS_LARGE_SAMPLES_OFFSET + LargeDrawLayout(k).total;
+}
+
+static int launch_draw_stats_large(const void* x, int dtype, int64_t n, int64_t k,
+                                   const SmqSmaqParams* p, void* ws, size_t ws_bytes,
+                                   hipStream_t st) {
+  LargeDrawArgs A;
+  int g = 0;
+  const int rc = launch_large_draw(n, k, p, ws, ws_bytes, st, &A, &g);
+  if (rc) return rc;
+  A.x = x;
+  A.clamp_lo = p->clamp_lo;
+  A.clamp_hi = p->clamp_hi;
+  A.range_coef = range_coef_for(p, k);
+  A.ws_stats = (SmqSmaqStats*)ws;
+#define SMQ_DRAW_STATS(TIN, RANGE)                                                                  \
+  do {                                                                                            \
+    hipLaunchKernelGGL((smaq_draw_gather_kernel<TIN, RANGE>), dim3(g), dim3(kBlock), 0, st, A);    \
+    hipLaunchKernelGGL((smaq_draw_finalize_kernel<TIN, RANGE>), dim3(1), dim3(kBlock), 0, st, A, g); \
+  } while (0)
+  const bool rg = p->use_range_std_dev != 0;
+  if (dtype == SMQ_DTYPE_F32) { if (rg) SMQ_DRAW_STATS(kF32, true); else SMQ_DRAW_STATS(kF32, false); }
+  else if (dtype == SMQ_DTYPE_F16) { if (rg) SMQ_DRAW_STATS(kF16, true); else SMQ_DRAW_STATS(kF16, false); }
+  else { if (rg) SMQ_DRAW_STATS(kBF16, true); else SMQ_DRAW_STATS(kBF16, false); }
+#undef SMQ_DRAW_STATS
+  return check_launch("smaq_draw_finalize_kernel");
+}
+
 static int launch_draw_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p,
                              void* ws, size_t ws_bytes, hipStream_t st) {
+  const int64_t k = p->num_samples < n ? p->num_samples : n;
+  if (k < 1 || k > SMQ_MAX_DRAW_SAMPLES) {
+    set_error("device-drawn sampled stats need 1 <= k <= %d, got %lld", SMQ_MAX_DRAW_SAMPLES,
+              (long long)k);
+    return SMQ_ERR_INVALID;
+  }
+  if (k > SMQ_MAX_DEVICE_SAMPLES) return launch_draw_stats_large(x, dtype, n, k, p, ws, ws_bytes, st);
   const size_t need = SMQ_WS_SAMPLES_OFFSET + 8 * (size_t)SMQ_MAX_DEVICE_SAMPLES;
   if (!ws || ws_bytes < need) {
     set_error("workspace too small for device-drawn samples: need %zu bytes, got %zu", need,
               ws_bytes);
     return SMQ_ERR_WORKSPACE;
-  }
-  const int64_t k = p->num_samples < n ? p->num_samples : n;
-  if (k < 1 || k > SMQ_MAX_DEVICE_SAMPLES) {
-    set_error("device-drawn sampled stats need 1 <= k <= %d, got %lld", SMQ_MAX_DEVICE_SAMPLES,
-              (long long)k);
-    return SMQ_ERR_INVALID;
   }
   DrawArgs D;
   D.x = x;
@@ -1042,6 +1263,10 @@ int smq_smaq_params_set(SmqSmaqParams* p, int num_bits_main, int num_bits_outlie
   p->range_main = (float)((pow(2.0, num_bits_main - 2) - 1.0) / main_thr);
   p->clamp_lo = precision == 16 ? 1e-4f : 1e-38f;
   p->clamp_hi = precision == 16 ? 1e4f : 1e38f;
+  p->main_std_dev_threshold_f64 = main_thr;
+  p->clamp_lo_f64 = precision == 16 ? 1e-4 : 1e-38;
+  p->clamp_hi_f64 = precision == 16 ? 1e4 : 1e38;
+  p->range_std_coef_f64 = -1.0;
   return SMQ_OK;
 }
 
@@ -1071,6 +1296,15 @@ int smq_smaq_draw_samples(SmqSmaqParams* p, int64_t n, int num_samples) {
 }
 
 size_t smq_smaq_workspace_bytes(int64_t n) { return stats_ws_bytes(n); }
+
+size_t smq_smaq_workspace_bytes_sampled(int64_t n, int64_t num_samples) {
+  static_assert(SMQ_WS_LARGE_SAMPLES_OFFSET >= SmaqWsLayout::kTagCounters + 8 * SmaqWsLayout::kTagWords,
+                "smq.h SMQ_WS_LARGE_SAMPLES_OFFSET overlaps the fixed layout");
+  const int64_t k = num_samples < n ? num_samples : n;
+  if (k <= SMQ_MAX_DEVICE_SAMPLES) return stats_ws_bytes(n);
+  if (k > SMQ_MAX_DRAW_SAMPLES) return 0;
+  return large_draw_ws_bytes(k);
+}
 
 int smq_smaq_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
                    size_t ws_bytes, void* stream) {

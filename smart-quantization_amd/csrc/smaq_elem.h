@@ -175,6 +175,7 @@ __device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, f
   out->n_used = (uint32_t)(n > 0xffffffffLL ? 0xffffffffu : (uint32_t)n);
   out->n_outlier = 0ull;
   out->inv_std_clamped = 1.0 / (double)sc;  // once per call, for the element transform
+  out->inv_std_clamped_f32 = (float)out->inv_std_clamped;  // half inputs: half_quot
   out->quot_check = quot_check_for(sc);
   // graph-safe random stream: snapshot the position for this call's element kernels, advance it
   unsigned long long base = 0ull;
@@ -195,6 +196,7 @@ struct ElemConsts {
   float zh, zl;           // 0 * -T_m, 0 * T_m  (the bool*float zero terms, smart.py:159-161)
   float r_main, r_out;    // ranges
   double inv_sc;          // RN64(1 / sc): written by the statistics finaliser
+  float inv_sc32;         // RN32(1 / sc): half inputs (half_quot)
   double inv_r_main, inv_r_out;  // RN64(1 / range): computed on the host
   uint64_t rng_off;       // the call's graph-safe stream position (SmqSmaqStats.rng_offset)
 };
@@ -219,6 +221,7 @@ __device__ __forceinline__ void init_consts(ElemConsts& c, const SmqSmaqStats* s
   c.sd = st->std_dev;
   c.sc = st->std_clamped;
   c.inv_sc = st->inv_std_clamped;
+  c.inv_sc32 = st->inv_std_clamped_f32;
   c.thr = thr;
   c.nthr = -thr;
   c.cthr = cthr;
@@ -282,6 +285,24 @@ struct BnTerm {
   float gamma, beta;
 };
 
+// Half-type z-score quotient RN_T(dm / sc) for fp16 / bf16 dm and sc as RN_T(RN32(dm * RN32(1/sc))):
+// one fp32 multiply instead of the fp64 reciprocal product. Verified exhaustively over every pair of
+// half values with a finite fp32 reciprocal (oracle/csrc/half_div_check.c: 1.7e9 fp16 and 2.0e9 bf16
+// pairs, 0 mismatches) for products at or above the type's smallest normal (2^-14 fp16, 2^-126
+// bf16). Below it exact midpoints of the coarse subnormal grid occur (fp16: 2,990 pairs), so those
+// quotients (and zeros, which the test cannot tell apart cheaply) take the fp64 path.
+template <int T>
+__device__ __forceinline__ float half_quot(float dm, const ElemConsts& c) {
+  const float p = dm * c.inv_sc32;
+  const float lim = T == kF16 ? 0x1p-14f : 0x1p-126f;
+  if (__builtin_expect(fabsf(p) < lim, 0)) {
+    float z = div_by_const(dm, c.inv_sc);
+    if (__builtin_amdgcn_classf(z, 0x90)) z = dm / c.sc;
+    return z;
+  }
+  return p;
+}
+
 // Template flags: AP all_positive; SUB keep the subnormal-quotient check (quot_check_for); SQ
 // divide q / range by IEEE division (RangeRecips::safe_q).
 
@@ -292,10 +313,15 @@ __device__ __forceinline__ float smaq_quant(float v, float u, const ElemConsts& 
   constexpr int TZ = BN ? kF32 : T;  // fp32 BN parameters promote the data to fp32
   if (BN) v = (v - bn.beta) / bn.gamma;                 // (data - beta) / gamma
   const float dm = round_in<TZ>(v - c.mean);            // data - mean
-  float z = div_by_const(dm, c.inv_sc);                 // / std.clamp(...)
-  // subnormal quotient (class mask 0x90 = -/+ denormal, one v_cmp_class_f32): IEEE division.
-  // (classf: the unsuffixed builtin takes a double, where a promoted float is never subnormal.)
-  if (SUB && __builtin_expect(__builtin_amdgcn_classf(z, 0x90), 0)) z = dm / c.sc;
+  float z;                                              // / std.clamp(...)
+  if (TZ != kF32) {
+    z = half_quot<TZ>(dm, c);
+  } else {
+    z = div_by_const(dm, c.inv_sc);
+    // subnormal quotient (class mask 0x90 = -/+ denormal, one v_cmp_class_f32): IEEE division.
+    // (classf: the unsuffixed builtin takes a double, where a promoted float is never subnormal.)
+    if (SUB && __builtin_expect(__builtin_amdgcn_classf(z, 0x90), 0)) z = dm / c.sc;
+  }
   z = round_in<TZ>(z);
   hi = z > c.cthr;                                      // is_outlier_higher
   lo = z < c.cnthr;                                     // is_outlier_lower
@@ -378,13 +404,9 @@ struct DrawLds {
   double shs[kBlock / kWave];
 };
 
-// The k distinct indices of draw position `pos` (Floyd) and the mean / biased std (or range-std)
-// of the gathered elements into *out, by one 256-thread workgroup (every thread calls it).
-// idx_out (optional) receives the indices in draw order.
-template <int TIN>
-__device__ void draw_sample_stats(const void* x, int64_t n, int k, uint32_t key, uint64_t pos,
-                                  int use_range, const FinalizeArgs& f, SmqSmaqStats* out,
-                                  int64_t* idx_out, DrawLds& L) {
+// Floyd's k distinct indices of draw position `pos` into L.pick (draw order), by one 256-thread
+// workgroup (every thread calls it; the picks are complete after the trailing barrier).
+static __device__ void draw_picks(int64_t n, int k, uint32_t key, uint64_t pos, DrawLds& L) {
   int64_t* pick = L.pick;
   uint16_t* table = L.table;
   for (int i = threadIdx.x; i < k; i += kBlock) pick[i] = floyd_candidate(key, pos, n, k, i);
@@ -427,6 +449,17 @@ __device__ void draw_sample_stats(const void* x, int64_t n, int k, uint32_t key,
     }
   }
   __syncthreads();
+}
+
+// The k distinct indices of draw position `pos` (Floyd) and the mean / biased std (or range-std)
+// of the gathered elements into *out, by one 256-thread workgroup (every thread calls it).
+// idx_out (optional) receives the indices in draw order.
+template <int TIN>
+__device__ void draw_sample_stats(const void* x, int64_t n, int k, uint32_t key, uint64_t pos,
+                                  int use_range, const FinalizeArgs& f, SmqSmaqStats* out,
+                                  int64_t* idx_out, DrawLds& L) {
+  const int64_t* pick = L.pick;
+  draw_picks(n, k, key, pos, L);
   // gather: thread t owns samples t, t + kBlock, ... (<= 16); fp64 sums in one fixed order
   constexpr int kPer = SMQ_MAX_DEVICE_SAMPLES / kBlock;
   float v[kPer];
@@ -476,5 +509,42 @@ __device__ void draw_sample_stats(const void* x, int64_t n, int k, uint32_t key,
     *out = st;
   }
 }
+
+// Workspace region and launch arguments of the multi-workgroup draw (smaq.hip).
+constexpr int kDrawGridCap = 1024;
+
+struct LargeDrawLayout {  // byte offsets from SMQ_WS_LARGE_SAMPLES_OFFSET
+  int bits = 1;
+  size_t pick = 0, hkey = 0, hdup = 0, h2key = 0, susp = 0, parts = 0, total = 0;
+  explicit LargeDrawLayout(int64_t k) {
+    while ((int64_t)1 << bits < 2 * k) ++bits;
+    const size_t slots = (size_t)1 << bits;
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    pick = 0;
+    hkey = up(pick + 8 * (size_t)k);
+    hdup = up(hkey + 8 * slots);
+    h2key = up(hdup + 4 * slots);
+    susp = up(h2key + 8 * slots);
+    parts = up(susp + 4 * (size_t)((k + 31) / 32));
+    total = up(parts + sizeof(StatPartial) * kDrawGridCap);
+  }
+};
+
+struct LargeDrawArgs {
+  const void* x;
+  int64_t n, k;
+  uint32_t key;                   // rng_key(seed ^ kDrawSalt)
+  uint64_t offset;                // params.offset
+  unsigned long long* rng_ctr;    // params.offset_counter or NULL
+  int bits;
+  int64_t* pick;
+  unsigned long long* hkey;       // candidate set (all ones = empty)
+  uint32_t* hdup;                 // 1: the slot's key occurs more than once among the candidates
+  unsigned long long* h2key;      // final picks of resolved suspects (all ones = empty)
+  uint32_t* susp;                 // suspect bitmap, bit i % 32 of word i / 32
+  StatPartial* parts;
+  float clamp_lo, clamp_hi, range_coef;
+  SmqSmaqStats* ws_stats;
+};
 
 }  // namespace smq

@@ -12,6 +12,17 @@ int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, v
                   size_t ws_bytes, hipStream_t st);
 // Workspace bytes prepare_stats needs for n elements.
 size_t smaq_stats_ws_bytes(int64_t n);
+// The multi-workgroup Floyd draw of k > SMQ_MAX_DEVICE_SAMPLES indices (smaq.hip): memsets and the
+// candidate / suspect / resolve launches on st; the picks are in A->pick (draw order) after them.
+// *grid = the grid the gather of the samples should use (A->parts has room for it).
+struct LargeDrawArgs;
+int launch_large_draw(int64_t n, int64_t k, const SmqSmaqParams* p, void* ws, size_t ws_bytes,
+                      hipStream_t st, LargeDrawArgs* A, int* grid);
+size_t large_draw_ws_bytes(int64_t k);
+// smq_float_quant of fp64 data (fp64.hip): arguments validated by the caller.
+int float_quant_f64(const double* x, void* y, int dtype_out, int64_t n, int exp_bits, int man_bits,
+                    int rounding, int check_inf, const uint32_t* rand_bits, uint64_t seed,
+                    uint64_t offset, uint64_t* offset_counter, float max_value, hipStream_t st);
 // Parameter block + dtype validation (sets the thread's last error).
 int smaq_validate(const SmqSmaqParams* p, int dtype);
 

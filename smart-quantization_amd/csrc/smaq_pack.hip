@@ -990,7 +990,13 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
     return SMQ_ERR_WORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
-  rc = prepare_stats(x, dtype, n, p, ws, ws_bytes, st);
+  // the statistics own only the first region (no room for a multi-workgroup sample draw)
+  if (p->stats_source == SMQ_STATS_SAMPLED_DEVICE &&
+      (p->num_samples < n ? p->num_samples : n) > SMQ_MAX_DEVICE_SAMPLES) {
+    set_error("compress: device-drawn samples are limited to %d here", SMQ_MAX_DEVICE_SAMPLES);
+    return SMQ_ERR_INVALID;
+  }
+  rc = prepare_stats(x, dtype, n, p, ws, L.meta, st);
   if (rc) return rc;
   char* wb = (char*)ws;
   PackArgs A;

@@ -19,9 +19,11 @@ LIB_PATH = os.environ.get(
     "SMQ_LIB", os.path.join(os.path.dirname(_PKG_DIR), "lib", "libsmq.so")
 )
 
-SMQ_ABI_VERSION = 3
+SMQ_ABI_VERSION = 4
 SMQ_MAX_SAMPLES = 64
 SMQ_MAX_DEVICE_SAMPLES = 4096
+SMQ_MAX_DRAW_SAMPLES = 1 << 28
+SMQ_WS_LARGE_SAMPLES_OFFSET = 99584
 SMQ_WS_OUTLIER_SLOTS_OFFSET = 128
 SMQ_WS_OUTLIER_SLOTS = 64
 SMQ_WS_SAMPLES_OFFSET = 66176
@@ -39,6 +41,7 @@ SMQ_PACK_SINGLE = 2
 SMQ_DTYPE_F32 = 0
 SMQ_DTYPE_F16 = 1
 SMQ_DTYPE_BF16 = 2
+SMQ_DTYPE_F64 = 3
 SMQ_ROUND_NEAREST = 0
 SMQ_ROUND_STOCHASTIC = 1
 
@@ -67,6 +70,10 @@ class SmqSmaqParams(ctypes.Structure):
         ("bn_inner", ctypes.c_int64),
         ("sample_idx", ctypes.c_int64 * SMQ_MAX_SAMPLES),
         ("offset_counter", ctypes.c_void_p),
+        ("main_std_dev_threshold_f64", ctypes.c_double),
+        ("clamp_lo_f64", ctypes.c_double),
+        ("clamp_hi_f64", ctypes.c_double),
+        ("range_std_coef_f64", ctypes.c_double),
     ]
 
 
@@ -83,7 +90,8 @@ class SmqSmaqStats(ctypes.Structure):
         ("n_outlier", ctypes.c_ulonglong),
         ("inv_std_clamped", ctypes.c_double),
         ("rng_offset", ctypes.c_ulonglong),
-        ("reserved", ctypes.c_uint32 * 2),
+        ("inv_std_clamped_f32", ctypes.c_float),
+        ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -141,7 +149,40 @@ class SmqS2fp8Stats(ctypes.Structure):
     ]
 
 
+class SmqSmaqStatsF64(ctypes.Structure):
+    _fields_ = [
+        ("mean", ctypes.c_double),
+        ("std_dev", ctypes.c_double),
+        ("std_clamped", ctypes.c_double),
+        ("raw_std", ctypes.c_double),
+        ("min_val", ctypes.c_double),
+        ("max_val", ctypes.c_double),
+        ("n_used", ctypes.c_uint32),
+        ("reserved0", ctypes.c_uint32),
+        ("rng_offset", ctypes.c_ulonglong),
+        ("reserved", ctypes.c_ulonglong * 2),
+    ]
+
+
+class SmqS2fp8StatsF64(ctypes.Structure):
+    _fields_ = [
+        ("mu", ctypes.c_double),
+        ("m", ctypes.c_double),
+        ("alpha", ctypes.c_double),
+        ("beta", ctypes.c_double),
+        ("beta_pow2", ctypes.c_double),
+        ("inv_beta_pow2", ctypes.c_double),
+        ("inv_alpha", ctypes.c_double),
+        ("n_used", ctypes.c_uint32),
+        ("reserved0", ctypes.c_uint32),
+        ("rng_offset", ctypes.c_uint64),
+        ("reserved", ctypes.c_uint64 * 3),
+    ]
+
+
 assert ctypes.sizeof(SmqSmaqStats) == 64
+assert ctypes.sizeof(SmqSmaqStatsF64) == 80
+assert ctypes.sizeof(SmqS2fp8StatsF64) == 96
 assert ctypes.sizeof(SmqTensorDesc) == 40
 assert ctypes.sizeof(SmqS2fp8Stats) == 64
 
@@ -163,6 +204,7 @@ SIGNATURES = {
     ),
     "smq_smaq_draw_samples": (_I32, [ctypes.POINTER(SmqSmaqParams), _I64, _I32]),
     "smq_smaq_workspace_bytes": (_SZ, [_I64]),
+    "smq_smaq_workspace_bytes_sampled": (_SZ, [_I64, _I64]),
     "smq_smaq_stats_f32": (_I32, [_P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P]),
     "smq_smaq_apply_f32": (
         _I32,
@@ -229,6 +271,22 @@ SIGNATURES = {
     "smq_cpu_s2fp8_roundtrip": (
         _I32,
         [_P, _I32, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _SZ, _U32, _I32],
+    ),
+    "smq_smaq_roundtrip_f64": (
+        _I32,
+        [_P, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _P, _SZ, _P],
+    ),
+    "smq_cpu_smaq_roundtrip_f64": (
+        _I32,
+        [_P, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _P, _SZ, _I32],
+    ),
+    "smq_s2fp8_roundtrip_f64": (
+        _I32,
+        [_P, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _P, _SZ, _U32, _P],
+    ),
+    "smq_cpu_s2fp8_roundtrip_f64": (
+        _I32,
+        [_P, _P, _I64, _I32, _I32, _P, _U64, _U64, _P, _P, _SZ, _U32, _I32],
     ),
 }
 

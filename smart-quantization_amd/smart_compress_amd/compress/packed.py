@@ -80,6 +80,9 @@ class SmartFPPacked(SmartFP):
             raise NotImplementedError("SmartFPPacked: the BatchNorm variant is not supported")
         if not hp.main_std_dev_threshold > 0:
             raise NotImplementedError("SmartFPPacked: needs main_std_dev_threshold > 0")
+        if hp.use_sample_stats and min(numel, hp.num_samples) > N.SMQ_MAX_DEVICE_SAMPLES:
+            raise NotImplementedError(
+                f"SmartFPPacked: --num_samples above {N.SMQ_MAX_DEVICE_SAMPLES} is not supported")
         N.require_device(data, "SmartFPPacked")
         code = N.DTYPE_CODES.get(data.dtype)
         if code is None:

@@ -51,10 +51,13 @@ class S2FP8(CompressionAlgorithmBase):
         self.log_ratio(tag, tensor.numel(), 32, 8, overhead=64)
         precision = 16 if hp.precision == 16 else 32
         N.require_supported(tensor, "S2FP8")
+        if tensor.dtype == torch.float64:
+            return self._call_f64(tensor, precision)
         if precision == 32:
             if tensor.dtype != torch.float32:
                 raise NotImplementedError(
-                    f"S2FP8: dtype {tensor.dtype} at precision 32 is not supported (float32 only)")
+                    f"S2FP8: dtype {tensor.dtype} at precision 32 is not supported "
+                    "(float32/float64)")
             out_dtype = torch.float32
         else:
             if tensor.dtype not in (torch.float32, torch.float16, torch.bfloat16):
@@ -88,3 +91,30 @@ class S2FP8(CompressionAlgorithmBase):
             N.check(rc, "smq_s2fp8_roundtrip")
         return y
 
+
+    def _call_f64(self, tensor: torch.Tensor, precision: int) -> torch.Tensor:
+        """float64 data: s2fp8.py:27-48 in fp64 (smq_s2fp8_roundtrip_f64 / its host twin), output
+        float64 (the fp64 signs promote the precision-16 half inverse back to fp64)."""
+        hp = self.hparams
+        x = tensor.contiguous()
+        y = torch.empty_like(x, dtype=torch.float64)
+        n = x.numel()
+        if n == 0:
+            return y
+        lib = N.lib()
+        inf = 1 if hp.float_quantize_check_inf else 0
+        if N.on_cpu(x):
+            seed, offset = _q.quant_rng().take(n)
+            ws = N.cpu_workspace("s2fp8", lib.smq_s2fp8_workspace_bytes(n))
+            N.check(lib.smq_cpu_s2fp8_roundtrip_f64(
+                x.data_ptr(), y.data_ptr(), n, precision, inf, None, seed, offset, None,
+                ws.data_ptr(), ws.numel(), 0, N.cpu_threads()), "smq_cpu_s2fp8_roundtrip_f64")
+            return y
+        dev = x.device
+        st = N.stream_ptr(dev)
+        ws = N.workspace("s2fp8", dev, lib.smq_s2fp8_workspace_bytes(n), st)
+        seed, offset, ctr = _q.rng_stream(n, dev)
+        N.check(lib.smq_s2fp8_roundtrip_f64(
+            x.data_ptr(), y.data_ptr(), n, precision, inf, None, seed, offset, ctr, None,
+            ws.data_ptr(), ws.numel(), 0, st), "smq_s2fp8_roundtrip_f64")
+        return y

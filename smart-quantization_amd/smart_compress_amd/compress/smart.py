@@ -131,6 +131,11 @@ class SmartFP(CompressionAlgorithmBase):
         p.range_outlier = float(np.float32(self.range_outlier))
         p.clamp_lo = float(np.float32(self.clamped_range[0]))
         p.clamp_hi = float(np.float32(self.clamped_range[1]))
+        # fp64 data: the Python doubles themselves (smart.py:82-84, 154-156)
+        p.main_std_dev_threshold_f64 = float(hp.main_std_dev_threshold)
+        p.clamp_lo_f64 = float(self.clamped_range[0])
+        p.clamp_hi_f64 = float(self.clamped_range[1])
+        p.range_std_coef_f64 = -1.0
         p.stochastic_rounding = 1 if hp.stochastic_rounding else 0
         p.all_positive = 1 if all_positive else 0
         p.use_range_std_dev = 1 if hp.use_range_std_dev else 0
@@ -145,19 +150,26 @@ class SmartFP(CompressionAlgorithmBase):
             # smart.py:86-91: k indices drawn on the device (Floyd) from this call's stream
             # position, so eager calls and graph replays alike see a fresh set (smart.py:88)
             k = min(numel, hp.num_samples)
-            if k > N.SMQ_MAX_DEVICE_SAMPLES:
+            if k > N.SMQ_MAX_DRAW_SAMPLES:
                 raise NotImplementedError(
-                    f"--num_samples {hp.num_samples} > {N.SMQ_MAX_DEVICE_SAMPLES} is not supported"
+                    f"--num_samples {hp.num_samples} > {N.SMQ_MAX_DRAW_SAMPLES} is not supported"
                 )
             p.stats_source = N.SMQ_STATS_SAMPLED_DEVICE
             p.num_samples = k
             if hp.use_range_std_dev:
-                p.range_std_coef = range_std_coef(k, dtype)
+                self._set_range_coef(p, k, dtype)
         else:
             p.stats_source = N.SMQ_STATS_WORKSPACE
             if hp.use_range_std_dev:
-                p.range_std_coef = range_std_coef(numel, dtype)
+                self._set_range_coef(p, numel, dtype)
         return p
+
+    @staticmethod
+    def _set_range_coef(p, count: int, dtype: torch.dtype):
+        if dtype == torch.float64:
+            p.range_std_coef_f64 = range_std_coef(count, torch.float64)
+        else:
+            p.range_std_coef = range_std_coef(count, dtype)
 
     def _bind_batch_norm(self, p, data: torch.Tensor, bn: Tuple[torch.Tensor, torch.Tensor]):
         """smart.py:136-149: per-channel (x - beta) / gamma on dim 1 of NCHW."""
@@ -166,8 +178,10 @@ class SmartFP(CompressionAlgorithmBase):
         gamma, beta = bn
         if self.hparams.bn_scalar_params:
             gamma, beta = gamma.mean(), beta.mean()
-        gamma = gamma.detach().to(device=data.device, dtype=torch.float32).contiguous().reshape(-1)
-        beta = beta.detach().to(device=data.device, dtype=torch.float32).contiguous().reshape(-1)
+        # fp32 parameters (fp64 for fp64 data: the promoted (x - beta) / gamma of smart.py:146)
+        pdt = torch.float64 if data.dtype == torch.float64 else torch.float32
+        gamma = gamma.detach().to(device=data.device, dtype=pdt).contiguous().reshape(-1)
+        beta = beta.detach().to(device=data.device, dtype=pdt).contiguous().reshape(-1)
         channels = gamma.numel()
         if channels != beta.numel() or channels not in (1, data.shape[1]):
             raise RuntimeError(
@@ -198,10 +212,13 @@ class SmartFP(CompressionAlgorithmBase):
                 return data
 
             N.require_supported(data, "SmartFP")
+            if data.dtype == torch.float64:
+                return self._call_f64(data, tag, numel, all_positive, batch_norm_stats)
             code = N.DTYPE_CODES.get(data.dtype)
             if code is None:
                 raise NotImplementedError(
-                    f"SmartFP: dtype {data.dtype} is not supported (float32/float16/bfloat16)")
+                    f"SmartFP: dtype {data.dtype} is not supported "
+                    "(float32/float16/bfloat16/float64)")
             if data.dtype == torch.float16 and hp.precision != 16:
                 # the reference's std.clamp(1e-38, 1e38) on a half tensor (smart.py:154)
                 raise RuntimeError("value cannot be converted to type c10::Half without overflow")
@@ -218,7 +235,7 @@ class SmartFP(CompressionAlgorithmBase):
             if hp.use_batch_norm and batch_norm_stats is not None:
                 keep = self._bind_batch_norm(p, x, batch_norm_stats)
             st = N.stream_ptr(x.device)
-            ws = N.workspace("smaq", x.device, N.lib().smq_smaq_workspace_bytes(numel), st)
+            ws = N.workspace("smaq", x.device, self.workspace_bytes(numel), st)
             self._launch(x, y, numel, p, ws, code, st)
             del keep
 
@@ -240,7 +257,7 @@ class SmartFP(CompressionAlgorithmBase):
         if hp.use_batch_norm and batch_norm_stats is not None:
             keep = self._bind_batch_norm(p, x, batch_norm_stats)
         lib = N.lib()
-        ws = N.cpu_workspace("smaq", lib.smq_smaq_workspace_bytes(numel))
+        ws = N.cpu_workspace("smaq", self.workspace_bytes(numel))
         N.check(lib.smq_cpu_smaq_roundtrip(x.data_ptr(), code, y.data_ptr(), numel, p, None, None,
                                            ws.data_ptr(), ws.numel(), N.cpu_threads()),
                 "smq_cpu_smaq_roundtrip")
@@ -251,6 +268,41 @@ class SmartFP(CompressionAlgorithmBase):
                           n_out * hp.num_bits_outlier + (numel - n_out) * hp.num_bits_main)
         else:
             self.log_size(tag, numel * 32, None)
+        return y
+
+    def _call_f64(self, data, tag, numel, all_positive, batch_norm_stats):
+        """float64 data: smart.py:130-182 in fp64 (smq_smaq_roundtrip_f64 / its host twin), output
+        float64; header SmqSmaqStatsF64 (read_stats_f64)."""
+        hp = self.hparams
+        x = data.contiguous()
+        y = torch.empty(x.shape, dtype=torch.float64, device=x.device)
+        cpu = N.on_cpu(x)
+        p = self._params(numel, all_positive, torch.float64, None if cpu else x.device)
+        keep = None
+        if hp.use_batch_norm and batch_norm_stats is not None:
+            keep = self._bind_batch_norm(p, x, batch_norm_stats)
+        lib = N.lib()
+        if cpu:
+            ws = N.cpu_workspace("smaq", self.workspace_bytes(numel))
+            N.check(lib.smq_cpu_smaq_roundtrip_f64(x.data_ptr(), y.data_ptr(), numel, p, None, None,
+                                                   ws.data_ptr(), ws.numel(), N.cpu_threads()),
+                    "smq_cpu_smaq_roundtrip_f64")
+        else:
+            if hp.measure_compression_ratio and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("SmartFP: --measure_compression_ratio reads the outlier count "
+                                   "on the host; it cannot run inside a graph capture")
+            st = N.stream_ptr(x.device)
+            ws = N.workspace("smaq", x.device, self.workspace_bytes(numel), st)
+            N.check(lib.smq_smaq_roundtrip_f64(x.data_ptr(), y.data_ptr(), numel, p, None, None,
+                                               ws.data_ptr(), ws.numel(), st),
+                    "smq_smaq_roundtrip_f64")
+        del keep
+
+        def new_size():
+            n_out = self.outlier_count(ws)
+            return n_out * hp.num_bits_outlier + (numel - n_out) * hp.num_bits_main
+
+        self.log_size(tag, numel * 32, new_size if hp.measure_compression_ratio else None)
         return y
 
     # bench.py sets an event recorder here to time the apply launch on the codec's stream
@@ -277,13 +329,40 @@ class SmartFP(CompressionAlgorithmBase):
         if tr is not None:
             tr.end("apply")
 
+    def workspace_bytes(self, numel: int) -> int:
+        """Workspace of one call: above SMQ_MAX_DEVICE_SAMPLES device-drawn samples the
+        multi-workgroup draw needs its own region (include/smq.h SMQ_WS_LARGE_SAMPLES_OFFSET)."""
+        lib = N.lib()
+        if self.hparams.use_sample_stats:
+            return lib.smq_smaq_workspace_bytes_sampled(numel, self.hparams.num_samples)
+        return lib.smq_smaq_workspace_bytes(numel)
+
     # -- inspection helpers (tests / bench) --------------------------------------------------------
+    @staticmethod
+    def sample_indices(ws: torch.Tensor, k: int) -> np.ndarray:
+        """The k indices the last device-drawn sampled call on ``ws`` drew, in draw order."""
+        off = N.SMQ_WS_SAMPLES_OFFSET if k <= N.SMQ_MAX_DEVICE_SAMPLES else N.SMQ_WS_LARGE_SAMPLES_OFFSET
+        return ws[off: off + 8 * k].cpu().numpy().view(np.int64).copy()
+
     @staticmethod
     def outlier_count(ws: torch.Tensor) -> int:
         """Sum of the SMQ_WS_OUTLIER_SLOTS outlier-count slots (include/smq.h)."""
         off = N.SMQ_WS_OUTLIER_SLOTS_OFFSET
         slots = ws[off: off + 8 * N.SMQ_WS_OUTLIER_SLOTS].cpu().numpy().view(np.uint64)
         return int(slots.sum())
+
+    @staticmethod
+    def read_stats_f64(ws: torch.Tensor) -> dict:
+        """The SmqSmaqStatsF64 header of an fp64 call."""
+        raw = ws[:80].cpu().numpy()
+        d = raw[:48].view(np.float64)
+        return {
+            "mean": float(d[0]), "std_dev": float(d[1]), "std_clamped": float(d[2]),
+            "raw_std": float(d[3]), "min": float(d[4]), "max": float(d[5]),
+            "n_used": int(raw[48:52].view(np.uint32)[0]),
+            "rng_offset": int(raw[56:64].view(np.uint64)[0]),
+            "n_outlier": SmartFP.outlier_count(ws),
+        }
 
     @staticmethod
     def read_stats(ws: torch.Tensor) -> dict:

@@ -24,6 +24,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import torch
 from torch.optim import SGD, Adam, AdamW, Optimizer
 
+from ... import _native as N
 from ...compress.smart import SmartFP
 from .multi import SmaqMulti
 
@@ -56,6 +57,9 @@ def _fusable(fn) -> Optional[SmartFP]:
     """The SmartFP behind a wrap_optimizer quantiser (any statistics mode: full, range-std or
     sampled — SmaqMulti computes each exactly as the per-tensor call would)."""
     if isinstance(fn, TaggedQuant) and isinstance(fn.codec, SmartFP):
+        hp = fn.codec.hparams
+        if hp.use_sample_stats and hp.num_samples > N.SMQ_MAX_DEVICE_SAMPLES:
+            return None  # the multi-workgroup draw runs per tensor (SmartFP)
         return fn.codec
     return None
 

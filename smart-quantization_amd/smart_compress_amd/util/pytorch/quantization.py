@@ -79,25 +79,32 @@ def rng_stream(n: int, device):
 
 def float_quantize(x: torch.Tensor, exp: int, man: int, hparams) -> torch.Tensor:
     """Stochastic (exp, man) round trip of ``x`` (quantization.py:187-204). Precision 16: ``x``
-    (fp32 / fp16 / bf16) is quantised as ``x.float()`` and returned as fp16."""
+    (fp32 / fp16 / bf16 / fp64) is quantised as ``x.float()`` and returned as fp16. Precision 32:
+    fp32 in, fp32 out; fp64 in, fp64 out (the quantised fp32 rounding of each element: qtorch
+    0.2.0's kernel reads ``data_ptr<float>()`` and raises on fp64, so this is its dtype-generic
+    extension, include/smq.h SMQ_DTYPE_F64)."""
     half_io = hparams.precision == 16
     N.require_supported(x, "float_quantize")
+    f64 = x.dtype == torch.float64
     if half_io:
-        if x.dtype not in N.DTYPE_CODES:
+        if x.dtype not in N.DTYPE_CODES and not f64:
             raise NotImplementedError(f"float_quantize: dtype {x.dtype} is not supported")
-    elif x.dtype != torch.float32:
+    elif x.dtype != torch.float32 and not f64:
         raise NotImplementedError(
-            f"float_quantize: dtype {x.dtype} at precision 32 is not supported (float32 only)")
+            f"float_quantize: dtype {x.dtype} at precision 32 is not supported (float32/float64)")
     src = x.contiguous()
-    out = torch.empty_like(src, dtype=torch.float16 if half_io else torch.float32)
+    out_dt = torch.float16 if half_io else (torch.float64 if f64 else torch.float32)
+    out = torch.empty_like(src, dtype=out_dt)
+    code_in = N.SMQ_DTYPE_F64 if f64 else N.DTYPE_CODES[src.dtype]
+    code_out = {torch.float16: N.SMQ_DTYPE_F16, torch.float32: N.SMQ_DTYPE_F32,
+                torch.float64: N.SMQ_DTYPE_F64}[out_dt]
     n = src.numel()
     if n == 0:
         return out
     if N.on_cpu(src):  # the library's host path, host RNG offsets
         seed, offset = quant_rng().take(n)
         N.check(N.lib().smq_cpu_float_quant(
-            src.data_ptr(), N.DTYPE_CODES[src.dtype], out.data_ptr(),
-            N.SMQ_DTYPE_F16 if half_io else N.SMQ_DTYPE_F32, n, exp, man, N.SMQ_ROUND_STOCHASTIC,
+            src.data_ptr(), code_in, out.data_ptr(), code_out, n, exp, man, N.SMQ_ROUND_STOCHASTIC,
             1 if hparams.float_quantize_check_inf else 0, None, seed, offset, N.cpu_threads()),
             "smq_cpu_float_quant")
         return out
@@ -105,8 +112,7 @@ def float_quantize(x: torch.Tensor, exp: int, man: int, hparams) -> torch.Tensor
     if _fq is None:
         _fq = N.lib().smq_float_quant
     seed, offset, ctr = rng_stream(n, src.device)
-    rc = _fq(src.data_ptr(), N.DTYPE_CODES[src.dtype], out.data_ptr(),
-             N.SMQ_DTYPE_F16 if half_io else N.SMQ_DTYPE_F32, n, exp, man, N.SMQ_ROUND_STOCHASTIC,
+    rc = _fq(src.data_ptr(), code_in, out.data_ptr(), code_out, n, exp, man, N.SMQ_ROUND_STOCHASTIC,
              1 if hparams.float_quantize_check_inf else 0, None, seed, offset, ctr,
              N.stream_ptr(src.device))
     if rc:

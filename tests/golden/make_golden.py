@@ -65,7 +65,10 @@ def _install_stubs(record):
             record.setdefault("q_in", []).append(xn.copy())
             record.setdefault("q_rand", []).append(r)
             y = qf.quantize(xn, exp, man, r, stochastic=True)
-        return torch.from_numpy(y).to(x.device)
+        # fp64 input (gen_f64 only): the dtype-generic extension qtorch's data_ptr<float>() kernel
+        # lacks — zeros_like(x) filled with the quantised fp32(x) (include/smq.h SMQ_DTYPE_F64)
+        dt = torch.float64 if x.dtype == torch.float64 else torch.float32
+        return torch.from_numpy(y).to(device=x.device, dtype=dt)
 
     qmod.float_quantize = float_quantize
     for name in ("qtorch", "qtorch.quant"):
@@ -322,6 +325,105 @@ def gen_s2fp8_p16(out_dir, record):
         json.dump(index, f, indent=1, sort_keys=True)
 
 
+def gen_f64(out_dir, record):
+    """float64 tensors through SmartFP (every statistics mode, BN, thresholds that fp32 cannot
+    hold), FP8 (precision 32: dtype-generic quantiser; 16: x.float() / .half()) and S2FP8 (both
+    precisions). Own random streams and index file; the SmaQ uniforms are the fp64 draws."""
+    from smart_compress.compress.fp8 import FP8
+    from smart_compress.compress.s2fp8 import S2FP8
+    from smart_compress.compress.smart import SmartFP
+
+    g = torch.Generator().manual_seed(6464)
+
+    def normal(n, mu=0.0, sd=1.0):
+        return torch.randn(n, generator=g, dtype=torch.float64) * sd + mu
+
+    n = 16384
+    x4 = normal(2 * 8 * 6 * 5).reshape(2, 8, 6, 5)
+    gam = torch.rand(8, generator=g, dtype=torch.float64) + 0.5
+    bet = torch.randn(8, generator=g, dtype=torch.float64) * 0.1
+    smaq = [
+        ("normal", normal(n), [], False, None, 32),
+        ("trunc", normal(n, 0.3, 2.0), ["--no_stochastic_rounding"], False, None, 32),
+        ("range", normal(n), ["--use_range_std_dev"], False, None, 32),
+        ("sampled", normal(n), ["--use_sample_stats"], False, None, 32),
+        ("sampled_range", normal(n), ["--use_sample_stats", "--use_range_std_dev"], False, None, 32),
+        ("relu_allpos", torch.relu(normal(n)), [], True, None, 32),
+        ("thresholds", normal(n), ["--main_std_dev_threshold", "0.7",
+                                   "--outlier_std_dev_threshold", "2.9"], False, None, 32),
+        ("bits_3_5", normal(n), ["--num_bits_main", "3", "--num_bits_outlier", "5"], False, None, 32),
+        ("large_mean", normal(n, 1e6, 0.25), [], False, None, 32),
+        ("tiny", normal(n, 0.0, 1e-30), [], False, None, 16),
+        ("p16", normal(n, 2.0, 3.0), [], False, None, 16),
+        ("bn", x4, ["--use_batch_norm"], False, (gam, bet), 32),
+        ("constant", torch.full((4096,), 0.75, dtype=torch.float64), [], False, None, 32),
+    ]
+    index = {}
+    for name, x, argv, allpos, bn, precision in smaq:
+        hp = smaq_hparams(SmartFP, argv + ["--measure_compression_ratio"], precision)
+        codec = SmartFP(hp)
+        logged = {}
+        codec.log = lambda k, v, **kw: logged.__setitem__(k, v)
+        torch.manual_seed(len(index) + 64)
+        with Capture() as cap:
+            kwargs = dict(all_positive=allpos)
+            if bn is not None:
+                kwargs["batch_norm_stats"] = bn
+            y = codec(x, tag="golden", **kwargs)
+        rec = dict(x=x.numpy(), y=y.numpy(), y_dtype=np.array(str(y.dtype)))
+        if cap.uniforms:
+            rec["uniforms"] = cap.uniforms[0].astype(np.float64)
+        if cap.perms:
+            idx = cap.perms[0][: min(x.numel(), hp.num_samples)]
+            rec["sample_idx"] = idx.astype(np.int64)
+            sample = x.reshape(-1)[torch.from_numpy(idx)]
+            mean, std = sample.mean(), codec._get_std(sample, unbiased=False)
+        else:
+            mean, std = x.mean(), codec._get_std(x)
+        rec["mean"], rec["std"] = np.float64(mean.item()), np.float64(std.item())
+        if bn is not None:
+            rec["bn_gamma"], rec["bn_beta"] = bn[0].numpy(), bn[1].numpy()
+        new_size = logged.get("new_size")
+        if new_size is not None:
+            rec["n_outlier"] = np.int64(round((new_size - x.numel() * hp.num_bits_main)
+                                              / (hp.num_bits_outlier - hp.num_bits_main)))
+        np.savez_compressed(os.path.join(out_dir, f"f64_smaq_{name}.npz"), **rec)
+        meta = vars(hp).copy()
+        meta.update(all_positive=allpos, kind="smaq")
+        index[f"smaq_{name}"] = meta
+    record["_rs"] = np.random.default_rng(6400)
+    inputs = {
+        "normal": torch.randn(4096, generator=g, dtype=torch.float64),
+        "wide": torch.randn(4096, generator=g, dtype=torch.float64)
+        * torch.exp(torch.randn(4096, generator=g, dtype=torch.float64) * 3),
+    }
+    for cname, cls in (("fp8", FP8), ("s2fp8", S2FP8)):
+        for precision in (32, 16):
+            hp = cls.add_argparse_args(ArgumentParser()).parse_args([])
+            hp.precision = precision
+            codec = cls(hp)
+            for iname, x in inputs.items():
+                _clear(record)
+                y = codec(x.clone(), tag="golden")
+                rec = dict(x=x.numpy(), y=y.double().numpy(), y_dtype=np.array(str(y.dtype)),
+                           q_in=record["q_in"][0], q_rand=record["q_rand"][0])
+                if cname == "s2fp8":
+                    xa = x.abs()
+                    lg = torch.where(xa == 0.0, xa, torch.log2(xa))
+                    mu, mx = torch.mean(lg), torch.max(lg)
+                    alpha = 15.0 / (mx - mu)
+                    beta = -alpha * mu
+                    rec.update(mu=np.float64(mu.item()), m=np.float64(mx.item()),
+                               alpha=np.float64(alpha.item()), beta=np.float64(beta.item()),
+                               beta_pow2=np.float64((2.0 ** beta).item()))
+                key = f"{cname}_p{precision}_{iname}"
+                np.savez_compressed(os.path.join(out_dir, f"f64_{key}.npz"), **rec)
+                index[key] = dict(kind=cname, precision=precision, input=iname,
+                                  y_dtype=str(y.dtype))
+    with open(os.path.join(out_dir, "f64_cases.json"), "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True, default=str)
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; nothing to do")
@@ -336,6 +438,8 @@ def main():
         gen_float(out_dir, record)
     if only in (None, "s2fp8_p16"):
         gen_s2fp8_p16(out_dir, record)
+    if only in (None, "f64"):
+        gen_f64(out_dir, record)
     print("golden vectors written to", out_dir)
 
 

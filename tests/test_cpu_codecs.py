@@ -65,7 +65,8 @@ def _roundtrip(x, p, uniforms=None, stats_in=None, threads=0):
     N = _N()
     n = x.numel()
     y = torch.empty(x.shape, dtype=torch.float32)
-    ws = torch.zeros(N.lib().smq_smaq_workspace_bytes(n), dtype=torch.uint8)
+    ws = torch.zeros(N.lib().smq_smaq_workspace_bytes_sampled(n, max(p.num_samples, 1)),
+                     dtype=torch.uint8)
     if stats_in is not None:
         p.stats_source = N.SMQ_STATS_INJECTED
     u = None
@@ -205,23 +206,27 @@ def test_cpu_thread_count_invariant(threads):
     assert torch.equal(y.view(torch.int32), ref.view(torch.int32))
 
 
-@pytest.mark.parametrize("k", [16, 1000, 4096])
-def test_cpu_sampled_draw_matches_device_draw(k):
+@pytest.mark.parametrize("k,n", [(16, 200003), (1000, 200003), (4096, 200003), (4097, 200003),
+                                 (10000, 200003), (10000, 10000), (10000, 11000)])
+def test_cpu_sampled_draw_matches_device_draw(k, n):
     """SMQ_STATS_SAMPLED_DEVICE on the host: the same Floyd draw as the device (oracle/rng.py),
-    recorded in the workspace, and the oracle's sampled statistics / output from those indices."""
+    recorded in the workspace (above SMQ_MAX_DEVICE_SAMPLES in the large-draw region), and the
+    oracle's sampled statistics / output from those indices. k = n is a permutation; n close to k
+    substitutes most steps."""
     from oracle import rng as orng
     from oracle import smaq as osmaq
+    from smart_compress_amd.compress.smart import SmartFP
 
     N = _N()
-    n = 200003
     x = torch.randn(n, generator=torch.Generator().manual_seed(k)) + 0.5
     hp = smaq_hparams(use_sample_stats=True, num_samples=k)
     p = _params(hp, n, seed=77, offset=1000)
     assert p.stats_source == N.SMQ_STATS_SAMPLED_DEVICE
     y, ws, st = _roundtrip(x, p)
-    off = N.SMQ_WS_SAMPLES_OFFSET
-    idx = ws[off: off + 8 * k].numpy().view(np.int64)
+    idx = SmartFP.sample_indices(ws, min(n, k))
     assert np.array_equal(idx, orng.floyd_indices(77, 1000, n, k))
+    if k >= n:
+        assert sorted(idx.tolist()) == list(range(n))
     cfg = osmaq.SmaqConfig(use_sample_stats=True, num_samples=k)
     mo, so = osmaq.sampled_stats(x.numpy(), idx, cfg)
     assert ulp_diff(st["mean"], mo) <= 1 and ulp_diff(st["raw_std"], so) <= 1
@@ -449,8 +454,9 @@ def test_cpu_nonfinite_input_propagates_like_reference(special):
 
 
 def test_cpu_rejected_call_consumes_no_stream_positions():
-    """A call that fails validation (num_samples out of range, missing injected statistics)
-    leaves the graph-safe stream position where it was; a valid call advances it by n."""
+    """A call that fails validation (num_samples out of range or beyond what the workspace holds,
+    missing injected statistics) leaves the graph-safe stream position where it was; a valid call
+    advances it by n."""
     N = _N()
     n = 3 * N.SMQ_MAX_DEVICE_SAMPLES
     x = torch.randn(n)
@@ -458,6 +464,7 @@ def test_cpu_rejected_call_consumes_no_stream_positions():
     ws = torch.zeros(N.lib().smq_smaq_workspace_bytes(n), dtype=torch.uint8)
     ctr = torch.tensor([777], dtype=torch.int64)
     for src, k in ((N.SMQ_STATS_SAMPLED_DEVICE, N.SMQ_MAX_DEVICE_SAMPLES + 1),
+                   (N.SMQ_STATS_SAMPLED_DEVICE, 0),
                    (N.SMQ_STATS_SAMPLED, N.SMQ_MAX_SAMPLES + 1), (N.SMQ_STATS_INJECTED, 16)):
         p = _params(smaq_hparams(), n)
         p.offset_counter = ctr.data_ptr()
@@ -470,3 +477,20 @@ def test_cpu_rejected_call_consumes_no_stream_positions():
     assert N.lib().smq_cpu_smaq_roundtrip(x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p,
                                           None, None, ws.data_ptr(), ws.numel(), 1) == 0
     assert int(ctr.item()) == 777 + n
+
+
+def test_sampled_workspace_sizes():
+    """smq_smaq_workspace_bytes_sampled: the plain size up to SMQ_MAX_DEVICE_SAMPLES, the
+    large-draw region above it (growing with k), 0 beyond SMQ_MAX_DRAW_SAMPLES."""
+    N = _N()
+    lib = N.lib()
+    n = 1 << 30
+    base = lib.smq_smaq_workspace_bytes(n)
+    assert lib.smq_smaq_workspace_bytes_sampled(n, 16) == base
+    assert lib.smq_smaq_workspace_bytes_sampled(n, N.SMQ_MAX_DEVICE_SAMPLES) == base
+    assert N.SMQ_WS_LARGE_SAMPLES_OFFSET >= base
+    a = lib.smq_smaq_workspace_bytes_sampled(n, N.SMQ_MAX_DEVICE_SAMPLES + 1)
+    b = lib.smq_smaq_workspace_bytes_sampled(n, 10000)
+    assert N.SMQ_WS_LARGE_SAMPLES_OFFSET + 8 * 4097 < a <= b
+    assert lib.smq_smaq_workspace_bytes_sampled(5000, 10000) == lib.smq_smaq_workspace_bytes_sampled(5000, 5000)
+    assert lib.smq_smaq_workspace_bytes_sampled(n, N.SMQ_MAX_DRAW_SAMPLES + 1) == 0

@@ -2,8 +2,8 @@
 line 88 drawn by Floyd's algorithm on the device from the call's stream position).
 
 Contract, bit-exact: the indices a call records in its workspace equal oracle/rng.py
-floyd_indices(seed, position, n, k) for any k <= SMQ_MAX_DEVICE_SAMPLES (4096; the reference has
-no cap, round 1 had 64); the statistics equal the oracle's over those indices (fp32 within 1 ulp
+floyd_indices(seed, position, n, k) for any k (the reference has no cap; above SMQ_MAX_DEVICE_SAMPLES =
+4096 the draw runs across workgroups, include/smq.h SMQ_WS_LARGE_SAMPLES_OFFSET); the statistics equal the oracle's over those indices (fp32 within 1 ulp
 of the fp64 restatement); the output equals the oracle's apply with the device statistics and the
 same counter RNG. Consecutive eager calls draw different sets, and so do consecutive replays of a
 captured graph in graph-safe mode (round 1 reused one set there).
@@ -19,10 +19,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _idx(ws, k):
-    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.smart import SmartFP
 
-    o = N.SMQ_WS_SAMPLES_OFFSET
-    return ws[o: o + 8 * k].cpu().numpy().view(np.int64).copy()
+    return SmartFP.sample_indices(ws, k)
 
 
 def _check_call(x, y, ws, hp, seed, pos, k):
@@ -50,7 +49,10 @@ def _check_call(x, y, ws, hp, seed, pos, k):
                                          (1 << 18, 65, False), (1 << 20, 1000, False),
                                          (1 << 20, 4096, False), (4096, 4096, False),
                                          (3000, 4096, False), (10, 16, False),
-                                         (1 << 18, 16, True), (1 << 20, 2048, True)])
+                                         (1 << 18, 16, True), (1 << 20, 2048, True),
+                                         (1 << 20, 4097, False), (1 << 20, 10000, False),
+                                         (10000, 10000, False), (11000, 10000, False),
+                                         (1 << 22, 100000, True), (3 << 20, 10000, False)])
 def test_device_draw_eager_calls(n, k, rng_std):
     from smart_compress_amd import _native as N
     from smart_compress_amd.compress.smart import SmartFP
@@ -98,13 +100,35 @@ def test_device_draw_half_inputs():
         assert y.dtype == torch.float32
 
 
-def test_device_draw_k_cap():
+def test_device_draw_large_k_half_and_heavy_repeats():
+    """The multi-workgroup draw with fp16 input and with n barely above k (most steps are
+    suspects, resolved 64 at a time in draw order), against the oracle's Floyd draw."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
     from smart_compress_amd import _native as N
     from smart_compress_amd.compress.smart import SmartFP
 
-    codec = SmartFP(smaq_hparams(use_sample_stats=True, num_samples=N.SMQ_MAX_DEVICE_SAMPLES + 1))
-    with pytest.raises(NotImplementedError):
-        codec(torch.randn(1 << 16, device="cuda"))
+    for n, k, dt in ((1 << 18, 20000, torch.float16), (20001, 20000, torch.float32),
+                     (40000, 20000, torch.float32)):
+        hp = smaq_hparams(use_sample_stats=True, num_samples=k, precision=16)
+        codec = SmartFP(hp)
+        codec.rng.seed, codec.rng.offset = 31, 5
+        x = (torch.randn(n, device="cuda") * 2).to(dt)
+        y = codec(x)
+        torch.cuda.synchronize()
+        ws = N.workspace("smaq", x.device, 0)
+        idx = _idx(ws, k)
+        assert idx.tolist() == orng.floyd_indices(31, 5, n, k).tolist()
+        name = "f16" if dt == torch.float16 else "f32"
+        cfg = osmaq.SmaqConfig(use_sample_stats=True, num_samples=k, precision=16)
+        mo, so = osmaq.sampled_stats(x.float().cpu().numpy(), idx, cfg, name)
+        st = SmartFP.read_stats(ws)
+        if dt == torch.float16:
+            h = lambda v: int(np.array(v, np.float16).view(np.int16))
+            assert abs(h(st["mean"]) - h(mo)) <= 1 and abs(h(st["raw_std"]) - h(so)) <= 1
+        else:
+            assert ulp_diff(st["mean"], mo) <= 1 and ulp_diff(st["raw_std"], so) <= 1
+        assert st["n_used"] == k and y.dtype == torch.float32
 
 
 def test_device_draw_graph_replays_draw_fresh_sets():

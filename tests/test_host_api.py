@@ -90,8 +90,9 @@ def test_range_coef_matches_torch():
 
 
 def test_passthrough_cpu_path_and_rejections():
-    """n < min_size passes the same object through; CPU tensors take the library's host path;
-    fp64 and meta tensors are rejected with a clear error."""
+    """n < min_size passes the same object through; CPU tensors take the library's host path
+    (float64 ones in fp64, returning float64 as smart.py does); integer and meta tensors are
+    rejected with a clear error."""
     from smart_compress_amd.compress.smart import SmartFP
 
     c = SmartFP(smaq_hparams())
@@ -99,8 +100,9 @@ def test_passthrough_cpu_path_and_rejections():
     assert c(x) is x  # smart.py:123-128, no device needed
     y = c(torch.randn(100))
     assert y.shape == (100,) and y.device.type == "cpu"
-    with pytest.raises(NotImplementedError, match="float64"):
-        c(torch.randn(100, dtype=torch.float64))
+    assert c(torch.randn(100, dtype=torch.float64)).dtype == torch.float64
+    with pytest.raises(NotImplementedError, match="int32"):
+        c(torch.ones(100, dtype=torch.int32))
     with pytest.raises(RuntimeError, match="not supported"):
         c(torch.randn(100, device="meta"))
 
