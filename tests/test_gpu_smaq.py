@@ -435,8 +435,10 @@ def test_half_precision_rules():
         SmartFP(smaq_hparams(precision=32))(x)  # std.clamp(1e-38, 1e38) overflows half
     y = SmartFP(smaq_hparams(precision=32))(x.bfloat16())  # bf16 holds 1e38
     assert y.dtype == torch.float32
+    # fp64 data runs in fp64 and stays fp64 (smart.py's type flow; tests/test_f64.py)
+    assert SmartFP(smaq_hparams())(torch.randn(100, device="cuda").double()).dtype == torch.float64
     with pytest.raises(NotImplementedError):
-        SmartFP(smaq_hparams())(torch.randn(100, device="cuda").double())
+        SmartFP(smaq_hparams())(torch.ones(100, device="cuda", dtype=torch.int32))
 
 
 def _subnormal_mix(n, seed):
