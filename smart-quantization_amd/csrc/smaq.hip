@@ -1139,15 +1139,16 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   }();
   A.nt_loads = (int64_t)(dtype == SMQ_DTYPE_F32 ? 4 : 2) * n >= apply_nt_min ? 1 : 0;
   int tv = (rm == kRoundHash && vec && !A.bn_gamma) ? sr_tile_v() : 1;
-  // bf16 inputs: 8-B loads, so twice the slots for the bytes in flight per lane of fp32. 256M, two
-  // interleaved rounds, ms/step (tools/half_tv.sh): bf16 2 slots 0.401-0.404, 4 slots 0.384-0.390;
-  // fp16 0.4016 / 0.4016 vs 0.403 / 0.407 (its cvt-based element chain gains nothing), so 2
+  // half inputs: 8-B loads, so twice the slots for the bytes in flight per lane of fp32. 256M,
+  // interleaved rounds, ms/step (tools/half_tv.sh, tools/ab_env.sh): bf16 2 slots 0.401-0.404,
+  // 4 slots 0.384-0.390; fp16 (round 3, with the fp32-reciprocal z-score, half_quot) 4 slots
+  // 0.4005-0.406 vs 2 slots 0.408-0.422 (round 2, before half_quot: no gain from 4)
   static const int half_tv = [] {  // measurement knob SMQ_HALF_TV (2 | 4): both half types
     const char* e = getenv("SMQ_HALF_TV");
     return e ? (atoi(e) == 4 ? 4 : 2) : 0;
   }();
   if (tv == 2 && dtype != SMQ_DTYPE_F32)
-    tv = half_tv ? half_tv : (dtype == SMQ_DTYPE_BF16 ? 4 : 2);
+    tv = half_tv ? half_tv : 4;
   const int64_t tile_elems = (int64_t)kBlock * 4 * tv;
   const int64_t tiles = (n + tile_elems - 1) / tile_elems;
   if (tiles > 0x7fffffffLL) {
