@@ -23,9 +23,6 @@ constexpr int kWave = 64;
 // The 64-bit seed is folded into a 32-bit key once per launch on the host.
 // ---------------------------------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
-#ifdef SMQ_EXP_NOHASH  // timing experiment only (tools/build_variant.py): not a random function
-  return x ^ (x << 7) ^ (x >> 9);
-#endif
   x ^= x >> 16;
   x *= 0x7feb352dU;
   x ^= x >> 15;
