@@ -651,6 +651,9 @@ struct UnpackArgs {
   int wm, wo;                // the caller's widths (smq_smaq_decompress_ex), else 0
   int vec;
   int reverse;  // blocks in reverse order (measurement knob SMQ_UNPACK_REVERSE=1)
+  uint32_t nb;         // blocks
+  uint32_t n_full;     // blocks of SMQ_PACK_BLOCK elements
+  uint32_t lds_bytes;  // dynamic LDS of the launch (the widths' need, or the widest)
 };
 
 // Decode table of narrow codes (both widths <= 8 bits: the 6/8-bit default): every main code
@@ -674,77 +677,96 @@ __device__ __forceinline__ float decode_code(uint32_t v, bool is_o, int wm, int 
 // dynamic LDS of the decoder (words): fixed image, variable section (when it fits kVarCap), mask
 // prefix counts, escape bitmask and its prefix counts, decode table
 constexpr uint32_t kUnpackLdsWords = 128u * (kMaxWidth + 1) + kVarCap + 4u + 3u * kMaskWords + kLutMax;
+__host__ __device__ inline uint32_t unpack_lds_words(int wm) {
+  return fixed_words(wm) + kVarCap + 4u + 3u * kMaskWords + kLutMax;
+}
+// blocks per decoder workgroup: both blocks' loads are in flight before the first is decoded (at
+// 8 workgroups per CU one block each left ~4 KB of loads in flight per workgroup)
+constexpr int kUnpackPer = 2;
 
+// Where a block's sections are (from its directory entry and the widths).
+struct UnpackGeom {
+  uint32_t F, n_out, n_esc, n_ext, var_words, sh, nvec;
+  bool var_lds;
+  const uint32_t* vsrc;
+  const uint4* fsrc;
+};
+
+__device__ __forceinline__ UnpackGeom unpack_geom(const UnpackArgs& A, uint32_t b, uint64_t dent,
+                                                  int wm, int we) {
+  UnpackGeom G;
+  G.F = fixed_words(wm);
+  G.n_out = (uint32_t)(dent >> 38) & 0x1fffu;
+  G.n_esc = (uint32_t)(dent >> 51);
+  G.n_ext = ext_words(we, G.n_out);
+  G.var_words = G.n_ext + 2u * G.n_esc;
+  G.vsrc = A.var + (dent & ((1ull << 38) - 1ull));
+  G.var_lds = G.var_words <= (uint32_t)kVarCap;
+  G.sh = (uint32_t)(((uintptr_t)G.vsrc >> 2) & 3u);
+  G.nvec = G.var_lds ? (G.sh + G.var_words + 3u) >> 2 : 0u;
+  G.fsrc = reinterpret_cast<const uint4*>(A.fixed + (size_t)b * G.F);
+  return G;
+}
+
+// The loads of one block — its fixed section (one 16-B load per lane covers F <= 1024 words, i.e.
+// wm <= 7; wider planes copy the rest in unpack_decode) and its variable section (16-B windows from
+// its line on, the last window clipped with dword loads, so nothing past the stream is read) —
+// issued, not waited for: a workgroup requests both of its blocks' bytes before it decodes one.
+struct UnpackLoads {
+  uint4 f0, vv;
+};
+
+__device__ __forceinline__ UnpackLoads unpack_issue(const UnpackGeom& G) {
+  const int tid = threadIdx.x;
+  UnpackLoads L;
+  L.f0 = make_uint4(0u, 0u, 0u, 0u);
+  if ((uint32_t)tid < G.F / 4u) L.f0 = G.fsrc[tid];
+  L.vv = make_uint4(0u, 0u, 0u, 0u);
+  constexpr int kRV = (kVarCap + 4 + 4 * kBlock - 1) / (4 * kBlock);
+  static_assert(kRV == 1, "one 16-B window per lane covers the variable section");
+  if ((uint32_t)tid < G.nvec) {
+    const uint4* src = reinterpret_cast<const uint4*>((uintptr_t)G.vsrc - 4u * G.sh);
+    if (4u * tid + 4u <= G.sh + G.var_words) {
+      L.vv = src[tid];
+    } else {
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int idx = (int)(4u * tid) + k - (int)G.sh;
+        q[k] = (idx >= 0 && idx < (int)G.var_words) ? G.vsrc[idx] : 0u;
+      }
+      L.vv = make_uint4(q[0], q[1], q[2], q[3]);
+    }
+  }
+  return L;
+}
+
+// Decode one block whose loads unpack_issue requested (the decode table, if any, is in LDS).
 template <bool AP, bool SQ, bool FULL, int WM, int WO>
-__device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
-                                            uint64_t dent, int wm_rt, int wo_rt, uint32_t* lds) {
+__device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
+                                              const UnpackGeom& G, const UnpackLoads& L, int wm_rt,
+                                              int wo_rt, uint32_t* lds) {
   constexpr bool kLut = WM > 0 && WM <= 8 && WO > 0 && WO <= 8;
   const int wm = WM > 0 ? WM : wm_rt, wo = WO > 0 ? WO : wo_rt;
   const int we = wo > wm ? wo - wm : 0;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
-  const uint32_t F = fixed_words(wm);
+  const uint32_t F = G.F, n_esc = G.n_esc, n_ext = G.n_ext, sh = G.sh, nvec = G.nvec;
+  const bool var_lds = G.var_lds;
+  const uint32_t* vsrc = G.vsrc;
+  const uint4* fsrc = G.fsrc;
+  const uint32_t nf4 = F / 4u;
   uint32_t* fx = lds;                    // [F]: mask, plane
   uint32_t* vs = lds + F;                // [kVarCap + 4]: outlier bits, escapes (16-B shifted)
   uint32_t* pc = vs + kVarCap + 4;       // [128] outliers before each mask word
   uint32_t* esc_mask = pc + kMaskWords;  // [128]
   uint32_t* epc = esc_mask + kMaskWords; // [128] escapes before each mask word
   float* lut = reinterpret_cast<float*>(epc + kMaskWords);
-  const uint32_t n_out = (uint32_t)(dent >> 38) & 0x1fffu, n_esc = (uint32_t)(dent >> 51);
-  const uint32_t n_ext = ext_words(we, n_out);
-  const uint32_t var_words = n_ext + 2u * n_esc;
-  const uint32_t* vsrc = A.var + (dent & ((1ull << 38) - 1ull));
-  const bool var_lds = var_words <= (uint32_t)kVarCap;
-  // fixed section: F / 4 16-B loads; variable section: 16-B windows from its line on (the last
-  // window clipped with dword loads, so nothing past the stream is read); every load of a lane is
-  // issued before any LDS store
-  const uint4* fsrc = reinterpret_cast<const uint4*>(A.fixed + (size_t)b * F);
-  // (one 16-B load per lane covers F <= 1024 words, i.e. wm <= 7; wider planes copy the rest in a
-  // second loop below)
-  const uint32_t nf4 = F / 4u;
-  uint4 f0 = make_uint4(0u, 0u, 0u, 0u);
-  if ((uint32_t)tid < nf4) f0 = fsrc[tid];
-  const uintptr_t va = (uintptr_t)vsrc;
-  const uint32_t sh = (uint32_t)((va >> 2) & 3u);
-  const uint32_t nvec = var_lds ? (sh + var_words + 3u) >> 2 : 0u;
-  uint4 vv = make_uint4(0u, 0u, 0u, 0u);
-  constexpr int kRV = (kVarCap + 4 + 4 * kBlock - 1) / (4 * kBlock);
-  static_assert(kRV == 1, "one 16-B window per lane covers the variable section");
-  if ((uint32_t)tid < nvec) {
-    const uint4* src = reinterpret_cast<const uint4*>(va - 4u * sh);
-    if (4u * tid + 4u <= sh + var_words) {
-      vv = src[tid];
-    } else {
-      uint32_t q[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int idx = (int)(4u * tid) + k - (int)sh;
-        q[k] = (idx >= 0 && idx < (int)var_words) ? vsrc[idx] : 0u;
-      }
-      vv = make_uint4(q[0], q[1], q[2], q[3]);
-    }
-  }
-  if (kLut) {  // while the loads are in flight: the block's decode table
-    for (int i = tid; i < (1 << WM) + (1 << WO); i += kBlock) {
-      bool hi = false, lo = false;
-      float q;
-      if (i < (1 << WM)) {
-        q = (float)(((int32_t)((uint32_t)i << (32 - WM))) >> (32 - WM));  // sign-extend
-      } else {
-        const uint32_t v = (uint32_t)(i - (1 << WM));
-        lo = (v >> (WO - 1)) & 1u;
-        hi = !lo;
-        const int mag = (int)(v & ((1u << (WO - 1)) - 1u));
-        q = (float)(lo ? -mag : mag);
-      }
-      lut[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
-    }
-  }
   if (tid < kMaskWords) esc_mask[tid] = 0u;
-  if ((uint32_t)tid < nf4) reinterpret_cast<uint4*>(fx)[tid] = f0;
+  if ((uint32_t)tid < nf4) reinterpret_cast<uint4*>(fx)[tid] = L.f0;
   for (uint32_t i = tid + kBlock; i < nf4; i += kBlock) reinterpret_cast<uint4*>(fx)[i] = fsrc[i];
-  if ((uint32_t)tid < nvec) reinterpret_cast<uint4*>(vs)[tid] = vv;
+  if ((uint32_t)tid < nvec) reinterpret_cast<uint4*>(vs)[tid] = L.vv;
   __syncthreads();
   const uint32_t* ext = var_lds ? vs + sh : vsrc;
   const uint32_t* esc = ext + n_ext;
@@ -851,10 +873,62 @@ __device__ __forceinline__ void unpack_body(const UnpackArgs& A, const ElemConst
   }
 }
 
+// Decode table of narrow codes (kLut), once per workgroup: every main and outlier code de-quantised.
+template <bool AP, bool SQ, int WM, int WO>
+__device__ __forceinline__ void unpack_lut(const ElemConsts& c, uint32_t* lds, uint32_t F) {
+  float* lut = reinterpret_cast<float*>(lds + F + kVarCap + 4 + 3 * kMaskWords);
+  for (int i = threadIdx.x; i < (1 << WM) + (1 << WO); i += kBlock) {
+    bool hi = false, lo = false;
+    float q;
+    if (i < (1 << WM)) {
+      q = (float)(((int32_t)((uint32_t)i << (32 - WM))) >> (32 - WM));  // sign-extend
+    } else {
+      const uint32_t v = (uint32_t)(i - (1 << WM));
+      lo = (v >> (WO - 1)) & 1u;
+      hi = !lo;
+      const int mag = (int)(v & ((1u << (WO - 1)) - 1u));
+      q = (float)(lo ? -mag : mag);
+    }
+    lut[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
+  }
+}
+
+// The workgroup's kUnpackPer consecutive blocks: every block's loads first, the decode table while
+// they are in flight, then the blocks one after another (an LDS barrier between them).
+template <bool AP, bool SQ, bool FULL, int WM, int WO>
+__device__ __forceinline__ void unpack_blocks(const UnpackArgs& A, const ElemConsts& c, uint32_t b0,
+                                              int nblk, const uint64_t* dent, int wm, int wo,
+                                              uint32_t* lds) {
+  constexpr bool kLut = WM > 0 && WM <= 8 && WO > 0 && WO <= 8;
+  const int we = wo > wm ? wo - wm : 0;
+  UnpackGeom G[kUnpackPer];
+  UnpackLoads L[kUnpackPer];
+#pragma unroll
+  for (int i = 0; i < kUnpackPer; ++i)
+    if (i < nblk) {
+      G[i] = unpack_geom(A, b0 + i, dent[i], wm, we);
+      L[i] = unpack_issue(G[i]);
+    }
+  if constexpr (kLut) unpack_lut<AP, SQ, WM, WO>(c, lds, G[0].F);
+#pragma unroll
+  for (int i = 0; i < kUnpackPer; ++i) {
+    if (i >= nblk) break;
+    if (i > 0) __syncthreads();  // the previous block's LDS reads are done
+    unpack_decode<AP, SQ, FULL, WM, WO>(A, c, b0 + i, G[i], L[i], wm, wo, lds);
+  }
+}
+
+// FULL: the full blocks [0, n_full), kUnpackPer per workgroup; else the one short last block.
+// WM / WO: the 6/8-bit default's widths, or 0 (any widths, from the caller or the header).
+template <int WM, int WO, bool FULL>
 __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kUnpackLdsWords];
-  const uint32_t b = A.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
-  const uint64_t dent = A.dir[b];
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t g = A.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  const uint32_t b0 = FULL ? g * (uint32_t)kUnpackPer : A.nb - 1;
+  const int nblk = FULL ? (int)min((uint32_t)kUnpackPer, A.n_full - b0) : 1;
+  uint64_t dent[kUnpackPer];
+#pragma unroll
+  for (int i = 0; i < kUnpackPer; ++i) dent[i] = i < nblk ? A.dir[b0 + i] : 0ull;
   const SmqPackedHeader* h = A.hdr;
   int wm, wo;
   if (A.var) {  // widths from the caller: the fixed and variable sections' addresses do not wait
@@ -864,10 +938,11 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
     wm = h->num_bits_main - 1;
     wo = h->num_bits_outlier - 1;
     if (wm < 1 || wm > kMaxWidth || wo < 2 || wo > kMaxWidth) return;
-    A.var = A.fixed + (size_t)gridDim.x * fixed_words(wm);
+    A.var = A.fixed + (size_t)A.nb * fixed_words(wm);
   }
   if (h->magic != SMQ_PACK_MAGIC || h->version != SMQ_PACK_VERSION || h->n != A.n ||
-      h->num_bits_main != wm + 1 || h->num_bits_outlier != wo + 1)
+      h->num_bits_main != wm + 1 || h->num_bits_outlier != wo + 1 ||
+      unpack_lds_words(wm) * 4u > A.lds_bytes || (WM > 0 && (wm != WM || wo != WO)))
     return;
   ElemConsts c;
   c.mean = h->mean;
@@ -881,25 +956,13 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   c.inv_r_main = h->inv_range_main;
   c.inv_r_out = h->inv_range_outlier;
   const uint32_t f = h->flags;
-  const bool full = (int64_t)(b + 1) * kPB <= A.n;
-  const bool w57 = wm == 5 && wo == 7;
-#define SMQ_UNPACK_W(APV, SQV, FULLV)                                           \
-  do {                                                                          \
-    if (w57) unpack_body<APV, SQV, FULLV, 5, 7>(A, c, b, dent, wm, wo, lds);   \
-    else unpack_body<APV, SQV, FULLV, 0, 0>(A, c, b, dent, wm, wo, lds);       \
-  } while (0)
-#define SMQ_UNPACK(APV, SQV)                \
-  do {                                      \
-    if (full) SMQ_UNPACK_W(APV, SQV, true); \
-    else SMQ_UNPACK_W(APV, SQV, false);     \
-  } while (0)
+#define SMQ_UNPACK(APV, SQV) unpack_blocks<APV, SQV, FULL, WM, WO>(A, c, b0, nblk, dent, wm, wo, lds)
   if (f & 2u) {
     if (f & 1u) SMQ_UNPACK(true, true); else SMQ_UNPACK(false, true);
   } else {
     if (f & 1u) SMQ_UNPACK(true, false); else SMQ_UNPACK(false, false);
   }
 #undef SMQ_UNPACK
-#undef SMQ_UNPACK_W
 }
 
 inline bool aligned_to(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
@@ -1084,7 +1147,23 @@ static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int 
     return e ? atoi(e) : 0;
   }();
   A.reverse = rev;
-  hipLaunchKernelGGL(smaq_unpack_kernel, dim3((unsigned)nb), dim3(kBlock), 0, st, A);
+  A.nb = (uint32_t)nb;
+  A.n_full = (uint32_t)(n / kPB);
+  A.lds_bytes = 4u * (bm ? unpack_lds_words(A.wm) : kUnpackLdsWords);
+  const unsigned grid = (unsigned)((A.n_full + kUnpackPer - 1) / kUnpackPer);
+  const bool w57 = bm == 6 && bo == 8;  // the default widths, known from the caller
+#define SMQ_UNPACK_LAUNCH(WMV, WOV)                                                                \
+  do {                                                                                            \
+    if (grid)                                                                                     \
+      hipLaunchKernelGGL((smaq_unpack_kernel<WMV, WOV, true>), dim3(grid), dim3(kBlock),           \
+                         A.lds_bytes, st, A);                                                     \
+    if (A.n_full < A.nb)                                                                          \
+      hipLaunchKernelGGL((smaq_unpack_kernel<WMV, WOV, false>), dim3(1), dim3(kBlock), A.lds_bytes, \
+                         st, A);                                                                  \
+  } while (0)
+  if (w57) SMQ_UNPACK_LAUNCH(5, 7);
+  else SMQ_UNPACK_LAUNCH(0, 0);
+#undef SMQ_UNPACK_LAUNCH
   return check_launch("smaq_unpack_kernel");
 }
 
