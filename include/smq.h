@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SMQ_ABI_VERSION 4
+#define SMQ_ABI_VERSION 5
 
 #define SMQ_OK 0
 #define SMQ_ERR_INVALID -1  /* bad argument */
@@ -450,8 +450,15 @@ uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
  *                   block, q as float32 bits (any NaN q as 0x7fc00000)} in element order
  * Size: the same bits as an element-order stream of wm-bit main and wo-bit outlier codes, but the
  * fixed section can be written the moment its block is coded (no prefix over earlier blocks).
- * Decoding: q -> (q / range) - scalars, * std + mean (smart.py:171-182), bit-identical to
- * smq_smaq_apply for the same statistics, rounding mode and random stream. Needs T_m > 0.
+ *        | BatchNorm table (flag SMQ_PACK_FLAG_BN only): bn_channels gammas then bn_channels betas
+ *          (fp32), right after the variable region (word data_words of it)
+ * Decoding: q -> (q / range) - scalars, * std + mean (smart.py:171-182), then * gamma[c] + beta[c]
+ * with c = (element / bn_inner) % bn_channels for a BN stream (smart.py:174-179), bit-identical to
+ * smq_smaq_apply for the same statistics, BN parameters, rounding mode and random stream.
+ * Thresholds: T_m >= 0 makes the sides exclusive (mask bit = outlier). T_m < 0 (flag
+ * SMQ_PACK_FLAG_BOTH_SIDES) adds a third state, z above T_m and below -T_m at once (smart.py:157-158
+ * both true: scalars -T_m + T_m, range_outlier): such an element has mask bit 0 and codes as a main
+ * element (wm-bit two's complement q) that the decoder de-quantises with both sides set.
  * ------------------------------------------------------------------------------------------- */
 #define SMQ_PACK_MAGIC 0x50514d53u /* "SMQP" */
 #define SMQ_PACK_VERSION 2u
@@ -464,7 +471,8 @@ typedef struct SmqPackedHeader {
   uint32_t block_elems;       /* SMQ_PACK_BLOCK */
   uint32_t n_blocks;
   int32_t num_bits_main, num_bits_outlier;
-  uint32_t flags;             /* bit 0: all_positive, bit 1: IEEE q / range (absurd ranges) */
+  uint32_t flags;             /* bit 0: all_positive, bit 1: IEEE q / range (absurd ranges),
+                                 SMQ_PACK_FLAG_BOTH_SIDES, SMQ_PACK_FLAG_BN */
   float thr;                  /* T_m (fp32) */
   float range_main, range_outlier;
   float mean, std_dev;        /* de-normalisation statistics (std after the ==0 rule) */
@@ -472,12 +480,22 @@ typedef struct SmqPackedHeader {
   uint64_t data_words;        /* size of the data region in uint32 words */
   uint64_t total_bytes;       /* header + directory + data */
   uint32_t error;             /* 0 (no packing launch waits on another workgroup) */
-  uint32_t reserved[9];
+  uint32_t bn_channels;       /* BN streams: channels of the table (1: scalar parameters), else 0 */
+  int64_t bn_inner;           /* BN streams: elements per channel run (H * W of NCHW), else 0 */
+  uint32_t reserved[6];
 } SmqPackedHeader;
+
+#define SMQ_PACK_FLAG_ALL_POSITIVE 1u
+#define SMQ_PACK_FLAG_SAFE_Q 2u
+#define SMQ_PACK_FLAG_BOTH_SIDES 4u /* T_m < 0: a mask-0 element has both outlier sides */
+#define SMQ_PACK_FLAG_BN 8u         /* the BatchNorm table follows the variable region */
 
 /* Worst-case stream size (every element an outlier and escaped) for n elements; the stream's real
  * size is header.total_bytes. */
 size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier);
+/* The same for a BN stream of bn_channels channels (+ 8 bytes per channel for its table). */
+size_t smq_smaq_pack_bound_bn(int64_t n, int num_bits_main, int num_bits_outlier,
+                              int64_t bn_channels);
 /* Workspace of smq_smaq_compress: statistics, per-block sizes, group sums / prefixes and a
  * 3 KiB scratch slot per block for its variable section (0.75 B per element); needs no
  * initialisation. */
@@ -487,8 +505,8 @@ size_t smq_smaq_pack_workspace_bytes(int64_t n);
  * (header), the variable sections moved to their prefix (one workgroup per 64 blocks; a block
  * whose section outgrew its scratch slot is re-coded from x there). No launch waits on another
  * workgroup and the host is never synchronised; the stream incl. header.total_bytes is written on
- * the device. packed_bytes >= smq_smaq_pack_bound. The BN variant and injected uniforms are not
- * supported (SMQ_ERR_INVALID). */
+ * the device. packed_bytes >= smq_smaq_pack_bound (smq_smaq_pack_bound_bn with params->bn_gamma:
+ * the BN variant, whose parameters are copied into the stream). Any threshold but NaN. */
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
                       void* packed, size_t packed_bytes, void* workspace, size_t workspace_bytes,
                       void* stream);

@@ -23,7 +23,9 @@ VERSION = 2
 BLOCK = 4096
 HEADER_BYTES = 128
 MASK_WORDS = BLOCK // 32
-_HDR = struct.Struct("<IIqIIiiIfffffddQQI36x")
+_HDR = struct.Struct("<IIqIIiiIfffffddQQIIq24x")
+FLAG_BOTH_SIDES = 4
+FLAG_BN = 8
 assert _HDR.size == HEADER_BYTES
 
 
@@ -36,17 +38,20 @@ def fixed_words(wm: int) -> int:
     return MASK_WORDS + (wm * BLOCK) // 32
 
 
-def _flags(all_positive: bool, r_main: np.float32, r_out: np.float32) -> int:
+def _flags(all_positive: bool, r_main: np.float32, r_out: np.float32, thr=1.0, bn=False) -> int:
     lim = 2.0**100
     safe_q = not (abs(float(r_main)) <= lim and abs(float(r_out)) <= lim)  # smaq_elem.h RangeRecips
-    return (1 if all_positive else 0) | (2 if safe_q else 0)
+    return ((1 if all_positive else 0) | (2 if safe_q else 0) |
+            (FLAG_BOTH_SIDES if F32(thr) < 0 else 0) | (FLAG_BN if bn else 0))
 
 
 def block_codes(q, hi, lo, wm: int, wo: int):
-    """Per element: (code, is_outlier, escaped) — smq.h packed format rules. A main code is the
-    wm-bit two's complement q; an outlier code is side << (wo - 1) | |q| (wo bits); a code outside
-    the budget is 0 (main) or the side bit alone (outlier) and the element is escaped."""
-    o = hi | lo
+    """Per element: (code, mask bit, escaped) — smq.h packed format rules. The mask bit is "exactly
+    one side" (T < 0 also gives elements with both sides: they code as main elements). A main code
+    is the wm-bit two's complement q; an outlier code is side << (wo - 1) | |q| (wo bits); a code
+    outside the budget is 0 (main) or the side bit alone (outlier) and the element is escaped."""
+    o = hi ^ lo
+    hi, lo = hi & o, lo & o
     with np.errstate(invalid="ignore"):
         main_lo, main_hi = -(2 ** (wm - 1)), 2 ** (wm - 1) - 1
         mag_max = 2 ** (wo - 1) - 1
@@ -109,7 +114,7 @@ def block_var(cb, ob, eb, qb, wm: int, wo: int) -> np.ndarray:
 
 
 def pack_block(xb, mean, std, cfg: osmaq.SmaqConfig, uniforms=None, dtype: str = "f32"):
-    """(fixed, variable) sections of one block's elements."""
+    """(fixed, variable) sections of one block's elements (no BN)."""
     wm, wo = _widths(cfg.num_bits_main, cfg.num_bits_outlier)
     q, hi, lo, _ = osmaq.codes(np.asarray(xb, F32).ravel(), mean, std, cfg, uniforms, None, dtype)
     code, o, esc = block_codes(q, hi, lo, wm, wo)
@@ -117,16 +122,24 @@ def pack_block(xb, mean, std, cfg: osmaq.SmaqConfig, uniforms=None, dtype: str =
 
 
 def pack(x, mean, std, cfg: osmaq.SmaqConfig, uniforms: Optional[np.ndarray] = None,
-         all_positive: bool = False, dtype: str = "f32") -> np.ndarray:
+         all_positive: bool = False, dtype: str = "f32", bn=None) -> np.ndarray:
     """The stream smq_smaq_compress writes, given the device statistics (mean, raw std) and the
     same uniforms. Returns uint8 bytes: header | directory (padded to an even number of entries)
-    | fixed region | variable region — every region's place but the variable one's depends on n
-    alone, and the fixed region is 16-B aligned."""
-    x = np.asarray(x, dtype=F32).ravel()
+    | fixed region | variable region [| BN table] — every region's place but the variable one's
+    depends on n alone, and the fixed region is 16-B aligned. bn = (gamma, beta) of the channels
+    of dim 1 (x NCHW; one value each for scalar parameters)."""
+    x = np.asarray(x, dtype=F32)
+    inner = 0
+    if bn is not None:
+        assert x.ndim == 4
+        inner = x.shape[2] * x.shape[3]
+        bn = tuple(np.asarray(t, F32).reshape(-1) for t in bn)
+    q, hi, lo, std1 = osmaq.codes(x, mean, std, cfg, uniforms, bn, dtype)
+    q, hi, lo = q.ravel(), hi.ravel(), lo.ravel()
+    x = x.ravel()
     n = x.size
     bm, bo = cfg.num_bits_main, cfg.num_bits_outlier
     wm, wo = _widths(bm, bo)
-    q, hi, lo, std1 = osmaq.codes(x, mean, std, cfg, uniforms, None, dtype)
     code, o, esc = block_codes(q, hi, lo, wm, wo)
     nb = (n + BLOCK - 1) // BLOCK
     fixed, var, dirs, off = [], [], [], 0
@@ -142,27 +155,32 @@ def pack(x, mean, std, cfg: osmaq.SmaqConfig, uniforms: Optional[np.ndarray] = N
     var_w = np.concatenate(var) if var else np.zeros(0, np.uint32)
     r_main, r_out = F32(cfg.range_normal), F32(cfg.range_outlier)
     nbp = nb + (nb & 1)
-    total = HEADER_BYTES + 8 * nbp + 4 * (fixed_w.size + var_w.size)
-    hdr = _HDR.pack(MAGIC, VERSION, n, BLOCK, nb, bm, bo, _flags(all_positive, r_main, r_out),
-                    F32(cfg.main_std_dev_threshold), r_main, r_out, F32(mean), F32(std1),
+    bn_tab = np.concatenate([bn[0], bn[1]]).astype(F32) if bn is not None else np.zeros(0, F32)
+    total = HEADER_BYTES + 8 * nbp + 4 * (fixed_w.size + var_w.size + bn_tab.size)
+    thr = F32(cfg.main_std_dev_threshold)
+    hdr = _HDR.pack(MAGIC, VERSION, n, BLOCK, nb, bm, bo,
+                    _flags(all_positive, r_main, r_out, thr, bn is not None),
+                    thr, r_main, r_out, F32(mean), F32(std1),
                     1.0 / float(r_main) if r_main != 0 else float("inf"),
                     1.0 / float(r_out) if r_out != 0 else float("inf"),
-                    var_w.size, total, 0)
+                    var_w.size, total, 0, bn_tab.size // 2, inner)
     dirs += [0] * (nbp - nb)
     return np.concatenate([np.frombuffer(hdr, np.uint8), np.asarray(dirs, np.uint64).view(np.uint8),
-                           fixed_w.view(np.uint8), var_w.view(np.uint8)])
+                           fixed_w.view(np.uint8), var_w.view(np.uint8), bn_tab.view(np.uint8)])
 
 
 def header(stream: np.ndarray) -> dict:
     f = _HDR.unpack(bytes(np.asarray(stream[:HEADER_BYTES], np.uint8)))
     keys = ("magic", "version", "n", "block_elems", "n_blocks", "num_bits_main",
             "num_bits_outlier", "flags", "thr", "range_main", "range_outlier", "mean", "std_dev",
-            "inv_range_main", "inv_range_outlier", "data_words", "total_bytes", "error")
+            "inv_range_main", "inv_range_outlier", "data_words", "total_bytes", "error",
+            "bn_channels", "bn_inner")
     return dict(zip(keys, f))
 
 
 def regions(stream: np.ndarray):
-    """(header dict, directory uint64[nb], fixed region uint32[nb * F], variable region uint32)."""
+    """(header dict, directory uint64[nb], fixed region uint32[nb * F], variable region uint32
+    (without a BN stream's table: bn_table())."""
     h = header(stream)
     nb = h["n_blocks"]
     wm = h["num_bits_main"] - 1
@@ -171,8 +189,19 @@ def regions(stream: np.ndarray):
     f0 = HEADER_BYTES + 8 * nbp
     fb = 4 * nb * fixed_words(wm)
     fixed_w = np.asarray(stream[f0: f0 + fb], np.uint8).view(np.uint32)
-    var_w = np.asarray(stream[f0 + fb:], np.uint8).view(np.uint32)
+    var_w = np.asarray(stream[f0 + fb: f0 + fb + 4 * h["data_words"]], np.uint8).view(np.uint32)
     return h, dirs, fixed_w, var_w
+
+
+def bn_table(stream: np.ndarray):
+    """A BN stream's (gamma, beta) (fp32, bn_channels each), after the variable region."""
+    h = header(stream)
+    nb = h["n_blocks"]
+    off = (HEADER_BYTES + 8 * (nb + (nb & 1)) + 4 * nb * fixed_words(h["num_bits_main"] - 1)
+           + 4 * h["data_words"])
+    c = h["bn_channels"]
+    t = np.asarray(stream[off: off + 8 * c], np.uint8).view(F32)
+    return t[:c], t[c:]
 
 
 def unpack(stream: np.ndarray) -> np.ndarray:
@@ -205,8 +234,9 @@ def unpack(stream: np.ndarray) -> np.ndarray:
         mag = cd & ((1 << (wo - 1)) - 1)
         qo = np.where(side == 1, -mag, mag)
         qb = np.where(ob, qo, qm).astype(F32)
-        hb = ob & (side == 0)
-        lb = ob & (side == 1)
+        both = bool(h["flags"] & FLAG_BOTH_SIDES)  # a mask-0 element has both sides
+        hb = np.where(ob, side == 0, both)
+        lb = np.where(ob, side == 1, both)
         e = var_w[base + n_ext: base + n_ext + 2 * n_esc].reshape(-1, 2)
         qb[e[:, 0].astype(np.int64)] = e[:, 1].view(F32)
         s = slice(b * BLOCK, b * BLOCK + m)
@@ -215,6 +245,15 @@ def unpack(stream: np.ndarray) -> np.ndarray:
                            main_std_dev_threshold=float(F32(h["thr"])))
     # the ranges come from the header (the compressor's fp32 constants)
     cfg_r = _RangesCfg(cfg, F32(h["range_main"]), F32(h["range_outlier"]))
+    if h["flags"] & FLAG_BN:  # per element: channel (e / inner) % channels (NCHW dim 1)
+        g, b = bn_table(stream)
+        ch = (np.arange(n, dtype=np.int64) // h["bn_inner"]) % h["bn_channels"]
+        y = osmaq.dequant(q, hi, lo, h["mean"], h["std_dev"], cfg_r, False)
+        with np.errstate(all="ignore"):
+            y = (y * g[ch]) + b[ch]
+            if h["flags"] & 1:
+                y = np.where(y < F32(0), F32(0), y)
+        return y.astype(F32)
     return osmaq.dequant(q, hi, lo, h["mean"], h["std_dev"], cfg_r, bool(h["flags"] & 1))
 
 

@@ -77,6 +77,9 @@ struct PackArgs {
   uint32_t n_groups;
   uint32_t flags;
   uint32_t lds_words;        // dynamic LDS of the packing kernels (PackLds::words)
+  const float* bn_gamma;     // BN variant (general packer only), else NULL
+  const float* bn_beta;
+  int64_t bn_channels, bn_inner;
 };
 
 // smart.py:151-169 for one element, as smaq_quant computes it (same IEEE ops in the same order, so
@@ -120,6 +123,31 @@ __device__ __forceinline__ uint32_t code_sel(float q, bool o, bool lo, uint32_t 
   return esc ? sb : ((vv ^ hsel) | sb);
 }
 
+// The general packer's element (EXT kernels: the BN variant, T_m <= 0): smaq_quant itself, the
+// apply's own function, with the BN term of element e. The mask bit is "exactly one side" (o); an
+// element with both sides (T_m < 0) codes as a main element; lo_side = below -T_m alone.
+template <int RM, int TIN, bool SUB>
+__device__ __forceinline__ float ext_quant(const PackArgs& A, float v, float u, const ElemConsts& c,
+                                           int64_t e, bool& o, bool& lo_side) {
+  bool hi, lo;
+  float q;
+  if (A.bn_gamma) {
+    const int64_t ch = (e / A.bn_inner) % A.bn_channels;
+    q = smaq_quant<RM, true, TIN, SUB>(v, u, c, hi, lo, BnTerm{A.bn_gamma[ch], A.bn_beta[ch]});
+  } else {
+    q = smaq_quant<RM, false, TIN, SUB>(v, u, c, hi, lo);
+  }
+  o = hi != lo;
+  lo_side = lo && !hi;
+  return q;
+}
+
+// The packer's z-score threshold: in the input type, but fp32 for BN (the parameters promote).
+template <int TIN>
+__device__ __forceinline__ float pack_cthr(const PackArgs& A) {
+  return (TIN == kF32 || A.bn_gamma) ? A.thr : round_in<TIN>(A.thr);
+}
+
 // OR a chunk of up to 64 bits at bit pos of an LDS bit stream (two or three words; the third only
 // when bits land there).
 __device__ __forceinline__ void or_bits64(uint32_t* base, uint32_t pos, uint64_t chunk) {
@@ -157,7 +185,8 @@ struct PackLds {
 // at b * F, outlier ranks and escapes -> the variable section in the block's scratch slot (unless
 // it outgrows kVarCap or a segment's escape list: then the var kernel re-codes the block), the
 // section's size -> meta / the group sum.
-template <int RM, int TIN, bool VEC, bool FULL, bool SUB, int WM, int WO>
+// EXT: the general element (ext_quant; instantiated with runtime widths only).
+template <int RM, int TIN, bool VEC, bool FULL, bool SUB, int WM, int WO, bool EXT>
 __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, uint32_t* lds) {
   constexpr int kWE = (WM > 0 && WO > 0) ? (WO > WM ? WO - WM : 0) : -1;  // -1: runtime
   const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
@@ -172,8 +201,7 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
   uint32_t* elist = ext + 128 * we;                  // [kSegs][kSegEsc][2]
   uint32_t* seg = elist + 2 * kSegs * kSegEsc;
   ElemConsts c;
-  const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
-  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, pack_cthr<TIN>(A));
   float xv[4][4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -225,7 +253,10 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       bool o, lo, esc;
-      qv[i] = pack_quant<RM, TIN, SUB>(xv[k][i], u[i], c, o, lo);
+      if (EXT)
+        qv[i] = ext_quant<RM, TIN, SUB>(A, xv[k][i], u[i], c, e0 + el + i, o, lo);
+      else
+        qv[i] = pack_quant<RM, TIN, SUB>(xv[k][i], u[i], c, o, lo);
       code[i] = code_sel(qv[i], o, lo, hm, side, lim_m, esc);
       const bool valid = FULL || el + i < n_el;
       if (!FULL) code[i] = valid ? code[i] : 0u;
@@ -384,15 +415,15 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
 
 // One workgroup per full block, in reverse address order: the statistics sweep just read x front
 // to back, so its tail is still in the Infinity Cache. The short last block has its own launch.
-template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO>
+template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO, bool EXT>
 __global__ __launch_bounds__(kBlock) void smaq_pack_block_kernel(PackArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t b = FULL ? A.n_full - 1 - blockIdx.x : A.n_blocks - 1;
   // the subnormal-quotient check only where quot_check_for() asks for it (one uniform branch)
   if (A.stats->quot_check)
-    pack_block_body<RM, TIN, VEC, FULL, true, WM, WO>(A, b, lds);
+    pack_block_body<RM, TIN, VEC, FULL, true, WM, WO, EXT>(A, b, lds);
   else
-    pack_block_body<RM, TIN, VEC, FULL, false, WM, WO>(A, b, lds);
+    pack_block_body<RM, TIN, VEC, FULL, false, WM, WO, EXT>(A, b, lds);
 }
 
 constexpr int kScanThreads = 1024;
@@ -454,12 +485,22 @@ __global__ __launch_bounds__(kScanThreads) void smaq_pack_scan_kernel(PackArgs A
     h->inv_range_main = A.inv_r_main;
     h->inv_range_outlier = A.inv_r_out;
     h->data_words = carry;
+    const uint64_t bn_words = A.bn_gamma ? 2ull * (uint64_t)A.bn_channels : 0ull;
     h->total_bytes = sizeof(SmqPackedHeader) + 8ull * dir_entries(A.n_blocks) +
-                     4ull * A.n_blocks * fixed_words(A.wm) + 4ull * carry;
+                     4ull * A.n_blocks * fixed_words(A.wm) + 4ull * (carry + bn_words);
     h->error = 0u;
+    h->bn_channels = A.bn_gamma ? (uint32_t)A.bn_channels : 0u;
+    h->bn_inner = A.bn_gamma ? A.bn_inner : 0;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) h->reserved[i] = 0u;
+    for (int i = 0; i < 6; ++i) h->reserved[i] = 0u;
     if (A.n_blocks & 1u) A.dir[A.n_blocks] = 0ull;  // the directory's padding entry
+  }
+  if (A.bn_gamma) {  // the BN table after the variable region (which the var kernel fills next)
+    float* t = reinterpret_cast<float*>(A.var + carry);
+    for (int64_t i = tid; i < A.bn_channels; i += kScanThreads) {
+      t[i] = A.bn_gamma[i];
+      t[A.bn_channels + i] = A.bn_beta[i];
+    }
   }
 }
 
@@ -469,7 +510,7 @@ __global__ __launch_bounds__(kScanThreads) void smaq_pack_scan_kernel(PackArgs A
 // 16 passes of 256 consecutive elements, one per thread; outlier and escape ranks by wave ballots
 // and the passes' running totals; the outlier bits are ORed into LDS (ext, 128 * we words) and
 // copied out at the end, the escapes are written directly.
-template <int RM, int TIN>
+template <int RM, int TIN, bool EXT>
 __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_dst, uint32_t* ext,
                                    uint32_t* s_cnt) {
   const int wm = A.wm, wo = A.wo, we = wo > wm ? wo - wm : 0;
@@ -477,8 +518,7 @@ __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_d
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = (int)min((int64_t)kPB, A.n - e0);
   ElemConsts c;
-  const float cthr = (TIN == kF32) ? A.thr : round_in<TIN>(A.thr);
-  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+  init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, pack_cthr<TIN>(A));
   const uint32_t hm = 1u << (wm - 1), side = 1u << (wo - 1);
   for (uint32_t i = tid; i < 128u * (uint32_t)we; i += kBlock) ext[i] = 0u;
   __syncthreads();
@@ -497,7 +537,8 @@ __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_d
       uint32_t code = 0u;
       if (el < n_el) {
         const float u = (RM == kRoundHash) ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)(e0 + el)) : 0.0f;
-        q = pack_quant<RM, TIN, true>(load1<TIN>(A.x, e0 + el), u, c, o, lo);
+        q = EXT ? ext_quant<RM, TIN, true>(A, load1<TIN>(A.x, e0 + el), u, c, e0 + el, o, lo)
+                : pack_quant<RM, TIN, true>(load1<TIN>(A.x, e0 + el), u, c, o, lo);
         code = code_sel(q, o, lo, hm, side, 2u * hm, esc);
       }
       const unsigned long long bo = __ballot(o), be = __ballot(esc);
@@ -536,7 +577,7 @@ __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_d
 // every fourth block from its scratch slot to the stream (a lane copies words lane, lane + 64, ...;
 // four blocks' loads in flight before their stores); blocks whose section outgrew the slot are
 // re-coded from x by the whole workgroup (recode_var_section).
-template <int RM, int TIN, int WM, int WO>
+template <int RM, int TIN, int WM, int WO, bool EXT>
 __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // re-code: 128 * we words
   __shared__ uint32_t s_off[kGroup + 1];   // group-relative word offsets (s_off[64] = total)
@@ -609,34 +650,36 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A) {
   for (unsigned long long m = over; m; m &= m - 1) {
     const uint32_t j = (uint32_t)__builtin_ctzll(m);
     __syncthreads();
-    recode_var_section<RM, TIN>(A, b0 + j, base + s_off[j], lds, s_cnt);
+    recode_var_section<RM, TIN, EXT>(A, b0 + j, base + s_off[j], lds, s_cnt);
   }
 }
 
-template <int RM, int TIN, int WM, int WO>
+template <int RM, int TIN, int WM, int WO, bool EXT>
 void launch_pack_w(const PackArgs& A, bool vec, hipStream_t st) {
   const size_t lds = 4 * (size_t)A.lds_words;
   if (A.n_full > 0) {
     if (vec)
-      hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, true, true, WM, WO>), dim3(A.n_full),
+      hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, true, true, WM, WO, EXT>), dim3(A.n_full),
                          dim3(kBlock), lds, st, A);
     else
-      hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, false, true, WM, WO>), dim3(A.n_full),
-                         dim3(kBlock), lds, st, A);
+      hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, false, true, WM, WO, EXT>),
+                         dim3(A.n_full), dim3(kBlock), lds, st, A);
   }
   if (A.n_full < A.n_blocks)
-    hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, false, false, WM, WO>), dim3(1),
+    hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, false, false, WM, WO, EXT>), dim3(1),
                        dim3(kBlock), lds, st, A);
   hipLaunchKernelGGL(smaq_pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, A);
   const int we = A.wo > A.wm ? A.wo - A.wm : 0;
-  hipLaunchKernelGGL((smaq_pack_var_kernel<RM, TIN, WM, WO>), dim3(A.n_groups), dim3(kBlock),
+  hipLaunchKernelGGL((smaq_pack_var_kernel<RM, TIN, WM, WO, EXT>), dim3(A.n_groups), dim3(kBlock),
                      4 * 128 * (size_t)(we > 0 ? we : 1), st, A);
 }
 
+// ext: the BN variant or T_m <= 0 (ext_quant, runtime widths); else the packer's own element.
 template <int RM, int TIN>
-void launch_pack(const PackArgs& A, bool vec, hipStream_t st) {
-  if (A.wm == 5 && A.wo == 7) launch_pack_w<RM, TIN, 5, 7>(A, vec, st);  // the 6/8-bit default
-  else launch_pack_w<RM, TIN, 0, 0>(A, vec, st);
+void launch_pack(const PackArgs& A, bool vec, bool ext, hipStream_t st) {
+  if (ext) launch_pack_w<RM, TIN, 0, 0, true>(A, vec, st);
+  else if (A.wm == 5 && A.wo == 7) launch_pack_w<RM, TIN, 5, 7, false>(A, vec, st);  // 6/8-bit default
+  else launch_pack_w<RM, TIN, 0, 0, false>(A, vec, st);
 }
 
 // ---- decoder ------------------------------------------------------------------------------------
@@ -662,17 +705,48 @@ struct UnpackArgs {
 // arithmetic, same bits.
 constexpr int kLutMax = 512;
 
-// q and the outlier sides of a full code (plane bits | outlier bits << wm).
-__device__ __forceinline__ float decode_code(uint32_t v, bool is_o, int wm, int wo, bool& hi,
-                                             bool& lo) {
+// q and the outlier sides of a full code (plane bits | outlier bits << wm). both: a mask-0
+// element has both sides (SMQ_PACK_FLAG_BOTH_SIDES, T_m < 0).
+__device__ __forceinline__ float decode_code(uint32_t v, bool is_o, int wm, int wo, bool both,
+                                             bool& hi, bool& lo) {
   const uint32_t side_bit = 1u << (wo - 1);
   const uint32_t cm = v & ((1u << wm) - 1u);
   const float qm = (float)(((int32_t)(cm << (32 - wm))) >> (32 - wm));  // sign-extend
   const int mag = (int)(v & (side_bit - 1u));
-  lo = is_o && (v & side_bit);
-  hi = is_o && !(v & side_bit);
-  return is_o ? (float)(lo ? -mag : mag) : qm;
+  const bool sb = (v & side_bit) != 0u;
+  lo = is_o ? sb : both;
+  hi = is_o ? !sb : both;
+  return is_o ? (float)(sb ? -mag : mag) : qm;
 }
+
+// A BN stream's table (SMQ_PACK_FLAG_BN): gamma[c], beta[c] of element e, c = (e / inner) % C
+// (C, inner < 2^31). Per block the channel c0 and run offset r0 of its first element (two 64-bit
+// divisions per block); an element j of the block then needs 32-bit ones only (a 64-bit division
+// per element took 14 more VGPRs in the default decoder than it has).
+struct BnTable {
+  const float* gamma;
+  const float* beta;
+  uint32_t channels, inner;
+  uint32_t c0, r0;
+  __device__ __forceinline__ void block(int64_t e0) {
+    c0 = (uint32_t)((e0 / inner) % channels);
+    r0 = (uint32_t)(e0 % inner);
+  }
+  // channel and run offset of block element j
+  __device__ __forceinline__ void locate(uint32_t j, uint32_t& ch, uint32_t& r) const {
+    const uint32_t t = r0 + j, k = t / inner;
+    r = t - k * inner;
+    ch = (c0 + k) % channels;
+  }
+  // the next element's
+  __device__ __forceinline__ void step(uint32_t& ch, uint32_t& r) const {
+    if (++r == inner) {
+      r = 0u;
+      if (++ch == channels) ch = 0u;
+    }
+  }
+  __device__ __forceinline__ BnTerm term(uint32_t ch) const { return BnTerm{gamma[ch], beta[ch]}; }
+};
 
 // dynamic LDS of the decoder (words): fixed image, variable section (when it fits kVarCap), mask
 // prefix counts, escape bitmask and its prefix counts, decode table
@@ -742,16 +816,19 @@ __device__ __forceinline__ UnpackLoads unpack_issue(const UnpackGeom& G) {
 }
 
 // Decode one block whose loads unpack_issue requested (the decode table, if any, is in LDS).
-template <bool AP, bool SQ, bool FULL, int WM, int WO>
+// BN: the stream's BatchNorm table applies (the decode table then holds values before it).
+template <bool AP, bool SQ, bool FULL, int WM, int WO, bool BN>
 __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
                                               const UnpackGeom& G, const UnpackLoads& L, int wm_rt,
-                                              int wo_rt, uint32_t* lds) {
+                                              int wo_rt, bool both, BnTable bt,
+                                              uint32_t* lds) {
   constexpr bool kLut = WM > 0 && WM <= 8 && WO > 0 && WO <= 8;
   const int wm = WM > 0 ? WM : wm_rt, wo = WO > 0 ? WO : wo_rt;
   const int we = wo > wm ? wo - wm : 0;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int64_t e0 = (int64_t)b * kPB;
   const int n_el = FULL ? kPB : (int)(A.n - e0);
+  if (BN) bt.block(e0);
   const uint32_t F = G.F, n_esc = G.n_esc, n_ext = G.n_ext, sh = G.sh, nvec = G.nvec;
   const bool var_lds = G.var_lds;
   const uint32_t* vsrc = G.vsrc;
@@ -841,26 +918,36 @@ __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemCon
       }
     }
     float o[4];
+    uint32_t bch = 0u, brun = 0u;  // BN: the element's channel and offset in its run
+    if (BN) bt.locate((uint32_t)el0, bch, brun);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool is_o = (nib >> i) & 1u;
       bool hi, lo;
       float q;
+      if (BN && i > 0) bt.step(bch, brun);
+      const BnTerm bn = BN ? bt.term(bch) : BnTerm{1.0f, 0.0f};
       if (kLut) {
         o[i] = lut[is_o ? (1u << WM) + cd[i] : cd[i]];
-        if (__builtin_expect(!((enib >> i) & 1u), 1)) continue;
-        decode_code(cd[i], is_o, wm, wo, hi, lo);
-      } else {
-        q = decode_code(cd[i], is_o, wm, wo, hi, lo);
         if (__builtin_expect(!((enib >> i) & 1u), 1)) {
-          o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
+          if (BN) {  // smaq_dequant's last two statements on the table's value
+            o[i] = (o[i] * bn.gamma) + bn.beta;
+            if (AP) o[i] = (o[i] < 0.0f) ? 0.0f : o[i];
+          }
+          continue;
+        }
+        decode_code(cd[i], is_o, wm, wo, both, hi, lo);
+      } else {
+        q = decode_code(cd[i], is_o, wm, wo, both, hi, lo);
+        if (__builtin_expect(!((enib >> i) & 1u), 1)) {
+          o[i] = smaq_dequant<BN, AP, SQ>(q, hi, lo, c, bn);
           continue;
         }
       }
       // an escape: its q from the list, rank in O(1)
       const uint32_t s = sh0 + (uint32_t)i;
       q = __uint_as_float(esc[2u * (epc[wi] + __popc(em & ((1u << s) - 1u))) + 1u]);
-      o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
+      o[i] = smaq_dequant<BN, AP, SQ>(q, hi, lo, c, bn);
     }
     float* y = A.y + e0 + el0;
     if (A.vec && (FULL || el0 + 3 < n_el)) {
@@ -875,10 +962,11 @@ __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemCon
 
 // Decode table of narrow codes (kLut), once per workgroup: every main and outlier code de-quantised.
 template <bool AP, bool SQ, int WM, int WO>
-__device__ __forceinline__ void unpack_lut(const ElemConsts& c, uint32_t* lds, uint32_t F) {
+__device__ __forceinline__ void unpack_lut(const ElemConsts& c, bool both, uint32_t* lds,
+                                           uint32_t F) {
   float* lut = reinterpret_cast<float*>(lds + F + kVarCap + 4 + 3 * kMaskWords);
   for (int i = threadIdx.x; i < (1 << WM) + (1 << WO); i += kBlock) {
-    bool hi = false, lo = false;
+    bool hi = both, lo = both;
     float q;
     if (i < (1 << WM)) {
       q = (float)(((int32_t)((uint32_t)i << (32 - WM))) >> (32 - WM));  // sign-extend
@@ -895,12 +983,25 @@ __device__ __forceinline__ void unpack_lut(const ElemConsts& c, uint32_t* lds, u
 
 // The workgroup's kUnpackPer consecutive blocks: every block's loads first, the decode table while
 // they are in flight, then the blocks one after another (an LDS barrier between them).
-template <bool AP, bool SQ, bool FULL, int WM, int WO>
+template <bool AP, bool SQ, bool FULL, int WM, int WO, bool BN>
 __device__ __forceinline__ void unpack_blocks(const UnpackArgs& A, const ElemConsts& c, uint32_t b0,
                                               int nblk, const uint64_t* dent, int wm, int wo,
-                                              uint32_t* lds) {
+                                              bool both, const BnTable& bt, uint32_t* lds) {
   constexpr bool kLut = WM > 0 && WM <= 8 && WO > 0 && WO <= 8;
   const int we = wo > wm ? wo - wm : 0;
+  if constexpr (BN) {
+    // the BN variant one block at a time: no second block's loads held in registers while the
+    // table terms are (the default decoder keeps its 67 VGPRs, 7 waves per SIMD)
+    for (int i = 0; i < nblk; ++i) {
+      if (i > 0) __syncthreads();
+      const UnpackGeom G = unpack_geom(A, b0 + i, dent[i], wm, we);
+      const UnpackLoads L = unpack_issue(G);
+      if constexpr (kLut)
+        if (i == 0) unpack_lut<false, SQ, WM, WO>(c, both, lds, G.F);
+      unpack_decode<AP, SQ, FULL, WM, WO, BN>(A, c, b0 + i, G, L, wm, wo, both, bt, lds);
+    }
+    return;
+  }
   UnpackGeom G[kUnpackPer];
   UnpackLoads L[kUnpackPer];
 #pragma unroll
@@ -909,12 +1010,12 @@ __device__ __forceinline__ void unpack_blocks(const UnpackArgs& A, const ElemCon
       G[i] = unpack_geom(A, b0 + i, dent[i], wm, we);
       L[i] = unpack_issue(G[i]);
     }
-  if constexpr (kLut) unpack_lut<AP, SQ, WM, WO>(c, lds, G[0].F);
+  if constexpr (kLut) unpack_lut<AP, SQ, WM, WO>(c, both, lds, G[0].F);
 #pragma unroll
   for (int i = 0; i < kUnpackPer; ++i) {
     if (i >= nblk) break;
     if (i > 0) __syncthreads();  // the previous block's LDS reads are done
-    unpack_decode<AP, SQ, FULL, WM, WO>(A, c, b0 + i, G[i], L[i], wm, wo, lds);
+    unpack_decode<AP, SQ, FULL, WM, WO, BN>(A, c, b0 + i, G[i], L[i], wm, wo, both, bt, lds);
   }
 }
 
@@ -956,11 +1057,27 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   c.inv_r_main = h->inv_range_main;
   c.inv_r_out = h->inv_range_outlier;
   const uint32_t f = h->flags;
-#define SMQ_UNPACK(APV, SQV) unpack_blocks<APV, SQV, FULL, WM, WO>(A, c, b0, nblk, dent, wm, wo, lds)
-  if (f & 2u) {
-    if (f & 1u) SMQ_UNPACK(true, true); else SMQ_UNPACK(false, true);
+  const bool both = (f & SMQ_PACK_FLAG_BOTH_SIDES) != 0u;
+  BnTable bt;
+  bt.gamma = reinterpret_cast<const float*>(A.var + h->data_words);
+  bt.channels = h->bn_channels;
+  bt.beta = bt.gamma + bt.channels;
+  bt.inner = (uint32_t)h->bn_inner;
+  bt.c0 = bt.r0 = 0u;
+#define SMQ_UNPACK(APV, SQV, BNV) \
+  unpack_blocks<APV, SQV, FULL, WM, WO, BNV>(A, c, b0, nblk, dent, wm, wo, both, bt, lds)
+  if (f & SMQ_PACK_FLAG_BN) {  // the BN variant
+    if (bt.channels < 1 || bt.channels > 0x7fffffffu || h->bn_inner < 1 || h->bn_inner > 0x7fffffff)
+      return;
+    if (f & SMQ_PACK_FLAG_SAFE_Q) {
+      if (f & SMQ_PACK_FLAG_ALL_POSITIVE) SMQ_UNPACK(true, true, true); else SMQ_UNPACK(false, true, true);
+    } else {
+      if (f & SMQ_PACK_FLAG_ALL_POSITIVE) SMQ_UNPACK(true, false, true); else SMQ_UNPACK(false, false, true);
+    }
+  } else if (f & SMQ_PACK_FLAG_SAFE_Q) {
+    if (f & SMQ_PACK_FLAG_ALL_POSITIVE) SMQ_UNPACK(true, true, false); else SMQ_UNPACK(false, true, false);
   } else {
-    if (f & 1u) SMQ_UNPACK(true, false); else SMQ_UNPACK(false, false);
+    if (f & SMQ_PACK_FLAG_ALL_POSITIVE) SMQ_UNPACK(true, false, false); else SMQ_UNPACK(false, false, false);
   }
 #undef SMQ_UNPACK
 }
@@ -1000,6 +1117,12 @@ size_t smq_smaq_pack_bound(int64_t n, int num_bits_main, int num_bits_outlier) {
   return sizeof(SmqPackedHeader) + 8 * (size_t)dir_entries((int64_t)nb) + 4 * nb * per_block;
 }
 
+size_t smq_smaq_pack_bound_bn(int64_t n, int num_bits_main, int num_bits_outlier,
+                              int64_t bn_channels) {
+  return smq_smaq_pack_bound(n, num_bits_main, num_bits_outlier) +
+         8 * (size_t)(bn_channels > 0 ? bn_channels : 0);
+}
+
 size_t smq_smaq_pack_workspace_bytes(int64_t n) { return PackWs(n).total; }
 
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* packed,
@@ -1023,12 +1146,13 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
               kMaxWidth + 1, kMaxWidth + 1);
     return SMQ_ERR_INVALID;
   }
-  if (!(p->main_std_dev_threshold > 0.0f)) {
-    set_error("compress: needs main_std_dev_threshold > 0 (outlier sides must be exclusive)");
+  if (p->main_std_dev_threshold != p->main_std_dev_threshold) {
+    set_error("compress: main_std_dev_threshold is NaN");
     return SMQ_ERR_INVALID;
   }
-  if (p->bn_gamma) {
-    set_error("compress: the BatchNorm variant is not supported by the packed container");
+  if (p->bn_gamma && (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1 ||
+                      p->bn_channels > 0x7fffffffLL || p->bn_inner > 0x7fffffffLL)) {
+    set_error("compress: BN variant needs bn_beta, 1 <= bn_channels, bn_inner < 2^31");
     return SMQ_ERR_INVALID;
   }
   if (p->stats_source != SMQ_STATS_WORKSPACE && p->stats_source != SMQ_STATS_SAMPLED &&
@@ -1041,10 +1165,11 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
     set_error("compress: tensor too large (%lld elements)", (long long)n);
     return SMQ_ERR_INVALID;
   }
-  const size_t bound = smq_smaq_pack_bound(n, p->num_bits_main, p->num_bits_outlier);
+  const size_t bound = smq_smaq_pack_bound_bn(n, p->num_bits_main, p->num_bits_outlier,
+                                              p->bn_gamma ? p->bn_channels : 0);
   if (packed_bytes < bound) {
-    set_error("compress: packed buffer too small: need %zu bytes (smq_smaq_pack_bound), got %zu",
-              bound, packed_bytes);
+    set_error("compress: packed buffer too small: need %zu bytes (smq_smaq_pack_bound%s), got %zu",
+              bound, p->bn_gamma ? "_bn" : "", packed_bytes);
     return SMQ_ERR_WORKSPACE;
   }
   const PackWs L(n);
@@ -1091,7 +1216,13 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.offset = p->offset;
   A.n_blocks = (uint32_t)nb;
   A.n_full = (uint32_t)(n / kPB);
-  A.flags = (p->all_positive ? 1u : 0u) | (R.safe_q ? 2u : 0u);
+  A.bn_gamma = p->bn_gamma;
+  A.bn_beta = p->bn_beta;
+  A.bn_channels = p->bn_gamma ? p->bn_channels : 0;
+  A.bn_inner = p->bn_gamma ? p->bn_inner : 0;
+  A.flags = (p->all_positive ? SMQ_PACK_FLAG_ALL_POSITIVE : 0u) | (R.safe_q ? SMQ_PACK_FLAG_SAFE_Q : 0u) |
+            (A.thr < 0.0f ? SMQ_PACK_FLAG_BOTH_SIDES : 0u) | (p->bn_gamma ? SMQ_PACK_FLAG_BN : 0u);
+  const bool ext = p->bn_gamma || !(A.thr > 0.0f);
   A.lds_words = PackLds::words(A.wm, we);
   const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
   const bool sr = p->stochastic_rounding != 0;
@@ -1101,14 +1232,14 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
     return SMQ_ERR_LAUNCH;
   }
   if (dtype == SMQ_DTYPE_F32) {
-    if (sr) launch_pack<kRoundHash, kF32>(A, vec, st);
-    else launch_pack<kRoundTrunc, kF32>(A, vec, st);
+    if (sr) launch_pack<kRoundHash, kF32>(A, vec, ext, st);
+    else launch_pack<kRoundTrunc, kF32>(A, vec, ext, st);
   } else if (dtype == SMQ_DTYPE_F16) {
-    if (sr) launch_pack<kRoundHash, kF16>(A, vec, st);
-    else launch_pack<kRoundTrunc, kF16>(A, vec, st);
+    if (sr) launch_pack<kRoundHash, kF16>(A, vec, ext, st);
+    else launch_pack<kRoundTrunc, kF16>(A, vec, ext, st);
   } else {
-    if (sr) launch_pack<kRoundHash, kBF16>(A, vec, st);
-    else launch_pack<kRoundTrunc, kBF16>(A, vec, st);
+    if (sr) launch_pack<kRoundHash, kBF16>(A, vec, ext, st);
+    else launch_pack<kRoundTrunc, kBF16>(A, vec, ext, st);
   }
   return check_launch("smaq_pack_block_kernel / smaq_pack_var_kernel");
 }

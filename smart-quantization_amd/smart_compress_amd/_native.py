@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get(
     "SMQ_LIB", os.path.join(os.path.dirname(_PKG_DIR), "lib", "libsmq.so")
 )
 
-SMQ_ABI_VERSION = 4
+SMQ_ABI_VERSION = 5
 SMQ_MAX_SAMPLES = 64
 SMQ_MAX_DEVICE_SAMPLES = 4096
 SMQ_MAX_DRAW_SAMPLES = 1 << 28
@@ -115,12 +115,18 @@ class SmqPackedHeader(ctypes.Structure):
         ("data_words", ctypes.c_uint64),
         ("total_bytes", ctypes.c_uint64),
         ("error", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32 * 9),
+        ("bn_channels", ctypes.c_uint32),
+        ("bn_inner", ctypes.c_int64),
+        ("reserved", ctypes.c_uint32 * 6),
     ]
 
 
 SMQ_PACK_MAGIC = 0x50514D53
 SMQ_PACK_BLOCK = 4096
+SMQ_PACK_FLAG_ALL_POSITIVE = 1
+SMQ_PACK_FLAG_SAFE_Q = 2
+SMQ_PACK_FLAG_BOTH_SIDES = 4
+SMQ_PACK_FLAG_BN = 8
 
 
 class SmqTensorDesc(ctypes.Structure):
@@ -252,6 +258,7 @@ SIGNATURES = {
     ),
     "smq_rng_u32": (ctypes.c_uint32, [_U64, _U64]),
     "smq_smaq_pack_bound": (_SZ, [_I64, _I32, _I32]),
+    "smq_smaq_pack_bound_bn": (_SZ, [_I64, _I32, _I32, _I64]),
     "smq_smaq_pack_workspace_bytes": (_SZ, [_I64]),
     "smq_smaq_compress": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams),
                                          _P, _SZ, _P, _SZ, _P]),

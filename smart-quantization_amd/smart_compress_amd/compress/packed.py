@@ -15,9 +15,11 @@ the container of include/smq.h ("Packed SmaQ container"):
 * ``__call__`` = decompress(compress(x)), a drop-in SmaQ codec whose ``new_size`` log is the real
   stream size.
 
-Same flags as ``SmartFP`` (it is a subclass); not supported: the BatchNorm variant and
-``main_std_dev_threshold <= 0`` (outlier sides must be exclusive). ``compress`` reads the stream
-size back from the device (one host synchronisation) to return a right-sized buffer.
+Same flags as ``SmartFP`` (it is a subclass), incl. the BatchNorm variant (smart.py:136-149,
+174-179: the stream carries the compress-time gamma / beta, so ``decompress`` needs no arguments)
+and any threshold (``main_std_dev_threshold < 0``: an element above -T and below T at once is the
+third state smart.py:157-161 gives it). ``compress`` reads the stream size back from the device
+(one host synchronisation) to return a right-sized buffer.
 """
 
 import ctypes
@@ -76,10 +78,8 @@ class SmartFPPacked(SmartFP):
         if numel < hp.min_size:  # smart.py:123-128: kept as is
             raw = data.detach().to(torch.float32).contiguous().reshape(-1).view(torch.uint8)
             return SmaqPacked(raw.clone(), data.shape, numel, raw=True)
-        if batch_norm_stats is not None and hp.use_batch_norm:
-            raise NotImplementedError("SmartFPPacked: the BatchNorm variant is not supported")
-        if not hp.main_std_dev_threshold > 0:
-            raise NotImplementedError("SmartFPPacked: needs main_std_dev_threshold > 0")
+        if hp.main_std_dev_threshold != hp.main_std_dev_threshold:
+            raise NotImplementedError("SmartFPPacked: main_std_dev_threshold is NaN")
         if hp.use_sample_stats and min(numel, hp.num_samples) > N.SMQ_MAX_DEVICE_SAMPLES:
             raise NotImplementedError(
                 f"SmartFPPacked: --num_samples above {N.SMQ_MAX_DEVICE_SAMPLES} is not supported")
@@ -93,12 +93,17 @@ class SmartFPPacked(SmartFP):
         x = data.contiguous()
         lib = N.lib()
         p = self._params(numel, all_positive, x.dtype, x.device)
-        bound = lib.smq_smaq_pack_bound(numel, hp.num_bits_main, hp.num_bits_outlier)
+        keep = None
+        if hp.use_batch_norm and batch_norm_stats is not None:
+            keep = self._bind_batch_norm(p, x, batch_norm_stats)
+        bound = lib.smq_smaq_pack_bound_bn(numel, hp.num_bits_main, hp.num_bits_outlier,
+                                           p.bn_channels if keep is not None else 0)
         scratch = N.workspace("smaq_pack_out", x.device, bound)
         ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(numel))
         N.check(lib.smq_smaq_compress(x.data_ptr(), code, numel, p, scratch.data_ptr(),
                                       scratch.numel(), ws.data_ptr(), ws.numel(),
                                       N.stream_ptr(x.device)), "smq_smaq_compress")
+        del keep
         # host sync: the stream size, for a right-sized buffer
         total = int(scratch[_TOTAL_OFF:_TOTAL_OFF + 8].cpu().numpy().view(np.uint64)[0])
         return SmaqPacked(scratch[:total].clone(), data.shape, numel,

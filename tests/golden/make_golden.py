@@ -174,6 +174,13 @@ def gen_smaq(out_dir):
     case("bf16_trunc", normal(n), ["--no_stochastic_rounding"], dtype=torch.bfloat16, precision=16)
     case("bf16_sampled", normal(n), ["--use_sample_stats"], dtype=torch.bfloat16, precision=16)
     case("bf16_range", normal(n), ["--use_range_std_dev"], dtype=torch.bfloat16, precision=16)
+    # negative thresholds (T = 0 divides by zero at smart.py:78; T < 0 gives, smart.py:157-161,
+    # elements above -T and below T at once) — appended, so the cases above keep their draws
+    case("thr_neg", normal(n), ["--main_std_dev_threshold", "-0.5"])
+    case("thr_neg_trunc", normal(n), ["--main_std_dev_threshold", "-1.25", "--no_stochastic_rounding"])
+    case("f16_thr_neg", normal(n), ["--main_std_dev_threshold", "-0.5"], **h16)
+    case("bn_thr_neg", x4, ["--use_batch_norm", "--main_std_dev_threshold", "-0.5"], bn=(gam, bet),
+         all_positive=True)
 
     index = {}
     for name, x, argv, allpos, bn, precision in cases:

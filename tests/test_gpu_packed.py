@@ -146,12 +146,109 @@ def test_rejections():
     from smart_compress_amd.compress import SmartFPPacked
 
     with pytest.raises(NotImplementedError):
-        SmartFPPacked(smaq_hparams(main_std_dev_threshold=-1.0)).compress(
+        SmartFPPacked(smaq_hparams(main_std_dev_threshold=float("nan"))).compress(
             torch.randn(100, device="cuda"))
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError):  # the BN variant needs NCHW (smart.py:145 permutes 4 dims)
         SmartFPPacked(smaq_hparams(use_batch_norm=True)).compress(
-            torch.randn(2, 3, 4, 4, device="cuda"),
+            torch.randn(2, 3, 16, device="cuda"),
             batch_norm_stats=(torch.ones(3, device="cuda"), torch.zeros(3, device="cuda")))
+
+
+def _bn_stream_vs_oracle(x, packed, hp, seed, offset, bn, all_positive):
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from oracle import smaq_packed as P
+
+    h = packed.header()
+    cfg = osmaq.SmaqConfig(num_bits_main=hp.num_bits_main, num_bits_outlier=hp.num_bits_outlier,
+                           main_std_dev_threshold=hp.main_std_dev_threshold,
+                           outlier_std_dev_threshold=hp.outlier_std_dev_threshold,
+                           stochastic_rounding=hp.stochastic_rounding, precision=hp.precision)
+    u = orng.uniforms(seed, offset, x.numel()) if hp.stochastic_rounding else None
+    x_np = x.float().cpu().numpy()
+    bn_np = None if bn is None else tuple(t.float().cpu().numpy() for t in bn)
+    dt = {torch.float32: "f32", torch.float16: "f16", torch.bfloat16: "bf16"}[x.dtype]
+    return P.pack(x_np, h["mean"], h["std_dev"], cfg, u, all_positive, dt, bn_np)
+
+
+@pytest.mark.parametrize("thr", [-0.5, -1.25, -3.0])
+@pytest.mark.parametrize("bits", [(6, 8), (4, 6), (9, 12)])
+@pytest.mark.parametrize("sr", [True, False])
+def test_negative_threshold(thr, bits, sr):
+    """main_std_dev_threshold < 0 (smart.py:157-161): elements above -T and below T at once are the
+    third state (mask 0, main code, both sides in the decoder): round trip == SmartFP, stream ==
+    the oracle's (whose unpack is pinned to the reference's thr_neg goldens)."""
+    from oracle import smaq_packed as P
+
+    hp, pk, ref = _codecs(seed=9, offset=4, main_std_dev_threshold=thr, num_bits_main=bits[0],
+                          num_bits_outlier=bits[1], stochastic_rounding=sr)
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(3 * 4096 + 555, generator=gen, device="cuda") * 1.5 + 0.2
+    packed = pk.compress(x)
+    y = pk.decompress(packed)
+    y_ref = ref(x)
+    torch.cuda.synchronize()
+    assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), n_diff_f32(y.cpu().numpy(),
+                                                                      y_ref.cpu().numpy())
+    raw = packed.data.cpu().numpy()
+    assert P.header(raw)["flags"] & P.FLAG_BOTH_SIDES
+    assert np.array_equal(raw, _bn_stream_vs_oracle(x, packed, hp, 9, 4, None, False))
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 6, 5), (4, 64, 32, 32), (50, 1000, 1, 1), (3, 17, 7, 7),
+                                   (1, 3, 100, 100)])
+@pytest.mark.parametrize("bits", [(6, 8), (4, 6)])
+def test_batch_norm_variant(shape, bits):
+    """The BN variant (smart.py:136-149, 174-179): per-channel (x - beta) / gamma before the
+    z-score, * gamma + beta after; the stream carries the parameters (decompress needs none).
+    Channel runs shorter than, equal to and longer than a block (inner 1, 25, 49, 1024, 10000),
+    the default widths (decode table) and others; all_positive after the BN term; scalar
+    parameters; a negative threshold on top. Round trip == SmartFP, stream == the oracle's."""
+    from oracle import smaq_packed as P
+
+    C = shape[1]
+    gen = torch.Generator(device="cuda").manual_seed(C)
+    x = torch.randn(shape, generator=gen, device="cuda") * 2.0 + 0.3
+    gam = torch.rand(C, generator=gen, device="cuda") + 0.5
+    bet = torch.randn(C, generator=gen, device="cuda") * 0.1
+    for over, allpos in ((dict(), False), (dict(), True), (dict(bn_scalar_params=True), False),
+                         (dict(main_std_dev_threshold=-0.5), True),
+                         (dict(stochastic_rounding=False), False)):
+        hp, pk, ref = _codecs(seed=5, offset=2, use_batch_norm=True, num_bits_main=bits[0],
+                              num_bits_outlier=bits[1], **over)
+        packed = pk.compress(x, all_positive=allpos, batch_norm_stats=(gam, bet))
+        y = pk.decompress(packed)
+        y_ref = ref(x, all_positive=allpos, batch_norm_stats=(gam, bet))
+        torch.cuda.synchronize()
+        assert y.shape == x.shape
+        assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), (over, allpos, n_diff_f32(
+            y.cpu().numpy(), y_ref.cpu().numpy()))
+        raw = packed.data.cpu().numpy()
+        h = P.header(raw)
+        assert h["flags"] & P.FLAG_BN and h["bn_inner"] == shape[2] * shape[3]
+        bn = (gam.mean().reshape(1), bet.mean().reshape(1)) if over.get("bn_scalar_params") \
+            else (gam, bet)
+        assert h["bn_channels"] == bn[0].numel()
+        assert np.array_equal(raw, _bn_stream_vs_oracle(x, packed, hp, 5, 2, bn, allpos)), over
+        if x.numel() <= 1 << 16:
+            assert same_f32(P.unpack(raw).reshape(shape), y.cpu().numpy())
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_batch_norm_half_inputs(dt):
+    """Half inputs with fp32 BN parameters: the data are promoted to fp32 (z-score in fp32)."""
+    hp, pk, ref = _codecs(seed=3, offset=0, use_batch_norm=True, precision=16)
+    gen = torch.Generator(device="cuda").manual_seed(4)
+    x = (torch.randn(4, 16, 12, 12, generator=gen, device="cuda") * 3).to(dt)
+    gam = torch.rand(16, generator=gen, device="cuda") + 0.5
+    bet = torch.randn(16, generator=gen, device="cuda") * 0.1
+    packed = pk.compress(x, batch_norm_stats=(gam, bet))
+    y = pk.decompress(packed)
+    y_ref = ref(x, batch_norm_stats=(gam, bet))
+    torch.cuda.synchronize()
+    assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
+    assert np.array_equal(packed.data.cpu().numpy(),
+                          _bn_stream_vs_oracle(x, packed, hp, 3, 0, (gam, bet), False))
 
 
 def test_large_multiblock():

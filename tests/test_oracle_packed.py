@@ -1,7 +1,7 @@
 """The packed SmaQ container's restatement (oracle/smaq_packed.py) against the reference.
 
-unpack(pack(x)) must reproduce smart.py's outputs bit for bit: checked on every golden case the
-container supports (all but the BatchNorm variant), with the reference's own statistics and
+unpack(pack(x)) must reproduce smart.py's outputs bit for bit: checked on every golden case (the
+BatchNorm variant and negative thresholds included), with the reference's own statistics and
 recorded rand_like draws; plus escape-heavy inputs (NaN, +-inf, huge outliers, wrong-sign codes)
 and ragged sizes, where it must equal oracle.smaq.apply.
 """
@@ -12,8 +12,7 @@ import pytest
 from helpers import load_smaq, n_diff_f32, oracle_cfg, same_f32, smaq_cases
 
 CASES = smaq_cases()
-PACKABLE = sorted(k for k, m in CASES.items() if not k.startswith("n7")
-                  and not m.get("use_batch_norm") and m["main_std_dev_threshold"] > 0)
+PACKABLE = sorted(k for k in CASES if not k.startswith("n7"))  # (n7: below min_size, kept raw)
 
 
 @pytest.mark.parametrize("name", PACKABLE)
@@ -21,13 +20,17 @@ def test_packed_roundtrip_matches_reference(name):
     from oracle import smaq_packed as P
 
     meta, d = CASES[name], load_smaq(name)
+    bn = None
     if "bn_gamma" in d:
-        pytest.skip("BatchNorm variant")
+        bn = (d["bn_gamma_used"], d["bn_beta_used"]) if meta["bn_scalar_params"] else (
+            d["bn_gamma"], d["bn_beta"])
     cfg = oracle_cfg(meta)
     st = P.pack(d["x"], d["mean"], d["std"], cfg, d.get("uniforms"), meta["all_positive"],
-                meta["dtype"])
+                meta["dtype"], bn)
     h = P.header(st)
     assert h["total_bytes"] == st.size and h["n"] == d["x"].size
+    assert bool(h["flags"] & P.FLAG_BN) == (bn is not None)
+    assert bool(h["flags"] & P.FLAG_BOTH_SIDES) == (meta["main_std_dev_threshold"] < 0)
     y = P.unpack(st).reshape(d["y"].shape)
     assert same_f32(y, d["y"]), n_diff_f32(y, d["y"])
 
