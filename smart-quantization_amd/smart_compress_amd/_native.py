@@ -392,6 +392,13 @@ def device_index(device: torch.device) -> int:
     return device.index if device.index is not None else torch.cuda.current_device()
 
 
+def raw_stream(index: int) -> int:
+    """The current stream of device ``index`` as a hipStream_t value (one C call)."""
+    if _raw_stream is not None:
+        return _raw_stream(index)
+    return torch.cuda.current_stream(index).cuda_stream
+
+
 def stream_ptr(device: torch.device) -> int:
     if _raw_stream is not None:
         return _raw_stream(device_index(device))
