@@ -659,12 +659,17 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, ElemConsts& c
     const int64_t nv = n >> 2;
     const int64_t tile = A.reverse ? (int64_t)(gridDim.x - 1 - blockIdx.x) : (int64_t)blockIdx.x;
     const int64_t t0 = tile * (kBlock * TV) + threadIdx.x;
+    // fp16 inputs (no BN term) in pairs of raw halves: smaq_elem_f16x2 (interleaved A/B at 256M:
+    // apply 5.15 -> 5.34 TB/s event-timed, profiles/r3c_ab_f16pk.txt)
+    constexpr bool RAW16 = !BN && TIN == kF16;
     float4 v[TV], uu[TV];
+    uint2 hv[TV];
 #pragma unroll
     for (int u = 0; u < TV; ++u) {
       const int64_t j = t0 + u * kBlock;
       if (j < nv) {
-        v[u] = A.nt_loads ? load4_stream<TIN>(A.x, j) : load4<TIN>(A.x, j);
+        if constexpr (RAW16) hv[u] = static_cast<const uint2*>(A.x)[j];
+        else v[u] = A.nt_loads ? load4_stream<TIN>(A.x, j) : load4<TIN>(A.x, j);
         if (RM == kRoundUniform) uu[u] = u4[j];
       }
     }
@@ -681,10 +686,15 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, ElemConsts& c
       }
       bool b0, b1, b2, b3;
       float4 o;
-      o.x = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].x, u0, c, b0, bn_term<BN>(A, 4 * j + 0));
-      o.y = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].y, u1, c, b1, bn_term<BN>(A, 4 * j + 1));
-      o.z = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].z, u2, c, b2, bn_term<BN>(A, 4 * j + 2));
-      o.w = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].w, u3, c, b3, bn_term<BN>(A, 4 * j + 3));
+      if constexpr (RAW16) {
+        smaq_elem_f16x2<RM, AP>(hv[u].x, u0, u1, c, o.x, o.y, b0, b1);
+        smaq_elem_f16x2<RM, AP>(hv[u].y, u2, u3, c, o.z, o.w, b2, b3);
+      } else {
+        o.x = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].x, u0, c, b0, bn_term<BN>(A, 4 * j + 0));
+        o.y = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].y, u1, c, b1, bn_term<BN>(A, 4 * j + 1));
+        o.z = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].z, u2, c, b2, bn_term<BN>(A, 4 * j + 2));
+        o.w = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].w, u3, c, b3, bn_term<BN>(A, 4 * j + 3));
+      }
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
       store_stream(y4 + j, o);
     }

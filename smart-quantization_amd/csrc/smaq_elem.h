@@ -369,6 +369,48 @@ __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c
   return smaq_dequant<BN, AP, SQ>(q, hi, lo, c, bn);
 }
 
+// smart.py:155-169 from the z-score on (smaq_quant's tail, no BN term): the code q and the sides.
+template <int RM>
+__device__ __forceinline__ float smaq_quant_z(float z, float u, const ElemConsts& c, bool& hi,
+                                              bool& lo) {
+  hi = z > c.cthr;
+  lo = z < c.cnthr;
+  const bool o = hi | lo;
+  const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);
+  const float r = o ? c.r_out : c.r_main;
+  const float d = (z + a) * r;
+  if (RM == kRoundTrunc) return truncf(d);
+  const float f = floorf(d);
+  const float fr = d - f;
+  float t = ((RM == kRoundHash) ? __builtin_fmaf(u, -0x1p-24f, fr) : (fr - u)) + 0.5f;
+  t = (t < 0.0f) ? 0.0f : t;
+  return f + __builtin_rintf(t);
+}
+
+// Two fp16 elements (raw bits, low half first) through smart.py:154-182: data - mean as ONE
+// v_pk_add_f16 (RN16(v - mean) directly, which round_in<kF16>(v - mean) emulates through fp32) and
+// both z-scores rounded to fp16 by ONE v_cvt_pk_f16_f32 (RNE, as __float2half_rn); the rest of the
+// chain per element, exactly smaq_elem<RM, false, kF16, AP, SUB>.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+template <int RM, bool AP>
+__device__ __forceinline__ void smaq_elem_f16x2(uint32_t raw, float u0, float u1,
+                                                const ElemConsts& c, float& o0, float& o1,
+                                                bool& b0, bool& b1) {
+  const _Float16 m = (_Float16)c.mean;  // exact: the mean is an fp16 value
+  const h2v dh = __builtin_bit_cast(h2v, raw) - h2v{m, m};
+  const float dm0 = (float)dh.x, dm1 = (float)dh.y;
+  const f2v z = __builtin_convertvector(
+      __builtin_convertvector(f2v{half_quot<kF16>(dm0, c), half_quot<kF16>(dm1, c)}, h2v), f2v);
+  bool hi0, lo0, hi1, lo1;
+  const float q0 = smaq_quant_z<RM>(z.x, u0, c, hi0, lo0);
+  const float q1 = smaq_quant_z<RM>(z.y, u1, c, hi1, lo1);
+  b0 = hi0 | lo0;
+  b1 = hi1 | lo1;
+  o0 = smaq_dequant<false, AP, false>(q0, hi0, lo0, c);
+  o1 = smaq_dequant<false, AP, false>(q1, hi1, lo1, c);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Device-drawn sampled statistics (SMQ_STATS_SAMPLED_DEVICE): smart.py:86-91 with the randperm
 // of line 88 replaced by Floyd's algorithm on the device, so every call — and every replay of a
