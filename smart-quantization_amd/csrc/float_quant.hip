@@ -472,22 +472,31 @@ __device__ __forceinline__ float s2fp8_fwd(float xv, uint32_t r, float alpha, fl
 
 // s2_fwd_fast from lg = log2f(|x|) (the single launch keeps it from its statistics pass); an
 // element whose code the fast power's error could change (s2_fast_uncertain, margin E) takes powf.
+// The callers run it only with 0 < alpha < inf (`fast`), so Y = exp2(alpha lg) * 2^beta is +0..+inf
+// or the default (positive) NaN of 0 * inf: t never has its sign bit, which makes three shortcuts
+// exact (round 3, -10 VALU ns per element of the transform):
+//   * qtorch's clip_exponent (exponent > 142 -> +57344) and check_inf (+57344 -> +inf) are one
+//     unsigned compare, qn >= bits(57344): qn has two mantissa bits, so that is "exponent above 142,
+//     or 57344 itself", and the +inf / NaN patterns lie above it too;
+//   * the subnormal path's shift is the constant +2^-14, and "subnormal" is t < bits(2^-14);
+//   * a zero x (lg = -inf) needs no exclusion from the uncertainty test: Y = 0 on both paths, so a
+//     recompute changes nothing.
+// A NaN lg (NaN x) always takes the accurate path.
 __device__ __forceinline__ uint32_t s2_fwd_fast_lg(float xv, float lg, uint32_t r, float alpha,
                                                    float bp2, int check_inf, float max_value,
                                                    uint32_t E) {
   const float Y = __builtin_amdgcn_exp2f(alpha * lg) * bp2;
   const uint32_t t = __builtin_bit_cast(uint32_t, Y);
-  const uint32_t rm = r & 0x1fffffu;            // (1 << (23 - man)) - 1
-  uint32_t qn = (t + rm) & 0xffe00000u;          // round_bitwise
-  qn = ((qn >> 23) & 0xffu) > 142u ? ((t & 0x80000000u) | 0x47600000u) : qn;  // clip_exponent
-  const float sh = __builtin_bit_cast(float, 0x38800000u | (t & 0x80000000u));  // 2^-14
-  const float vs = Y + sh;
-  const uint32_t vsb = __builtin_bit_cast(uint32_t, vs);
-  const float qs = __builtin_bit_cast(float, (vsb + rm) & 0xffe00000u) - sh;
-  const bool sub = (t & 0x7f800000u) < 0x38800000u;
-  uint32_t T = sub ? __builtin_bit_cast(uint32_t, qs) : qn;
-  if (check_inf) T = (T == 0x47600000u) ? 0x7f800000u : T;
-  if (__builtin_expect(s2_fast_uncertain(sub ? vsb : t, rm, E, lg), 0))
+  const uint32_t rm = r & 0x1fffffu;                 // (1 << (23 - man)) - 1
+  const uint32_t qn = (t + rm) & 0xffe00000u;        // round_bitwise
+  const uint32_t clip = check_inf ? 0x7f800000u : 0x47600000u;
+  const uint32_t tn = qn >= 0x47600000u ? clip : qn;  // clip_exponent + check_inf
+  const uint32_t vsb = __builtin_bit_cast(uint32_t, Y + 0x1p-14f);
+  const float qs = __builtin_bit_cast(float, (vsb + rm) & 0xffe00000u) - 0x1p-14f;
+  const bool sub = t < 0x38800000u;
+  uint32_t T = sub ? __builtin_bit_cast(uint32_t, qs) : tn;
+  const uint32_t L = ((sub ? vsb : t) + rm) & 0x1fffffu;
+  if (__builtin_expect((L - E >= 0x200000u - 2u * E) || lg != lg, 0))
     T = __builtin_bit_cast(uint32_t, s2fp8_fwd<false>(xv, r, alpha, bp2, check_inf, max_value, 0));
   return T;
 }

@@ -229,3 +229,27 @@ def test_workspace_created_in_capture_keeps_counters_across_replays():
     torch.cuda.synchronize()
     # replay 2 equals the host's 3rd and 4th calls
     assert torch.equal(_bits(y1), _bits(refs[2])) and torch.equal(_bits(y2), _bits(refs[3]))
+
+
+@pytest.mark.parametrize("check_inf", [True, False])
+def test_s2fp8_class_eager_path_equals_c_abi(check_inf):
+    """S2FP8.__call__'s fp32 device path (its own stream query and cached workspace) returns what
+    smq_s2fp8_roundtrip returns for the same seed and stream position, for contiguous and strided
+    inputs, and advances the host stream by n per call."""
+    import smart_compress_amd.compress as C
+    from smart_compress_amd.util.pytorch import quantization as Q
+
+    g = _g()
+    hp = C.S2FP8.add_argparse_args(ArgumentParser()).parse_args([])
+    hp.precision = 32
+    hp.float_quantize_check_inf = check_inf
+    c = C.S2FP8(hp)
+    r = Q.quant_rng()
+    base = torch.randn(96, 4097, device="cuda") * 3
+    for x in (base, base[:, 1:], base.t()):
+        start = r.offset
+        y = c(x, tag="t")
+        assert r.offset == start + x.numel()
+        ref, _ = g.s2fp8(x.contiguous(), check_inf=check_inf, seed=r.seed, offset=start)
+        assert y.shape == x.shape and y.dtype == torch.float32
+        assert torch.equal(_bits(y.contiguous()), _bits(ref))
