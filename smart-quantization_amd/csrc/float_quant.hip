@@ -472,33 +472,42 @@ __device__ __forceinline__ float s2fp8_fwd(float xv, uint32_t r, float alpha, fl
 
 // s2_fwd_fast from lg = log2f(|x|) (the single launch keeps it from its statistics pass); an
 // element whose code the fast power's error could change (s2_fast_uncertain, margin E) takes powf.
-// The callers run it only with 0 < alpha < inf (`fast`), so Y = exp2(alpha lg) * 2^beta is +0..+inf
-// or the default (positive) NaN of 0 * inf: t never has its sign bit, which makes three shortcuts
-// exact (round 3, -10 VALU ns per element of the transform):
+// The callers run it only with 0 < alpha < inf (`fast`). Every element's log2|x| entered the
+// statistics, so a NaN or infinite x would have made alpha NaN or 0: here x is finite, lg is not
+// NaN, and Y = exp2(alpha lg) * 2^beta is +0 .. +inf or the default (positive) NaN of 0 * inf. Y
+// never has its sign bit, which makes these shortcuts exact (round 3; oracle/csrc/s2_clip_check.c
+// checks every such Y):
 //   * qtorch's clip_exponent (exponent > 142 -> +57344) and check_inf (+57344 -> +inf) are one
-//     unsigned compare, qn >= bits(57344): qn has two mantissa bits, so that is "exponent above 142,
-//     or 57344 itself", and the +inf / NaN patterns lie above it too;
-//   * the subnormal path's shift is the constant +2^-14, and "subnormal" is t < bits(2^-14);
-//   * a zero x (lg = -inf) needs no exclusion from the uncertainty test: Y = 0 on both paths, so a
-//     recompute changes nothing.
-// A NaN lg (NaN x) always takes the accurate path.
+//     unsigned compare, t + rm >= bits(57344): after the rounding's mask that is "exponent above
+//     142, or 57344 itself", and the +inf / NaN patterns lie above it too;
+//   * the subnormal path's shift is the constant +2^-14, "subnormal" is t < bits(2^-14), and both
+//     paths round the same sum (t or bits(Y + 2^-14)) + rm, whose low 21 bits the uncertainty test
+//     reads;
+//   * a zero x (lg = -inf) needs no exclusion from that test: Y = 0 on both paths.
+// Returns the code in bits 21..31 (what the inverse table is indexed by); bits 0..20 are unspecified.
 __device__ __forceinline__ uint32_t s2_fwd_fast_lg(float xv, float lg, uint32_t r, float alpha,
                                                    float bp2, int check_inf, float max_value,
                                                    uint32_t E) {
   const float Y = __builtin_amdgcn_exp2f(alpha * lg) * bp2;
   const uint32_t t = __builtin_bit_cast(uint32_t, Y);
-  const uint32_t rm = r & 0x1fffffu;                 // (1 << (23 - man)) - 1
-  const uint32_t qn = (t + rm) & 0xffe00000u;        // round_bitwise
-  const uint32_t clip = check_inf ? 0x7f800000u : 0x47600000u;
-  const uint32_t tn = qn >= 0x47600000u ? clip : qn;  // clip_exponent + check_inf
   const uint32_t vsb = __builtin_bit_cast(uint32_t, Y + 0x1p-14f);
-  const float qs = __builtin_bit_cast(float, (vsb + rm) & 0xffe00000u) - 0x1p-14f;
   const bool sub = t < 0x38800000u;
-  uint32_t T = sub ? __builtin_bit_cast(uint32_t, qs) : tn;
-  const uint32_t L = ((sub ? vsb : t) + rm) & 0x1fffffu;
-  if (__builtin_expect((L - E >= 0x200000u - 2u * E) || lg != lg, 0))
+  const uint32_t sum = (sub ? vsb : t) + (r & 0x1fffffu);  // round_bitwise's sum, either path
+  const float qs = __builtin_bit_cast(float, sum & 0xffe00000u) - 0x1p-14f;
+  const uint32_t clip = check_inf ? 0x7f800000u : 0x47600000u;
+  uint32_t T = sub ? __builtin_bit_cast(uint32_t, qs) : (sum >= 0x47600000u ? clip : sum);
+  if (__builtin_expect((sum & 0x1fffffu) - E >= 0x200000u - 2u * E, 0))
     T = __builtin_bit_cast(uint32_t, s2fp8_fwd<false>(xv, r, alpha, bp2, check_inf, max_value, 0));
   return T;
+}
+
+// torch.sign(x) for a FINITE x (the fast paths): +-1, and +0 for +-0. x * 2^127 * 2^127 maps every
+// nonzero finite x to at least 2^105 in magnitude (the smallest subnormal is 2^-149) or to +-inf,
+// the + 0 turns -0 into +0, and the median with -1 and 1 clamps: three ops instead of two compares
+// and two selects.
+__device__ __forceinline__ float s2_sign_finite(float x) {
+  const float s = __builtin_fmaf(x * 0x1p127f, 0x1p127f, 0.0f);
+  return __builtin_amdgcn_fmed3f(s, -1.0f, 1.0f);
 }
 
 __device__ __forceinline__ uint32_t s2_fwd_fast(float xv, uint32_t r, float alpha, float bp2,
@@ -657,16 +666,15 @@ __global__ __launch_bounds__(kBlock) void s2fp8_apply_kernel(S2Args A) {
     for (int u = 0; u < kFqTileV; ++u)
 #pragma unroll
       for (int k = 0; k < 4; ++k) t2[u][k] = lut[T[u][k] >> 21];
-    auto sgn = [](float xv) { return (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f); };
 #pragma unroll
     for (int u = 0; u < kFqTileV; ++u) {
       const int64_t j = t0 + u * kBlock;
       if (j >= nv) continue;
       float4 o;
-      o.x = t2[u][0] * sgn(v[u].x);
-      o.y = t2[u][1] * sgn(v[u].y);
-      o.z = t2[u][2] * sgn(v[u].z);
-      o.w = t2[u][3] * sgn(v[u].w);
+      o.x = t2[u][0] * s2_sign_finite(v[u].x);
+      o.y = t2[u][1] * s2_sign_finite(v[u].y);
+      o.z = t2[u][2] * s2_sign_finite(v[u].z);
+      o.w = t2[u][3] * s2_sign_finite(v[u].w);
       store4_out<HOUT>(A.y, j, o);
     }
     if (tile == last_tile && threadIdx.x < (int)(n & 3)) {
@@ -1109,16 +1117,15 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
         T[u][q] = s2_fwd_fast_lg(xq, lg[u][q], rw[u][q], alpha, bp2, A.check_inf, A.max_value, E);
       }
     }
-    auto sgn = [](float xv) { return (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f); };
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       const int64_t j = base + (int64_t)u * kS2FT;
       if (j >= A.nv) continue;
       float4 o;
-      o.x = lut[T[u][0] >> 21] * sgn(v[u].x);
-      o.y = lut[T[u][1] >> 21] * sgn(v[u].y);
-      o.z = lut[T[u][2] >> 21] * sgn(v[u].z);
-      o.w = lut[T[u][3] >> 21] * sgn(v[u].w);
+      o.x = lut[T[u][0] >> 21] * s2_sign_finite(v[u].x);
+      o.y = lut[T[u][1] >> 21] * s2_sign_finite(v[u].y);
+      o.z = lut[T[u][2] >> 21] * s2_sign_finite(v[u].z);
+      o.w = lut[T[u][3] >> 21] * s2_sign_finite(v[u].w);
       store_stream(reinterpret_cast<float4*>(A.y) + j, o);
     }
   } else {
