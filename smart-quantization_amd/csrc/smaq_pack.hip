@@ -799,7 +799,8 @@ __device__ __forceinline__ UnpackLoads unpack_issue(const UnpackGeom& G) {
   constexpr int kRV = (kVarCap + 4 + 4 * kBlock - 1) / (4 * kBlock);
   static_assert(kRV == 1, "one 16-B window per lane covers the variable section");
   if ((uint32_t)tid < G.nvec) {
-    const uint4* src = reinterpret_cast<const uint4*>((uintptr_t)G.vsrc - 4u * G.sh);
+    // (pointer arithmetic, not an integer round trip: it stays a global pointer, no flat loads)
+    const uint4* src = reinterpret_cast<const uint4*>(G.vsrc - G.sh);
     if (4u * tid + 4u <= G.sh + G.var_words) {
       L.vv = src[tid];
     } else {
@@ -817,7 +818,15 @@ __device__ __forceinline__ UnpackLoads unpack_issue(const UnpackGeom& G) {
 
 // Decode one block whose loads unpack_issue requested (the decode table, if any, is in LDS).
 // BN: the stream's BatchNorm table applies (the decode table then holds values before it).
-template <bool AP, bool SQ, bool FULL, int WM, int WO, bool BN>
+// M (where the variable section is read from): kVarLds — the block's section fits kVarCap and is
+// in LDS, read through an LDS pointer; kVarMem — it does not, read from the stream; kVarAny — either,
+// chosen per block. Through a pointer that may be global or LDS the reads are flat loads, and a flat
+// load waits (vmcnt) for every store its wave has in flight: each 4-element slot with an outlier
+// waited for the previous slot's output store. The full-block launch therefore decodes only kVarLds
+// blocks, and a second launch (smaq_unpack_big_kernel) the rare others.
+enum UnpackVarMode { kVarAny = 0, kVarLds = 1, kVarMem = 2 };
+
+template <bool AP, bool SQ, bool FULL, int WM, int WO, bool BN, int M>
 __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemConsts& c, uint32_t b,
                                               const UnpackGeom& G, const UnpackLoads& L, int wm_rt,
                                               int wo_rt, bool both, BnTable bt,
@@ -845,7 +854,7 @@ __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemCon
   for (uint32_t i = tid + kBlock; i < nf4; i += kBlock) reinterpret_cast<uint4*>(fx)[i] = fsrc[i];
   if ((uint32_t)tid < nvec) reinterpret_cast<uint4*>(vs)[tid] = L.vv;
   __syncthreads();
-  const uint32_t* ext = var_lds ? vs + sh : vsrc;
+  const uint32_t* ext = M == kVarLds ? vs + sh : (M == kVarMem ? vsrc : (var_lds ? vs + sh : vsrc));
   const uint32_t* esc = ext + n_ext;
   if (tid < kWave) {  // wave 0: exclusive popcount prefix of the 128 outlier-mask words
     const uint32_t a = __popc(fx[2 * lane]), bb = __popc(fx[2 * lane + 1]);
@@ -983,7 +992,7 @@ __device__ __forceinline__ void unpack_lut(const ElemConsts& c, bool both, uint3
 
 // The workgroup's kUnpackPer consecutive blocks: every block's loads first, the decode table while
 // they are in flight, then the blocks one after another (an LDS barrier between them).
-template <bool AP, bool SQ, bool FULL, int WM, int WO, bool BN>
+template <bool AP, bool SQ, bool FULL, int WM, int WO, bool BN, int M>
 __device__ __forceinline__ void unpack_blocks(const UnpackArgs& A, const ElemConsts& c, uint32_t b0,
                                               int nblk, const uint64_t* dent, int wm, int wo,
                                               bool both, const BnTable& bt, uint32_t* lds) {
@@ -998,7 +1007,8 @@ __device__ __forceinline__ void unpack_blocks(const UnpackArgs& A, const ElemCon
       const UnpackLoads L = unpack_issue(G);
       if constexpr (kLut)
         if (i == 0) unpack_lut<false, SQ, WM, WO>(c, both, lds, G.F);
-      unpack_decode<AP, SQ, FULL, WM, WO, BN>(A, c, b0 + i, G, L, wm, wo, both, bt, lds);
+      if ((M == kVarLds && !G.var_lds) || (M == kVarMem && G.var_lds)) continue;  // the other launch's
+      unpack_decode<AP, SQ, FULL, WM, WO, BN, M>(A, c, b0 + i, G, L, wm, wo, both, bt, lds);
     }
     return;
   }
@@ -1015,32 +1025,33 @@ __device__ __forceinline__ void unpack_blocks(const UnpackArgs& A, const ElemCon
   for (int i = 0; i < kUnpackPer; ++i) {
     if (i >= nblk) break;
     if (i > 0) __syncthreads();  // the previous block's LDS reads are done
-    unpack_decode<AP, SQ, FULL, WM, WO, BN>(A, c, b0 + i, G[i], L[i], wm, wo, both, bt, lds);
+    if ((M == kVarLds && !G[i].var_lds) || (M == kVarMem && G[i].var_lds)) continue;
+    unpack_decode<AP, SQ, FULL, WM, WO, BN, M>(A, c, b0 + i, G[i], L[i], wm, wo, both, bt, lds);
   }
 }
 
-// FULL: the full blocks [0, n_full), kUnpackPer per workgroup; else the one short last block.
-// WM / WO: the 6/8-bit default's widths, or 0 (any widths, from the caller or the header).
-template <int WM, int WO, bool FULL>
-__global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t g = A.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
-  const uint32_t b0 = FULL ? g * (uint32_t)kUnpackPer : A.nb - 1;
-  const int nblk = FULL ? (int)min((uint32_t)kUnpackPer, A.n_full - b0) : 1;
-  uint64_t dent[kUnpackPer];
-#pragma unroll
-  for (int i = 0; i < kUnpackPer; ++i) dent[i] = i < nblk ? A.dir[b0 + i] : 0ull;
+// The widths a decoder launch works with: the caller's, else the header's (false: a corrupt header).
+__device__ __forceinline__ bool unpack_widths(UnpackArgs& A, int& wm, int& wo) {
   const SmqPackedHeader* h = A.hdr;
-  int wm, wo;
   if (A.var) {  // widths from the caller: the fixed and variable sections' addresses do not wait
     wm = A.wm;  // for the header; a stream of other widths (or n, magic) is left alone
     wo = A.wo;
-  } else {
-    wm = h->num_bits_main - 1;
-    wo = h->num_bits_outlier - 1;
-    if (wm < 1 || wm > kMaxWidth || wo < 2 || wo > kMaxWidth) return;
-    A.var = A.fixed + (size_t)A.nb * fixed_words(wm);
+    return true;
   }
+  wm = h->num_bits_main - 1;
+  wo = h->num_bits_outlier - 1;
+  if (wm < 1 || wm > kMaxWidth || wo < 2 || wo > kMaxWidth) return false;
+  A.var = A.fixed + (size_t)A.nb * fixed_words(wm);
+  return true;
+}
+
+// nblk blocks from b0 (directory entries dent) with the header's constants and flags.
+template <int WM, int WO, bool FULL, int M>
+__device__ __forceinline__ void unpack_run(UnpackArgs A, uint32_t b0, int nblk, const uint64_t* dent,
+                                           uint32_t* lds) {
+  const SmqPackedHeader* h = A.hdr;
+  int wm, wo;
+  if (!unpack_widths(A, wm, wo)) return;
   if (h->magic != SMQ_PACK_MAGIC || h->version != SMQ_PACK_VERSION || h->n != A.n ||
       h->num_bits_main != wm + 1 || h->num_bits_outlier != wo + 1 ||
       unpack_lds_words(wm) * 4u > A.lds_bytes || (WM > 0 && (wm != WM || wo != WO)))
@@ -1065,7 +1076,7 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   bt.inner = (uint32_t)h->bn_inner;
   bt.c0 = bt.r0 = 0u;
 #define SMQ_UNPACK(APV, SQV, BNV) \
-  unpack_blocks<APV, SQV, FULL, WM, WO, BNV>(A, c, b0, nblk, dent, wm, wo, both, bt, lds)
+  unpack_blocks<APV, SQV, FULL, WM, WO, BNV, M>(A, c, b0, nblk, dent, wm, wo, both, bt, lds)
   if (f & SMQ_PACK_FLAG_BN) {  // the BN variant
     if (bt.channels < 1 || bt.channels > 0x7fffffffu || h->bn_inner < 1 || h->bn_inner > 0x7fffffff)
       return;
@@ -1080,6 +1091,49 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
     if (f & SMQ_PACK_FLAG_ALL_POSITIVE) SMQ_UNPACK(true, false, false); else SMQ_UNPACK(false, false, false);
   }
 #undef SMQ_UNPACK
+}
+
+// FULL: the full blocks [0, n_full), kUnpackPer per workgroup, those whose variable section is in
+// LDS (kVarLds); else the one short last block (kVarAny).
+// WM / WO: the 6/8-bit default's widths, or 0 (any widths, from the caller or the header).
+template <int WM, int WO, bool FULL>
+__global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t g = A.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  const uint32_t b0 = FULL ? g * (uint32_t)kUnpackPer : A.nb - 1;
+  const int nblk = FULL ? (int)min((uint32_t)kUnpackPer, A.n_full - b0) : 1;
+  uint64_t dent[kUnpackPer];
+#pragma unroll
+  for (int i = 0; i < kUnpackPer; ++i) dent[i] = i < nblk ? A.dir[b0 + i] : 0ull;
+  unpack_run<WM, WO, FULL, FULL ? kVarLds : kVarAny>(A, b0, nblk, dent, lds);
+}
+
+// The full blocks whose variable section outgrew kVarCap (escape-heavy data; none on N(0,1)):
+// kBlock directory entries per workgroup, the listed blocks decoded from the stream one by one.
+template <int WM, int WO>
+__global__ __launch_bounds__(kBlock) void smaq_unpack_big_kernel(UnpackArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t list[kBlock];
+  __shared__ uint32_t n_list;
+  int wm, wo;
+  UnpackArgs W = A;
+  if (!unpack_widths(W, wm, wo)) return;
+  const int we = wo > wm ? wo - wm : 0;
+  if (threadIdx.x == 0) n_list = 0u;
+  __syncthreads();
+  const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+  if (b < A.n_full) {
+    const uint64_t d = A.dir[b];
+    const uint32_t n_out = (uint32_t)(d >> 38) & 0x1fffu, n_esc = (uint32_t)(d >> 51);
+    if (ext_words(we, n_out) + 2u * n_esc > (uint32_t)kVarCap) list[atomicAdd(&n_list, 1u)] = b;
+  }
+  __syncthreads();
+  const uint32_t m = n_list;
+  for (uint32_t i = 0; i < m; ++i) {
+    __syncthreads();  // the previous block's LDS reads are done
+    const uint64_t d = A.dir[list[i]];
+    unpack_run<WM, WO, true, kVarMem>(A, list[i], 1, &d, lds);
+  }
 }
 
 inline bool aligned_to(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
@@ -1285,9 +1339,12 @@ static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int 
   const bool w57 = bm == 6 && bo == 8;  // the default widths, known from the caller
 #define SMQ_UNPACK_LAUNCH(WMV, WOV)                                                                \
   do {                                                                                            \
-    if (grid)                                                                                     \
+    if (grid) {                                                                                   \
       hipLaunchKernelGGL((smaq_unpack_kernel<WMV, WOV, true>), dim3(grid), dim3(kBlock),           \
                          A.lds_bytes, st, A);                                                     \
+      hipLaunchKernelGGL((smaq_unpack_big_kernel<WMV, WOV>), dim3((A.n_full + kBlock - 1) / kBlock), \
+                         dim3(kBlock), A.lds_bytes, st, A);                                       \
+    }                                                                                             \
     if (A.n_full < A.nb)                                                                          \
       hipLaunchKernelGGL((smaq_unpack_kernel<WMV, WOV, false>), dim3(1), dim3(kBlock), A.lds_bytes, \
                          st, A);                                                                  \

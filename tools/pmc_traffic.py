@@ -31,6 +31,7 @@ SHORT = {
     "s2fp8_apply_kernel": "s2fp8_apply_kernel",
     "smaq_pack_kernel": "smaq_pack_kernel",
     "smaq_unpack_kernel": "smaq_unpack_kernel",
+    "smaq_unpack_big_kernel": "smaq_unpack_big_kernel",
     "smaq_pack_block_kernel": "smaq_pack_block_kernel",
     "smaq_pack_var_kernel": "smaq_pack_var_kernel",
     "smaq_pack_scan_kernel": "smaq_pack_scan_kernel",
