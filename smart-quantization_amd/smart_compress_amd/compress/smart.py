@@ -30,6 +30,20 @@ from .. import _native as N
 from ..util.globals import profile
 from .base import CompressionAlgorithmBase
 
+_F32 = {}
+_WS_BYTES = {}  # (numel, device-drawn samples or -1) -> workspace bytes
+
+
+def _f32(v: float) -> float:
+    """The fp32 value of a Python number (what torch's fp32 scalar ops see), memoised: the flags'
+    constants repeat on every call, and a numpy conversion costs ~0.75 us of host time each."""
+    r = _F32.get(v)
+    if r is None:
+        if len(_F32) > 1024:  # (NaN keys never hit; keep the table bounded)
+            _F32.clear()
+        r = _F32[v] = float(np.float32(v))
+    return r
+
 # (flag, argparse kwargs) exactly as smart.py:11-70 declares them
 _SMAQ_FLAGS = (
     ("--num_samples", dict(type=int, default=16,
@@ -126,11 +140,11 @@ class SmartFP(CompressionAlgorithmBase):
         p = N.SmqSmaqParams()
         p.num_bits_main = hp.num_bits_main
         p.num_bits_outlier = hp.num_bits_outlier
-        p.main_std_dev_threshold = float(np.float32(hp.main_std_dev_threshold))
-        p.range_main = float(np.float32(self.range_normal))
-        p.range_outlier = float(np.float32(self.range_outlier))
-        p.clamp_lo = float(np.float32(self.clamped_range[0]))
-        p.clamp_hi = float(np.float32(self.clamped_range[1]))
+        p.main_std_dev_threshold = _f32(hp.main_std_dev_threshold)
+        p.range_main = _f32(self.range_normal)
+        p.range_outlier = _f32(self.range_outlier)
+        p.clamp_lo = _f32(self.clamped_range[0])
+        p.clamp_hi = _f32(self.clamped_range[1])
         # fp64 data: the Python doubles themselves (smart.py:82-84, 154-156)
         p.main_std_dev_threshold_f64 = float(hp.main_std_dev_threshold)
         p.clamp_lo_f64 = float(self.clamped_range[0])
@@ -332,10 +346,18 @@ class SmartFP(CompressionAlgorithmBase):
     def workspace_bytes(self, numel: int) -> int:
         """Workspace of one call: above SMQ_MAX_DEVICE_SAMPLES device-drawn samples the
         multi-workgroup draw needs its own region (include/smq.h SMQ_WS_LARGE_SAMPLES_OFFSET)."""
-        lib = N.lib()
-        if self.hparams.use_sample_stats:
-            return lib.smq_smaq_workspace_bytes_sampled(numel, self.hparams.num_samples)
-        return lib.smq_smaq_workspace_bytes(numel)
+        key = (numel, self.hparams.num_samples if self.hparams.use_sample_stats else -1)
+        nb = _WS_BYTES.get(key)
+        if nb is None:  # (one library query per size: ~1 us of host time per call otherwise)
+            lib = N.lib()
+            if key[1] >= 0:
+                nb = lib.smq_smaq_workspace_bytes_sampled(numel, key[1])
+            else:
+                nb = lib.smq_smaq_workspace_bytes(numel)
+            if len(_WS_BYTES) > 4096:
+                _WS_BYTES.clear()
+            _WS_BYTES[key] = nb
+        return nb
 
     # -- inspection helpers (tests / bench) --------------------------------------------------------
     @staticmethod

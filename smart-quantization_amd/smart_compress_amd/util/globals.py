@@ -13,8 +13,11 @@ class Globals:
     profiler = None
 
 
+_NO_PROFILER = contextlib.nullcontext()  # reusable: entered once per codec call when no profiler
+
+
 def profile(name: str):
     prof = Globals.profiler
     if prof is None:
-        return contextlib.nullcontext()
+        return _NO_PROFILER
     return prof.profile(name)
