@@ -832,6 +832,7 @@ __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemCon
                                               int wo_rt, bool both, BnTable bt,
                                               uint32_t* lds) {
   constexpr bool kLut = WM > 0 && WM <= 8 && WO > 0 && WO <= 8;
+  constexpr bool kWide = kLut && M == kVarLds && WO > WM;
   const int wm = WM > 0 ? WM : wm_rt, wo = WO > 0 ? WO : wo_rt;
   const int we = wo > wm ? wo - wm : 0;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
@@ -898,8 +899,24 @@ __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemCon
         cd[i] = __builtin_amdgcn_alignbit(plane[(p >> 5) + 1], plane[p >> 5], p & 31u) & pm;
       }
     }
+    // kWide (narrow codes, variable section in LDS): every element's table index straight from the
+    // bits, without branches — the plane code, the we bits at its would-be outlier rank, and the mask
+    // bit on top; main entries of the table repeat over the we bits (unpack_lut<.., true>), so a main
+    // element's (meaningless) bits there select the same value.
+    uint32_t idx[4];
+    if constexpr (kWide) {
+      constexpr uint32_t kWE = (uint32_t)(WO - WM), kEmk = (1u << kWE) - 1u;
+      const uint32_t r = pc[wi] + __popc(mw & ((1u << sh0) - 1u));
+      const uint32_t p = kWE * r;  // (the word after the section is still LDS of this workgroup)
+      const uint32_t win = __builtin_amdgcn_alignbit(ext[(p >> 5) + 1], ext[p >> 5], p & 31u);
+      const uint32_t sft[4] = {0u, kWE * (nib & 1u), kWE * (uint32_t)__popc(nib & 3u),
+                               kWE * (uint32_t)__popc(nib & 7u)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        idx[i] = cd[i] | (((win >> sft[i]) & kEmk) << WM) | (((nib >> i) & 1u) << WO);
+    }
     // outlier bits above the plane: we bits per outlier from bit we * rank
-    if (we > 0 && nib) {
+    if (!kWide && we > 0 && nib) {
       uint32_t r = pc[wi] + __popc(mw & ((1u << sh0) - 1u));
       const uint32_t emk = (we >= 32) ? 0xffffffffu : ((1u << we) - 1u);
       // (the word after the last holds no bits of it; not read past the section when it lives
@@ -929,15 +946,32 @@ __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemCon
     float o[4];
     uint32_t bch = 0u, brun = 0u;  // BN: the element's channel and offset in its run
     if (BN) bt.locate((uint32_t)el0, bch, brun);
+    if constexpr (kWide && !BN) {
+      // the four table reads, then (rarely) the slot's escapes
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = lut[idx[i]];
+      if (__builtin_expect(enib != 0u, 0)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (!((enib >> i) & 1u)) continue;
+          bool hi, lo;
+          decode_code(idx[i], (nib >> i) & 1u, wm, wo, both, hi, lo);
+          const uint32_t s = sh0 + (uint32_t)i;
+          const float q = __uint_as_float(esc[2u * (epc[wi] + __popc(em & ((1u << s) - 1u))) + 1u]);
+          o[i] = smaq_dequant<false, AP, SQ>(q, hi, lo, c);
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if (kWide && !BN) break;
       const bool is_o = (nib >> i) & 1u;
       bool hi, lo;
       float q;
       if (BN && i > 0) bt.step(bch, brun);
       const BnTerm bn = BN ? bt.term(bch) : BnTerm{1.0f, 0.0f};
       if (kLut) {
-        o[i] = lut[is_o ? (1u << WM) + cd[i] : cd[i]];
+        o[i] = kWide ? lut[idx[i]] : lut[is_o ? (1u << WM) + cd[i] : cd[i]];
         if (__builtin_expect(!((enib >> i) & 1u), 1)) {
           if (BN) {  // smaq_dequant's last two statements on the table's value
             o[i] = (o[i] * bn.gamma) + bn.beta;
@@ -945,7 +979,7 @@ __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemCon
           }
           continue;
         }
-        decode_code(cd[i], is_o, wm, wo, both, hi, lo);
+        decode_code(kWide ? idx[i] : cd[i], is_o, wm, wo, both, hi, lo);
       } else {
         q = decode_code(cd[i], is_o, wm, wo, both, hi, lo);
         if (__builtin_expect(!((enib >> i) & 1u), 1)) {
@@ -970,17 +1004,23 @@ __device__ __forceinline__ void unpack_decode(const UnpackArgs& A, const ElemCon
 }
 
 // Decode table of narrow codes (kLut), once per workgroup: every main and outlier code de-quantised.
-template <bool AP, bool SQ, int WM, int WO>
+// WIDE (the branch-free indexing of unpack_decode): 2^(WO+1) entries, index = mask bit << WO | the
+// WO code bits; a main element's index carries WO - WM further bits above its code, so its entry
+// repeats over them.
+template <bool AP, bool SQ, int WM, int WO, bool WIDE = false>
 __device__ __forceinline__ void unpack_lut(const ElemConsts& c, bool both, uint32_t* lds,
                                            uint32_t F) {
+  static_assert(!WIDE || (2 << WO) <= kLutMax, "decode table size");
+  constexpr int kMain = WIDE ? (1 << WO) : (1 << WM);  // entries before the outlier codes
   float* lut = reinterpret_cast<float*>(lds + F + kVarCap + 4 + 3 * kMaskWords);
-  for (int i = threadIdx.x; i < (1 << WM) + (1 << WO); i += kBlock) {
+  for (int i = threadIdx.x; i < kMain + (1 << WO); i += kBlock) {
     bool hi = both, lo = both;
     float q;
-    if (i < (1 << WM)) {
-      q = (float)(((int32_t)((uint32_t)i << (32 - WM))) >> (32 - WM));  // sign-extend
+    if (i < kMain) {
+      const uint32_t cm = (uint32_t)i & ((1u << WM) - 1u);
+      q = (float)(((int32_t)(cm << (32 - WM))) >> (32 - WM));  // sign-extend
     } else {
-      const uint32_t v = (uint32_t)(i - (1 << WM));
+      const uint32_t v = (uint32_t)(i - kMain);
       lo = (v >> (WO - 1)) & 1u;
       hi = !lo;
       const int mag = (int)(v & ((1u << (WO - 1)) - 1u));
@@ -1006,7 +1046,7 @@ __device__ __forceinline__ void unpack_blocks(const UnpackArgs& A, const ElemCon
       const UnpackGeom G = unpack_geom(A, b0 + i, dent[i], wm, we);
       const UnpackLoads L = unpack_issue(G);
       if constexpr (kLut)
-        if (i == 0) unpack_lut<false, SQ, WM, WO>(c, both, lds, G.F);
+        if (i == 0) unpack_lut<false, SQ, WM, WO, (M == kVarLds && WO > WM)>(c, both, lds, G.F);
       if ((M == kVarLds && !G.var_lds) || (M == kVarMem && G.var_lds)) continue;  // the other launch's
       unpack_decode<AP, SQ, FULL, WM, WO, BN, M>(A, c, b0 + i, G, L, wm, wo, both, bt, lds);
     }
@@ -1020,7 +1060,7 @@ __device__ __forceinline__ void unpack_blocks(const UnpackArgs& A, const ElemCon
       G[i] = unpack_geom(A, b0 + i, dent[i], wm, we);
       L[i] = unpack_issue(G[i]);
     }
-  if constexpr (kLut) unpack_lut<AP, SQ, WM, WO>(c, both, lds, G[0].F);
+  if constexpr (kLut) unpack_lut<AP, SQ, WM, WO, (M == kVarLds && WO > WM)>(c, both, lds, G[0].F);
 #pragma unroll
   for (int i = 0; i < kUnpackPer; ++i) {
     if (i >= nblk) break;
