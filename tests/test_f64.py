@@ -382,7 +382,22 @@ def test_gpu_float_codecs_f64(precision):
     d_alpha = os2.derive_f64(hdr[0], hdr[1])
     assert all(_rel(st[k], d_alpha[k]) <= 1e-15 for k in st)
     yo, st, Y, T = os2.roundtrip_f64(xn, words, True, precision, st=st)
-    d = np.abs(ys.cpu().numpy().view(np.int64) - yo.view(np.int64))
+    yd = ys.cpu().numpy()
+    if precision == 16:
+        # y = t2 * sign with t2 an fp16 value (s2_elem_f64<true>: powf in float, as torch's half pow
+        # computes; the oracle takes libm's double pow). t1 = RN16(T * 2^-beta) has at most ~131
+        # distinct values per call, so one of them whose power lies at a half rounding boundary
+        # moves every element of that E5M2 code by one half ulp (measured: 1.9 % of the elements on
+        # one draw, none on others): compare in fp16 ulps, the target format (north_star: 1 ulp).
+        fin = np.isfinite(yd)
+        assert np.array_equal(fin, np.isfinite(yo))
+        assert np.array_equal(np.signbit(yd[fin]), np.signbit(yo[fin]))
+        hd = np.abs(yd[fin]).astype(np.float16).view(np.int16).astype(np.int32)
+        ho = np.abs(yo[fin]).astype(np.float16).view(np.int16).astype(np.int32)
+        dh = np.abs(hd - ho)
+        assert np.mean(dh == 0) > 0.5 and dh.max() <= 1, np.bincount(np.minimum(dh, 9))
+        return
+    d = np.abs(yd.view(np.int64) - yo.view(np.int64))
     frac_same = np.mean(d == 0)
     hist = np.bincount(np.minimum(d, 9).astype(np.int64), minlength=10).tolist()
     assert frac_same > 0.5, hist
