@@ -13,7 +13,8 @@ its own tensors and seed ("weak" scaling). `bench.py --gpus N` launches the N ra
 one rank. Ranks meet in a CPU (gloo) process group that only carries the start/stop barriers and
 the reduction of the timings: no RCCL. Rank 0 prints the one JSON line with every rank's time.
 
-Other configs (--config smaq_sampled | fp8 | s2fp8 | multi | packed | autograd | smaq_cpu) are measurement
+Other configs (--config smaq_sampled | fp8 | s2fp8 | multi | packed | autograd | autograd_resnet34 |
+smaq_cpu) are measurement
 aids (BASELINE configs 1 and 3-5), not the line the driver records; each carries its own
 `roofline` and, at N=1, a `cpu_baseline`.
 
@@ -866,12 +867,88 @@ def _vgg_cifar():
     return nn.Sequential(*layers)
 
 
+class _BasicBlock(torch.nn.Module):
+    """The reference's CIFAR ResNet BasicBlock (models/pytorch/resnet.py:31-79), written here (the
+    reference's model zoo is not imported): conv3x3-BN-ReLU(inplace)-conv3x3-BN, identity or the
+    1x1-conv + BN downsample, in-place add, ReLU."""
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        nn = torch.nn
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        out += identity
+        return self.relu(out)
+
+
+class _ResNet(torch.nn.Module):
+    """The reference's CIFAR ResNet (models/pytorch/resnet.py:133-260): 3x3 stride-1 stem, BN,
+    ReLU, 3x3 / 2 max-pool, four BasicBlock layers, average pool, fc; Kaiming fan-out init."""
+
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=10):
+        super().__init__()
+        nn = torch.nn
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 3, 1, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0])
+        self.layer2 = self._make_layer(128, layers[1], 2)
+        self.layer3 = self._make_layer(256, layers[2], 2)
+        self.layer4 = self._make_layer(512, layers[3], 2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    def _make_layer(self, planes, blocks, stride=1):
+        nn = torch.nn
+        down = None
+        if stride != 1 or self.inplanes != planes:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes, 1, stride, bias=False),
+                                 nn.BatchNorm2d(planes))
+        layers = [_BasicBlock(self.inplanes, planes, stride, down)]
+        self.inplanes = planes
+        layers += [_BasicBlock(planes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = self.avgpool(x)
+        return self.fc(x.reshape(x.size(0), -1))
+
+
+# quantization.py:164-180 always wraps the classes of the reference's model zoo (module path
+# smart_compress.models.pytorch.*): BasicBlock and the whole ResNet get their outputs compressed
+# too (SURVEY 3B: 132 module outputs per forward). These stand-ins carry that module path so the
+# mirrored is_valid_layer_type selects exactly the reference's call set.
+_BasicBlock.__module__ = _ResNet.__module__ = "smart_compress.models.pytorch.resnet"
+
+
 def run_autograd(args, world, rank, device):
-    """SURVEY 8f-2 at model scale: a CIFAR-shaped VGG-style CNN (batch 128) trained with SmaQ on
-    every selected layer's activation (forward) and grad-map (backward) through the mirrored
-    register_autograd_module (autograd.py:50-77). Three variants: no compression, codec calls
-    eager, and the whole training step captured in a hipGraph (SmartFP.graph_safe: fresh random
-    streams per replay)."""
+    """SURVEY 8f-2 at model scale: a CIFAR network at batch 128 trained with SmaQ on every selected
+    module's activation (forward) and grad-map (backward) through the mirrored
+    register_autograd_module (autograd.py:50-77). --config autograd_resnet34: the reference's
+    CIFAR ResNet-34 (models/pytorch/resnet.py:133-303, SURVEY 3B: the reference's own model);
+    --config autograd: a VGG-style CNN. Three variants: no compression, codec calls eager, and the
+    whole training step captured in a hipGraph (SmartFP.graph_safe: fresh random streams per
+    replay). The codec's share of a step = compressed - uncompressed, reported with its
+    algorithmic bytes (12 B per compressed element)."""
     from argparse import Namespace
 
     import torch.nn.functional as F
@@ -880,6 +957,7 @@ def run_autograd(args, world, rank, device):
     from smart_compress_amd.util.pytorch.autograd import register_autograd_module
 
     batch = 128
+    resnet = args.config == "autograd_resnet34"
     torch.manual_seed(rank)
     x = torch.randn(batch, 3, 32, 32, device=device)
     t = torch.randint(0, 10, (batch,), device=device)
@@ -888,7 +966,7 @@ def run_autograd(args, world, rank, device):
 
     def build(compress):
         torch.manual_seed(0)
-        net = _vgg_cifar().to(device)
+        net = (_ResNet() if resnet else _vgg_cifar()).to(device)
         opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9)
         codec = None
         if compress:
@@ -942,15 +1020,31 @@ def run_autograd(args, world, rank, device):
                                  compressed_elements_per_step=per_step[1])
     calls_per, elems = results["smaq_eager"]["codec_calls_per_step"], \
         results["smaq_eager"]["compressed_elements_per_step"]
+    base_ms = results["uncompressed"]["ms_per_step"]
+    for name in ("smaq_eager", "smaq_graph"):
+        codec_ms = results[name]["ms_per_step"] - base_ms
+        results[name]["codec_ms_per_step"] = round(codec_ms, 4)
+        results[name]["codec_gbps_12B"] = round(12.0 * elems / (codec_ms * 1e-3) / 1e9, 1) \
+            if codec_ms > 0 else None
     g_ms = results["smaq_graph"]["ms_per_step"]
+    g_codec = results["smaq_graph"]["codec_ms_per_step"]
+    g_gbps = results["smaq_graph"]["codec_gbps_12B"]
     return {"metric": "Training step with SmaQ on every layer (activations + grad-maps), ms/step",
             "value": g_ms, "unit": "ms/step", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": g_ms, "higher_is_better": False,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": "vgg_cifar_b128_register_autograd_module",
+            "config": {"workload": ("resnet34" if resnet else "vgg") +
+                       "_cifar_b128_register_autograd_module",
                        "codec_calls_per_step": calls_per,
                        "compressed_elements_per_step": elems},
-            "variants": results}
+            "variants": results,
+            # the codec's share of the graph step (compressed - uncompressed) over its algorithmic
+            # bytes: every codec call of the step, as one number
+            "roofline": {"bound": "hbm", "kernel": "all SmaQ launches of the step",
+                         "achieved": g_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(g_gbps / HBM_PEAK_GBPS, 4) if g_gbps else None,
+                         "alg_bytes_per_launch": int(12 * elems), "avg_launch_ms": g_codec,
+                         "traffic": None}}
 
 
 def run_smaq_cpu(args, world, rank, device):
@@ -1023,7 +1117,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="smaq",
                     choices=["smaq", "smaq_sampled", "fp8", "s2fp8", "multi", "packed",
-                             "autograd", "smaq_cpu", "mock"])
+                             "autograd", "autograd_resnet34", "smaq_cpu", "mock"])
     ap.add_argument("--elements", type=int, default=0, help="override elements (smaq configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
@@ -1038,6 +1132,7 @@ def main():
     device = torch.device("cuda", local) if not on_host else torch.device("cpu")
     runner = {"smaq": run_smaq, "smaq_sampled": run_smaq, "fp8": run_fp8, "s2fp8": run_s2fp8,
               "multi": run_multi, "packed": run_packed, "autograd": run_autograd,
+              "autograd_resnet34": run_autograd,
               "smaq_cpu": run_smaq_cpu, "mock": run_mock}[args.config]
     res = runner(args, world, rank, device)
     if world > 1:

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SMQ_ABI_VERSION 5
+#define SMQ_ABI_VERSION 6
 
 #define SMQ_OK 0
 #define SMQ_ERR_INVALID -1  /* bad argument */
@@ -63,10 +63,13 @@ extern "C" {
  * (params.count_outliers: the count is their sum; spread so 10^5 workgroups do not serialise on
  * one address), [640, SMQ_WS_SAMPLES_OFFSET) the statistics partials, then the
  * SMQ_MAX_DEVICE_SAMPLES int64 indices the last SMQ_STATS_SAMPLED_DEVICE call drew (in draw
- * order; read them after the stream has reached the call), then 64 tagged arrival counters. */
+ * order; read them after the stream has reached the call), then 64 tagged arrival counters, then
+ * at SMQ_WS_FUSED_OFFSET the single-launch round trip's exchange region (generation word, arrival
+ * word, epoch-tagged partial granules; smq_smaq_roundtrip on tensors up to 8,388,611 elements). */
 #define SMQ_WS_OUTLIER_SLOTS_OFFSET 128
 #define SMQ_WS_OUTLIER_SLOTS 64
 #define SMQ_WS_SAMPLES_OFFSET 66176
+#define SMQ_WS_FUSED_OFFSET 99584
 
 /* Device-drawn samples beyond SMQ_MAX_DEVICE_SAMPLES, up to SMQ_MAX_DRAW_SAMPLES: the draw runs
  * across workgroups (smaq.hip, "multi-workgroup draw") and needs
@@ -74,7 +77,7 @@ extern "C" {
  * (int64, draw order) instead of SMQ_WS_SAMPLES_OFFSET. The indices are the same Floyd draw either
  * way (smq_smaq_draw_samples / oracle/rng.py floyd_indices). */
 #define SMQ_MAX_DRAW_SAMPLES (1 << 28)
-#define SMQ_WS_LARGE_SAMPLES_OFFSET 99584
+#define SMQ_WS_LARGE_SAMPLES_OFFSET 198016
 
 /* Where smq_smaq_apply_f32 takes (mean, std) from. */
 #define SMQ_STATS_WORKSPACE 0 /* written by smq_smaq_stats_f32 into the workspace header */
@@ -264,12 +267,26 @@ int smq_smaq_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, 
 int smq_smaq_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                    const float* uniforms, const SmqSmaqStats* stats_in, void* ws, size_t ws_bytes,
                    void* stream);
-/* The round trip as one entry point. Up to 12M elements (aligned x / y, no BN term) it leaves the
- * statistics' final reduction to the apply launch (every apply workgroup reduces the statistics
- * partials itself; workgroup 0 writes the header): same output, header and stream position as
- * smq_smaq_stats + smq_smaq_apply, ~1.1-2.5 us less per call. Knob: SMQ_DEFER_MAX_N (0 = off). */
+/* The round trip as one entry point, always with the same output, header and stream position as
+ * smq_smaq_stats + smq_smaq_apply (both statistics paths compute the same partials and reduce them
+ * in one fixed order):
+ *  - up to 8,388,611 elements (full statistics, fp32 / fp16 / bf16 x 16-B / 8-B aligned, y 16-B
+ *    aligned, no BN term, no injected uniforms): ONE launch that holds the tensor in registers
+ *    (smaq_fused.hip: every workgroup publishes its statistics partial, gathers all of them, reduces
+ *    them and transforms its registers; 8 B/elem of HBM traffic);
+ *  - otherwise up to 12M elements (aligned x / y, no BN term): two launches, the statistics' final
+ *    reduction deferred to every apply workgroup;
+ *  - above: the statistics launch's last workgroup finalises, then the apply launch. */
 int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                        const float* uniforms, void* ws, size_t ws_bytes, void* stream);
+/* smq_smaq_roundtrip with path flags (tests and measurement; every path gives the same bytes). */
+#define SMQ_SMAQ_SPLIT 1u     /* no single launch: the two-launch path (deferred reduction) */
+#define SMQ_SMAQ_NO_DEFER 2u  /* two launches, the statistics launch finalises the header */
+#define SMQ_SMAQ_TEST_LATE 4u /* single launch: half of the workgroups start ~500 us late and the
+                                 others take missing partials after 20 us (no co-residency) */
+int smq_smaq_roundtrip_ex(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                          const float* uniforms, void* ws, size_t ws_bytes, uint32_t flags,
+                          void* stream);
 /* fp64 data (smart.py:130-182 on a float64 tensor): statistics, z-score, stochastic or truncating
  * rounding and de-quantisation in fp64, output fp64; every stats_source (k of SMQ_STATS_SAMPLED_DEVICE
  * up to SMQ_MAX_DRAW_SAMPLES with a workspace of smq_smaq_workspace_bytes_sampled), BN
@@ -386,12 +403,13 @@ int smq_s2fp8_roundtrip_f64(const double* x, double* y, int64_t n, int precision
 /* ---- CPU tensors ----
  * The codecs on host pointers, for tensors that live on the CPU (the reference's plugins run on
  * any device; BASELINE config 1 is a CPU run). Same argument meaning as the device entry points,
- * minus the stream; n_threads <= 0 uses the library's pool (SMQ_CPU_THREADS, else
- * OMP_NUM_THREADS, else all hardware threads). Each element uses the device path's arithmetic, so
+ * minus the stream; n_threads <= 0 uses all hardware threads (at most 256; the library reads no
+ * environment variable). Each element uses the device path's arithmetic, so
  * for the same statistics and random stream the SmaQ and float_quant outputs are the device's
  * bytes; statistics are fp64 sums in a fixed order independent of the thread count. S2FP8 uses the
  * C library's powf / log2f (the device's SMQ_S2FP8_EXACT_POW semantics). */
-/* Number of threads of the library's CPU pool. */
+/* Threads the library's CPU pool has started so far (the calling thread included); it grows to
+ * what the calls ask for. */
 int smq_cpu_threads(void);
 /* SmaQ round trip; ws: host buffer of smq_smaq_workspace_bytes(n) bytes that receives the
  * SmqSmaqStats header, the outlier count (slot 0 of SMQ_WS_OUTLIER_SLOTS, when

@@ -45,11 +45,14 @@ namespace cpu {
 constexpr int64_t kTask = 1 << 16;  // elements per task
 
 // ---- thread pool ----------------------------------------------------------------------------------
+// Workers are started on demand (a call asking for T threads makes sure T - 1 exist, at most
+// kMaxThreads - 1): the library reads no environment variable for its thread count; the caller
+// passes it (the Python host: torch's intra-op thread count).
+constexpr int kMaxThreads = 256;
+
 class Pool {
  public:
-  explicit Pool(int n_workers) {
-    for (int i = 0; i < n_workers; ++i) workers_.emplace_back([this, i] { loop(i); });
-  }
+  Pool() = default;
   ~Pool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -63,6 +66,7 @@ class Pool {
   // fn(task) for task in [0, n_tasks) on up to n_threads threads (the caller included)
   void run(int64_t n_tasks, int n_threads, const std::function<void(int64_t)>& fn) {
     std::lock_guard<std::mutex> one_job(job_mu_);
+    grow(std::min<int64_t>((int64_t)std::max(n_threads, 1) - 1, n_tasks - 1));
     int helpers = std::min<int64_t>((int64_t)std::max(n_threads, 1) - 1, n_tasks - 1);
     helpers = std::max(0, std::min(helpers, (int)workers_.size()));
     if (helpers == 0) {
@@ -93,8 +97,20 @@ class Pool {
       (*fn_)(t);
     }
   }
-  void loop(int idx) {
-    uint64_t seen = 0;
+  // called under job_mu_: no job is running, so a new worker starts from the current generation
+  void grow(int64_t want) {
+    want = std::min<int64_t>(want, kMaxThreads - 1);
+    uint64_t g;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      g = gen_;
+    }
+    while ((int64_t)workers_.size() < want) {
+      const int i = (int)workers_.size();
+      workers_.emplace_back([this, i, g] { loop(i, g); });
+    }
+  }
+  void loop(int idx, uint64_t seen) {
     for (;;) {
       {
         std::unique_lock<std::mutex> lk(mu_);
@@ -120,21 +136,17 @@ class Pool {
   bool stop_ = false;
 };
 
-static int default_threads() {
-  for (const char* name : {"SMQ_CPU_THREADS", "OMP_NUM_THREADS"}) {
-    const char* e = getenv(name);
-    if (e && atoi(e) > 0) return std::min(atoi(e), 256);
-  }
-  const unsigned hc = std::thread::hardware_concurrency();
-  return hc ? (int)std::min(hc, 256u) : 1;
-}
-
 static Pool& pool() {
-  static Pool* p = new Pool(default_threads() - 1);  // never destroyed: no join at exit
+  static Pool* p = new Pool();  // never destroyed: no join at exit
   return *p;
 }
 
-static int threads_for(int n_threads) { return n_threads > 0 ? n_threads : pool().size(); }
+// n_threads <= 0: the machine's hardware threads (capped)
+static int threads_for(int n_threads) {
+  if (n_threads > 0) return std::min(n_threads, kMaxThreads);
+  const unsigned hc = std::thread::hardware_concurrency();
+  return hc ? (int)std::min(hc, (unsigned)kMaxThreads) : 1;
+}
 
 template <class F>
 static void parallel_tasks(int64_t n, int n_threads, F&& f) {

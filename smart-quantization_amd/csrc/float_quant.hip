@@ -212,7 +212,7 @@ constexpr int kS2Loads = 16;         // dwordx4 per lane in flight per round
 // loads and the log2 chains of one wave hide behind the others'.
 static inline int s2_partial_threads() {
   static const int v = [] {
-    const char* e = getenv("SMQ_S2_PTHREADS");
+    const char* e = knob_env("SMQ_S2_PTHREADS");
     const int t = e ? atoi(e) : 1024;
     return (t == 256 || t == 1024) ? t : 1024;
   }();
@@ -223,7 +223,7 @@ static inline int s2_partial_threads() {
 // the summation order — and the statistics — are a function of n
 static inline int64_t s2_groups_per_wg(int64_t ng) {
   static const int np = [] {  // measurement knob SMQ_S2_PARTIALS (<= kS2Partials)
-    const char* e = getenv("SMQ_S2_PARTIALS");
+    const char* e = knob_env("SMQ_S2_PARTIALS");
     const int v = e ? atoi(e) : kS2Partials;
     return (v >= 1 && v <= kS2Partials) ? v : kS2Partials;
   }();
@@ -1175,7 +1175,7 @@ static inline bool aligned16f(const void* p) { return ((uintptr_t)p & 15u) == 0;
 
 static int fq_tile_v() {
   static const int v = [] {
-    const char* e = getenv("SMQ_FQ_TILE");
+    const char* e = knob_env("SMQ_FQ_TILE");
     const int t = e ? atoi(e) : kFqDefaultTileV;
     return (t == 1 || t == 2 || t == 4) ? t : kFqDefaultTileV;
   }();
@@ -1186,7 +1186,7 @@ static int fq_tile_v() {
 // pays the partial reduction and the inverse-power table once per tile
 static int s2_tile_v() {
   static const int v = [] {
-    const char* e = getenv("SMQ_S2_TILE");
+    const char* e = knob_env("SMQ_S2_TILE");
     const int t = e ? atoi(e) : 4;  // C4 (bench, 48 buffers): 1 / 2 / 4 -> 18.9 / 15.4 / 14.8 us
     return (t == 1 || t == 2 || t == 4) ? t : 4;
   }();
@@ -1226,7 +1226,7 @@ static size_t s2_ws_bytes() { return kS2WsGran + (size_t)kS2FRep * 3 * 8 * kS2FM
 // single-launch path (SMQ_S2_FUSED=0 keeps the two launches: measurement knob)
 static bool s2_fused_enabled() {
   static const bool v = [] {
-    const char* e = getenv("SMQ_S2_FUSED");
+    const char* e = knob_env("SMQ_S2_FUSED");
     return e ? atoi(e) != 0 : true;
   }();
   return v;
@@ -1287,7 +1287,7 @@ int smq_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t
   // non-temporal loads only for inputs beyond the Infinity Cache, the SmaQ policy (smaq.hip):
   // nt loads of cache-resident data lose its hits (C3 with 8 rotating buffers, cold: nt +2 %)
   static const int64_t nt_min = [] {
-    const char* e = getenv("SMQ_STATS_NT_MIN_MB");
+    const char* e = knob_env("SMQ_STATS_NT_MIN_MB");
     return (int64_t)(e ? atoll(e) : 512) << 20;
   }();
   A.nt_loads = (int64_t)(dtype_in == SMQ_DTYPE_F32 ? 4 : 2) * n >= nt_min ? 1 : 0;
@@ -1429,7 +1429,7 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
       F.exact_pow = (flags & SMQ_S2FP8_EXACT_POW) ? 1 : 0;
       F.test_late = (flags & SMQ_S2FP8_TEST_LATE) ? 1 : 0;
       static const bool trace_env = [] {
-        const char* e = getenv("SMQ_S2_TRACE");
+        const char* e = knob_env("SMQ_S2_TRACE");
         return e && atoi(e) != 0;
       }();
       F.trace = (trace_env && ws_bytes >= s2_ws_bytes() + 128 * (size_t)kS2FMaxG)
@@ -1453,7 +1453,7 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
         return SMQ_ERR_LAUNCH;
       }
       static const int lds_bytes = [] {  // measurement knob SMQ_S2_LDS_KB (default: 1 per CU)
-        const char* e = getenv("SMQ_S2_LDS_KB");
+        const char* e = knob_env("SMQ_S2_LDS_KB");
         const int v = e ? atoi(e) * 1024 : kS2FLds;
         return (v >= 0 && v <= kS2FLds) ? v : kS2FLds;
       }();
@@ -1515,7 +1515,7 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
   A.tiles_per_chunk = 0;
   A.n_chunks = 0;
   static const int xcd_env = [] {  // measurement knob SMQ_S2_XCD=0: tiles in index order
-    const char* e = getenv("SMQ_S2_XCD");
+    const char* e = knob_env("SMQ_S2_XCD");
     return e ? atoi(e) : 1;
   }();
   if (xcd_env && part && vec && xal) {

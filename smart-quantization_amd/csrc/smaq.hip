@@ -30,6 +30,7 @@
 #include "smq_common.h"
 #include "smaq_elem.h"
 #include "smaq_host.h"
+#include "smaq_small.h"
 
 namespace smq {
 
@@ -72,7 +73,7 @@ ArriveTag arrive_tag(const void* ws, hipStream_t st) {
 // sweep, one float4 of elements per apply slot)
 static bool half_tile_env() {
   static const bool v = [] {
-    const char* e = getenv("SMQ_HALF_TILE");
+    const char* e = knob_env("SMQ_HALF_TILE");
     return e ? atoi(e) != 0 : true;
   }();
   return v;
@@ -102,6 +103,7 @@ constexpr int kStatsTileGrid = 512;  // tile-stride sweep: 2 workgroups per CU (
 // 15.1; 8M 26.0 -> 23.6; 16M 40.1 -> 44.0; 32M 66.5 -> 79.6 (there the apply grid's partial
 // loads and the 256-workgroup sweep cost more than the hand-off they replace).
 constexpr int kDeferMaxG = 256;
+static_assert(kDeferMaxG == kSmallMaxG, "reduce_partials_w0 reduces <= kSmallMaxG partials");
 constexpr int64_t kDeferMaxN = 12ll << 20;
 // plain-load tail of an nt sweep (launch_stats): the Infinity Cache's size. 256M headline, two
 // interleaved rounds, ms/step: tail 0: 0.497 / 0.497; 128: 0.495 / 0.491; 160: 0.488 / 0.486;
@@ -110,56 +112,6 @@ constexpr int64_t kStatsPlainTailMB = 256;
 constexpr int64_t kStatsNtMinMB = 512;  // non-temporal statistics loads from this tensor size on
 
 static inline bool aligned(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
-
-// Wave-0 reduction of g <= kDeferMaxG statistics partials in ONE fixed order: lane l sums
-// partials l, l + 64, l + 128, l + 192 in that order, then the ascending DPP butterfly. Used by the
-// deferred path (every apply workgroup, plain loads: the partials come from an earlier launch) and by
-// the last statistics workgroup of a grid of <= kDeferMaxG (sc1 loads: same launch), so both give
-// the same fp64 totals bit for bit. Every load is issued before any is consumed. Call from wave 0
-// (all 64 lanes); the result is wave-uniform.
-template <bool SC1>
-__device__ __forceinline__ void reduce_partials_w0(const StatPartial* parts, int g, bool range,
-                                                   double& s1, double& s2, float& mn, float& mx) {
-  constexpr int K = kDeferMaxG / kWave;
-  const int l = threadIdx.x & (kWave - 1);
-  double2 sv[K];
-  float2 mv[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    const int b = l + i * kWave;
-    if (b < g) {
-      if (SC1) {
-        sv[i].x = ld_sc1_f64(&parts[b].s1);
-        sv[i].y = ld_sc1_f64(&parts[b].s2);
-        if (range) ld_sc1_f32x2(&parts[b].mn, mv[i].x, mv[i].y);
-      } else {
-        sv[i] = *reinterpret_cast<const double2*>(&parts[b].s1);
-        if (range) mv[i] = *reinterpret_cast<const float2*>(&parts[b].mn);
-      }
-    }
-  }
-  s1 = 0.0;
-  s2 = 0.0;
-  mn = INFINITY;
-  mx = -INFINITY;
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    if (l + i * kWave < g) {
-      s1 += sv[i].x;
-      s2 += sv[i].y;
-      if (range) {
-        mn = fminf(mn, mv[i].x);
-        mx = fmaxf(mx, mv[i].y);
-      }
-    }
-  }
-  s1 = wave_sum_asc(s1);
-  s2 = wave_sum_asc(s2);
-  if (range) {
-    mn = wave_min(mn);
-    mx = wave_max(mx);
-  }
-}
 
 template <bool RANGE, int TIN, bool TILE = false, bool NT = false>
 __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restrict__ x, int64_t n,
@@ -794,7 +746,7 @@ static size_t stats_ws_bytes(int64_t n) {
   (void)n;
   static_assert(SmaqWsLayout::kPartials + sizeof(StatPartial) * (size_t)kStatsGridCap ==
                     SMQ_WS_SAMPLES_OFFSET, "smq.h SMQ_WS_SAMPLES_OFFSET");
-  return SmaqWsLayout::kTagCounters + 8 * (size_t)SmaqWsLayout::kTagWords;
+  return SmaqWsLayout::kTotal;
 }
 
 static int check_dtype(int dtype) {
@@ -808,16 +760,27 @@ static int check_dtype(int dtype) {
 // def_g != NULL: deferred statistics (defer_consts) — *def_g = the number of partials left for the
 // apply launch, or 0 when a single workgroup finalised the header itself.
 static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
-                        size_t ws_bytes, hipStream_t st, int* def_g = nullptr) {
-  if (!ws || ws_bytes < stats_ws_bytes(n)) {
-    set_error("workspace too small: need %zu bytes, got %zu", stats_ws_bytes(n), ws_bytes);
+                        size_t ws_bytes, hipStream_t st, int* def_g = nullptr,
+                        SmqSmaqStats* out = nullptr) {
+  // (the single launch's exchange region above the tag counters is not needed here)
+  const size_t need = SmaqWsLayout::kTagCounters + 8 * (size_t)SmaqWsLayout::kTagWords;
+  if (!ws || ws_bytes < need) {
+    set_error("workspace too small: need %zu bytes, got %zu", need, ws_bytes);
     return SMQ_ERR_WORKSPACE;
   }
   char* base = (char*)ws;
-  SmqSmaqStats* hdr = (SmqSmaqStats*)base;
+  SmqSmaqStats* hdr = out ? out : (SmqSmaqStats*)base;
   unsigned long long* counter = (unsigned long long*)(base + SmaqWsLayout::kTagCounters);
   StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
   const int vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) ? 1 : 0;
+  if (n <= kSmallMaxN && !out) {
+    // activation-sized tensors: the partition the single launch uses (smaq_small.h), so every path
+    // gives the same statistics bit for bit
+    const FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n),
+                           (unsigned long long*)p->offset_counter, n};
+    return launch_stats_small(x, dtype, n, vec != 0, p->use_range_std_dev != 0, fin, ws, st,
+                              def_g != nullptr, def_g);
+  }
   // fp32 sweeps tile-stride (smaq_stats_kernel<.., TILE>) on at most kStatsTileGrid workgroups;
   // measured on the 256M headline (bench, 3 interleaved rounds): grid-stride at 2048 workgroups
   // 0.542 ms/step; tile-stride at 1024 / 768 / 640 / 512 / 384 / 256 workgroups 0.529 / 0.528 /
@@ -827,7 +790,7 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   // slot (256M: 112 -> 90 us, 0.422-0.431 -> 0.407-0.408 ms/step fp16, tools/half_tile.sh; with
   // 8-B loads the tile form had lost, 0.636 vs 0.463); an 8-B aligned x keeps the grid-stride sweep.
   static const int tile_env = [] {  // measurement knob SMQ_STATS_TILE=0: grid-stride sweep
-    const char* e = getenv("SMQ_STATS_TILE");
+    const char* e = knob_env("SMQ_STATS_TILE");
     return e ? atoi(e) : 1;
   }();
   // half inputs take the tile sweep with 16-B loads when x is 16-B aligned (vec = 2)
@@ -835,7 +798,7 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   const bool tile = tile_env != 0 && (dtype == SMQ_DTYPE_F32 || x16);
   const int vec_arg = x16 ? 2 : vec;
   static const int grid_env = [] {  // measurement knob SMQ_STATS_GRID (64 .. kStatsGridCap)
-    const char* e = getenv("SMQ_STATS_GRID");
+    const char* e = knob_env("SMQ_STATS_GRID");
     const int v = e ? atoi(e) : 0;
     return (v >= 64 && v <= kStatsGridCap) ? v : 0;
   }();
@@ -843,7 +806,7 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   // >= 16K elements per workgroup: mid-size tensors (activations, 1-30M elements) are bound by
   // the arrival of their workgroups, not by bandwidth; at 256M the cap decides
   static const int per_wg = [] {  // measurement knob SMQ_STATS_PER_WG (elements, >= 1024)
-    const char* e = getenv("SMQ_STATS_PER_WG");
+    const char* e = knob_env("SMQ_STATS_PER_WG");
     const int v = e ? atoi(e) : kBlock * 4 * 16;
     return v >= kBlock * 4 ? v : kBlock * 4 * 16;
   }();
@@ -866,7 +829,7 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   // launch re-reads x from the cache the plain loads filled (64 / 128 / 256 MiB tensors: 0.047 /
   // 0.075 / 0.131 ms/step plain against 0.051 / 0.080 / 0.138 nt; tools/ntsize_exp.sh)
   static const int64_t nt_min_bytes = [] {  // measurement knob SMQ_STATS_NT_MIN_MB
-    const char* e = getenv("SMQ_STATS_NT_MIN_MB");
+    const char* e = knob_env("SMQ_STATS_NT_MIN_MB");
     return (int64_t)(e ? atoll(e) : kStatsNtMinMB) << 20;
   }();
   const bool nt = tile && 4 * n >= nt_min_bytes;
@@ -874,7 +837,7 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   // Infinity Cache for the apply launch, which walks its tiles from the end (measurement knob
   // SMQ_STATS_PLAIN_TAIL_MB)
   static const int64_t plain_tail = [] {
-    const char* e = getenv("SMQ_STATS_PLAIN_TAIL_MB");
+    const char* e = knob_env("SMQ_STATS_PLAIN_TAIL_MB");
     return (int64_t)(e ? atoll(e) : kStatsPlainTailMB) << 20;
   }();
   const int64_t nt_end = (n >> 2) - plain_tail / 16;
@@ -906,7 +869,7 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
 // 0.358 vs 0.368 ms) and halve the outlier-count atomics; truncation always uses 1.
 static int sr_tile_v() {
   static const int v = [] {
-    const char* e = getenv("SMQ_APPLY_TILE");
+    const char* e = knob_env("SMQ_APPLY_TILE");
     return (e && atoi(e) == 1) ? 1 : 2;
   }();
   return v;
@@ -1136,7 +1099,7 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
     }
   }
   static const int rev_env = [] {
-    const char* e = getenv("SMQ_APPLY_REVERSE");
+    const char* e = knob_env("SMQ_APPLY_REVERSE");
     return e ? atoi(e) : 1;
   }();
   // reverse only pays after a forward statistics sweep of the same tensor
@@ -1144,7 +1107,7 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   // non-temporal loads only where they do not forfeit Infinity-Cache hits: a tensor that fits is
   // re-read from the cache (multi-tensor chunks, same policy: nt loads 86.5 vs 80.8 us per step)
   static const int64_t apply_nt_min = [] {
-    const char* e = getenv("SMQ_STATS_NT_MIN_MB");
+    const char* e = knob_env("SMQ_STATS_NT_MIN_MB");
     return (int64_t)(e ? atoll(e) : kStatsNtMinMB) << 20;
   }();
   A.nt_loads = (int64_t)(dtype == SMQ_DTYPE_F32 ? 4 : 2) * n >= apply_nt_min ? 1 : 0;
@@ -1154,7 +1117,7 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   // 4 slots 0.384-0.390; fp16 (round 3, with the fp32-reciprocal z-score, half_quot) 4 slots
   // 0.4005-0.406 vs 2 slots 0.408-0.422 (round 2, before half_quot: no gain from 4)
   static const int half_tv = [] {  // measurement knob SMQ_HALF_TV (2 | 4): both half types
-    const char* e = getenv("SMQ_HALF_TV");
+    const char* e = knob_env("SMQ_HALF_TV");
     return e ? (atoi(e) == 4 ? 4 : 2) : 0;
   }();
   if (tv == 2 && dtype != SMQ_DTYPE_F32)
@@ -1230,6 +1193,10 @@ int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, v
 }
 
 size_t smaq_stats_ws_bytes(int64_t n) { return stats_ws_bytes(n); }
+int stats_into(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
+               size_t ws_bytes, hipStream_t st, SmqSmaqStats* out) {
+  return launch_stats(x, dtype, n, p, ws, ws_bytes, st, nullptr, out);
+}
 int smaq_validate(const SmqSmaqParams* p, int dtype) {
   int rc = validate_params(p);
   if (!rc) rc = check_dtype(dtype);
@@ -1343,7 +1310,7 @@ int smq_smaq_apply(const void* x, int dtype, float* y, int64_t n, const SmqSmaqP
 static bool defer_eligible(const void* x, int dtype, const float* y, int64_t n,
                            const SmqSmaqParams* p, const float* uniforms) {
   static const int64_t max_n = [] {  // measurement knob SMQ_DEFER_MAX_N (elements; 0 = off)
-    const char* e = getenv("SMQ_DEFER_MAX_N");
+    const char* e = knob_env("SMQ_DEFER_MAX_N");
     return e ? (int64_t)atoll(e) : kDeferMaxN;
   }();
   if (n > max_n || p->bn_gamma) return false;
@@ -1352,16 +1319,44 @@ static bool defer_eligible(const void* x, int dtype, const float* y, int64_t n,
   return !range_recips(p->range_main, p->range_outlier).safe_q;
 }
 
-int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
-                       const float* uniforms, void* ws, size_t ws_bytes, void* stream) {
+// The single launch (smaq_fused.hip) needs the vector body without the BN term, the in-kernel
+// random draws and its workspace region.
+static bool fused_eligible(const void* x, int dtype, const float* y, int64_t n,
+                           const SmqSmaqParams* p, const float* uniforms, size_t ws_bytes) {
+  static const bool on = [] {  // measurement knob SMQ_FUSED=0: the two-launch paths
+    const char* e = knob_env("SMQ_FUSED");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (!on || n < 4 || n > kSmallMaxN || p->bn_gamma) return false;
+  if (p->stochastic_rounding && uniforms) return false;
+  if (ws_bytes < SmaqWsLayout::kTotal) return false;
+  if (!aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) || !aligned(y, 16)) return false;
+  return !range_recips(p->range_main, p->range_outlier).safe_q;
+}
+
+int smq_smaq_roundtrip_ex(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                          const float* uniforms, void* ws, size_t ws_bytes, uint32_t flags,
+                          void* stream) {
   int rc = validate_params(p);
   if (!rc) rc = check_dtype(dtype);
   if (!rc) rc = check_tensor_args(x, y, n);
   if (rc) return rc;
+  if (flags & ~(SMQ_SMAQ_SPLIT | SMQ_SMAQ_NO_DEFER | SMQ_SMAQ_TEST_LATE)) {
+    set_error("roundtrip: unknown flags 0x%x", flags);
+    return SMQ_ERR_INVALID;
+  }
+  if (p->stats_source == SMQ_STATS_WORKSPACE && !(flags & (SMQ_SMAQ_SPLIT | SMQ_SMAQ_NO_DEFER)) &&
+      ws && fused_eligible(x, dtype, y, n, p, uniforms, ws_bytes)) {
+    const RangeRecips R = range_recips(p->range_main, p->range_outlier);
+    FusedCall c{x, dtype, y, n, p, range_coef_for(p, n), R.inv_main, R.inv_out, ws,
+                (flags & SMQ_SMAQ_TEST_LATE) ? 1 : 0};
+    return launch_fused(c, (hipStream_t)stream);
+  }
   int def_g = 0;
   if (p->stats_source == SMQ_STATS_WORKSPACE) {
+    const bool defer = !(flags & SMQ_SMAQ_NO_DEFER) && defer_eligible(x, dtype, y, n, p, uniforms);
     rc = launch_stats(x, dtype, n, p, ws, ws_bytes, (hipStream_t)stream,
-                      defer_eligible(x, dtype, y, n, p, uniforms) ? &def_g : nullptr);
+                      defer ? &def_g : nullptr);
     if (rc) return rc;
   } else if (p->stats_source == SMQ_STATS_INJECTED) {
     set_error("roundtrip: use smq_smaq_apply for injected statistics");
@@ -1369,6 +1364,11 @@ int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqS
   }
   return launch_apply(x, dtype, y, n, p, uniforms, nullptr, ws, ws_bytes, (hipStream_t)stream,
                       def_g);
+}
+
+int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                       const float* uniforms, void* ws, size_t ws_bytes, void* stream) {
+  return smq_smaq_roundtrip_ex(x, dtype, y, n, p, uniforms, ws, ws_bytes, 0u, stream);
 }
 
 int smq_smaq_stats_f32(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,

@@ -1,0 +1,597 @@
+// smaq_fused.hip — SmaQ compress->decompress round trip of activation-sized tensors in ONE launch
+// (gfx950), and the statistics launch of the two-launch paths for the same sizes.
+//
+// Reference: smart_compress/compress/smart.py:110-190 (SmartFP.__call__), called per module output
+// and per grad-map by util/pytorch/autograd.py:30-42 — tensors of 10^5 .. 8.4 * 10^6 elements
+// (CIFAR ResNet-34 at batch 128: 132 forward calls, the largest 128x64x32x32). At these sizes the
+// two-launch shape (statistics sweep, then a transform that re-reads x) pays a kernel boundary, a
+// second launch ramp and a second read of x; the call is latency-bound, not bandwidth-bound.
+//
+// smaq_fused_kernel: workgroup b (1024 threads) loads its chunk of the smaq_small.h partition — V
+// float4 groups per lane — into registers ONCE, computes the chunk's statistics partial exactly as
+// the two-launch statistics launch does (smaq_stats_small_kernel, same lanes, same chains, same
+// butterflies), publishes it, waits until every chunk's partial is there, reduces them in
+// reduce_partials_w0's order, finalises (smart.py:130-134, 100-108, 151-152), and transforms its
+// registers (smart.py:154-182). 8 B/elem of HBM traffic (x read once, y written); the statistics,
+// outputs and stream position equal smq_smaq_stats + smq_smaq_apply bit for bit by construction.
+//
+// Hand-off (cdna_hip_programming.md Guideline 16 R2, as the single-launch S2FP8 in float_quant.hip):
+// a partial is 4 (6 with range-std: + min, max) aligned 8-byte granules {epoch, 32-bit word}, each
+// ONE relaxed agent-scope (sc1) store, written to 8 replicas (replica r is polled by the workgroups
+// b % 8 == r, spreading 256 readers over 8x the memory channels). One wave per workgroup re-reads
+// the granules it still misses until every tag is this call's epoch. The epoch is (generation << 1)
+// | 1: every workgroup reads the generation word at its start; the last workgroup past the wait (an
+// arrival word tagged with the generation: the add is issued early and looked at at the end)
+// advances it, the graph-safe stream counter and the arrival word. Calls on one workspace are
+// serialised by the stream, so consecutive calls — eager or replayed from a graph — see
+// consecutive generations and never a stale granule of an earlier call as their own.
+//
+// No co-residency assumption: a workgroup that has waited kFusedStealTicks computes the partials it
+// still misses itself, from memory (a partial is a pure function of its chunk: duplicates store the
+// same bytes), so a grid that is only partly resident (other kernels holding CUs) still finishes.
+#include <limits.h>
+#include <string.h>
+
+#include "smq_common.h"
+#include "smaq_elem.h"
+#include "smaq_small.h"
+
+namespace smq {
+
+constexpr int kFusedRep = SmaqWsLayout::kFusedRep;
+constexpr int kFusedWords = SmaqWsLayout::kFusedWords;
+constexpr uint64_t kFusedStealTicks = 20000;  // s_memrealtime at 100 MHz: 200 us
+constexpr int kFusedLds = 88 * 1024;          // dynamic LDS request: one workgroup per CU
+
+// ------------------------------------------------------------------------------------------------
+// statistics launch of the two-launch paths (smq_smaq_stats, and smq_smaq_roundtrip when the single
+// launch does not apply): one workgroup per partial
+// ------------------------------------------------------------------------------------------------
+template <int TIN>
+__global__ __launch_bounds__(kSmallT) void smaq_stats_small_kernel(const void* __restrict__ x,
+                                                                   int64_t n, int V, int vec,
+                                                                   int range, FinalizeArgs fin,
+                                                                   StatPartial* partials,
+                                                                   unsigned long long* counter,
+                                                                   ArriveTag tag,
+                                                                   SmqSmaqStats* out,
+                                                                   double* def_rec) {
+  __shared__ SmallWaveLds W;
+  __shared__ uint32_t arrive_slot;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const double shift = stats_shift<TIN>(x, n);
+  const StatAcc w = small_wave(small_lane<TIN, kSmallMaxV>(x, n, V, G, b, threadIdx.x, vec != 0,
+                                                           shift));
+  if (lane == 0) {
+    W.s1[wave] = w.s1;
+    W.s2[wave] = w.s2;
+    W.mn[wave] = w.mn;
+    W.mx[wave] = w.mx;
+  }
+  __syncthreads();
+  if (G == 1) {  // the partial is the total: finalise without a hand-off
+    if (threadIdx.x == 0) {
+      const StatAcc a = small_combine(W);
+      if (range) finalize_stats<true, TIN>(a.s1, a.s2, a.mn, a.mx, n, shift, false, fin, out);
+      else finalize_stats<false, TIN>(a.s1, a.s2, a.mn, a.mx, n, shift, false, fin, out);
+    }
+    return;
+  }
+  if (def_rec) {  // deferred statistics: every apply workgroup reduces the partials (defer_consts)
+    if (threadIdx.x == 0) {
+      const StatAcc a = small_combine(W);
+      StatPartial* p = partials + b;
+      p->s1 = a.s1;
+      p->s2 = a.s2;
+      p->mn = a.mn;
+      p->mx = a.mx;
+      if (b == 0) {  // the shift, and the call's graph-safe stream position
+        unsigned long long base = 0ull;
+        if (fin.rng_ctr) {
+          base = *fin.rng_ctr;
+          *fin.rng_ctr = base + (unsigned long long)fin.rng_n;
+        }
+        def_rec[0] = shift;
+        def_rec[1] = __builtin_bit_cast(double, base);
+      }
+    }
+    return;
+  }
+  if (threadIdx.x == 0) {
+    const StatAcc a = small_combine(W);
+    StatPartial* p = partials + b;
+    st_sc1_f64(&p->s1, a.s1);
+    st_sc1_f64(&p->s2, a.s2);
+    st_sc1_f32x2(&p->mn, a.mn, a.mx);
+  }
+  const uint32_t prev = block_arrive_tagged(counter + (tag.tag & (SmaqWsLayout::kTagWords - 1)),
+                                            tag.tag, &arrive_slot);
+  if (prev != (uint32_t)G - 1) return;
+  if (threadIdx.x < kWave) {
+    double t1, t2;
+    float tmn, tmx;
+    reduce_partials_w0<true>(partials, G, true, t1, t2, tmn, tmx);
+    if (threadIdx.x == 0) {
+      if (range) finalize_stats<true, TIN>(t1, t2, tmn, tmx, n, shift, false, fin, out);
+      else finalize_stats<false, TIN>(t1, t2, tmn, tmx, n, shift, false, fin, out);
+      arrive_reset(counter + (tag.next & (SmaqWsLayout::kTagWords - 1)), tag.next);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// the single launch
+// ------------------------------------------------------------------------------------------------
+struct FusedArgs {
+  const void* x;
+  float* y;
+  int64_t n, nv;
+  int G;
+  uint32_t key;
+  uint64_t offset;
+  uint64_t* ctr;                 // graph-safe stream position (nullable)
+  SmqSmaqStats* hdr;
+  uint32_t* gen;                 // generation word
+  unsigned long long* left;      // workgroups past the wait, tagged with the generation
+  unsigned long long* gran;      // [kFusedRep][kSmallMaxG][kFusedWords] granules
+  unsigned long long* out_slots; // outlier-count slots (count)
+  float thr, r_main, r_out, clamp_lo, clamp_hi, range_coef;
+  double inv_r_main, inv_r_out;
+  int all_pos, count, range, test_late;
+};
+
+// The partial of chunk k by the whole workgroup from the lanes' groups g; every thread gets it.
+template <int TIN, int V>
+__device__ __forceinline__ StatAcc fused_partial(const FusedArgs& A, int k, const float4 (&g)[V],
+                                                 double shift, SmallWaveLds& W) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const StatAcc w = small_wave(small_lane_sum<TIN, V>(A.x, A.n, V, A.G, k, threadIdx.x, g, shift));
+  if (lane == 0) {
+    W.s1[wave] = w.s1;
+    W.s2[wave] = w.s2;
+    W.mn[wave] = w.mn;
+    W.mx[wave] = w.mx;
+  }
+  lds_barrier();
+  const StatAcc r = small_combine(W);
+  lds_barrier();  // W may be rewritten
+  return r;
+}
+
+// The rare path: partial k computed from memory by the whole workgroup (one group per lane in
+// flight), every thread gets it. Not inlined: its registers would otherwise add to the kernel's
+// peak (the chunk held in registers stays live across it); a call costs register saves only on
+// this path.
+template <int TIN>
+__device__ __noinline__ StatAcc fused_steal(const void* x, int64_t n, int V, int G, int k,
+                                            double shift, SmallWaveLds* W) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const StatAcc w = small_wave(small_lane_seq<TIN>(x, n, V, G, k, threadIdx.x, shift));
+  if (lane == 0) {
+    W->s1[wave] = w.s1;
+    W->s2[wave] = w.s2;
+    W->mn[wave] = w.mn;
+    W->mx[wave] = w.mx;
+  }
+  lds_barrier();
+  const StatAcc r = small_combine(*W);
+  lds_barrier();
+  return r;
+}
+
+// Lanes 0 .. kFusedRep * words - 1 of wave 0 store partial k's granules (nobody waits for them).
+__device__ __forceinline__ void fused_publish(const StatAcc& a, const FusedArgs& A, int k,
+                                              uint32_t epoch) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int words = A.range ? 6 : 4;
+  if (lane >= kFusedRep * words) return;
+  const int r = words == 4 ? lane >> 2 : (lane * 43) >> 8;  // lane / words (lane < 48)
+  const int c = lane - r * words;
+  const uint64_t b1 = __builtin_bit_cast(uint64_t, a.s1), b2 = __builtin_bit_cast(uint64_t, a.s2);
+  uint32_t word;
+  switch (c) {
+    case 0: word = (uint32_t)b1; break;
+    case 1: word = (uint32_t)(b1 >> 32); break;
+    case 2: word = (uint32_t)b2; break;
+    case 3: word = (uint32_t)(b2 >> 32); break;
+    case 4: word = __builtin_bit_cast(uint32_t, a.mn); break;
+    default: word = __builtin_bit_cast(uint32_t, a.mx); break;
+  }
+  st_sc1_u64(&A.gran[((size_t)r * kSmallMaxG + k) * kFusedWords + c],
+             ((unsigned long long)epoch << 32) | word);
+}
+
+__device__ __forceinline__ float rfl(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double rfl(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void uniform_consts(ElemConsts& c) {
+  c.mean = rfl(c.mean);
+  c.sd = rfl(c.sd);
+  c.sc = rfl(c.sc);
+  c.inv_sc = rfl(c.inv_sc);
+  c.inv_sc32 = rfl(c.inv_sc32);
+  c.zh = rfl(c.zh);
+  c.zl = rfl(c.zl);
+}
+
+// The element transform of the registers (smart.py:154-182) and their stores. PRE: the rounding
+// draws uu were computed ahead (during the gather), else they are hashed here.
+template <int RM, int V, int TIN, bool AP, bool SUB, bool PRE>
+__device__ __forceinline__ uint32_t fused_transform(const FusedArgs& A, const float4 (&vr)[V],
+                                                    const float4* park, const float (&uu)[V][4],
+                                                    const ElemConsts& c, int64_t base,
+                                                    uint64_t off) {
+  constexpr int VR = V < 4 ? V : 4;
+  uint32_t n_out = 0;
+  float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const int64_t j = base + (int64_t)u * kSmallT;
+    if (j >= A.nv) continue;
+    const float4 x4 = u < VR ? vr[u] : park[(u - VR) * kSmallT + threadIdx.x];
+    float u0 = uu[u][0], u1 = uu[u][1], u2 = uu[u][2], u3 = uu[u][3];
+    if (RM == kRoundHash && !PRE) rng_hu4(A.key, off + ((uint64_t)j << 2), u0, u1, u2, u3);
+    bool b0, b1, b2, b3;
+    float4 o;
+    o.x = smaq_elem<RM, false, TIN, AP, SUB, false>(x4.x, u0, c, b0);
+    o.y = smaq_elem<RM, false, TIN, AP, SUB, false>(x4.y, u1, c, b1);
+    o.z = smaq_elem<RM, false, TIN, AP, SUB, false>(x4.z, u2, c, b2);
+    o.w = smaq_elem<RM, false, TIN, AP, SUB, false>(x4.w, u3, c, b3);
+    n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
+    store_stream(y4 + j, o);
+  }
+  return n_out;
+}
+
+template <int RM, int TIN, bool AP, bool SUB>
+__device__ __forceinline__ uint32_t fused_tail(const FusedArgs& A, const ElemConsts& c,
+                                               uint64_t off) {
+  const int64_t e = (A.nv << 2) + threadIdx.x;
+  const float u = RM == kRoundHash ? rng_hu(A.key, off + (uint64_t)e) : 0.0f;
+  bool bt;
+  A.y[e] = smaq_elem<RM, false, TIN, AP, SUB, false>(load1<TIN>(A.x, e), u, c, bt);
+  return (uint32_t)bt;
+}
+
+template <int RM, int V, int TIN>
+__global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
+  __shared__ SmallWaveLds W;
+  __shared__ SmqSmaqStats sst;
+  __shared__ float4 u0lds[V <= 4 ? V : 1][kWave];  // wave 0's rounding draws (PRE)
+  __shared__ uint32_t sh_cnt[kSmallWaves];
+  __shared__ uint32_t pw[kSmallMaxG][kFusedWords];  // the gathered partials' words
+  __shared__ uint32_t pw_have[kSmallMaxG];            // pw holds partial k (pollers' bookkeeping)
+  __shared__ int smiss[4];
+  const int b = blockIdx.x, G = A.G;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t base = (int64_t)b * V * kSmallT + threadIdx.x;
+  const uint64_t steal_ticks = A.test_late ? 2000 : kFusedStealTicks;
+  if (A.test_late && 2 * b >= G && G > 1) {  // test aid: half of the grid starts ~500 us late
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 50000) __builtin_amdgcn_s_sleep(127);
+  }
+  // this chunk into registers (branch-free: indices past the end re-read the last group and are
+  // ignored), so every load is in flight before the first wait
+  float4 v[V];
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const int64_t j = base + (int64_t)u * kSmallT;
+    v[u] = load4<TIN>(A.x, j < A.nv ? j : A.nv - 1);
+  }
+  // groups VR .. V-1 wait in LDS (dynamic, park[(u - VR) * kSmallT + t]) once the statistics have
+  // consumed them: registers for more than four groups would spill across the gather
+  constexpr int VR = V < 4 ? V : 4;
+  extern __shared__ float4 park[];
+  const double shift = stats_shift<TIN>(A.x, A.n);
+  const uint32_t gen = G > 1 ? ld_sc1_u32(A.gen) : 0u;
+  const uint64_t ctr_word = A.ctr ? ld_sc1_u64(A.ctr) : 0ull;
+  const uint64_t off0 = ctr_word;
+  const uint32_t epoch = (gen << 1) | 1u;
+  // materialised here: both reads have returned before this workgroup can be counted past the
+  // wait (after which the last workgroup may advance them)
+  asm volatile("" ::"v"(off0), "v"(epoch));
+  const uint64_t off = A.offset + off0;
+
+  const StatAcc part = fused_partial<TIN, V>(A, b, v, shift, W);
+#pragma unroll
+  for (int u = VR; u < V; ++u) park[(u - VR) * kSmallT + threadIdx.x] = v[u];
+  if (G > 1 && wave == 0) fused_publish(part, A, b, epoch);
+
+  // the rounding draws depend on the stream position only: every wave computes its own now (wave
+  // 0's by waves 4..4+V-1, handed over in LDS), while waves 0..3 gather the partials. Above 3
+  // groups per lane they would hold 4V more VGPRs across the gather: hashed in the transform.
+  constexpr bool PRE = RM == kRoundHash && V <= 3;
+  float uu[V][4];
+#pragma unroll
+  for (int u = 0; u < V; ++u) uu[u][0] = uu[u][1] = uu[u][2] = uu[u][3] = 0.0f;
+  if (PRE && wave != 0) {
+#pragma unroll
+    for (int u = 0; u < V; ++u)
+      rng_hu4(A.key, off + ((uint64_t)(base + (int64_t)u * kSmallT) << 2), uu[u][0], uu[u][1],
+              uu[u][2], uu[u][3]);
+    if (wave >= 4 && wave < 4 + V) {
+      const int u = wave - 4;
+      float4 w;
+      rng_hu4(A.key, off + ((uint64_t)((int64_t)b * V * kSmallT + lane + (int64_t)u * kSmallT) << 2),
+              w.x, w.y, w.z, w.w);
+      u0lds[u][lane] = w;
+    }
+  }
+
+  unsigned long long left_old = 0;
+  if (G > 1) {
+    // waves 0..3 gather the G partials from replica b % 8 — lane l of wave w polls partial
+    // 4l + w (its granules are one contiguous 48-B run) — until every granule carries the epoch;
+    // accepted words go to LDS (pw). One loop for the whole workgroup: the pollers wait (the first
+    // time until every granule is there or their patience runs out, afterwards one pass); a
+    // partial still missing then is computed by the whole workgroup from memory and published, and
+    // the pollers look again.
+    const int words = A.range ? 6 : 4;
+    const unsigned long long* rep = A.gran + (size_t)(b % kFusedRep) * kSmallMaxG * kFusedWords;
+    const bool poller = wave < 4;
+    const int pk = 4 * lane + wave;  // the partial this lane polls (pollers)
+    const unsigned long long* mine = rep + (size_t)pk * kFusedWords;
+    if (poller) pw_have[pk] = 0u;
+    bool stealing = false;
+    for (;;) {
+      if (poller) {
+        uint32_t miss_bits = (pk < G && pw_have[pk] == 0u) ? (1u << words) - 1u : 0u;
+        const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+        uint32_t polls = 0;
+        for (;;) {
+          unsigned long long g[kFusedWords];
+#pragma unroll
+          for (int c = 0; c < kFusedWords; ++c) g[c] = c < words ? ld_sc1_u64(mine + c) : 0ull;
+#pragma unroll
+          for (int c = 0; c < kFusedWords; ++c) {
+            if (((miss_bits >> c) & 1u) && (uint32_t)(g[c] >> 32) == epoch) {
+              miss_bits &= ~(1u << c);
+              pw[pk][c] = (uint32_t)g[c];
+            }
+          }
+          if (__all(miss_bits == 0u) || stealing) break;
+          if ((++polls & 7) != 0) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t_start > steal_ticks) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (pk < G) pw_have[pk] = miss_bits == 0u ? 1u : 0u;
+        // first missing partial after b (cyclically)
+        int d = pk - b;
+        d += d < 0 ? G : 0;
+        int miss = miss_bits ? d : INT_MAX;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, kWave));
+        if (lane == 0) smiss[wave] = miss;
+      }
+      lds_barrier();
+      const int m = min(min(smiss[0], smiss[1]), min(smiss[2], smiss[3]));
+      if (m == INT_MAX) break;
+      // the patience ran out: compute partial (m + b) % G from memory (one group per lane in
+      // flight) and publish it
+      const int k = m + b < G ? m + b : m + b - G;
+      stealing = true;
+      const StatAcc pk_acc = fused_steal<TIN>(A.x, A.n, V, G, k, shift, &W);
+      if (wave == 0) fused_publish(pk_acc, A, k, epoch);
+    }
+    // count this workgroup past the wait now; the returned word is looked at only at the end
+    if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.left);
+    if (wave == 0) {
+      // reduce_partials_w0's order: lane l adds partials 4l .. 4l+3 from 0.0, then one ascending
+      // butterfly
+      double s1 = 0.0, s2 = 0.0;
+      float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = 4 * lane + q;
+        if (k >= G) continue;
+        s1 += __builtin_bit_cast(double, ((uint64_t)pw[k][1] << 32) | pw[k][0]);
+        s2 += __builtin_bit_cast(double, ((uint64_t)pw[k][3] << 32) | pw[k][2]);
+        if (A.range) {
+          mn = fminf(mn, __builtin_bit_cast(float, pw[k][4]));
+          mx = fmaxf(mx, __builtin_bit_cast(float, pw[k][5]));
+        }
+      }
+      s1 = wave_sum_asc(s1);
+      s2 = wave_sum_asc(s2);
+      if (A.range) {
+        mn = wave_min(mn);
+        mx = wave_max(mx);
+      }
+      if (lane == 0) {
+        const FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, nullptr, 0};
+        SmqSmaqStats st;
+        if (A.range) finalize_stats<true, TIN>(s1, s2, mn, mx, A.n, shift, false, f, &st);
+        else finalize_stats<false, TIN>(s1, s2, mn, mx, A.n, shift, false, f, &st);
+        st.rng_offset = off0;
+        sst = st;
+        if (b == 0) *A.hdr = st;
+      }
+    }
+  } else if (threadIdx.x == 0) {  // one chunk: the partial is the total
+    const FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, nullptr, 0};
+    SmqSmaqStats st;
+    if (A.range) finalize_stats<true, TIN>(part.s1, part.s2, part.mn, part.mx, A.n, shift, false, f, &st);
+    else finalize_stats<false, TIN>(part.s1, part.s2, part.mn, part.mx, A.n, shift, false, f, &st);
+    st.rng_offset = off0;
+    sst = st;
+    *A.hdr = st;
+    if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
+  }
+  lds_barrier();
+  if (PRE && wave == 0) {
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const float4 w = u0lds[u][lane];
+      uu[u][0] = w.x;
+      uu[u][1] = w.y;
+      uu[u][2] = w.z;
+      uu[u][3] = w.w;
+    }
+  }
+  // the last workgroup past the wait (its add, issued after the gather, has long returned)
+  // advances the generation and the stream and re-arms the arrival word, before its own stores
+  if (G > 1 && threadIdx.x == 0 &&
+      arrive_tagged_finish(A.left, gen, left_old) == (uint32_t)G - 1) {
+    st_sc1_u32(A.gen, gen + 1u);
+    if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
+    st_sc1_u64(A.left, (unsigned long long)(gen + 1u) << 32);
+  }
+  ElemConsts c;
+  const float cthr = TIN == kF32 ? A.thr : round_in<TIN>(A.thr);
+  init_consts(c, &sst, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
+  uniform_consts(c);  // LDS reads land in VGPRs: the constants are wave-uniform, keep them in SGPRs
+  const bool tail = b == G - 1 && threadIdx.x < (int)(A.n & 3);
+  uint32_t n_out;
+  if (sst.quot_check) {
+    if (A.all_pos) {
+      n_out = fused_transform<RM, V, TIN, true, true, PRE>(A, v, park, uu, c, base, off);
+      if (tail) n_out += fused_tail<RM, TIN, true, true>(A, c, off);
+    } else {
+      n_out = fused_transform<RM, V, TIN, false, true, PRE>(A, v, park, uu, c, base, off);
+      if (tail) n_out += fused_tail<RM, TIN, false, true>(A, c, off);
+    }
+  } else {
+    if (A.all_pos) {
+      n_out = fused_transform<RM, V, TIN, true, false, PRE>(A, v, park, uu, c, base, off);
+      if (tail) n_out += fused_tail<RM, TIN, true, false>(A, c, off);
+    } else {
+      n_out = fused_transform<RM, V, TIN, false, false, PRE>(A, v, park, uu, c, base, off);
+      if (tail) n_out += fused_tail<RM, TIN, false, false>(A, c, off);
+    }
+  }
+  if (A.count) {  // outlier count for log_size (smart.py:184-188), spread over the slots
+    const uint32_t t = wave_sum_u32(n_out);
+    if (lane == 0) sh_cnt[wave] = t;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      unsigned long long s = 0;
+#pragma unroll
+      for (int w = 0; w < kSmallWaves; ++w) s += sh_cnt[w];
+      if (s) atomicAdd(A.out_slots + (b & (SMQ_WS_OUTLIER_SLOTS - 1)), s);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host
+// ------------------------------------------------------------------------------------------------
+int launch_stats_small(const void* x, int dtype, int64_t n, bool vec, bool range,
+                       const FinalizeArgs& fin, void* ws, hipStream_t st, bool defer,
+                       int* def_g) {
+  const SmallGeom g = small_geom(n);
+  char* base = (char*)ws;
+  SmqSmaqStats* hdr = (SmqSmaqStats*)base;
+  unsigned long long* counter = (unsigned long long*)(base + SmaqWsLayout::kTagCounters);
+  StatPartial* partials = (StatPartial*)(base + SmaqWsLayout::kPartials);
+  double* def_rec = nullptr;
+  ArriveTag tag{};
+  if (defer) {
+    if (def_g) *def_g = g.G > 1 ? g.G : 0;
+    if (g.G > 1) def_rec = (double*)(base + SmaqWsLayout::kDeferRec);
+  }
+  if (!def_rec) tag = arrive_tag(ws, st);  // the tag prediction follows the calls that arrive
+  const dim3 grid((unsigned)g.G), block(kSmallT);
+  const int vi = vec ? 1 : 0, ri = range ? 1 : 0;
+  if (dtype == SMQ_DTYPE_F32)
+    hipLaunchKernelGGL(smaq_stats_small_kernel<kF32>, grid, block, 0, st, x, n, g.V, vi, ri, fin,
+                       partials, counter, tag, hdr, def_rec);
+  else if (dtype == SMQ_DTYPE_F16)
+    hipLaunchKernelGGL(smaq_stats_small_kernel<kF16>, grid, block, 0, st, x, n, g.V, vi, ri, fin,
+                       partials, counter, tag, hdr, def_rec);
+  else
+    hipLaunchKernelGGL(smaq_stats_small_kernel<kBF16>, grid, block, 0, st, x, n, g.V, vi, ri, fin,
+                       partials, counter, tag, hdr, def_rec);
+  return check_launch("smaq_stats_small_kernel");
+}
+
+template <int RM, int V, int TIN>
+static int launch_fused_v(const FusedArgs& F, hipStream_t st) {
+  // one workgroup per CU: without the LDS request two small-V workgroups could share a CU while
+  // another stays idle
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&smaq_fused_kernel<RM, V, TIN>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLds);
+  if (attr != hipSuccess) {
+    set_error("smaq_fused_kernel: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed: %s",
+              hipGetErrorString(attr));
+    return SMQ_ERR_LAUNCH;
+  }
+  const int lds = (F.G > 1 || V > 4) ? kFusedLds : 0;  // parking (V > 4): (V - 4) * 16 KiB
+  static_assert(kFusedLds >= (kSmallMaxV - 4) * kSmallT * 16, "LDS parking");
+  hipLaunchKernelGGL((smaq_fused_kernel<RM, V, TIN>), dim3((unsigned)F.G), dim3(kSmallT), lds, st,
+                     F);
+  return check_launch("smaq_fused_kernel");
+}
+
+template <int RM, int TIN>
+static int launch_fused_rm(const FusedArgs& F, int V, hipStream_t st) {
+  switch (V) {
+    case 1: return launch_fused_v<RM, 1, TIN>(F, st);
+    case 2: return launch_fused_v<RM, 2, TIN>(F, st);
+    case 3: return launch_fused_v<RM, 3, TIN>(F, st);
+    case 4: return launch_fused_v<RM, 4, TIN>(F, st);
+    case 5: return launch_fused_v<RM, 5, TIN>(F, st);
+    case 6: return launch_fused_v<RM, 6, TIN>(F, st);
+    case 7: return launch_fused_v<RM, 7, TIN>(F, st);
+    default: return launch_fused_v<RM, 8, TIN>(F, st);
+  }
+}
+
+int launch_fused(const FusedCall& c, hipStream_t st) {
+  const SmqSmaqParams* p = c.p;
+  const SmallGeom g = small_geom(c.n);
+  char* base = (char*)c.ws;
+  FusedArgs F;
+  memset(&F, 0, sizeof(F));
+  F.x = c.x;
+  F.y = c.y;
+  F.n = c.n;
+  F.nv = c.n >> 2;
+  F.G = g.G;
+  F.key = rng_key(p->seed);
+  F.offset = p->offset;
+  F.ctr = p->offset_counter;
+  F.hdr = (SmqSmaqStats*)base;
+  F.gen = (uint32_t*)(base + SmaqWsLayout::kFusedGen);
+  F.left = (unsigned long long*)(base + SmaqWsLayout::kFusedLeft);
+  F.gran = (unsigned long long*)(base + SmaqWsLayout::kFusedGran);
+  F.out_slots = (unsigned long long*)(base + SmaqWsLayout::kSlots);
+  F.thr = p->main_std_dev_threshold;
+  F.r_main = p->range_main;
+  F.r_out = p->range_outlier;
+  F.clamp_lo = p->clamp_lo;
+  F.clamp_hi = p->clamp_hi;
+  F.range_coef = c.range_coef;
+  F.inv_r_main = c.inv_r_main;
+  F.inv_r_out = c.inv_r_out;
+  F.all_pos = p->all_positive;
+  F.count = p->count_outliers;
+  F.range = p->use_range_std_dev;
+  F.test_late = c.test_late;
+  if (p->count_outliers &&
+      hipMemsetAsync(F.out_slots, 0, 8 * SMQ_WS_OUTLIER_SLOTS, st) != hipSuccess) {
+    set_error("hipMemsetAsync of the outlier slots failed");
+    return SMQ_ERR_LAUNCH;
+  }
+  const bool sr = p->stochastic_rounding != 0;
+  if (c.dtype == SMQ_DTYPE_F32)
+    return sr ? launch_fused_rm<kRoundHash, kF32>(F, g.V, st)
+              : launch_fused_rm<kRoundTrunc, kF32>(F, g.V, st);
+  if (c.dtype == SMQ_DTYPE_F16)
+    return sr ? launch_fused_rm<kRoundHash, kF16>(F, g.V, st)
+              : launch_fused_rm<kRoundTrunc, kF16>(F, g.V, st);
+  return sr ? launch_fused_rm<kRoundHash, kBF16>(F, g.V, st)
+            : launch_fused_rm<kRoundTrunc, kBF16>(F, g.V, st);
+}
+
+}  // namespace smq

@@ -10,6 +10,10 @@ namespace smq {
 // Full or sampled statistics of x into the workspace header (SmqSmaqStats at offset 0).
 int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
                   size_t ws_bytes, hipStream_t st);
+// Full statistics of x (the single-tensor statistics launch, finalised by its last workgroup) into
+// *out instead of the workspace header (multi-tensor calls: tensors above the small partition).
+int stats_into(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
+               size_t ws_bytes, hipStream_t st, SmqSmaqStats* out);
 // Workspace bytes prepare_stats needs for n elements.
 size_t smaq_stats_ws_bytes(int64_t n);
 // The multi-workgroup Floyd draw of k > SMQ_MAX_DEVICE_SAMPLES indices (smaq.hip): memsets and the

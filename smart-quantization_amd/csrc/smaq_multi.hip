@@ -4,10 +4,17 @@
 // (grads, weights, momenta), each of which runs smart.py:110-190 separately (~24 ATen launches
 // + 1 host sync per tensor; a ResNet-34 step has 148 such tensors, median 256 elements).
 //
-// Design: the tensors are cut into fixed chunks (4096 elements by default); one workgroup per chunk.
-//   launch 1 (stats): per-chunk shifted fp64 sums; a tensor with one chunk finalises in place,
-//            a larger tensor's last-arriving chunk reduces that tensor's partials in chunk order.
-//   launch 2 (apply): per chunk, the tensor's SmqSmaqStats + the element transform of smaq.hip,
+// Design: a multi call computes, per tensor, EXACTLY what a single-tensor call computes — the same
+// statistics partials, reduced in the same order, the same element transform at the same counter
+// offsets — so its outputs equal the per-tensor calls' bit for bit by construction.
+//   statistics of tensors up to kSmallMaxN elements (smaq_small.h): one launch for all of them; a
+//            workgroup computes a run of consecutive partials of one tensor (each the 1024-lane
+//            partial of the single-tensor partition, emulated with four lanes per thread), stores
+//            them and arrives on the tensor's counter; the tensor's last workgroup reduces its
+//            partials in reduce_partials_w0's order and finalises.
+//   statistics of larger tensors: the single-tensor statistics launch itself (smaq.hip
+//            launch_stats), one per such tensor, into the tensor's record.
+//   apply: per 4096-element chunk, the tensor's SmqSmaqStats + the element transform of smaq.hip,
 //            RNG counter = params.offset + desc.rng_offset + element index (so a multi call equals
 //            the sequence of single-tensor calls at those offsets, and a plan is reusable).
 // y may alias x: every element is read once by the apply launch before it is written.
@@ -23,17 +30,23 @@
 
 #include "smq_common.h"
 #include "smaq_elem.h"
+#include "smaq_host.h"
+#include "smaq_small.h"
 
 namespace smq {
 
-// Elements per workgroup, separately for the two launches (env SMQ_MULTI_CHUNK / _STATS_CHUNK,
+// Elements per workgroup, separately for the two launches (knobs SMQ_MULTI_CHUNK / _STATS_CHUNK,
 // multiples of 4096). Measured on the ResNet-34 set (42.5M elements, 148 tensors): the statistics
 // launch wants few, long chunks (each chunk's partial hand-off is a store-drain + atomic round
 // trip: 8K chunks 62 us, 32K chunks 34 us; with the next 16 KiB step prefetched, r04: 32K 32.6 us,
 // 64K 30.7 us, 128K 38.3 us), the apply launch wants many short ones (8K 60 us, 32K 80 us; with
-// sc0 sc1 nt output stores the whole step: 4K 79.9 us, 8K 82.3 us).
+// sc0 sc1 nt output stores the whole step: 4K 79.9 us, 8K 82.3 us). A statistics workgroup takes
+// as many whole partials of its tensor as fit its chunk (at least one).
 constexpr int64_t kDefaultChunk = 4096;
 constexpr int64_t kDefaultStatsChunk = 65536;
+// workspace region of the single-tensor statistics launches of the large tensors
+constexpr size_t kBigWsBytes = (SmaqWsLayout::kTagCounters + 8 * SmaqWsLayout::kTagWords + 255) &
+                               ~(size_t)255;
 constexpr size_t kSnapBytes = 64;  // workspace slot: the call's random-stream snapshot
 
 struct MultiHeader {
@@ -41,7 +54,7 @@ struct MultiHeader {
   int32_t n_chunks;       // apply chunks
   int64_t chunk;
   int32_t n_stat_chunks;  // statistics chunks (their records follow the apply chunk records)
-  int32_t reserved0;
+  int32_t n_partials;     // statistics partials of the small tensors
   int64_t stat_chunk;
 };
 
@@ -51,11 +64,12 @@ struct ChunkDesc {
   const void* x;        // tensor base (element type: the call's dtype)
   float* y;
   int64_t n;            // tensor elements
-  int64_t begin, end;   // element range of this chunk within the tensor
+  int64_t begin, end;   // apply: element range of this chunk; statistics: its partials [begin, end)
   uint64_t rng_offset;  // tensor's RNG offset relative to params.offset
   int32_t tensor;
-  int32_t first_chunk;  // global index of the tensor's first chunk
-  int32_t n_chunks;     // chunks of this tensor
+  int32_t first_chunk;  // apply: global index of the tensor's first chunk; statistics: of its first
+                        // partial in the partial array
+  int32_t n_chunks;     // chunks of this tensor (statistics: workgroups arriving on its counter)
   int32_t all_positive;
 };
 
@@ -93,9 +107,17 @@ __device__ __forceinline__ float multi_range_coef(const MultiArgs& A, int t, int
   return c >= 0.0f ? c : 1.0f / sqrtf(2.0f * logf((float)n));
 }
 
+// Statistics of the tensors up to kSmallMaxN elements. Workgroup = partials [begin, end) of one
+// tensor in the single-tensor partition (smaq_small.h); a step = virtual lane t + 256 k of one
+// partial (its V groups), the next step's loads in flight while the current one is summed; the 16
+// virtual wave values of a partial are combined in small_combine's order (LDS, double-buffered by
+// partial parity). A tensor of one partial finalises in place; otherwise the partials are stored
+// (sc1) and the tensor's last workgroup reduces them in reduce_partials_w0's order — the
+// single-tensor call's statistics, bit for bit.
 template <int TIN, bool RANGE>
 __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   __shared__ uint32_t slot;
+  __shared__ SmallWaveLds W[2];
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // one snapshot + advance per call
     uint64_t o = 0;
     if (A.rng_ctr) {
@@ -107,95 +129,80 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   const ChunkDesc ch = A.stat_chunks[blockIdx.x];
   const void* __restrict__ x = ch.x;
   const int64_t n = ch.n;
-  const float k0 = load1<TIN>(x, 0), k1 = load1<TIN>(x, n >> 1), k2 = load1<TIN>(x, n - 1);
-  const double shift = (double)fmaxf(fminf(k0, k1), fminf(fmaxf(k0, k1), k2));
-  StatAcc acc, ay, az, aw;
-  if (((uintptr_t)x & (TIN == kF32 ? 15u : 7u)) == 0) {
-    const int64_t b4 = ch.begin >> 2, e4 = ch.end >> 2;  // begin is a multiple of the chunk
-    // 16 KiB steps; the next step's four loads are in flight while the current one is summed
-    float4 cur[4], nxt[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t j = b4 + threadIdx.x + u * kBlock;
-      cur[u] = j < e4 ? load4<TIN>(x, j) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    for (int64_t t0 = b4; t0 < e4; t0 += 4 * kBlock) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t j = t0 + 4 * kBlock + threadIdx.x + u * kBlock;
-        nxt[u] = j < e4 ? load4<TIN>(x, j) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t j = t0 + threadIdx.x + u * kBlock;
-        if (j < e4) {  // four independent fp64 chains (one per component), as the single sweep
-          acc.add<RANGE>(cur[u].x, shift);
-          ay.add<RANGE>(cur[u].y, shift);
-          az.add<RANGE>(cur[u].z, shift);
-          aw.add<RANGE>(cur[u].w, shift);
-        }
-        cur[u] = nxt[u];
-      }
-    }
-    if (threadIdx.x < (int)(ch.end - (e4 << 2))) acc.add<RANGE>(load1<TIN>(x, (e4 << 2) + threadIdx.x), shift);
-    acc.s1 = (acc.s1 + ay.s1) + (az.s1 + aw.s1);
-    acc.s2 = (acc.s2 + ay.s2) + (az.s2 + aw.s2);
-    if (RANGE) {
-      acc.mn = fminf(fminf(acc.mn, ay.mn), fminf(az.mn, aw.mn));
-      acc.mx = fmaxf(fmaxf(acc.mx, ay.mx), fmaxf(az.mx, aw.mx));
-    }
-  } else {
-    for (int64_t j = ch.begin + threadIdx.x; j < ch.end; j += kBlock) acc.add<RANGE>(load1<TIN>(x, j), shift);
-  }
-  block_reduce_stats<RANGE>(acc);
+  const SmallGeom g = small_geom(n);
+  const int V = g.V, G = g.G;
+  const int64_t nv = n >> 2;
+  const double shift = stats_shift<TIN>(x, n);
+  const bool vec = ((uintptr_t)x & (TIN == kF32 ? 15u : 7u)) == 0;
+  const int p = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
+  const int w0 = (int)ch.begin;
+  const int steps = 4 * (int)(ch.end - ch.begin);
   const FinalizeArgs fin{A.clamp_lo, A.clamp_hi, RANGE ? multi_range_coef(A, ch.tensor, n) : 0.0f};
-  if (ch.n_chunks == 1) {
-    if (threadIdx.x == 0)
-      finalize_stats<RANGE, TIN>(acc.s1, acc.s2, acc.mn, acc.mx, n, shift, false, fin,
-                                 &A.stats[ch.tensor]);
-    return;
+  auto load_step = [&](int s, float4 (&dst)[kSmallMaxV]) {
+    const int64_t base = (int64_t)(w0 + (s >> 2)) * V * kSmallT + threadIdx.x + kBlock * (s & 3);
+#pragma unroll
+    for (int u = 0; u < kSmallMaxV; ++u) {
+      const int64_t j = base + (int64_t)u * kSmallT;
+      if (u < V && j < nv) dst[u] = small_group<TIN>(x, j, vec);
+    }
+  };
+  float4 cur[kSmallMaxV], nxt[kSmallMaxV];
+  load_step(0, cur);
+  for (int st = 0; st < steps; ++st) {
+    if (st + 1 < steps) load_step(st + 1, nxt);
+    const int w = w0 + (st >> 2), k = st & 3;
+    const StatAcc a = small_wave(small_lane_sum<TIN, kSmallMaxV>(x, n, V, G, w,
+                                                                 threadIdx.x + kBlock * k, cur,
+                                                                 shift));
+    SmallWaveLds& Wb = W[w & 1];
+    if (l == 0) {
+      Wb.s1[p + 4 * k] = a.s1;
+      Wb.s2[p + 4 * k] = a.s2;
+      Wb.mn[p + 4 * k] = a.mn;
+      Wb.mx[p + 4 * k] = a.mx;
+    }
+    if (k == 3) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const StatAcc r = small_combine(Wb);
+        if (G == 1) {
+          finalize_stats<RANGE, TIN>(r.s1, r.s2, r.mn, r.mx, n, shift, false, fin,
+                                     &A.stats[ch.tensor]);
+        } else {
+          StatPartial* q = A.partials + ch.first_chunk + w;
+          st_sc1_f64(&q->s1, r.s1);
+          st_sc1_f64(&q->s2, r.s2);
+          st_sc1_f32x2(&q->mn, r.mn, r.mx);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kSmallMaxV; ++u) cur[u] = nxt[u];
   }
-  if (threadIdx.x == 0) {
-    StatPartial* p = A.partials + blockIdx.x;
-    st_sc1_f64(&p->s1, acc.s1);
-    st_sc1_f64(&p->s2, acc.s2);
-    if (RANGE) st_sc1_f32x2(&p->mn, acc.mn, acc.mx);
-  }
+  if (G == 1) return;
   const uint32_t prev = block_arrive_tagged(&A.counters[ch.tensor], A.tag.tag, &slot);
   if (prev != (uint32_t)ch.n_chunks - 1) return;
-  // batches of loads issued before they are consumed (one round trip per batch, not per partial)
-  constexpr int K = 8;
-  StatAcc tot;
-  for (int b0 = 0; b0 < ch.n_chunks; b0 += K * kBlock) {
-    double s1v[K], s2v[K];
-    float mnv[K], mxv[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const int b = b0 + threadIdx.x + i * kBlock;
-      if (b < ch.n_chunks) {
-        const StatPartial* p = A.partials + ch.first_chunk + b;
-        s1v[i] = ld_sc1_f64(&p->s1);
-        s2v[i] = ld_sc1_f64(&p->s2);
-        if (RANGE) ld_sc1_f32x2(&p->mn, mnv[i], mxv[i]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      if (b0 + threadIdx.x + i * kBlock < ch.n_chunks) {
-        tot.s1 += s1v[i];
-        tot.s2 += s2v[i];
-        if (RANGE) {
-          tot.mn = fminf(tot.mn, mnv[i]);
-          tot.mx = fmaxf(tot.mx, mxv[i]);
-        }
-      }
+  if (threadIdx.x < kWave) {
+    double t1, t2;
+    float tmn, tmx;
+    reduce_partials_w0<true>(A.partials + ch.first_chunk, G, true, t1, t2, tmn, tmx);
+    if (threadIdx.x == 0) {
+      finalize_stats<RANGE, TIN>(t1, t2, tmn, tmx, n, shift, false, fin, &A.stats[ch.tensor]);
+      arrive_reset(&A.counters[ch.tensor], A.tag.next);
     }
   }
-  block_reduce_stats<RANGE>(tot);
+}
+
+// Only the call's stream snapshot (no tensor of the call is small enough for the statistics launch
+// above, which takes it otherwise).
+__global__ void smaq_multi_snap_kernel(MultiArgs A) {
   if (threadIdx.x == 0) {
-    finalize_stats<RANGE, TIN>(tot.s1, tot.s2, tot.mn, tot.mx, n, shift, false, fin,
-                               &A.stats[ch.tensor]);
-    arrive_reset(&A.counters[ch.tensor], A.tag.next);
+    uint64_t o = 0;
+    if (A.rng_ctr) {
+      o = *A.rng_ctr;
+      *A.rng_ctr = o + A.rng_span;
+    }
+    *A.rng_snap = o;
   }
 }
 
@@ -322,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_apply_kernel(MultiArgs A) {
 
 static int64_t chunk_elems() {
   static const int64_t c = [] {
-    const char* e = getenv("SMQ_MULTI_CHUNK");
+    const char* e = knob_env("SMQ_MULTI_CHUNK");
     const int64_t v = e ? atoll(e) : kDefaultChunk;
     return (v >= 4096 && v % 4096 == 0) ? v : kDefaultChunk;
   }();
@@ -331,7 +338,7 @@ static int64_t chunk_elems() {
 
 static int64_t stats_chunk_elems() {
   static const int64_t c = [] {
-    const char* e = getenv("SMQ_MULTI_STATS_CHUNK");
+    const char* e = knob_env("SMQ_MULTI_STATS_CHUNK");
     const int64_t v = e ? atoll(e) : kDefaultStatsChunk;
     return (v >= 4096 && v % 4096 == 0) ? v : kDefaultStatsChunk;
   }();
@@ -342,24 +349,64 @@ static int64_t chunks_of(int64_t n, int64_t c) { return (n + c - 1) / c; }
 
 struct PlanSizes {
   size_t hdr, descs, chunks, stat_chunks, total;
-  int64_t n_chunks, n_stat_chunks;
+  int64_t n_chunks, n_stat_chunks, n_partials;
+  bool big;  // a tensor above kSmallMaxN (its statistics: the single-tensor launch)
 };
 
+// Statistics workgroups of a small tensor: whole partials, as many as fit the statistics chunk.
+static int64_t partials_per_wg(int64_t n) {
+  const SmallGeom g = small_geom(n);
+  const int64_t per = stats_chunk_elems() / ((int64_t)g.V * kSmallT * 4);
+  return per < 1 ? 1 : per;
+}
+
 static bool plan_sizes(const int64_t* sizes, int count, PlanSizes* ps) {
-  int64_t nc = 0, ns = 0;
+  int64_t nc = 0, ns = 0, np = 0;
+  bool big = false;
   for (int t = 0; t < count; ++t) {
     if (sizes[t] < 1) return false;
     nc += chunks_of(sizes[t], chunk_elems());
-    ns += chunks_of(sizes[t], stats_chunk_elems());
+    if (sizes[t] > kSmallMaxN) {
+      big = true;
+      continue;
+    }
+    const int64_t G = small_geom(sizes[t]).G;
+    np += G;
+    ns += chunks_of(G, partials_per_wg(sizes[t]));
   }
   ps->n_chunks = nc;
   ps->n_stat_chunks = ns;
+  ps->n_partials = np;
+  ps->big = big;
   ps->hdr = sizeof(MultiHeader);
   ps->descs = ((sizeof(SmqTensorDesc) * (size_t)count) + 31) & ~(size_t)31;
   ps->chunks = sizeof(ChunkDesc) * (size_t)nc;
   ps->stat_chunks = sizeof(ChunkDesc) * (size_t)ns;
   ps->total = ps->hdr + ps->descs + ps->chunks + ps->stat_chunks;
   return true;
+}
+
+// Statistics records: per small tensor, runs of partials_per_wg partials.
+static void fill_stat_chunks(ChunkDesc* ch, const SmqTensorDesc* descs, int count) {
+  int32_t g = 0, part = 0;
+  for (int t = 0; t < count; ++t) {
+    const int64_t n = descs[t].n;
+    if (n > kSmallMaxN) continue;
+    const int64_t G = small_geom(n).G, per = partials_per_wg(n), wgs = chunks_of(G, per);
+    for (int64_t c = 0; c < wgs; ++c, ++g) {
+      ch[g].x = descs[t].x;
+      ch[g].y = descs[t].y;
+      ch[g].n = n;
+      ch[g].begin = c * per;
+      ch[g].end = (c + 1) * per < G ? (c + 1) * per : G;
+      ch[g].rng_offset = descs[t].rng_offset;
+      ch[g].tensor = t;
+      ch[g].first_chunk = part;
+      ch[g].n_chunks = (int32_t)wgs;
+      ch[g].all_positive = descs[t].all_positive;
+    }
+    part += (int32_t)G;
+  }
 }
 
 // Chunk records of one map (element chunks of C) for every tensor, starting at ch.
@@ -428,19 +475,25 @@ int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_
   h->n_chunks = (int32_t)ps.n_chunks;
   h->chunk = chunk_elems();
   h->n_stat_chunks = (int32_t)ps.n_stat_chunks;
+  h->n_partials = (int32_t)ps.n_partials;
   h->stat_chunk = stats_chunk_elems();
   memcpy(base + ps.hdr, descs, sizeof(SmqTensorDesc) * (size_t)count);
   fill_chunks((ChunkDesc*)(base + ps.hdr + ps.descs), descs, count, h->chunk);
-  fill_chunks((ChunkDesc*)(base + ps.hdr + ps.descs + ps.chunks), descs, count, h->stat_chunk);
+  fill_stat_chunks((ChunkDesc*)(base + ps.hdr + ps.descs + ps.chunks), descs, count);
   return SMQ_OK;
+}
+
+static size_t multi_ws_bytes(int count, int64_t n_partials, bool big) {
+  const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
+  const size_t counters = ((sizeof(uint64_t) * (size_t)count) + 63) & ~(size_t)63;
+  const size_t parts = (sizeof(StatPartial) * (size_t)n_partials + 255) & ~(size_t)255;
+  return ((stats + counters + kSnapBytes + 255) & ~(size_t)255) + parts + (big ? kBigWsBytes : 0);
 }
 
 size_t smq_smaq_multi_workspace_bytes(const int64_t* sizes, int count) {
   PlanSizes ps;
   if (!sizes || count < 1 || !plan_sizes(sizes, count, &ps)) return 0;
-  const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
-  const size_t counters = ((sizeof(uint64_t) * (size_t)count) + 63) & ~(size_t)63;
-  return stats + counters + kSnapBytes + sizeof(StatPartial) * (size_t)ps.n_stat_chunks;
+  return multi_ws_bytes(count, ps.n_partials, ps.big);
 }
 
 }  // extern "C"
@@ -450,6 +503,8 @@ static int launch_multi(const MultiArgs& A, bool sampled, bool range, int n_stat
                         int count, int n_chunks, hipStream_t st) {
   if (sampled) {
     hipLaunchKernelGGL((smaq_multi_draw_kernel<TIN>), dim3(count), dim3(kBlock), 0, st, A);
+  } else if (n_stat_chunks == 0) {  // only large tensors: their statistics are launched already
+    hipLaunchKernelGGL(smaq_multi_snap_kernel, dim3(1), dim3(kWave), 0, st, A);
   } else if (range) {
     hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kBlock), 0,
                        st, A);
@@ -480,7 +535,8 @@ extern "C" int smq_smaq_multi(const void* dev_plan, const void* host_plan, int d
   const int count = hh->count;
   const int n_chunks = hh->n_chunks;
   const int n_stat_chunks = hh->n_stat_chunks;
-  if (!dev_plan || count < 1 || n_chunks < 1 || n_stat_chunks < 1 || !p || !ws) {
+  const int n_partials = hh->n_partials;
+  if (!dev_plan || count < 1 || n_chunks < 1 || n_stat_chunks < 0 || !p || !ws) {
     set_error("multi: bad arguments");
     return SMQ_ERR_INVALID;
   }
@@ -502,15 +558,17 @@ extern "C" int smq_smaq_multi(const void* dev_plan, const void* host_plan, int d
     set_error("multi: the BN variant is per activation tensor (smq_smaq_apply)");
     return SMQ_ERR_INVALID;
   }
+  const SmqTensorDesc* hd = (const SmqTensorDesc*)((const char*)host_plan + sizeof(MultiHeader));
+  bool big = false;
+  for (int t = 0; t < count && !big; ++t) big = hd[t].n > kSmallMaxN;
   const size_t stats = sizeof(SmqSmaqStats) * (size_t)count;
   const size_t counters = ((sizeof(uint64_t) * (size_t)count) + 63) & ~(size_t)63;
-  const size_t need = stats + counters + kSnapBytes + sizeof(StatPartial) * (size_t)n_stat_chunks;
+  const size_t need = multi_ws_bytes(count, n_partials, big);
   if (ws_bytes < need) {
     set_error("multi: workspace too small: need %zu bytes, got %zu", need, ws_bytes);
     return SMQ_ERR_WORKSPACE;
   }
   if (dtype != SMQ_DTYPE_F32) {  // fp32 outputs: an in-place half tensor cannot hold them
-    const SmqTensorDesc* hd = (const SmqTensorDesc*)((const char*)host_plan + sizeof(MultiHeader));
     for (int t = 0; t < count; ++t)
       if ((const void*)hd[t].x == (const void*)hd[t].y) {
         set_error("multi: tensor %d: fp16 / bf16 inputs write fp32 outputs, y cannot alias x", t);
@@ -530,11 +588,11 @@ extern "C" int smq_smaq_multi(const void* dev_plan, const void* host_plan, int d
   A.counters = (unsigned long long*)(wb + stats);
   A.tag = arrive_tag(ws, (hipStream_t)stream);
   A.rng_snap = (uint64_t*)(wb + stats + counters);
-  A.partials = (StatPartial*)(wb + stats + counters + kSnapBytes);
+  const size_t parts_at = (stats + counters + kSnapBytes + 255) & ~(size_t)255;
+  A.partials = (StatPartial*)(wb + parts_at);
   A.rng_ctr = p->offset_counter;
   uint64_t span = 0;  // the stream span of the call, from the host copy of the descriptors
   if (A.rng_ctr) {
-    const SmqTensorDesc* hd = (const SmqTensorDesc*)((const char*)host_plan + sizeof(MultiHeader));
     for (int t = 0; t < count; ++t) {
       const uint64_t e = hd[t].rng_offset + (uint64_t)hd[t].n;
       span = e > span ? e : span;
@@ -560,6 +618,20 @@ extern "C" int smq_smaq_multi(const void* dev_plan, const void* host_plan, int d
   A.advance_in_apply = sampled ? 1 : 0;
   hipStream_t st = (hipStream_t)stream;
   const bool range = p->use_range_std_dev != 0;
+  if (big && !sampled) {
+    // tensors above kSmallMaxN: the single-tensor statistics launch, into the tensor's record (its
+    // own partition and reduction order, so the statistics are a single call's); no stream
+    // position is taken here (the element kernels read the call's snapshot)
+    char* bws = wb + parts_at + ((sizeof(StatPartial) * (size_t)n_partials + 255) & ~(size_t)255);
+    for (int t = 0; t < count; ++t) {
+      if (hd[t].n <= kSmallMaxN) continue;
+      SmqSmaqParams q = *p;
+      q.offset_counter = nullptr;
+      q.range_std_coef = hd[t].range_std_coef;
+      const int rc = stats_into(hd[t].x, dtype, hd[t].n, &q, bws, kBigWsBytes, st, &A.stats[t]);
+      if (rc) return rc;
+    }
+  }
   if (dtype == SMQ_DTYPE_F32)
     return launch_multi<kF32>(A, sampled, range, n_stat_chunks, count, n_chunks, st);
   if (dtype == SMQ_DTYPE_F16)

@@ -1368,7 +1368,7 @@ static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int 
   // head of the stream is the part still in the Infinity Cache right after a compress (256M: 325 ->
   // 293 us). Measurement knob SMQ_UNPACK_REVERSE=1.
   static const int rev = [] {
-    const char* e = getenv("SMQ_UNPACK_REVERSE");
+    const char* e = knob_env("SMQ_UNPACK_REVERSE");
     return e ? atoi(e) : 0;
   }();
   A.reverse = rev;

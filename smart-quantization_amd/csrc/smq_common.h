@@ -11,7 +11,25 @@
 
 #include "smq.h"
 
+#include <stdlib.h>
+
 namespace smq {
+
+// Measurement knobs: environment overrides of tuning constants, read ONLY by experiment builds
+// (tools/build_variant.py <name> -DSMQ_KNOBS=1). The shipped library never consults the
+// environment for them, so no stray variable can change a launch shape or a reduction order (and
+// with it the bits a caller gets).
+#ifndef SMQ_KNOBS
+#define SMQ_KNOBS 0
+#endif
+static inline const char* knob_env(const char* name) {
+#if SMQ_KNOBS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 constexpr int kBlock = 256;  // 4 wave64 per workgroup
 constexpr int kWave = 64;
@@ -281,7 +299,21 @@ struct SmaqWsLayout {
   // workspace captured into one graph each find their own word on every replay.
   static constexpr size_t kTagCounters = SMQ_WS_SAMPLES_OFFSET + 8 * SMQ_MAX_DEVICE_SAMPLES;
   static constexpr int kTagWords = 64;
+  // single-launch round trip (smaq_fused.hip): generation word, arrival word, then the granules
+  // [kFusedRep][kFusedWords][256] of the partials
+  static constexpr size_t kFused = SMQ_WS_FUSED_OFFSET;
+  static constexpr size_t kFusedGen = kFused;
+  static constexpr size_t kFusedLeft = kFused + 64;
+  static constexpr size_t kFusedGran = kFused + 128;
+  static constexpr int kFusedRep = 8;
+  static constexpr int kFusedWords = 6;  // s1 low / high, s2 low / high, min, max
+  static constexpr size_t kFusedEnd = kFusedGran + 8 * (size_t)kFusedRep * kFusedWords * 256;
+  static constexpr size_t kTotal = kFusedEnd;
 };
+static_assert(SmaqWsLayout::kTagCounters + 8 * SmaqWsLayout::kTagWords <= SMQ_WS_FUSED_OFFSET,
+              "smq.h SMQ_WS_FUSED_OFFSET overlaps the tag counters");
+static_assert(SmaqWsLayout::kFusedEnd <= SMQ_WS_LARGE_SAMPLES_OFFSET,
+              "smq.h SMQ_WS_LARGE_SAMPLES_OFFSET overlaps the fused region");
 
 // Inclusive wave64 prefix sum by DPP row shifts and row broadcasts (GFX9 rows of 16 lanes; the
 // classic AMDGPU scan: row_shr 1, 2, 4, 8, then row_bcast:15 into rows 1 and 3 and row_bcast:31

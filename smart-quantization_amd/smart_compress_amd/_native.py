@@ -19,11 +19,12 @@ LIB_PATH = os.environ.get(
     "SMQ_LIB", os.path.join(os.path.dirname(_PKG_DIR), "lib", "libsmq.so")
 )
 
-SMQ_ABI_VERSION = 5
+SMQ_ABI_VERSION = 6
 SMQ_MAX_SAMPLES = 64
 SMQ_MAX_DEVICE_SAMPLES = 4096
 SMQ_MAX_DRAW_SAMPLES = 1 << 28
-SMQ_WS_LARGE_SAMPLES_OFFSET = 99584
+SMQ_WS_FUSED_OFFSET = 99584
+SMQ_WS_LARGE_SAMPLES_OFFSET = 198016
 SMQ_WS_OUTLIER_SLOTS_OFFSET = 128
 SMQ_WS_OUTLIER_SLOTS = 64
 SMQ_WS_SAMPLES_OFFSET = 66176
@@ -31,6 +32,9 @@ SMQ_STATS_WORKSPACE = 0
 SMQ_STATS_SAMPLED = 1
 SMQ_STATS_INJECTED = 2
 SMQ_STATS_SAMPLED_DEVICE = 3
+SMQ_SMAQ_SPLIT = 1
+SMQ_SMAQ_NO_DEFER = 2
+SMQ_SMAQ_TEST_LATE = 4
 SMQ_S2FP8_OUT_Y = 1
 SMQ_S2FP8_OUT_T = 2
 SMQ_S2FP8_EXACT_POW = 4
@@ -228,6 +232,10 @@ SIGNATURES = {
     "smq_smaq_roundtrip": (
         _I32,
         [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _SZ, _P],
+    ),
+    "smq_smaq_roundtrip_ex": (
+        _I32,
+        [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _SZ, _U32, _P],
     ),
     "smq_smaq_multi_plan_bytes": (_SZ, [ctypes.POINTER(_I64), _I32]),
     "smq_smaq_multi_plan_build": (_I32, [ctypes.POINTER(SmqTensorDesc), _I32, _P, _SZ]),

@@ -5,7 +5,10 @@ Reference: util/pytorch/optimizer.py:69-127 runs ``SmartFP.__call__`` once per p
 ``SmaqMulti`` computes exactly what those per-tensor calls compute — each tensor keeps its own
 statistics (full, range-std or device-drawn samples: smart.py:86-108), its own ``all_positive``
 flag and passthrough below ``min_size`` — in two launches of libsmq (``smq_smaq_multi``) per input
-dtype of the list (fp32 / fp16 / bf16; outputs fp32 like the single-tensor path).
+dtype of the list (fp32 / fp16 / bf16; outputs fp32 like the single-tensor path), plus the
+single-tensor statistics launch of each tensor above 8,388,611 elements. Each tensor's statistics
+are computed in the single-tensor call's partition and reduction order, so the outputs equal the
+per-tensor calls at the same stream offsets bit for bit.
 
 The plan (descriptor table + chunk map) is cached by the list's pointers and sizes, so a training
 loop whose parameter and gradient buffers stay put uploads it once.

@@ -181,19 +181,25 @@ def test_validation_errors_without_device():
 
 
 def test_multi_plan_layout():
+    """Plan = header, descriptors, the apply map (4096-element chunks) and the statistics map: per
+    tensor up to 8,388,611 elements, runs of whole partials of the single-tensor partition
+    (csrc/smaq_small.h: V groups of 4 per lane of 1024, G partials), at most 65536 elements per
+    workgroup; larger tensors have no record (their statistics are the single-tensor launch)."""
     from smart_compress_amd import _native as N
 
     lib = N.lib()
     C, S = 4096, 65536  # default apply / statistics chunks (csrc/smaq_multi.hip)
-    sizes = [10, C, C + 1, 3 * C + 5, S + 1]
+    sizes = [10, C, C + 1, 3 * C + 5, S + 1, 300000, 9 << 20]
     count = len(sizes)
     arr = (ctypes.c_int64 * count)(*sizes)
     nbytes = lib.smq_smaq_multi_plan_bytes(arr, count)
-    nl = -(-(S + 1) // C)  # chunks of the last tensor
-    chunks = [1, 1, 2, 4, nl]
-    schunks = [1, 1, 1, 1, 2]
+    chunks = [-(-n // C) for n in sizes]
+    nl = chunks[4]
+    # partials G = ceil((n // 4) / 1024) (V = 1 below 2^20 groups); 16 partials per workgroup
+    parts = [1, 1, 1, 4, 16, 74]
+    wgs = [1, 1, 1, 1, 1, 5]
     dbytes = ((40 * count + 31) // 32) * 32
-    assert nbytes == 32 + dbytes + 64 * (sum(chunks) + sum(schunks))
+    assert nbytes == 32 + dbytes + 64 * (sum(chunks) + sum(wgs))
     descs = (N.SmqTensorDesc * count)()
     rel = 0
     for i, n in enumerate(sizes):
@@ -207,13 +213,13 @@ def test_multi_plan_layout():
     raw = np.frombuffer(bytes(host), dtype=np.uint8)
     assert list(raw[:8].view(np.int32)) == [count, sum(chunks)]
     assert int(raw[8:16].view(np.int64)[0]) == C
-    assert int(raw[16:20].view(np.int32)[0]) == sum(schunks)
+    assert list(raw[16:24].view(np.int32)) == [sum(wgs), sum(parts)]
     assert int(raw[24:32].view(np.int64)[0]) == S
     rec = raw[32 + dbytes:].reshape(-1, 64)
-    assert rec.shape[0] == sum(chunks) + sum(schunks)
+    assert rec.shape[0] == sum(chunks) + sum(wgs)
     q = rec[:, :48].copy().view(np.int64)  # x, y, n, begin, end, rng_offset
     i32 = rec[:, 48:].copy().view(np.int32)  # tensor, first_chunk, n_chunks, all_positive
-    a = slice(0, sum(chunks))
+    a = slice(0, 8 + nl)
     assert list(i32[a, 0]) == [0, 1, 2, 2, 3, 3, 3, 3] + [4] * nl
     assert list(i32[a, 1]) == [0, 1, 2, 2, 4, 4, 4, 4] + [8] * nl
     assert list(i32[a, 2]) == [1, 1, 2, 2, 4, 4, 4, 4] + [nl] * nl
@@ -221,12 +227,13 @@ def test_multi_plan_layout():
     assert list(q[a, 3])[:8] == [0, 0, 0, C, 0, C, 2 * C, 3 * C]
     assert list(q[a, 4])[:8] == [10, C, C, C + 1, C, 2 * C, 3 * C, 3 * C + 5]
     assert list(q[a, 5])[:5] == [0, 10, 10 + C, 10 + C, 10 + 2 * C + 1]
-    b = slice(sum(chunks), None)  # the statistics map
-    assert list(i32[b, 0]) == [0, 1, 2, 3, 4, 4]
-    assert list(i32[b, 1]) == [0, 1, 2, 3, 4, 4]
-    assert list(i32[b, 2]) == [1, 1, 1, 1, 2, 2]
-    assert list(q[b, 3]) == [0, 0, 0, 0, 0, S] and list(q[b, 4]) == [10, C, C + 1, 3 * C + 5, S, S + 1]
-    assert lib.smq_smaq_multi_workspace_bytes(arr, count) >= 64 * count + 32 * sum(schunks)
+    b = slice(sum(chunks), None)  # the statistics map: partial runs [begin, end)
+    assert list(i32[b, 0]) == [0, 1, 2, 3, 4] + [5] * 5
+    assert list(i32[b, 1]) == [0, 1, 2, 3, 7] + [23] * 5  # first partial of the tensor
+    assert list(i32[b, 2]) == [1, 1, 1, 1, 1] + [5] * 5
+    assert list(q[b, 3]) == [0, 0, 0, 0, 0, 0, 16, 32, 48, 64]
+    assert list(q[b, 4]) == [1, 1, 1, 4, 16, 16, 32, 48, 64, 74]
+    assert lib.smq_smaq_multi_workspace_bytes(arr, count) >= 64 * count + 32 * sum(parts)
     descs[1].n = 0
     assert lib.smq_smaq_multi_plan_build(descs, count, host, nbytes) == -1
 

@@ -85,13 +85,13 @@ def test_multi_c5_full_resnet34_set():
     gradients + the 38 non-BN weights (fc bias included) = 148 tensors, 42,547,220 elements, in one
     bound SmaqMulti call. Every tensor equals the oracle fed its device statistics and counter
     stream bit for bit, statistics within 1 ulp of fp64, and the fused call equals the per-tensor
-    SmartFP calls at the same stream offsets. (The multi statistics sum 64K-element chunks, the
-    single call 16K-element tiles: the fp64 totals differ in summation order only, ~2^-50
-    relative, so the fp32 statistics agree unless a total lies that close to an fp32 rounding
-    boundary — odds ~2^-27 per statistic; the per-tensor oracle checks hold regardless.)"""
+    SmartFP calls at the same stream offsets for EVERY tensor, bit for bit: the multi statistics
+    launch computes each tensor's partials in the single-tensor partition and reduces them in its
+    order (csrc/smaq_small.h, smaq_multi.hip)."""
     import bench
     from oracle import rng as orng
     from oracle import smaq as osmaq
+    from smart_compress_amd import _native as N
     from smart_compress_amd.compress.smart import SmartFP
     from smart_compress_amd.util.pytorch.multi import SmaqMulti
 
@@ -114,9 +114,11 @@ def test_multi_c5_full_resnet34_set():
         y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], osmaq.SmaqConfig(),
                               orng.uniforms(21, m.offset_of(t), xn.size))
         assert same_f32(y.cpu().numpy().ravel(), y_or), t
-        if t % 7 == 0:  # the per-tensor path at the same offset
-            single.rng.offset = m.offset_of(t)
-            assert torch.equal(single(x).view(torch.int32), y.view(torch.int32)), t
+        # the per-tensor path at the same offset
+        single.rng.offset = m.offset_of(t)
+        assert torch.equal(single(x).view(torch.int32), y.view(torch.int32)), t
+        sst = SmartFP.read_stats(next(v for k, v in N._ws.items() if k[0] == "smaq"))
+        assert (sst["mean"], sst["raw_std"]) == (st["mean"], st["raw_std"]), t
 
 
 MODES = [dict(use_sample_stats=True), dict(use_sample_stats=True, num_samples=300),
@@ -154,6 +156,45 @@ def test_multi_modes_equal_single_calls(mode, dt):
         assert torch.equal(ref.view(torch.int32), y.view(torch.int32)), t
         assert stats[m.index_of(t)]["mean"] == st["mean"], t
         assert stats[m.index_of(t)]["raw_std"] == st["raw_std"], t
+
+
+@pytest.mark.parametrize("mode", [dict(), dict(use_range_std_dev=True),
+                                  dict(stochastic_rounding=False)],
+                         ids=["full", "range", "trunc"])
+@pytest.mark.parametrize("dt", ["f32", "f16", "bf16"])
+def test_multi_full_stats_equal_single_calls(mode, dt):
+    """Full statistics (the default): every size class — the small partition with one partial,
+    several partials in one workgroup, several workgroups per tensor (300,000 and 3M elements),
+    V = 8 (8,388,611) and tensors above it (9M: the deferred grid; 13M: 512 workgroups), whose
+    statistics are the single-tensor launch itself — equal the per-tensor SmartFP calls at the
+    same stream offsets, outputs and statistics bit for bit."""
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.smart import SmartFP
+    from smart_compress_amd.util.pytorch.multi import SmaqMulti
+
+    tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[dt]
+    hp = smaq_hparams(precision=16 if dt == "f16" else 32, **mode)
+    gen = torch.Generator(device="cuda").manual_seed(31)
+    sizes = [5, 4099, 65537, 300000, 3 * (1 << 20) + 5, 8388611, 9 << 20, 13 << 20]
+    xs = [(torch.randn(n, generator=gen, device="cuda") * (0.5 + i)).to(tdt)
+          for i, n in enumerate(sizes)]
+    m = SmaqMulti(hp, seed=12)
+    ys = m(xs)
+    torch.cuda.synchronize()
+    stats = m.read_stats()
+    single = SmartFP(hp)
+    single.rng.seed = 12
+    for t, (x, y) in enumerate(zip(xs, ys)):
+        if x.numel() < hp.min_size:
+            assert y is x
+            continue
+        single.rng.offset = m.offset_of(t)
+        ref = single(x)
+        torch.cuda.synchronize()
+        st = SmartFP.read_stats(N.workspace("smaq", x.device, 0))
+        assert torch.equal(ref.view(torch.int32), y.view(torch.int32)), t
+        for k in ("mean", "raw_std", "std_clamped"):
+            assert stats[m.index_of(t)][k] == st[k], (t, k)
 
 
 def test_multi_mixed_dtypes_one_call_per_group():

@@ -72,12 +72,11 @@ def test_fused_equals_per_tensor(opt_name, sr):
         if opt_name == "adam":
             for st in base.state.values():
                 assert (st["exp_avg_sq"] >= 0).all()
-    same = total = 0
+    # the fused multi-tensor call computes each tensor's statistics in the single-tensor
+    # partition and reduction order (csrc/smaq_multi.hip), at the same stream offsets: every
+    # parameter after training is bit-identical
     for a, b in zip(*results):
-        same += int((a == b).sum())
-        total += a.size
-        assert np.allclose(a, b, atol=0.05, rtol=0.05)
-    assert same / total > 0.97, same / total  # identical RNG streams and arithmetic per tensor
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
 def test_bn_weights_untouched_and_logging():

@@ -1,8 +1,9 @@
-"""Per-call time of smq_smaq_roundtrip (stats + apply) against tensor size, back to back on one
-stream over 8 rotating input buffers (activation-like: written just before, MALL-warm).
+"""Per-call time of smq_smaq_roundtrip against tensor size, back to back on one stream over 8
+rotating input buffers (activation-like: written just before, MALL-warm).
 
-python tools/defer_sweep.py  ->  one line per size: n, us per call.  A/B of the deferred
-statistics: run it under SMQ_DEFER_MAX_N=0 (off) and unset (default), tools/defer_exp.sh.
+python tools/defer_sweep.py  ->  one line per size: n, us per call. DS_FLAGS: smq_smaq_roundtrip_ex
+flags (0: the product's choice — the single launch up to 8,388,611 elements; 1: SMQ_SMAQ_SPLIT, the
+deferred two-launch path; 2: SMQ_SMAQ_NO_DEFER). tools/fused_exp.sh interleaves them.
 """
 
 import os
@@ -21,6 +22,7 @@ SIZES = [int(s) for s in os.environ.get(
     "DS_SIZES", "65536,262144,1048576,2097152,4194304,8388608,16777216,33554432").split(",")]
 CALLS = int(os.environ.get("DS_CALLS", "200"))
 GRAPH = os.environ.get("DS_GRAPH") == "1"
+FLAGS = int(os.environ.get("DS_FLAGS", "0"))
 
 
 def main():
@@ -37,9 +39,9 @@ def main():
 
         def call(i):
             st = torch.cuda.current_stream().cuda_stream
-            N.check(lib.smq_smaq_roundtrip(xs[i % 8].data_ptr(), N.SMQ_DTYPE_F32,
-                                           ys[i % 8].data_ptr(), n, p, None, ws.data_ptr(),
-                                           ws.numel(), st), "roundtrip")
+            N.check(lib.smq_smaq_roundtrip_ex(xs[i % 8].data_ptr(), N.SMQ_DTYPE_F32,
+                                              ys[i % 8].data_ptr(), n, p, None, ws.data_ptr(),
+                                              ws.numel(), FLAGS, st), "roundtrip")
 
         for i in range(20):
             call(i)
@@ -63,7 +65,7 @@ def main():
             b.record()
             b.synchronize()
             best.append(a.elapsed_time(b) * 1e3 / CALLS)
-        print(f"n={n} us_per_call={min(best):.2f} runs={' '.join(f'{t:.2f}' for t in best)}",
+        print(f"flags={FLAGS} n={n} us_per_call={min(best):.2f} runs={' '.join(f'{t:.2f}' for t in best)}",
               flush=True)
 
 
