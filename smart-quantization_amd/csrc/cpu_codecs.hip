@@ -608,12 +608,15 @@ static inline float s2_elem32(float xv, uint32_t r, const SmqS2fp8Stats& s, int 
 template <int TIN>
 static inline float s2_elem16(float xv, uint32_t r, const SmqS2fp8Stats& s, int check_inf,
                               float max_value) {
-  float Y = powf(fabsf(xv), s.alpha);
+  // powers rounded to a half type: the correctly rounded float power (double pow, then float),
+  // which the reference's torch half pow reproduces (tests/golden f64_s2fp8_p16_powcase); fp32 data
+  // keeps powf (its Y is not rounded further)
+  float Y = TIN == kF32 ? powf(fabsf(xv), s.alpha) : (float)pow((double)fabsf(xv), (double)s.alpha);
   Y = rin<TIN>(rin<TIN>(Y) * s.beta_pow2);
   float T = qtorch_quant(Y, r, 5, 2, true);
   if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
   const float t1 = rin<kF16>(T * s.inv_beta_pow2);
-  const float t2 = rin<kF16>(powf(t1, rin<kF16>(s.inv_alpha)));
+  const float t2 = rin<kF16>((float)pow((double)t1, (double)rin<kF16>(s.inv_alpha)));
   if (xv > 0.0f) return t2;
   if (xv < 0.0f) return u2f(f2u(t2) ^ 0x80000000u);
   return t2 * 0.0f;

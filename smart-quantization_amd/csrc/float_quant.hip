@@ -566,13 +566,18 @@ __device__ __forceinline__ float s2fp8_elem16(float xv, uint32_t r, float alpha,
     const float lg = log2f(a);
     Y = exp2f(alpha * lg) * bp2;
     if (__builtin_expect(s2_fast_uncertain_y(Y, r, alpha, lg), 0)) Y = powf(a, alpha) * bp2;
-  } else {
-    Y = s2_round<TIN>(s2_round<TIN>(powf(a, alpha)) * bp2);
+  } else if (TIN == kF32) {
+    Y = powf(a, alpha) * bp2;
+  } else {  // a power rounded to a half type: the correctly rounded float power (double pow)
+    Y = s2_round<TIN>(s2_round<TIN>((float)pow((double)a, (double)alpha)) * bp2);
   }
   float T = qtorch_quant(Y, r, 5, 2, true);
   if (check_inf && fabsf(T - max_value) <= FLT_EPSILON) T = INFINITY;
   const float t1 = s2_round<kF16>(T * ibp2);
-  const float t2 = s2_round<kF16>(powf(t1, ialpha_h));
+  // `** alpha.reciprocal_()` on half values: torch's result equals the correctly rounded float
+  // power rounded to half; a float powf that is not correctly rounded moves whole E5M2 codes by a
+  // half ulp on some draws (tests/golden f64_s2fp8_p16_powcase: 19 of 4096 elements)
+  const float t2 = s2_round<kF16>((float)pow((double)t1, (double)ialpha_h));
   // `* signs` (fp16 output for fp16 inputs, fp32 otherwise). t2 is >= +0 or NaN, so the product is
   // a sign flip — written as one: `fptrunc(t2 * sgn)` is otherwise emitted as v_fma_mixlo_f16 with
   // a +0 addend, which turns -1 * +0 = -0 into +0 (measured on gfx950).

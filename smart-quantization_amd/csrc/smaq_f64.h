@@ -161,7 +161,10 @@ __host__ __device__ __forceinline__ double s2_elem_f64(double xv, uint32_t r,
   const float T16 = rn16_f32(T);
   const float t1 = rn16_f32(T16 * (float)s.inv_beta_pow2);
   const float e16 = rn16_f32((float)s.inv_alpha);
-  const float t2 = rn16_f32(powf(t1, e16));
+  // the correctly rounded float power, rounded to half: torch's half pow (powf that is not
+  // correctly rounded moves whole E5M2 codes by a half ulp on some draws,
+  // tests/golden/f64_s2fp8_p16_powcase)
+  const float t2 = rn16_f32((float)pow((double)t1, (double)e16));
   return (double)t2 * sgn;
 }
 

@@ -404,8 +404,18 @@ def gen_f64(out_dir, record):
         "wide": torch.randn(4096, generator=g, dtype=torch.float64)
         * torch.exp(torch.randn(4096, generator=g, dtype=torch.float64) * 3),
     }
+    # S2FP8 at precision 16 computes `t1 ** (1 / alpha)` on half values (s2fp8.py:48); on this draw
+    # (found by a 400-draw search against the reference) a float pow that is not correctly
+    # rounded (a libm powf) moves 23 elements by one half ulp, while double pow rounded to float
+    # then half reproduces every element: it decides which pow the oracle and the device follow
+    g2 = torch.Generator().manual_seed(1015)
+    pow_case = torch.randn(4096, generator=g2, dtype=torch.float64) * 3.0
     for cname, cls in (("fp8", FP8), ("s2fp8", S2FP8)):
         for precision in (32, 16):
+            if cname == "s2fp8" and precision == 16:
+                inputs["powcase"] = pow_case
+            else:
+                inputs.pop("powcase", None)
             hp = cls.add_argparse_args(ArgumentParser()).parse_args([])
             hp.precision = precision
             codec = cls(hp)

@@ -102,7 +102,13 @@ def test_oracle_float_f64_matches_reference(name):
         assert same_f64(want, r["y"])
         assert meta["y_dtype"] == ("torch.float64" if meta["precision"] == 32 else "torch.float16")
         return
-    y, st, Y, T = os2.roundtrip_f64(x, r["q_rand"], True, meta["precision"])
+    # the oracle's statistics: the mean within an ulp of torch's (its summation order is not
+    # restated), the max exact; the rest of the chain on the reference's own (mu, m) must then
+    # reproduce alpha, beta, 2^beta, the quantiser inputs and the outputs bit for bit
+    st0 = os2.stats_f64(x)
+    assert abs(st0["mu"] - r["mu"]) <= 2.0 ** -52 * abs(r["mu"]) and st0["m"] == r["m"]
+    st_ref = os2.derive_f64(r["mu"], r["m"])
+    y, st, Y, T = os2.roundtrip_f64(x, r["q_rand"], True, meta["precision"], st=st_ref)
     for k in ("mu", "m", "alpha", "beta", "beta_pow2"):
         assert st[k] == r[k], k
     assert np.array_equal(Y.astype(np.float32), r["q_in"])
@@ -384,21 +390,35 @@ def test_gpu_float_codecs_f64(precision):
     yo, st, Y, T = os2.roundtrip_f64(xn, words, True, precision, st=st)
     yd = ys.cpu().numpy()
     if precision == 16:
-        # y = t2 * sign with t2 an fp16 value (s2_elem_f64<true>: powf in float, as torch's half pow
-        # computes; the oracle takes libm's double pow). t1 = RN16(T * 2^-beta) has at most ~131
-        # distinct values per call, so one of them whose power lies at a half rounding boundary
-        # moves every element of that E5M2 code by one half ulp (measured: 1.9 % of the elements on
-        # one draw, none on others): compare in fp16 ulps, the target format (north_star: 1 ulp).
-        fin = np.isfinite(yd)
-        assert np.array_equal(fin, np.isfinite(yo))
-        assert np.array_equal(np.signbit(yd[fin]), np.signbit(yo[fin]))
-        hd = np.abs(yd[fin]).astype(np.float16).view(np.int16).astype(np.int32)
-        ho = np.abs(yo[fin]).astype(np.float16).view(np.int16).astype(np.int32)
-        dh = np.abs(hd - ho)
-        assert np.mean(dh == 0) > 0.5 and dh.max() <= 1, np.bincount(np.minimum(dh, 9))
+        # y = t2 * sign, t2 = RN16(correctly rounded float power of an fp16 value): the device's
+        # double pow rounded to float, the oracle's libm pow — pinned against the reference's torch
+        # half pow by tests/golden/f64_s2fp8_p16_powcase (a float powf moves 19 of its elements)
+        assert np.array_equal(yd.view(np.int64), yo.view(np.int64))
         return
+    # precision 32: the device's fp64 pow against libm's differs by an ulp, and where that moved Y
+    # across a stochastic-rounding boundary the element's E5M2 code is the adjacent one; every
+    # element is bounded: within 2 ulp of the oracle, or (adjacent code) within 2 ulp of the
+    # oracle's inverse of the device's own code
     d = np.abs(yd.view(np.int64) - yo.view(np.int64))
-    frac_same = np.mean(d == 0)
     hist = np.bincount(np.minimum(d, 9).astype(np.int64), minlength=10).tolist()
-    assert frac_same > 0.5, hist
-    assert np.mean(d <= 4) > 0.9999, hist
+    assert np.mean(d == 0) > 0.5, hist
+    far = np.nonzero(d > 2)[0]
+    if far.size:
+        tdev = torch.empty(n, dtype=torch.float64, device="cuda")
+        N.check(lib.smq_s2fp8_roundtrip_f64(x.data_ptr(), tdev.data_ptr(), n, precision, 1, None,
+                                            12, 900, None, None, ws.data_ptr(), ws.numel(),
+                                            N.SMQ_S2FP8_OUT_T, N.stream_ptr(x.device)), "s2 T")
+        td = tdev.cpu().numpy()[far].astype(np.float32)
+        to = np.asarray(T, dtype=np.float32)[far]
+        # one E5M2 code apart: positions in the ordered list of E5M2 magnitudes (T >= +0 here)
+        grid = np.array([m * 2.0 ** -16 for m in range(4)] +
+                        [(1 + m / 4) * 2.0 ** (e - 15) for e in range(1, 31) for m in range(4)]
+                        + [np.inf])
+        step = np.abs(np.searchsorted(grid, td.astype(np.float64))
+                      - np.searchsorted(grid, to.astype(np.float64)))
+        assert np.all(step == 1), (td, to)
+        sgn = np.sign(xn[far])
+        inv = np.array([os2._libm_pow(float(t) * float(st["inv_beta_pow2"]), float(st["inv_alpha"]))
+                        for t in td]) * sgn
+        dd = np.abs(yd[far].view(np.int64) - inv.view(np.int64))
+        assert dd.max() <= 2, dd
