@@ -18,8 +18,8 @@ smaq_cpu) are measurement
 aids (BASELINE configs 1 and 3-5), not the line the driver records; each carries its own
 `roofline` and, at N=1, a `cpu_baseline`.
 
-roofline: the dominant kernel is smaq_apply_kernel (8 B/elem algorithmic); its average duration is
-measured with events on the codec's stream around each launch (over K steps after the timed ones).
+roofline: the call's launches (at 256M the statistics + apply kernels, 12 B/elem algorithmic) timed
+with an event pair on the codec's stream around each call (over K steps after the timed ones).
 cpu_baseline: the CPU restatement in oracle/ (kind "port"): smart.py's own torch-CPU op sequence
 (oracle/smaq_torch.py, 16 intra-op threads) for SmaQ, the numpy qtorch / s2fp8 restatements (one
 thread) for FP8 / S2FP8, on a bounded sample.
@@ -493,10 +493,10 @@ def run_smaq(args, world, rank, device):
     prewarm(step, device)
     for _ in range(args.warmup):
         step()
-    # the K timed steps carry no per-launch event markers (an event pair between two launches
-    # costs a few us per step); the apply launch duration for `roofline` is then measured with an
-    # event pair around each apply launch over K more steps of the same workload, on the codec's
-    # stream (SMQ_BENCH_EVENTS_IN_TIMED=1: events inside the timed steps instead)
+    # the K timed steps carry no event markers; the call's device time for `roofline` is then
+    # measured with an event pair around each call (the product entry point smq_smaq_roundtrip: its
+    # statistics and apply launches) over K more steps of the same workload, on the codec's stream
+    # (SMQ_BENCH_EVENTS_IN_TIMED=1: events inside the timed steps instead)
     in_timed = os.environ.get("SMQ_BENCH_EVENTS_IN_TIMED") == "1"
     trace.enabled = in_timed
     elapsed = time_steps(step, args.steps, 0, world, device)
@@ -509,8 +509,16 @@ def run_smaq(args, world, rank, device):
     alg_per_elem = (in_bytes + 4) if sampled else (2 * in_bytes + 4)
     total_bytes = sum_over_ranks(alg_per_elem * n * args.steps, world, device)
     value = total_bytes / elapsed / 1e9
-    apply_ms = trace.mean_ms("apply")
-    apply_gbps = (in_bytes + 4.0) * n / (apply_ms * 1e-3) / 1e9
+    call_ms = trace.mean_ms("call")
+    call_gbps = alg_per_elem * n / (call_ms * 1e-3) / 1e9
+    # the launches of one call: one register-resident launch up to 8,388,611 elements (full
+    # statistics), else the statistics launch + the apply launch (include/smq.h)
+    if sampled:
+        kernels = "smaq_draw_stats_kernel+smaq_apply_kernel"
+    elif n <= 8388611:
+        kernels = "smaq_fused_kernel"
+    else:
+        kernels = "smaq_stats_kernel+smaq_apply_kernel"
     res = {
         "metric": METRIC.format(size=size_label(n)), "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -529,17 +537,18 @@ def run_smaq(args, world, rank, device):
         # GB/s (statistics read + apply read: the north star's "HBM-read roofline" reading)
         "tensor_gbps": round(value * in_bytes / alg_per_elem, 2),
         "read_gbps": round(value * (alg_per_elem - 4) / alg_per_elem, 2),
-        "roofline": {"bound": "hbm", "kernel": "smaq_apply_kernel",
-                     "achieved": round(apply_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(apply_gbps / HBM_PEAK_GBPS, 4),
-                     "alg_bytes_per_launch": int((in_bytes + 4) * n),
-                     "avg_launch_ms": round(apply_ms, 5),
+        # the whole call (all of its launches) over its algorithmic bytes; traffic = the sum of
+        # the call's kernels' PMC bytes (profiles/traffic_<config>.json)
+        "roofline": {"bound": "hbm", "kernel": kernels,
+                     "achieved": round(call_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(call_gbps / HBM_PEAK_GBPS, 4),
+                     "alg_bytes_per_launch": int(alg_per_elem * n),
+                     "avg_launch_ms": round(call_ms, 5),
                      "traffic": traffic_from_profile(
                          args.config, n, "f32" if in_dt is None else os.environ["SMQ_BENCH_DTYPE"],
+                         whole_call=True,
                          profile=args.config if in_dt is None
                          else f"{args.config}_{os.environ['SMQ_BENCH_DTYPE']}")},
-        # the statistics launch is not bracketed by events (an event between the two launches
-        # costs ~1 %); its duration is in the committed rocprofv3 summary (profiles/)
         "host_enqueue_ms_per_step": round(HOST.get("enqueue_ms_per_step", 0.0), 4),
         "input_buffers": 2,
     }

@@ -1349,7 +1349,7 @@ int smq_smaq_roundtrip_ex(const void* x, int dtype, float* y, int64_t n, const S
       ws && fused_eligible(x, dtype, y, n, p, uniforms, ws_bytes)) {
     const RangeRecips R = range_recips(p->range_main, p->range_outlier);
     FusedCall c{x, dtype, y, n, p, range_coef_for(p, n), R.inv_main, R.inv_out, ws,
-                (flags & SMQ_SMAQ_TEST_LATE) ? 1 : 0};
+                (flags & SMQ_SMAQ_TEST_LATE) ? 1 : 0, ws_bytes};
     return launch_fused(c, (hipStream_t)stream);
   }
   int def_g = 0;

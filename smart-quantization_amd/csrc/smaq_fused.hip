@@ -139,7 +139,24 @@ struct FusedArgs {
   float thr, r_main, r_out, clamp_lo, clamp_hi, range_coef;
   double inv_r_main, inv_r_out;
   int all_pos, count, range, test_late;
+  uint64_t* trace;  // experiment builds (-DSMQ_FUSED_TRACE=1): 8 timestamps per workgroup
 };
+
+// s_memrealtime stamps (100 MHz) of workgroup milestones, experiment builds only
+#ifndef SMQ_FUSED_TRACE
+#define SMQ_FUSED_TRACE 0
+#endif
+#if SMQ_FUSED_TRACE
+#define FSTAMP(i)                                                                   \
+  do {                                                                              \
+    if (A.trace && threadIdx.x == 0)                                                \
+      A.trace[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define FSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
 
 // The partial of chunk k by the whole workgroup from the lanes' groups g; every thread gets it.
 template <int TIN, int V>
@@ -273,6 +290,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int64_t base = (int64_t)b * V * kSmallT + threadIdx.x;
   const uint64_t steal_ticks = A.test_late ? 2000 : kFusedStealTicks;
+  FSTAMP(0);
   if (A.test_late && 2 * b >= G && G > 1) {  // test aid: half of the grid starts ~500 us late
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < 50000) __builtin_amdgcn_s_sleep(127);
@@ -300,6 +318,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   const uint64_t off = A.offset + off0;
 
   const StatAcc part = fused_partial<TIN, V>(A, b, v, shift, W);
+  FSTAMP(1);
 #pragma unroll
   for (int u = VR; u < V; ++u) park[(u - VR) * kSmallT + threadIdx.x] = v[u];
   if (G > 1 && wave == 0) fused_publish(part, A, b, epoch);
@@ -383,6 +402,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       const StatAcc pk_acc = fused_steal<TIN>(A.x, A.n, V, G, k, shift, &W);
       if (wave == 0) fused_publish(pk_acc, A, k, epoch);
     }
+    FSTAMP(2);
     // count this workgroup past the wait now; the returned word is looked at only at the end
     if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.left);
     if (wave == 0) {
@@ -446,6 +466,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
     if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
     st_sc1_u64(A.left, (unsigned long long)(gen + 1u) << 32);
   }
+  FSTAMP(3);
   ElemConsts c;
   const float cthr = TIN == kF32 ? A.thr : round_in<TIN>(A.thr);
   init_consts(c, &sst, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
@@ -469,6 +490,16 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       if (tail) n_out += fused_tail<RM, TIN, false, false>(A, c, off);
     }
   }
+  FSTAMP(4);
+#if SMQ_FUSED_TRACE
+  if (A.trace && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    A.trace[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    A.trace[(size_t)blockIdx.x * 8 + 6] = xcc;
+  }
+#endif
   if (A.count) {  // outlier count for log_size (smart.py:184-188), spread over the slots
     const uint32_t t = wave_sum_u32(n_out);
     if (lane == 0) sh_cnt[wave] = t;
@@ -578,6 +609,11 @@ int launch_fused(const FusedCall& c, hipStream_t st) {
   F.count = p->count_outliers;
   F.range = p->use_range_std_dev;
   F.test_late = c.test_late;
+  F.trace = nullptr;
+#if SMQ_FUSED_TRACE
+  if (c.ws_bytes >= SmaqWsLayout::kTotal + 8 * 8 * (size_t)kSmallMaxG)
+    F.trace = (uint64_t*)(base + SmaqWsLayout::kTotal);
+#endif
   if (p->count_outliers &&
       hipMemsetAsync(F.out_slots, 0, 8 * SMQ_WS_OUTLIER_SLOTS, st) != hipSuccess) {
     set_error("hipMemsetAsync of the outlier slots failed");

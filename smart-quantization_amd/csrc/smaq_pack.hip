@@ -1142,6 +1142,10 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   const uint32_t g = A.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
   const uint32_t b0 = FULL ? g * (uint32_t)kUnpackPer : A.nb - 1;
   const int nblk = FULL ? (int)min((uint32_t)kUnpackPer, A.n_full - b0) : 1;
+  // the stream is this call's (magic, n) before any directory entry is read: a caller's n beyond
+  // the stream's would index past its directory (one scalar load; the rest of the header is
+  // checked in unpack_run)
+  if (A.hdr->magic != SMQ_PACK_MAGIC || A.hdr->n != A.n) return;
   uint64_t dent[kUnpackPer];
 #pragma unroll
   for (int i = 0; i < kUnpackPer; ++i) dent[i] = i < nblk ? A.dir[b0 + i] : 0ull;
@@ -1158,6 +1162,7 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_big_kernel(UnpackArgs A) {
   int wm, wo;
   UnpackArgs W = A;
   if (!unpack_widths(W, wm, wo)) return;
+  if (A.hdr->magic != SMQ_PACK_MAGIC || A.hdr->n != A.n) return;  // before the directory reads
   const int we = wo > wm ? wo - wm : 0;
   if (threadIdx.x == 0) n_list = 0u;
   __syncthreads();

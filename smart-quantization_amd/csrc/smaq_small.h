@@ -252,6 +252,7 @@ struct FusedCall {
   double inv_r_main, inv_r_out;
   void* ws;
   int test_late;
+  size_t ws_bytes;
 };
 int launch_fused(const FusedCall& c, hipStream_t st);
 

@@ -18,8 +18,13 @@ the container of include/smq.h ("Packed SmaQ container"):
 Same flags as ``SmartFP`` (it is a subclass), incl. the BatchNorm variant (smart.py:136-149,
 174-179: the stream carries the compress-time gamma / beta, so ``decompress`` needs no arguments)
 and any threshold (``main_std_dev_threshold < 0``: an element above -T and below T at once is the
-third state smart.py:157-161 gives it). ``compress`` reads the stream size back from the device
-(one host synchronisation) to return a right-sized buffer.
+third state smart.py:157-161 gives it).
+
+No call synchronises the host: ``compress`` writes into a buffer of the worst-case size
+(``smq_smaq_pack_bound``) whose real stream size stays on the device (header ``total_bytes``);
+``SmaqPacked.nbytes`` reads it when asked (one synchronisation, cached), and ``compact()`` returns a
+right-sized copy for a caller that keeps the stream (the memory saving). ``__call__`` and a
+``compress`` + ``decompress`` pair therefore run inside a captured hipGraph.
 """
 
 import ctypes
@@ -39,20 +44,35 @@ _TOTAL_OFF = N.SmqPackedHeader.total_bytes.offset
 
 
 class SmaqPacked:
-    """A packed SmaQ tensor: ``data`` (uint8, on the device) plus the original shape.
-    ``raw``: a tensor below ``min_size``, kept as its original fp32 bytes (smart.py:123-128)."""
+    """A packed SmaQ tensor: ``data`` (uint8, on the device; the stream, possibly followed by unused
+    capacity) plus the original shape. ``raw``: a tensor below ``min_size``, kept as its original
+    fp32 bytes (smart.py:123-128)."""
 
     def __init__(self, data: torch.Tensor, shape: torch.Size, n: int, raw: bool = False,
-                 widths=None):
+                 widths=None, total: Optional[int] = None):
         self.data = data
         self.shape = torch.Size(shape)
         self.n = int(n)
         self.raw = raw
         self.widths = widths  # (num_bits_main, num_bits_outlier) the stream was written with
+        # the stream size when known on the host (raw data: all of it)
+        self._total = int(data.numel()) if raw else total
 
     @property
     def nbytes(self) -> int:
-        return int(self.data.numel())
+        """The stream size in bytes (header ``total_bytes``: one host synchronisation the first
+        time it is asked for)."""
+        if self._total is None:
+            self._total = int(self.data[_TOTAL_OFF:_TOTAL_OFF + 8].cpu().numpy().view(np.uint64)[0])
+        return self._total
+
+    def compact(self) -> "SmaqPacked":
+        """A right-sized copy of the stream (the memory a kept stream should take)."""
+        total = self.nbytes
+        if total == self.data.numel():
+            return self
+        return SmaqPacked(self.data[:total].clone(), self.shape, self.n, widths=self.widths,
+                          total=total)
 
     @property
     def bits_per_element(self) -> float:
@@ -98,28 +118,30 @@ class SmartFPPacked(SmartFP):
             keep = self._bind_batch_norm(p, x, batch_norm_stats)
         bound = lib.smq_smaq_pack_bound_bn(numel, hp.num_bits_main, hp.num_bits_outlier,
                                            p.bn_channels if keep is not None else 0)
-        scratch = N.workspace("smaq_pack_out", x.device, bound)
+        out = torch.empty(bound, dtype=torch.uint8, device=x.device)
         ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(numel))
-        N.check(lib.smq_smaq_compress(x.data_ptr(), code, numel, p, scratch.data_ptr(),
-                                      scratch.numel(), ws.data_ptr(), ws.numel(),
-                                      N.stream_ptr(x.device)), "smq_smaq_compress")
+        N.check(lib.smq_smaq_compress(x.data_ptr(), code, numel, p, out.data_ptr(), out.numel(),
+                                      ws.data_ptr(), ws.numel(), N.stream_ptr(x.device)),
+                "smq_smaq_compress")
         del keep
-        # host sync: the stream size, for a right-sized buffer
-        total = int(scratch[_TOTAL_OFF:_TOTAL_OFF + 8].cpu().numpy().view(np.uint64)[0])
-        return SmaqPacked(scratch[:total].clone(), data.shape, numel,
-                          widths=(hp.num_bits_main, hp.num_bits_outlier))
+        # the stream size stays on the device (SmaqPacked.nbytes / compact read it when asked)
+        return SmaqPacked(out, data.shape, numel, widths=(hp.num_bits_main, hp.num_bits_outlier))
 
     def decompress(self, packed: SmaqPacked) -> torch.Tensor:
         if packed.raw:
             return packed.data.view(torch.float32).reshape(packed.shape).clone()
         N.require_device(packed.data, "SmartFPPacked.decompress")
         y = torch.empty(packed.shape, dtype=torch.float32, device=packed.data.device)
-        # the widths this codec wrote the stream with (read from its header when the stream came
-        # from elsewhere: the ex entry point then rejects a mismatch by leaving y alone)
-        bm, bo = packed.widths or (self.hparams.num_bits_main, self.hparams.num_bits_outlier)
-        N.check(N.lib().smq_smaq_decompress_ex(packed.data.data_ptr(), y.data_ptr(), packed.n,
-                                               bm, bo, N.stream_ptr(y.device)),
-                "smq_smaq_decompress_ex")
+        lib, st = N.lib(), N.stream_ptr(y.device)
+        if packed.widths is not None:
+            # the widths the stream was written with: the decoder locates its sections without
+            # waiting for the header
+            bm, bo = packed.widths
+            N.check(lib.smq_smaq_decompress_ex(packed.data.data_ptr(), y.data_ptr(), packed.n, bm,
+                                               bo, st), "smq_smaq_decompress_ex")
+        else:  # a stream from elsewhere: the widths its header records
+            N.check(lib.smq_smaq_decompress(packed.data.data_ptr(), y.data_ptr(), packed.n, st),
+                    "smq_smaq_decompress")
         return y
 
     def __call__(self, data: torch.Tensor, tag: str = None, all_positive=False,
@@ -131,5 +153,6 @@ class SmartFPPacked(SmartFP):
                 return data
             packed = self.compress(data, all_positive, batch_norm_stats)
             y = self.decompress(packed)
-            self.log_size(tag, numel * 32, packed.nbytes * 8)
+            # the real stream size, read (one synchronisation) only if the ratio is measured
+            self.log_size(tag, numel * 32, lambda: packed.nbytes * 8)
             return y

@@ -8,7 +8,8 @@ smart.py:123-128) and ``log_size`` metrics (smart.py:184-188).
 Below the boundary, the reference's ~24 ATen launches + one host sync (smart.py:151) become one or
 two launches of libsmq (include/smq.h):
 
-* full statistics (default): ``smq_smaq_stats_f32`` + ``smq_smaq_apply_f32`` (12 B/elem);
+* full statistics (default): ``smq_smaq_roundtrip`` — up to 8,388,611 elements ONE launch that
+  holds the tensor in registers (8 B/elem of traffic), above it statistics + apply (12 B/elem);
 * ``--use_sample_stats``: ``smq_smaq_apply`` with ``SMQ_STATS_SAMPLED_DEVICE``: a one-workgroup
   launch draws k distinct indices (Floyd, on the device, from the call's stream position),
   gathers them and writes mean / biased std, then the apply launch (8 B/elem).
@@ -319,7 +320,8 @@ class SmartFP(CompressionAlgorithmBase):
         self.log_size(tag, numel * 32, new_size if hp.measure_compression_ratio else None)
         return y
 
-    # bench.py sets an event recorder here to time the apply launch on the codec's stream
+    # bench.py sets an event recorder here: an event pair on the codec's stream around the call's
+    # launches (the product entry point either way)
     _trace = None
 
     def _launch(self, x: torch.Tensor, y: torch.Tensor, numel: int, p, ws: torch.Tensor,
@@ -327,21 +329,18 @@ class SmartFP(CompressionAlgorithmBase):
         lib = N.lib()
         st = N.stream_ptr(x.device) if st is None else st
         tr = self._trace
-        if tr is None and p.stats_source == N.SMQ_STATS_WORKSPACE:
-            # one entry point for both launches: it may defer the statistics' final reduction
-            # into the apply launch (smaq.hip defer_consts)
+        if tr is not None:
+            tr.begin("call")
+        if p.stats_source == N.SMQ_STATS_WORKSPACE:
+            # one entry point: the single launch (tensors up to 8,388,611 elements), the deferred
+            # two-launch path, or statistics + apply (smq.h smq_smaq_roundtrip)
             N.check(lib.smq_smaq_roundtrip(x.data_ptr(), code, y.data_ptr(), numel, p, None,
                                            ws.data_ptr(), ws.numel(), st), "smq_smaq_roundtrip")
-            return
-        if p.stats_source == N.SMQ_STATS_WORKSPACE:
-            N.check(lib.smq_smaq_stats(x.data_ptr(), code, numel, p, ws.data_ptr(), ws.numel(), st),
-                    "smq_smaq_stats")
+        else:
+            N.check(lib.smq_smaq_apply(x.data_ptr(), code, y.data_ptr(), numel, p, None, None,
+                                       ws.data_ptr(), ws.numel(), st), "smq_smaq_apply")
         if tr is not None:
-            tr.begin("apply")
-        N.check(lib.smq_smaq_apply(x.data_ptr(), code, y.data_ptr(), numel, p, None, None,
-                                   ws.data_ptr(), ws.numel(), st), "smq_smaq_apply")
-        if tr is not None:
-            tr.end("apply")
+            tr.end("call")
 
     def workspace_bytes(self, numel: int) -> int:
         """Workspace of one call: above SMQ_MAX_DEVICE_SAMPLES device-drawn samples the

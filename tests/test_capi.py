@@ -255,3 +255,20 @@ def test_integration_doc_binding_matches_the_library_struct():
     lib_fields = [(f[0], getattr(N.SmqSmaqParams, f[0]).offset) for f in N.SmqSmaqParams._fields_]
     doc_fields = [(f[0], getattr(mirror, f[0]).offset) for f in mirror._fields_]
     assert doc_fields == lib_fields
+
+
+def test_shipped_library_reads_no_environment():
+    """The measurement knobs (SMQ_STATS_GRID, SMQ_DEFER_MAX_N, SMQ_MULTI_STATS_CHUNK, ...) change
+    launch shapes and reduction orders; the shipped library is built without them (smq_common.h
+    knob_env): it imports no getenv and holds none of their names."""
+    import subprocess
+
+    from smart_compress_amd import _native as N
+
+    syms = subprocess.run(["nm", "-D", "--undefined-only", N.LIB_PATH], capture_output=True,
+                          text=True, check=True).stdout
+    assert "getenv" not in syms
+    blob = open(N.LIB_PATH, "rb").read()
+    for knob in (b"SMQ_STATS_GRID", b"SMQ_STATS_PER_WG", b"SMQ_DEFER_MAX_N",
+                 b"SMQ_MULTI_STATS_CHUNK", b"SMQ_MULTI_CHUNK", b"SMQ_FUSED", b"SMQ_CPU_THREADS"):
+        assert knob not in blob, knob

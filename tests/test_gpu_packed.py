@@ -70,7 +70,7 @@ def test_stream_bytes_and_roundtrip(n, sr):
     torch.cuda.synchronize()
     assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
     stream, _, _ = _oracle_stream(x.cpu().numpy(), packed, hp, 21, 3)
-    got = packed.data.cpu().numpy()
+    got = packed.compact().data.cpu().numpy()
     assert got.size == stream.size, (got.size, stream.size)
     assert np.array_equal(got, stream), int(np.argmax(got != stream))
     assert packed.bits_per_element < 8.0 or n < (1 << 16)  # per-block header amortised
@@ -90,7 +90,7 @@ def test_escapes_bits_and_all_positive(bits):
         torch.cuda.synchronize()
         assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), n_diff_f32(
             y.cpu().numpy(), y_ref.cpu().numpy())
-        got = packed.data.cpu().numpy()
+        got = packed.compact().data.cpu().numpy()
         assert P.header(got)["n"] == x_np.size
         assert same_f32(P.unpack(got), y.cpu().numpy())  # the oracle decodes the device stream
 
@@ -107,7 +107,7 @@ def test_half_inputs(dt):
     torch.cuda.synchronize()
     assert y.dtype == torch.float32 and same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
     stream, _, _ = _oracle_stream(x.float().cpu().numpy(), packed, hp, 21, 3, dtype=dt)
-    assert np.array_equal(packed.data.cpu().numpy(), stream)
+    assert np.array_equal(packed.compact().data.cpu().numpy(), stream)
 
 
 def test_sampled_and_range_stats():
@@ -190,7 +190,7 @@ def test_negative_threshold(thr, bits, sr):
     torch.cuda.synchronize()
     assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), n_diff_f32(y.cpu().numpy(),
                                                                       y_ref.cpu().numpy())
-    raw = packed.data.cpu().numpy()
+    raw = packed.compact().data.cpu().numpy()
     assert P.header(raw)["flags"] & P.FLAG_BOTH_SIDES
     assert np.array_equal(raw, _bn_stream_vs_oracle(x, packed, hp, 9, 4, None, False))
 
@@ -223,7 +223,7 @@ def test_batch_norm_variant(shape, bits):
         assert y.shape == x.shape
         assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), (over, allpos, n_diff_f32(
             y.cpu().numpy(), y_ref.cpu().numpy()))
-        raw = packed.data.cpu().numpy()
+        raw = packed.compact().data.cpu().numpy()
         h = P.header(raw)
         assert h["flags"] & P.FLAG_BN and h["bn_inner"] == shape[2] * shape[3]
         bn = (gam.mean().reshape(1), bet.mean().reshape(1)) if over.get("bn_scalar_params") \
@@ -247,7 +247,7 @@ def test_batch_norm_half_inputs(dt):
     y_ref = ref(x, batch_norm_stats=(gam, bet))
     torch.cuda.synchronize()
     assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
-    assert np.array_equal(packed.data.cpu().numpy(),
+    assert np.array_equal(packed.compact().data.cpu().numpy(),
                           _bn_stream_vs_oracle(x, packed, hp, 3, 0, (gam, bet), False))
 
 
@@ -269,7 +269,7 @@ def test_large_multiblock():
     torch.cuda.synchronize()
     assert torch.equal(y.view(torch.int32), y_ref.view(torch.int32))
     del y, y_ref
-    raw = packed.data.cpu().numpy()
+    raw = packed.compact().data.cpu().numpy()
     h, dirs, fixed_w, var_w = P.regions(raw)
     nb = h["n_blocks"]
     assert nb == n // 4096 and h["error"] == 0 and h["total_bytes"] == raw.size
@@ -298,9 +298,9 @@ def test_compress_is_repeatable():
     """Same seed/offset twice on one workspace: identical streams."""
     hp, pk, _ = _codecs(seed=4, offset=0)
     x = torch.randn(3 * 4096 + 77, device="cuda")
-    a = pk.compress(x).data.clone()
+    a = pk.compress(x).compact().data.clone()
     pk.rng.offset = 0
-    b = pk.compress(x).data
+    b = pk.compress(x).compact().data
     assert torch.equal(a, b)
 
 
@@ -429,3 +429,70 @@ def test_decompress_with_and_without_caller_widths():
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     assert not torch.equal(a, torch.full_like(a, 7.0))
     assert torch.equal(c, torch.full_like(c, 7.0))
+
+
+def test_decompress_wrong_n_leaves_y_untouched():
+    """A caller's n larger than the stream's (a right-sized buffer, so the stream's directory and
+    fixed region end well before the caller's n would reach): the decoder checks the header's magic
+    and n before it reads any directory entry or section, leaves y alone and does not fault."""
+    from smart_compress_amd import _native as N
+
+    hp, pk, _ = _codecs(seed=5, offset=0)
+    n = 7 * 4096 + 19
+    packed = pk.compress(torch.randn(n, device="cuda")).compact()
+    lib = N.lib()
+    st = N.stream_ptr(packed.data.device)
+    for n2 in (n + 1, 64 * 4096, 1 << 22):
+        for ex in (False, True):
+            y = torch.full((n2,), 7.0, device="cuda")
+            if ex:
+                N.check(lib.smq_smaq_decompress_ex(packed.data.data_ptr(), y.data_ptr(), n2, 6, 8,
+                                                   st), "dex")
+            else:
+                N.check(lib.smq_smaq_decompress(packed.data.data_ptr(), y.data_ptr(), n2, st), "dec")
+            torch.cuda.synchronize()
+            assert torch.equal(y, torch.full_like(y, 7.0)), (n2, ex)
+
+
+def test_stream_from_elsewhere_decodes_with_header_widths():
+    """A SmaqPacked without recorded widths (a stream received from elsewhere) is decoded with the
+    widths its header records, whatever the decoding codec's own flags."""
+    from smart_compress_amd.compress.packed import SmaqPacked
+
+    hp, pk, single = _codecs(seed=9, offset=0, num_bits_main=4, num_bits_outlier=6)
+    x = torch.randn(5 * 4096 + 3, device="cuda")
+    packed = pk.compress(x).compact()
+    want = pk.decompress(packed)
+    _, other, _ = _codecs(seed=1, offset=0)  # 6/8 bits
+    got = other.decompress(SmaqPacked(packed.data, packed.shape, packed.n))
+    assert torch.equal(got.view(torch.int32), want.view(torch.int32))
+
+
+def test_compress_decompress_in_a_captured_graph():
+    """compress + decompress never synchronise the host: the pair is captured into a hipGraph
+    (graph-safe random stream) and two replays equal two eager round trips of SmartFP at the same
+    stream positions, bit for bit; the stream size is read only when asked (nbytes)."""
+    from smart_compress_amd.compress.packed import SmartFPPacked
+    from smart_compress_amd.compress.smart import SmartFP
+
+    hp = smaq_hparams()
+    x = torch.randn(9 * 4096 + 5, device="cuda")
+    eager = SmartFP(hp)
+    eager.rng.seed, eager.rng.offset = 44, 0
+    want = [eager(x).clone() for _ in range(2)]
+    pk = SmartFPPacked(hp)
+    pk.rng.seed, pk.rng.offset = 44, 0
+    pk.graph_safe(True, device="cuda")
+    pk.decompress(pk.compress(x))  # eager call: workspaces and the device counter exist
+    torch.cuda.synchronize()
+    pk.rng.load_state_dict({"seed": 44, "offset": 0})
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        packed = pk.compress(x)
+        y = pk.decompress(packed)
+    for r in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y.view(torch.int32), want[r].view(torch.int32)), r
+    assert 0 < packed.nbytes < 4 * x.numel()
+    pk.graph_safe(False)

@@ -192,3 +192,44 @@ def test_optimlp_host_contract():
     o.step(lambda: None)
     kinds = [s[0] for s in seen]
     assert kinds.count("g") == 4 and kinds.count("w") == 2 and kinds.count("m") == 2
+
+
+def test_bench_trace_takes_the_product_entry_point(monkeypatch):
+    """bench.py attaches an event recorder (SmartFP._trace); the codec must still run its product
+    entry point, smq_smaq_roundtrip (the single launch / deferred / two-launch choice is the
+    library's), bracketed as a whole — never the split statistics + apply calls."""
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.smart import SmartFP
+
+    calls = []
+
+    class FakeLib:
+        def __getattr__(self, name):
+            def fn(*a):
+                calls.append(name)
+                return 0
+            return fn
+
+    class Trace:
+        def __init__(self):
+            self.marks = []
+
+        def begin(self, k):
+            self.marks.append(("begin", k, len(calls)))
+
+        def end(self, k):
+            self.marks.append(("end", k, len(calls)))
+
+    monkeypatch.setattr(N, "lib", lambda: FakeLib())
+    codec = SmartFP(smaq_hparams())
+    tr = codec._trace = Trace()
+    x = torch.randn(1 << 12)
+    y = torch.empty_like(x)
+    ws = torch.zeros(256, dtype=torch.uint8)
+    for n_elems in (1 << 12, 300000000):  # one launch and the statistics + apply pair alike
+        calls.clear()
+        tr.marks.clear()
+        p = codec._params(n_elems, False)
+        codec._launch(x, y, n_elems, p, ws, N.SMQ_DTYPE_F32, st=0)
+        assert calls == ["smq_smaq_roundtrip"], calls
+        assert tr.marks == [("begin", "call", 0), ("end", "call", 1)]

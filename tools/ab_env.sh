@@ -1,6 +1,9 @@
 #!/bin/bash
 # A/B of environment settings on one bench config, interleaved rounds.
 # Usage: bash tools/ab_env.sh <rounds> "<bench args>" "<env A>" "<env B>" ...
+# The SMQ_* environment knobs are read only by an experiment build (smq_common.h knob_env):
+#   python tools/build_variant.py knobs -DSMQ_KNOBS=1   (this script then loads it via SMQ_LIB)
+export SMQ_LIB="${SMQ_LIB:-${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}/exp/knobs/libsmq.so}"
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 ROUNDS=$1; ARGS=$2; shift 2

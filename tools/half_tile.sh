@@ -1,5 +1,8 @@
 #!/bin/bash
 # Half-precision inputs: 16-B loads (default) vs 8-B loads (SMQ_HALF_TILE=0), 256M, interleaved.
+# The SMQ_* environment knobs are read only by an experiment build (smq_common.h knob_env):
+#   python tools/build_variant.py knobs -DSMQ_KNOBS=1   (this script then loads it via SMQ_LIB)
+export SMQ_LIB="${SMQ_LIB:-${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}/exp/knobs/libsmq.so}"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for r in 1 2; do for dt in f16 bf16; do for m in 0 1; do
   SMQ_HALF_TILE=$m SMQ_BENCH_DTYPE=$dt timeout -k 10 120 python bench.py --no-cpu-baseline > gpurun_out/ht_${dt}_${m}_$r.log 2>&1 || exit 1

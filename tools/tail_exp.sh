@@ -1,6 +1,9 @@
 #!/bin/bash
 # A/B of the plain-load tail of the nt statistics sweep (SMQ_STATS_PLAIN_TAIL_MB), headline bench,
 # interleaved rounds. Prints ms/step and the event-timed apply per setting.
+# The SMQ_* environment knobs are read only by an experiment build (smq_common.h knob_env):
+#   python tools/build_variant.py knobs -DSMQ_KNOBS=1   (this script then loads it via SMQ_LIB)
+export SMQ_LIB="${SMQ_LIB:-${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}/exp/knobs/libsmq.so}"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for round in 1 2; do
   for mb in ${TAILS:-0 128 192 256}; do
