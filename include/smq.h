@@ -77,7 +77,7 @@ extern "C" {
  * (int64, draw order) instead of SMQ_WS_SAMPLES_OFFSET. The indices are the same Floyd draw either
  * way (smq_smaq_draw_samples / oracle/rng.py floyd_indices). */
 #define SMQ_MAX_DRAW_SAMPLES (1 << 28)
-#define SMQ_WS_LARGE_SAMPLES_OFFSET 198016
+#define SMQ_WS_LARGE_SAMPLES_OFFSET 199168
 
 /* Where smq_smaq_apply_f32 takes (mean, std) from. */
 #define SMQ_STATS_WORKSPACE 0 /* written by smq_smaq_stats_f32 into the workspace header */

@@ -18,18 +18,22 @@
 // Hand-off (cdna_hip_programming.md Guideline 16 R2, as the single-launch S2FP8 in float_quant.hip):
 // a partial is 4 (6 with range-std: + min, max) aligned 8-byte granules {epoch, 32-bit word}, each
 // ONE relaxed agent-scope (sc1) store, written to 8 replicas (replica r is polled by the workgroups
-// b % 8 == r, spreading 256 readers over 8x the memory channels). One wave per workgroup re-reads
-// the granules it still misses until every tag is this call's epoch. The epoch is (generation << 1)
-// | 1: every workgroup reads the generation word at its start; the last workgroup past the wait (an
-// arrival word tagged with the generation: the add is issued early and looked at at the end)
-// advances it, the graph-safe stream counter and the arrival word. Calls on one workspace are
-// serialised by the stream, so consecutive calls — eager or replayed from a graph — see
-// consecutive generations and never a stale granule of an earlier call as their own.
+// b % 8 == r, spreading 256 readers over 8x the memory channels). A replica is dense (partial k's
+// words at k * words): every thread re-reads the two words it owns while any is missing, so a wave
+// load is 512 consecutive bytes (4 lines, not 64) — 12 KB per pass in 96 lines. The epoch is
+// (generation << 1) | 1: every workgroup reads the generation word at its start; the arrival words
+// (eight per residue b % 8, one on top: same-address atomics serialise at ~12 ns each, so 256 adds
+// on one word would cost ~3 us) are tagged with the generation, added to after the gather and
+// looked at after the transform; the last arrival advances the generation, the graph-safe stream
+// counter and re-arms the arrival words. Calls on one workspace are serialised by the stream, so
+// consecutive calls — eager or replayed from a graph — see consecutive generations and never a
+// stale granule of an earlier call as their own.
 //
 // No co-residency assumption: a workgroup that has waited kFusedStealTicks computes the partials it
 // still misses itself, from memory (a partial is a pure function of its chunk: duplicates store the
 // same bytes), so a grid that is only partly resident (other kernels holding CUs) still finishes.
 #include <limits.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "smq_common.h"
@@ -42,6 +46,7 @@ constexpr int kFusedRep = SmaqWsLayout::kFusedRep;
 constexpr int kFusedWords = SmaqWsLayout::kFusedWords;
 constexpr uint64_t kFusedStealTicks = 20000;  // s_memrealtime at 100 MHz: 200 us
 constexpr int kFusedLds = 88 * 1024;          // dynamic LDS request: one workgroup per CU
+constexpr int kSubStride = (int)(SmaqWsLayout::kFusedSubStride / 8);  // residue words (u64 units)
 
 // ------------------------------------------------------------------------------------------------
 // statistics launch of the two-launch paths (smq_smaq_stats, and smq_smaq_roundtrip when the single
@@ -133,12 +138,14 @@ struct FusedArgs {
   uint64_t* ctr;                 // graph-safe stream position (nullable)
   SmqSmaqStats* hdr;
   uint32_t* gen;                 // generation word
-  unsigned long long* left;      // workgroups past the wait, tagged with the generation
+  unsigned long long* left;      // residues whose workgroups are all past the wait (tagged)
+  unsigned long long* sub;       // workgroups b % 8 == s past the wait: word s * kSubStride
   unsigned long long* gran;      // [kFusedRep][kSmallMaxG][kFusedWords] granules
   unsigned long long* out_slots; // outlier-count slots (count)
   float thr, r_main, r_out, clamp_lo, clamp_hi, range_coef;
   double inv_r_main, inv_r_out;
   int all_pos, count, range, test_late;
+  int poll_sleep;   // s_sleep between poll passes
   uint64_t* trace;  // experiment builds (-DSMQ_FUSED_TRACE=1): 8 timestamps per workgroup
 };
 
@@ -158,12 +165,26 @@ struct FusedArgs {
   } while (0)
 #endif
 
-// The partial of chunk k by the whole workgroup from the lanes' groups g; every thread gets it.
+// s_sleep between poll passes (units of 64 clocks; a compile-time immediate, so a small switch)
+__device__ __forceinline__ void fused_sleep(int s) {
+  switch (s) {
+    case 0: break;
+    case 1: __builtin_amdgcn_s_sleep(1); break;
+    case 2: __builtin_amdgcn_s_sleep(2); break;
+    case 4: __builtin_amdgcn_s_sleep(4); break;
+    case 8: __builtin_amdgcn_s_sleep(8); break;
+    default: __builtin_amdgcn_s_sleep(16); break;
+  }
+}
+
+// The partial of chunk k by the whole workgroup from the lanes' groups g; valid in wave 0 (the
+// next writer of W, fused_steal, runs behind a barrier wave 0 reaches after reading it).
 template <int TIN, int V>
 __device__ __forceinline__ StatAcc fused_partial(const FusedArgs& A, int k, const float4 (&g)[V],
                                                  double shift, SmallWaveLds& W) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const StatAcc w = small_wave(small_lane_sum<TIN, V>(A.x, A.n, V, A.G, k, threadIdx.x, g, shift));
+  const StatAcc w = small_wave(small_lane_sum<TIN, V>(A.x, A.n, V, A.G, k, threadIdx.x, g, shift),
+                               A.range != 0);
   if (lane == 0) {
     W.s1[wave] = w.s1;
     W.s2[wave] = w.s2;
@@ -171,8 +192,8 @@ __device__ __forceinline__ StatAcc fused_partial(const FusedArgs& A, int k, cons
     W.mx[wave] = w.mx;
   }
   lds_barrier();
-  const StatAcc r = small_combine(W);
-  lds_barrier();  // W may be rewritten
+  StatAcc r;
+  if (wave == 0) r = small_combine(W);
   return r;
 }
 
@@ -184,7 +205,7 @@ template <int TIN>
 __device__ __noinline__ StatAcc fused_steal(const void* x, int64_t n, int V, int G, int k,
                                             double shift, SmallWaveLds* W) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const StatAcc w = small_wave(small_lane_seq<TIN>(x, n, V, G, k, threadIdx.x, shift));
+  const StatAcc w = small_wave(small_lane_seq<TIN>(x, n, V, G, k, threadIdx.x, shift), true);
   if (lane == 0) {
     W->s1[wave] = w.s1;
     W->s2[wave] = w.s2;
@@ -197,6 +218,19 @@ __device__ __noinline__ StatAcc fused_steal(const void* x, int64_t n, int V, int
   return r;
 }
 
+// Word c of a partial: s1 low / high, s2 low / high, min, max.
+__device__ __forceinline__ uint32_t partial_word(const StatAcc& a, int c) {
+  const uint64_t b1 = __builtin_bit_cast(uint64_t, a.s1), b2 = __builtin_bit_cast(uint64_t, a.s2);
+  switch (c) {
+    case 0: return (uint32_t)b1;
+    case 1: return (uint32_t)(b1 >> 32);
+    case 2: return (uint32_t)b2;
+    case 3: return (uint32_t)(b2 >> 32);
+    case 4: return __builtin_bit_cast(uint32_t, a.mn);
+    default: return __builtin_bit_cast(uint32_t, a.mx);
+  }
+}
+
 // Lanes 0 .. kFusedRep * words - 1 of wave 0 store partial k's granules (nobody waits for them).
 __device__ __forceinline__ void fused_publish(const StatAcc& a, const FusedArgs& A, int k,
                                               uint32_t epoch) {
@@ -205,17 +239,8 @@ __device__ __forceinline__ void fused_publish(const StatAcc& a, const FusedArgs&
   if (lane >= kFusedRep * words) return;
   const int r = words == 4 ? lane >> 2 : (lane * 43) >> 8;  // lane / words (lane < 48)
   const int c = lane - r * words;
-  const uint64_t b1 = __builtin_bit_cast(uint64_t, a.s1), b2 = __builtin_bit_cast(uint64_t, a.s2);
-  uint32_t word;
-  switch (c) {
-    case 0: word = (uint32_t)b1; break;
-    case 1: word = (uint32_t)(b1 >> 32); break;
-    case 2: word = (uint32_t)b2; break;
-    case 3: word = (uint32_t)(b2 >> 32); break;
-    case 4: word = __builtin_bit_cast(uint32_t, a.mn); break;
-    default: word = __builtin_bit_cast(uint32_t, a.mx); break;
-  }
-  st_sc1_u64(&A.gran[((size_t)r * kSmallMaxG + k) * kFusedWords + c],
+  const uint32_t word = partial_word(a, c);
+  st_sc1_u64(A.gran + (size_t)r * kSmallMaxG * kFusedWords + (size_t)k * words + c,
              ((unsigned long long)epoch << 32) | word);
 }
 
@@ -283,9 +308,8 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   __shared__ SmqSmaqStats sst;
   __shared__ float4 u0lds[V <= 4 ? V : 1][kWave];  // wave 0's rounding draws (PRE)
   __shared__ uint32_t sh_cnt[kSmallWaves];
-  __shared__ uint32_t pw[kSmallMaxG][kFusedWords];  // the gathered partials' words
-  __shared__ uint32_t pw_have[kSmallMaxG];            // pw holds partial k (pollers' bookkeeping)
-  __shared__ int smiss[4];
+  __shared__ uint32_t pw[kSmallMaxG * kFusedWords];  // the gathered partials' words (k * words + c)
+  __shared__ int smiss[kSmallWaves];
   const int b = blockIdx.x, G = A.G;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int64_t base = (int64_t)b * V * kSmallT + threadIdx.x;
@@ -324,7 +348,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   if (G > 1 && wave == 0) fused_publish(part, A, b, epoch);
 
   // the rounding draws depend on the stream position only: every wave computes its own now (wave
-  // 0's by waves 4..4+V-1, handed over in LDS), while waves 0..3 gather the partials. Above 3
+  // 0's by waves 4..4+V-1, handed over in LDS), before it polls for the partials. Above 3
   // groups per lane they would hold 4V more VGPRs across the gather: hashed in the transform.
   constexpr bool PRE = RM == kRoundHash && V <= 3;
   float uu[V][4];
@@ -346,54 +370,59 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
 
   unsigned long long left_old = 0;
   if (G > 1) {
-    // waves 0..3 gather the G partials from replica b % 8 — lane l of wave w polls partial
-    // 4l + w (its granules are one contiguous 48-B run) — until every granule carries the epoch;
-    // accepted words go to LDS (pw). One loop for the whole workgroup: the pollers wait (the first
-    // time until every granule is there or their patience runs out, afterwards one pass); a
-    // partial still missing then is computed by the whole workgroup from memory and published, and
-    // the pollers look again.
+    // every thread gathers the words t and t + 1024 of replica b % 8 (G * words words, dense:
+    // partial k's word c at k * words + c), so each wave load reads 512 consecutive bytes, until
+    // every granule carries the epoch; accepted words go to LDS (pw). One loop for the whole
+    // workgroup: each wave waits (the first time until its words are there or its patience runs
+    // out, afterwards one pass); a partial still missing then is computed by the whole workgroup
+    // from memory and published, and the waves look again.
     const int words = A.range ? 6 : 4;
-    const unsigned long long* rep = A.gran + (size_t)(b % kFusedRep) * kSmallMaxG * kFusedWords;
-    const bool poller = wave < 4;
-    const int pk = 4 * lane + wave;  // the partial this lane polls (pollers)
-    const unsigned long long* mine = rep + (size_t)pk * kFusedWords;
-    if (poller) pw_have[pk] = 0u;
+    const int total = G * words;
+    const unsigned long long* rep =
+        A.gran + (size_t)(b % kFusedRep) * kSmallMaxG * kFusedWords;
+    const int i0 = threadIdx.x, i1 = threadIdx.x + kSmallT;
+    uint32_t miss_bits = (i0 < total ? 1u : 0u) | (i1 < total ? 2u : 0u);
     bool stealing = false;
     for (;;) {
-      if (poller) {
-        uint32_t miss_bits = (pk < G && pw_have[pk] == 0u) ? (1u << words) - 1u : 0u;
-        const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-        uint32_t polls = 0;
-        for (;;) {
-          unsigned long long g[kFusedWords];
-#pragma unroll
-          for (int c = 0; c < kFusedWords; ++c) g[c] = c < words ? ld_sc1_u64(mine + c) : 0ull;
-#pragma unroll
-          for (int c = 0; c < kFusedWords; ++c) {
-            if (((miss_bits >> c) & 1u) && (uint32_t)(g[c] >> 32) == epoch) {
-              miss_bits &= ~(1u << c);
-              pw[pk][c] = (uint32_t)g[c];
-            }
-          }
-          if (__all(miss_bits == 0u) || stealing) break;
-          if ((++polls & 7) != 0) {
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-          }
-          if (__builtin_amdgcn_s_memrealtime() - t_start > steal_ticks) break;
-          __builtin_amdgcn_s_sleep(2);
+      const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+      uint32_t polls = 0;
+      for (;;) {
+        const unsigned long long g0 = (miss_bits & 1u) ? ld_sc1_u64(rep + i0) : 0ull;
+        const unsigned long long g1 = (miss_bits & 2u) ? ld_sc1_u64(rep + i1) : 0ull;
+        if ((miss_bits & 1u) && (uint32_t)(g0 >> 32) == epoch) {
+          miss_bits &= ~1u;
+          pw[i0] = (uint32_t)g0;
         }
-        if (pk < G) pw_have[pk] = miss_bits == 0u ? 1u : 0u;
-        // first missing partial after b (cyclically)
-        int d = pk - b;
-        d += d < 0 ? G : 0;
-        int miss = miss_bits ? d : INT_MAX;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, kWave));
-        if (lane == 0) smiss[wave] = miss;
+        if ((miss_bits & 2u) && (uint32_t)(g1 >> 32) == epoch) {
+          miss_bits &= ~2u;
+          pw[i1] = (uint32_t)g1;
+        }
+        if (__all(miss_bits == 0u) || stealing) break;
+        if ((++polls & 7) != 0) {
+          fused_sleep(A.poll_sleep);
+          continue;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t_start > steal_ticks) break;
+        fused_sleep(A.poll_sleep);
       }
+      // the first missing partial after b (cyclically); i / words without a division (i < 1536)
+      int miss = INT_MAX;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (!((miss_bits >> h) & 1u)) continue;
+        const int i = h ? i1 : i0;
+        const int k = words == 4 ? i >> 2 : (i * 43691) >> 18;
+        int d = k - b;
+        d += d < 0 ? G : 0;
+        miss = min(miss, d);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, kWave));
+      if (lane == 0) smiss[wave] = miss;
       lds_barrier();
-      const int m = min(min(smiss[0], smiss[1]), min(smiss[2], smiss[3]));
+      int m = smiss[0];
+#pragma unroll
+      for (int w = 1; w < kSmallWaves; ++w) m = min(m, smiss[w]);
       if (m == INT_MAX) break;
       // the patience ran out: compute partial (m + b) % G from memory (one group per lane in
       // flight) and publish it
@@ -401,10 +430,22 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       stealing = true;
       const StatAcc pk_acc = fused_steal<TIN>(A.x, A.n, V, G, k, shift, &W);
       if (wave == 0) fused_publish(pk_acc, A, k, epoch);
+      // its words need no poll here (and the others' next pass may precede the stores)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = h ? i1 : i0;
+        const int c = i - k * words;
+        if (((miss_bits >> h) & 1u) && c >= 0 && c < words) {
+          pw[i] = partial_word(pk_acc, c);
+          miss_bits &= ~(1u << h);
+        }
+      }
     }
     FSTAMP(2);
-    // count this workgroup past the wait now; the returned word is looked at only at the end
-    if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.left);
+    // count this workgroup past the wait now, on its residue's word (eight words of <= 32 arrivals
+    // each instead of one word of 256: same-address atomics serialise at ~12 ns each); the
+    // returned word is looked at only after the transform
+    if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.sub + (b & 7) * kSubStride);
     if (wave == 0) {
       // reduce_partials_w0's order: lane l adds partials 4l .. 4l+3 from 0.0, then one ascending
       // butterfly
@@ -414,11 +455,12 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       for (int q = 0; q < 4; ++q) {
         const int k = 4 * lane + q;
         if (k >= G) continue;
-        s1 += __builtin_bit_cast(double, ((uint64_t)pw[k][1] << 32) | pw[k][0]);
-        s2 += __builtin_bit_cast(double, ((uint64_t)pw[k][3] << 32) | pw[k][2]);
+        const uint32_t* w = pw + k * words;
+        s1 += __builtin_bit_cast(double, ((uint64_t)w[1] << 32) | w[0]);
+        s2 += __builtin_bit_cast(double, ((uint64_t)w[3] << 32) | w[2]);
         if (A.range) {
-          mn = fminf(mn, __builtin_bit_cast(float, pw[k][4]));
-          mx = fmaxf(mx, __builtin_bit_cast(float, pw[k][5]));
+          mn = fminf(mn, __builtin_bit_cast(float, w[4]));
+          mx = fmaxf(mx, __builtin_bit_cast(float, w[5]));
         }
       }
       s1 = wave_sum_asc(s1);
@@ -457,14 +499,6 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       uu[u][2] = w.z;
       uu[u][3] = w.w;
     }
-  }
-  // the last workgroup past the wait (its add, issued after the gather, has long returned)
-  // advances the generation and the stream and re-arms the arrival word, before its own stores
-  if (G > 1 && threadIdx.x == 0 &&
-      arrive_tagged_finish(A.left, gen, left_old) == (uint32_t)G - 1) {
-    st_sc1_u32(A.gen, gen + 1u);
-    if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
-    st_sc1_u64(A.left, (unsigned long long)(gen + 1u) << 32);
   }
   FSTAMP(3);
   ElemConsts c;
@@ -511,6 +545,22 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       if (s) atomicAdd(A.out_slots + (b & (SMQ_WS_OUTLIER_SLOTS - 1)), s);
     }
   }
+  // the last workgroup of its residue arrives on the top word; the last residue's advances the
+  // generation and the stream and re-arms the arrival words. Every workgroup has read the
+  // generation, the stream position and the granules before its add.
+  if (G > 1 && threadIdx.x == 0) {
+    const uint32_t s = (uint32_t)b & 7u;
+    const uint32_t n_s = ((uint32_t)G - 1u - s) / 8u + 1u;  // workgroups of residue s
+    if (arrive_tagged_finish(A.sub + s * kSubStride, gen, left_old) == n_s - 1u &&
+        arrive_tagged(A.left, gen) == (G < 8 ? (uint32_t)G : 8u) - 1u) {
+      st_sc1_u32(A.gen, gen + 1u);
+      if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
+      const unsigned long long armed = (unsigned long long)(gen + 1u) << 32;
+      st_sc1_u64(A.left, armed);
+      for (int r = 0; r < 8; ++r) st_sc1_u64(A.sub + r * kSubStride, armed);
+    }
+  }
+  FSTAMP(7);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -595,6 +645,7 @@ int launch_fused(const FusedCall& c, hipStream_t st) {
   F.hdr = (SmqSmaqStats*)base;
   F.gen = (uint32_t*)(base + SmaqWsLayout::kFusedGen);
   F.left = (unsigned long long*)(base + SmaqWsLayout::kFusedLeft);
+  F.sub = (unsigned long long*)(base + SmaqWsLayout::kFusedSub);
   F.gran = (unsigned long long*)(base + SmaqWsLayout::kFusedGran);
   F.out_slots = (unsigned long long*)(base + SmaqWsLayout::kSlots);
   F.thr = p->main_std_dev_threshold;
@@ -609,6 +660,11 @@ int launch_fused(const FusedCall& c, hipStream_t st) {
   F.count = p->count_outliers;
   F.range = p->use_range_std_dev;
   F.test_late = c.test_late;
+  static const int poll_sleep = [] {  // measurement knob SMQ_FUSED_SLEEP (0, 1, 2, 4, 8, 16)
+    const char* e = knob_env("SMQ_FUSED_SLEEP");
+    return e ? atoi(e) : 2;
+  }();
+  F.poll_sleep = poll_sleep;
   F.trace = nullptr;
 #if SMQ_FUSED_TRACE
   if (c.ws_bytes >= SmaqWsLayout::kTotal + 8 * 8 * (size_t)kSmallMaxG)

@@ -132,12 +132,15 @@ __device__ __forceinline__ StatAcc small_lane(const void* x, int64_t n, int V, i
   return small_lane_sum<TIN, MAXV>(x, n, V, G, b, t, g, shift);
 }
 
-// Wave value of 64 lane values (every lane gets it).
-__device__ __forceinline__ StatAcc small_wave(StatAcc a) {
+// Wave value of 64 lane values (every lane gets it); the extrema only with range-std (their
+// reduction order does not matter, so any path may skip or compute them).
+__device__ __forceinline__ StatAcc small_wave(StatAcc a, bool range = true) {
   a.s1 = wave_sum_asc(a.s1);
   a.s2 = wave_sum_asc(a.s2);
-  a.mn = wave_min(a.mn);
-  a.mx = wave_max(a.mx);
+  if (range) {
+    a.mn = wave_min_dpp(a.mn);
+    a.mx = wave_max_dpp(a.mx);
+  }
   return a;
 }
 

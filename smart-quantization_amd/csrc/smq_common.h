@@ -159,6 +159,31 @@ __device__ __forceinline__ float wave_nanmax_asc(float v) {
   return nan_max2(nan_max2(r0, r1), nan_max2(r2, r3));
 }
 
+// fminf / fmaxf over the wave by DPP moves and readlanes (no LDS round trips; order-free up to the
+// sign of a zero result); every lane gets the result.
+__device__ __forceinline__ float wave_min_dpp(float v) {
+  v = fminf(v, dpp_f32<kDppXor1>(v));
+  v = fminf(v, dpp_f32<kDppXor2>(v));
+  v = fminf(v, dpp_f32<kDppHalfMirror>(v));
+  v = fminf(v, dpp_f32<kDppMirror>(v));
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return fminf(fminf(r0, r1), fminf(r2, r3));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_f32<kDppXor1>(v));
+  v = fmaxf(v, dpp_f32<kDppXor2>(v));
+  v = fmaxf(v, dpp_f32<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_f32<kDppMirror>(v));
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
@@ -299,12 +324,15 @@ struct SmaqWsLayout {
   // workspace captured into one graph each find their own word on every replay.
   static constexpr size_t kTagCounters = SMQ_WS_SAMPLES_OFFSET + 8 * SMQ_MAX_DEVICE_SAMPLES;
   static constexpr int kTagWords = 64;
-  // single-launch round trip (smaq_fused.hip): generation word, arrival word, then the granules
-  // [kFusedRep][kFusedWords][256] of the partials
+  // single-launch round trip (smaq_fused.hip): generation word, the arrival words (one top word,
+  // eight per-residue words of workgroups b % 8 == s, each on a 128-B line of its own), then the
+  // granules [kFusedRep][256][kFusedWords] of the partials
   static constexpr size_t kFused = SMQ_WS_FUSED_OFFSET;
   static constexpr size_t kFusedGen = kFused;
-  static constexpr size_t kFusedLeft = kFused + 64;
-  static constexpr size_t kFusedGran = kFused + 128;
+  static constexpr size_t kFusedLeft = kFused + 128;
+  static constexpr size_t kFusedSub = kFused + 256;
+  static constexpr size_t kFusedSubStride = 128;
+  static constexpr size_t kFusedGran = kFusedSub + 8 * kFusedSubStride;
   static constexpr int kFusedRep = 8;
   static constexpr int kFusedWords = 6;  // s1 low / high, s2 low / high, min, max
   static constexpr size_t kFusedEnd = kFusedGran + 8 * (size_t)kFusedRep * kFusedWords * 256;

@@ -24,7 +24,7 @@ SMQ_MAX_SAMPLES = 64
 SMQ_MAX_DEVICE_SAMPLES = 4096
 SMQ_MAX_DRAW_SAMPLES = 1 << 28
 SMQ_WS_FUSED_OFFSET = 99584
-SMQ_WS_LARGE_SAMPLES_OFFSET = 198016
+SMQ_WS_LARGE_SAMPLES_OFFSET = 199168
 SMQ_WS_OUTLIER_SLOTS_OFFSET = 128
 SMQ_WS_OUTLIER_SLOTS = 64
 SMQ_WS_SAMPLES_OFFSET = 66176
@@ -414,8 +414,22 @@ def stream_ptr(device: torch.device) -> int:
 
 
 # ---- per (device, stream) workspaces (the library needs them neither zeroed nor reset) ----------
+# Keyed by the raw stream handle, which the table does not own: a program that creates streams
+# without end would grow it without end, so it holds at most WORKSPACE_LIMIT entries. A new entry
+# past the limit evicts the oldest one after synchronising that device (its stream may still have
+# calls queued). A captured graph keeps using the buffers its calls were given, so eviction stops
+# for good once graph-safe random streams (the precondition of capturing a codec call) exist in
+# the process (RngState.counter) or a workspace is created during a capture.
+WORKSPACE_LIMIT = 256  # above torch's per-device stream pool (2 x 32) times the workspace kinds
 _ws: Dict[Tuple[str, int, int], torch.Tensor] = {}
+_ws_evictable = True
 _ws_lock = threading.Lock()
+
+
+def pin_workspaces() -> None:
+    """Stop evicting workspaces (a hipGraph may hold any of them from now on)."""
+    global _ws_evictable
+    _ws_evictable = False
 
 
 def workspace(kind: str, device: torch.device, nbytes: int, stream: int = None) -> torch.Tensor:
@@ -426,6 +440,10 @@ def workspace(kind: str, device: torch.device, nbytes: int, stream: int = None) 
     if buf is not None and buf.numel() >= nbytes:
         return buf
     with _ws_lock:
+        capturing = (torch.device(device).type == "cuda"
+                     and torch.cuda.is_current_stream_capturing())
+        if capturing:
+            pin_workspaces()
         buf = _ws.get(key)
         if buf is None or buf.numel() < nbytes:
             # Allocated while a graph is being captured, a zero-fill would become a graph node
@@ -433,12 +451,15 @@ def workspace(kind: str, device: torch.device, nbytes: int, stream: int = None) 
             # arrival counters cleared and take the slow re-tagging path (include/smq.h: the
             # SmaQ and S2FP8 workspaces need no initialisation). The packed codec's look-back
             # status words do need it; for them a per-replay clear is only a redundant memset.
-            capturing = (torch.device(device).type == "cuda"
-                         and torch.cuda.is_current_stream_capturing())
             if capturing and kind in ("smaq", "s2fp8"):
                 buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
             else:
                 buf = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
+            if key not in _ws and len(_ws) >= WORKSPACE_LIMIT and _ws_evictable:
+                old = next(iter(_ws))
+                if old[1] >= 0 and torch.cuda.is_available():
+                    torch.cuda.synchronize(old[1])
+                del _ws[old]
             _ws[key] = buf
     return buf
 
@@ -475,6 +496,7 @@ class RngState:
             v = self.offset - 2**64 if self.offset >= 2**63 else self.offset  # int64 bit pattern
             c = torch.tensor([v], dtype=torch.int64, device=torch.device("cuda", idx))
             self._counters[idx] = c
+            pin_workspaces()  # calls may now be captured: their workspaces must stay alive
         return c
 
     def position(self) -> int:

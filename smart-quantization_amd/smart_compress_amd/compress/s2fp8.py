@@ -45,8 +45,6 @@ class S2FP8(CompressionAlgorithmBase):
     _fn = None  # the bound C entry point and its workspace size, resolved on first use
     _ws_bytes = 0
 
-    _ws_cache = {}  # (device index, raw stream) -> workspace, for the device fast path
-
     @torch.no_grad()
     def __call__(self, tensor: torch.Tensor, tag: str = None, **_):
         hp = self.hparams
@@ -99,8 +97,8 @@ class S2FP8(CompressionAlgorithmBase):
 
     def _call_device_f32(self, tensor: torch.Tensor) -> torch.Tensor:
         """The eager hot path (an fp32 device tensor at precision 32): the same call as the general
-        path with its per-call Python trimmed — a C-level stream query, a workspace cached per
-        (device, stream) — since at BERT-hidden size (C4) the host enqueue is as long as the launch."""
+        path with its per-call Python trimmed — a C-level stream query, one lookup in the bounded
+        per-(device, stream) workspace table (_native.workspace) — since at BERT-hidden size (C4) the host enqueue is as long as the launch."""
         x = tensor if tensor.is_contiguous() else tensor.contiguous()
         y = torch.empty_like(x)
         n = x.numel()
@@ -113,9 +111,9 @@ class S2FP8(CompressionAlgorithmBase):
             fn = S2FP8._fn = lib.smq_s2fp8_roundtrip
         dev = x.get_device()
         st = N.raw_stream(dev)
-        ws = S2FP8._ws_cache.get((dev, st))
+        ws = N._ws.get(("s2fp8", dev, st))  # the bounded workspace table's hit path, inlined
         if ws is None:
-            ws = S2FP8._ws_cache[(dev, st)] = N.workspace("s2fp8", x.device, S2FP8._ws_bytes, st)
+            ws = N.workspace("s2fp8", x.device, S2FP8._ws_bytes, st)
         seed, offset, ctr = _q.rng_stream(n, x.device)
         rc = fn(x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, 32,
                 1 if self.hparams.float_quantize_check_inf else 0, None, seed, offset, ctr, None,

@@ -233,3 +233,24 @@ def test_bench_trace_takes_the_product_entry_point(monkeypatch):
         codec._launch(x, y, n_elems, p, ws, N.SMQ_DTYPE_F32, st=0)
         assert calls == ["smq_smaq_roundtrip"], calls
         assert tr.marks == [("begin", "call", 0), ("end", "call", 1)]
+
+
+def test_workspace_table_is_bounded(monkeypatch):
+    """The per-(kind, device, stream) workspace table keeps at most WORKSPACE_LIMIT entries,
+    evicting the oldest, until graph-safe random streams exist (a captured graph may hold any
+    workspace from then on): after pin_workspaces() nothing is evicted."""
+    from smart_compress_amd import _native as N
+
+    monkeypatch.setattr(N, "_ws", {})
+    monkeypatch.setattr(N, "_ws_evictable", True)
+    monkeypatch.setattr(N, "WORKSPACE_LIMIT", 8)
+    dev = torch.device("cpu", 0)
+    bufs = [N.workspace("s2fp8", dev, 300, stream=s) for s in range(20)]
+    assert len(N._ws) == 8
+    assert [k[2] for k in N._ws] == list(range(12, 20))
+    assert N.workspace("s2fp8", dev, 300, stream=19) is bufs[19]  # a hit creates nothing
+    assert N.workspace("s2fp8", dev, 10, stream=19) is bufs[19]
+    N.pin_workspaces()
+    for s in range(20, 30):
+        N.workspace("s2fp8", dev, 300, stream=s)
+    assert len(N._ws) == 18

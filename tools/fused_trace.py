@@ -3,7 +3,8 @@ experiment build with -DSMQ_FUSED_TRACE=1 (tools/build_variant.py fused_trace -D
 run with SMQ_LIB=exp/fused_trace/libsmq.so). Back-to-back calls, each on its own workspace (the
 stamps live past its end); medians over the calls of: loads + partial published, every partial
 gathered, statistics final, transform issued, stores drained (us from the call's first workgroup
-start), the slowest workgroup's end, and the gap to the next call's first start."""
+start; max: the slowest workgroup's), the arrival words' hand-off after the transform, the
+slowest workgroup's end, and the gap to the next call's first start."""
 
 import os
 import sys
@@ -45,14 +46,17 @@ def main():
         for i in range(CALLS - 1):
             t = tr[i][:G].astype(np.int64)
             t0 = t[:, 0].min()
-            rel = (t[:, :6] - t0) / 100.0  # 100 MHz -> us
-            gap = (tr[i + 1][:G, 0].astype(np.int64).min() - t[:, 5].max()) / 100.0
-            rows.append([np.median(rel[:, k]) for k in range(6)] + [rel[:, 5].max(), gap,
-                                                                     rel[:, 0].max()])
+            rel = (t - t0) / 100.0  # 100 MHz -> us
+            end = max(t[:, 5].max(), t[:, 7].max())
+            gap = (tr[i + 1][:G, 0].astype(np.int64).min() - end) / 100.0
+            rows.append([np.median(rel[:, k]) for k in range(6)] + [
+                (end - t0) / 100.0, gap, rel[:, 0].max(), rel[:, 1].max(), rel[:, 2].max(),
+                np.median(rel[:, 7])])
         m = np.median(np.array(rows), axis=0)
-        print(f"n={n} G={G} start_spread={m[8]:.2f} published={m[1]:.2f} gathered={m[2]:.2f} "
-              f"final={m[3]:.2f} transformed={m[4]:.2f} drained={m[5]:.2f} last={m[6]:.2f} "
-              f"gap_to_next={m[7]:.2f} (us, medians over {len(rows)} calls)", flush=True)
+        print(f"n={n} G={G} start_spread={m[8]:.2f} published={m[1]:.2f} (max {m[9]:.2f}) "
+              f"gathered={m[2]:.2f} (max {m[10]:.2f}) final={m[3]:.2f} transformed={m[4]:.2f} "
+              f"drained={m[5]:.2f} arrived={m[11]:.2f} last={m[6]:.2f} gap_to_next={m[7]:.2f} "
+              f"(us, medians over {len(rows)} calls)", flush=True)
 
 
 if __name__ == "__main__":
