@@ -742,6 +742,7 @@ constexpr int kS2FT = 1024;       // threads per workgroup
 constexpr int kS2FMaxV = 4;       // float4 per lane held in registers (4.2M elements)
 constexpr int kS2FMaxG = 256;     // chunks (= partials; four per lane of the polling wave)
 constexpr int kS2FLds = 88 * 1024;  // dynamic LDS request: one workgroup per CU
+constexpr int kS2SubStride = 16;   // residue arrival words, u64 units (128 B apart)
 constexpr int kS2FRep = 8;          // granule replicas: replica r is read by the blocks b % 8 == r
 constexpr uint64_t kS2StealTicks = 20000;       // s_memrealtime runs at 100 MHz: 200 us
 
@@ -755,7 +756,8 @@ struct S2FArgs {
   uint64_t* ctr;  // graph-safe stream position (nullable)
   SmqS2fp8Stats* hdr;
   uint32_t* gen;               // generation word
-  unsigned long long* left;    // count of workgroups past the wait, tagged with the generation
+  unsigned long long* left;    // residues whose workgroups are all past the wait (tagged)
+  unsigned long long* sub;     // workgroups b % 8 == s past the wait: word s * kS2SubStride
   unsigned long long* gran;    // [kS2FRep][3][kS2FMaxG] granules: sum low word, sum high word, max
   uint32_t tag;                // host tag of the call (mixed into the epoch)
   int check_inf;
@@ -1050,9 +1052,10 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
     lds_barrier();
   }
   s2f_stamp(A, 3);
-  // count this workgroup past the wait now; the returned word is looked at only at the end
+  // count this workgroup past the wait now (on its residue's word); the returned word is looked at
+  // only after the transform
   unsigned long long left_old = 0;
-  if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.left);
+  if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.sub + (b & 7) * kS2SubStride);
   // wave 0: reduce the partials in the two-launch apply's order (lane l: partials l + 64q summed
   // as (q0 + q1) + (q2 + q3), then one ascending butterfly — four butterflies before, 0.7 us) and
   // derive; then threads 0-130 tabulate the inverse powers
@@ -1089,13 +1092,6 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
   s2f_stamp(A, 10);
   lds_barrier();
   s2f_stamp(A, 4);
-  // the last workgroup past the wait (its `left` add, issued after the gather, has long returned)
-  // advances the generation and the stream and re-arms `left`, before its own stores
-  if (threadIdx.x == 0 && arrive_tagged_finish(A.left, gen, left_old) == (uint32_t)A.G - 1) {
-    st_sc1_u32(A.gen, gen + 1u);
-    if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
-    st_sc1_u64(A.left, (unsigned long long)(gen + 1u) << 32);
-  }
   const float alpha = sst.alpha, bp2 = sst.beta_pow2, ialpha = sst.inv_alpha;
   const bool fast = !A.exact_pow && alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f &&
                     ialpha < INFINITY;
@@ -1164,6 +1160,14 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
     const float sg = (xv > 0.0f) ? 1.0f : ((xv < 0.0f) ? -1.0f : 0.0f);
     A.y[e] = A.out_mode ? T : s2_inverse_lut(T, lut) * sg;
   }
+  // the call's last arrival (every workgroup has read the generation, the stream position and the
+  // granules before its add) advances the generation and the stream and re-arms the arrival words
+  if (threadIdx.x == 0 &&
+      arrive_sharded_finish(A.left, A.sub, kS2SubStride, b, A.G, gen, left_old)) {
+    st_sc1_u32(A.gen, gen + 1u);
+    if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
+    rearm_sharded(A.left, A.sub, kS2SubStride, gen + 1u);
+  }
   if (A.trace && threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     A.trace[(size_t)blockIdx.x * 16 + 5] = __builtin_amdgcn_s_memrealtime();
@@ -1222,10 +1226,12 @@ static float host_max_value(int exp_bits, int man_bits) {
   return qtorch_quant(FLT_MAX, 0u, exp_bits, man_bits, false);
 }
 
-// workspace: header, partials, then the single-launch words (own 64-B lines) and granules
-constexpr size_t kS2WsGen = 128 + sizeof(S2Partial) * (size_t)kS2Partials;
-constexpr size_t kS2WsLeft = kS2WsGen + 64;
-constexpr size_t kS2WsGran = kS2WsLeft + 64;
+// workspace: header, partials, then the single-launch words (generation, top arrival word, eight
+// residue arrival words: own 128-B lines) and granules
+constexpr size_t kS2WsGen = (128 + sizeof(S2Partial) * (size_t)kS2Partials + 127) & ~(size_t)127;
+constexpr size_t kS2WsLeft = kS2WsGen + 128;
+constexpr size_t kS2WsSub = kS2WsLeft + 128;
+constexpr size_t kS2WsGran = kS2WsSub + 8 * 8 * (size_t)kS2SubStride;
 static size_t s2_ws_bytes() { return kS2WsGran + (size_t)kS2FRep * 3 * 8 * kS2FMaxG; }
 
 // single-launch path (SMQ_S2_FUSED=0 keeps the two launches: measurement knob)
@@ -1426,6 +1432,7 @@ int smq_s2fp8_roundtrip_ex(const void* x, int dtype, void* y, int64_t n, int pre
       F.hdr = hdr;
       F.gen = reinterpret_cast<uint32_t*>(base + kS2WsGen);
       F.left = reinterpret_cast<unsigned long long*>(base + kS2WsLeft);
+      F.sub = reinterpret_cast<unsigned long long*>(base + kS2WsSub);
       F.gran = reinterpret_cast<unsigned long long*>(base + kS2WsGran);
       F.tag = tg.tag;
       F.check_inf = check_inf;

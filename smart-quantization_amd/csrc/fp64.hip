@@ -386,10 +386,7 @@ static int smaq_f64_impl(const double* x, double* y, int64_t n, const SmqSmaqPar
   A.p = *p;
   A.key = rng_key(p->seed);
   A.count = p->count_outliers;
-  if (p->count_outliers && hipMemsetAsync(A.out_slots, 0, 8 * SMQ_WS_OUTLIER_SLOTS, st) != hipSuccess) {
-    set_error("hipMemsetAsync of the outlier slots failed");
-    return SMQ_ERR_LAUNCH;
-  }
+  if (p->count_outliers) fill_async(A.out_slots, 0ull, SMQ_WS_OUTLIER_SLOTS, st);
   const int rm = !p->stochastic_rounding ? kRoundTrunc : (uniforms ? kRoundUniform : kRoundHash);
   const bool bn = p->bn_gamma != nullptr, ap = p->all_positive != 0;
   const dim3 grid((unsigned)tiles);

@@ -954,12 +954,9 @@ int launch_large_draw(int64_t n, int64_t k, const SmqSmaqParams* p, void* ws, si
   A->susp = (uint32_t*)(r + L.susp);
   A->parts = (StatPartial*)(r + L.parts);
   const size_t slots = (size_t)1 << L.bits;
-  if (hipMemsetAsync(A->hkey, 0xff, 8 * slots, st) != hipSuccess ||
-      hipMemsetAsync(A->hdup, 0, 4 * slots, st) != hipSuccess ||
-      hipMemsetAsync(A->h2key, 0xff, 8 * slots, st) != hipSuccess) {
-    set_error("hipMemsetAsync of the draw's hash sets failed");
-    return SMQ_ERR_LAUNCH;
-  }
+  fill_async(A->hkey, ~0ull, slots, st);
+  fill_async(A->hdup, 0u, slots, st);
+  fill_async(A->h2key, ~0ull, slots, st);
   const int g = (int)std::min<int64_t>(kDrawGridCap, (k + 4 * kBlock - 1) / (4 * kBlock));
   hipLaunchKernelGGL(smaq_draw_candidates_kernel, dim3(g), dim3(kBlock), 0, st, *A);
   hipLaunchKernelGGL(smaq_draw_suspects_kernel, dim3(g), dim3(kBlock), 0, st, *A);
@@ -1092,12 +1089,7 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   const bool vec = aligned(x, dtype == SMQ_DTYPE_F32 ? 16 : 8) && aligned(y, 16) &&
                    (rm != kRoundUniform || aligned(uniforms, 16)) && !A.safe_q;
   A.out_slots = (unsigned long long*)((char*)ws + SmaqWsLayout::kSlots);
-  if (p->count_outliers) {
-    if (hipMemsetAsync(A.out_slots, 0, 8 * SMQ_WS_OUTLIER_SLOTS, st) != hipSuccess) {
-      set_error("hipMemsetAsync of the outlier slots failed");
-      return SMQ_ERR_LAUNCH;
-    }
-  }
+  if (p->count_outliers) fill_async(A.out_slots, 0ull, SMQ_WS_OUTLIER_SLOTS, st);
   static const int rev_env = [] {
     const char* e = knob_env("SMQ_APPLY_REVERSE");
     return e ? atoi(e) : 1;

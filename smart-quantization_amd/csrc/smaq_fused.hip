@@ -146,7 +146,7 @@ struct FusedArgs {
   double inv_r_main, inv_r_out;
   int all_pos, count, range, test_late;
   int poll_sleep;   // s_sleep between poll passes
-  uint64_t* trace;  // experiment builds (-DSMQ_FUSED_TRACE=1): 8 timestamps per workgroup
+  uint64_t* trace;  // experiment builds (-DSMQ_FUSED_TRACE=1): 16 timestamps per workgroup
 };
 
 // s_memrealtime stamps (100 MHz) of workgroup milestones, experiment builds only
@@ -157,7 +157,7 @@ struct FusedArgs {
 #define FSTAMP(i)                                                                   \
   do {                                                                              \
     if (A.trace && threadIdx.x == 0)                                                \
-      A.trace[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();     \
+      A.trace[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime();     \
   } while (0)
 #else
 #define FSTAMP(i) \
@@ -463,12 +463,14 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
           mx = fmaxf(mx, __builtin_bit_cast(float, w[5]));
         }
       }
+      FSTAMP(10);
       s1 = wave_sum_asc(s1);
       s2 = wave_sum_asc(s2);
       if (A.range) {
         mn = wave_min(mn);
         mx = wave_max(mx);
       }
+      FSTAMP(8);
       if (lane == 0) {
         const FinalizeArgs f{A.clamp_lo, A.clamp_hi, A.range_coef, nullptr, 0};
         SmqSmaqStats st;
@@ -476,6 +478,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
         else finalize_stats<false, TIN>(s1, s2, mn, mx, A.n, shift, false, f, &st);
         st.rng_offset = off0;
         sst = st;
+        FSTAMP(9);
         if (b == 0) *A.hdr = st;
       }
     }
@@ -528,10 +531,10 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
 #if SMQ_FUSED_TRACE
   if (A.trace && threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    A.trace[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+    A.trace[(size_t)blockIdx.x * 16 + 5] = __builtin_amdgcn_s_memrealtime();
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    A.trace[(size_t)blockIdx.x * 8 + 6] = xcc;
+    A.trace[(size_t)blockIdx.x * 16 + 6] = xcc;
   }
 #endif
   if (A.count) {  // outlier count for log_size (smart.py:184-188), spread over the slots
@@ -548,17 +551,11 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   // the last workgroup of its residue arrives on the top word; the last residue's advances the
   // generation and the stream and re-arms the arrival words. Every workgroup has read the
   // generation, the stream position and the granules before its add.
-  if (G > 1 && threadIdx.x == 0) {
-    const uint32_t s = (uint32_t)b & 7u;
-    const uint32_t n_s = ((uint32_t)G - 1u - s) / 8u + 1u;  // workgroups of residue s
-    if (arrive_tagged_finish(A.sub + s * kSubStride, gen, left_old) == n_s - 1u &&
-        arrive_tagged(A.left, gen) == (G < 8 ? (uint32_t)G : 8u) - 1u) {
-      st_sc1_u32(A.gen, gen + 1u);
-      if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
-      const unsigned long long armed = (unsigned long long)(gen + 1u) << 32;
-      st_sc1_u64(A.left, armed);
-      for (int r = 0; r < 8; ++r) st_sc1_u64(A.sub + r * kSubStride, armed);
-    }
+  if (G > 1 && threadIdx.x == 0 &&
+      arrive_sharded_finish(A.left, A.sub, kSubStride, b, G, gen, left_old)) {
+    st_sc1_u32(A.gen, gen + 1u);
+    if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
+    rearm_sharded(A.left, A.sub, kSubStride, gen + 1u);
   }
   FSTAMP(7);
 }
@@ -667,14 +664,10 @@ int launch_fused(const FusedCall& c, hipStream_t st) {
   F.poll_sleep = poll_sleep;
   F.trace = nullptr;
 #if SMQ_FUSED_TRACE
-  if (c.ws_bytes >= SmaqWsLayout::kTotal + 8 * 8 * (size_t)kSmallMaxG)
+  if (c.ws_bytes >= SmaqWsLayout::kTotal + 16 * 8 * (size_t)kSmallMaxG)
     F.trace = (uint64_t*)(base + SmaqWsLayout::kTotal);
 #endif
-  if (p->count_outliers &&
-      hipMemsetAsync(F.out_slots, 0, 8 * SMQ_WS_OUTLIER_SLOTS, st) != hipSuccess) {
-    set_error("hipMemsetAsync of the outlier slots failed");
-    return SMQ_ERR_LAUNCH;
-  }
+  if (p->count_outliers) fill_async(F.out_slots, 0ull, SMQ_WS_OUTLIER_SLOTS, st);
   const bool sr = p->stochastic_rounding != 0;
   if (c.dtype == SMQ_DTYPE_F32)
     return sr ? launch_fused_rm<kRoundHash, kF32>(F, g.V, st)

@@ -43,7 +43,6 @@ namespace smq {
 // sc0 sc1 nt output stores the whole step: 4K 79.9 us, 8K 82.3 us). A statistics workgroup takes
 // as many whole partials of its tensor as fit its chunk (at least one).
 constexpr int64_t kDefaultChunk = 4096;
-constexpr int64_t kDefaultStatsChunk = 65536;
 // workspace region of the single-tensor statistics launches of the large tensors
 constexpr size_t kBigWsBytes = (SmaqWsLayout::kTagCounters + 8 * SmaqWsLayout::kTagWords + 255) &
                                ~(size_t)255;
@@ -107,17 +106,15 @@ __device__ __forceinline__ float multi_range_coef(const MultiArgs& A, int t, int
   return c >= 0.0f ? c : 1.0f / sqrtf(2.0f * logf((float)n));
 }
 
-// Statistics of the tensors up to kSmallMaxN elements. Workgroup = partials [begin, end) of one
-// tensor in the single-tensor partition (smaq_small.h); a step = virtual lane t + 256 k of one
-// partial (its V groups), the next step's loads in flight while the current one is summed; the 16
-// virtual wave values of a partial are combined in small_combine's order (LDS, double-buffered by
-// partial parity). A tensor of one partial finalises in place; otherwise the partials are stored
-// (sc1) and the tensor's last workgroup reduces them in reduce_partials_w0's order — the
-// single-tensor call's statistics, bit for bit.
+// Statistics of the tensors up to kSmallMaxN elements: one 256-thread workgroup per record of
+// partials_per_wg partials of the single-tensor partition (smaq_small.h), in runs of 4 / V partials
+// at V <= 4 (all of a run's loads in flight at once; above, one partial with the loads a lane
+// ahead), four lanes per thread, the wave values and combine of smaq_stats_small_kernel. A tensor
+// of one partial finalises in place; otherwise the partials are stored and
+// smaq_multi_final_kernel reduces them.
 template <int TIN, bool RANGE>
 __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
-  __shared__ uint32_t slot;
-  __shared__ SmallWaveLds W[2];
+  __shared__ SmallWaveLds W[2][4];  // the runs' wave values, double-buffered
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // one snapshot + advance per call
     uint64_t o = 0;
     if (A.rng_ctr) {
@@ -130,66 +127,62 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   const void* __restrict__ x = ch.x;
   const int64_t n = ch.n;
   const SmallGeom g = small_geom(n);
-  const int V = g.V, G = g.G;
-  const int64_t nv = n >> 2;
+  const int G = g.G, V = g.V, end = (int)ch.end;
+  const int P = V <= 4 ? 4 / V : 1;  // partials per run
   const double shift = stats_shift<TIN>(x, n);
   const bool vec = ((uintptr_t)x & (TIN == kF32 ? 15u : 7u)) == 0;
-  const int p = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
-  const int w0 = (int)ch.begin;
-  const int steps = 4 * (int)(ch.end - ch.begin);
-  const FinalizeArgs fin{A.clamp_lo, A.clamp_hi, RANGE ? multi_range_coef(A, ch.tensor, n) : 0.0f};
-  auto load_step = [&](int s, float4 (&dst)[kSmallMaxV]) {
-    const int64_t base = (int64_t)(w0 + (s >> 2)) * V * kSmallT + threadIdx.x + kBlock * (s & 3);
-#pragma unroll
-    for (int u = 0; u < kSmallMaxV; ++u) {
-      const int64_t j = base + (int64_t)u * kSmallT;
-      if (u < V && j < nv) dst[u] = small_group<TIN>(x, j, vec);
+  StatPartial* const parts = A.partials + ch.first_chunk;
+  int par = 0;
+  for (int r0 = (int)ch.begin; r0 < end; r0 += P, par ^= 1) {
+    SmallWaveLds* Wr = W[par];
+    switch (V) {
+      case 1: small_waves_256_runs<TIN, 1, RANGE>(x, n, G, r0, vec, shift, Wr); break;
+      case 2: small_waves_256_runs<TIN, 2, RANGE>(x, n, G, r0, vec, shift, Wr); break;
+      case 3: small_waves_256_runs<TIN, 3, RANGE>(x, n, G, r0, vec, shift, Wr); break;
+      case 4: small_waves_256_runs<TIN, 4, RANGE>(x, n, G, r0, vec, shift, Wr); break;
+      default: small_waves_256<TIN>(x, n, V, G, r0, vec, shift, RANGE, Wr[0]);
     }
-  };
-  float4 cur[kSmallMaxV], nxt[kSmallMaxV];
-  load_step(0, cur);
-  for (int st = 0; st < steps; ++st) {
-    if (st + 1 < steps) load_step(st + 1, nxt);
-    const int w = w0 + (st >> 2), k = st & 3;
-    const StatAcc a = small_wave(small_lane_sum<TIN, kSmallMaxV>(x, n, V, G, w,
-                                                                 threadIdx.x + kBlock * k, cur,
-                                                                 shift));
-    SmallWaveLds& Wb = W[w & 1];
-    if (l == 0) {
-      Wb.s1[p + 4 * k] = a.s1;
-      Wb.s2[p + 4 * k] = a.s2;
-      Wb.mn[p + 4 * k] = a.mn;
-      Wb.mx[p + 4 * k] = a.mx;
+    // threads 0 .. P-1 store the run's partials while the others load the next run (whose wave
+    // values go to the other buffer; this one is rewritten only behind the next run's barrier,
+    // which they reach after these stores)
+    if (threadIdx.x < P && G > 1 && r0 + (int)threadIdx.x < end) {  // one partial per thread
+      const int k = r0 + (int)threadIdx.x;
+      const StatAcc r = small_combine(Wr[threadIdx.x]);
+      parts[k].s1 = r.s1;
+      parts[k].s2 = r.s2;
+      parts[k].mn = r.mn;
+      parts[k].mx = r.mx;
     }
-    if (k == 3) {
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const StatAcc r = small_combine(Wb);
-        if (G == 1) {
-          finalize_stats<RANGE, TIN>(r.s1, r.s2, r.mn, r.mx, n, shift, false, fin,
-                                     &A.stats[ch.tensor]);
-        } else {
-          StatPartial* q = A.partials + ch.first_chunk + w;
-          st_sc1_f64(&q->s1, r.s1);
-          st_sc1_f64(&q->s2, r.s2);
-          st_sc1_f32x2(&q->mn, r.mn, r.mx);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kSmallMaxV; ++u) cur[u] = nxt[u];
   }
-  if (G == 1) return;
-  const uint32_t prev = block_arrive_tagged(&A.counters[ch.tensor], A.tag.tag, &slot);
-  if (prev != (uint32_t)ch.n_chunks - 1) return;
-  if (threadIdx.x < kWave) {
-    double t1, t2;
-    float tmn, tmx;
-    reduce_partials_w0<true>(A.partials + ch.first_chunk, G, true, t1, t2, tmn, tmx);
-    if (threadIdx.x == 0) {
-      finalize_stats<RANGE, TIN>(t1, t2, tmn, tmx, n, shift, false, fin, &A.stats[ch.tensor]);
-      arrive_reset(&A.counters[ch.tensor], A.tag.next);
-    }
+  if (G == 1 && threadIdx.x == 0) {
+    const FinalizeArgs fin{A.clamp_lo, A.clamp_hi, RANGE ? multi_range_coef(A, ch.tensor, n) : 0.0f};
+    const StatAcc r = small_combine(W[0][0]);
+    finalize_stats<RANGE, TIN>(r.s1, r.s2, r.mn, r.mx, n, shift, false, fin, &A.stats[ch.tensor]);
+  }
+}
+
+// The totals of every small tensor of more than one partial (one workgroup per statistics record;
+// the record that starts the tensor's partials does the work): reduce_partials_w0's order over its
+// partials, stored by the statistics launch just before (plain loads: a launch boundary between),
+// then the finalisation — the single-tensor call's statistics, bit for bit. Its own launch (4.8 us
+// at C5): the last-arriving statistics workgroup reducing instead needs every workgroup's partial
+// stores released before its arrival — sc1 stores + atomic: 45.7 us for the sweep against 40.7 +
+// 4.8; plain stores + release fence: 111 us.
+template <int TIN, bool RANGE>
+__global__ __launch_bounds__(kWave) void smaq_multi_final_kernel(MultiArgs A) {
+  const ChunkDesc ch = A.stat_chunks[blockIdx.x];
+  if (ch.begin != 0) return;
+  const int64_t n = ch.n;
+  const int G = small_geom(n).G;
+  if (G == 1) return;  // finalised by the statistics launch
+  const double shift = stats_shift<TIN>(ch.x, n);
+  double t1, t2;
+  float tmn, tmx;
+  reduce_partials_w0<false>(A.partials + ch.first_chunk, G, true, t1, t2, tmn, tmx);
+  if (threadIdx.x == 0) {
+    const FinalizeArgs fin{A.clamp_lo, A.clamp_hi,
+                           RANGE ? multi_range_coef(A, ch.tensor, n) : 0.0f};
+    finalize_stats<RANGE, TIN>(t1, t2, tmn, tmx, n, shift, false, fin, &A.stats[ch.tensor]);
   }
 }
 
@@ -336,15 +329,6 @@ static int64_t chunk_elems() {
   return c;
 }
 
-static int64_t stats_chunk_elems() {
-  static const int64_t c = [] {
-    const char* e = knob_env("SMQ_MULTI_STATS_CHUNK");
-    const int64_t v = e ? atoll(e) : kDefaultStatsChunk;
-    return (v >= 4096 && v % 4096 == 0) ? v : kDefaultStatsChunk;
-  }();
-  return c;
-}
-
 static int64_t chunks_of(int64_t n, int64_t c) { return (n + c - 1) / c; }
 
 struct PlanSizes {
@@ -353,11 +337,24 @@ struct PlanSizes {
   bool big;  // a tensor above kSmallMaxN (its statistics: the single-tensor launch)
 };
 
-// Statistics workgroups of a small tensor: whole partials, as many as fit the statistics chunk.
+// Partials per statistics workgroup: stat_runs() runs of 4 / V partials at V <= 4 (a run: up to 16
+// float4 groups per thread, all in flight at once), else 1. Not a reduction-order parameter: every
+// partial is stored and reduced in one order whatever the grouping. (Measured at C5: a workgroup
+// walking 16 partials one 12-KB step of loads ahead at a time, 139 us; one run per workgroup with
+// the last arrival reducing, 45.7 us, ~11 of them the arrivals' contended round trips.)
+constexpr int kDefaultStatRuns = 1;
+
+static int stat_runs() {
+  static const int r = [] {  // measurement knob SMQ_MULTI_RUNS (experiment builds)
+    const char* e = knob_env("SMQ_MULTI_RUNS");
+    const int v = e ? atoi(e) : kDefaultStatRuns;
+    return v >= 1 && v <= 64 ? v : kDefaultStatRuns;
+  }();
+  return r;
+}
 static int64_t partials_per_wg(int64_t n) {
-  const SmallGeom g = small_geom(n);
-  const int64_t per = stats_chunk_elems() / ((int64_t)g.V * kSmallT * 4);
-  return per < 1 ? 1 : per;
+  const int V = small_geom(n).V;
+  return V <= 4 ? stat_runs() * (4 / V) : 1;
 }
 
 static bool plan_sizes(const int64_t* sizes, int count, PlanSizes* ps) {
@@ -476,7 +473,7 @@ int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_
   h->chunk = chunk_elems();
   h->n_stat_chunks = (int32_t)ps.n_stat_chunks;
   h->n_partials = (int32_t)ps.n_partials;
-  h->stat_chunk = stats_chunk_elems();
+  h->stat_chunk = 0;  // statistics records are runs of partials_per_wg partials
   memcpy(base + ps.hdr, descs, sizeof(SmqTensorDesc) * (size_t)count);
   fill_chunks((ChunkDesc*)(base + ps.hdr + ps.descs), descs, count, h->chunk);
   fill_stat_chunks((ChunkDesc*)(base + ps.hdr + ps.descs + ps.chunks), descs, count);
@@ -508,8 +505,12 @@ static int launch_multi(const MultiArgs& A, bool sampled, bool range, int n_stat
   } else if (range) {
     hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kBlock), 0,
                        st, A);
+    hipLaunchKernelGGL((smaq_multi_final_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kWave), 0,
+                       st, A);
   } else {
     hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, false>), dim3(n_stat_chunks), dim3(kBlock),
+                       0, st, A);
+    hipLaunchKernelGGL((smaq_multi_final_kernel<TIN, false>), dim3(n_stat_chunks), dim3(kWave),
                        0, st, A);
   }
   int rc = check_launch(sampled ? "smaq_multi_draw_kernel" : "smaq_multi_stats_kernel");

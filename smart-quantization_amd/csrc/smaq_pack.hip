@@ -1325,11 +1325,8 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.lds_words = PackLds::words(A.wm, we);
   const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
   const bool sr = p->stochastic_rounding != 0;
-  // the group sums start at zero
-  if (hipMemsetAsync(A.gsum, 0, 4 * (size_t)A.n_groups, st) != hipSuccess) {
-    set_error("compress: hipMemsetAsync failed");
-    return SMQ_ERR_LAUNCH;
-  }
+  // the group sums start at zero (fill_async: smq_common.h)
+  fill_async(A.gsum, 0u, A.n_groups, st);
   if (dtype == SMQ_DTYPE_F32) {
     if (sr) launch_pack<kRoundHash, kF32>(A, vec, ext, st);
     else launch_pack<kRoundTrunc, kF32>(A, vec, ext, st);

@@ -73,7 +73,7 @@ __device__ __forceinline__ void small_lane_load(const void* x, int64_t n, int V,
 }
 
 // The lane value of lane t of partial b from its groups g (entries past nv ignored).
-template <int TIN, int MAXV>
+template <int TIN, int MAXV, bool RANGE = true>
 __device__ __forceinline__ StatAcc small_lane_sum(const void* x, int64_t n, int V, int G, int b,
                                                   int t, const float4 (&g)[MAXV], double shift) {
   const int64_t nv = n >> 2;
@@ -83,12 +83,12 @@ __device__ __forceinline__ StatAcc small_lane_sum(const void* x, int64_t n, int 
   for (int u = 0; u < MAXV; ++u) {
     if (u >= V) break;
     if (base + (int64_t)u * kSmallT >= nv) continue;
-    c0.add<true>(g[u].x, shift);
-    c1.add<true>(g[u].y, shift);
-    c2.add<true>(g[u].z, shift);
-    c3.add<true>(g[u].w, shift);
+    c0.add<RANGE>(g[u].x, shift);
+    c1.add<RANGE>(g[u].y, shift);
+    c2.add<RANGE>(g[u].z, shift);
+    c3.add<RANGE>(g[u].w, shift);
   }
-  if (b == G - 1 && t < (int)(n & 3)) c0.add<true>(load1<TIN>(x, (nv << 2) + t), shift);
+  if (b == G - 1 && t < (int)(n & 3)) c0.add<RANGE>(load1<TIN>(x, (nv << 2) + t), shift);
   StatAcc r;
   r.s1 = (c0.s1 + c1.s1) + (c2.s1 + c3.s1);
   r.s2 = (c0.s2 + c1.s2) + (c2.s2 + c3.s2);
@@ -184,6 +184,88 @@ __device__ __forceinline__ StatAcc small_partial_256(const void* x, int64_t n, i
   const StatAcc r = small_combine(W);
   __syncthreads();
   return r;
+}
+
+// Partial b by a 256-thread workgroup with its loads in flight ahead of the sums (multi-tensor
+// statistics: one partial per workgroup): thread t = 64 p + l holds the lanes t + 256 k, k = 0..3,
+// i.e. lane l of the virtual waves p + 4k. V <= 2: all 4 V groups of a thread loaded at once;
+// else lane k + 1's groups load while lane k is summed. The wave values go to W; after the
+// barrier every thread may combine them (small_combine).
+template <int TIN>
+__device__ __forceinline__ void small_waves_256(const void* x, int64_t n, int V, int G, int b,
+                                                bool vec, double shift, bool range,
+                                                SmallWaveLds& W) {
+  const int p = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
+  constexpr int K = kSmallT / kBlock;
+  auto put = [&](int k, const StatAcc& a) {
+    const StatAcc w = small_wave(a, range);
+    if (l == 0) {
+      W.s1[p + 4 * k] = w.s1;
+      W.s2[p + 4 * k] = w.s2;
+      W.mn[p + 4 * k] = w.mn;
+      W.mx[p + 4 * k] = w.mx;
+    }
+  };
+  if (V <= 2) {
+    float4 g[K][2];
+#pragma unroll
+    for (int k = 0; k < K; ++k) small_lane_load<TIN, 2>(x, n, V, b, threadIdx.x + kBlock * k, vec, g[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      put(k, small_lane_sum<TIN, 2>(x, n, V, G, b, threadIdx.x + kBlock * k, g[k], shift));
+  } else {
+    float4 cur[kSmallMaxV], nxt[kSmallMaxV];
+    small_lane_load<TIN, kSmallMaxV>(x, n, V, b, threadIdx.x, vec, cur);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (k + 1 < K) small_lane_load<TIN, kSmallMaxV>(x, n, V, b, threadIdx.x + kBlock * (k + 1), vec, nxt);
+      put(k, small_lane_sum<TIN, kSmallMaxV>(x, n, V, G, b, threadIdx.x + kBlock * k, cur, shift));
+#pragma unroll
+      for (int u = 0; u < kSmallMaxV; ++u) cur[u] = nxt[u];
+    }
+  }
+  __syncthreads();
+}
+
+// The 4 / V partials b0 .. (those < G) of a tensor with V <= 4 groups per lane by a 256-thread
+// workgroup, every load of them in flight at once (<= 16 float4 groups per thread, coalesced:
+// thread tau holds the lanes tau + 256 k, i.e. lane tau % 64 of the virtual waves tau / 64 + 4k):
+// partial b0 + p's 16 wave values in W[p]; valid after the trailing barrier. (Measured at C5
+// against two mappings that hold a lane quad per thread so that one DPP pass serves four virtual
+// waves: with the quad loaded by the thread itself, 64-B lane-strided loads, 44 us; with the lane
+// values transposed through LDS, 41 us; this form, four butterflies per partial and wave, 35-37.)
+template <int TIN, int V, bool RANGE>
+__device__ __forceinline__ void small_waves_256_runs(const void* x, int64_t n, int G, int b0,
+                                                     bool vec, double shift, SmallWaveLds* W) {
+  static_assert(V >= 1 && V <= 4, "runs of partials: V <= 4");
+  constexpr int P = 4 / V, K = kSmallT / kBlock;
+  const int pw = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
+  float4 g[P][K][V];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    if (b0 + p >= G) break;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      small_lane_load<TIN, V>(x, n, V, b0 + p, threadIdx.x + kBlock * k, vec, g[p][k]);
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    if (b0 + p >= G) break;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const StatAcc w = small_wave(small_lane_sum<TIN, V, RANGE>(x, n, V, G, b0 + p,
+                                                                 threadIdx.x + kBlock * k, g[p][k],
+                                                                 shift),
+                                   RANGE);
+      if (l == 0) {
+        W[p].s1[pw + 4 * k] = w.s1;
+        W[p].s2[pw + 4 * k] = w.s2;
+        W[p].mn[pw + 4 * k] = w.mn;
+        W[p].mx[pw + 4 * k] = w.mx;
+      }
+    }
+  }
+  __syncthreads();
 }
 
 // Wave-0 reduction of g <= kSmallMaxG statistics partials in ONE fixed order: lane l sums

@@ -232,6 +232,21 @@ __device__ __forceinline__ uint32_t ld_sc1_u32(const void* p) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Fill of n words on the stream: the library's replacement of hipMemsetAsync. A captured small
+// memset node (4 bytes: the packer's group sums) was seen to leave its bytes unzeroed on hipGraph
+// replays interleaved with other device work (tests/test_gpu_packed.py, captured-graph test); a
+// kernel node has no such problem and costs the same dispatch.
+template <typename T>
+__global__ __launch_bounds__(256) void smq_fill_kernel(T* p, T v, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+template <typename T>
+static inline void fill_async(T* p, T v, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(smq_fill_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, v,
+                     (uint32_t)n);
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // outstanding global loads, stores and atomics (__syncthreads' workgroup fence also drains those).
 __device__ __forceinline__ void lds_barrier() {
@@ -279,12 +294,38 @@ __device__ __forceinline__ uint32_t arrive_tagged_finish(unsigned long long* ctr
 
 // arrive_tagged in two halves: the add (issue it early) and, where the count is needed, the check
 // of the word it returned (arrive_tagged_finish).
+// An atomic INC (with the bound 2^64 - 1: a plain +1), not an add: the atomic optimizer rewrites a
+// lane-divergent add into one wave-level add whose return value it broadcasts to the lanes right
+// away — an s_waitcnt vmcnt(0) at the issue, which would stall the issuing wave for the whole
+// contended round trip. It leaves inc alone, so the value is waited for only where it is used.
 __device__ __forceinline__ unsigned long long arrive_tagged_issue(unsigned long long* ctr) {
-  return __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  typedef __attribute__((address_space(1))) volatile unsigned long gu64v;
+  return __builtin_amdgcn_atomic_inc64((gu64v*)(ctr), ~0ul,
+                                       __ATOMIC_RELAXED, "agent");
 }
 
 __device__ __forceinline__ uint32_t arrive_tagged(unsigned long long* ctr, uint32_t tag) {
   return arrive_tagged_finish(ctr, tag, arrive_tagged_issue(ctr));
+}
+
+// Arrivals of G workgroups sharded by residue: workgroup b adds to sub[(b & 7) * stride] (issued
+// with arrive_tagged_issue, `old` its return), the last of each residue adds to `top`. Same-address
+// atomics serialise at ~12 ns each (MI355X_MICROARCH.md, fanin): eight words of <= 32 arrivals and
+// one of <= 8 instead of one word of 256. True for the call's last arrival.
+__device__ __forceinline__ bool arrive_sharded_finish(unsigned long long* top,
+                                                      unsigned long long* sub, int stride, int b,
+                                                      int G, uint32_t tag, unsigned long long old) {
+  const uint32_t s = (uint32_t)b & 7u;
+  const uint32_t n_s = ((uint32_t)G - 1u - s) / 8u + 1u;  // workgroups of residue s
+  return arrive_tagged_finish(sub + s * stride, tag, old) == n_s - 1u &&
+         arrive_tagged(top, tag) == (G < 8 ? (uint32_t)G : 8u) - 1u;
+}
+__device__ __forceinline__ void rearm_sharded(unsigned long long* top, unsigned long long* sub,
+                                              int stride, uint32_t next_tag) {
+  const unsigned long long armed = (unsigned long long)next_tag << 32;
+  st_sc1_u64(top, armed);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) st_sc1_u64(sub + r * stride, armed);
 }
 
 // The same for a workgroup whose thread 0 stored a partial with st_sc1_*: drain, arrive, and hand

@@ -183,21 +183,22 @@ def test_validation_errors_without_device():
 def test_multi_plan_layout():
     """Plan = header, descriptors, the apply map (4096-element chunks) and the statistics map: per
     tensor up to 8,388,611 elements, runs of whole partials of the single-tensor partition
-    (csrc/smaq_small.h: V groups of 4 per lane of 1024, G partials), at most 65536 elements per
-    workgroup; larger tensors have no record (their statistics are the single-tensor launch)."""
+    (csrc/smaq_small.h: V groups of 4 per lane of 1024, G partials), one run of 4 / V partials
+    (V <= 4, else 1 partial) per statistics workgroup; larger tensors have no record (their statistics are the
+    single-tensor launch)."""
     from smart_compress_amd import _native as N
 
     lib = N.lib()
-    C, S = 4096, 65536  # default apply / statistics chunks (csrc/smaq_multi.hip)
-    sizes = [10, C, C + 1, 3 * C + 5, S + 1, 300000, 9 << 20]
+    C = 4096  # default apply chunk (csrc/smaq_multi.hip)
+    sizes = [10, C, C + 1, 3 * C + 5, 65537, 300000, 9 << 20]
     count = len(sizes)
     arr = (ctypes.c_int64 * count)(*sizes)
     nbytes = lib.smq_smaq_multi_plan_bytes(arr, count)
     chunks = [-(-n // C) for n in sizes]
     nl = chunks[4]
-    # partials G = ceil((n // 4) / 1024) (V = 1 below 2^20 groups); 16 partials per workgroup
+    # partials G = ceil((n // 4) / 1024) (V = 1 below 2^20 groups); one run of 4 per workgroup
     parts = [1, 1, 1, 4, 16, 74]
-    wgs = [1, 1, 1, 1, 1, 5]
+    wgs = [-(-g // 4) for g in parts]
     dbytes = ((40 * count + 31) // 32) * 32
     assert nbytes == 32 + dbytes + 64 * (sum(chunks) + sum(wgs))
     descs = (N.SmqTensorDesc * count)()
@@ -214,7 +215,7 @@ def test_multi_plan_layout():
     assert list(raw[:8].view(np.int32)) == [count, sum(chunks)]
     assert int(raw[8:16].view(np.int64)[0]) == C
     assert list(raw[16:24].view(np.int32)) == [sum(wgs), sum(parts)]
-    assert int(raw[24:32].view(np.int64)[0]) == S
+    assert int(raw[24:32].view(np.int64)[0]) == 0
     rec = raw[32 + dbytes:].reshape(-1, 64)
     assert rec.shape[0] == sum(chunks) + sum(wgs)
     q = rec[:, :48].copy().view(np.int64)  # x, y, n, begin, end, rng_offset
@@ -228,11 +229,13 @@ def test_multi_plan_layout():
     assert list(q[a, 4])[:8] == [10, C, C, C + 1, C, 2 * C, 3 * C, 3 * C + 5]
     assert list(q[a, 5])[:5] == [0, 10, 10 + C, 10 + C, 10 + 2 * C + 1]
     b = slice(sum(chunks), None)  # the statistics map: partial runs [begin, end)
-    assert list(i32[b, 0]) == [0, 1, 2, 3, 4] + [5] * 5
-    assert list(i32[b, 1]) == [0, 1, 2, 3, 7] + [23] * 5  # first partial of the tensor
-    assert list(i32[b, 2]) == [1, 1, 1, 1, 1] + [5] * 5
-    assert list(q[b, 3]) == [0, 0, 0, 0, 0, 0, 16, 32, 48, 64]
-    assert list(q[b, 4]) == [1, 1, 1, 4, 16, 16, 32, 48, 64, 74]
+    tens = [t for t, w in enumerate(wgs) for _ in range(w)]
+    first = [sum(parts[:t]) for t in tens]  # first partial of the tensor
+    assert list(i32[b, 0]) == tens
+    assert list(i32[b, 1]) == first
+    assert list(i32[b, 2]) == [wgs[t] for t in tens]
+    assert list(q[b, 3]) == [4 * c for w in wgs for c in range(w)]
+    assert list(q[b, 4]) == [min(4 * c + 4, g) for g, w in zip(parts, wgs) for c in range(w)]
     assert lib.smq_smaq_multi_workspace_bytes(arr, count) >= 64 * count + 32 * sum(parts)
     descs[1].n = 0
     assert lib.smq_smaq_multi_plan_build(descs, count, host, nbytes) == -1
@@ -258,7 +261,7 @@ def test_integration_doc_binding_matches_the_library_struct():
 
 
 def test_shipped_library_reads_no_environment():
-    """The measurement knobs (SMQ_STATS_GRID, SMQ_DEFER_MAX_N, SMQ_MULTI_STATS_CHUNK, ...) change
+    """The measurement knobs (SMQ_STATS_GRID, SMQ_DEFER_MAX_N, SMQ_MULTI_RUNS, ...) change
     launch shapes and reduction orders; the shipped library is built without them (smq_common.h
     knob_env): it imports no getenv and holds none of their names."""
     import subprocess
@@ -270,5 +273,5 @@ def test_shipped_library_reads_no_environment():
     assert "getenv" not in syms
     blob = open(N.LIB_PATH, "rb").read()
     for knob in (b"SMQ_STATS_GRID", b"SMQ_STATS_PER_WG", b"SMQ_DEFER_MAX_N",
-                 b"SMQ_MULTI_STATS_CHUNK", b"SMQ_MULTI_CHUNK", b"SMQ_FUSED", b"SMQ_CPU_THREADS"):
+                 b"SMQ_MULTI_RUNS", b"SMQ_MULTI_CHUNK", b"SMQ_FUSED", b"SMQ_CPU_THREADS"):
         assert knob not in blob, knob

@@ -164,10 +164,11 @@ def test_multi_modes_equal_single_calls(mode, dt):
 @pytest.mark.parametrize("dt", ["f32", "f16", "bf16"])
 def test_multi_full_stats_equal_single_calls(mode, dt):
     """Full statistics (the default): every size class — the small partition with one partial,
-    several partials in one workgroup, several workgroups per tensor (300,000 and 3M elements),
-    V = 8 (8,388,611) and tensors above it (9M: the deferred grid; 13M: 512 workgroups), whose
-    statistics are the single-tensor launch itself — equal the per-tensor SmartFP calls at the
-    same stream offsets, outputs and statistics bit for bit."""
+    runs of 4 / V partials per workgroup at V = 1 .. 4 (300,000; 1.18M; ResNet-34's 2,359,296;
+    3M), one partial per workgroup with the lane-ahead loads (V = 5: 5M; V = 8: 8,388,611) and
+    tensors above it (9M: the deferred grid; 13M: 512 workgroups), whose statistics are the
+    single-tensor launch itself — equal the per-tensor SmartFP calls at the same stream offsets,
+    outputs and statistics bit for bit."""
     from smart_compress_amd import _native as N
     from smart_compress_amd.compress.smart import SmartFP
     from smart_compress_amd.util.pytorch.multi import SmaqMulti
@@ -175,7 +176,8 @@ def test_multi_full_stats_equal_single_calls(mode, dt):
     tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[dt]
     hp = smaq_hparams(precision=16 if dt == "f16" else 32, **mode)
     gen = torch.Generator(device="cuda").manual_seed(31)
-    sizes = [5, 4099, 65537, 300000, 3 * (1 << 20) + 5, 8388611, 9 << 20, 13 << 20]
+    sizes = [5, 4099, 65537, 300000, 1179655, 2359296, 3 * (1 << 20) + 5, 5 * (1 << 20) + 1,
+             8388611, 9 << 20, 13 << 20]
     xs = [(torch.randn(n, generator=gen, device="cuda") * (0.5 + i)).to(tdt)
           for i, n in enumerate(sizes)]
     m = SmaqMulti(hp, seed=12)

@@ -29,7 +29,7 @@ def main():
     for n in SIZES:
         xs = [torch.randn(n, device="cuda") for _ in range(8)]
         ys = [torch.empty(n, device="cuda") for _ in range(8)]
-        nb = lib.smq_smaq_workspace_bytes(n) + 8 * 8 * 256
+        nb = lib.smq_smaq_workspace_bytes(n) + 16 * 8 * 256
         wss = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(CALLS)]
         p = codec._params(n, False)
         st = torch.cuda.current_stream().cuda_stream
@@ -40,7 +40,7 @@ def main():
                                                nb, st), "roundtrip")
             torch.cuda.synchronize()
         off = lib.smq_smaq_workspace_bytes(n)
-        tr = [w[off:off + 8 * 8 * 256].cpu().numpy().view(np.uint64).reshape(256, 8) for w in wss]
+        tr = [w[off:off + 16 * 8 * 256].cpu().numpy().view(np.uint64).reshape(256, 16) for w in wss]
         G = int(np.count_nonzero(tr[0][:, 0]))
         rows = []
         for i in range(CALLS - 1):
@@ -51,10 +51,12 @@ def main():
             gap = (tr[i + 1][:G, 0].astype(np.int64).min() - end) / 100.0
             rows.append([np.median(rel[:, k]) for k in range(6)] + [
                 (end - t0) / 100.0, gap, rel[:, 0].max(), rel[:, 1].max(), rel[:, 2].max(),
-                np.median(rel[:, 7])])
+                np.median(rel[:, 7]), np.median(rel[:, 10]), np.median(rel[:, 8]),
+                np.median(rel[:, 9])])
         m = np.median(np.array(rows), axis=0)
         print(f"n={n} G={G} start_spread={m[8]:.2f} published={m[1]:.2f} (max {m[9]:.2f}) "
-              f"gathered={m[2]:.2f} (max {m[10]:.2f}) final={m[3]:.2f} transformed={m[4]:.2f} "
+              f"gathered={m[2]:.2f} (max {m[10]:.2f}) [summed {m[12]:.2f} reduced {m[13]:.2f} "
+              f"finalised {m[14]:.2f}] final={m[3]:.2f} transformed={m[4]:.2f} "
               f"drained={m[5]:.2f} arrived={m[11]:.2f} last={m[6]:.2f} gap_to_next={m[7]:.2f} "
               f"(us, medians over {len(rows)} calls)", flush=True)
 
