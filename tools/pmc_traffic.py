@@ -37,6 +37,10 @@ SHORT = {
     "smaq_pack_scan_kernel": "smaq_pack_scan_kernel",
     "smaq_draw_stats_kernel": "smaq_draw_stats_kernel",
     "smaq_multi_draw_kernel": "smaq_multi_draw_kernel",
+    "smaq_multi_final_kernel": "smaq_multi_final_kernel",
+    "smaq_fused_kernel": "smaq_fused_kernel",
+    "smaq_stats_small_kernel": "smaq_stats_small_kernel",
+    "smq_fill_kernel": "smq_fill_kernel",
 }
 
 
