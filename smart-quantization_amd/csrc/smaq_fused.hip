@@ -308,7 +308,9 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   __shared__ SmqSmaqStats sst;
   __shared__ float4 u0lds[V <= 4 ? V : 1][kWave];  // wave 0's rounding draws (PRE)
   __shared__ uint32_t sh_cnt[kSmallWaves];
-  __shared__ uint32_t pw[kSmallMaxG * kFusedWords];  // the gathered partials' words (k * words + c)
+  // the gathered partials' words, word c of partial k = 4l + q at (4c + q) * 64 + l: the reduction's
+  // lane l reads them bank-conflict free
+  __shared__ uint32_t pw[kSmallMaxG * kFusedWords];
   __shared__ int smiss[kSmallWaves];
   const int b = blockIdx.x, G = A.G;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
@@ -382,6 +384,13 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
         A.gran + (size_t)(b % kFusedRep) * kSmallMaxG * kFusedWords;
     const int i0 = threadIdx.x, i1 = threadIdx.x + kSmallT;
     uint32_t miss_bits = (i0 < total ? 1u : 0u) | (i1 < total ? 2u : 0u);
+    // partial and word of granule i (i / words without a division: i < 1536), and its LDS slot
+    auto part_of = [&](int i) { return words == 4 ? i >> 2 : (i * 43691) >> 18; };
+    auto slot_of = [&](int i) {
+      const int k = part_of(i), c = i - k * words;
+      return ((c << 2) + (k & 3)) * kWave + (k >> 2);
+    };
+    const int sl0 = slot_of(i0), sl1 = slot_of(i1);
     bool stealing = false;
     for (;;) {
       const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -391,11 +400,11 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
         const unsigned long long g1 = (miss_bits & 2u) ? ld_sc1_u64(rep + i1) : 0ull;
         if ((miss_bits & 1u) && (uint32_t)(g0 >> 32) == epoch) {
           miss_bits &= ~1u;
-          pw[i0] = (uint32_t)g0;
+          pw[sl0] = (uint32_t)g0;
         }
         if ((miss_bits & 2u) && (uint32_t)(g1 >> 32) == epoch) {
           miss_bits &= ~2u;
-          pw[i1] = (uint32_t)g1;
+          pw[sl1] = (uint32_t)g1;
         }
         if (__all(miss_bits == 0u) || stealing) break;
         if ((++polls & 7) != 0) {
@@ -405,13 +414,12 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
         if (__builtin_amdgcn_s_memrealtime() - t_start > steal_ticks) break;
         fused_sleep(A.poll_sleep);
       }
-      // the first missing partial after b (cyclically); i / words without a division (i < 1536)
+      // the first missing partial after b (cyclically)
       int miss = INT_MAX;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         if (!((miss_bits >> h) & 1u)) continue;
-        const int i = h ? i1 : i0;
-        const int k = words == 4 ? i >> 2 : (i * 43691) >> 18;
+        const int k = part_of(h ? i1 : i0);
         int d = k - b;
         d += d < 0 ? G : 0;
         miss = min(miss, d);
@@ -436,7 +444,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
         const int i = h ? i1 : i0;
         const int c = i - k * words;
         if (((miss_bits >> h) & 1u) && c >= 0 && c < words) {
-          pw[i] = partial_word(pk_acc, c);
+          pw[h ? sl1 : sl0] = partial_word(pk_acc, c);
           miss_bits &= ~(1u << h);
         }
       }
@@ -453,22 +461,21 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       float mn = INFINITY, mx = -INFINITY;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int k = 4 * lane + q;
-        if (k >= G) continue;
-        const uint32_t* w = pw + k * words;
-        s1 += __builtin_bit_cast(double, ((uint64_t)w[1] << 32) | w[0]);
-        s2 += __builtin_bit_cast(double, ((uint64_t)w[3] << 32) | w[2]);
+        if (4 * lane + q >= G) continue;
+        const uint32_t* w = pw + q * kWave + lane;  // word c at w[4c * 64]
+        s1 += __builtin_bit_cast(double, ((uint64_t)w[4 * kWave] << 32) | w[0]);
+        s2 += __builtin_bit_cast(double, ((uint64_t)w[12 * kWave] << 32) | w[8 * kWave]);
         if (A.range) {
-          mn = fminf(mn, __builtin_bit_cast(float, w[4]));
-          mx = fmaxf(mx, __builtin_bit_cast(float, w[5]));
+          mn = fminf(mn, __builtin_bit_cast(float, w[16 * kWave]));
+          mx = fmaxf(mx, __builtin_bit_cast(float, w[20 * kWave]));
         }
       }
       FSTAMP(10);
       s1 = wave_sum_asc(s1);
       s2 = wave_sum_asc(s2);
       if (A.range) {
-        mn = wave_min(mn);
-        mx = wave_max(mx);
+        mn = wave_min_dpp(mn);
+        mx = wave_max_dpp(mx);
       }
       FSTAMP(8);
       if (lane == 0) {

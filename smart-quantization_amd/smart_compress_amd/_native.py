@@ -336,6 +336,34 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+_fast = None
+_fast_tried = False
+
+
+def fast():
+    """The CPython fast-call binding of smq_smaq_roundtrip (csrc/pyfast.cpp) built next to the
+    library being used, or None (an experiment library elsewhere, SMQ_LIB: then ctypes). It calls
+    the same libsmq.so (rpath $ORIGIN = the directory of LIB_PATH), only without ctypes' ~4 us of
+    argument conversion per call."""
+    global _fast, _fast_tried
+    if _fast_tried:
+        return _fast
+    lib()  # the ABI check, and the library every entry point shares
+    import importlib.machinery
+    import importlib.util
+    import sysconfig
+
+    path = os.path.join(os.path.dirname(LIB_PATH), "_smqfast" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if os.path.exists(path):
+        loader = importlib.machinery.ExtensionFileLoader("_smqfast", path)
+        spec = importlib.util.spec_from_file_location("_smqfast", path, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _fast = mod
+    _fast_tried = True
+    return _fast
+
+
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib().smq_last_error().decode(errors="replace")

@@ -21,6 +21,7 @@ torch's default generator at construction (so ``torch.manual_seed`` makes runs r
 ``hparams.smq_seed``; the offset advances by the elements consumed per call.
 """
 
+import ctypes
 from argparse import ArgumentParser, Namespace
 from typing import Optional, Tuple
 
@@ -28,7 +29,7 @@ import numpy as np
 import torch
 
 from .. import _native as N
-from ..util.globals import profile
+from ..util.globals import Globals, profile
 from .base import CompressionAlgorithmBase
 
 _F32 = {}
@@ -209,7 +210,6 @@ class SmartFP(CompressionAlgorithmBase):
         return gamma, beta  # keep alive until the launch is enqueued
 
     # -- call --------------------------------------------------------------------------------------
-    @torch.no_grad()
     def __call__(
         self,
         data: torch.Tensor,
@@ -218,6 +218,36 @@ class SmartFP(CompressionAlgorithmBase):
         batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
         **_,
     ):
+        # The hot path — a ROCm fp32 / fp16 / bf16 tensor of at least min_size elements, no BN
+        # term, no ratio logging, no profiler: the library writes a fresh output buffer and no
+        # autograd op runs, so there is no grad-mode switch (torch.no_grad costs ~1.5 us), and the
+        # launch goes through the fast-call binding (ctypes' argument conversion costs ~4 us).
+        # An eager training step that compresses every layer is bound by this host time
+        # (bench.py --config autograd_resnet34). Everything else: _call, under torch.no_grad as
+        # smart.py:110.
+        hp = self.hparams
+        fast = N._fast if N._fast_tried else N.fast()
+        if (fast is not None and data.is_cuda and not hp.measure_compression_ratio
+                and Globals.profiler is None and self._trace is None
+                and (batch_norm_stats is None or not hp.use_batch_norm)):
+            code = N.DTYPE_CODES.get(data.dtype)
+            numel = data.numel()
+            if (code is not None and numel >= hp.min_size and not hp.use_sample_stats
+                    and (data.dtype != torch.float16 or hp.precision == 16)):
+                x = data if data.is_contiguous() else data.detach().contiguous()
+                y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+                p = self._params(numel, all_positive, x.dtype, x.device)
+                st = N.stream_ptr(x.device)
+                ws = N.workspace("smaq", x.device, self.workspace_bytes(numel), st)
+                rc = fast.smaq_roundtrip(x.data_ptr(), code, y.data_ptr(), numel,
+                                         ctypes.addressof(p), ws.data_ptr(), ws.numel(), st)
+                if rc:
+                    N.check(rc, "smq_smaq_roundtrip")
+                return y
+        return self._call(data, tag, all_positive, batch_norm_stats)
+
+    @torch.no_grad()
+    def _call(self, data, tag, all_positive, batch_norm_stats):
         with profile("smaq"):
             hp = self.hparams
             numel = data.numel()

@@ -275,3 +275,17 @@ def test_shipped_library_reads_no_environment():
     for knob in (b"SMQ_STATS_GRID", b"SMQ_STATS_PER_WG", b"SMQ_DEFER_MAX_N",
                  b"SMQ_MULTI_RUNS", b"SMQ_MULTI_CHUNK", b"SMQ_FUSED", b"SMQ_CPU_THREADS"):
         assert knob not in blob, knob
+
+
+def test_fastcall_binding_loads_next_to_the_library():
+    """The CPython fast-call binding of smq_smaq_roundtrip (csrc/pyfast.cpp) is built next to
+    libsmq.so and calls that same library: a bad argument count raises, and a call with a NULL
+    params block returns the library's status (no launch: the library validates first)."""
+    from smart_compress_amd import _native as N
+
+    f = N.fast()
+    assert f is not None and callable(f.smaq_roundtrip)
+    with pytest.raises(TypeError):
+        f.smaq_roundtrip(1, 2, 3)
+    rc = f.smaq_roundtrip(0, 0, 0, 16, 0, 0, 0, 0)
+    assert rc != 0 and N.lib().smq_last_error()
