@@ -852,7 +852,7 @@ __device__ __forceinline__ void s2f_hash4(uint32_t key, uint64_t c, uint32_t r[4
 // workgroups sweeping the same 6 KB queue on the few memory channels that hold it (first poll pass
 // 2.1 us); replica b % 8 spreads the readers over 8x the channels.
 __device__ void s2f_publish(double s, float m, const S2FArgs& A, int k, uint32_t epoch,
-                            double* shs, float* shm) {
+                            double* shs, float* shm, uint32_t* gw = nullptr) {
   constexpr int W = kS2FT / kWave;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   s = wave_sum_asc(s);
@@ -875,6 +875,7 @@ __device__ void s2f_publish(double s, float m, const S2FArgs& A, int k, uint32_t
     const uint32_t word = c == 0 ? (uint32_t)sb
                                  : (c == 1 ? (uint32_t)(sb >> 32) : __builtin_bit_cast(uint32_t, M));
     st_sc1_u64(&A.gran[(r * 3 + c) * kS2FMaxG + k], ((unsigned long long)epoch << 32) | word);
+    if (gw && lane < 3) gw[c * kS2FMaxG + k] = word;  // the gather's LDS copy (a stolen partial)
   }
 }
 
@@ -884,8 +885,9 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
   __shared__ double shs[kS2FT / kWave];
   __shared__ float shm[kS2FT / kWave];
   __shared__ SmqS2fp8Stats sst;
-  __shared__ int sflag;
   __shared__ uint4 r0lds[kS2FMaxV][kWave];  // wave 0's rounding words, computed by waves 1..V
+  __shared__ uint32_t gw[3 * kS2FMaxG];      // the gathered words: granule c of partial k at c*256+k
+  __shared__ int smiss[kS2FT / kWave];
   const int b = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int64_t base = (int64_t)b * A.V * kS2FT + threadIdx.x;
@@ -940,69 +942,70 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
       r0lds[u][lane] = make_uint4(r0[0], r0[1], r0[2], r0[3]);
     }
   }
-  // wave 0 gathers the G partials (lane l: partials l + 64q) from replica b % 8 until every granule
-  // carries the epoch
+  // every thread t < 768 gathers word t of replica b % 8 (granule c = t / 256 of partial
+  // k = t % 256: each wave load reads 512 consecutive bytes) until every granule carries the epoch;
+  // accepted words go to LDS (gw), then wave 0 takes its lanes' four partials from there
   const unsigned long long* rep = A.gran + (size_t)(b % kS2FRep) * 3 * kS2FMaxG;
-  double ps[4] = {0.0, 0.0, 0.0, 0.0};
-  float pm[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  const int gk = threadIdx.x & (kS2FMaxG - 1);
+  uint32_t miss = (threadIdx.x < 3 * kS2FMaxG && gk < A.G) ? 1u : 0u;
   int n_stolen = 0;
-  if (wave == 0) {
-    uint32_t lo[4], hi[4], mx[4];
-    uint32_t have = 0;  // bit 3q + c: granule c of partial l + 64q holds the epoch
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (lane + 64 * q >= A.G) have |= 7u << (3 * q);
+  bool stealing = false;
+  for (;;) {
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t polls = 0;
     for (;;) {
-      // every granule load of the pass in flight at once, one wait
-      unsigned long long g[4][3];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          g[q][c] = lane + 64 * q < A.G ? ld_sc1_u64(&rep[c * kS2FMaxG + lane + 64 * q]) : 0ull;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          if ((uint32_t)(g[q][c] >> 32) != epoch || (have & (1u << (3 * q + c)))) continue;
-          have |= 1u << (3 * q + c);
-          const uint32_t w = (uint32_t)g[q][c];
-          if (c == 0) lo[q] = w;
-          else if (c == 1) hi[q] = w;
-          else mx[q] = w;
-        }
+      const unsigned long long g = miss ? ld_sc1_u64(rep + threadIdx.x) : 0ull;
+      if (miss && (uint32_t)(g >> 32) == epoch) {
+        miss = 0u;
+        gw[threadIdx.x] = (uint32_t)g;
       }
-      const bool all = __all(have == 0xfffu);
-      if (polls == 0) s2f_stamp(A, 11);
-      if (all) break;
+      if (polls == 0 && threadIdx.x == 0) s2f_stamp(A, 11);
+      if (__all(miss == 0u) || stealing) break;
       if ((++polls & 7) != 0) {
         __builtin_amdgcn_s_sleep(2);
         continue;
       }
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      if (now - t_start > steal_ticks) break;  // compute the missing partials below
+      if (__builtin_amdgcn_s_memrealtime() - t_start > steal_ticks) break;
       __builtin_amdgcn_s_sleep(2);
     }
+    // the first missing partial after b (cyclically)
+    int d = INT_MAX;
+    if (miss) {
+      d = gk - b;
+      d += d < 0 ? A.G : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = min(d, __shfl_xor(d, o, kWave));
+    if (lane == 0) smiss[wave] = d;
+    lds_barrier();
+    int m = smiss[0];
+#pragma unroll
+    for (int w = 1; w < kS2FT / kWave; ++w) m = min(m, smiss[w]);
+    if (m == INT_MAX) break;
+    // the patience ran out: the whole workgroup computes partial (m + b) % G from memory and
+    // publishes it (its words also go straight to LDS, so no poll waits for them)
+    const int k = m + b < A.G ? m + b : m + b - A.G;
+    stealing = true;
+    lds_barrier();
+    double s;
+    float mm;
+    s2f_lane_sums(nullptr, A, k, s, mm);
+    s2f_publish(s, mm, A, k, epoch, shs, shm, gw);
+    ++n_stolen;
+    lds_barrier();
+    if (miss && gk == k) miss = 0u;
+  }
+  double ps[4] = {0.0, 0.0, 0.0, 0.0};
+  float pm[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  if (wave == 0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (lane + 64 * q < A.G && (have & (7u << (3 * q))) == (7u << (3 * q))) {
-        ps[q] = __builtin_bit_cast(double, ((uint64_t)hi[q] << 32) | lo[q]);
-        pm[q] = __builtin_bit_cast(float, mx[q]);
+      const int k = lane + 64 * q;
+      if (k < A.G) {
+        ps[q] = __builtin_bit_cast(double, ((uint64_t)gw[kS2FMaxG + k] << 32) | gw[k]);
+        pm[q] = __builtin_bit_cast(float, gw[2 * kS2FMaxG + k]);
       }
     }
-    // first missing partial after b (cyclically), or -1 when complete
-    int miss = INT_MAX;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if ((have & (7u << (3 * q))) != (7u << (3 * q))) miss = min(miss, (lane + 64 * q - b + A.G) % A.G);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, kWave));
-    if (lane == 0) sflag = miss == INT_MAX ? -1 : (miss + b) % A.G;
-  }
-  lds_barrier();
-  if (wave == 0) {
 #pragma unroll
     for (int u = 0; u < kS2FMaxV; ++u) {
       if (u < V) {
@@ -1013,43 +1016,6 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
         rw[u][3] = w.w;
       }
     }
-  }
-  // missing partials after the patience ran out: the whole workgroup computes them one by one from
-  // memory; after each, wave 0 re-reads every granule and names the next missing one
-  while (sflag >= 0) {
-    const int k = sflag;
-    lds_barrier();
-    double s;
-    float m;
-    s2f_lane_sums(nullptr, A, k, s, m);
-    s2f_publish(s, m, A, k, epoch, shs, shm);
-    ++n_stolen;
-    if (wave == 0) {  // next missing partial, or -1 when all are present
-      int miss = INT_MAX;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int kk = lane + 64 * q;
-        if (kk >= A.G) continue;
-        bool ok = true;
-        uint32_t wd[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const unsigned long long g = ld_sc1_u64(&rep[c * kS2FMaxG + kk]);
-          ok &= (uint32_t)(g >> 32) == epoch;
-          wd[c] = (uint32_t)g;
-        }
-        if (ok) {
-          ps[q] = __builtin_bit_cast(double, ((uint64_t)wd[1] << 32) | wd[0]);
-          pm[q] = __builtin_bit_cast(float, wd[2]);
-        } else {
-          miss = min(miss, (kk - b + A.G) % A.G);
-        }
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) miss = min(miss, __shfl_xor(miss, o, kWave));
-      if (lane == 0) sflag = miss == INT_MAX ? -1 : (miss + b) % A.G;
-    }
-    lds_barrier();
   }
   s2f_stamp(A, 3);
   // count this workgroup past the wait now (on its residue's word); the returned word is looked at

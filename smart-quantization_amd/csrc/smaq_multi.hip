@@ -106,15 +106,14 @@ __device__ __forceinline__ float multi_range_coef(const MultiArgs& A, int t, int
   return c >= 0.0f ? c : 1.0f / sqrtf(2.0f * logf((float)n));
 }
 
-// Statistics of the tensors up to kSmallMaxN elements: one 256-thread workgroup per record of
-// partials_per_wg partials of the single-tensor partition (smaq_small.h), in runs of 4 / V partials
-// at V <= 4 (all of a run's loads in flight at once; above, one partial with the loads a lane
-// ahead), four lanes per thread, the wave values and combine of smaq_stats_small_kernel. A tensor
-// of one partial finalises in place; otherwise the partials are stored and
+// Statistics of the tensors up to kSmallMaxN elements: one 1024-thread workgroup (two per CU) per
+// record of partials_per_wg partials of the single-tensor partition (smaq_small.h): the native
+// partial shape, smaq_stats_small_kernel's lane function, wave butterfly and combine. A tensor of
+// one partial finalises in place; otherwise the partials are stored (plain) and
 // smaq_multi_final_kernel reduces them.
 template <int TIN, bool RANGE>
-__global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
-  __shared__ SmallWaveLds W[2][4];  // the runs' wave values, double-buffered
+__global__ __launch_bounds__(kSmallT, 8) void smaq_multi_stats_kernel(MultiArgs A) {
+  __shared__ SmallWaveLds W[8];
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // one snapshot + advance per call
     uint64_t o = 0;
     if (A.rng_ctr) {
@@ -127,47 +126,45 @@ __global__ __launch_bounds__(kBlock) void smaq_multi_stats_kernel(MultiArgs A) {
   const void* __restrict__ x = ch.x;
   const int64_t n = ch.n;
   const SmallGeom g = small_geom(n);
-  const int G = g.G, V = g.V, end = (int)ch.end;
-  const int P = V <= 4 ? 4 / V : 1;  // partials per run
+  const int G = g.G, b0 = (int)ch.begin, end = (int)ch.end;
   const double shift = stats_shift<TIN>(x, n);
   const bool vec = ((uintptr_t)x & (TIN == kF32 ? 15u : 7u)) == 0;
-  StatPartial* const parts = A.partials + ch.first_chunk;
-  int par = 0;
-  for (int r0 = (int)ch.begin; r0 < end; r0 += P, par ^= 1) {
-    SmallWaveLds* Wr = W[par];
-    switch (V) {
-      case 1: small_waves_256_runs<TIN, 1, RANGE>(x, n, G, r0, vec, shift, Wr); break;
-      case 2: small_waves_256_runs<TIN, 2, RANGE>(x, n, G, r0, vec, shift, Wr); break;
-      case 3: small_waves_256_runs<TIN, 3, RANGE>(x, n, G, r0, vec, shift, Wr); break;
-      case 4: small_waves_256_runs<TIN, 4, RANGE>(x, n, G, r0, vec, shift, Wr); break;
-      default: small_waves_256<TIN>(x, n, V, G, r0, vec, shift, RANGE, Wr[0]);
-    }
-    // threads 0 .. P-1 store the run's partials while the others load the next run (whose wave
-    // values go to the other buffer; this one is rewritten only behind the next run's barrier,
-    // which they reach after these stores)
-    if (threadIdx.x < P && G > 1 && r0 + (int)threadIdx.x < end) {  // one partial per thread
-      const int k = r0 + (int)threadIdx.x;
-      const StatAcc r = small_combine(Wr[threadIdx.x]);
-      parts[k].s1 = r.s1;
-      parts[k].s2 = r.s2;
-      parts[k].mn = r.mn;
-      parts[k].mx = r.mx;
-    }
+  switch (g.V) {
+    case 1: small_waves_1024_runs<TIN, 1, RANGE>(x, n, G, b0, vec, shift, W); break;
+    case 2: small_waves_1024_runs<TIN, 2, RANGE>(x, n, G, b0, vec, shift, W); break;
+    case 3: small_waves_1024_runs<TIN, 3, RANGE>(x, n, G, b0, vec, shift, W); break;
+    case 4: small_waves_1024_runs<TIN, 4, RANGE>(x, n, G, b0, vec, shift, W); break;
+    default: small_waves_1024_seq<TIN, RANGE>(x, n, g.V, G, b0, vec, shift, W);
   }
-  if (G == 1 && threadIdx.x == 0) {
-    const FinalizeArgs fin{A.clamp_lo, A.clamp_hi, RANGE ? multi_range_coef(A, ch.tensor, n) : 0.0f};
-    const StatAcc r = small_combine(W[0][0]);
-    finalize_stats<RANGE, TIN>(r.s1, r.s2, r.mn, r.mx, n, shift, false, fin, &A.stats[ch.tensor]);
+  if (G == 1) {
+    if (threadIdx.x == 0) {
+      const FinalizeArgs fin{A.clamp_lo, A.clamp_hi,
+                             RANGE ? multi_range_coef(A, ch.tensor, n) : 0.0f};
+      const StatAcc r = small_combine(W[0]);
+      finalize_stats<RANGE, TIN>(r.s1, r.s2, r.mn, r.mx, n, shift, false, fin,
+                                 &A.stats[ch.tensor]);
+    }
+    return;
+  }
+  if (b0 + (int)threadIdx.x < end) {  // one partial per thread
+    const int k = b0 + (int)threadIdx.x;
+    const StatAcc r = small_combine(W[threadIdx.x]);
+    StatPartial* q = A.partials + ch.first_chunk + k;
+    q->s1 = r.s1;
+    q->s2 = r.s2;
+    q->mn = r.mn;
+    q->mx = r.mx;
   }
 }
 
 // The totals of every small tensor of more than one partial (one workgroup per statistics record;
 // the record that starts the tensor's partials does the work): reduce_partials_w0's order over its
 // partials, stored by the statistics launch just before (plain loads: a launch boundary between),
-// then the finalisation — the single-tensor call's statistics, bit for bit. Its own launch (4.8 us
-// at C5): the last-arriving statistics workgroup reducing instead needs every workgroup's partial
-// stores released before its arrival — sc1 stores + atomic: 45.7 us for the sweep against 40.7 +
-// 4.8; plain stores + release fence: 111 us.
+// then the finalisation — the single-tensor call's statistics, bit for bit. Its own launch (5 us at
+// C5): the last-arriving statistics workgroup reducing instead needs every workgroup's partial
+// stores released before its arrival (sc1 stores + atomic: 45.7 us for the sweep against 40.7 +
+// 4.8; plain stores + a release fence: 111 us), and every apply workgroup reducing its tensor's
+// partials itself cost the apply 8 us.
 template <int TIN, bool RANGE>
 __global__ __launch_bounds__(kWave) void smaq_multi_final_kernel(MultiArgs A) {
   const ChunkDesc ch = A.stat_chunks[blockIdx.x];
@@ -337,24 +334,16 @@ struct PlanSizes {
   bool big;  // a tensor above kSmallMaxN (its statistics: the single-tensor launch)
 };
 
-// Partials per statistics workgroup: stat_runs() runs of 4 / V partials at V <= 4 (a run: up to 16
-// float4 groups per thread, all in flight at once), else 1. Not a reduction-order parameter: every
-// partial is stored and reduced in one order whatever the grouping. (Measured at C5: a workgroup
-// walking 16 partials one 12-KB step of loads ahead at a time, 139 us; one run per workgroup with
-// the last arrival reducing, 45.7 us, ~11 of them the arrivals' contended round trips.)
-constexpr int kDefaultStatRuns = 1;
-
-static int stat_runs() {
-  static const int r = [] {  // measurement knob SMQ_MULTI_RUNS (experiment builds)
-    const char* e = knob_env("SMQ_MULTI_RUNS");
-    const int v = e ? atoi(e) : kDefaultStatRuns;
-    return v >= 1 && v <= 64 ? v : kDefaultStatRuns;
-  }();
-  return r;
-}
+// Partials per statistics workgroup (1024 threads, the partial's native shape, two per CU): 4 / V
+// at V <= 4, i.e. 4 float4 groups per thread, all in flight at once; else 1 (loaded a group at a
+// time: holding V > 4 groups spills at that occupancy). Not a reduction-order parameter:
+// every partial is stored and reduced in one order whatever the grouping. (Measured at C5: a
+// 256-thread workgroup walking 16 partials one 12-KB step of loads ahead at a time, 139 us; 256
+// threads with four lanes each, a run of 4 / V partials in flight, 41 us — of which 22.6 us of
+// VALU alone, four wave butterflies per partial and wave: repo:tools/multi_exp.sh.)
 static int64_t partials_per_wg(int64_t n) {
   const int V = small_geom(n).V;
-  return V <= 4 ? stat_runs() * (4 / V) : 1;
+  return V <= 4 ? 4 / V : 1;
 }
 
 static bool plan_sizes(const int64_t* sizes, int count, PlanSizes* ps) {
@@ -503,12 +492,12 @@ static int launch_multi(const MultiArgs& A, bool sampled, bool range, int n_stat
   } else if (n_stat_chunks == 0) {  // only large tensors: their statistics are launched already
     hipLaunchKernelGGL(smaq_multi_snap_kernel, dim3(1), dim3(kWave), 0, st, A);
   } else if (range) {
-    hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kBlock), 0,
+    hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kSmallT), 0,
                        st, A);
     hipLaunchKernelGGL((smaq_multi_final_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kWave), 0,
                        st, A);
   } else {
-    hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, false>), dim3(n_stat_chunks), dim3(kBlock),
+    hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, false>), dim3(n_stat_chunks), dim3(kSmallT),
                        0, st, A);
     hipLaunchKernelGGL((smaq_multi_final_kernel<TIN, false>), dim3(n_stat_chunks), dim3(kWave),
                        0, st, A);

@@ -16,8 +16,7 @@
 //   S = 0; for w = 0, 4, 8, 12: S += (v[w] + v[w+1]) + (v[w+2] + v[w+3]).
 // min / max are order-free (fminf / fmaxf, NaN ignored like the big sweep). The totals are then
 // reduce_partials_w0's order over the G partials (smaq.hip), or the partial itself when G == 1.
-// A 1024-thread workgroup computes a partial natively; a 256-thread workgroup emulates it with four
-// lanes per thread (small_partial_256) — the same values, since every rounding step is the same.
+// Every path computes a partial with a 1024-thread workgroup, thread t = lane t.
 #pragma once
 
 #include "smaq_elem.h"
@@ -101,7 +100,7 @@ __device__ __forceinline__ StatAcc small_lane_sum(const void* x, int64_t n, int 
 // path that computes a missing partial while its own registers stay live).
 template <int TIN>
 __device__ __forceinline__ StatAcc small_lane_seq(const void* x, int64_t n, int V, int G, int b,
-                                                  int t, double shift) {
+                                                  int t, double shift, bool vec = true) {
   const int64_t nv = n >> 2;
   const int64_t base = (int64_t)b * V * kSmallT + t;
   StatAcc c0, c1, c2, c3;
@@ -109,7 +108,7 @@ __device__ __forceinline__ StatAcc small_lane_seq(const void* x, int64_t n, int 
   for (int u = 0; u < V; ++u) {
     const int64_t j = base + (int64_t)u * kSmallT;
     if (j >= nv) break;
-    const float4 g = load4<TIN>(x, j);
+    const float4 g = small_group<TIN>(x, j, vec);
     c0.add<true>(g.x, shift);
     c1.add<true>(g.y, shift);
     c2.add<true>(g.z, shift);
@@ -162,108 +161,50 @@ __device__ __forceinline__ StatAcc small_combine(const SmallWaveLds& w) {
   return r;
 }
 
-// Partial b by a 256-thread workgroup (multi-tensor statistics): thread t = 64 p + l holds the
-// lanes t + 256 k, k = 0..3, i.e. lane l of the virtual waves p + 4k. Every thread calls it; the
-// result is valid in every thread after the trailing barrier. W: the caller's LDS.
-template <int TIN>
-__device__ __forceinline__ StatAcc small_partial_256(const void* x, int64_t n, int V, int G, int b,
-                                                     bool vec, double shift, SmallWaveLds& W) {
-  const int p = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
-#pragma unroll
-  for (int k = 0; k < kSmallT / kBlock; ++k) {
-    const StatAcc w = small_wave(
-        small_lane<TIN, kSmallMaxV>(x, n, V, G, b, threadIdx.x + kBlock * k, vec, shift));
-    if (l == 0) {
-      W.s1[p + 4 * k] = w.s1;
-      W.s2[p + 4 * k] = w.s2;
-      W.mn[p + 4 * k] = w.mn;
-      W.mx[p + 4 * k] = w.mx;
-    }
-  }
-  __syncthreads();
-  const StatAcc r = small_combine(W);
-  __syncthreads();
-  return r;
-}
-
-// Partial b by a 256-thread workgroup with its loads in flight ahead of the sums (multi-tensor
-// statistics: one partial per workgroup): thread t = 64 p + l holds the lanes t + 256 k, k = 0..3,
-// i.e. lane l of the virtual waves p + 4k. V <= 2: all 4 V groups of a thread loaded at once;
-// else lane k + 1's groups load while lane k is summed. The wave values go to W; after the
-// barrier every thread may combine them (small_combine).
-template <int TIN>
-__device__ __forceinline__ void small_waves_256(const void* x, int64_t n, int V, int G, int b,
-                                                bool vec, double shift, bool range,
-                                                SmallWaveLds& W) {
-  const int p = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
-  constexpr int K = kSmallT / kBlock;
-  auto put = [&](int k, const StatAcc& a) {
-    const StatAcc w = small_wave(a, range);
-    if (l == 0) {
-      W.s1[p + 4 * k] = w.s1;
-      W.s2[p + 4 * k] = w.s2;
-      W.mn[p + 4 * k] = w.mn;
-      W.mx[p + 4 * k] = w.mx;
-    }
-  };
-  if (V <= 2) {
-    float4 g[K][2];
-#pragma unroll
-    for (int k = 0; k < K; ++k) small_lane_load<TIN, 2>(x, n, V, b, threadIdx.x + kBlock * k, vec, g[k]);
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-      put(k, small_lane_sum<TIN, 2>(x, n, V, G, b, threadIdx.x + kBlock * k, g[k], shift));
-  } else {
-    float4 cur[kSmallMaxV], nxt[kSmallMaxV];
-    small_lane_load<TIN, kSmallMaxV>(x, n, V, b, threadIdx.x, vec, cur);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (k + 1 < K) small_lane_load<TIN, kSmallMaxV>(x, n, V, b, threadIdx.x + kBlock * (k + 1), vec, nxt);
-      put(k, small_lane_sum<TIN, kSmallMaxV>(x, n, V, G, b, threadIdx.x + kBlock * k, cur, shift));
-#pragma unroll
-      for (int u = 0; u < kSmallMaxV; ++u) cur[u] = nxt[u];
-    }
-  }
-  __syncthreads();
-}
-
-// The 4 / V partials b0 .. (those < G) of a tensor with V <= 4 groups per lane by a 256-thread
-// workgroup, every load of them in flight at once (<= 16 float4 groups per thread, coalesced:
-// thread tau holds the lanes tau + 256 k, i.e. lane tau % 64 of the virtual waves tau / 64 + 4k):
-// partial b0 + p's 16 wave values in W[p]; valid after the trailing barrier. (Measured at C5
-// against two mappings that hold a lane quad per thread so that one DPP pass serves four virtual
-// waves: with the quad loaded by the thread itself, 64-B lane-strided loads, 44 us; with the lane
-// values transposed through LDS, 41 us; this form, four butterflies per partial and wave, 35-37.)
+// The 4 / V partials b0 .. (those < G) of a tensor with V <= 4 by a 1024-thread workgroup, the
+// native partial shape (thread t = lane t: smaq_stats_small_kernel's lane function and wave
+// butterfly, one butterfly per wave and partial), every load of the run in flight at once (4 float4
+// per thread): partial b0 + p's 16 wave values in W[p]; valid after the trailing barrier.
 template <int TIN, int V, bool RANGE>
-__device__ __forceinline__ void small_waves_256_runs(const void* x, int64_t n, int G, int b0,
-                                                     bool vec, double shift, SmallWaveLds* W) {
+__device__ __forceinline__ void small_waves_1024_runs(const void* x, int64_t n, int G, int b0,
+                                                      bool vec, double shift, SmallWaveLds* W) {
   static_assert(V >= 1 && V <= 4, "runs of partials: V <= 4");
-  constexpr int P = 4 / V, K = kSmallT / kBlock;
-  const int pw = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
-  float4 g[P][K][V];
+  constexpr int P = 4 / V;
+  const int wave = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
+  float4 g[P][V];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     if (b0 + p >= G) break;
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-      small_lane_load<TIN, V>(x, n, V, b0 + p, threadIdx.x + kBlock * k, vec, g[p][k]);
+    small_lane_load<TIN, V>(x, n, V, b0 + p, threadIdx.x, vec, g[p]);
   }
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     if (b0 + p >= G) break;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const StatAcc w = small_wave(small_lane_sum<TIN, V, RANGE>(x, n, V, G, b0 + p,
-                                                                 threadIdx.x + kBlock * k, g[p][k],
-                                                                 shift),
-                                   RANGE);
-      if (l == 0) {
-        W[p].s1[pw + 4 * k] = w.s1;
-        W[p].s2[pw + 4 * k] = w.s2;
-        W[p].mn[pw + 4 * k] = w.mn;
-        W[p].mx[pw + 4 * k] = w.mx;
-      }
+    const StatAcc w = small_wave(
+        small_lane_sum<TIN, V, RANGE>(x, n, V, G, b0 + p, threadIdx.x, g[p], shift), RANGE);
+    if (l == 0) {
+      W[p].s1[wave] = w.s1;
+      W[p].s2[wave] = w.s2;
+      W[p].mn[wave] = w.mn;
+      W[p].mx[wave] = w.mx;
     }
+  }
+  __syncthreads();
+}
+
+// Partial b0 alone the same way with one group per lane in flight (small_lane_seq: few registers;
+// for V > 4 where holding all V groups would spill at two 1024-thread workgroups per CU).
+template <int TIN, bool RANGE>
+__device__ __forceinline__ void small_waves_1024_seq(const void* x, int64_t n, int V, int G, int b0,
+                                                     bool vec, double shift, SmallWaveLds* W) {
+  const int wave = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
+  const StatAcc w =
+      small_wave(small_lane_seq<TIN>(x, n, V, G, b0, threadIdx.x, shift, vec), RANGE);
+  if (l == 0) {
+    W[0].s1[wave] = w.s1;
+    W[0].s2[wave] = w.s2;
+    W[0].mn[wave] = w.mn;
+    W[0].mx[wave] = w.mx;
   }
   __syncthreads();
 }

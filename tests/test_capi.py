@@ -183,8 +183,8 @@ def test_validation_errors_without_device():
 def test_multi_plan_layout():
     """Plan = header, descriptors, the apply map (4096-element chunks) and the statistics map: per
     tensor up to 8,388,611 elements, runs of whole partials of the single-tensor partition
-    (csrc/smaq_small.h: V groups of 4 per lane of 1024, G partials), one run of 4 / V partials
-    (V <= 4, else 1 partial) per statistics workgroup; larger tensors have no record (their statistics are the
+    (csrc/smaq_small.h: V groups of 4 per lane of 1024, G partials), runs of 4 / V partials
+    (V <= 4, else 1) per 1024-thread statistics workgroup; larger tensors have no record (their statistics are the
     single-tensor launch)."""
     from smart_compress_amd import _native as N
 
@@ -196,7 +196,7 @@ def test_multi_plan_layout():
     nbytes = lib.smq_smaq_multi_plan_bytes(arr, count)
     chunks = [-(-n // C) for n in sizes]
     nl = chunks[4]
-    # partials G = ceil((n // 4) / 1024) (V = 1 below 2^20 groups); one run of 4 per workgroup
+    # partials G = ceil((n // 4) / 1024) (V = 1 below 2^20 groups); 4 / V = 4 per workgroup
     parts = [1, 1, 1, 4, 16, 74]
     wgs = [-(-g // 4) for g in parts]
     dbytes = ((40 * count + 31) // 32) * 32
