@@ -80,6 +80,7 @@ struct MultiArgs {
   const SmqTensorDesc* descs;
   const ChunkDesc* chunks;       // apply chunks
   const ChunkDesc* stat_chunks;  // statistics chunks
+  const int32_t* final_rec;      // [count] first statistics record of a tensor to finalize, or -1
   SmqSmaqStats* stats;       // [count]
   unsigned long long* counters;  // [count] tagged arrival counters (block_arrive_tagged)
   ArriveTag tag;
@@ -157,8 +158,8 @@ __global__ __launch_bounds__(kSmallT, 8) void smaq_multi_stats_kernel(MultiArgs 
   }
 }
 
-// The totals of every small tensor of more than one partial (one workgroup per statistics record;
-// the record that starts the tensor's partials does the work): reduce_partials_w0's order over its
+// The totals of every small tensor of more than one partial (one workgroup per tensor, its first
+// statistics record from the plan's table): reduce_partials_w0's order over its
 // partials, stored by the statistics launch just before (plain loads: a launch boundary between),
 // then the finalisation — the single-tensor call's statistics, bit for bit. Its own launch (5 us at
 // C5): the last-arriving statistics workgroup reducing instead needs every workgroup's partial
@@ -167,11 +168,11 @@ __global__ __launch_bounds__(kSmallT, 8) void smaq_multi_stats_kernel(MultiArgs 
 // partials itself cost the apply 8 us.
 template <int TIN, bool RANGE>
 __global__ __launch_bounds__(kWave) void smaq_multi_final_kernel(MultiArgs A) {
-  const ChunkDesc ch = A.stat_chunks[blockIdx.x];
-  if (ch.begin != 0) return;
+  const int rec = A.final_rec[blockIdx.x];
+  if (rec < 0) return;  // a large tensor, or one partial: its statistics are final already
+  const ChunkDesc ch = A.stat_chunks[rec];
   const int64_t n = ch.n;
   const int G = small_geom(n).G;
-  if (G == 1) return;  // finalised by the statistics launch
   const double shift = stats_shift<TIN>(ch.x, n);
   double t1, t2;
   float tmn, tmx;
@@ -329,7 +330,7 @@ static int64_t chunk_elems() {
 static int64_t chunks_of(int64_t n, int64_t c) { return (n + c - 1) / c; }
 
 struct PlanSizes {
-  size_t hdr, descs, chunks, stat_chunks, total;
+  size_t hdr, descs, chunks, stat_chunks, final_tab, total;
   int64_t n_chunks, n_stat_chunks, n_partials;
   bool big;  // a tensor above kSmallMaxN (its statistics: the single-tensor launch)
 };
@@ -368,7 +369,8 @@ static bool plan_sizes(const int64_t* sizes, int count, PlanSizes* ps) {
   ps->descs = ((sizeof(SmqTensorDesc) * (size_t)count) + 31) & ~(size_t)31;
   ps->chunks = sizeof(ChunkDesc) * (size_t)nc;
   ps->stat_chunks = sizeof(ChunkDesc) * (size_t)ns;
-  ps->total = ps->hdr + ps->descs + ps->chunks + ps->stat_chunks;
+  ps->final_tab = ((sizeof(int32_t) * (size_t)count) + 63) & ~(size_t)63;
+  ps->total = ps->hdr + ps->descs + ps->chunks + ps->stat_chunks + ps->final_tab;
   return true;
 }
 
@@ -465,7 +467,14 @@ int smq_smaq_multi_plan_build(const SmqTensorDesc* descs, int count, void* host_
   h->stat_chunk = 0;  // statistics records are runs of partials_per_wg partials
   memcpy(base + ps.hdr, descs, sizeof(SmqTensorDesc) * (size_t)count);
   fill_chunks((ChunkDesc*)(base + ps.hdr + ps.descs), descs, count, h->chunk);
-  fill_stat_chunks((ChunkDesc*)(base + ps.hdr + ps.descs + ps.chunks), descs, count);
+  ChunkDesc* sc = (ChunkDesc*)(base + ps.hdr + ps.descs + ps.chunks);
+  fill_stat_chunks(sc, descs, count);
+  // per tensor: its first statistics record when the finalize launch reduces its partials (a
+  // small tensor of more than one partial), else -1
+  int32_t* fin = (int32_t*)(base + ps.hdr + ps.descs + ps.chunks + ps.stat_chunks);
+  for (int t = 0; t < count; ++t) fin[t] = -1;
+  for (int64_t r = 0; r < ps.n_stat_chunks; ++r)
+    if (sc[r].begin == 0 && small_geom(sc[r].n).G > 1) fin[sc[r].tensor] = (int32_t)r;
   return SMQ_OK;
 }
 
@@ -494,13 +503,11 @@ static int launch_multi(const MultiArgs& A, bool sampled, bool range, int n_stat
   } else if (range) {
     hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kSmallT), 0,
                        st, A);
-    hipLaunchKernelGGL((smaq_multi_final_kernel<TIN, true>), dim3(n_stat_chunks), dim3(kWave), 0,
-                       st, A);
+    hipLaunchKernelGGL((smaq_multi_final_kernel<TIN, true>), dim3(count), dim3(kWave), 0, st, A);
   } else {
     hipLaunchKernelGGL((smaq_multi_stats_kernel<TIN, false>), dim3(n_stat_chunks), dim3(kSmallT),
                        0, st, A);
-    hipLaunchKernelGGL((smaq_multi_final_kernel<TIN, false>), dim3(n_stat_chunks), dim3(kWave),
-                       0, st, A);
+    hipLaunchKernelGGL((smaq_multi_final_kernel<TIN, false>), dim3(count), dim3(kWave), 0, st, A);
   }
   int rc = check_launch(sampled ? "smaq_multi_draw_kernel" : "smaq_multi_stats_kernel");
   if (rc) return rc;
@@ -573,6 +580,7 @@ extern "C" int smq_smaq_multi(const void* dev_plan, const void* host_plan, int d
   A.descs = (const SmqTensorDesc*)(pb + sizeof(MultiHeader));
   A.chunks = (const ChunkDesc*)(pb + sizeof(MultiHeader) + descs_bytes);
   A.stat_chunks = A.chunks + n_chunks;
+  A.final_rec = reinterpret_cast<const int32_t*>(A.stat_chunks + n_stat_chunks);
   char* wb = (char*)ws;
   A.stats = (SmqSmaqStats*)wb;
   A.counters = (unsigned long long*)(wb + stats);

@@ -200,7 +200,8 @@ def test_multi_plan_layout():
     parts = [1, 1, 1, 4, 16, 74]
     wgs = [-(-g // 4) for g in parts]
     dbytes = ((40 * count + 31) // 32) * 32
-    assert nbytes == 32 + dbytes + 64 * (sum(chunks) + sum(wgs))
+    tab = (4 * count + 63) // 64 * 64  # per tensor: its first statistics record to finalize
+    assert nbytes == 32 + dbytes + 64 * (sum(chunks) + sum(wgs)) + tab
     descs = (N.SmqTensorDesc * count)()
     rel = 0
     for i, n in enumerate(sizes):
@@ -216,8 +217,11 @@ def test_multi_plan_layout():
     assert int(raw[8:16].view(np.int64)[0]) == C
     assert list(raw[16:24].view(np.int32)) == [sum(wgs), sum(parts)]
     assert int(raw[24:32].view(np.int64)[0]) == 0
-    rec = raw[32 + dbytes:].reshape(-1, 64)
+    rec = raw[32 + dbytes:nbytes - tab].reshape(-1, 64)
     assert rec.shape[0] == sum(chunks) + sum(wgs)
+    fin = raw[nbytes - tab:nbytes - tab + 4 * count].view(np.int32)
+    firsts = [sum(wgs[:t]) for t in range(len(wgs))]
+    assert list(fin) == [firsts[t] if parts[t] > 1 else -1 for t in range(len(parts))] + [-1]
     q = rec[:, :48].copy().view(np.int64)  # x, y, n, begin, end, rng_offset
     i32 = rec[:, 48:].copy().view(np.int32)  # tensor, first_chunk, n_chunks, all_positive
     a = slice(0, 8 + nl)
