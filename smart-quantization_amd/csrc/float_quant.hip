@@ -1051,17 +1051,22 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
     s2f_stamp(A, 9);
   }
   lds_barrier();
+  // threads 0-130 (waves 0-2) tabulate the inverse powers; no barrier before the forward transform,
+  // so the other waves' forward powers cover the powf latency (the table is read only after the
+  // barrier behind the forward)
   if (threadIdx.x < kS2LutArgs) {
     const float T = s2_lut_arg(threadIdx.x);
     lut[__builtin_bit_cast(uint32_t, T) >> 21] = powf(T * sst.inv_beta_pow2, sst.inv_alpha);
   }
   s2f_stamp(A, 10);
-  lds_barrier();
-  s2f_stamp(A, 4);
   const float alpha = sst.alpha, bp2 = sst.beta_pow2, ialpha = sst.inv_alpha;
   const bool fast = !A.exact_pow && alpha > 0.0f && alpha < INFINITY && ialpha > 0.0f &&
                     ialpha < INFINITY;
   const bool last_chunk = b == A.G - 1;
+  if (!(fast && A.out_mode == 0)) {  // (uniform over the workgroup: sst and A are)
+    lds_barrier();
+    s2f_stamp(A, 4);
+  }
   if (fast && A.out_mode == 0) {
     // one margin for the lane's elements: the largest |log2|x|| among them (zeros and NaN aside)
     float lgmax = 1.0f;
@@ -1084,6 +1089,8 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
         T[u][q] = s2_fwd_fast_lg(xq, lg[u][q], rw[u][q], alpha, bp2, A.check_inf, A.max_value, E);
       }
     }
+    lds_barrier();  // the table is complete
+    s2f_stamp(A, 4);
 #pragma unroll
     for (int u = 0; u < V; ++u) {
       const int64_t j = base + (int64_t)u * kS2FT;

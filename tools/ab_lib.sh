@@ -11,7 +11,7 @@ for r in $(seq 1 "$ROUNDS"); do
     IFS='|' read -r label envs args <<< "$spec"
     for lib in "$A" "$B"; do
       line=$(env $envs SMQ_LIB="$lib" timeout -k 10 180 python3 "$R/bench.py" --no-cpu-baseline $args 2>/dev/null | tail -n 1) || exit 1
-      ms=$(python3 -c "import json,sys; d=json.loads(sys.argv[1]); print(d['ms_per_step'], d.get('roofline',{}).get('achieved'))" "$line")
+      ms=$(python3 -c "import json,sys; d=json.loads(sys.argv[1]); print(d['ms_per_step'], d.get('roofline',{}).get('achieved'), d.get('roofline',{}).get('avg_launch_ms'))" "$line")
       echo "round $r $label $(basename $(dirname $lib)) $ms"
     done
   done
