@@ -459,13 +459,26 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       // butterfly
       double s1 = 0.0, s2 = 0.0;
       float mn = INFINITY, mx = -INFINITY;
+      // every word read first (one LDS round trip instead of one per partial; the words of
+      // partials >= G are not used), then the adds in the same order, skipped ones as selects
+      uint32_t wd[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wd[q][c] = pw[(4 * c + q) * kWave + lane];  // word c at w[4c * 64]
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if (4 * lane + q >= G) continue;
-        const uint32_t* w = pw + q * kWave + lane;  // word c at w[4c * 64]
-        s1 += __builtin_bit_cast(double, ((uint64_t)w[4 * kWave] << 32) | w[0]);
-        s2 += __builtin_bit_cast(double, ((uint64_t)w[12 * kWave] << 32) | w[8 * kWave]);
-        if (A.range) {
+        const bool ok = 4 * lane + q < G;
+        const double a1 = __builtin_bit_cast(double, ((uint64_t)wd[q][1] << 32) | wd[q][0]);
+        const double a2 = __builtin_bit_cast(double, ((uint64_t)wd[q][3] << 32) | wd[q][2]);
+        s1 = ok ? s1 + a1 : s1;
+        s2 = ok ? s2 + a2 : s2;
+      }
+      if (A.range) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (4 * lane + q >= G) continue;
+          const uint32_t* w = pw + q * kWave + lane;
           mn = fminf(mn, __builtin_bit_cast(float, w[16 * kWave]));
           mx = fmaxf(mx, __builtin_bit_cast(float, w[20 * kWave]));
         }
