@@ -69,6 +69,32 @@ def test_params_block():
     assert np.float32(p.clamp_lo) == np.float32(1e-4) and p.all_positive == 1
 
 
+def test_hot_params_equal_params():
+    """The hot path's parameter block (a copy of a cached flag template + this call's stream
+    position) is byte-identical to _params at the same stream position, follows flags changed
+    between calls, and advances the stream the same way."""
+    from smart_compress_amd.compress.smart import SmartFP
+
+    for kw in ({}, {"use_range_std_dev": True}, {"stochastic_rounding": False},
+               {"measure_compression_ratio": True}, {"precision": 16}):
+        for ap in (False, True):
+            for dt in (torch.float32, torch.float16):
+                a = SmartFP(smaq_hparams(smq_seed=3, **kw))
+                b = SmartFP(smaq_hparams(smq_seed=3, **kw))
+                for n in (1000, 77, 1 << 20):
+                    assert bytes(a._params(n, ap, dt)) == bytes(b._hot_params(n, ap, dt, None))
+    c = SmartFP(smaq_hparams(smq_seed=3))
+    d = SmartFP(smaq_hparams(smq_seed=3))
+    c._hot_params(10, False, torch.float32, None)
+    d._params(10, False, torch.float32)
+    for hp in (c.hparams, d.hparams):  # a flag changed after the first call takes effect
+        hp.main_std_dev_threshold = 1.5
+        hp.stochastic_rounding = False
+    pc = c._hot_params(10, False, torch.float32, None)
+    assert bytes(pc) == bytes(d._params(10, False, torch.float32))
+    assert pc.stochastic_rounding == 0 and pc.main_std_dev_threshold == 1.5 and pc.offset == 10
+
+
 def test_rng_offsets_advance():
     from smart_compress_amd.compress.smart import SmartFP
 
