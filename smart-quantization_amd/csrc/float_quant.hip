@@ -926,6 +926,16 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
     s2f_publish(s, m, A, b, epoch, shs, shm);
   }
   s2f_stamp(A, 2);
+  // one margin for the lane's elements (s2_fast_margin): the largest |log2|x|| among them (zeros
+  // and NaN aside), taken here, off the path behind the gather
+  float lgmax = 1.0f;
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    if (base + (int64_t)u * kS2FT >= A.nv) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      lgmax = fmaxf(lgmax, lg[u][q] == -INFINITY ? 0.0f : fabsf(lg[u][q]));
+  }
   // The stochastic-rounding words depend on the stream position only: waves 1..15, idle while wave
   // 0 gathers the partials, compute their own now, and waves 1..V also wave 0's slot u = wave - 1
   // (handed over in LDS behind the gather's barrier), so the transform after the statistics starts
@@ -1068,15 +1078,6 @@ __global__ __launch_bounds__(kS2FT) void s2fp8_fused_kernel(S2FArgs A) {
     s2f_stamp(A, 4);
   }
   if (fast && A.out_mode == 0) {
-    // one margin for the lane's elements: the largest |log2|x|| among them (zeros and NaN aside)
-    float lgmax = 1.0f;
-#pragma unroll
-    for (int u = 0; u < V; ++u) {
-      if (base + (int64_t)u * kS2FT >= A.nv) continue;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        lgmax = fmaxf(lgmax, lg[u][q] == -INFINITY ? 0.0f : fabsf(lg[u][q]));
-    }
     const uint32_t E = s2_fast_margin(alpha, lgmax);
     uint32_t T[kS2FMaxV][4];
 #pragma unroll
