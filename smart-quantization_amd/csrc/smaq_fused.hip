@@ -264,8 +264,9 @@ __device__ __forceinline__ void uniform_consts(ElemConsts& c) {
 }
 
 // The element transform of the registers (smart.py:154-182) and their stores. PRE: the rounding
-// draws uu were computed ahead (during the gather), else they are hashed here.
-template <int RM, int V, int TIN, bool AP, bool SUB, bool PRE>
+// draws uu were computed ahead (during the gather); PL: likewise, but they wait in LDS (park[u *
+// kSmallT + t], V = 4: no group is parked there); else they are hashed here.
+template <int RM, int V, int TIN, bool AP, bool SUB, bool PRE, bool PL = false>
 __device__ __forceinline__ uint32_t fused_transform(const FusedArgs& A, const float4 (&vr)[V],
                                                     const float4* park, const float (&uu)[V][4],
                                                     const ElemConsts& c, int64_t base,
@@ -279,7 +280,15 @@ __device__ __forceinline__ uint32_t fused_transform(const FusedArgs& A, const fl
     if (j >= A.nv) continue;
     const float4 x4 = u < VR ? vr[u] : park[(u - VR) * kSmallT + threadIdx.x];
     float u0 = uu[u][0], u1 = uu[u][1], u2 = uu[u][2], u3 = uu[u][3];
-    if (RM == kRoundHash && !PRE) rng_hu4(A.key, off + ((uint64_t)j << 2), u0, u1, u2, u3);
+    if (PL) {
+      const float4 w = park[u * kSmallT + threadIdx.x];
+      u0 = w.x;
+      u1 = w.y;
+      u2 = w.z;
+      u3 = w.w;
+    } else if (RM == kRoundHash && !PRE) {
+      rng_hu4(A.key, off + ((uint64_t)j << 2), u0, u1, u2, u3);
+    }
     bool b0, b1, b2, b3;
     float4 o;
     o.x = smaq_elem<RM, false, TIN, AP, SUB, false>(x4.x, u0, c, b0);
@@ -351,8 +360,10 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
 
   // the rounding draws depend on the stream position only: every wave computes its own now (wave
   // 0's by waves 4..4+V-1, handed over in LDS), before it polls for the partials. Above 3
-  // groups per lane they would hold 4V more VGPRs across the gather: hashed in the transform.
+  // groups per lane they would hold 4V more VGPRs across the gather: at V = 4 they wait in the
+  // (then unused) parking LDS instead, above it they are hashed in the transform.
   constexpr bool PRE = RM == kRoundHash && V <= 3;
+  constexpr bool PL = RM == kRoundHash && V == 4;
   float uu[V][4];
 #pragma unroll
   for (int u = 0; u < V; ++u) uu[u][0] = uu[u][1] = uu[u][2] = uu[u][3] = 0.0f;
@@ -367,6 +378,23 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       rng_hu4(A.key, off + ((uint64_t)((int64_t)b * V * kSmallT + lane + (int64_t)u * kSmallT) << 2),
               w.x, w.y, w.z, w.w);
       u0lds[u][lane] = w;
+    }
+  }
+  if (PL) {  // (the launcher gives V >= 4 the dynamic LDS whatever G is)
+    if (wave != 0) {
+#pragma unroll
+      for (int u = 0; u < V; ++u) {
+        float4 w;
+        rng_hu4(A.key, off + ((uint64_t)(base + (int64_t)u * kSmallT) << 2), w.x, w.y, w.z, w.w);
+        park[u * kSmallT + threadIdx.x] = w;
+      }
+    }
+    if (wave >= 4 && wave < 4 + V) {  // wave 0's slot u
+      const int u = wave - 4;
+      float4 w;
+      rng_hu4(A.key, off + ((uint64_t)((int64_t)b * V * kSmallT + lane + (int64_t)u * kSmallT) << 2),
+              w.x, w.y, w.z, w.w);
+      park[u * kSmallT + lane] = w;
     }
   }
 
@@ -532,18 +560,18 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   uint32_t n_out;
   if (sst.quot_check) {
     if (A.all_pos) {
-      n_out = fused_transform<RM, V, TIN, true, true, PRE>(A, v, park, uu, c, base, off);
+      n_out = fused_transform<RM, V, TIN, true, true, PRE, PL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, true, true>(A, c, off);
     } else {
-      n_out = fused_transform<RM, V, TIN, false, true, PRE>(A, v, park, uu, c, base, off);
+      n_out = fused_transform<RM, V, TIN, false, true, PRE, PL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, false, true>(A, c, off);
     }
   } else {
     if (A.all_pos) {
-      n_out = fused_transform<RM, V, TIN, true, false, PRE>(A, v, park, uu, c, base, off);
+      n_out = fused_transform<RM, V, TIN, true, false, PRE, PL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, true, false>(A, c, off);
     } else {
-      n_out = fused_transform<RM, V, TIN, false, false, PRE>(A, v, park, uu, c, base, off);
+      n_out = fused_transform<RM, V, TIN, false, false, PRE, PL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, false, false>(A, c, off);
     }
   }
@@ -624,8 +652,10 @@ static int launch_fused_v(const FusedArgs& F, hipStream_t st) {
               hipGetErrorString(attr));
     return SMQ_ERR_LAUNCH;
   }
-  const int lds = (F.G > 1 || V > 4) ? kFusedLds : 0;  // parking (V > 4): (V - 4) * 16 KiB
+  // parking (V > 4): (V - 4) * 16 KiB; the rounding draws at V = 4: 64 KiB
+  const int lds = (F.G > 1 || V >= 4) ? kFusedLds : 0;
   static_assert(kFusedLds >= (kSmallMaxV - 4) * kSmallT * 16, "LDS parking");
+  static_assert(kFusedLds >= 4 * kSmallT * 16, "rounding draws at V = 4");
   hipLaunchKernelGGL((smaq_fused_kernel<RM, V, TIN>), dim3((unsigned)F.G), dim3(kSmallT), lds, st,
                      F);
   return check_launch("smaq_fused_kernel");

@@ -7,7 +7,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
 for r in 1 2 3; do
   for v in "$@"; do
-    out=$(SMQ_LIB="$R/exp/$v/libsmq.so" DS_SIZES=1048576,4194304,8388608 timeout -k 10 120 python3 tools/defer_sweep.py 2>/dev/null) || exit 1
+    out=$(SMQ_LIB="$R/exp/$v/libsmq.so" DS_SIZES=${FA_SIZES:-1048576,4194304,8388608} timeout -k 10 120 python3 tools/defer_sweep.py 2>/dev/null) || exit 1
     echo "round $r $v: $(echo "$out" | tr '\n' ' ')"
   done
 done
