@@ -45,7 +45,22 @@ namespace smq {
 constexpr int kFusedRep = SmaqWsLayout::kFusedRep;
 constexpr int kFusedWords = SmaqWsLayout::kFusedWords;
 constexpr uint64_t kFusedStealTicks = 20000;  // s_memrealtime at 100 MHz: 200 us
-constexpr int kFusedLds = 88 * 1024;          // dynamic LDS request: one workgroup per CU
+// dynamic LDS request (one workgroup per CU): the parked groups (V > 4) and then the rounding
+// draws of the first fused_draw_groups(V) groups, 16 KiB per group
+constexpr int kFusedLdsGroups = 9;
+constexpr int kFusedLds = kFusedLdsGroups * 16 * 1024;
+// groups whose rounding draws are hashed during the gather into LDS (V >= 4; V <= 3 keeps them in
+// registers): as many as fit next to the parked groups
+// (V = 8: 5 of its 8 groups would fit, and measured 19.41 -> 19.53 us at 8M: left in the transform)
+__host__ __device__ constexpr int fused_draw_groups(int V) {
+  return (V < 4 || V > 7) ? 0 : (V < kFusedLdsGroups - (V - 4) ? V : kFusedLdsGroups - (V - 4));
+}
+// the launch's dynamic LDS: the parked groups and the draws, at least 88 KiB (one workgroup per CU)
+__host__ __device__ constexpr int fused_lds_bytes(int V) {
+  return ((V > 4 ? V - 4 : 0) + fused_draw_groups(V)) * 16 * 1024 > 88 * 1024
+             ? ((V > 4 ? V - 4 : 0) + fused_draw_groups(V)) * 16 * 1024
+             : 88 * 1024;
+}
 constexpr int kSubStride = (int)(SmaqWsLayout::kFusedSubStride / 8);  // residue words (u64 units)
 
 // ------------------------------------------------------------------------------------------------
@@ -264,9 +279,10 @@ __device__ __forceinline__ void uniform_consts(ElemConsts& c) {
 }
 
 // The element transform of the registers (smart.py:154-182) and their stores. PRE: the rounding
-// draws uu were computed ahead (during the gather); PL: likewise, but they wait in LDS (park[u *
-// kSmallT + t], V = 4: no group is parked there); else they are hashed here.
-template <int RM, int V, int TIN, bool AP, bool SUB, bool PRE, bool PL = false>
+// draws uu were computed ahead (during the gather); DL > 0: those of groups u < DL likewise, but
+// they wait in LDS (park[(VP + u) * kSmallT + t], behind the VP parked groups); else they are
+// hashed here.
+template <int RM, int V, int TIN, bool AP, bool SUB, bool PRE, int DL = 0>
 __device__ __forceinline__ uint32_t fused_transform(const FusedArgs& A, const float4 (&vr)[V],
                                                     const float4* park, const float (&uu)[V][4],
                                                     const ElemConsts& c, int64_t base,
@@ -280,8 +296,8 @@ __device__ __forceinline__ uint32_t fused_transform(const FusedArgs& A, const fl
     if (j >= A.nv) continue;
     const float4 x4 = u < VR ? vr[u] : park[(u - VR) * kSmallT + threadIdx.x];
     float u0 = uu[u][0], u1 = uu[u][1], u2 = uu[u][2], u3 = uu[u][3];
-    if (PL) {
-      const float4 w = park[u * kSmallT + threadIdx.x];
+    if (u < DL) {
+      const float4 w = park[((V > 4 ? V - 4 : 0) + u) * kSmallT + threadIdx.x];
       u0 = w.x;
       u1 = w.y;
       u2 = w.z;
@@ -363,7 +379,8 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   // groups per lane they would hold 4V more VGPRs across the gather: at V = 4 they wait in the
   // (then unused) parking LDS instead, above it they are hashed in the transform.
   constexpr bool PRE = RM == kRoundHash && V <= 3;
-  constexpr bool PL = RM == kRoundHash && V == 4;
+  constexpr int DL = RM == kRoundHash ? fused_draw_groups(V) : 0;
+  constexpr int VP = V > 4 ? V - 4 : 0;
   float uu[V][4];
 #pragma unroll
   for (int u = 0; u < V; ++u) uu[u][0] = uu[u][1] = uu[u][2] = uu[u][3] = 0.0f;
@@ -380,21 +397,21 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       u0lds[u][lane] = w;
     }
   }
-  if (PL) {  // (the launcher gives V >= 4 the dynamic LDS whatever G is)
+  if (DL > 0) {  // (the launcher gives V >= 4 the dynamic LDS whatever G is)
     if (wave != 0) {
 #pragma unroll
-      for (int u = 0; u < V; ++u) {
+      for (int u = 0; u < DL; ++u) {
         float4 w;
         rng_hu4(A.key, off + ((uint64_t)(base + (int64_t)u * kSmallT) << 2), w.x, w.y, w.z, w.w);
-        park[u * kSmallT + threadIdx.x] = w;
+        park[(VP + u) * kSmallT + threadIdx.x] = w;
       }
     }
-    if (wave >= 4 && wave < 4 + V) {  // wave 0's slot u
+    if (wave >= 4 && wave < 4 + DL) {  // wave 0's slot u
       const int u = wave - 4;
       float4 w;
       rng_hu4(A.key, off + ((uint64_t)((int64_t)b * V * kSmallT + lane + (int64_t)u * kSmallT) << 2),
               w.x, w.y, w.z, w.w);
-      park[u * kSmallT + lane] = w;
+      park[(VP + u) * kSmallT + lane] = w;
     }
   }
 
@@ -560,18 +577,18 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   uint32_t n_out;
   if (sst.quot_check) {
     if (A.all_pos) {
-      n_out = fused_transform<RM, V, TIN, true, true, PRE, PL>(A, v, park, uu, c, base, off);
+      n_out = fused_transform<RM, V, TIN, true, true, PRE, DL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, true, true>(A, c, off);
     } else {
-      n_out = fused_transform<RM, V, TIN, false, true, PRE, PL>(A, v, park, uu, c, base, off);
+      n_out = fused_transform<RM, V, TIN, false, true, PRE, DL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, false, true>(A, c, off);
     }
   } else {
     if (A.all_pos) {
-      n_out = fused_transform<RM, V, TIN, true, false, PRE, PL>(A, v, park, uu, c, base, off);
+      n_out = fused_transform<RM, V, TIN, true, false, PRE, DL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, true, false>(A, c, off);
     } else {
-      n_out = fused_transform<RM, V, TIN, false, false, PRE, PL>(A, v, park, uu, c, base, off);
+      n_out = fused_transform<RM, V, TIN, false, false, PRE, DL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, false, false>(A, c, off);
     }
   }
@@ -653,9 +670,11 @@ static int launch_fused_v(const FusedArgs& F, hipStream_t st) {
     return SMQ_ERR_LAUNCH;
   }
   // parking (V > 4): (V - 4) * 16 KiB; the rounding draws at V = 4: 64 KiB
-  const int lds = (F.G > 1 || V >= 4) ? kFusedLds : 0;
+  const int lds = (F.G > 1 || V >= 4) ? fused_lds_bytes(V) : 0;
   static_assert(kFusedLds >= (kSmallMaxV - 4) * kSmallT * 16, "LDS parking");
-  static_assert(kFusedLds >= 4 * kSmallT * 16, "rounding draws at V = 4");
+  static_assert(kFusedLds >= ((V > 4 ? V - 4 : 0) + fused_draw_groups(V)) * kSmallT * 16,
+                "parked groups + rounding draws");
+  static_assert(kFusedLds + 8 * 1024 <= 160 * 1024, "LDS of one workgroup (static part < 8 KiB)");
   hipLaunchKernelGGL((smaq_fused_kernel<RM, V, TIN>), dim3((unsigned)F.G), dim3(kSmallT), lds, st,
                      F);
   return check_launch("smaq_fused_kernel");
