@@ -40,6 +40,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SMALL_MAX_N = 8388611  # smq_smaq_roundtrip: one register-resident launch up to this many elements
 METRIC = "SmaQ 6/8-bit quant+dequant round-trip GB/s (and % HBM peak), {size} fp32"
 
 
@@ -510,15 +511,19 @@ def run_smaq(args, world, rank, device):
     total_bytes = sum_over_ranks(alg_per_elem * n * args.steps, world, device)
     value = total_bytes / elapsed / 1e9
     call_ms = trace.mean_ms("call")
-    call_gbps = alg_per_elem * n / (call_ms * 1e-3) / 1e9
     # the launches of one call: one register-resident launch up to 8,388,611 elements (full
-    # statistics), else the statistics launch + the apply launch (include/smq.h)
+    # statistics: x read once, y written = in_bytes + 4 per element), else the statistics launch +
+    # the apply launch (include/smq.h). `value` keeps the metric's convention (alg_per_elem);
+    # the roofline divides the bytes the call's launches must move.
+    moved_per_elem = alg_per_elem
     if sampled:
         kernels = "smaq_draw_stats_kernel+smaq_apply_kernel"
-    elif n <= 8388611:
+    elif n <= SMALL_MAX_N:
         kernels = "smaq_fused_kernel"
+        moved_per_elem = in_bytes + 4
     else:
         kernels = "smaq_stats_kernel+smaq_apply_kernel"
+    call_gbps = moved_per_elem * n / (call_ms * 1e-3) / 1e9
     res = {
         "metric": METRIC.format(size=size_label(n)), "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -542,7 +547,7 @@ def run_smaq(args, world, rank, device):
         "roofline": {"bound": "hbm", "kernel": kernels,
                      "achieved": round(call_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(call_gbps / HBM_PEAK_GBPS, 4),
-                     "alg_bytes_per_launch": int(alg_per_elem * n),
+                     "alg_bytes_per_launch": int(moved_per_elem * n),
                      "avg_launch_ms": round(call_ms, 5),
                      "traffic": traffic_from_profile(
                          args.config, n, "f32" if in_dt is None else os.environ["SMQ_BENCH_DTYPE"],
@@ -971,9 +976,11 @@ def run_autograd(args, world, rank, device):
     x = torch.randn(batch, 3, 32, 32, device=device)
     t = torch.randint(0, 10, (batch,), device=device)
     flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
-    calls = {"n": 0, "elems": 0}
 
-    def build(compress):
+    def build(compress, sizes=None):
+        """The network; with compression the SmartFP codec itself is registered (train.py:198-213
+        passes the codec instance), so Compressor takes the codec's C autograd path. sizes: a list
+        that records the element count of every codec call instead (one counting step)."""
         torch.manual_seed(0)
         net = (_ResNet() if resnet else _vgg_cifar()).to(device)
         opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9)
@@ -981,12 +988,11 @@ def run_autograd(args, world, rank, device):
         if compress:
             codec = SmartFP(smaq_hparams())
             codec.rng.seed = 3000 + rank
-
-            def fn(v, tag=None, **kw):
-                calls["n"] += 1
-                calls["elems"] += v.numel()
-                return codec(v, tag=tag, **kw)
-
+            fn = codec
+            if sizes is not None:
+                def fn(v, tag=None, **kw):
+                    sizes.append(v.numel())
+                    return codec(v, tag=tag, **kw)
             register_autograd_module(net, fn, flags)
         return net, opt, codec
 
@@ -997,6 +1003,17 @@ def run_autograd(args, world, rank, device):
             loss.backward()
             opt.step()
         return step
+
+    # the codec calls of one step and their sizes (a separate, counting network)
+    sizes = []
+    net, opt, _ = build(True, sizes)
+    step_fn(net, opt)()
+    torch.cuda.synchronize()
+    calls_per, elems = len(sizes), sum(sizes)
+    # bytes the calls must move: 8 B/elem for the single launch (x read once, y written), 12 B/elem
+    # for the two-launch calls above SMALL_MAX_N (statistics read + apply read and write)
+    alg_bytes = sum(8 * n if n <= SMALL_MAX_N else 12 * n for n in sizes)
+    del net, opt
 
     results = {}
     for name in ("uncompressed", "smaq_eager", "smaq_graph"):
@@ -1016,28 +1033,36 @@ def run_autograd(args, world, rank, device):
             run = g.replay
         else:
             run = step
-        calls["n"] = calls["elems"] = 0
         run()
         torch.cuda.synchronize()
-        per_step = (calls["n"], calls["elems"])
         for _ in range(args.warmup):
             run()
         elapsed = time_steps(run, args.steps, 0, world, device)
         results[name] = {"ms_per_step": round(elapsed / args.steps * 1e3, 4)}
-        if name != "uncompressed" and per_step[0]:
-            results[name].update(codec_calls_per_step=per_step[0],
-                                 compressed_elements_per_step=per_step[1])
-    calls_per, elems = results["smaq_eager"]["codec_calls_per_step"], \
-        results["smaq_eager"]["compressed_elements_per_step"]
+        if name != "uncompressed":
+            results[name].update(codec_calls_per_step=calls_per,
+                                 compressed_elements_per_step=elems)
+        del net, opt, codec, run
     base_ms = results["uncompressed"]["ms_per_step"]
     for name in ("smaq_eager", "smaq_graph"):
         codec_ms = results[name]["ms_per_step"] - base_ms
         results[name]["codec_ms_per_step"] = round(codec_ms, 4)
         results[name]["codec_gbps_12B"] = round(12.0 * elems / (codec_ms * 1e-3) / 1e9, 1) \
             if codec_ms > 0 else None
+        results[name]["codec_gbps_alg"] = round(alg_bytes / (codec_ms * 1e-3) / 1e9, 1) \
+            if codec_ms > 0 else None
     g_ms = results["smaq_graph"]["ms_per_step"]
     g_codec = results["smaq_graph"]["codec_ms_per_step"]
-    g_gbps = results["smaq_graph"]["codec_gbps_12B"]
+    g_gbps = results["smaq_graph"]["codec_gbps_alg"]
+    # HBM bytes of the step's SmaQ launches from the committed PMC passes
+    # (tools/autograd_profile.py -> profiles/traffic_<config>.json)
+    traffic = None
+    tp = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tp):
+        with open(tp) as f:
+            tj = json.load(f)
+        if tj.get("calls_per_step") == calls_per and tj.get("elements_per_step") == elems:
+            traffic = tj["hbm_bytes_per_step"]
     return {"metric": "Training step with SmaQ on every layer (activations + grad-maps), ms/step",
             "value": g_ms, "unit": "ms/step", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": g_ms, "higher_is_better": False,
@@ -1045,15 +1070,16 @@ def run_autograd(args, world, rank, device):
             "config": {"workload": ("resnet34" if resnet else "vgg") +
                        "_cifar_b128_register_autograd_module",
                        "codec_calls_per_step": calls_per,
-                       "compressed_elements_per_step": elems},
+                       "compressed_elements_per_step": elems,
+                       "alg_bytes_per_step": alg_bytes},
             "variants": results,
-            # the codec's share of the graph step (compressed - uncompressed) over its algorithmic
-            # bytes: every codec call of the step, as one number
+            # the codec's share of the graph step (compressed - uncompressed) over the bytes its
+            # calls must move (8 B/elem single launch, 12 B/elem above): every call as one number
             "roofline": {"bound": "hbm", "kernel": "all SmaQ launches of the step",
                          "achieved": g_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(g_gbps / HBM_PEAK_GBPS, 4) if g_gbps else None,
-                         "alg_bytes_per_launch": int(12 * elems), "avg_launch_ms": g_codec,
-                         "traffic": None}}
+                         "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": g_codec,
+                         "traffic": traffic}}
 
 
 def run_smaq_cpu(args, world, rank, device):

@@ -1,0 +1,409 @@
+// torchfast.cpp — the eager per-call host path of SmartFP and S2FP8 in one C call, and the
+// autograd wrapper of SmartFP as a C++ graph node (module _smqtorch, built next to libsmq.so and
+// linked to it and to libtorch).
+//
+// An eager training step that compresses every layer's activation and grad-map issues one codec
+// call per layer output in the forward pass and one per grad-map in the backward pass (reference:
+// smart_compress/util/pytorch/autograd.py:18-47 around smart.py:110-190; bench.py --config
+// autograd_resnet34: 264 calls per step). With ~8 us of device time per call the eager step is
+// bound by the host time of those calls: the Python codec path spent ~6.75 us per call (output
+// allocation through torch's Python binding, the parameter-block copy, the stream query, the
+// workspace lookup, the offset update, the argument conversion), the Python autograd Function
+// around it as much again in each direction. Here:
+//
+//   smaq(state, x, all_positive, bn)        one SmartFP call on the at::Tensor (smq_smaq_roundtrip)
+//   smaq_autograd(state, x, codec, bwd)     Compressor.forward for a SmartFP codec: the forward
+//                                           call plus a C++ Node whose backward compresses the
+//                                           grad-map the same way (autograd.py:37-47)
+//   s2fp8(x, check_inf, rng, getter)        one S2FP8 call on an fp32 device tensor
+//
+// The state object (a capsule of a shared SmaqState) holds the flag templates of the parameter
+// block, built by the Python codec from its hparams, and a snapshot of the hparams values they were
+// built from: a flag changed between calls returns NotImplemented and the codec rebuilds the state.
+// Anything this path does not handle (CPU tensors, float64, sampled or range statistics, BN terms,
+// ratio logging, graph-safe streams, tensors below min_size) returns None and the codec takes its
+// general Python path (in the backward node: the Python codec object is called). Values are those
+// of the Python path bit for bit: the same entry point, parameter block and stream positions, taken
+// in the same call order. Host code only; nothing here crosses the C-ABI (include/smq.h).
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <ATen/core/Tensor.h>
+#include <ATen/ops/empty.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/csrc/autograd/function.h>
+#include <torch/csrc/autograd/functions/utils.h>
+#include <torch/csrc/autograd/python_variable.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+#include "smq.h"
+
+namespace {
+
+// Python objects held by C++ objects that may die on an autograd worker thread
+struct PyRef {
+  PyObject* o = nullptr;
+  PyRef() = default;
+  explicit PyRef(PyObject* p) : o(p) { Py_XINCREF(o); }
+  PyRef(const PyRef&) = delete;
+  PyRef& operator=(const PyRef&) = delete;
+  ~PyRef() {
+    if (o && Py_IsInitialized()) {
+      PyGILState_STATE g = PyGILState_Ensure();
+      Py_DECREF(o);
+      PyGILState_Release(g);
+    }
+  }
+};
+
+// The (device, stream) workspace of the last call: the Python table (smart_compress_amd/_native.py
+// workspace) is asked only when the device, the stream or the needed size changes. The tensor is
+// held here, so the table evicting it never frees memory a queued call still uses.
+struct WsSlot {
+  int dev = -1;
+  hipStream_t st = nullptr;
+  at::Tensor t;
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+// Python getter(device_index, stream, nbytes) -> uint8 device tensor (the codec's _native.workspace)
+bool ws_lookup(WsSlot& w, PyObject* getter, int dev, hipStream_t st, size_t need) {
+  if (w.ptr && w.dev == dev && w.st == st && w.bytes >= need) return true;
+  PyObject* r = PyObject_CallFunction(getter, "iKn", dev, (unsigned long long)(uintptr_t)st,
+                                      (Py_ssize_t)need);
+  if (!r) return false;
+  if (!THPVariable_Check(r)) {
+    Py_DECREF(r);
+    PyErr_SetString(PyExc_TypeError, "workspace getter must return a tensor");
+    return false;
+  }
+  w.t = THPVariable_Unpack(r);
+  Py_DECREF(r);
+  w.dev = dev;
+  w.st = st;
+  w.ptr = w.t.data_ptr();
+  w.bytes = (size_t)w.t.numel();
+  return true;
+}
+
+// rng.__dict__ holds seed / offset (smart_compress_amd/_native.py RngState); the call takes n
+// positions of the stream, under the GIL, as RngState.take.
+PyObject* g_seed = nullptr;
+PyObject* g_offset = nullptr;
+PyObject* g_tag = nullptr;
+PyObject* g_bwd_tag = nullptr;
+
+bool rng_take(PyObject* rng_dict, uint64_t n, uint64_t* seed, uint64_t* offset) {
+  PyObject* s = PyDict_GetItem(rng_dict, g_seed);
+  PyObject* o = PyDict_GetItem(rng_dict, g_offset);
+  if (!s || !o) {
+    PyErr_SetString(PyExc_AttributeError, "RngState without seed / offset");
+    return false;
+  }
+  *seed = PyLong_AsUnsignedLongLongMask(s);
+  *offset = PyLong_AsUnsignedLongLongMask(o);
+  if (PyErr_Occurred()) return false;
+  PyObject* nv = PyLong_FromUnsignedLongLong(*offset + n);  // mod 2^64, as RngState.take
+  if (!nv) return false;
+  const int rc = PyDict_SetItem(rng_dict, g_offset, nv);
+  Py_DECREF(nv);
+  return rc == 0;
+}
+
+// ---- SmartFP ----------------------------------------------------------------------------------
+constexpr int kSnap = 11;
+const char* const kSnapKeys[kSnap] = {
+    "num_bits_main", "num_bits_outlier", "main_std_dev_threshold", "outlier_std_dev_threshold",
+    "stochastic_rounding", "use_range_std_dev", "measure_compression_ratio", "use_sample_stats",
+    "min_size", "precision", "use_batch_norm"};
+PyObject* g_snap_keys[kSnap];
+
+struct SmaqState {
+  SmqSmaqParams tmpl[2];  // [all_positive]
+  int64_t min_size = 8;
+  bool allow_f16 = false;  // precision 16 (smart.py:154's clamp on a half tensor otherwise raises)
+  bool use_bn = false;
+  bool decline = false;    // range or sampled statistics, ratio logging: the Python path
+  PyRef hp_dict;           // hparams.__dict__
+  PyRef snap[kSnap];       // its values when the templates were built
+  PyRef rng_dict;          // codec.rng.__dict__
+  PyRef ws_getter;
+  WsSlot ws;
+};
+using StatePtr = std::shared_ptr<SmaqState>;
+
+void state_capsule_free(PyObject* cap) {
+  delete static_cast<StatePtr*>(PyCapsule_GetPointer(cap, "smq.SmaqState"));
+}
+
+StatePtr* state_of(PyObject* cap) {
+  return static_cast<StatePtr*>(PyCapsule_GetPointer(cap, "smq.SmaqState"));
+}
+
+// smaq_state(template_bytes_allpos0, template_bytes_allpos1, hparams_dict, rng_dict, ws_getter)
+PyObject* smaq_state(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
+  if (nargs != 5) {
+    PyErr_SetString(PyExc_TypeError, "smaq_state(tmpl0, tmpl1, hparams_dict, rng_dict, ws_getter)");
+    return nullptr;
+  }
+  Py_buffer b0, b1;
+  if (PyObject_GetBuffer(a[0], &b0, PyBUF_SIMPLE) < 0) return nullptr;
+  if (PyObject_GetBuffer(a[1], &b1, PyBUF_SIMPLE) < 0) {
+    PyBuffer_Release(&b0);
+    return nullptr;
+  }
+  const bool ok = b0.len == (Py_ssize_t)sizeof(SmqSmaqParams) &&
+                  b1.len == (Py_ssize_t)sizeof(SmqSmaqParams) && PyDict_Check(a[2]) &&
+                  PyDict_Check(a[3]) && PyCallable_Check(a[4]);
+  if (!ok) {
+    PyBuffer_Release(&b0);
+    PyBuffer_Release(&b1);
+    PyErr_SetString(PyExc_TypeError, "smaq_state: bad arguments");
+    return nullptr;
+  }
+  auto s = std::make_shared<SmaqState>();
+  memcpy(&s->tmpl[0], b0.buf, sizeof(SmqSmaqParams));
+  memcpy(&s->tmpl[1], b1.buf, sizeof(SmqSmaqParams));
+  PyBuffer_Release(&b0);
+  PyBuffer_Release(&b1);
+  s->hp_dict.o = a[2];
+  Py_INCREF(a[2]);
+  for (int i = 0; i < kSnap; ++i) {
+    PyObject* v = PyDict_GetItem(a[2], g_snap_keys[i]);  // borrowed (or NULL: absent)
+    Py_XINCREF(v);
+    s->snap[i].o = v;
+  }
+  if (s->snap[8].o) s->min_size = PyLong_AsLongLong(s->snap[8].o);
+  s->allow_f16 = s->snap[9].o && PyLong_AsLong(s->snap[9].o) == 16;
+  s->use_bn = s->snap[10].o && PyObject_IsTrue(s->snap[10].o) == 1;
+  for (int i = 5; i <= 7; ++i)  // use_range_std_dev, measure_compression_ratio, use_sample_stats
+    if (s->snap[i].o && PyObject_IsTrue(s->snap[i].o) == 1) s->decline = true;
+  s->rng_dict.o = a[3];
+  Py_INCREF(a[3]);
+  s->ws_getter.o = a[4];
+  Py_INCREF(a[4]);
+  if (PyErr_Occurred()) return nullptr;
+  auto* holder = new StatePtr(std::move(s));
+  PyObject* cap = PyCapsule_New(holder, "smq.SmaqState", state_capsule_free);
+  if (!cap) delete holder;
+  return cap;
+}
+
+enum RunResult { kError = -1, kDecline = 0, kDone = 1, kStale = 2 };
+
+// One SmartFP call on t (GIL held): kDone with *out set, kDecline (the Python path handles it),
+// kStale (the hparams changed since the state was built), kError (Python error set).
+RunResult smaq_run(SmaqState& s, const at::Tensor& t, bool all_positive, at::Tensor* out) {
+  for (int i = 0; i < kSnap; ++i)
+    if (PyDict_GetItem(s.hp_dict.o, g_snap_keys[i]) != s.snap[i].o) return kStale;
+  if (s.decline || !t.is_cuda()) return kDecline;
+  int code;
+  switch (t.scalar_type()) {
+    case at::kFloat: code = SMQ_DTYPE_F32; break;
+    case at::kBFloat16: code = SMQ_DTYPE_BF16; break;
+    case at::kHalf:
+      if (!s.allow_f16) return kDecline;
+      code = SMQ_DTYPE_F16;
+      break;
+    default: return kDecline;
+  }
+  const int64_t n = t.numel();
+  if (n < s.min_size) return kDecline;
+  at::Tensor x = t.is_contiguous() ? t : t.detach().contiguous();
+  const int dev = x.get_device();
+  const hipStream_t st = c10::hip::getCurrentHIPStream(dev).stream();
+  if (!ws_lookup(s.ws, s.ws_getter.o, dev, st, smq_smaq_workspace_bytes(n))) return kError;
+  SmqSmaqParams p = s.tmpl[all_positive ? 1 : 0];
+  if (!rng_take(s.rng_dict.o, (uint64_t)n, &p.seed, &p.offset)) return kError;
+  at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kFloat));
+  const int rc = smq_smaq_roundtrip(x.const_data_ptr(), code, y.mutable_data_ptr<float>(), n, &p,
+                                    nullptr, s.ws.ptr, s.ws.bytes, st);
+  if (rc) {
+    PyErr_Format(PyExc_RuntimeError, "smq_smaq_roundtrip failed (rc=%d): %s", rc,
+                 smq_last_error());
+    return kError;
+  }
+  *out = std::move(y);
+  return kDone;
+}
+
+// smaq(state, x, all_positive, batch_norm_stats) -> y | None (not handled here) |
+// NotImplemented (the hparams changed: rebuild the state)
+PyObject* smaq(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
+  if (nargs != 4) {
+    PyErr_SetString(PyExc_TypeError, "smaq(state, x, all_positive, batch_norm_stats)");
+    return nullptr;
+  }
+  StatePtr* sp = state_of(a[0]);
+  if (!sp) return nullptr;
+  SmaqState& s = **sp;
+  if (a[3] != Py_None && s.use_bn) Py_RETURN_NONE;
+  if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
+  const int ap = PyObject_IsTrue(a[2]);
+  if (ap < 0) return nullptr;
+  at::Tensor y;
+  switch (smaq_run(s, THPVariable_Unpack(a[1]), ap != 0, &y)) {
+    case kDone: return THPVariable_Wrap(std::move(y));
+    case kDecline: Py_RETURN_NONE;
+    case kStale: Py_RETURN_NOTIMPLEMENTED;
+    default: return nullptr;
+  }
+}
+
+// ---- the autograd wrapper (autograd.py:18-47: Compressor with a SmartFP compress_fn) -----------
+// The backward of `y = compress(x)` is `compress(grad_y)` (tag "backward_autograd"); with the
+// backward direction switched off the grad passes unchanged (autograd.py:40-41).
+struct SmaqCompressBackward : public torch::autograd::Node {
+  StatePtr state;   // nullptr: backward compression off
+  PyRef codec;      // the Python codec: what the C path declines or a stale state goes to
+
+  torch::autograd::variable_list apply(torch::autograd::variable_list&& grads) override {
+    at::Tensor g = grads[0];
+    if (!task_should_compute_output(0)) return {at::Tensor()};
+    if (!g.defined() || !state) return {g};
+    PyGILState_STATE gs = PyGILState_Ensure();
+    at::Tensor out;
+    RunResult r = smaq_run(*state, g, false, &out);
+    if (r == kDecline || r == kStale) {  // the codec's own call (it rebuilds a stale state)
+      PyObject* gv = THPVariable_Wrap(g);
+      PyObject* res = nullptr;
+      if (gv) {
+        PyObject* args = PyTuple_Pack(1, gv);
+        PyObject* kw = args ? PyDict_New() : nullptr;
+        if (kw && PyDict_SetItem(kw, g_tag, g_bwd_tag) == 0)
+          res = PyObject_Call(codec.o, args, kw);
+        Py_XDECREF(kw);
+        Py_XDECREF(args);
+        Py_DECREF(gv);
+      }
+      if (res && THPVariable_Check(res)) {
+        out = THPVariable_Unpack(res);
+        r = kDone;
+      } else {
+        if (res) PyErr_SetString(PyExc_TypeError, "codec returned a non-tensor");
+        r = kError;
+      }
+      Py_XDECREF(res);
+    }
+    if (r != kDone) {
+      std::string msg = "SmaqCompressBackward: codec call failed";
+      PyObject *t, *v, *tb;
+      PyErr_Fetch(&t, &v, &tb);
+      if (v) {
+        PyObject* str = PyObject_Str(v);
+        if (str) {
+          const char* c = PyUnicode_AsUTF8(str);
+          if (c) msg += std::string(": ") + c;
+          Py_DECREF(str);
+        }
+      }
+      Py_XDECREF(t);
+      Py_XDECREF(v);
+      Py_XDECREF(tb);
+      PyErr_Clear();
+      PyGILState_Release(gs);
+      throw std::runtime_error(msg);
+    }
+    PyGILState_Release(gs);
+    return {out};
+  }
+  std::string name() const override { return "SmaqCompressBackward"; }
+};
+
+// smaq_autograd(state, x, codec, backward) -> y | None | NotImplemented: Compressor.forward for
+// x alone (no batch_norm_stats argument); y carries a SmaqCompressBackward node when x requires
+// grad and grad mode is on.
+PyObject* smaq_autograd(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
+  if (nargs != 4) {
+    PyErr_SetString(PyExc_TypeError, "smaq_autograd(state, x, codec, backward)");
+    return nullptr;
+  }
+  StatePtr* sp = state_of(a[0]);
+  if (!sp) return nullptr;
+  if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
+  const int bwd = PyObject_IsTrue(a[3]);
+  if (bwd < 0) return nullptr;
+  const at::Tensor& x = THPVariable_Unpack(a[1]);
+  at::Tensor y;
+  switch (smaq_run(**sp, x, false, &y)) {
+    case kDone: break;
+    case kDecline: Py_RETURN_NONE;
+    case kStale: Py_RETURN_NOTIMPLEMENTED;
+    default: return nullptr;
+  }
+  if (torch::autograd::compute_requires_grad(x)) {
+    auto node = std::shared_ptr<SmaqCompressBackward>(new SmaqCompressBackward(),
+                                                      torch::autograd::deleteNode);
+    if (bwd) node->state = *sp;
+    node->codec.o = a[2];
+    Py_INCREF(a[2]);
+    node->set_next_edges(torch::autograd::collect_next_edges(x));
+    torch::autograd::set_history(y, node);
+  }
+  return THPVariable_Wrap(std::move(y));
+}
+
+// ---- S2FP8 (fp32 device tensors at precision 32, s2fp8.py:27-48) --------------------------------
+WsSlot g_s2_ws;
+
+// s2fp8(x, check_inf, rng_dict, ws_getter) -> y | None (not an fp32 device tensor)
+PyObject* s2fp8(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
+  if (nargs != 4) {
+    PyErr_SetString(PyExc_TypeError, "s2fp8(x, check_inf, rng_dict, ws_getter)");
+    return nullptr;
+  }
+  if (!THPVariable_Check(a[0]) || !PyDict_Check(a[2])) Py_RETURN_NONE;
+  const at::Tensor& t = THPVariable_Unpack(a[0]);
+  if (!t.is_cuda() || t.scalar_type() != at::kFloat) Py_RETURN_NONE;
+  const int64_t n = t.numel();
+  const int check_inf = PyObject_IsTrue(a[1]);
+  if (check_inf < 0) return nullptr;
+  at::Tensor x = t.is_contiguous() ? t : t.detach().contiguous();
+  at::Tensor y = at::empty(x.sizes(), x.options());
+  if (n == 0) return THPVariable_Wrap(std::move(y));
+  const int dev = x.get_device();
+  const hipStream_t st = c10::hip::getCurrentHIPStream(dev).stream();
+  if (!ws_lookup(g_s2_ws, a[3], dev, st, smq_s2fp8_workspace_bytes(1))) return nullptr;
+  uint64_t seed, offset;
+  if (!rng_take(a[2], (uint64_t)n, &seed, &offset)) return nullptr;
+  const int rc = smq_s2fp8_roundtrip(x.const_data_ptr(), SMQ_DTYPE_F32, y.mutable_data_ptr(), n, 32,
+                                     check_inf, nullptr, seed, offset, nullptr, nullptr,
+                                     g_s2_ws.ptr, g_s2_ws.bytes, st);
+  if (rc) {
+    PyErr_Format(PyExc_RuntimeError, "smq_s2fp8_roundtrip failed (rc=%d): %s", rc,
+                 smq_last_error());
+    return nullptr;
+  }
+  return THPVariable_Wrap(std::move(y));
+}
+
+PyMethodDef kMethods[] = {
+    {"smaq_state", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_state)),
+     METH_FASTCALL, "SmartFP hot-path state from its parameter templates and hparams"},
+    {"smaq", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq)), METH_FASTCALL,
+     "one eager SmartFP call (smq_smaq_roundtrip), or None / NotImplemented"},
+    {"smaq_autograd",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_autograd)), METH_FASTCALL,
+     "Compressor.forward with a SmartFP codec: y and its SmaqCompressBackward node"},
+    {"s2fp8", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(s2fp8)), METH_FASTCALL,
+     "one eager S2FP8 call on an fp32 device tensor (smq_s2fp8_roundtrip), or None"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_smqtorch", nullptr, -1, kMethods,
+                       nullptr, nullptr, nullptr, nullptr};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__smqtorch(void) {
+  g_seed = PyUnicode_InternFromString("seed");
+  g_offset = PyUnicode_InternFromString("offset");
+  g_tag = PyUnicode_InternFromString("tag");
+  g_bwd_tag = PyUnicode_InternFromString("backward_autograd");
+  for (int i = 0; i < kSnap; ++i) g_snap_keys[i] = PyUnicode_InternFromString(kSnapKeys[i]);
+  return PyModule_Create(&kModule);
+}

@@ -340,28 +340,60 @@ _fast = None
 _fast_tried = False
 
 
-def fast():
-    """The CPython fast-call binding of smq_smaq_roundtrip (csrc/pyfast.cpp) built next to the
-    library being used, or None (an experiment library elsewhere, SMQ_LIB: then ctypes). It calls
-    the same libsmq.so (rpath $ORIGIN = the directory of LIB_PATH), only without ctypes' ~4 us of
-    argument conversion per call."""
-    global _fast, _fast_tried
-    if _fast_tried:
-        return _fast
+def _load_binding(name: str):
+    """A binding module built next to the library being used (lib/<name><EXT_SUFFIX>), or None
+    when there is none (an experiment library elsewhere, SMQ_LIB). Bindings call the same
+    libsmq.so (rpath $ORIGIN = the directory of LIB_PATH)."""
     lib()  # the ABI check, and the library every entry point shares
     import importlib.machinery
     import importlib.util
     import sysconfig
 
-    path = os.path.join(os.path.dirname(LIB_PATH), "_smqfast" + sysconfig.get_config_var("EXT_SUFFIX"))
-    if os.path.exists(path):
-        loader = importlib.machinery.ExtensionFileLoader("_smqfast", path)
-        spec = importlib.util.spec_from_file_location("_smqfast", path, loader=loader)
-        mod = importlib.util.module_from_spec(spec)
-        loader.exec_module(mod)
-        _fast = mod
+    path = os.path.join(os.path.dirname(LIB_PATH), name + sysconfig.get_config_var("EXT_SUFFIX"))
+    if not os.path.exists(path):
+        return None
+    loader = importlib.machinery.ExtensionFileLoader(name, path)
+    spec = importlib.util.spec_from_file_location(name, path, loader=loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    return mod
+
+
+def fast():
+    """The CPython fast-call binding of smq_smaq_roundtrip / smq_s2fp8_roundtrip
+    (csrc/pyfast.cpp), or None (then ctypes): the same calls without ctypes' ~4 us of argument
+    conversion per call."""
+    global _fast, _fast_tried
+    if _fast_tried:
+        return _fast
+    _fast = _load_binding("_smqfast")
     _fast_tried = True
     return _fast
+
+
+_torch_fast = None
+_torch_fast_tried = False
+
+
+def torch_fast():
+    """The at::Tensor-level binding (csrc/torchfast.cpp: the eager SmartFP / S2FP8 call and the
+    SmartFP autograd node), or None (then the Python hot paths). SMQ_TORCHFAST=0 disables it (the
+    A/B switch of tools/host_cost_smaq.py)."""
+    global _torch_fast, _torch_fast_tried
+    if _torch_fast_tried:
+        return _torch_fast
+    if os.environ.get("SMQ_TORCHFAST", "1") != "0":
+        _torch_fast = _load_binding("_smqtorch")
+    _torch_fast_tried = True
+    return _torch_fast
+
+
+def ws_getter(kind: str):
+    """The workspace callback of the C hot paths: (device index, stream, nbytes) -> the
+    (kind, device, stream) workspace of this table."""
+    def get(dev: int, stream: int, nbytes: int) -> torch.Tensor:
+        return workspace(kind, torch.device("cuda", dev), nbytes, stream)
+    return get
 
 
 def check(rc: int, what: str) -> None:

@@ -102,11 +102,23 @@ class S2FP8(CompressionAlgorithmBase):
         return y
 
 
+    _ws_get = None
+
     def _call_device_f32(self, tensor: torch.Tensor) -> torch.Tensor:
-        """The eager hot path (an fp32 device tensor at precision 32): the same call as the general
-        path with its per-call Python trimmed — a C-level stream query, one lookup in the bounded
-        per-(device, stream) workspace table (_native.workspace), the fast-call binding — since at
-        BERT-hidden size (C4) the host enqueue is as long as the launch."""
+        """The eager hot path (an fp32 device tensor at precision 32): at BERT-hidden size (C4) the
+        host enqueue is as long as the launch. Host offsets: one C call on the tensor
+        (csrc/torchfast.cpp: allocation, stream, workspace, stream position, launch); graph-safe
+        streams or no binding: the same call with its per-call Python trimmed — a C-level stream
+        query, one lookup in the bounded per-(device, stream) workspace table
+        (_native.workspace), the fast-call binding."""
+        T = N._torch_fast if N._torch_fast_tried else N.torch_fast()
+        if T is not None and not _q._graph_safe:
+            get = S2FP8._ws_get
+            if get is None:
+                get = S2FP8._ws_get = N.ws_getter("s2fp8")
+            y = T.s2fp8(tensor, self.hparams.float_quantize_check_inf, _q.quant_rng().__dict__, get)
+            if y is not None:
+                return y
         x = tensor if tensor.is_contiguous() else tensor.detach().contiguous()
         y = torch.empty_like(x, requires_grad=False)
         n = x.numel()

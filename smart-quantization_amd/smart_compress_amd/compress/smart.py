@@ -239,6 +239,46 @@ class SmartFP(CompressionAlgorithmBase):
         p.bn_inner = data.shape[2] * data.shape[3]
         return gamma, beta  # keep alive until the launch is enqueued
 
+    # -- the C hot path (csrc/torchfast.cpp) --------------------------------------------------------
+    # A capsule holding the flag templates of the parameter block and a snapshot of the hparams
+    # they were built from; None: not built yet; False: unavailable (no binding, graph-safe random
+    # stream, a subclass with its own __call__). Rebuilt when the hparams, the random stream or the
+    # graph-safe switch are replaced (__setattr__), or when the C side finds a flag changed.
+    _hot = None
+
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if name in ("hparams", "rng", "_graph_safe"):
+            object.__setattr__(self, "_hot", None)
+
+    def _build_hot(self):
+        T = N.torch_fast()
+        hp = self.hparams
+        d = hp if isinstance(hp, dict) else getattr(hp, "__dict__", None)
+        hot = False
+        if (T is not None and not self._graph_safe and type(d) is dict
+                and type(self).__call__ is SmartFP.__call__):
+            hot = T.smaq_state(bytes(self._flag_params(False)), bytes(self._flag_params(True)),
+                               d, self.rng.__dict__, N.ws_getter("smaq"))
+        object.__setattr__(self, "_hot", hot)
+        return hot
+
+    def _autograd_fast(self, x: torch.Tensor, backward: bool):
+        """Compressor.forward for this codec in C (util/pytorch/autograd.py): y = self(x) and a
+        C++ autograd node whose backward is self(grad_y, tag="backward_autograd"); None when the C
+        path does not take this call (the Python Function then does)."""
+        hot = self._hot
+        if hot is None:
+            hot = self._build_hot()
+        if hot is False or Globals.profiler is not None or self._trace is not None:
+            return None
+        y = N._torch_fast.smaq_autograd(hot, x, self, backward)
+        if y is NotImplemented:  # a flag changed since the state was built
+            if self._build_hot() is False:
+                return None
+            y = N._torch_fast.smaq_autograd(self._hot, x, self, backward)
+        return y
+
     # -- call --------------------------------------------------------------------------------------
     def __call__(
         self,
@@ -248,13 +288,26 @@ class SmartFP(CompressionAlgorithmBase):
         batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
         **_,
     ):
-        # The hot path — a ROCm fp32 / fp16 / bf16 tensor of at least min_size elements, no BN
-        # term, no ratio logging, no profiler: the library writes a fresh output buffer and no
-        # autograd op runs, so there is no grad-mode switch (torch.no_grad costs ~1.5 us), and the
-        # launch goes through the fast-call binding (ctypes' argument conversion costs ~4 us).
-        # An eager training step that compresses every layer is bound by this host time
-        # (bench.py --config autograd_resnet34). Everything else: _call, under torch.no_grad as
-        # smart.py:110.
+        # The hot path — a ROCm fp32 / fp16 / bf16 tensor of at least min_size elements, full
+        # statistics, no BN term, no ratio logging, no profiler — is one C call on the tensor
+        # (csrc/torchfast.cpp): an eager training step that compresses every layer is bound by the
+        # host time of these calls (bench.py --config autograd_resnet34). No autograd op runs on
+        # it (a fresh output the library writes), so it needs no grad-mode switch.
+        hot = self._hot
+        if hot is None:
+            hot = self._build_hot()
+        if hot is not False and Globals.profiler is None and self._trace is None:
+            y = N._torch_fast.smaq(hot, data, all_positive, batch_norm_stats)
+            if y is not None:
+                if y is not NotImplemented:
+                    return y
+                if self._build_hot() is not False:  # a flag changed: rebuild, call again
+                    y = N._torch_fast.smaq(self._hot, data, all_positive, batch_norm_stats)
+                    if y is not None:
+                        return y
+        # Without the binding (or on graph-safe streams): the same call through the CPython
+        # fast-call binding (ctypes' argument conversion costs ~4 us). Everything else: _call,
+        # under torch.no_grad as smart.py:110.
         hp = self.hparams
         fast = N._fast if N._fast_tried else N.fast()
         if (fast is not None and data.is_cuda and not hp.measure_compression_ratio

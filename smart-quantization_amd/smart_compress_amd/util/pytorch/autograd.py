@@ -10,8 +10,13 @@ every layer ``is_valid_layer_type`` selects.
 
 Implementation note: one module-level autograd Function carries a small spec object (codec +
 direction flags) instead of a Function class built per Compressor. With this package's codecs
-each call is two launches on the caller's stream and no host synchronisation (unless
-compression-ratio logging is on).
+each call is one or two launches on the caller's stream and no host synchronisation (unless
+compression-ratio logging is on). When ``compress_fn`` is a ``SmartFP`` codec (the reference's
+train.py:198-213 passes the codec instance itself), the forward call and a C++ autograd node whose
+backward compresses the grad-map are created in one C call (csrc/torchfast.cpp,
+``SmartFP._autograd_fast``): an eager step that compresses every layer is bound by the host time
+of these calls, and the Python Function costs as much as the codec call in each direction. The
+calls, their order and their values are the same as through the Python Function.
 """
 
 from argparse import Namespace
@@ -67,11 +72,18 @@ class Compressor(nn.Module):
     def __init__(self, compress_fn, forward=True, backward=True):
         super().__init__()
         self._spec = _Spec(compress_fn, bool(forward), bool(backward))
+        # the codec's C autograd path (SmartFP._autograd_fast), for the forward-compressing case
+        self._fast = getattr(compress_fn, "_autograd_fast", None) if forward else None
 
     def compress_fn(self, x: torch.Tensor, *args):
         return _CodecFunction.apply(x, self._spec, *args)
 
     def forward(self, x: torch.Tensor, *args):
+        fast = self._fast
+        if fast is not None and not args:
+            y = fast(x, self._spec.backward)
+            if y is not None:
+                return y
         return self.compress_fn(x, *args)
 
 

@@ -14,8 +14,11 @@ from helpers import smaq_hparams
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [5, 4095, 4099, 65536, 1 << 20, (1 << 20) + 3, 3 * (1 << 20) + 5, 1 << 22, (1 << 22) + 16,
-         6 << 20, 8 << 20, 8388611, (8 << 20) + 4]
+# groups per lane V = ceil((n / 4) / 2^18): every V from 1 to 8 (V = 2 / 3 take the u0lds hand-off
+# from waves 4..4+V-1; V = 7 splits its rounding draws between LDS and the transform and makes the
+# largest LDS request), both sides of the 8,388,611 single-launch limit
+SIZES = [5, 4095, 4099, 65536, 1 << 20, (1 << 20) + 3, 1_500_000, 2_500_000, 3 * (1 << 20) + 5,
+         1 << 22, (1 << 22) + 16, 6 << 20, 6_500_000, 7 << 20, 8 << 20, 8388611, (8 << 20) + 4]
 MODES = ["normal", "trunc", "range", "allpos", "counter", "count", "f16", "bf16"]
 
 
@@ -91,7 +94,7 @@ def test_single_launch_equals_two_launch_paths(n, mode):
             assert o == o0, path
 
 
-@pytest.mark.parametrize("n", [(1 << 20) + 3, (1 << 22) + 16, 8388611])
+@pytest.mark.parametrize("n", [(1 << 20) + 3, 2_500_000, (1 << 22) + 16, 6_500_000, 8388611])
 @pytest.mark.parametrize("mode", ["normal", "range", "f16"])
 def test_single_launch_vs_oracle(n, mode):
     """Device statistics within 1 ulp (fp32) / one half step of the fp64 oracle; outputs equal the
@@ -120,7 +123,8 @@ def test_single_launch_vs_oracle(n, mode):
     assert int((yh.view(np.uint32) != y_or.view(np.uint32)).sum()) == 0
 
 
-@pytest.mark.parametrize("n", [1 << 20, (1 << 22) + 16, 8388611])
+@pytest.mark.parametrize("n", [1 << 20, 1_500_000, 2_500_000, (1 << 22) + 16, 6_500_000, 7 << 20,
+                               8388611])
 def test_single_launch_without_co_residency(n):
     """SMQ_SMAQ_TEST_LATE: half of the workgroups start ~500 us late and the others compute the
     partials they miss after 20 us. Same bytes as the undisturbed call."""

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-5 evidence on one box: the GPU suite, smoke, a bench line of every config, then a kernel
+# trace + FETCH / WRITE passes per profiled config (tools/profile_round.sh; summarised on the host
+# by tools/pmc_traffic.py into profiles/<tag>_*). Each step under its own time limit; the first
+# failure ends the script.
+# Usage: bash tools/gpu_round5.sh <tag>
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R"
+TAG=${1:-r5a}
+mkdir -p gpurun_out
+timeout -k 10 800 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu \
+  > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { tail -n 30 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
+tail -n 2 gpurun_out/${TAG}_gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit 1
+tail -n 1 gpurun_out/${TAG}_smoke.log
+: > gpurun_out/${TAG}_bench.jsonl
+timeout -k 10 300 python -u bench.py >> gpurun_out/${TAG}_bench.jsonl 2> gpurun_out/${TAG}_bench.err || exit 1
+for c in multi packed s2fp8 fp8 autograd autograd_resnet34; do
+  timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline >> gpurun_out/${TAG}_bench.jsonl \
+    2>> gpurun_out/${TAG}_bench.err || exit 1
+done
+for c in smaq multi packed s2fp8 fp8 autograd_resnet34; do
+  bash tools/profile_round.sh ${TAG}_$c $c > /dev/null || exit 1
+done
+echo done

@@ -51,10 +51,35 @@ def main():
     def fwd_bwd():
         comp(xg).sum().backward()
 
+    slow = SmartFP(hp)
+    object.__setattr__(slow, "_hot", False)  # the Python hot path (no C state)
+    slow(x)
+    comp_py = Compressor(lambda v, tag=None, **kw: c(v, tag=tag, **kw))  # the Python Function
+
+    def fwd_bwd_py():
+        comp_py(xg).sum().backward()
+
+    # a chain of 16 compressors: the backward of one call is the next call's input, so the
+    # per-call backward cost is not hidden behind one engine start per backward()
+    chain, chain_py = [Compressor(c) for _ in range(16)], [comp_py] * 16
+
+    def chain_fn(cs):
+        def f():
+            v = xg
+            for cc in cs:
+                v = cc(v)
+            v.sum().backward()
+        return f
+
     out = {
         "smartfp_call": per_call(lambda: c(x)),
+        "smartfp_call_python_path": per_call(lambda: slow(x)),
         "autograd_fwd": per_call(lambda: comp(xg)),
+        "autograd_fwd_python_function": per_call(lambda: comp_py(xg)),
+        "autograd_chain16_fwd_bwd": per_call(chain_fn(chain), 300),
+        "autograd_chain16_fwd_bwd_python_function": per_call(chain_fn(chain_py), 300),
         "autograd_fwd_bwd": per_call(fwd_bwd, 1000),
+        "autograd_fwd_bwd_python_function": per_call(fwd_bwd_py, 1000),
         "plain_fwd_bwd": per_call(lambda: (xg * 1.0).sum().backward(), 1000),
         "params": per_call(lambda: c._params(n, False, x.dtype, x.device)),
         "empty": per_call(lambda: torch.empty(x.shape, dtype=torch.float32, device=x.device)),
