@@ -297,6 +297,30 @@ def _cpu_threads():
     return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
 
 
+def _host_info():
+    """What the CPU baseline ran on: the host CPU model, the machine's logical CPUs and its load
+    (the baseline moves between boxes with both)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    load = os.getloadavg() if hasattr(os, "getloadavg") else None
+    return {"cpu_model": model, "machine_cpus": os.cpu_count(),
+            "loadavg_1m": None if load is None else round(load[0], 2)}
+
+
+def _spread(per_rep_bytes, ts):
+    """min / median / max of the per-repetition rate (GB/s) over the timed repetitions."""
+    r = sorted(per_rep_bytes / t / 1e9 for t in ts)
+    return {"min": round(r[0], 4), "median": round(float(np.median(r)), 4), "max": round(r[-1], 4),
+            "reps": len(r)}
+
+
 def _time_reps(fn, budget_s, min_reps=2):
     fn()  # warm-up (allocator, thread pool)
     reps, t_tot, ts = 0, 0.0, []
@@ -323,8 +347,8 @@ def cpu_baseline_smaq(args, sampled=False):
     ns = 16 if sampled else 0
     try:
         x = torch.randn(args.cpu_sample, generator=torch.Generator().manual_seed(0))
-        reps, t_tot, _ = _time_reps(lambda: smaq_torch.roundtrip(x, num_samples=ns),
-                                    args.cpu_budget)
+        reps, t_tot, ts = _time_reps(lambda: smaq_torch.roundtrip(x, num_samples=ns),
+                                     args.cpu_budget)
         torch.manual_seed(0)
         x1 = torch.randn(1 << 20)
         _, _, t1 = _time_reps(lambda: smaq_torch.roundtrip(x1, num_samples=ns), 0.0, min_reps=30)
@@ -337,7 +361,9 @@ def cpu_baseline_smaq(args, sampled=False):
             "sample": f"{reps} x {args.cpu_sample} fp32 N(0,1) round trips, oracle/smaq_torch.py "
                       f"(smart.py's torch-CPU op sequence, {'sampled(16)' if sampled else 'full'} "
                       f"stats + rand_like SR), {threads} threads, {t_tot:.1f} s",
-            "c1_1M": {"ms_median": round(c1_ms, 3),
+            "spread_gbps": _spread(per * args.cpu_sample, ts),
+            "c1_1M": {"ms_median": round(c1_ms, 3), "ms_min": round(min(t1) * 1e3, 3),
+                      "ms_max": round(max(t1) * 1e3, 3),
                       "gbps": round(per * (1 << 20) / (c1_ms * 1e-3) / 1e9, 4), "reps": len(t1)}}
 
 
@@ -967,8 +993,10 @@ def run_autograd(args, world, rank, device):
 
     import torch.nn.functional as F
 
+    from smart_compress_amd.compress.packed import SmartFPPacked
     from smart_compress_amd.compress.smart import SmartFP
     from smart_compress_amd.util.pytorch.autograd import register_autograd_module
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
 
     batch = 128
     resnet = args.config == "autograd_resnet34"
@@ -977,29 +1005,36 @@ def run_autograd(args, world, rank, device):
     t = torch.randint(0, 10, (batch,), device=device)
     flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
 
-    def build(compress, sizes=None):
+    def build(compress, sizes=None, packed=False):
         """The network; with compression the SmartFP codec itself is registered (train.py:198-213
         passes the codec instance), so Compressor takes the codec's C autograd path. sizes: a list
-        that records the element count of every codec call instead (one counting step)."""
+        that records the element count of every codec call instead (one counting step). packed:
+        the activations autograd saves are held as SmaQ streams (util/pytorch/saved.py)."""
         torch.manual_seed(0)
         net = (_ResNet() if resnet else _vgg_cifar()).to(device)
         opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9)
         codec = None
         if compress:
-            codec = SmartFP(smaq_hparams())
+            codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
             codec.rng.seed = 3000 + rank
-            fn = codec
+            fn = PackedActivations(codec) if packed else codec
             if sizes is not None:
                 def fn(v, tag=None, **kw):
                     sizes.append(v.numel())
                     return codec(v, tag=tag, **kw)
             register_autograd_module(net, fn, flags)
+            if packed:
+                codec = fn
         return net, opt, codec
 
-    def step_fn(net, opt):
+    def step_fn(net, opt, acts=None):
         def step():
             opt.zero_grad(set_to_none=False)
-            loss = F.cross_entropy(net(x), t)
+            if acts is None:
+                loss = F.cross_entropy(net(x), t)
+            else:
+                with acts:  # saved activations held as streams
+                    loss = F.cross_entropy(net(x), t)
             loss.backward()
             opt.step()
         return step
@@ -1016,9 +1051,10 @@ def run_autograd(args, world, rank, device):
     del net, opt
 
     results = {}
-    for name in ("uncompressed", "smaq_eager", "smaq_graph"):
-        net, opt, codec = build(name != "uncompressed")
-        step = step_fn(net, opt)
+    for name in ("uncompressed", "smaq_eager", "smaq_graph", "smaq_eager_packed_saved"):
+        packed = name == "smaq_eager_packed_saved"
+        net, opt, codec = build(name != "uncompressed", packed=packed)
+        step = step_fn(net, opt, codec if packed else None)
         if name == "smaq_graph":
             codec.graph_safe(device=device)
             s = torch.cuda.Stream(device)
@@ -1035,16 +1071,32 @@ def run_autograd(args, world, rank, device):
             run = step
         run()
         torch.cuda.synchronize()
+        mem = None
+        if name != "smaq_graph":  # (a graph's memory is its private pool, allocated at capture)
+            before = torch.cuda.memory_allocated(device)
+            torch.cuda.reset_peak_memory_stats(device)
+            run()
+            torch.cuda.synchronize()
+            peak = torch.cuda.max_memory_allocated(device)
+            mem = {"peak_allocated_mib": round(peak / 2**20, 1),
+                   "step_peak_above_resident_mib": round((peak - before) / 2**20, 1)}
         for _ in range(args.warmup):
             run()
         elapsed = time_steps(run, args.steps, 0, world, device)
         results[name] = {"ms_per_step": round(elapsed / args.steps * 1e3, 4)}
+        if mem:
+            results[name]["memory"] = mem
         if name != "uncompressed":
             results[name].update(codec_calls_per_step=calls_per,
                                  compressed_elements_per_step=elems)
+        if packed:
+            st = codec.stats()
+            results[name]["saved_streams"] = {
+                "saved_tensors_packed_per_step": round(st["saved_packed"] / (args.steps + args.warmup + 2), 1),
+                "bits_per_element": round(st["bits_per_element"], 3) if st["bits_per_element"] else None}
         del net, opt, codec, run
     base_ms = results["uncompressed"]["ms_per_step"]
-    for name in ("smaq_eager", "smaq_graph"):
+    for name in ("smaq_eager", "smaq_graph", "smaq_eager_packed_saved"):
         codec_ms = results[name]["ms_per_step"] - base_ms
         results[name]["codec_ms_per_step"] = round(codec_ms, 4)
         results[name]["codec_gbps_12B"] = round(12.0 * elems / (codec_ms * 1e-3) / 1e9, 1) \
@@ -1176,6 +1228,7 @@ def main():
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and args.config in CPU_BASELINES:
             res["cpu_baseline"] = CPU_BASELINES[args.config](args)
+            res["cpu_baseline"]["host"] = _host_info()
         print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist

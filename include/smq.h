@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SMQ_ABI_VERSION 6
+#define SMQ_ABI_VERSION 7
 
 #define SMQ_OK 0
 #define SMQ_ERR_INVALID -1  /* bad argument */
@@ -544,6 +544,21 @@ int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream);
  * ~6 % faster). A stream whose header records other widths leaves y untouched. */
 int smq_smaq_decompress_ex(const void* packed, float* y, int64_t n, int num_bits_main,
                            int num_bits_outlier, void* stream);
+/* Workspace of smq_smaq_compress / smq_cpu_smaq_compress with SMQ_STATS_SAMPLED_DEVICE and
+ * num_samples samples (above SMQ_MAX_DEVICE_SAMPLES the multi-workgroup draw's region comes first:
+ * smart.py:86-91 for any k the unpacked codec takes). Equals smq_smaq_pack_workspace_bytes(n) for
+ * num_samples <= SMQ_MAX_DEVICE_SAMPLES. */
+size_t smq_smaq_pack_workspace_bytes_sampled(int64_t n, int64_t num_samples);
+/* Host twins for CPU tensors (host pointers; smart.py:110-190 runs on any device): the same
+ * statistics as smq_cpu_smaq_roundtrip, the same codes and the same stream layout as
+ * smq_smaq_compress — byte for byte the device stream whenever the statistics agree (they are fp64
+ * sums in another fixed order: equal but for rare last-bit cases) — and its decoder, which reads
+ * any version-2 stream. Synchronous, on n_threads threads; workspace as smq_smaq_compress's first
+ * region (smq_smaq_workspace_bytes[_sampled] bytes: the statistics header is left at its start). */
+int smq_cpu_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
+                          void* packed, size_t packed_bytes, void* workspace,
+                          size_t workspace_bytes, int n_threads);
+int smq_cpu_smaq_decompress(const void* packed, float* y, int64_t n, int n_threads);
 
 #ifdef __cplusplus
 }

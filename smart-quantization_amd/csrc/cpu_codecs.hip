@@ -436,14 +436,17 @@ static float range_coef_host(const SmqSmaqParams* p, int64_t n) {
   return 1.0f / sqrtf(2.0f * lg);
 }
 
+// The call's statistics (full, host-given or drawn samples, injected) into *st; *base = the host
+// mirror of the graph-safe stream position (params.offset_counter), not yet advanced.
 template <int T>
-static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParams* p,
-                          const float* uniforms, const SmqSmaqStats* stats_in, char* ws,
-                          size_t ws_bytes, int n_threads) {
-  SmqSmaqStats st;
+static int host_stats(const void* x, int64_t n, const SmqSmaqParams* p,
+                      const SmqSmaqStats* stats_in, char* ws, size_t ws_bytes, int n_threads,
+                      SmqSmaqStats* out, uint64_t* base_out) {
+  SmqSmaqStats& st = *out;
   // a host uint64 stream position (graph-safe mirror), advanced by n only once the call is
   // validated: a rejected call consumes no stream positions, like the device entry points
   const uint64_t base = p->offset_counter ? *p->offset_counter : 0ull;
+  *base_out = base;
   switch (p->stats_source) {
     case SMQ_STATS_WORKSPACE:
       full_stats<T>(x, n, p, range_coef_host(p, n), n_threads, &st);
@@ -490,6 +493,17 @@ static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParam
       st.quot_check = quot_check_for(st.std_clamped);
     }
   }
+  return SMQ_OK;
+}
+
+template <int T>
+static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParams* p,
+                          const float* uniforms, const SmqSmaqStats* stats_in, char* ws,
+                          size_t ws_bytes, int n_threads) {
+  SmqSmaqStats st;
+  uint64_t base = 0;
+  const int rc = host_stats<T>(x, n, p, stats_in, ws, ws_bytes, n_threads, &st, &base);
+  if (rc) return rc;
   if (p->offset_counter) *p->offset_counter = base + (uint64_t)n;
   st.rng_offset = base;
   SmaqCtx c;
@@ -521,6 +535,311 @@ static int smaq_roundtrip(const void* x, float* y, int64_t n, const SmqSmaqParam
   uint64_t* slots = reinterpret_cast<uint64_t*>(ws + SMQ_WS_OUTLIER_SLOTS_OFFSET);
   for (int i = 0; i < SMQ_WS_OUTLIER_SLOTS; ++i) slots[i] = 0;
   if (p->count_outliers) slots[0] = n_out;
+  return SMQ_OK;
+}
+
+// ---- packed container (include/smq.h "Packed SmaQ container", format version 2) -----------------
+// The host twin of smq_smaq_compress / smq_smaq_decompress (smaq_pack.hip): the same codes (the
+// quantisation of smaq_task, i.e. the device's smaq_quant), the same block layout, the same bytes
+// for the same statistics and random stream (oracle/smaq_packed.py restates the format; the GPU
+// tests compare the two libraries' streams). Tasks of kPackTaskBlocks blocks: every block's fixed
+// section is written in place, its variable section into a per-block buffer that is copied to its
+// prefix-sum place once all sizes are known.
+constexpr int kPB = SMQ_PACK_BLOCK;
+constexpr int kPackTaskBlocks = 16;
+
+static inline size_t pk_fixed_words(int wm) { return 128 + (size_t)wm * (kPB / 32); }
+static inline int64_t pk_dir_entries(int64_t nb) { return nb + (nb & 1); }
+
+// LSB-first bit writer over uint32 words (zeroed by the caller)
+static inline void put_bits(uint32_t* w, uint64_t bitpos, uint32_t v, int width) {
+  const uint64_t word = bitpos >> 5;
+  const int sh = (int)(bitpos & 31);
+  w[word] |= v << sh;
+  if (sh + width > 32) w[word + 1] |= v >> (32 - sh);
+}
+
+static inline uint32_t get_bits(const uint32_t* w, uint64_t bitpos, int width) {
+  const uint64_t word = bitpos >> 5;
+  const int sh = (int)(bitpos & 31);
+  uint64_t v = w[word] >> sh;
+  if (sh + width > 32) v |= (uint64_t)w[word + 1] << (32 - sh);
+  return (uint32_t)(v & ((1ull << width) - 1ull));
+}
+
+struct PackHostCtx {
+  SmaqCtx c;
+  int wm, wo, we, rm;
+  int64_t n;
+};
+
+// smart.py:144-169 for element i: q and the two sides (smaq_task's quantisation)
+template <int T, int RM, bool BN>
+static inline float quant_host(const SmaqCtx& c, int64_t i, bool& hi, bool& lo) {
+  constexpr int TZ = BN ? kF32 : T;
+  float v = ld<T>(c.x, i);
+  if (BN) {
+    const int64_t ch = (i / c.bn_inner) % c.bn_channels;
+    v = (v - c.bn_beta[ch]) / c.bn_gamma[ch];
+  }
+  const float dm = rin<TZ>(v - c.mean);
+  const float z = rin<TZ>(dm / c.sc);
+  hi = z > c.cthr;
+  lo = z < c.cnthr;
+  const bool o = hi || lo;
+  const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);
+  const float r = o ? c.r_out : c.r_main;
+  const float d = (z + a) * r;
+  if (RM == kRoundTrunc) return truncf(d);
+  const float f = floorf(d);
+  const float fr = d - f;
+  float t;
+  if (RM == kRoundHash)
+    t = fmaf(hash_u24(c.key, c.off + (uint64_t)i), -0x1p-24f, fr) + 0.5f;
+  else
+    t = (fr - c.uniforms[i]) + 0.5f;
+  t = (t < 0.0f) ? 0.0f : t;
+  return f + rintf(t);
+}
+
+// One block: its fixed section written at fx (fk words, zeroed here), its variable section
+// appended to var; *n_out / *n_esc as the directory records them.
+template <int T, int RM, bool BN>
+static void pack_block_host(const PackHostCtx& P, int64_t b, uint32_t* fx,
+                            std::vector<uint32_t>& var, uint32_t* n_out, uint32_t* n_esc) {
+  const int wm = P.wm, wo = P.wo, we = P.we;
+  const int64_t e0 = b * kPB, m = std::min<int64_t>(kPB, P.n - e0);
+  memset(fx, 0, 4 * pk_fixed_words(wm));
+  uint32_t* plane = fx + 128;
+  const float main_lo = -ldexpf(1.0f, wm - 1), main_hi = ldexpf(1.0f, wm - 1) - 1.0f;
+  const float mag_max = ldexpf(1.0f, wo - 1) - 1.0f;
+  const uint32_t wmask = (uint32_t)((1ull << wm) - 1ull);
+  std::vector<uint32_t> ext;  // outlier code bits above the plane, element order
+  std::vector<uint32_t> esc;  // {index, q bits}
+  for (int64_t e = 0; e < m; ++e) {
+    bool hi, lo;
+    const float q = quant_host<T, RM, BN>(P.c, e0 + e, hi, lo);
+    const bool o = hi != lo;
+    const bool h1 = hi && o, l1 = lo && o;
+    bool ok;
+    if (o) ok = h1 ? (q >= 0.0f && q <= mag_max) : (q <= 0.0f && -q <= mag_max);
+    else ok = q >= main_lo && q <= main_hi;
+    const int64_t qi = ok ? (int64_t)q : 0;
+    uint32_t code;
+    if (o) {
+      const uint32_t side = (uint32_t)l1 << (wo - 1);
+      code = ok ? (side | (uint32_t)(h1 ? qi : -qi)) : side;
+      fx[e >> 5] |= 1u << (e & 31);
+      if (we > 0) ext.push_back(code >> wm);
+    } else {
+      code = ok ? ((uint32_t)qi & wmask) : 0u;
+    }
+    put_bits(plane, (uint64_t)e * (uint64_t)wm, code & wmask, wm);
+    if (!ok) {
+      esc.push_back((uint32_t)e);
+      esc.push_back(q != q ? 0x7fc00000u : f2u(q));
+    }
+  }
+  *n_out = (uint32_t)ext.size();
+  if (we == 0) {  // (no outlier bits above the plane: count the mask)
+    uint32_t c = 0;
+    for (int w = 0; w < 128; ++w) c += (uint32_t)__builtin_popcount(fx[w]);
+    *n_out = c;
+  }
+  *n_esc = (uint32_t)(esc.size() / 2);
+  const size_t ext_words = ((size_t)we * ext.size() + 31) / 32;
+  const size_t at = var.size();
+  var.resize(at + ext_words, 0u);
+  for (size_t k = 0; k < ext.size(); ++k) put_bits(var.data() + at, (uint64_t)k * we, ext[k], we);
+  var.insert(var.end(), esc.begin(), esc.end());
+}
+
+template <int T>
+static int pack_host(const void* x, int64_t n, const SmqSmaqParams* p, uint8_t* out,
+                     size_t out_bytes, char* ws, size_t ws_bytes, int n_threads) {
+  SmqSmaqStats st;
+  uint64_t base = 0;
+  int rc = host_stats<T>(x, n, p, nullptr, ws, ws_bytes, n_threads, &st, &base);
+  if (rc) return rc;
+  if (p->offset_counter) *p->offset_counter = base + (uint64_t)n;
+  st.rng_offset = base;
+  memcpy(ws, &st, sizeof(st));  // the header the device packer leaves in its workspace
+  PackHostCtx P;
+  SmaqCtx& c = P.c;
+  memset(&c, 0, sizeof(c));
+  c.x = x;
+  c.bn_gamma = p->bn_gamma;
+  c.bn_beta = p->bn_beta;
+  c.bn_channels = p->bn_channels;
+  c.bn_inner = p->bn_inner;
+  c.mean = st.mean;
+  c.sd = st.std_dev;
+  c.sc = st.std_clamped;
+  c.thr = p->main_std_dev_threshold;
+  c.nthr = -c.thr;
+  const bool bn = p->bn_gamma != nullptr;
+  c.cthr = bn ? c.thr : rin<T>(c.thr);
+  c.cnthr = -c.cthr;
+  c.zh = 0.0f * c.nthr;
+  c.zl = 0.0f * c.thr;
+  c.r_main = p->range_main;
+  c.r_out = p->range_outlier;
+  c.key = rng_key(p->seed);
+  c.off = p->offset + base;
+  P.wm = p->num_bits_main - 1;
+  P.wo = p->num_bits_outlier - 1;
+  P.we = P.wo > P.wm ? P.wo - P.wm : 0;
+  P.n = n;
+  const int rm = p->stochastic_rounding ? kRoundHash : kRoundTrunc;
+  const int64_t nb = (n + kPB - 1) / kPB;
+  const size_t fk = pk_fixed_words(P.wm);
+  SmqPackedHeader* hdr = reinterpret_cast<SmqPackedHeader*>(out);
+  uint64_t* dir = reinterpret_cast<uint64_t*>(out + sizeof(SmqPackedHeader));
+  uint32_t* fixed = reinterpret_cast<uint32_t*>(dir + pk_dir_entries(nb));
+  std::vector<std::vector<uint32_t>> var((size_t)nb);
+  std::vector<uint32_t> nout((size_t)nb), nesc((size_t)nb);
+  const int64_t tasks = (nb + kPackTaskBlocks - 1) / kPackTaskBlocks;
+  const std::function<void(int64_t)> fn = [&](int64_t t) {
+    const int64_t b1 = std::min(nb, (t + 1) * kPackTaskBlocks);
+    for (int64_t b = t * kPackTaskBlocks; b < b1; ++b) {
+      uint32_t* fx = fixed + (size_t)b * fk;
+      auto& v = var[(size_t)b];
+      if (rm == kRoundHash) {
+        if (bn) pack_block_host<T, kRoundHash, true>(P, b, fx, v, &nout[b], &nesc[b]);
+        else pack_block_host<T, kRoundHash, false>(P, b, fx, v, &nout[b], &nesc[b]);
+      } else {
+        if (bn) pack_block_host<T, kRoundTrunc, true>(P, b, fx, v, &nout[b], &nesc[b]);
+        else pack_block_host<T, kRoundTrunc, false>(P, b, fx, v, &nout[b], &nesc[b]);
+      }
+    }
+  };
+  pool().run(tasks, threads_for(n_threads), fn);
+  uint64_t off = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    dir[b] = off | ((uint64_t)nout[b] << 38) | ((uint64_t)nesc[b] << 51);
+    off += var[(size_t)b].size();
+  }
+  if (nb & 1) dir[nb] = 0;
+  uint32_t* vr = fixed + (size_t)nb * fk;
+  const size_t bn_words = bn ? 2 * (size_t)p->bn_channels : 0;
+  const size_t total = sizeof(SmqPackedHeader) + 8 * (size_t)pk_dir_entries(nb) +
+                       4 * ((size_t)nb * fk + off + bn_words);
+  if (total > out_bytes) {  // (cannot happen below smq_smaq_pack_bound; checked all the same)
+    set_error("cpu compress: stream of %zu bytes exceeds the buffer (%zu)", total, out_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  uint64_t at = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    const auto& v = var[(size_t)b];
+    if (!v.empty()) memcpy(vr + at, v.data(), 4 * v.size());
+    at += v.size();
+  }
+  if (bn) {
+    float* tab = reinterpret_cast<float*>(vr + off);
+    memcpy(tab, p->bn_gamma, 4 * (size_t)p->bn_channels);
+    memcpy(tab + p->bn_channels, p->bn_beta, 4 * (size_t)p->bn_channels);
+  }
+  const RangeRecips R = range_recips(p->range_main, p->range_outlier);
+  SmqPackedHeader h;
+  memset(&h, 0, sizeof(h));
+  h.magic = SMQ_PACK_MAGIC;
+  h.version = SMQ_PACK_VERSION;
+  h.n = n;
+  h.block_elems = kPB;
+  h.n_blocks = (uint32_t)nb;
+  h.num_bits_main = p->num_bits_main;
+  h.num_bits_outlier = p->num_bits_outlier;
+  h.flags = (p->all_positive ? SMQ_PACK_FLAG_ALL_POSITIVE : 0u) | (R.safe_q ? SMQ_PACK_FLAG_SAFE_Q : 0u) |
+            (c.thr < 0.0f ? SMQ_PACK_FLAG_BOTH_SIDES : 0u) | (bn ? SMQ_PACK_FLAG_BN : 0u);
+  h.thr = c.thr;
+  h.range_main = p->range_main;
+  h.range_outlier = p->range_outlier;
+  h.mean = st.mean;
+  h.std_dev = st.std_dev;
+  h.inv_range_main = R.inv_main;
+  h.inv_range_outlier = R.inv_out;
+  h.data_words = off;
+  h.total_bytes = total;
+  h.bn_channels = bn ? (uint32_t)p->bn_channels : 0u;
+  h.bn_inner = bn ? p->bn_inner : 0;
+  memcpy(hdr, &h, sizeof(h));
+  return SMQ_OK;
+}
+
+// The decoder (smq_smaq_decompress on the host): every block's codes, outlier bits and escapes
+// back to q and the sides, then smart.py:171-182 (and the BN term, all_positive) as smaq_dequant.
+static int unpack_host(const uint8_t* in, float* y, int64_t n, int n_threads) {
+  SmqPackedHeader h;
+  memcpy(&h, in, sizeof(h));
+  if (h.magic != SMQ_PACK_MAGIC || h.version != SMQ_PACK_VERSION || h.n != n ||
+      h.block_elems != (uint32_t)kPB || h.n_blocks != (uint32_t)((n + kPB - 1) / kPB) ||
+      h.num_bits_main < 2 || h.num_bits_main > 25 || h.num_bits_outlier < 3 ||
+      h.num_bits_outlier > 25) {
+    set_error("cpu decompress: not a version-%u stream of %lld elements", SMQ_PACK_VERSION,
+              (long long)n);
+    return SMQ_ERR_INVALID;
+  }
+  const int wm = h.num_bits_main - 1, wo = h.num_bits_outlier - 1, we = wo > wm ? wo - wm : 0;
+  const int64_t nb = h.n_blocks;
+  const size_t fk = pk_fixed_words(wm);
+  const uint64_t* dir = reinterpret_cast<const uint64_t*>(in + sizeof(SmqPackedHeader));
+  const uint32_t* fixed = reinterpret_cast<const uint32_t*>(dir + pk_dir_entries(nb));
+  const uint32_t* vr = fixed + (size_t)nb * fk;
+  const bool bn = (h.flags & SMQ_PACK_FLAG_BN) != 0, ap = (h.flags & 1u) != 0;
+  const bool both = (h.flags & SMQ_PACK_FLAG_BOTH_SIDES) != 0;
+  const float* g = bn ? reinterpret_cast<const float*>(vr + h.data_words) : nullptr;
+  const float* bb = bn ? g + h.bn_channels : nullptr;
+  const float thr = h.thr, nthr = -thr, zh = 0.0f * nthr, zl = 0.0f * thr;
+  const int64_t tasks = (nb + kPackTaskBlocks - 1) / kPackTaskBlocks;
+  const std::function<void(int64_t)> fn = [&](int64_t t) {
+    std::vector<float> qb(kPB);
+    std::vector<uint8_t> sides(kPB);  // bit 0: hi, bit 1: lo
+    const uint8_t both2 = both ? 3 : 0;
+    const int64_t b1 = std::min(nb, (t + 1) * kPackTaskBlocks);
+    for (int64_t b = t * kPackTaskBlocks; b < b1; ++b) {
+      const int64_t e0 = b * kPB, m = std::min<int64_t>(kPB, n - e0);
+      const uint64_t d = dir[b];
+      const uint64_t vbase = d & ((1ull << 38) - 1ull);
+      const uint32_t n_out = (uint32_t)((d >> 38) & 0x1fffu), n_esc = (uint32_t)(d >> 51);
+      const uint32_t* fx = fixed + (size_t)b * fk;
+      const uint32_t* ext = vr + vbase;
+      const uint32_t* esc = ext + ((size_t)we * n_out + 31) / 32;
+      uint32_t rank = 0;
+      for (int64_t e = 0; e < m; ++e) {
+        uint32_t code = get_bits(fx + 128, (uint64_t)e * wm, wm);
+        if ((fx[e >> 5] >> (e & 31)) & 1u) {  // outlier: side bit on top of |q|
+          if (we > 0) code |= get_bits(ext, (uint64_t)rank * we, we) << wm;
+          ++rank;
+          const uint32_t side = (code >> (wo - 1)) & 1u;
+          const float mag = (float)(code & ((1u << (wo - 1)) - 1u));
+          qb[(size_t)e] = side ? -mag : mag;
+          sides[(size_t)e] = side ? 2 : 1;
+        } else {  // main: wm-bit two's complement
+          qb[(size_t)e] = (float)((code >= (1u << (wm - 1))) ? (int32_t)code - (1 << wm)
+                                                             : (int32_t)code);
+          sides[(size_t)e] = both2;
+        }
+      }
+      for (uint32_t k = 0; k < n_esc; ++k)
+        if (esc[2 * k] < (uint32_t)m) qb[esc[2 * k]] = u2f(esc[2 * k + 1]);
+      for (int64_t e = 0; e < m; ++e) {
+        const bool hi = sides[(size_t)e] & 1, lo = sides[(size_t)e] & 2;
+        const float a = (hi ? nthr : zh) + (lo ? thr : zl);
+        const float r = (hi || lo) ? h.range_outlier : h.range_main;
+        float out = qb[(size_t)e] / r - a;
+        out = out * h.std_dev;
+        out = out + h.mean;
+        if (bn) {
+          const int64_t ch = ((e0 + e) / h.bn_inner) % (int64_t)h.bn_channels;
+          out = out * g[ch];
+          out = out + bb[ch];
+        }
+        if (ap) out = (out < 0.0f) ? 0.0f : out;
+        y[e0 + e] = out;
+      }
+    }
+  };
+  pool().run(tasks, threads_for(n_threads), fn);
   return SMQ_OK;
 }
 
@@ -845,6 +1164,56 @@ int smq_cpu_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const 
   if (dtype == SMQ_DTYPE_F32) return cpu::smaq_roundtrip<kF32>(x, y, n, p, uniforms, stats_in, w, ws_bytes, n_threads);
   if (dtype == SMQ_DTYPE_F16) return cpu::smaq_roundtrip<kF16>(x, y, n, p, uniforms, stats_in, w, ws_bytes, n_threads);
   return cpu::smaq_roundtrip<kBF16>(x, y, n, p, uniforms, stats_in, w, ws_bytes, n_threads);
+}
+
+int smq_cpu_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* p,
+                          void* packed, size_t packed_bytes, void* ws, size_t ws_bytes,
+                          int n_threads) {
+  int rc = smaq_validate(p, dtype);
+  if (rc) return rc;
+  if (n < 1 || !x || !packed) {
+    set_error("cpu compress: n must be >= 1, x and packed non-NULL");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->num_bits_main < 2 || p->num_bits_main > 25 || p->num_bits_outlier < 3 ||
+      p->num_bits_outlier > 25) {
+    set_error("cpu compress: needs 2 <= num_bits_main <= 25 and 3 <= num_bits_outlier <= 25");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->bn_gamma && (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1)) {
+    set_error("cpu compress: batch-norm parameters incomplete");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->stats_source == SMQ_STATS_INJECTED) {
+    set_error("cpu compress: computes its statistics (SMQ_STATS_WORKSPACE or _SAMPLED*)");
+    return SMQ_ERR_INVALID;
+  }
+  const size_t bound = smq_smaq_pack_bound_bn(n, p->num_bits_main, p->num_bits_outlier,
+                                              p->bn_gamma ? p->bn_channels : 0);
+  if (packed_bytes < bound) {
+    set_error("cpu compress: packed buffer too small: need %zu bytes, got %zu", bound, packed_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  const int64_t k = p->stats_source == SMQ_STATS_SAMPLED_DEVICE
+                        ? std::min<int64_t>(p->num_samples, n) : 0;
+  const size_t need = k > 0 ? smq_smaq_workspace_bytes_sampled(n, k) : smq_smaq_workspace_bytes(n);
+  if (!ws || ws_bytes < need) {
+    set_error("cpu compress: workspace too small: need %zu bytes", need);
+    return SMQ_ERR_WORKSPACE;
+  }
+  uint8_t* out = static_cast<uint8_t*>(packed);
+  char* w = static_cast<char*>(ws);
+  if (dtype == SMQ_DTYPE_F32) return cpu::pack_host<kF32>(x, n, p, out, packed_bytes, w, ws_bytes, n_threads);
+  if (dtype == SMQ_DTYPE_F16) return cpu::pack_host<kF16>(x, n, p, out, packed_bytes, w, ws_bytes, n_threads);
+  return cpu::pack_host<kBF16>(x, n, p, out, packed_bytes, w, ws_bytes, n_threads);
+}
+
+int smq_cpu_smaq_decompress(const void* packed, float* y, int64_t n, int n_threads) {
+  if (n < 1 || !packed || !y) {
+    set_error("cpu decompress: n must be >= 1, packed and y non-NULL");
+    return SMQ_ERR_INVALID;
+  }
+  return cpu::unpack_host(static_cast<const uint8_t*>(packed), y, n, n_threads);
 }
 
 int smq_cpu_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t n,

@@ -1188,10 +1188,17 @@ inline int64_t n_blocks_of(int64_t n) { return (n + kPB - 1) / kPB; }
 // workspace: statistics | meta [nb] | group sums [ng] | group prefixes [ng] | scratch [nb][kVarCap]
 struct PackWs {
   size_t meta, gsum, gpre, scratch, total;
-  explicit PackWs(int64_t n) {
+  // k: device-drawn samples (0: none); above SMQ_MAX_DEVICE_SAMPLES the statistics region holds
+  // the multi-workgroup draw (smq_smaq_workspace_bytes_sampled)
+  explicit PackWs(int64_t n, int64_t k = 0) {
     const size_t nb = (size_t)n_blocks_of(n < 1 ? 1 : n);
     const size_t ng = (nb + kGroup - 1) / kGroup;
-    meta = (smaq_stats_ws_bytes(n) + 255) & ~(size_t)255;
+    size_t st = smaq_stats_ws_bytes(n);
+    if (k > SMQ_MAX_DEVICE_SAMPLES) {
+      const size_t big = smq_smaq_workspace_bytes_sampled(n, k);
+      st = big > st ? big : st;
+    }
+    meta = (st + 255) & ~(size_t)255;
     gsum = meta + 4 * nb;
     gpre = (gsum + 4 * ng + 7) & ~(size_t)7;
     scratch = (gpre + 8 * ng + 255) & ~(size_t)255;
@@ -1223,6 +1230,12 @@ size_t smq_smaq_pack_bound_bn(int64_t n, int num_bits_main, int num_bits_outlier
 }
 
 size_t smq_smaq_pack_workspace_bytes(int64_t n) { return PackWs(n).total; }
+
+size_t smq_smaq_pack_workspace_bytes_sampled(int64_t n, int64_t num_samples) {
+  const int64_t k = num_samples < n ? num_samples : n;
+  if (k > SMQ_MAX_DRAW_SAMPLES) return 0;
+  return PackWs(n, k).total;
+}
 
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* packed,
                       size_t packed_bytes, void* ws, size_t ws_bytes, void* stream) {
@@ -1271,18 +1284,15 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
               bound, p->bn_gamma ? "_bn" : "", packed_bytes);
     return SMQ_ERR_WORKSPACE;
   }
-  const PackWs L(n);
+  const int64_t k_draw = p->stats_source == SMQ_STATS_SAMPLED_DEVICE
+                             ? (p->num_samples < n ? p->num_samples : n) : 0;
+  const PackWs L(n, k_draw);
   if (!ws || ws_bytes < L.total) {
     set_error("compress: workspace too small: need %zu bytes, got %zu", L.total, ws_bytes);
     return SMQ_ERR_WORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
-  // the statistics own only the first region (no room for a multi-workgroup sample draw)
-  if (p->stats_source == SMQ_STATS_SAMPLED_DEVICE &&
-      (p->num_samples < n ? p->num_samples : n) > SMQ_MAX_DEVICE_SAMPLES) {
-    set_error("compress: device-drawn samples are limited to %d here", SMQ_MAX_DEVICE_SAMPLES);
-    return SMQ_ERR_INVALID;
-  }
+  // the statistics own the first region (sized for the multi-workgroup draw above 4096 samples)
   rc = prepare_stats(x, dtype, n, p, ws, L.meta, st);
   if (rc) return rc;
   char* wb = (char*)ws;

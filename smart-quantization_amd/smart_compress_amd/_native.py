@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get(
     "SMQ_LIB", os.path.join(os.path.dirname(_PKG_DIR), "lib", "libsmq.so")
 )
 
-SMQ_ABI_VERSION = 6
+SMQ_ABI_VERSION = 7
 SMQ_MAX_SAMPLES = 64
 SMQ_MAX_DEVICE_SAMPLES = 4096
 SMQ_MAX_DRAW_SAMPLES = 1 << 28
@@ -273,6 +273,10 @@ SIGNATURES = {
     "smq_smaq_compress_ex": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams),
                                      _P, _SZ, _P, _SZ, _U32, _P]),
     "smq_smaq_decompress": (_I32, [_P, _P, _I64, _P]),
+    "smq_smaq_pack_workspace_bytes_sampled": (_SZ, [_I64, _I64]),
+    "smq_cpu_smaq_compress": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P,
+                                     _SZ, _I32]),
+    "smq_cpu_smaq_decompress": (_I32, [_P, _P, _I64, _I32]),
     "smq_smaq_decompress_ex": (_I32, [_P, _P, _I64, _I32, _I32, _P]),
     "smq_cpu_threads": (_I32, []),
     "smq_cpu_smaq_roundtrip": (

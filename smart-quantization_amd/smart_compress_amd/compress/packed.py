@@ -93,6 +93,11 @@ class SmaqPacked:
 class SmartFPPacked(SmartFP):
     def compress(self, data: torch.Tensor, all_positive: bool = False,
                  batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SmaqPacked:
+        """The stream of ``data`` (smart.py:110-190's codes). A ROCm tensor: ``smq_smaq_compress``
+        on the caller's stream, no host synchronisation, into a buffer of the worst-case size
+        (``smq_smaq_pack_bound``: several times the tensor; ``SmaqPacked.compact()`` or
+        ``nbytes`` trim / read the real size). A CPU tensor: ``smq_cpu_smaq_compress``, the same
+        bytes, right-sized at once (the call is synchronous)."""
         hp = self.hparams
         numel = data.numel()
         if numel < hp.min_size:  # smart.py:123-128: kept as is
@@ -100,10 +105,7 @@ class SmartFPPacked(SmartFP):
             return SmaqPacked(raw.clone(), data.shape, numel, raw=True)
         if hp.main_std_dev_threshold != hp.main_std_dev_threshold:
             raise NotImplementedError("SmartFPPacked: main_std_dev_threshold is NaN")
-        if hp.use_sample_stats and min(numel, hp.num_samples) > N.SMQ_MAX_DEVICE_SAMPLES:
-            raise NotImplementedError(
-                f"SmartFPPacked: --num_samples above {N.SMQ_MAX_DEVICE_SAMPLES} is not supported")
-        N.require_device(data, "SmartFPPacked")
+        N.require_supported(data, "SmartFPPacked")
         code = N.DTYPE_CODES.get(data.dtype)
         if code is None:
             raise NotImplementedError(
@@ -112,27 +114,48 @@ class SmartFPPacked(SmartFP):
             raise RuntimeError("value cannot be converted to type c10::Half without overflow")
         x = data.contiguous()
         lib = N.lib()
-        p = self._params(numel, all_positive, x.dtype, x.device)
+        cpu = N.on_cpu(x)
+        p = self._params(numel, all_positive, x.dtype, None if cpu else x.device)
         keep = None
         if hp.use_batch_norm and batch_norm_stats is not None:
             keep = self._bind_batch_norm(p, x, batch_norm_stats)
         bound = lib.smq_smaq_pack_bound_bn(numel, hp.num_bits_main, hp.num_bits_outlier,
                                            p.bn_channels if keep is not None else 0)
+        widths = (hp.num_bits_main, hp.num_bits_outlier)
+        sampled = p.stats_source == N.SMQ_STATS_SAMPLED_DEVICE
+        if cpu:
+            out = torch.empty(bound, dtype=torch.uint8)
+            ws = N.cpu_workspace("smaq", self.workspace_bytes(numel))
+            N.check(lib.smq_cpu_smaq_compress(x.data_ptr(), code, numel, p, out.data_ptr(),
+                                              out.numel(), ws.data_ptr(), ws.numel(),
+                                              N.cpu_threads()), "smq_cpu_smaq_compress")
+            del keep
+            total = int(out[_TOTAL_OFF:_TOTAL_OFF + 8].numpy().view(np.uint64)[0])
+            return SmaqPacked(out[:total].clone(), data.shape, numel, widths=widths, total=total)
         out = torch.empty(bound, dtype=torch.uint8, device=x.device)
-        ws = N.workspace("smaq_pack", x.device, lib.smq_smaq_pack_workspace_bytes(numel))
+        nws = (lib.smq_smaq_pack_workspace_bytes_sampled(numel, p.num_samples) if sampled
+               else lib.smq_smaq_pack_workspace_bytes(numel))
+        ws = N.workspace("smaq_pack", x.device, nws)
         N.check(lib.smq_smaq_compress(x.data_ptr(), code, numel, p, out.data_ptr(), out.numel(),
                                       ws.data_ptr(), ws.numel(), N.stream_ptr(x.device)),
                 "smq_smaq_compress")
         del keep
         # the stream size stays on the device (SmaqPacked.nbytes / compact read it when asked)
-        return SmaqPacked(out, data.shape, numel, widths=(hp.num_bits_main, hp.num_bits_outlier))
+        return SmaqPacked(out, data.shape, numel, widths=widths)
 
     def decompress(self, packed: SmaqPacked) -> torch.Tensor:
+        """fp32 values, bit-identical to ``SmartFP`` on the compressed tensor (same flags and random
+        stream), on the device the stream is on (a CPU stream: ``smq_cpu_smaq_decompress``)."""
         if packed.raw:
             return packed.data.view(torch.float32).reshape(packed.shape).clone()
-        N.require_device(packed.data, "SmartFPPacked.decompress")
+        N.require_supported(packed.data, "SmartFPPacked.decompress")
         y = torch.empty(packed.shape, dtype=torch.float32, device=packed.data.device)
-        lib, st = N.lib(), N.stream_ptr(y.device)
+        lib = N.lib()
+        if N.on_cpu(packed.data):
+            N.check(lib.smq_cpu_smaq_decompress(packed.data.data_ptr(), y.data_ptr(), packed.n,
+                                                N.cpu_threads()), "smq_cpu_smaq_decompress")
+            return y
+        st = N.stream_ptr(y.device)
         if packed.widths is not None:
             # the widths the stream was written with: the decoder locates its sections without
             # waiting for the header

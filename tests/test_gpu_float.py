@@ -415,21 +415,32 @@ def test_s2fp8_flag_validation():
         g.s2fp8(x, flags=64)
 
 
-def test_fp8_c3_full_size_vs_oracle():
-    """BASELINE config 3 at full size ([128,256,28,28] = 25,690,112 elements, ReLU(N(0,1)) like an
-    activation): E5M2 stochastic float_quantize + check_inf equals the oracle bit for bit with the
-    same counter words."""
+@pytest.mark.parametrize("dist,check_inf", [("relu", True), ("normal", True), ("wide", True),
+                                            ("wide", False)])
+def test_fp8_c3_full_size_vs_oracle(dist, check_inf):
+    """BASELINE config 3 at full size ([128,256,28,28] = 25,690,112 elements): E5M2 stochastic
+    float_quantize (+ check_inf) equals the oracle bit for bit with the same counter words, on the
+    SURVEY 8d value sets — ReLU(N(0,1)) like an activation, plain N(0,1) (negative values), and
+    N(0,1) * 3e4 (both signs past the E5M2 max 57344: saturation to -max / +max, and +max -> +inf
+    under check_inf)."""
     from oracle import qtorch_float as qf
     from oracle import rng as orng
 
     g = _g()
     gen = torch.Generator(device="cuda").manual_seed(3)
-    x = torch.relu(torch.randn(128, 256, 28, 28, generator=gen, device="cuda"))
-    y = g.float_quant(x, 5, 2, check_inf=True, seed=7, offset=12345)
+    x = torch.randn(128, 256, 28, 28, generator=gen, device="cuda")
+    if dist == "relu":
+        x = torch.relu(x)
+    elif dist == "wide":
+        x = x * 3e4
+    y = g.float_quant(x, 5, 2, check_inf=check_inf, seed=7, offset=12345)
     xn = x.cpu().numpy().ravel()
-    y_or = qf.float_quantize(xn, 5, 2, orng.rng_u32(7, 12345, xn.size), True)
+    y_or = qf.float_quantize(xn, 5, 2, orng.rng_u32(7, 12345, xn.size), check_inf)
     yh = y.cpu().numpy().ravel()
     assert same_f32(yh, y_or), n_diff_f32(yh, y_or)
+    if dist == "wide":  # the saturating paths were exercised
+        assert (yh == -57344.0).any() and ((yh == np.inf).any() if check_inf
+                                           else (yh == 57344.0).any())
 
 
 @pytest.mark.parametrize("n,shift", [(3 * 2**20 + 3, 0), (3 * 2**20 + 3, 1), (4096 * 7, 0), (5, 0)])

@@ -496,3 +496,66 @@ def test_compress_decompress_in_a_captured_graph():
         assert torch.equal(y.view(torch.int32), want[r].view(torch.int32)), r
     assert 0 < packed.nbytes < 4 * x.numel()
     pk.graph_safe(False)
+
+
+@pytest.mark.parametrize("k", [5000, 100_000])
+def test_sampled_above_4096_device_draw(k):
+    """smart.py:86-91 with more samples than one workgroup draws: the multi-workgroup draw in the
+    packer's workspace (smq_smaq_pack_workspace_bytes_sampled); the round trip equals SmartFP."""
+    hp, pk, ref = _codecs(use_sample_stats=True, num_samples=k)
+    x = torch.randn(1_000_003, device="cuda") * 0.7 + 0.2
+    for _ in range(2):  # consecutive calls: fresh draws, same stream positions
+        y = pk.decompress(pk.compress(x))
+        y_ref = ref(x)
+        torch.cuda.synchronize()
+        assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
+    assert pk.rng.offset == ref.rng.offset
+
+
+def _golden_packable():
+    from helpers import smaq_cases
+
+    cases = smaq_cases()
+    return sorted(k for k, m in cases.items()
+                  if not k.startswith("n7") and not m.get("use_sample_stats"))
+
+
+@pytest.mark.parametrize("name", _golden_packable())
+def test_device_stream_equals_host_stream(name):
+    """The host packer (smq_cpu_smaq_compress) and the device packer write the same bytes for the
+    same input and random stream whenever their statistics agree (fp64 sums in two fixed orders:
+    equal but for rare last-bit cases, where the header tells); either library decodes the other's
+    stream to the same values."""
+    from helpers import load_smaq, smaq_cases
+
+    from smart_compress_amd.compress import SmartFPPacked
+
+    meta, d = smaq_cases()[name], load_smaq(name)
+    hp = smaq_hparams(meta, measure_compression_ratio=False)
+    dt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[meta["dtype"]]
+    x = torch.from_numpy(np.ascontiguousarray(d["x"])).to(dt)
+    bn = None
+    if "bn_gamma" in d:
+        hp.use_batch_norm = True
+        bn = (torch.from_numpy(d["bn_gamma"]), torch.from_numpy(d["bn_beta"]))
+    streams = []
+    for dev in ("cpu", "cuda"):
+        pk = SmartFPPacked(hp)
+        pk.rng.seed, pk.rng.offset = 13, 5
+        xb = x.to(dev)
+        bnb = None if bn is None else tuple(t.to(dev) for t in bn)
+        streams.append(pk.compress(xb, meta["all_positive"], bnb).compact())
+    hc, hd = streams[0].header(), streams[1].header()
+    if (hc["mean"], hc["std_dev"]) == (hd["mean"], hd["std_dev"]):
+        assert np.array_equal(streams[0].data.numpy(), streams[1].data.cpu().numpy())
+    else:  # (rare) statistics a last bit apart: both within one ulp
+        for k in ("mean", "std_dev"):
+            assert abs(int(np.float32(hc[k]).view(np.int32)) -
+                       int(np.float32(hd[k]).view(np.int32))) <= 1
+    pk = SmartFPPacked(hp)
+    for s in streams:  # each stream decoded on the other side equals its own decode
+        other = type(s)(s.data.cuda() if not s.data.is_cuda else s.data.cpu(), s.shape, s.n,
+                        widths=s.widths, total=s.nbytes)
+        a, b = pk.decompress(s), pk.decompress(other)
+        torch.cuda.synchronize()
+        assert same_f32(a.cpu().numpy(), b.cpu().numpy())

@@ -1,0 +1,97 @@
+"""SmaQ-packed saved activations (util/pytorch/saved.py) against the unpacked SmaQ training step.
+
+The reference keeps every compressed activation as fp32 (autograd.py:18-77); PackedActivations
+keeps the ones autograd saves for backward as SmaQ streams and decodes them in backward. Because
+decode(encode(x)) == SmartFP(x) bit for bit (include/smq.h "Packed SmaQ container"), the loss and
+every gradient must equal the SmartFP run's bit for bit, while the saved bytes shrink."""
+
+from argparse import Namespace
+
+import pytest
+import torch
+import torch.nn as nn
+
+from helpers import smaq_hparams
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(inplace):
+    def block(cin, cout):
+        return nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1, bias=False), nn.BatchNorm2d(cout),
+                             nn.ReLU(inplace=inplace))
+
+    return nn.Sequential(block(3, 32), block(32, 32), nn.MaxPool2d(2), block(32, 64),
+                         block(64, 64), nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(64, 10))
+
+
+def _eq(a, b):
+    return torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_packed_saved_activations_bitexact(inplace):
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import register_autograd_module
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
+
+    def run(packed):
+        torch.manual_seed(3)
+        net = _net(inplace).cuda()
+        codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
+        codec.rng.seed, codec.rng.offset = 21, 0
+        acts = PackedActivations(codec, trim_bytes=8 << 20) if packed else None
+        register_autograd_module(net, acts if packed else codec, flags)
+        opt = torch.optim.SGD(net.parameters(), lr=0.05, momentum=0.9)
+        g = torch.Generator(device="cuda").manual_seed(9)
+        out, peaks = [], []
+        for _ in range(2):
+            x = torch.randn(64, 3, 32, 32, device="cuda", generator=g, requires_grad=True)
+            tgt = torch.arange(64, device="cuda") % 10
+            opt.zero_grad()
+            torch.cuda.synchronize()
+            base = torch.cuda.memory_allocated()
+            torch.cuda.reset_peak_memory_stats()
+            if packed:
+                with acts:
+                    loss = nn.functional.cross_entropy(net(x), tgt)
+            else:
+                loss = nn.functional.cross_entropy(net(x), tgt)
+            torch.cuda.synchronize()
+            peaks.append(torch.cuda.memory_allocated() - base)  # held for backward
+            loss.backward()
+            opt.step()
+            out.append((loss.detach(), x.grad.clone(), [p.grad.clone() for p in net.parameters()]))
+        return out, codec.rng.offset, peaks, acts
+
+    a, off_a, held_a, _ = run(False)
+    b, off_b, held_b, acts = run(True)
+    assert off_a == off_b > 0
+    for (la, xa, ga), (lb, xb, gb) in zip(a, b):
+        assert _eq(la, lb) and _eq(xa, xb)
+        assert all(_eq(p, q) for p, q in zip(ga, gb))
+    st = acts.stats()
+    assert st["saved_packed"] >= 8 and 6.0 < st["bits_per_element"] < 9.0, st
+    # the memory held between forward and backward shrinks by the packed activations' share
+    assert max(held_b) < 0.8 * min(held_a), (held_a, held_b)
+
+
+def test_packed_saved_outside_context_and_backward_calls():
+    """Outside the context (and for backward-direction calls) the compress_fn is the plain codec
+    call: the same outputs and random stream as SmartFP."""
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    x = torch.randn(100_000, device="cuda")
+    ref = SmartFP(smaq_hparams())
+    pk = SmartFPPacked(smaq_hparams())
+    for c in (ref, pk):
+        c.rng.seed, c.rng.offset = 4, 0
+    acts = PackedActivations(pk)
+    assert _eq(acts(x, tag="forward_autograd"), ref(x))
+    with acts:
+        assert _eq(acts(x, tag="backward_autograd"), ref(x))
+        assert _eq(acts(x, tag="forward_autograd"), ref(x))
+    assert pk.rng.offset == ref.rng.offset
