@@ -443,6 +443,10 @@ int smq_cpu_s2fp8_roundtrip_f64(const double* x, double* y, int64_t n, int preci
 
 /* ---- host reference helpers shared with the oracle (pure functions, no GPU) ---- */
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
+/* SmaQ's stochastic-rounding draw of counter `counter` (an integer < 2^24; the uniform is it times
+ * 2^-24): the top 24 bits of quad_word(key, counter >> 2) * an odd multiplier of counter & 3 — one
+ * hash per four consecutive counters (oracle/rng.py smaq_u24 restates it). */
+uint32_t smq_smaq_u24(uint64_t seed, uint64_t counter);
 
 
 /* ---------------------------------------------------------------------------------------------

@@ -1,5 +1,7 @@
-"""Counter-based RNG of libsmq, restated in numpy (bit-exact with smq_common.h: mix32, rng_key,
-rng_u32, u32_to_unit). Element i of a call with (seed, offset) uses counter offset + i."""
+"""TEST INFRASTRUCTURE ONLY — the counter-based RNG of libsmq, restated in numpy (bit-exact with
+smq_common.h: mix32, rng_key, rng_u32, mix32x3 / quad_word / draw_mul / smaq_u24). Element i of a call with (seed,
+offset) uses counter offset + i: the float quantiser draws rng_u32(counter) per element, SmaQ's
+stochastic rounding smaq_u24(counter) — one hash per four consecutive counters."""
 
 import numpy as np
 
@@ -13,6 +15,20 @@ def mix32(x):
     x ^= x >> np.uint32(15)
     x *= np.uint32(0x846CA68B)
     x ^= x >> np.uint32(16)
+    return x
+
+
+def mix32x3(x):
+    """triple32 (smq_common.h mix32x3): the quad hash of SmaQ's draws."""
+    x = np.asarray(x, dtype=np.uint32).copy()
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint32(17)
+        x *= np.uint32(0xED5AD4BB)
+        x ^= x >> np.uint32(11)
+        x *= np.uint32(0xAC4C1B51)
+        x ^= x >> np.uint32(15)
+        x *= np.uint32(0x31848BAB)
+        x ^= x >> np.uint32(14)
     return x
 
 
@@ -39,8 +55,27 @@ def u32_to_unit(h: np.ndarray) -> np.ndarray:
     return (h >> np.uint32(8)).astype(np.float32) * np.float32(2.0**-24)
 
 
+DRAW_MUL = np.array([1, 0x9E3779B1, 0x85EBCA77, 0xC2B2AE3D], dtype=np.uint32)
+
+
+def smaq_u24(seed: int, offset: int, n: int, start: int = 0) -> np.ndarray:
+    """SmaQ's draws (smq_common.h smaq_u24) for elements start..start+n-1 of a call keyed by
+    (seed, offset): quad word h = mix32x3(lo ^ rotl16(hi) ^ key) of q = counter >> 2, lane
+    counter & 3 takes the top 24 bits of h * DRAW_MUL[lane] (uint32 wrap-around)."""
+    key = np.uint32(rng_key(seed))
+    ctr = (np.uint64(offset) + np.arange(start, start + n, dtype=np.uint64))
+    q = ctr >> np.uint64(2)
+    lo = (q & np.uint64(_M32)).astype(np.uint32)
+    hi = (q >> np.uint64(32)).astype(np.uint32)
+    rot = (hi << np.uint32(16)) | (hi >> np.uint32(16))
+    h = mix32x3(lo ^ rot ^ key)
+    with np.errstate(over="ignore"):
+        return (h * DRAW_MUL[(ctr & np.uint64(3)).astype(np.intp)]) >> np.uint32(8)
+
+
 def uniforms(seed: int, offset: int, n: int, start: int = 0) -> np.ndarray:
-    return u32_to_unit(rng_u32(seed, offset, n, start))
+    """SmaQ's stochastic-rounding uniforms (smaq_u24 * 2^-24), fp32."""
+    return smaq_u24(seed, offset, n, start).astype(np.float32) * np.float32(2.0**-24)
 
 
 DRAW_SALT = 0xD1B54A32D192ED03

@@ -271,4 +271,4 @@ def uniforms_f64(seed: int, offset: int, n: int, start: int = 0) -> np.ndarray:
     """The counter RNG's fp64 uniforms (the same 24-bit values as the fp32 path)."""
     from . import rng as _rng
 
-    return (_rng.rng_u32(seed, offset, n, start) >> np.uint32(8)).astype(F64) * F64(2.0**-24)
+    return _rng.smaq_u24(seed, offset, n, start).astype(F64) * F64(2.0**-24)

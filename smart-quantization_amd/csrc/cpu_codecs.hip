@@ -9,7 +9,7 @@
 // statistics and random stream the bytes are the same as the GPU's (SmaQ, float_quantize):
 //   * z = (x - mean) / std_clamped and q / range as IEEE fp32 divisions — the device's
 //     RN32(RN64(a * RN64(1/b))) equals them (smaq_elem.h div_by_const, proven exact);
-//   * SR draws u = rng_u32(key, offset + i) >> 8, t = fma(u, -2^-24, fr) + 0.5 (one rounding);
+//   * SR draws u = smaq_u24(key, offset + i), t = fma(u, -2^-24, fr) + 0.5 (one rounding);
 //   * fp16 / bf16 inputs follow the torch type flow with the same round-to-nearest-even steps.
 // Statistics are fp64 sums in a fixed order (per 64K-element task, combined in task order: the
 // result does not depend on the thread count); the device sums in another fixed order, so mean /
@@ -201,8 +201,8 @@ static inline float ld(const void* p, int64_t i) {
   return T == kF16 ? h2f(h) : bf2f(h);
 }
 
-static inline float hash_u24(uint32_t key, uint64_t ctr) {  // rng_hu: h >> 8 as a float
-  return (float)(rng_u32(key, ctr) >> 8);
+static inline float hash_u24(uint32_t key, uint64_t ctr) {  // rng_hu: smaq_u24 as a float
+  return (float)smaq_u24(key, ctr);
 }
 
 // ---- SmaQ statistics ----------------------------------------------------------------------------
@@ -1074,7 +1074,7 @@ static int smaq_roundtrip_f64(const double* x, double* y, int64_t n, const SmqSm
       uint64_t cnt = 0;
       for (int64_t i = i0; i < i1; ++i) {
         double u = 0.0, g = 1.0, b = 0.0;
-        if (RM == kRoundHash) u = (double)(rng_u32(key, off + (uint64_t)i) >> 8);
+        if (RM == kRoundHash) u = (double)smaq_u24(key, off + (uint64_t)i);
         if (RM == kRoundUniform) u = uniforms[i];
         if (BN) {
           const int64_t ch = (i / p->bn_inner) % p->bn_channels;

@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void smaq_f64_apply_kernel(ApplyF64Args A) 
     const int64_t e = e0 + j * kBlock;
     if (e >= A.n) continue;
     double uu = u[j];
-    if (RM == kRoundHash) uu = (double)(rng_u32(A.key, off + (uint64_t)e) >> 8);
+    if (RM == kRoundHash) uu = (double)smaq_u24(A.key, off + (uint64_t)e);
     double g = 1.0, b = 0.0;
     if (BN) {
       const int64_t ch = (e / A.p.bn_inner) % A.p.bn_channels;

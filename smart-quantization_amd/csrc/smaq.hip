@@ -1205,6 +1205,7 @@ int smq_abi_version(void) { return SMQ_ABI_VERSION; }
 const char* smq_last_error(void) { return g_err; }
 
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter) { return rng_u32(rng_key(seed), counter); }
+uint32_t smq_smaq_u24(uint64_t seed, uint64_t counter) { return smaq_u24(rng_key(seed), counter); }
 
 void smq_smaq_params_init(SmqSmaqParams* p) {
   memset(p, 0, sizeof(*p));

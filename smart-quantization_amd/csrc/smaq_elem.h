@@ -251,28 +251,30 @@ static inline RangeRecips range_recips(float r_main, float r_out) {
   return R;
 }
 
-// kRoundHash draws: h >> 8 of the counter hash as a float (exact, < 2^24), see smaq_elem.
+// kRoundHash draws: smaq_u24 (smq_common.h) as a float (exact, < 2^24), see smaq_elem.
 __device__ __forceinline__ float rng_hu(uint32_t key, uint64_t ctr) {
-  return (float)(rng_u32(key, ctr) >> 8);
+  return (float)smaq_u24(key, ctr);
 }
 
-// Draws for counters ctr .. ctr+3 (one float4 of elements): the same values as four rng_hu calls;
-// the high counter word is rotated once unless the low word wraps inside the group.
+// Draws for counters ctr .. ctr+3 (one float4 of elements): the same values as four rng_hu calls.
+// ctr & 3 is the call's stream position mod 4 (wave-uniform): 0 (every activation-sized stream)
+// takes ONE quad hash; otherwise the four counters straddle two quads.
 __device__ __forceinline__ void rng_hu4(uint32_t key, uint64_t ctr, float& u0, float& u1, float& u2,
                                         float& u3) {
-  const uint32_t lo = (uint32_t)ctr;
-  if (__builtin_expect(lo <= 0xfffffffcu, 1)) {
-    const uint32_t hi = (uint32_t)(ctr >> 32);
-    const uint32_t kk = ((hi << 16) | (hi >> 16)) ^ key;
-    u0 = (float)(mix32(lo ^ kk) >> 8);
-    u1 = (float)(mix32((lo + 1u) ^ kk) >> 8);
-    u2 = (float)(mix32((lo + 2u) ^ kk) >> 8);
-    u3 = (float)(mix32((lo + 3u) ^ kk) >> 8);
+  const uint32_t s = (uint32_t)ctr & 3u;
+  if (__builtin_expect(s == 0u, 1)) {
+    const uint32_t h = quad_word(key, ctr >> 2);
+    u0 = (float)(h >> 8);
+    u1 = (float)((h * draw_mul(1u)) >> 8);
+    u2 = (float)((h * draw_mul(2u)) >> 8);
+    u3 = (float)((h * draw_mul(3u)) >> 8);
   } else {
-    u0 = rng_hu(key, ctr);
-    u1 = rng_hu(key, ctr + 1);
-    u2 = rng_hu(key, ctr + 2);
-    u3 = rng_hu(key, ctr + 3);
+    const uint64_t q = ctr >> 2;
+    const uint32_t h0 = quad_word(key, q), h1 = quad_word(key, q + 1);
+    u0 = (float)((h0 * draw_mul(s)) >> 8);
+    u1 = (float)(((s + 1u < 4u ? h0 : h1) * draw_mul((s + 1u) & 3u)) >> 8);
+    u2 = (float)(((s + 2u < 4u ? h0 : h1) * draw_mul((s + 2u) & 3u)) >> 8);
+    u3 = (float)((h1 * draw_mul((s + 3u) & 3u)) >> 8);
   }
 }
 

@@ -37,7 +37,8 @@ constexpr int kWave = 64;
 // ---------------------------------------------------------------------------------------------
 // Counter-based RNG. Element i of a call draws from counter c = offset + i, so the value of an
 // element never depends on the launch geometry and the CPU oracle reproduces it bit for bit
-// (oracle/rng.py). One "lowbias32" finaliser (C. Wellons) = 2 v_mul_lo_u32 per element.
+// (oracle/rng.py). One "lowbias32" finaliser (C. Wellons) = 2 v_mul_lo_u32 per hash: per element
+// for the float quantiser (rng_u32), per four elements for SmaQ's rounding draws (smaq_u24).
 // The 64-bit seed is folded into a 32-bit key once per launch on the host.
 // ---------------------------------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -57,6 +58,40 @@ __host__ __device__ __forceinline__ uint32_t rng_u32(uint32_t key, uint64_t ctr)
   const uint32_t lo = (uint32_t)ctr;
   const uint32_t hi = (uint32_t)(ctr >> 32);
   return mix32(lo ^ ((hi << 16) | (hi >> 16)) ^ key);
+}
+
+// SmaQ's stochastic-rounding draws (smart.py:93-98's rand_like): 24-bit uniforms as integers
+// < 2^24, ONE counter hash per four consecutive counters. Counter c reads the quad word
+// h = quad_word(key, c >> 2); lane r = c & 3 takes the top 24 bits of h * draw_mul(r), an odd
+// multiplier (a bijection of the 32-bit word: every lane is uniform; lane 0's is 1). An aligned
+// float4 of elements costs one hash, 3 multiplies, 4 shifts and 4 conversions instead of four
+// hashes (the packer and the half-input apply are VALU-bound: DESIGN.md §3). The quad hash is
+// "triple32" (C. Wellons; 3 multiplies): lowbias32 over 2^22 consecutive counters leaves the top
+// 12 bits 8-11 sigma off uniform (chi-square), triple32 within 4 (tests/test_rng_quality.py).
+// The float quantiser (qtorch) keeps rng_u32 per element: it reads the low bits of its words too.
+__host__ __device__ __forceinline__ uint32_t mix32x3(uint32_t x) {
+  x ^= x >> 17;
+  x *= 0xed5ad4bbU;
+  x ^= x >> 11;
+  x *= 0xac4c1b51U;
+  x ^= x >> 15;
+  x *= 0x31848babU;
+  x ^= x >> 14;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t quad_word(uint32_t key, uint64_t q) {
+  const uint32_t lo = (uint32_t)q;
+  const uint32_t hi = (uint32_t)(q >> 32);
+  return mix32x3(lo ^ ((hi << 16) | (hi >> 16)) ^ key);
+}
+
+__host__ __device__ __forceinline__ uint32_t draw_mul(uint32_t r) {
+  return r == 0u ? 1u : r == 1u ? 0x9e3779b1u : r == 2u ? 0x85ebca77u : 0xc2b2ae3du;
+}
+
+__host__ __device__ __forceinline__ uint32_t smaq_u24(uint32_t key, uint64_t c) {
+  return (quad_word(key, c >> 2) * draw_mul((uint32_t)c & 3u)) >> 8;
 }
 
 // U[0,1) with 24 random bits, the resolution of torch.rand_like for fp32.

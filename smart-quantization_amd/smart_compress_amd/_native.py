@@ -265,6 +265,7 @@ SIGNATURES = {
         [_P, _I32, _P, _I32, _I64, _I32, _I32, _I32, _I32, _P, _U64, _U64, _P, _P],
     ),
     "smq_rng_u32": (ctypes.c_uint32, [_U64, _U64]),
+    "smq_smaq_u24": (ctypes.c_uint32, [_U64, _U64]),
     "smq_smaq_pack_bound": (_SZ, [_I64, _I32, _I32]),
     "smq_smaq_pack_bound_bn": (_SZ, [_I64, _I32, _I32, _I64]),
     "smq_smaq_pack_workspace_bytes": (_SZ, [_I64]),

@@ -293,3 +293,18 @@ def test_fastcall_binding_loads_next_to_the_library():
         f.smaq_roundtrip(1, 2, 3)
     rc = f.smaq_roundtrip(0, 0, 0, 16, 0, 0, 0, 0)
     assert rc != 0 and N.lib().smq_last_error()
+
+
+def test_smaq_draws_match_oracle():
+    """smq_smaq_u24 (the SmaQ rounding draw: one hash per four counters) equals oracle/rng.py
+    smaq_u24 for every alignment of the stream position, across the 2^32 counter boundary and for
+    64-bit counters."""
+    from oracle import rng
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    for seed in (0, 1, 2**63 + 5):
+        for off in (0, 1, 2, 3, 2**32 - 6, 2**34 + 1, 2**64 - 16):
+            got = [lib.smq_smaq_u24(seed, off + i) for i in range(8)]
+            assert got == [int(v) for v in rng.smaq_u24(seed, off, 8)]
+            assert all(g < 2**24 for g in got)
