@@ -92,12 +92,15 @@ class SmaqPacked:
 
 class SmartFPPacked(SmartFP):
     def compress(self, data: torch.Tensor, all_positive: bool = False,
-                 batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> SmaqPacked:
+                 batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                 out: Optional[torch.Tensor] = None) -> SmaqPacked:
         """The stream of ``data`` (smart.py:110-190's codes). A ROCm tensor: ``smq_smaq_compress``
         on the caller's stream, no host synchronisation, into a buffer of the worst-case size
         (``smq_smaq_pack_bound``: several times the tensor; ``SmaqPacked.compact()`` or
-        ``nbytes`` trim / read the real size). A CPU tensor: ``smq_cpu_smaq_compress``, the same
-        bytes, right-sized at once (the call is synchronous)."""
+        ``nbytes`` trim / read the real size) — ``out``, a caller's uint8 device buffer of at least
+        that size (reused across calls: the returned stream then lives in it), or a new one. A CPU
+        tensor: ``smq_cpu_smaq_compress``, the same bytes, right-sized at once (the call is
+        synchronous)."""
         hp = self.hparams
         numel = data.numel()
         if numel < hp.min_size:  # smart.py:123-128: kept as is
@@ -132,7 +135,11 @@ class SmartFPPacked(SmartFP):
             del keep
             total = int(out[_TOTAL_OFF:_TOTAL_OFF + 8].numpy().view(np.uint64)[0])
             return SmaqPacked(out[:total].clone(), data.shape, numel, widths=widths, total=total)
-        out = torch.empty(bound, dtype=torch.uint8, device=x.device)
+        if out is None:
+            out = torch.empty(bound, dtype=torch.uint8, device=x.device)
+        elif out.dtype != torch.uint8 or out.device != x.device or out.numel() < bound:
+            raise ValueError(f"SmartFPPacked.compress: out must be a uint8 buffer of >= {bound} "
+                             f"bytes on {x.device}")
         nws = (lib.smq_smaq_pack_workspace_bytes_sampled(numel, p.num_samples) if sampled
                else lib.smq_smaq_pack_workspace_bytes(numel))
         ws = N.workspace("smaq_pack", x.device, nws)

@@ -13,13 +13,18 @@ random stream (include/smq.h "Packed SmaQ container"). Inside ``with activations
 ``torch.autograd.graph.saved_tensors_hooks`` pair replaces every saved tensor that IS such a ``y``
 (same storage, shape, strides, and not modified in place since) by ``P``, and the backward decodes
 it again: the gradients equal those of the unpacked SmaQ run bit for bit, while a saved activation
-takes ~7.4 bits per element (6/8-bit codes on N(0,1)-like data) instead of 32.
+takes ~8 bits per element (6/8-bit codes) instead of 32.
 
-The packer writes into a buffer of the worst-case size and leaves the stream size on the device
-(no host synchronisation per call); saved streams are trimmed to their size in batches: when the
-untrimmed ones exceed ``trim_bytes`` and when the context exits (one host synchronisation per
-batch, every stream's size read in one copy). Backward-direction calls (grad-maps, never saved)
-and calls outside the context run as the plain codec call.
+Memory without host synchronisation per call: the packer writes into a scratch stream of the
+worst-case size (``smq_smaq_pack_bound``, reused: one per device and stream), and the saved copy
+is a device-to-device copy of its first ``capacity`` bytes — the fixed region (known from n) plus
+room for every element being an outlier and 1 % escapes (``stream_capacity``). Only a stream larger
+than that (escape-heavy data) would be cut, so until its size is checked the saved ``y`` is kept
+too: checks run in batches — one host synchronisation reads every pending stream's size — when
+the pending ``y`` exceed ``verify_bytes`` and when the context exits; a checked stream drops its
+``y``, a cut one (never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
+Backward-direction calls (grad-maps, never saved) and calls outside the context run as the plain
+codec call.
 """
 
 import weakref
@@ -27,95 +32,144 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ...compress.packed import SmaqPacked, SmartFPPacked, _TOTAL_OFF
+from ... import _native as N
+from ...compress.packed import SmaqPacked, SmartFPPacked, _HDR_BYTES, _TOTAL_OFF
 
-__all__ = ["PackedActivations"]
+__all__ = ["PackedActivations", "stream_capacity"]
 
 FORWARD_TAG = "forward_autograd"
 
 
+def stream_capacity(n: int, num_bits_main: int, num_bits_outlier: int, bn_channels: int = 0,
+                    escape_frac: float = 0.01) -> int:
+    """Bytes of a stream of n elements (format v2) with every element an outlier and up to
+    ``escape_frac`` of them escaped: the header, the directory, the fixed region, per block the
+    outlier bits above the plane (rounded up to a word), the escapes, the BN table."""
+    nb = (n + N.SMQ_PACK_BLOCK - 1) // N.SMQ_PACK_BLOCK
+    wm, wo = num_bits_main - 1, num_bits_outlier - 1
+    we = max(0, wo - wm)
+    fixed_words = 128 + 128 * wm
+    var_words = (we * n + 31) // 32 + nb + 2 * int(escape_frac * n + nb)
+    return (_HDR_BYTES + 8 * (nb + (nb & 1)) + 4 * (nb * fixed_words + var_words)
+            + 8 * bn_channels)
+
+
 class _Saved:
-    """What autograd holds instead of a saved activation: the packed stream and the decoder."""
+    """What autograd holds instead of a saved activation: the stream (and, until its size is
+    checked, the activation itself)."""
 
-    __slots__ = ("packed", "codec")
+    __slots__ = ("packed", "y", "codec")
 
-    def __init__(self, packed: SmaqPacked, codec: SmartFPPacked):
-        self.packed, self.codec = packed, codec
+    def __init__(self, packed: SmaqPacked, y: torch.Tensor, codec: SmartFPPacked):
+        self.packed, self.y, self.codec = packed, y, codec
 
 
 class _Entry:
-    __slots__ = ("ref", "packed", "version", "shape", "stride", "dtype")
+    __slots__ = ("ref", "packed", "cap", "version", "shape", "stride", "dtype", "handle")
 
 
 class PackedActivations:
-    def __init__(self, codec: SmartFPPacked, trim_bytes: int = 256 << 20):
+    def __init__(self, codec: SmartFPPacked, verify_bytes: int = 128 << 20):
         if not isinstance(codec, SmartFPPacked):
             raise TypeError("PackedActivations needs a SmartFPPacked codec")
         self.codec = codec
-        self.trim_bytes = int(trim_bytes)
+        self.verify_bytes = int(verify_bytes)
         self._live: Dict[int, _Entry] = {}  # data_ptr of a forward output -> its stream
-        self._untrimmed: List[SmaqPacked] = []
-        self._untrimmed_bytes = 0
+        self._pending: List[_Saved] = []     # saved, size not yet checked (y still held)
+        self._pending_bytes = 0
+        self._scratch: Dict[tuple, torch.Tensor] = {}
         self._hooks = None
         self.saved_packed = 0    # saved tensors held as streams (since construction)
-        self.saved_bytes = 0     # the distinct streams' trimmed bytes
-        self.saved_elements = 0  # and elements
+        self.saved_bytes = 0     # the distinct verified streams' bytes
+        self.saved_capacity = 0  # and the bytes allocated for them
+        self.saved_elements = 0  # and their elements
+        self.kept_fp32 = 0       # streams cut at their capacity (the activation kept instead)
+
+    def _scratch_for(self, device: torch.device, nbytes: int) -> torch.Tensor:
+        key = (device.index, N.stream_ptr(device))
+        buf = self._scratch.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = self._scratch[key] = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        return buf
 
     # -- the compress_fn of register_autograd_module ---------------------------------------------
     def __call__(self, x: torch.Tensor, tag: str = None, all_positive=False,
                  batch_norm_stats=None, **kw):
         codec = self.codec
-        if (self._hooks is None or tag != FORWARD_TAG or x.numel() < codec.hparams.min_size
+        hp = codec.hparams
+        if (self._hooks is None or tag != FORWARD_TAG or x.numel() < hp.min_size
                 or not x.is_cuda):
             return codec(x, tag=tag, all_positive=all_positive, batch_norm_stats=batch_norm_stats,
                          **kw)
-        packed = codec.compress(x, all_positive, batch_norm_stats)
-        y = codec.decompress(packed)
-        codec.log_size(tag, x.numel() * 32, lambda: packed.nbytes * 8)
+        n = x.numel()
+        bn = batch_norm_stats is not None and hp.use_batch_norm
+        channels = (1 if hp.bn_scalar_params else x.shape[1]) if bn else 0
+        lib = N.lib()
+        bound = lib.smq_smaq_pack_bound_bn(n, hp.num_bits_main, hp.num_bits_outlier, channels)
+        scratch = self._scratch_for(x.device, bound)
+        full = codec.compress(x, all_positive, batch_norm_stats, out=scratch)
+        y = codec.decompress(full)
+        codec.log_size(tag, n * 32, lambda: full.nbytes * 8)
+        cap = min(bound, stream_capacity(n, hp.num_bits_main, hp.num_bits_outlier, channels))
+        data = torch.empty(cap, dtype=torch.uint8, device=x.device)
+        data.copy_(scratch[:cap])  # stream order: before the next call reuses the scratch
         e = _Entry()
         key = y.data_ptr()
         e.ref = weakref.ref(y, lambda _r, k=key, d=self._live: d.pop(k, None))
-        e.packed, e.version = packed, y._version
+        e.packed = SmaqPacked(data, full.shape, n, widths=full.widths)
+        e.cap, e.version = cap, y._version
         e.shape, e.stride, e.dtype = y.shape, y.stride(), y.dtype
+        e.handle = None
         self._live[key] = e
         return y
 
     # -- saved_tensors_hooks ------------------------------------------------------------------------
     def _pack(self, t: torch.Tensor):
         e = self._live.get(t.data_ptr()) if t.is_cuda else None
-        if (e is None or e.ref() is None or t._version != e.version or t.shape != e.shape
+        if (e is None or t._version != e.version or t.shape != e.shape
                 or t.stride() != e.stride or t.dtype != e.dtype):
             return t  # not a forward output of this codec, or modified in place since
-        p = e.packed
-        if p._total is None and not any(q is p for q in self._untrimmed):
-            self._untrimmed.append(p)
-            self._untrimmed_bytes += p.data.numel()
-            if self._untrimmed_bytes > self.trim_bytes:
-                self.trim()
+        y = e.ref()
+        if y is None:
+            return t
         self.saved_packed += 1
-        return _Saved(p, self.codec)
+        if e.handle is not None:  # saved again (another consumer): the same stream
+            return e.handle
+        h = e.handle = _Saved(e.packed, y, self.codec)
+        self._pending.append(h)
+        self._pending_bytes += 4 * y.numel()
+        if self._pending_bytes > self.verify_bytes:
+            self.verify()
+        return h
 
     @staticmethod
     def _unpack(h):
         if isinstance(h, _Saved):
+            if h.y is not None:  # not checked yet, or cut at its capacity: the activation itself
+                return h.y
             return h.codec.decompress(h.packed)
         return h
 
-    def trim(self) -> None:
-        """Cut every untrimmed saved stream to its size: one host synchronisation (every header's
-        stream size in one copy), then right-sized device copies."""
-        ps = self._untrimmed
-        if not ps:
+    def verify(self) -> None:
+        """Check every pending stream's size against its capacity: one host synchronisation
+        (every header's total_bytes in one copy); a stream that fits drops its activation."""
+        hs = self._pending
+        if not hs:
             return
-        sizes = torch.cat([p.data[_TOTAL_OFF:_TOTAL_OFF + 8] for p in ps]).cpu()
-        for p, total in zip(ps, sizes.view(torch.int64).tolist()):
-            p._total = int(total)
-            if p.data.numel() > total:
-                p.data = p.data[:total].clone()
-            self.saved_bytes += int(total)
-            self.saved_elements += p.n
-        self._untrimmed = []
-        self._untrimmed_bytes = 0
+        sizes = torch.cat([h.packed.data[_TOTAL_OFF:_TOTAL_OFF + 8] for h in hs]).cpu()
+        for h, total in zip(hs, sizes.view(torch.int64).tolist()):
+            cap = h.packed.data.numel()
+            if total <= cap:
+                h.packed._total = int(total)
+                h.y = None
+                self.saved_bytes += int(total)
+                self.saved_capacity += cap
+                self.saved_elements += h.packed.n
+            else:
+                h.packed = None
+                self.kept_fp32 += 1
+        self._pending = []
+        self._pending_bytes = 0
 
     def __enter__(self):
         self._hooks = torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack)
@@ -125,16 +179,18 @@ class PackedActivations:
     def __exit__(self, *exc):
         hooks, self._hooks = self._hooks, None
         try:
-            self.trim()
+            self.verify()
         finally:
             self._live.clear()
             hooks.__exit__(*exc)
         return False
 
     def stats(self) -> Dict[str, Optional[float]]:
-        """Saved tensors held as streams, and the bytes / bits per element of the distinct streams
-        trimmed so far."""
-        return {"saved_packed": self.saved_packed, "saved_elements": self.saved_elements,
+        """Saved tensors held as streams; bits per element of the verified streams (their real
+        size and the capacity allocated for them); streams cut and kept as fp32."""
+        el = self.saved_elements
+        return {"saved_packed": self.saved_packed, "saved_elements": el,
                 "saved_stream_bytes": self.saved_bytes,
-                "bits_per_element": (8.0 * self.saved_bytes / self.saved_elements
-                                     if self.saved_elements else None)}
+                "bits_per_element": 8.0 * self.saved_bytes / el if el else None,
+                "allocated_bits_per_element": 8.0 * self.saved_capacity / el if el else None,
+                "kept_fp32": self.kept_fp32}

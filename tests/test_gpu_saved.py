@@ -42,7 +42,7 @@ def test_packed_saved_activations_bitexact(inplace):
         net = _net(inplace).cuda()
         codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
         codec.rng.seed, codec.rng.offset = 21, 0
-        acts = PackedActivations(codec, trim_bytes=8 << 20) if packed else None
+        acts = PackedActivations(codec, verify_bytes=8 << 20) if packed else None
         register_autograd_module(net, acts if packed else codec, flags)
         opt = torch.optim.SGD(net.parameters(), lr=0.05, momentum=0.9)
         g = torch.Generator(device="cuda").manual_seed(9)
@@ -66,16 +66,56 @@ def test_packed_saved_activations_bitexact(inplace):
             out.append((loss.detach(), x.grad.clone(), [p.grad.clone() for p in net.parameters()]))
         return out, codec.rng.offset, peaks, acts
 
-    a, off_a, held_a, _ = run(False)
-    b, off_b, held_b, acts = run(True)
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:  # (deterministic weight-gradient kernels: the parameter gradients compare bit for bit)
+        a, off_a, held_a, _ = run(False)
+        b, off_b, held_b, acts = run(True)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
     assert off_a == off_b > 0
     for (la, xa, ga), (lb, xb, gb) in zip(a, b):
         assert _eq(la, lb) and _eq(xa, xb)
         assert all(_eq(p, q) for p, q in zip(ga, gb))
     st = acts.stats()
     assert st["saved_packed"] >= 8 and 6.0 < st["bits_per_element"] < 9.0, st
+    assert st["kept_fp32"] == 0 and st["allocated_bits_per_element"] < 10.5, st
     # the memory held between forward and backward shrinks by the packed activations' share
     assert max(held_b) < 0.8 * min(held_a), (held_a, held_b)
+
+
+def test_stream_capacity_cut_keeps_the_activation():
+    """A stream larger than its capacity (escape-heavy data: 8 % of the elements at +-1e6, whose
+    outlier codes exceed the 8-bit budget: ~93 KB against a 71 KB capacity at 64K elements) is
+    detected when the pending streams are checked: the saved value is then the activation itself,
+    still exact."""
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import Compressor
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(1 << 16, device="cuda", generator=g)
+    x[::25] = 1e6
+    x[12::25] = -1e6  # z ~ +-3.5: |q| ~ 105 > 63, escaped
+    res = []
+    for packed in (False, True):
+        codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
+        codec.rng.seed, codec.rng.offset = 2, 0
+        acts = PackedActivations(codec) if packed else None
+        comp = Compressor(acts if packed else codec)
+        w = torch.linspace(0.5, 1.5, x.numel(), device="cuda").requires_grad_(True)
+        if packed:
+            with acts:
+                y = comp(x * w)
+                loss = (y * y).sum()  # (y saved by the multiply)
+        else:
+            y = comp(x * w)
+            loss = (y * y).sum()
+        loss.backward()
+        res.append((y.detach(), w.grad.clone()))
+        if packed:
+            assert acts.stats()["kept_fp32"] == 1
+    assert _eq(res[0][0], res[1][0]) and _eq(res[0][1], res[1][1])
 
 
 def test_packed_saved_outside_context_and_backward_calls():
