@@ -1051,7 +1051,9 @@ def run_autograd(args, world, rank, device):
     del net, opt
 
     results = {}
-    for name in ("uncompressed", "smaq_eager", "smaq_graph", "smaq_eager_packed_saved"):
+    # (the graph variant last: its capture keeps a private memory pool alive, which would count in
+    # the following variants' allocated memory)
+    for name in ("uncompressed", "smaq_eager", "smaq_eager_packed_saved", "smaq_graph"):
         packed = name == "smaq_eager_packed_saved"
         net, opt, codec = build(name != "uncompressed", packed=packed)
         step = step_fn(net, opt, codec if packed else None)
@@ -1072,7 +1074,9 @@ def run_autograd(args, world, rank, device):
         run()
         torch.cuda.synchronize()
         mem = None
-        if name != "smaq_graph":  # (a graph's memory is its private pool, allocated at capture)
+        if name != "smaq_graph":  # peak allocated over one step, and its excess over the memory
+            # resident before the step (parameters, gradients, optimizer state, workspaces); a
+            # graph's memory is its private pool, allocated at capture
             before = torch.cuda.memory_allocated(device)
             torch.cuda.reset_peak_memory_stats(device)
             run()

@@ -646,12 +646,56 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A) {
       for (uint32_t i = (uint32_t)lane + kW * kWave; i < sz; i += kWave) out[o0 + i] = src[i];
     }
   }
-  // blocks whose variable section outgrew the scratch slot
-  for (unsigned long long m = over; m; m &= m - 1) {
-    const uint32_t j = (uint32_t)__builtin_ctzll(m);
+  (void)lds;
+  (void)s_cnt;
+}
+
+// Blocks whose variable section outgrew the scratch slot (escape-heavy data: a channel of an
+// activation far from the tensor's mean escapes as a whole), re-coded from x: one workgroup per
+// `per` consecutive blocks (per = 1 up to 1024 blocks), so the re-coded blocks of a tensor run in
+// parallel — the var kernel's workgroups had re-coded their group's blocks one after another
+// (a CIFAR ResNet activation: up to 0.7 ms per call). A block's offset: its group's prefix plus the
+// sizes of the group's blocks before it (from meta).
+template <int RM, int TIN, bool EXT>
+__global__ __launch_bounds__(kBlock) void smaq_pack_recode_kernel(PackArgs A, uint32_t per) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // 128 * we words
+  __shared__ uint32_t s_cnt[kBlock / kWave];
+  __shared__ uint32_t list[kBlock];
+  __shared__ uint32_t n_list;
+  __shared__ uint64_t s_dst;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int we = A.wo > A.wm ? A.wo - A.wm : 0;
+  // the workgroup's blocks' flags in one round of loads (per <= kBlock), the re-code list in LDS
+  if (threadIdx.x == 0) n_list = 0u;
+  __syncthreads();
+  const uint32_t bt = blockIdx.x * per + threadIdx.x;
+  if (threadIdx.x < per && bt < A.n_blocks && (A.meta[bt] & kMetaRecode))
+    list[atomicAdd(&n_list, 1u)] = bt;
+  __syncthreads();
+  const uint32_t m = n_list;
+  for (uint32_t i = 0; i < m; ++i) {
+    const uint32_t b = list[i];
+    if (threadIdx.x < kWave) {
+      const uint32_t g = b / kGroup, b0 = g * kGroup;
+      uint32_t sz = 0u;
+      if (b0 + (uint32_t)lane < b) {
+        const uint32_t t = A.meta[b0 + lane] & ~kMetaRecode;
+        sz = ext_words(we, t & 0xffffu) + 2u * (t >> 16);
+      }
+      const uint32_t before = wave_incl_scan_u32(sz);
+      if (lane == kWave - 1) s_dst = A.gpre[g] + before;
+    }
     __syncthreads();
-    recode_var_section<RM, TIN, EXT>(A, b0 + j, base + s_off[j], lds, s_cnt);
+    recode_var_section<RM, TIN, EXT>(A, b, s_dst, lds, s_cnt);
+    __syncthreads();
   }
+}
+
+// workgroups of the per-block rare-path launches (re-code, big-block decode): about 1024, at least
+// one block each
+__host__ __device__ inline uint32_t rare_per(uint32_t nb) {
+  const uint32_t p = nb > 1024u ? (nb + 1023u) / 1024u : 1u;
+  return p < (uint32_t)kBlock ? p : (uint32_t)kBlock;
 }
 
 template <int RM, int TIN, int WM, int WO, bool EXT>
@@ -672,6 +716,9 @@ void launch_pack_w(const PackArgs& A, bool vec, hipStream_t st) {
   const int we = A.wo > A.wm ? A.wo - A.wm : 0;
   hipLaunchKernelGGL((smaq_pack_var_kernel<RM, TIN, WM, WO, EXT>), dim3(A.n_groups), dim3(kBlock),
                      4 * 128 * (size_t)(we > 0 ? we : 1), st, A);
+  const uint32_t per = rare_per(A.n_blocks);
+  hipLaunchKernelGGL((smaq_pack_recode_kernel<RM, TIN, EXT>), dim3((A.n_blocks + per - 1) / per),
+                     dim3(kBlock), 4 * 128 * (size_t)(we > 0 ? we : 1), st, A, per);
 }
 
 // ext: the BN variant or T_m <= 0 (ext_quant, runtime widths); else the packer's own element.
@@ -697,6 +744,7 @@ struct UnpackArgs {
   uint32_t nb;         // blocks
   uint32_t n_full;     // blocks of SMQ_PACK_BLOCK elements
   uint32_t lds_bytes;  // dynamic LDS of the launch (the widths' need, or the widest)
+  uint32_t big_per;    // smaq_unpack_big_kernel: full blocks per workgroup (rare_per, <= kBlock)
 };
 
 // Decode table of narrow codes (both widths <= 8 bits: the 6/8-bit default): every main code
@@ -1166,8 +1214,8 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_big_kernel(UnpackArgs A) {
   const int we = wo > wm ? wo - wm : 0;
   if (threadIdx.x == 0) n_list = 0u;
   __syncthreads();
-  const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
-  if (b < A.n_full) {
+  const uint32_t b = blockIdx.x * A.big_per + threadIdx.x;
+  if (threadIdx.x < A.big_per && b < A.n_full) {
     const uint64_t d = A.dir[b];
     const uint32_t n_out = (uint32_t)(d >> 38) & 0x1fffu, n_esc = (uint32_t)(d >> 51);
     if (ext_words(we, n_out) + 2u * n_esc > (uint32_t)kVarCap) list[atomicAdd(&n_list, 1u)] = b;
@@ -1387,6 +1435,10 @@ static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int 
   A.nb = (uint32_t)nb;
   A.n_full = (uint32_t)(n / kPB);
   A.lds_bytes = 4u * (bm ? unpack_lds_words(A.wm) : kUnpackLdsWords);
+  // big blocks (a variable section beyond the LDS window: escape-heavy data) are decoded one after
+  // another by their workgroup: about 1024 workgroups, so a tensor's big blocks decode in parallel
+  A.big_per = rare_per(A.n_full);
+  if (A.big_per > (uint32_t)kBlock) A.big_per = kBlock;
   const unsigned grid = (unsigned)((A.n_full + kUnpackPer - 1) / kUnpackPer);
   const bool w57 = bm == 6 && bo == 8;  // the default widths, known from the caller
 #define SMQ_UNPACK_LAUNCH(WMV, WOV)                                                                \
@@ -1394,7 +1446,7 @@ static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int 
     if (grid) {                                                                                   \
       hipLaunchKernelGGL((smaq_unpack_kernel<WMV, WOV, true>), dim3(grid), dim3(kBlock),           \
                          A.lds_bytes, st, A);                                                     \
-      hipLaunchKernelGGL((smaq_unpack_big_kernel<WMV, WOV>), dim3((A.n_full + kBlock - 1) / kBlock), \
+      hipLaunchKernelGGL((smaq_unpack_big_kernel<WMV, WOV>), dim3((A.n_full + A.big_per - 1) / A.big_per), \
                          dim3(kBlock), A.lds_bytes, st, A);                                       \
     }                                                                                             \
     if (A.n_full < A.nb)                                                                          \
