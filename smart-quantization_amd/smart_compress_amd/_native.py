@@ -503,6 +503,11 @@ def workspace(kind: str, device: torch.device, nbytes: int, stream: int = None) 
     key = (kind, device_index(device), stream_ptr(device) if stream is None else stream)
     buf = _ws.get(key)
     if buf is not None and buf.numel() >= nbytes:
+        # a capture may hold this buffer from now on (even one taken without graph-safe streams):
+        # stop evicting. (Only while eviction is still on; the C hot path keeps its own reference.)
+        if _ws_evictable and torch.device(device).type == "cuda" and \
+                torch.cuda.is_current_stream_capturing():
+            pin_workspaces()
         return buf
     with _ws_lock:
         capturing = (torch.device(device).type == "cuda"
@@ -521,6 +526,9 @@ def workspace(kind: str, device: torch.device, nbytes: int, stream: int = None) 
             else:
                 buf = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
             if key not in _ws and len(_ws) >= WORKSPACE_LIMIT and _ws_evictable:
+                # (a thread still holding the evicted tensor keeps its memory; when it drops it,
+                # the caching allocator reuses the block only in the order of the stream the
+                # buffer was made and used on, i.e. after that thread's queued calls)
                 old = next(iter(_ws))
                 if old[1] >= 0 and torch.cuda.is_available():
                     torch.cuda.synchronize(old[1])

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-5 evidence on one box: the GPU suite, smoke, a bench line of every config, then a kernel
 # trace + FETCH / WRITE passes per profiled config (tools/profile_round.sh; summarised on the host
-# by tools/pmc_traffic.py into profiles/<tag>_*). Each step under its own time limit; the first
+# by tools/pmc_traffic.py / tools/autograd_profile.py into profiles/<tag>_*) and the single-launch
+# SmaQ at 1M / 4M / 8M (tools/profile_fused.sh). Each step under its own time limit; the first
 # failure ends the script.
 # Usage: bash tools/gpu_round5.sh <tag>
 set -o pipefail
@@ -20,7 +21,14 @@ for c in multi packed s2fp8 fp8 autograd autograd_resnet34; do
   timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline >> gpurun_out/${TAG}_bench.jsonl \
     2>> gpurun_out/${TAG}_bench.err || exit 1
 done
+for d in f16 bf16; do
+  SMQ_BENCH_DTYPE=$d timeout -k 10 300 python -u bench.py --no-cpu-baseline >> gpurun_out/${TAG}_bench.jsonl \
+    2>> gpurun_out/${TAG}_bench.err || exit 1
+done
 for c in smaq multi packed s2fp8 fp8 autograd_resnet34; do
   bash tools/profile_round.sh ${TAG}_$c $c > /dev/null || exit 1
 done
+SMQ_BENCH_DTYPE=f16 bash tools/profile_round.sh ${TAG}_smaq_f16 smaq > /dev/null || exit 1
+SMQ_BENCH_DTYPE=bf16 bash tools/profile_round.sh ${TAG}_smaq_bf16 smaq > /dev/null || exit 1
+bash tools/profile_fused.sh ${TAG}_fused > /dev/null || exit 1
 echo done
