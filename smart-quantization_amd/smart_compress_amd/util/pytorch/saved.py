@@ -21,7 +21,8 @@ is a device-to-device copy of its first ``capacity`` bytes — the fixed region 
 room for every element being an outlier and 1 % escapes (``stream_capacity``). Only a stream larger
 than that (escape-heavy data) would be cut, so until its size is checked the saved ``y`` is kept
 too: checks run in batches — one host synchronisation reads every pending stream's size — when
-the pending ``y`` exceed ``verify_bytes`` and when the context exits; a checked stream drops its
+the pending ``y`` exceed ``verify_bytes`` (32 MiB: the memory the mode may hold beyond the streams)
+and when the context exits; a checked stream drops its
 ``y``, a cut one (never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
 Backward-direction calls (grad-maps, never saved) and calls outside the context run as the plain
 codec call.
@@ -69,7 +70,7 @@ class _Entry:
 
 
 class PackedActivations:
-    def __init__(self, codec: SmartFPPacked, verify_bytes: int = 128 << 20):
+    def __init__(self, codec: SmartFPPacked, verify_bytes: int = 32 << 20):
         if not isinstance(codec, SmartFPPacked):
             raise TypeError("PackedActivations needs a SmartFPPacked codec")
         self.codec = codec
@@ -125,10 +126,16 @@ class PackedActivations:
 
     # -- saved_tensors_hooks ------------------------------------------------------------------------
     def _pack(self, t: torch.Tensor):
-        e = self._live.get(t.data_ptr()) if t.is_cuda else None
-        if (e is None or t._version != e.version or t.shape != e.shape
-                or t.stride() != e.stride or t.dtype != e.dtype):
-            return t  # not a forward output of this codec, or modified in place since
+        key = t.data_ptr() if t.is_cuda else None
+        e = self._live.get(key) if key is not None else None
+        if e is None:
+            return t  # not a forward output of this codec
+        if t._version != e.version:  # modified in place since (e.g. an in-place ReLU): its stream
+            if e.handle is None:     # no longer describes it
+                self._live.pop(key, None)
+            return t
+        if t.shape != e.shape or t.stride() != e.stride or t.dtype != e.dtype:
+            return t  # a view of it
         y = e.ref()
         if y is None:
             return t

@@ -81,7 +81,8 @@ def test_packed_saved_activations_bitexact(inplace):
     assert st["saved_packed"] >= 8 and 6.0 < st["bits_per_element"] < 9.0, st
     assert st["kept_fp32"] == 0 and st["allocated_bits_per_element"] < 10.5, st
     # the memory held between forward and backward shrinks by the packed activations' share
-    assert max(held_b) < 0.8 * min(held_a), (held_a, held_b)
+    # (second step: the first one also allocates workspaces)
+    assert held_b[1] < 0.8 * held_a[1], (held_a, held_b)
 
 
 def test_stream_capacity_cut_keeps_the_activation():

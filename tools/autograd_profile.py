@@ -22,6 +22,9 @@ import statistics
 import sys
 
 SMAQ = re.compile(r"smq::(smaq_\w+_kernel)(?:<([^>]*)>)?")
+# SmartFP's launches (the single launch, or statistics + apply); the packed codec's kernels of a
+# bench variant with packed saved activations are not counted
+KERNELS = ("smaq_fused_kernel", "smaq_stats_kernel", "smaq_apply_kernel")
 
 
 def classify(name, grid_threads, wg):
@@ -29,6 +32,8 @@ def classify(name, grid_threads, wg):
     if not m:
         return None
     kern, targs = m.group(1), m.group(2) or ""
+    if kern not in KERNELS:
+        return None
     g = int(grid_threads) // max(1, int(wg))
     if kern == "smaq_fused_kernel":
         v = int(targs.split(",")[1])

@@ -28,7 +28,13 @@ done
 for c in smaq multi packed s2fp8 fp8 autograd_resnet34; do
   bash tools/profile_round.sh ${TAG}_$c $c > /dev/null || exit 1
 done
+# the autograd trace and counter files are large (thousands of dispatches with long names): keep the
+# per-size-class summary (tools/autograd_profile.py) and the stats, drop the raw CSVs
+AG=gpurun_out/prof_${TAG}_autograd_resnet34
+python tools/autograd_profile.py $AG gpurun_out/${TAG}_autograd_resnet34_summary.json > /dev/null || exit 1
+rm -f $AG/trace/run_kernel_trace.csv $AG/fetch/run_counter_collection.csv $AG/write/run_counter_collection.csv
 SMQ_BENCH_DTYPE=f16 bash tools/profile_round.sh ${TAG}_smaq_f16 smaq > /dev/null || exit 1
 SMQ_BENCH_DTYPE=bf16 bash tools/profile_round.sh ${TAG}_smaq_bf16 smaq > /dev/null || exit 1
 bash tools/profile_fused.sh ${TAG}_fused > /dev/null || exit 1
+du -sh gpurun_out
 echo done
