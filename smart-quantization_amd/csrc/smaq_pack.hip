@@ -577,13 +577,21 @@ __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_d
 // every fourth block from its scratch slot to the stream (a lane copies words lane, lane + 64, ...;
 // four blocks' loads in flight before their stores); blocks whose section outgrew the slot are
 // re-coded from x by the whole workgroup (recode_var_section).
+template <int RM, int TIN, bool EXT>
+__device__ void pack_recode_blocks(const PackArgs& A, uint32_t wg, uint32_t per, uint32_t* lds);
+
+// Workgroups [0, n_groups): one group of kGroup blocks each (the copy described above); the
+// workgroups after them re-code the escape-heavy blocks (pack_recode_blocks), one launch for both.
 template <int RM, int TIN, int WM, int WO, bool EXT>
-__global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A) {
+__global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A, uint32_t per) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // re-code: 128 * we words
   __shared__ uint32_t s_off[kGroup + 1];   // group-relative word offsets (s_off[64] = total)
   __shared__ uint64_t s_base;
   __shared__ unsigned long long s_over;    // blocks of the group re-coded from x
-  __shared__ uint32_t s_cnt[kBlock / kWave];
+  if (blockIdx.x >= A.n_groups) {
+    pack_recode_blocks<RM, TIN, EXT>(A, blockIdx.x - A.n_groups, per, lds);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
   const int we = wo > wm ? wo - wm : 0;
@@ -646,8 +654,6 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A) {
       for (uint32_t i = (uint32_t)lane + kW * kWave; i < sz; i += kWave) out[o0 + i] = src[i];
     }
   }
-  (void)lds;
-  (void)s_cnt;
 }
 
 // Blocks whose variable section outgrew the scratch slot (escape-heavy data: a channel of an
@@ -657,8 +663,7 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A) {
 // (a CIFAR ResNet activation: up to 0.7 ms per call). A block's offset: its group's prefix plus the
 // sizes of the group's blocks before it (from meta).
 template <int RM, int TIN, bool EXT>
-__global__ __launch_bounds__(kBlock) void smaq_pack_recode_kernel(PackArgs A, uint32_t per) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // 128 * we words
+__device__ void pack_recode_blocks(const PackArgs& A, uint32_t wg, uint32_t per, uint32_t* lds) {
   __shared__ uint32_t s_cnt[kBlock / kWave];
   __shared__ uint32_t list[kBlock];
   __shared__ uint32_t n_list;
@@ -668,7 +673,7 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_recode_kernel(PackArgs A, ui
   // the workgroup's blocks' flags in one round of loads (per <= kBlock), the re-code list in LDS
   if (threadIdx.x == 0) n_list = 0u;
   __syncthreads();
-  const uint32_t bt = blockIdx.x * per + threadIdx.x;
+  const uint32_t bt = wg * per + threadIdx.x;
   if (threadIdx.x < per && bt < A.n_blocks && (A.meta[bt] & kMetaRecode))
     list[atomicAdd(&n_list, 1u)] = bt;
   __syncthreads();
@@ -714,11 +719,10 @@ void launch_pack_w(const PackArgs& A, bool vec, hipStream_t st) {
                        dim3(kBlock), lds, st, A);
   hipLaunchKernelGGL(smaq_pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, A);
   const int we = A.wo > A.wm ? A.wo - A.wm : 0;
-  hipLaunchKernelGGL((smaq_pack_var_kernel<RM, TIN, WM, WO, EXT>), dim3(A.n_groups), dim3(kBlock),
-                     4 * 128 * (size_t)(we > 0 ? we : 1), st, A);
   const uint32_t per = rare_per(A.n_blocks);
-  hipLaunchKernelGGL((smaq_pack_recode_kernel<RM, TIN, EXT>), dim3((A.n_blocks + per - 1) / per),
-                     dim3(kBlock), 4 * 128 * (size_t)(we > 0 ? we : 1), st, A, per);
+  hipLaunchKernelGGL((smaq_pack_var_kernel<RM, TIN, WM, WO, EXT>),
+                     dim3(A.n_groups + (A.n_blocks + per - 1) / per), dim3(kBlock),
+                     4 * 128 * (size_t)(we > 0 ? we : 1), st, A, per);
 }
 
 // ext: the BN variant or T_m <= 0 (ext_quant, runtime widths); else the packer's own element.

@@ -41,6 +41,7 @@ SHORT = {
     "smaq_fused_kernel": "smaq_fused_kernel",
     "smaq_stats_small_kernel": "smaq_stats_small_kernel",
     "smq_fill_kernel": "smq_fill_kernel",
+    "smaq_pack_recode_kernel": "smaq_pack_recode_kernel",
 }
 
 
