@@ -447,6 +447,13 @@ uint32_t smq_rng_u32(uint64_t seed, uint64_t counter);
  * 2^-24): the top 24 bits of quad_word(key, counter >> 2) * an odd multiplier of counter & 3 — one
  * hash per four consecutive counters (oracle/rng.py smaq_u24 restates it). */
 uint32_t smq_smaq_u24(uint64_t seed, uint64_t counter);
+/* Half inputs (dtype SMQ_DTYPE_F16 / BF16, no BN term): the two-op fp32 quotient the apply launch
+ * uses for q / range, out[0..3] = {h_main, l_main, h_outlier, l_outlier} with h = RN32(1 / r),
+ * l = RN32(1 / r - h), q / r == fmaf(q, h, q * l). Returns 1 when that equals the IEEE quotient for
+ * every code the flags can produce (every half z-score; floor + 0/1/2 when stochastic, else trunc),
+ * 0 when the launch keeps the fp64 form. oracle/csrc/half_div_check.c (qr mode) restates it. */
+int smq_half_quot_split(int dtype, float main_std_dev_threshold, float range_main,
+                        float range_outlier, int stochastic_rounding, float* out);
 
 
 /* ---------------------------------------------------------------------------------------------

@@ -318,6 +318,7 @@ struct ApplyArgs {
   float thr, r_main, r_out, clamp_lo, clamp_hi, range_coef;
   double inv_r_main, inv_r_out;  // host-computed reciprocals of the ranges
   int safe_q;
+  QuotSplit qs;                  // half inputs without BN: the checked two-op quotient (qs.ok)
   unsigned long long* rng_ctr;   // params.offset_counter (graph-safe stream) or NULL
   uint32_t key;
   int all_pos;
@@ -597,7 +598,8 @@ __global__ void smaq_prep_injected_kernel(const SmqSmaqStats* in, SmqSmaqStats* 
 // kBlock * TV float4 dispatched in (reverse) address order, one front across the grid.
 // SUB: see quot_check_for. The unaligned (!VEC) variant always keeps the subnormal check and
 // divides q / range by IEEE division (the launcher routes safe_q calls to it).
-template <int RM, bool VEC, bool BN, int TIN, int TV, bool AP, bool SUB, bool DEF = false>
+template <int RM, bool VEC, bool BN, int TIN, int TV, bool AP, bool SUB, bool DEF = false,
+          bool QF = false>
 __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, ElemConsts& c, uint64_t off,
                                                float cthr) {
   constexpr int kTileElems = kBlock * TV * 4;
@@ -639,13 +641,13 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, ElemConsts& c
       bool b0, b1, b2, b3;
       float4 o;
       if constexpr (RAW16) {
-        smaq_elem_f16x2<RM, AP>(hv[u].x, u0, u1, c, o.x, o.y, b0, b1);
-        smaq_elem_f16x2<RM, AP>(hv[u].y, u2, u3, c, o.z, o.w, b2, b3);
+        smaq_elem_f16x2<RM, AP, QF>(hv[u].x, u0, u1, c, o.x, o.y, b0, b1);
+        smaq_elem_f16x2<RM, AP, QF>(hv[u].y, u2, u3, c, o.z, o.w, b2, b3);
       } else {
-        o.x = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].x, u0, c, b0, bn_term<BN>(A, 4 * j + 0));
-        o.y = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].y, u1, c, b1, bn_term<BN>(A, 4 * j + 1));
-        o.z = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].z, u2, c, b2, bn_term<BN>(A, 4 * j + 2));
-        o.w = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(v[u].w, u3, c, b3, bn_term<BN>(A, 4 * j + 3));
+        o.x = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC, QF>(v[u].x, u0, c, b0, bn_term<BN>(A, 4 * j + 0));
+        o.y = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC, QF>(v[u].y, u1, c, b1, bn_term<BN>(A, 4 * j + 1));
+        o.z = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC, QF>(v[u].z, u2, c, b2, bn_term<BN>(A, 4 * j + 2));
+        o.w = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC, QF>(v[u].w, u3, c, b3, bn_term<BN>(A, 4 * j + 3));
       }
       n_out += (unsigned)b0 + (unsigned)b1 + (unsigned)b2 + (unsigned)b3;
       store_stream(y4 + j, o);
@@ -657,7 +659,7 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, ElemConsts& c
       if (RM == kRoundHash) uf = rng_hu(A.key, off + (uint64_t)e);
       if (RM == kRoundUniform) uf = A.uniforms[e];
       bool bt;
-      A.y[e] = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC>(load1<TIN>(A.x, e), uf, c, bt, bn_term<BN>(A, e));
+      A.y[e] = smaq_elem<RM, BN, TIN, AP, SUB || !VEC, !VEC, QF>(load1<TIN>(A.x, e), uf, c, bt, bn_term<BN>(A, e));
       n_out += (unsigned)bt;
     }
   } else {
@@ -693,7 +695,12 @@ __global__ __launch_bounds__(kBlock) void smaq_apply_kernel(ApplyArgs A) {
   } else {
     init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, cthr);
     const uint64_t off = A.offset + A.stats->rng_offset;  // + graph-safe stream position
-    if (!VEC) {
+    constexpr bool kQF = VEC && !BN && TIN != kF32;  // (SUB has no effect on half z-scores)
+    if (kQF && A.qs.ok) {
+      c.qs = A.qs;
+      n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true, false, kQF>(A, c, off, cthr)
+                        : apply_body<RM, VEC, BN, TIN, TV, false, true, false, kQF>(A, c, off, cthr);
+    } else if (!VEC) {
       n_out = A.all_pos ? apply_body<RM, VEC, BN, TIN, TV, true, true>(A, c, off, cthr)
                         : apply_body<RM, VEC, BN, TIN, TV, false, true>(A, c, off, cthr);
     } else if (A.stats->quot_check) {
@@ -1061,6 +1068,15 @@ static int launch_apply(const void* x, int dtype, float* y, int64_t n, const Smq
   A.all_pos = p->all_positive;
   A.count = p->count_outliers;
   A.use_range = p->use_range_std_dev;
+  // half inputs: the fp32 quotient form when every reachable code checks (measurement knob
+  // SMQ_HALF_QF=0 keeps the fp64 form)
+  static const int qf_env = [] {
+    const char* e = knob_env("SMQ_HALF_QF");
+    return e ? atoi(e) : 1;
+  }();
+  if (dtype != SMQ_DTYPE_F32 && !p->bn_gamma && !def_g && qf_env)
+    A.qs = quot_split_for(dtype, A.thr, A.r_main, A.r_out,
+                          p->stochastic_rounding ? kRoundHash : kRoundTrunc);
   if (def_g) {  // the statistics launch left def_g partials (launch_stats)
     A.def_parts = (const StatPartial*)((const char*)ws + SmaqWsLayout::kPartials);
     A.def_rec = (const double*)((const char*)ws + SmaqWsLayout::kDeferRec);
@@ -1206,6 +1222,20 @@ const char* smq_last_error(void) { return g_err; }
 
 uint32_t smq_rng_u32(uint64_t seed, uint64_t counter) { return rng_u32(rng_key(seed), counter); }
 uint32_t smq_smaq_u24(uint64_t seed, uint64_t counter) { return smaq_u24(rng_key(seed), counter); }
+
+int smq_half_quot_split(int dtype, float thr, float r_main, float r_out, int stochastic_rounding,
+                        float* out) {
+  if (dtype != SMQ_DTYPE_F16 && dtype != SMQ_DTYPE_BF16) return 0;
+  const QuotSplit s = quot_split_compute(dtype, thr, r_main, r_out,
+                                         stochastic_rounding ? kRoundHash : kRoundTrunc);
+  if (out) {
+    out[0] = s.hm;
+    out[1] = s.lm;
+    out[2] = s.ho;
+    out[3] = s.lo;
+  }
+  return s.ok;
+}
 
 void smq_smaq_params_init(SmqSmaqParams* p) {
   memset(p, 0, sizeof(*p));

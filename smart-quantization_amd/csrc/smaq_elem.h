@@ -189,6 +189,12 @@ __device__ __forceinline__ void finalize_stats(double s1, double s2, float mn, f
 // ------------------------------------------------------------------------------------------------
 // element transform
 // ------------------------------------------------------------------------------------------------
+// The two-op fp32 quotient q / range for half inputs (quot_split_compute below).
+struct QuotSplit {
+  float hm, lm, ho, lo;  // main / outlier range: h = RN32(1 / r), l = RN32(1 / r - h)
+  int ok;                // every reachable code checked
+};
+
 struct ElemConsts {
   float mean, sd, sc;     // mean, std (after ==0 rule), clamped std
   float thr, nthr;        // fp32(T_m), -fp32(T_m): the values of the scalars tensor (fp32)
@@ -198,7 +204,8 @@ struct ElemConsts {
   double inv_sc;          // RN64(1 / sc): written by the statistics finaliser
   float inv_sc32;         // RN32(1 / sc): half inputs (half_quot)
   double inv_r_main, inv_r_out;  // RN64(1 / range): computed on the host
-  uint64_t rng_off;       // the call's graph-safe stream position (SmqSmaqStats.rng_offset)
+  QuotSplit qs;           // half inputs: the two-op fp32 quotient (quot_split_for), QF forms only
+  uint64_t rng_off;      // the call's graph-safe stream position (SmqSmaqStats.rng_offset)
 };
 
 // Correctly rounded fp32 quotient a / b from a double reciprocal: RN32(RN64(a * RN64(1/b))).
@@ -251,6 +258,108 @@ static inline RangeRecips range_recips(float r_main, float r_out) {
   return R;
 }
 
+enum RoundMode { kRoundHash = 0, kRoundUniform = 1, kRoundTrunc = 2 };
+
+// Half inputs without the BN term: the z-score is a half value (65,536 bit patterns), so the codes
+// the element transform can produce form a finite set fixed by the flags — per z-score floor(d) and
+// floor(d) + 1 or + 2 (stochastic rounding, whatever the draw) or trunc(d). Over that set the quotient
+// q / range takes two fp32 ops,
+//     RN32(q / r) == fmaf(q, h, RN32(q * l)),   h = RN32(1 / r),  l = RN32(1 / r - h),
+// checked exhaustively on the host against the IEEE quotient, once per flag set (~130K codes,
+// <1 ms, cached); when every code passes (ok), the half apply launch takes this form instead of
+// the fp64 reciprocal product (a 64-bit select, cvt, v_mul_f64, cvt). A flag set with one failing
+// code keeps the fp64 form. Sweep of 17,640 SmaQ flag sets (num_bits 3-16, thresholds on a grid):
+// every stochastic-rounding set passes; under truncation q = +-inf is reachable (an overflowing
+// z-score) and fails whenever l < 0 (inf - inf), so most truncating sets keep the fp64 form.
+// The reachable-set argument and the check are restated in oracle/csrc/half_div_check.c (qr mode).
+// (struct QuotSplit: above ElemConsts)
+
+static inline float host_half_value(int tin, uint32_t b) {  // fp16 / bf16 bits -> fp32 (exact)
+  if (tin == kBF16) return __builtin_bit_cast(float, b << 16);
+  const uint32_t s = (b & 0x8000u) << 16, e = (b >> 10) & 0x1fu, m = b & 0x3ffu;
+  if (e == 0x1fu) return __builtin_bit_cast(float, s | 0x7f800000u | (m << 13));
+  if (e == 0) return m ? (s ? -1.0f : 1.0f) * (float)m * 0x1p-24f : __builtin_bit_cast(float, s);
+  return __builtin_bit_cast(float, s | ((e + 112u) << 23) | (m << 13));
+}
+
+static inline float host_round_half(int tin, float v) {  // round_in<tin> on the host (finite v)
+  const uint32_t x = __builtin_bit_cast(uint32_t, v), s = x & 0x80000000u, ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return v;
+  if (tin == kBF16) return __builtin_bit_cast(float, (x + 0x7fffu + ((x >> 16) & 1u)) & 0xffff0000u);
+  if (ax >= 0x477ff000u) return __builtin_bit_cast(float, s | 0x7f800000u);
+  if (ax < 0x38800000u)
+    return __builtin_bit_cast(float, s | __builtin_bit_cast(uint32_t, nearbyintf(__builtin_bit_cast(float, ax) * 0x1p24f) * 0x1p-24f));
+  return __builtin_bit_cast(float, s | ((ax + 0x0fffu + ((ax >> 13) & 1u)) & ~0x1fffu));
+}
+
+// rm: RoundMode (kRoundTrunc or a stochastic one; the draw does not matter).
+static inline QuotSplit quot_split_compute(int tin, float thr, float r_main, float r_out, int rm) {
+  QuotSplit s;
+  s.hm = (float)(1.0 / (double)r_main);
+  s.lm = (float)(1.0 / (double)r_main - (double)s.hm);
+  s.ho = (float)(1.0 / (double)r_out);
+  s.lo = (float)(1.0 / (double)r_out - (double)s.ho);
+  s.ok = 0;
+  if (!(__builtin_isfinite(r_main) && __builtin_isfinite(r_out) && __builtin_isfinite(s.hm) &&
+        __builtin_isfinite(s.ho)))
+    return s;
+  const float cthr = host_round_half(tin, thr), cnthr = -cthr;
+  const float nthr = -thr, zh = 0.0f * nthr, zl = 0.0f * thr;
+  for (uint32_t b = 0; b < 0x10000u; ++b) {
+    const float z = host_half_value(tin, b);
+    const bool hi = z > cthr, lo = z < cnthr, o = hi || lo;
+    const float a = (hi ? nthr : zh) + (lo ? thr : zl);
+    const float r = o ? r_out : r_main;
+    const volatile float za = z + a;  // two roundings, as on the device
+    const float d = za * r;
+    float qs[3];
+    int nq = 1;
+    if (rm == kRoundTrunc) {
+      qs[0] = truncf(d);
+    } else {
+      // f + rint(relu(RN(fr - u) + 0.5)) with fr = d - f in [0, 1): 0 or 1 is added, and 2 when
+      // RN(fr + 0.5) ties up to 1.5 (fr = 1 - 2^-24, d < 1). d = +-inf: fr = NaN, q = NaN.
+      if (__builtin_isinf(d)) continue;
+      qs[0] = floorf(d);
+      const volatile float f1 = qs[0] + 1.0f, f2 = qs[0] + 2.0f;
+      qs[1] = f1;
+      qs[2] = f2;
+      nq = 3;
+    }
+    for (int i = 0; i < nq; ++i) {
+      const float q = qs[i];
+      const volatile float want = q / r;
+      const volatile float ql = q * (o ? s.lo : s.lm);
+      const float got = fmaf(q, o ? s.ho : s.hm, ql);
+      const float w = want;
+      if (!(__builtin_bit_cast(uint32_t, w) == __builtin_bit_cast(uint32_t, got) ||
+            (w != w && got != got)))
+        return s;
+    }
+  }
+  s.ok = 1;
+  return s;
+}
+
+// The check cached per flag set (per thread: no lock on the launch path).
+static inline QuotSplit quot_split_for(int tin, float thr, float r_main, float r_out, int rm) {
+  struct Key {
+    int tin, rm;
+    float thr, r_main, r_out;
+  };
+  thread_local Key key{-1, -1, 0.0f, 0.0f, 0.0f};
+  thread_local QuotSplit val{};
+  const bool trunc = rm == kRoundTrunc;
+  if (key.tin != tin || (key.rm == kRoundTrunc) != trunc ||
+      __builtin_bit_cast(uint32_t, key.thr) != __builtin_bit_cast(uint32_t, thr) ||
+      __builtin_bit_cast(uint32_t, key.r_main) != __builtin_bit_cast(uint32_t, r_main) ||
+      __builtin_bit_cast(uint32_t, key.r_out) != __builtin_bit_cast(uint32_t, r_out)) {
+    val = quot_split_compute(tin, thr, r_main, r_out, rm);
+    key = Key{tin, rm, thr, r_main, r_out};
+  }
+  return val;
+}
+
 // kRoundHash draws: smaq_u24 (smq_common.h) as a float (exact, < 2^24), see smaq_elem.
 __device__ __forceinline__ float rng_hu(uint32_t key, uint64_t ctr) {
   return (float)smaq_u24(key, ctr);
@@ -279,8 +388,8 @@ __device__ __forceinline__ void rng_hu4(uint32_t key, uint64_t ctr, float& u0, f
 }
 
 // kRoundHash: u arrives as the integer h >> 8 (a float in [0, 2^24)); fr - u is then the single
-// rounding fma(h, -2^-24, fr) == RN(fr - h * 2^-24) (the product is exact), one op fewer.
-enum RoundMode { kRoundHash = 0, kRoundUniform = 1, kRoundTrunc = 2 };
+// rounding fma(h, -2^-24, fr) == RN(fr - h * 2^-24) (the product is exact), one op fewer
+// (RoundMode above).
 
 // Per-channel BatchNorm fold (smart.py:144-149 before, 174-179 after); scale = gamma[c].
 struct BnTerm {
@@ -345,14 +454,20 @@ __device__ __forceinline__ float smaq_quant(float v, float u, const ElemConsts& 
 }
 
 // smart.py:171-182: de-quantise a code q with its outlier sides.
-template <bool BN = false, bool AP = false, bool SQ = false>
+// QF: the two-op fp32 quotient of a checked flag set (QuotSplit; half inputs without BN only).
+template <bool BN = false, bool AP = false, bool SQ = false, bool QF = false>
 __device__ __forceinline__ float smaq_dequant(float q, bool hi, bool lo, const ElemConsts& c,
                                               BnTerm bn = BnTerm{1.0f, 0.0f}) {
   const bool o = hi | lo;
   const float a = (hi ? c.nthr : c.zh) + (lo ? c.thr : c.zl);  // scalars
-  const float r = o ? c.r_out : c.r_main;               // ranges
-  const double inv_r = o ? c.inv_r_out : c.inv_r_main;
-  const float qr = SQ ? q / r : div_by_const(q, inv_r);  // data / ranges
+  float qr;                                             // data / ranges
+  if (QF) {
+    qr = __builtin_fmaf(q, o ? c.qs.ho : c.qs.hm, q * (o ? c.qs.lo : c.qs.lm));
+  } else if (SQ) {
+    qr = q / (o ? c.r_out : c.r_main);
+  } else {
+    qr = div_by_const(q, o ? c.inv_r_out : c.inv_r_main);
+  }
   float out = qr - a;                                   //   - scalars
   out = (out * c.sd) + c.mean;
   if (BN) out = (out * bn.gamma) + bn.beta;             // (data * gamma) + beta
@@ -362,13 +477,15 @@ __device__ __forceinline__ float smaq_dequant(float q, bool hi, bool lo, const E
 
 // One element of smart.py:154-182 (quant then dequant, every statement one rounded fp32 op of the
 // reference). T = input type (z-score rounded to it unless BN already promoted the data to fp32).
-template <int RM, bool BN = false, int T = kF32, bool AP = false, bool SUB = true, bool SQ = false>
+template <int RM, bool BN = false, int T = kF32, bool AP = false, bool SUB = true, bool SQ = false,
+          bool QF = false>
 __device__ __forceinline__ float smaq_elem(float v, float u, const ElemConsts& c,
                                            bool& is_outlier, BnTerm bn = BnTerm{1.0f, 0.0f}) {
+  static_assert(!QF || (!BN && T != kF32 && !SQ), "QF: half inputs without BN");
   bool hi, lo;
   const float q = smaq_quant<RM, BN, T, SUB>(v, u, c, hi, lo, bn);
   is_outlier = hi | lo;
-  return smaq_dequant<BN, AP, SQ>(q, hi, lo, c, bn);
+  return smaq_dequant<BN, AP, SQ, QF>(q, hi, lo, c, bn);
 }
 
 // smart.py:155-169 from the z-score on (smaq_quant's tail, no BN term): the code q and the sides.
@@ -395,7 +512,7 @@ __device__ __forceinline__ float smaq_quant_z(float z, float u, const ElemConsts
 // chain per element, exactly smaq_elem<RM, false, kF16, AP, SUB>.
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-template <int RM, bool AP>
+template <int RM, bool AP, bool QF = false>
 __device__ __forceinline__ void smaq_elem_f16x2(uint32_t raw, float u0, float u1,
                                                 const ElemConsts& c, float& o0, float& o1,
                                                 bool& b0, bool& b1) {
@@ -409,8 +526,8 @@ __device__ __forceinline__ void smaq_elem_f16x2(uint32_t raw, float u0, float u1
   const float q1 = smaq_quant_z<RM>(z.y, u1, c, hi1, lo1);
   b0 = hi0 | lo0;
   b1 = hi1 | lo1;
-  o0 = smaq_dequant<false, AP, false>(q0, hi0, lo0, c);
-  o1 = smaq_dequant<false, AP, false>(q1, hi1, lo1, c);
+  o0 = smaq_dequant<false, AP, false, QF>(q0, hi0, lo0, c);
+  o1 = smaq_dequant<false, AP, false, QF>(q1, hi1, lo1, c);
 }
 
 // ------------------------------------------------------------------------------------------------

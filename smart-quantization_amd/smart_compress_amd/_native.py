@@ -266,6 +266,8 @@ SIGNATURES = {
     ),
     "smq_rng_u32": (ctypes.c_uint32, [_U64, _U64]),
     "smq_smaq_u24": (ctypes.c_uint32, [_U64, _U64]),
+    "smq_half_quot_split": (ctypes.c_int, [ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                           ctypes.c_float, ctypes.c_int, _P]),
     "smq_smaq_pack_bound": (_SZ, [_I64, _I32, _I32]),
     "smq_smaq_pack_bound_bn": (_SZ, [_I64, _I32, _I32, _I64]),
     "smq_smaq_pack_workspace_bytes": (_SZ, [_I64]),

@@ -9,6 +9,8 @@ Tolerances (north_star: "within 1 ulp of the target low-precision format"):
     1.001 quantisation steps (step = std / range of the element's class).
 """
 
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -423,6 +425,42 @@ def test_half_inputs_end_to_end(dt, offset_elems, n):
     _assert_stats_close(st["mean"], mo, dt)
     _assert_stats_close(st["raw_std"], so, dt)
     y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], cfg, orng.uniforms(3, 10, xn.size),
+                          dtype=dt)
+    assert same_f32(y.cpu().numpy(), y_or)
+
+
+@pytest.mark.parametrize("dt", ["f16", "bf16"])
+def test_half_apply_fp32_quotient_extremes(dt):
+    """The non-deferred half apply takes the two-op fp32 quotient q / range (smq_half_quot_split,
+    checked over every reachable code): data whose std exceeds the precision-16 clamp (1e4) gives
+    z-scores far beyond the thresholds — bf16 at 1e30 scale: codes up to ~1e27, fp16 near its
+    maximum: z ~ 6 and every class — still bit-exact against the oracle."""
+    from oracle import rng as orng
+    from oracle import smaq as osmaq
+    from smart_compress_amd import _native as N
+    from smart_compress_amd.compress.smart import SmartFP
+
+    g = _gpu()
+    n = (3 << 22) + 8  # above kDeferMaxN: the statistics + apply launches
+    gen = torch.Generator(device="cuda").manual_seed(12)
+    base = torch.randn(n, generator=gen, device="cuda")
+    base = base * 1e30 if dt == "bf16" else (base * 2e4).clamp(-6e4, 6e4)
+    x = base.to(g.TORCH_DT[dt])
+    hp = smaq_hparams(precision=16)
+    codec = SmartFP(hp)
+    codec.rng.seed, codec.rng.offset = 5, 3
+    out = (ctypes.c_float * 4)()
+    assert N.lib().smq_half_quot_split(N.SMQ_DTYPE_F16 if dt == "f16" else N.SMQ_DTYPE_BF16,
+                                       float(np.float32(hp.main_std_dev_threshold)),
+                                       float(np.float32(codec.range_normal)),
+                                       float(np.float32(codec.range_outlier)), 1, out) == 1
+    y = codec(x)
+    torch.cuda.synchronize()
+    st = g.read_stats(_smaq_ws())
+    assert st["std_clamped"] < st["raw_std"]  # the clamp is active
+    xn = x.float().cpu().numpy()
+    cfg = osmaq.SmaqConfig(precision=16)
+    y_or, _ = osmaq.apply(xn, st["mean"], st["raw_std"], cfg, orng.uniforms(5, 3, xn.size),
                           dtype=dt)
     assert same_f32(y.cpu().numpy(), y_or)
 

@@ -1,0 +1,62 @@
+// Host cost of one smq_smaq_roundtrip call (the library's enqueue: argument checks, parameter
+// block, hipLaunchKernel) against a bare hipLaunchKernel of an empty kernel with the same
+// argument size, both back to back on one stream without synchronisation (the device keeps up:
+// 64K-element calls). Microseconds of host time per call.
+//
+// hipcc --offload-arch=gfx950 -O2 -I include tools/launch_cost.hip -L smart-quantization_amd/lib
+//   -lsmq -Wl,-rpath,$PWD/smart-quantization_amd/lib -o tools/launch_cost
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <vector>
+
+#include "smq.h"
+
+struct Big {
+  char b[256];
+};
+__global__ void empty_kernel(Big) {}
+
+static double us_per(int reps, auto&& fn) {
+  for (int i = 0; i < 200; ++i) fn();
+  hipDeviceSynchronize();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < reps; ++i) fn();
+  const auto t1 = std::chrono::steady_clock::now();
+  hipDeviceSynchronize();
+  return std::chrono::duration<double, std::micro>(t1 - t0).count() / reps;
+}
+
+int main() {
+  const int64_t n = 1 << 16;
+  float *x, *y;
+  void* ws;
+  const size_t wsb = smq_smaq_workspace_bytes(n);
+  hipMalloc(&x, 4 * n);
+  hipMalloc(&y, 4 * n);
+  hipMalloc(&ws, wsb);
+  hipMemset(ws, 0, wsb);
+  std::vector<float> h(n);
+  for (int64_t i = 0; i < n; ++i) h[i] = (float)((i * 7919) % 1000) / 500.0f - 1.0f;
+  hipMemcpy(x, h.data(), 4 * n, hipMemcpyHostToDevice);
+  hipStream_t st;
+  hipStreamCreate(&st);
+  SmqSmaqParams p;
+  smq_smaq_params_init(&p);
+  p.seed = 1;
+  Big big{};
+  const int reps = 20000;
+  const double t_empty = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel, dim3(16), dim3(1024), 0, st, big); });
+  const double t_empty_small = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st, big); });
+  uint64_t off = 0;
+  const double t_smaq = us_per(reps, [&] {
+    p.offset = off;
+    off += n;
+    smq_smaq_roundtrip(x, SMQ_DTYPE_F32, y, n, &p, nullptr, ws, wsb, st);
+  });
+  const double t_err = us_per(reps, [&] { (void)hipGetLastError(); });
+  std::printf("{\"empty_launch_us\": %.3f, \"empty_launch_1wg_us\": %.3f, \"smq_smaq_roundtrip_us\": %.3f, "
+              "\"hipGetLastError_us\": %.3f}\n", t_empty, t_empty_small, t_smaq, t_err);
+  return 0;
+}
