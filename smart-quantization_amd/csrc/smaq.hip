@@ -628,13 +628,14 @@ __device__ __forceinline__ uint32_t apply_body(const ApplyArgs& A, ElemConsts& c
       }
     }
     if (DEF) defer_consts<TIN>(A, c, off, cthr);  // with this tile's loads in flight
+    const QuadRun R = quad_run(A.key, off, (uint64_t)nv);
 #pragma unroll
     for (int u = 0; u < TV; ++u) {
       const int64_t j = t0 + u * kBlock;
       if (j >= nv) continue;
       float u0 = 0.0f, u1 = 0.0f, u2 = 0.0f, u3 = 0.0f;
       if (RM == kRoundHash) {
-        rng_hu4(A.key, off + ((uint64_t)j << 2), u0, u1, u2, u3);
+        rng_hu4_run(R, (uint32_t)j, u0, u1, u2, u3);
       } else if (RM == kRoundUniform) {
         u0 = uu[u].x; u1 = uu[u].y; u2 = uu[u].z; u3 = uu[u].w;
       }

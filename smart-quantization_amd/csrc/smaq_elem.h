@@ -387,6 +387,61 @@ __device__ __forceinline__ void rng_hu4(uint32_t key, uint64_t ctr, float& u0, f
   }
 }
 
+// The same draws for the float4 groups j = 0, 1, ... of a run starting at counter c0: group j's
+// counters are c0 + 4j .. + 3, so its quads are (c0 >> 2) + j (and the next one when c0 & 3 != 0).
+// c0 is a per-launch (or per-workgroup) value, so the offset within the quad, the quad's high word
+// and its contribution to quad_word are scalar; as long as (c0 >> 2) + j + 1 does not carry into
+// the high word for any group of the run (flat: checked once, on the scalar unit) a group costs a
+// 32-bit add and the mix instead of a 64-bit add, the high-word rotate and a per-lane test of
+// c & 3. A run that crosses a 2^32-quad boundary (one call in 2^34 stream elements) takes rng_hu4.
+struct QuadRun {
+  uint64_t c0;
+  uint32_t key, keyx;  // keyx = key ^ rot16(high word of the quad index)
+  uint32_t qlo, s;     // low word of c0 >> 2, c0 & 3
+  bool flat;
+};
+
+__device__ __forceinline__ QuadRun quad_run(uint32_t key, uint64_t c0, uint64_t groups) {
+  QuadRun R;
+  // c0 is uniform, but read from memory (the statistics record) the compiler cannot prove it:
+  // readfirstlane puts it (and everything derived) in SGPRs, so the tests below are scalar branches
+  c0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)c0) |
+       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(c0 >> 32)) << 32);
+  key = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+  const uint64_t q = c0 >> 2;
+  const uint32_t hi = (uint32_t)(q >> 32);
+  R.c0 = c0;
+  R.key = key;
+  R.keyx = key ^ ((hi << 16) | (hi >> 16));
+  R.qlo = (uint32_t)q;
+  R.s = (uint32_t)c0 & 3u;
+  R.flat = (uint64_t)R.qlo + groups + 1u <= 0xffffffffull;
+  return R;
+}
+
+__device__ __forceinline__ void rng_hu4_run(const QuadRun& R, uint32_t j, float& u0, float& u1,
+                                            float& u2, float& u3) {
+  if (__builtin_expect(!R.flat, 0)) {
+    rng_hu4(R.key, R.c0 + ((uint64_t)j << 2), u0, u1, u2, u3);
+    return;
+  }
+  const uint32_t q = R.qlo + j;
+  const uint32_t s = R.s;
+  if (__builtin_expect(s == 0u, 1)) {
+    const uint32_t h = mix32x3(q ^ R.keyx);
+    u0 = (float)(h >> 8);
+    u1 = (float)((h * draw_mul(1u)) >> 8);
+    u2 = (float)((h * draw_mul(2u)) >> 8);
+    u3 = (float)((h * draw_mul(3u)) >> 8);
+  } else {
+    const uint32_t h0 = mix32x3(q ^ R.keyx), h1 = mix32x3((q + 1u) ^ R.keyx);
+    u0 = (float)((h0 * draw_mul(s)) >> 8);
+    u1 = (float)(((s + 1u < 4u ? h0 : h1) * draw_mul((s + 1u) & 3u)) >> 8);
+    u2 = (float)(((s + 2u < 4u ? h0 : h1) * draw_mul((s + 2u) & 3u)) >> 8);
+    u3 = (float)((h1 * draw_mul((s + 3u) & 3u)) >> 8);
+  }
+}
+
 // kRoundHash: u arrives as the integer h >> 8 (a float in [0, 2^24)); fr - u is then the single
 // rounding fma(h, -2^-24, fr) == RN(fr - h * 2^-24) (the product is exact), one op fewer
 // (RoundMode above).

@@ -233,6 +233,7 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
   const bool mwriter = (lane & 7) == 7;
   const uint32_t ppos0 = 4u * (uint32_t)wm * (uint32_t)tid;
   const uint32_t pw0 = ppos0 >> 5, psft = ppos0 & 31u;
+  const QuadRun R = quad_run(A.key, A.offset + c.rng_off + (uint64_t)e0, kPB / 4);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int el = 1024 * k + 4 * tid;
@@ -241,7 +242,7 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
     if (RM == kRoundHash) {
       const uint64_t ctr = A.offset + c.rng_off + (uint64_t)(e0 + el);
       if (full4) {
-        rng_hu4(A.key, ctr, u[0], u[1], u[2], u[3]);
+        rng_hu4_run(R, 256u * (uint32_t)k + (uint32_t)tid, u[0], u[1], u[2], u[3]);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)

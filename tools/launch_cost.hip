@@ -13,10 +13,12 @@
 
 #include "smq.h"
 
-struct Big {
-  char b[256];
+template <int B>
+struct Args {
+  char b[B];
 };
-__global__ void empty_kernel(Big) {}
+template <int B>
+__global__ void empty_kernel(Args<B>) {}
 
 static double us_per(int reps, auto&& fn) {
   for (int i = 0; i < 200; ++i) fn();
@@ -45,10 +47,19 @@ int main() {
   SmqSmaqParams p;
   smq_smaq_params_init(&p);
   p.seed = 1;
-  Big big{};
   const int reps = 20000;
-  const double t_empty = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel, dim3(16), dim3(1024), 0, st, big); });
-  const double t_empty_small = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st, big); });
+  Args<256> big{};
+  Args<16> a16{};
+  Args<64> a64{};
+  Args<1024> a1k{};
+  const double t_empty = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel<256>, dim3(16), dim3(1024), 0, st, big); });
+  const double t_empty_small = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel<256>, dim3(1), dim3(64), 0, st, big); });
+  const double t16 = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel<16>, dim3(16), dim3(256), 0, st, a16); });
+  const double t64 = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel<64>, dim3(16), dim3(256), 0, st, a64); });
+  const double t1k = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel<1024>, dim3(16), dim3(256), 0, st, a1k); });
+  hipStream_t st2;
+  hipStreamCreateWithFlags(&st2, hipStreamNonBlocking);
+  const double t16nb = us_per(reps, [&] { hipLaunchKernelGGL(empty_kernel<16>, dim3(16), dim3(256), 0, st2, a16); });
   uint64_t off = 0;
   const double t_smaq = us_per(reps, [&] {
     p.offset = off;
@@ -57,6 +68,8 @@ int main() {
   });
   const double t_err = us_per(reps, [&] { (void)hipGetLastError(); });
   std::printf("{\"empty_launch_us\": %.3f, \"empty_launch_1wg_us\": %.3f, \"smq_smaq_roundtrip_us\": %.3f, "
-              "\"hipGetLastError_us\": %.3f}\n", t_empty, t_empty_small, t_smaq, t_err);
+              "\"hipGetLastError_us\": %.3f, \"args16_us\": %.3f, \"args64_us\": %.3f, "
+              "\"args1024_us\": %.3f, \"args16_nonblocking_us\": %.3f}\n", t_empty, t_empty_small,
+              t_smaq, t_err, t16, t64, t1k, t16nb);
   return 0;
 }
