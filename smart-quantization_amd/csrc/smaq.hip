@@ -121,6 +121,7 @@ __global__ __launch_bounds__(kBlock) void smaq_stats_kernel(const void* __restri
                                                             ArriveTag tag, SmqSmaqStats* out,
                                                             int64_t nt_end, double* def_rec) {
   __shared__ uint32_t arrive_slot;
+  clear_aux(fin);
   // Shift = median of three fixed elements: keeps sum(x-K)^2 - (sum(x-K))^2/n well conditioned
   // unless the mean is > 2^14 standard deviations away from all three.
   const float k0 = load1<TIN>(x, 0), k1 = load1<TIN>(x, n >> 1), k2 = load1<TIN>(x, n - 1);
@@ -767,9 +768,11 @@ static int check_dtype(int dtype) {
 
 // def_g != NULL: deferred statistics (defer_consts) — *def_g = the number of partials left for the
 // apply launch, or 0 when a single workgroup finalised the header itself.
+// zero / zero_n: words the launch clears on the way (FinalizeArgs::zero).
 static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
                         size_t ws_bytes, hipStream_t st, int* def_g = nullptr,
-                        SmqSmaqStats* out = nullptr) {
+                        SmqSmaqStats* out = nullptr, uint32_t* zero = nullptr,
+                        uint32_t zero_n = 0) {
   // (the single launch's exchange region above the tag counters is not needed here)
   const size_t need = SmaqWsLayout::kTagCounters + 8 * (size_t)SmaqWsLayout::kTagWords;
   if (!ws || ws_bytes < need) {
@@ -785,7 +788,7 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
     // activation-sized tensors: the partition the single launch uses (smaq_small.h), so every path
     // gives the same statistics bit for bit
     const FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n),
-                           (unsigned long long*)p->offset_counter, n};
+                           (unsigned long long*)p->offset_counter, n, zero, zero_n};
     return launch_stats_small(x, dtype, n, vec != 0, p->use_range_std_dev != 0, fin, ws, st,
                               def_g != nullptr, def_g);
   }
@@ -831,7 +834,7 @@ static int launch_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams
   // the host's tag prediction follows the calls that use the arrival counter
   if (!def_rec) tag = arrive_tag(ws, st);
   FinalizeArgs fin{p->clamp_lo, p->clamp_hi, range_coef_for(p, n),
-                   (unsigned long long*)p->offset_counter, n};
+                   (unsigned long long*)p->offset_counter, n, zero, zero_n};
   // non-temporal loads only for tensors well beyond the Infinity Cache: there they keep the
   // sweep from thrashing it (1 GiB: 0.506-0.508 -> 0.499-0.502 ms/step); up to 256 MiB the apply
   // launch re-reads x from the cache the plain loads filled (64 / 128 / 256 MiB tensors: 0.047 /
@@ -1174,8 +1177,12 @@ static int check_tensor_args(const void* x, const float* y, int64_t n) {
 // Statistics for a consumer other than the apply kernel (the packed codec): full or sampled
 // statistics of x into the workspace header (smaq_host.h).
 int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
-                  size_t ws_bytes, hipStream_t st) {
-  if (p->stats_source == SMQ_STATS_WORKSPACE) return launch_stats(x, dtype, n, p, ws, ws_bytes, st);
+                  size_t ws_bytes, hipStream_t st, uint32_t* zero, uint32_t zero_n, bool* zeroed) {
+  if (zeroed) *zeroed = false;
+  if (p->stats_source == SMQ_STATS_WORKSPACE) {
+    if (zeroed) *zeroed = zero != nullptr;
+    return launch_stats(x, dtype, n, p, ws, ws_bytes, st, nullptr, nullptr, zero, zero_n);
+  }
   if (p->stats_source == SMQ_STATS_SAMPLED_DEVICE)
     return launch_draw_stats(x, dtype, n, p, ws, ws_bytes, st);
   if (p->stats_source != SMQ_STATS_SAMPLED) {

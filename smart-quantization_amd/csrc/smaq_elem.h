@@ -128,7 +128,16 @@ struct FinalizeArgs {
   float clamp_lo, clamp_hi, range_coef;  // range_coef is representable in the input type
   unsigned long long* rng_ctr = nullptr;  // graph-safe stream position (params.offset_counter)
   int64_t rng_n = 0;                      // elements the call consumes from it
+  uint32_t* zero = nullptr;               // words the statistics launch clears for the next
+  uint32_t zero_n = 0;                    // launch of the call (the packer's group sums)
 };
+
+// The statistics launch's first workgroup clears fin.zero (all its threads, before the sweep): the
+// packer's group sums then need no launch of their own.
+__device__ __forceinline__ void clear_aux(const FinalizeArgs& f) {
+  if (f.zero && blockIdx.x == 0)
+    for (uint32_t i = threadIdx.x; i < f.zero_n; i += blockDim.x) f.zero[i] = 0u;
+}
 
 // mean / std from shifted sums -> SmqSmaqStats (smart.py:130-134, 100-108, 151-152, 154).
 // T = input type: torch reduces half tensors in fp32/fp64 and rounds the 0-dim result to half
@@ -446,6 +455,13 @@ __device__ __forceinline__ void rng_hu4_run(const QuadRun& R, uint32_t j, float&
 // rounding fma(h, -2^-24, fr) == RN(fr - h * 2^-24) (the product is exact), one op fewer
 // (RoundMode above).
 
+// F.relu of the stochastic-rounding term t = RN(RN(fr - u) + 0.5) (smart.py:93-98) in ONE op:
+// v_maximum3_f32 (IEEE 754-2019 maximum: NaN propagates, as relu keeps it) instead of a compare
+// and a select. The two differ only for t = -0 (maximum gives +0), and t is never -0: fr = d -
+// floor(d) is never -0, so neither is w = RN(fr - u) (fma(u, -2^-24, fr) with u = 0 gives +0), and
+// w + 0.5 cannot be -0 (a sum is -0 only when both addends are; an exact cancellation gives +0).
+__device__ __forceinline__ float relu_t(float t) { return __builtin_elementwise_maximum(t, 0.0f); }
+
 // Per-channel BatchNorm fold (smart.py:144-149 before, 174-179 after); scale = gamma[c].
 struct BnTerm {
   float gamma, beta;
@@ -502,7 +518,7 @@ __device__ __forceinline__ float smaq_quant(float v, float u, const ElemConsts& 
     const float f = floorf(d);                          // _round_stochastic, smart.py:93-98
     const float fr = d - f;
     float t = ((RM == kRoundHash) ? __builtin_fmaf(u, -0x1p-24f, fr) : (fr - u)) + 0.5f;
-    t = (t < 0.0f) ? 0.0f : t;                          // F.relu
+    t = relu_t(t);                                      // F.relu
     q = f + __builtin_rintf(t);                         // .round() = half to even
   }
   return q;
@@ -557,7 +573,7 @@ __device__ __forceinline__ float smaq_quant_z(float z, float u, const ElemConsts
   const float f = floorf(d);
   const float fr = d - f;
   float t = ((RM == kRoundHash) ? __builtin_fmaf(u, -0x1p-24f, fr) : (fr - u)) + 0.5f;
-  t = (t < 0.0f) ? 0.0f : t;
+  t = relu_t(t);
   return f + __builtin_rintf(t);
 }
 

@@ -78,6 +78,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_stats_small_kernel(const void* _
                                                                    double* def_rec) {
   __shared__ SmallWaveLds W;
   __shared__ uint32_t arrive_slot;
+  clear_aux(fin);
   const int G = gridDim.x, b = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const double shift = stats_shift<TIN>(x, n);

@@ -8,8 +8,10 @@
 namespace smq {
 
 // Full or sampled statistics of x into the workspace header (SmqSmaqStats at offset 0).
+// zero / zero_n: words to clear on the way (full statistics only: *zeroed tells whether it did).
 int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
-                  size_t ws_bytes, hipStream_t st);
+                  size_t ws_bytes, hipStream_t st, uint32_t* zero = nullptr, uint32_t zero_n = 0,
+                  bool* zeroed = nullptr);
 // Full statistics of x (the single-tensor statistics launch, finalised by its last workgroup) into
 // *out instead of the workspace header (multi-tensor calls: tensors above the small partition).
 int stats_into(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,

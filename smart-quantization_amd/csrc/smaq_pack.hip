@@ -77,6 +77,7 @@ struct PackArgs {
   uint32_t n_groups;
   uint32_t flags;
   uint32_t lds_words;        // dynamic LDS of the packing kernels (PackLds::words)
+  uint32_t inline_scan;      // the var kernel sums the group prefixes itself (no scan launch)
   const float* bn_gamma;     // BN variant (general packer only), else NULL
   const float* bn_beta;
   int64_t bn_channels, bn_inner;
@@ -102,7 +103,7 @@ __device__ __forceinline__ float pack_quant(float v, float u, const ElemConsts& 
   const float f = floorf(d);                            // _round_stochastic
   const float fr = d - f;
   float t = __builtin_fmaf(u, -0x1p-24f, fr) + 0.5f;
-  t = (t < 0.0f) ? 0.0f : t;
+  t = relu_t(t);
   return f + __builtin_rintf(t);
 }
 
@@ -428,6 +429,36 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_block_kernel(PackArgs A) {
 }
 
 constexpr int kScanThreads = 1024;
+// up to this many groups of kGroup blocks (2048 groups: 537M elements) the var kernel's workgroups
+// sum the group prefixes themselves (<= 2048 loads each, 8 KB from L2) instead of waiting for a
+// one-workgroup scan launch (4.9 us at 256M)
+constexpr uint32_t kInlineScanGroups = 2048;
+
+__device__ void write_header(const PackArgs& A, uint64_t carry, int tid, int nthr);
+
+// Inline scan: the sum of the group sums before group g, and of all of them (every thread of the
+// workgroup takes part; the values fit 32 bits: <= 2048 groups of <= 64 * 11,136 words).
+__device__ __forceinline__ uint32_t group_prefix(const PackArgs& A, uint32_t g, uint32_t& total) {
+  __shared__ uint32_t s_p[kBlock / kWave], s_t[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  uint32_t p = 0u, t = 0u;
+  for (uint32_t i = threadIdx.x; i < A.n_groups; i += kBlock) {
+    const uint32_t v = A.gsum[i];
+    t += v;
+    p += i < g ? v : 0u;
+  }
+  p = wave_total_u32(p);
+  t = wave_total_u32(t);
+  if (lane == 0) {
+    s_p[w] = p;
+    s_t[w] = t;
+  }
+  __syncthreads();
+  p = (s_p[0] + s_p[1]) + (s_p[2] + s_p[3]);
+  total = (s_t[0] + s_t[1]) + (s_t[2] + s_t[3]);
+  __syncthreads();
+  return p;
+}
 
 __global__ __launch_bounds__(kScanThreads) void smaq_pack_scan_kernel(PackArgs A) {
   __shared__ uint64_t s_wave[kScanThreads / kWave];
@@ -467,6 +498,12 @@ __global__ __launch_bounds__(kScanThreads) void smaq_pack_scan_kernel(PackArgs A
     carry += total;
     __syncthreads();
   }
+  write_header(A, carry, tid, kScanThreads);
+}
+
+// The header, the directory's padding entry and the BN table (after the variable region of
+// `carry` words): thread 0 the header, all nthr threads the table.
+__device__ void write_header(const PackArgs& A, uint64_t carry, int tid, int nthr) {
   if (tid == 0) {
     SmqPackedHeader* h = A.hdr;
     const SmqSmaqStats* st = A.stats;
@@ -498,7 +535,7 @@ __global__ __launch_bounds__(kScanThreads) void smaq_pack_scan_kernel(PackArgs A
   }
   if (A.bn_gamma) {  // the BN table after the variable region (which the var kernel fills next)
     float* t = reinterpret_cast<float*>(A.var + carry);
-    for (int64_t i = tid; i < A.bn_channels; i += kScanThreads) {
+    for (int64_t i = tid; i < A.bn_channels; i += nthr) {
       t[i] = A.bn_gamma[i];
       t[A.bn_channels + i] = A.bn_beta[i];
     }
@@ -599,6 +636,12 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A, uint3
   const uint32_t g = blockIdx.x;
   const uint32_t b0 = g * kGroup;
   const uint32_t nb = min((uint32_t)kGroup, A.n_blocks - b0);
+  uint64_t ibase = 0;
+  if (A.inline_scan) {
+    uint32_t total;
+    ibase = group_prefix(A, g, total);
+    if (g == 0) write_header(A, total, tid, kBlock);
+  }
   if (tid < kWave) {
     uint32_t sz = 0u, t = 0u;
     bool rec = false;
@@ -610,7 +653,7 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A, uint3
     }
     const uint32_t incl = wave_incl_scan_u32(sz);
     const uint32_t ex = incl - sz;
-    const uint64_t base = A.gpre[g];
+    const uint64_t base = A.inline_scan ? ibase : A.gpre[g];
     s_off[lane] = ex;
     if (lane == kWave - 1) s_off[kGroup] = incl;
     if ((uint32_t)lane < nb)
@@ -681,6 +724,11 @@ __device__ void pack_recode_blocks(const PackArgs& A, uint32_t wg, uint32_t per,
   const uint32_t m = n_list;
   for (uint32_t i = 0; i < m; ++i) {
     const uint32_t b = list[i];
+    uint64_t gbase = 0;
+    if (A.inline_scan) {
+      uint32_t total;
+      gbase = group_prefix(A, b / kGroup, total);
+    }
     if (threadIdx.x < kWave) {
       const uint32_t g = b / kGroup, b0 = g * kGroup;
       uint32_t sz = 0u;
@@ -689,7 +737,7 @@ __device__ void pack_recode_blocks(const PackArgs& A, uint32_t wg, uint32_t per,
         sz = ext_words(we, t & 0xffffu) + 2u * (t >> 16);
       }
       const uint32_t before = wave_incl_scan_u32(sz);
-      if (lane == kWave - 1) s_dst = A.gpre[g] + before;
+      if (lane == kWave - 1) s_dst = (A.inline_scan ? gbase : A.gpre[g]) + before;
     }
     __syncthreads();
     recode_var_section<RM, TIN, EXT>(A, b, s_dst, lds, s_cnt);
@@ -718,7 +766,8 @@ void launch_pack_w(const PackArgs& A, bool vec, hipStream_t st) {
   if (A.n_full < A.n_blocks)
     hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, false, false, WM, WO, EXT>), dim3(1),
                        dim3(kBlock), lds, st, A);
-  hipLaunchKernelGGL(smaq_pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, A);
+  if (!A.inline_scan)
+    hipLaunchKernelGGL(smaq_pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, A);
   const int we = A.wo > A.wm ? A.wo - A.wm : 0;
   const uint32_t per = rare_per(A.n_blocks);
   hipLaunchKernelGGL((smaq_pack_var_kernel<RM, TIN, WM, WO, EXT>),
@@ -1346,9 +1395,11 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   }
   hipStream_t st = (hipStream_t)stream;
   // the statistics own the first region (sized for the multi-workgroup draw above 4096 samples)
-  rc = prepare_stats(x, dtype, n, p, ws, L.meta, st);
-  if (rc) return rc;
   char* wb = (char*)ws;
+  const uint32_t n_groups = (uint32_t)(((size_t)nb + kGroup - 1) / kGroup);
+  bool zeroed = false;  // the group sums start at zero: cleared by the statistics launch
+  rc = prepare_stats(x, dtype, n, p, ws, L.meta, st, (uint32_t*)(wb + L.gsum), n_groups, &zeroed);
+  if (rc) return rc;
   PackArgs A;
   memset(&A, 0, sizeof(A));
   A.x = x;
@@ -1367,7 +1418,8 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.gsum = (uint32_t*)(wb + L.gsum);
   A.gpre = (uint64_t*)(wb + L.gpre);
   A.scratch = (uint32_t*)(wb + L.scratch);
-  A.n_groups = (uint32_t)(((size_t)nb + kGroup - 1) / kGroup);
+  A.n_groups = n_groups;
+  A.inline_scan = n_groups <= kInlineScanGroups ? 1u : 0u;
   A.thr = p->main_std_dev_threshold;
   A.r_main = p->range_main;
   A.r_out = p->range_outlier;
@@ -1388,8 +1440,7 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.lds_words = PackLds::words(A.wm, we);
   const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
   const bool sr = p->stochastic_rounding != 0;
-  // the group sums start at zero (fill_async: smq_common.h)
-  fill_async(A.gsum, 0u, A.n_groups, st);
+  if (!zeroed) fill_async(A.gsum, 0u, A.n_groups, st);  // (sampled statistics: smq_common.h)
   if (dtype == SMQ_DTYPE_F32) {
     if (sr) launch_pack<kRoundHash, kF32>(A, vec, ext, st);
     else launch_pack<kRoundTrunc, kF32>(A, vec, ext, st);
