@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SMQ_ABI_VERSION 7
+#define SMQ_ABI_VERSION 8
 
 #define SMQ_OK 0
 #define SMQ_ERR_INVALID -1  /* bad argument */
@@ -488,6 +488,11 @@ int smq_half_quot_split(int dtype, float main_std_dev_threshold, float range_mai
  * SMQ_PACK_FLAG_BOTH_SIDES) adds a third state, z above T_m and below -T_m at once (smart.py:157-158
  * both true: scalars -T_m + T_m, range_outlier): such an element has mask bit 0 and codes as a main
  * element (wm-bit two's complement q) that the decoder de-quantises with both sides set.
+ * float64 streams (flag SMQ_PACK_FLAG_F64; smq_smaq_compress_f64): the codes of the fp64 chain
+ * (smart.py on a float64 tensor: z, q and the de-quantisation in fp64, scalars and ranges the fp32
+ * values), the same sections, with three words per escape {element index, q as float64 bits low
+ * word, high word} (any NaN q as 0x7ff8000000000000), the statistics as doubles (header
+ * mean_f64 / std_dev_f64) and a BN table of fp64 gammas then betas; decoded to float64.
  * ------------------------------------------------------------------------------------------- */
 #define SMQ_PACK_MAGIC 0x50514d53u /* "SMQP" */
 #define SMQ_PACK_VERSION 2u
@@ -511,13 +516,15 @@ typedef struct SmqPackedHeader {
   uint32_t error;             /* 0 (no packing launch waits on another workgroup) */
   uint32_t bn_channels;       /* BN streams: channels of the table (1: scalar parameters), else 0 */
   int64_t bn_inner;           /* BN streams: elements per channel run (H * W of NCHW), else 0 */
-  uint32_t reserved[6];
+  double mean_f64, std_dev_f64; /* float64 streams (SMQ_PACK_FLAG_F64): the statistics, else 0 */
+  uint32_t reserved[2];
 } SmqPackedHeader;
 
 #define SMQ_PACK_FLAG_ALL_POSITIVE 1u
 #define SMQ_PACK_FLAG_SAFE_Q 2u
 #define SMQ_PACK_FLAG_BOTH_SIDES 4u /* T_m < 0: a mask-0 element has both outlier sides */
 #define SMQ_PACK_FLAG_BN 8u         /* the BatchNorm table follows the variable region */
+#define SMQ_PACK_FLAG_F64 16u       /* float64 stream: 3-word escapes, fp64 statistics / BN table */
 
 /* Worst-case stream size (every element an outlier and escaped) for n elements; the stream's real
  * size is header.total_bytes. */
@@ -570,6 +577,29 @@ int smq_cpu_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqPara
                           void* packed, size_t packed_bytes, void* workspace,
                           size_t workspace_bytes, int n_threads);
 int smq_cpu_smaq_decompress(const void* packed, float* y, int64_t n, int n_threads);
+
+/* float64 tensors (smart.py:110-190 on a float64 tensor: the fp64 chain of smq_smaq_roundtrip_f64)
+ * in a float64 stream (flag SMQ_PACK_FLAG_F64): decompress_f64(compress_f64(x)) equals
+ * smq_smaq_roundtrip_f64(x) bit for bit for the same statistics and random stream. Statistics:
+ * params.stats_source SMQ_STATS_WORKSPACE, _SAMPLED or _SAMPLED_DEVICE (params' *_f64 fields set);
+ * rounding: hash or truncation; BN parameters (bn_gamma / bn_beta) as doubles. Not bandwidth-tuned:
+ * statistics, a counting launch (codes per block), a one-workgroup scan (directory, header) and a
+ * writing launch that recomputes the codes and stores both sections at their final places. */
+size_t smq_smaq_pack_bound_f64(int64_t n, int num_bits_main, int num_bits_outlier,
+                               int64_t bn_channels);
+size_t smq_smaq_pack_workspace_bytes_f64(int64_t n, int64_t num_samples);
+int smq_smaq_compress_f64(const double* x, int64_t n, const SmqSmaqParams* params, void* packed,
+                          size_t packed_bytes, void* workspace, size_t workspace_bytes,
+                          void* stream);
+/* The widths the stream was written with (a stream that is not a float64 stream of n elements and
+ * these widths is left undecoded: y unchanged). */
+int smq_smaq_decompress_f64(const void* packed, double* y, int64_t n, int num_bits_main,
+                            int num_bits_outlier, void* stream);
+/* Host twins (the same bytes as the device stream whenever the statistics agree). */
+int smq_cpu_smaq_compress_f64(const double* x, int64_t n, const SmqSmaqParams* params,
+                              void* packed, size_t packed_bytes, void* workspace,
+                              size_t workspace_bytes, int n_threads);
+int smq_cpu_smaq_decompress_f64(const void* packed, double* y, int64_t n, int n_threads);
 
 #ifdef __cplusplus
 }

@@ -219,6 +219,67 @@ def sampled_stats_f64(x: np.ndarray, idx: np.ndarray, cfg: SmaqConfig) -> Tuple[
     return mean, float(np.sqrt(float(np.dot(d, d)) / s.size))
 
 
+def codes_f64(x: np.ndarray, mean: float, std: float, cfg: SmaqConfig,
+              uniforms: Optional[np.ndarray] = None,
+              bn: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+    """smart.py:144-169 on float64 data: (q float64, hi, lo) — apply_f64's codes (the packed
+    container's input)."""
+    x = np.asarray(x, dtype=F64)
+    shape = x.shape
+    mean, std = F64(mean), F64(std)
+    thr = F64(cfg.main_std_dev_threshold)
+    sthr = F64(F32(cfg.main_std_dev_threshold))
+    r_out, r_main = F64(F32(cfg.range_outlier)), F64(F32(cfg.range_normal))
+    lo_c, hi_c = (F64(v) for v in cfg.clamped_range)
+    data = x
+    if bn is not None:
+        g, b = [np.asarray(t, dtype=F64).reshape((1, -1, 1, 1)) for t in bn]
+        data = (data - b) / g
+    if std == F64(0):
+        std = F64(1)
+    sc = std
+    if sc < lo_c:
+        sc = lo_c
+    if sc > hi_c:
+        sc = hi_c
+    with np.errstate(all="ignore"):
+        z = (data - mean) / sc
+        hi = z > thr
+        lo = z < -thr
+        scal = (np.where(hi, -sthr, F64(F32(0) * -F32(cfg.main_std_dev_threshold)))
+                + np.where(lo, sthr, F64(F32(0) * F32(cfg.main_std_dev_threshold))))
+        ranges = np.where(hi | lo, r_out, r_main)
+        d = (z + scal) * ranges
+        if cfg.stochastic_rounding:
+            u = np.asarray(uniforms, dtype=F64).reshape(shape)
+            f = np.floor(d)
+            t = (d - f) - u
+            t = t + F64(0.5)
+            t = np.where(t < F64(0), F64(0), t)
+            q = f + np.rint(t)
+        else:
+            q = np.trunc(d)
+    return q.reshape(shape), hi.reshape(shape), lo.reshape(shape)
+
+
+def dequant_f64(q, hi, lo, mean: float, std_dev: float, thr32: float, r_main32: float,
+                r_out32: float, all_positive: bool = False, bn=None, channel=None):
+    """smart.py:171-182 on float64 codes: (q / ranges) - scalars, * std + mean (std after the ==0
+    rule), then * gamma + beta per channel, clamp_min(0)."""
+    sthr = F64(F32(thr32))
+    ranges = np.where(hi | lo, F64(F32(r_out32)), F64(F32(r_main32)))
+    scal = (np.where(hi, -sthr, F64(F32(0) * -F32(thr32)))
+            + np.where(lo, sthr, F64(F32(0) * F32(thr32))))
+    with np.errstate(all="ignore"):
+        y = (np.asarray(q, F64) / ranges) - scal
+        y = (y * F64(std_dev)) + F64(mean)
+        if bn is not None:
+            y = (y * bn[0][channel]) + bn[1][channel]
+        if all_positive:
+            y = np.where(y < F64(0), F64(0), y)
+    return y
+
+
 def apply_f64(x: np.ndarray, mean: float, std: float, cfg: SmaqConfig,
               uniforms: Optional[np.ndarray] = None, all_positive: bool = False,
               bn: Optional[Tuple[np.ndarray, np.ndarray]] = None):

@@ -23,9 +23,11 @@ VERSION = 2
 BLOCK = 4096
 HEADER_BYTES = 128
 MASK_WORDS = BLOCK // 32
-_HDR = struct.Struct("<IIqIIiiIfffffddQQIIq24x")
+_HDR = struct.Struct("<IIqIIiiIfffffddQQIIqdd8x")
 FLAG_BOTH_SIDES = 4
 FLAG_BN = 8
+FLAG_F64 = 16
+NAN64 = 0x7FF8000000000000
 assert _HDR.size == HEADER_BYTES
 
 
@@ -163,7 +165,7 @@ def pack(x, mean, std, cfg: osmaq.SmaqConfig, uniforms: Optional[np.ndarray] = N
                     thr, r_main, r_out, F32(mean), F32(std1),
                     1.0 / float(r_main) if r_main != 0 else float("inf"),
                     1.0 / float(r_out) if r_out != 0 else float("inf"),
-                    var_w.size, total, 0, bn_tab.size // 2, inner)
+                    var_w.size, total, 0, bn_tab.size // 2, inner, 0.0, 0.0)
     dirs += [0] * (nbp - nb)
     return np.concatenate([np.frombuffer(hdr, np.uint8), np.asarray(dirs, np.uint64).view(np.uint8),
                            fixed_w.view(np.uint8), var_w.view(np.uint8), bn_tab.view(np.uint8)])
@@ -174,7 +176,7 @@ def header(stream: np.ndarray) -> dict:
     keys = ("magic", "version", "n", "block_elems", "n_blocks", "num_bits_main",
             "num_bits_outlier", "flags", "thr", "range_main", "range_outlier", "mean", "std_dev",
             "inv_range_main", "inv_range_outlier", "data_words", "total_bytes", "error",
-            "bn_channels", "bn_inner")
+            "bn_channels", "bn_inner", "mean_f64", "std_dev_f64")
     return dict(zip(keys, f))
 
 
@@ -204,15 +206,78 @@ def bn_table(stream: np.ndarray):
     return t[:c], t[c:]
 
 
+def block_var_f64(cb, ob, eb, qb, wm: int, wo: int) -> np.ndarray:
+    """A float64 stream's variable section: the outlier bits above the plane, then the escapes
+    {element index, q as float64 bits low word, high word} (any NaN q as 0x7ff8000000000000)."""
+    we = max(0, wo - wm)
+    ext = _pack_bits(cb[ob] >> np.uint64(wm), we)
+    esc_idx = np.nonzero(eb)[0].astype(np.uint32)
+    qe = np.asarray(qb, np.float64)[esc_idx]
+    qbits = np.where(np.isnan(qe), np.uint64(NAN64), qe.view(np.uint64))
+    esc = np.stack([esc_idx, (qbits & np.uint64(0xFFFFFFFF)).astype(np.uint32),
+                    (qbits >> np.uint64(32)).astype(np.uint32)], axis=1).ravel()
+    return np.concatenate([ext, esc.astype(np.uint32)])
+
+
+def pack_f64(x, mean, std, cfg: osmaq.SmaqConfig, uniforms: Optional[np.ndarray] = None,
+             all_positive: bool = False, bn=None) -> np.ndarray:
+    """The float64 stream smq_smaq_compress_f64 writes (flag FLAG_F64), given the device's fp64
+    statistics (mean, raw std) and the same uniforms: the codes of osmaq.codes_f64 (smart.py on a
+    float64 tensor), 3-word escapes, the statistics (std after the ==0 rule) as doubles, an fp64
+    BN table."""
+    x = np.asarray(x, dtype=np.float64)
+    inner = 0
+    if bn is not None:
+        assert x.ndim == 4
+        inner = x.shape[2] * x.shape[3]
+        bn = tuple(np.asarray(t, np.float64).reshape(-1) for t in bn)
+    q, hi, lo = osmaq.codes_f64(x, mean, std, cfg, uniforms, bn)
+    q, hi, lo = q.ravel(), hi.ravel(), lo.ravel()
+    n = x.size
+    bm, bo = cfg.num_bits_main, cfg.num_bits_outlier
+    wm, wo = _widths(bm, bo)
+    code, o, esc = block_codes(q, hi, lo, wm, wo)
+    nb = (n + BLOCK - 1) // BLOCK
+    fixed, var, dirs, off = [], [], [], 0
+    for b in range(nb):
+        s = slice(b * BLOCK, min(n, (b + 1) * BLOCK))
+        fixed.append(block_fixed(code[s], o[s], wm))
+        v = block_var_f64(code[s], o[s], esc[s], q[s], wm, wo)
+        dirs.append(off | (int(o[s].sum()) << 38) | (int(esc[s].sum()) << 51))
+        off += v.size
+        var.append(v)
+    fixed_w = np.concatenate(fixed) if fixed else np.zeros(0, np.uint32)
+    var_w = np.concatenate(var) if var else np.zeros(0, np.uint32)
+    r_main, r_out = F32(cfg.range_normal), F32(cfg.range_outlier)
+    nbp = nb + (nb & 1)
+    bn_tab = (np.concatenate([bn[0], bn[1]]).astype(np.float64) if bn is not None
+              else np.zeros(0, np.float64))
+    total = HEADER_BYTES + 8 * nbp + 4 * (fixed_w.size + var_w.size) + 8 * bn_tab.size
+    thr = F32(cfg.main_std_dev_threshold)
+    std1 = np.float64(std) if np.float64(std) != 0 else np.float64(1.0)
+    hdr = _HDR.pack(MAGIC, VERSION, n, BLOCK, nb, bm, bo,
+                    FLAG_F64 | _flags(all_positive, r_main, r_out, thr, bn is not None),
+                    thr, r_main, r_out, F32(mean), F32(std1),
+                    1.0 / float(r_main) if r_main != 0 else float("inf"),
+                    1.0 / float(r_out) if r_out != 0 else float("inf"),
+                    var_w.size, total, 0, bn_tab.size // 2, inner, float(mean), float(std1))
+    dirs += [0] * (nbp - nb)
+    return np.concatenate([np.frombuffer(hdr, np.uint8), np.asarray(dirs, np.uint64).view(np.uint8),
+                           fixed_w.view(np.uint8), var_w.view(np.uint8), bn_tab.view(np.uint8)])
+
+
 def unpack(stream: np.ndarray) -> np.ndarray:
-    """Decode a stream (smq_smaq_decompress): fp32 values in element order."""
+    """Decode a stream (smq_smaq_decompress[_f64]): fp32 values in element order (float64 for a
+    float64 stream)."""
     h, dirs, fixed_w, var_w = regions(stream)
     assert h["magic"] == MAGIC and h["version"] == VERSION
+    f64 = bool(h["flags"] & FLAG_F64)
+    ew = 3 if f64 else 2
     n, nb = h["n"], h["n_blocks"]
     wm, wo = _widths(h["num_bits_main"], h["num_bits_outlier"])
     we = max(0, wo - wm)
     F = fixed_words(wm)
-    q = np.zeros(n, F32)
+    q = np.zeros(n, np.float64 if f64 else F32)
     hi = np.zeros(n, bool)
     lo = np.zeros(n, bool)
     for b in range(nb):
@@ -233,14 +298,30 @@ def unpack(stream: np.ndarray) -> np.ndarray:
         side = (cd >> (wo - 1)) & 1
         mag = cd & ((1 << (wo - 1)) - 1)
         qo = np.where(side == 1, -mag, mag)
-        qb = np.where(ob, qo, qm).astype(F32)
+        qb = np.where(ob, qo, qm).astype(np.float64 if f64 else F32)
         both = bool(h["flags"] & FLAG_BOTH_SIDES)  # a mask-0 element has both sides
         hb = np.where(ob, side == 0, both)
         lb = np.where(ob, side == 1, both)
-        e = var_w[base + n_ext: base + n_ext + 2 * n_esc].reshape(-1, 2)
-        qb[e[:, 0].astype(np.int64)] = e[:, 1].view(F32)
+        e = var_w[base + n_ext: base + n_ext + ew * n_esc].reshape(-1, ew)
+        if f64:
+            qb[e[:, 0].astype(np.int64)] = (e[:, 1].astype(np.uint64)
+                                            | (e[:, 2].astype(np.uint64) << np.uint64(32))
+                                            ).view(np.float64)
+        else:
+            qb[e[:, 0].astype(np.int64)] = e[:, 1].view(F32)
         s = slice(b * BLOCK, b * BLOCK + m)
         q[s], hi[s], lo[s] = qb, hb, lb
+    if f64:
+        bn, ch = None, None
+        if h["flags"] & FLAG_BN:
+            nbp = nb + (nb & 1)
+            off = (HEADER_BYTES + 8 * nbp + 4 * nb * fixed_words(wm) + 4 * h["data_words"])
+            c = h["bn_channels"]
+            t = np.asarray(stream[off: off + 16 * c], np.uint8).view(np.float64)
+            bn = (t[:c], t[c:])
+            ch = (np.arange(n, dtype=np.int64) // h["bn_inner"]) % c
+        return osmaq.dequant_f64(q, hi, lo, h["mean_f64"], h["std_dev_f64"], h["thr"],
+                                 h["range_main"], h["range_outlier"], bool(h["flags"] & 1), bn, ch)
     cfg = osmaq.SmaqConfig(num_bits_main=h["num_bits_main"], num_bits_outlier=h["num_bits_outlier"],
                            main_std_dev_threshold=float(F32(h["thr"])))
     # the ranges come from the header (the compressor's fp32 constants)

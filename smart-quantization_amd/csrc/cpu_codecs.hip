@@ -960,9 +960,11 @@ static void s2_pass(const void* x, void* y, int64_t n, bool p16, bool hout, int 
 
 
 // ---- fp64 tensors (smaq_f64.h holds the shared finaliser and element transforms) -----------------
-static int smaq_roundtrip_f64(const double* x, double* y, int64_t n, const SmqSmaqParams* p,
-                              const double* uniforms, const SmqSmaqStatsF64* stats_in, char* ws,
-                              size_t ws_bytes, int n_threads) {
+// The statistics of an fp64 call (full / sampled / injected) and the stream position it takes
+// (*base; params.offset_counter advanced by n).
+static int stats_f64(const double* x, int64_t n, const SmqSmaqParams* p,
+                     const SmqSmaqStatsF64* stats_in, char* ws, size_t ws_bytes, int n_threads,
+                     SmqSmaqStatsF64* out, uint64_t* base_out) {
   SmqSmaqStatsF64 st;
   memset(&st, 0, sizeof(st));
   const uint64_t base = p->offset_counter ? *p->offset_counter : 0ull;
@@ -1059,6 +1061,18 @@ static int smaq_roundtrip_f64(const double* x, double* y, int64_t n, const SmqSm
   }
   if (p->offset_counter) *p->offset_counter = base + (uint64_t)n;
   st.rng_offset = base;
+  *out = st;
+  *base_out = base;
+  return SMQ_OK;
+}
+
+static int smaq_roundtrip_f64(const double* x, double* y, int64_t n, const SmqSmaqParams* p,
+                              const double* uniforms, const SmqSmaqStatsF64* stats_in, char* ws,
+                              size_t ws_bytes, int n_threads) {
+  SmqSmaqStatsF64 st;
+  uint64_t base = 0;
+  const int rc = stats_f64(x, n, p, stats_in, ws, ws_bytes, n_threads, &st, &base);
+  if (rc) return rc;
   const ElemF64 c = elem_f64_consts(st, *p);
   const uint32_t key = rng_key(p->seed);
   const uint64_t off = p->offset + base;
@@ -1134,6 +1148,259 @@ static void s2_stats_f64(const double* x, int64_t n, int n_threads, SmqS2fp8Stat
   }
   s2_derive_f64(s, m, n, o);
 }
+// ---- float64 streams (flag SMQ_PACK_FLAG_F64; smaq_pack_f64.hip is the device twin) -------------
+// The fp64 chain's codes (smaq_quant_f64) in the version-2 sections, escapes {element, q low word,
+// q high word}, the statistics as doubles in the header, an fp64 BN table.
+static inline uint32_t code_f64(double q, bool o, bool los, int wm, int wo, bool& esc) {
+  const double hm = (double)(1u << (wm - 1)), mag_max = (double)((1u << (wo - 1)) - 1u);
+  bool ok;
+  if (o) ok = los ? (q <= 0.0 && -q <= mag_max) : (q >= 0.0 && q <= mag_max);
+  else ok = q >= -hm && q <= hm - 1.0;
+  esc = !ok;
+  const int64_t qi = ok ? (int64_t)q : 0;
+  if (o) {
+    const uint32_t side = (uint32_t)los << (wo - 1);
+    return ok ? (side | (uint32_t)(los ? -qi : qi)) : side;
+  }
+  return ok ? ((uint32_t)qi & ((1u << wm) - 1u)) : 0u;
+}
+
+struct PackF64Ctx {
+  const double* x;
+  const double* gam;
+  const double* bet;
+  int64_t channels, inner, n;
+  ElemF64 c;
+  uint32_t key;
+  uint64_t off;
+  int wm, wo, we;
+};
+
+template <int RM, bool BN>
+static void pack_block_host_f64(const PackF64Ctx& P, int64_t b, uint32_t* fx,
+                                std::vector<uint32_t>& var, uint32_t* n_out, uint32_t* n_esc) {
+  const int wm = P.wm, wo = P.wo, we = P.we;
+  const int64_t e0 = b * kPB, m = std::min<int64_t>(kPB, P.n - e0);
+  memset(fx, 0, 4 * pk_fixed_words(wm));
+  uint32_t* plane = fx + 128;
+  const uint32_t wmask = (uint32_t)((1ull << wm) - 1ull);
+  std::vector<uint32_t> ext, esc;
+  uint32_t no = 0;
+  for (int64_t e = 0; e < m; ++e) {
+    const int64_t i = e0 + e;
+    const double u = RM == kRoundHash ? (double)smaq_u24(P.key, P.off + (uint64_t)i) : 0.0;
+    double g = 1.0, bb = 0.0;
+    if (BN) {
+      const int64_t ch = (i / P.inner) % P.channels;
+      g = P.gam[ch];
+      bb = P.bet[ch];
+    }
+    bool hi, lo, es;
+    const double q = smaq_quant_f64<RM, BN>(P.x[i], u, P.c, hi, lo, g, bb);
+    const bool o = hi != lo, los = lo && !hi;
+    const uint32_t code = code_f64(q, o, los, wm, wo, es);
+    if (o) {
+      fx[e >> 5] |= 1u << (e & 31);
+      ++no;
+      if (we > 0) ext.push_back(code >> wm);
+    }
+    put_bits(plane, (uint64_t)e * (uint64_t)wm, code & wmask, wm);
+    if (es) {
+      const uint64_t qb = q != q ? 0x7ff8000000000000ull : __builtin_bit_cast(uint64_t, q);
+      esc.push_back((uint32_t)e);
+      esc.push_back((uint32_t)qb);
+      esc.push_back((uint32_t)(qb >> 32));
+    }
+  }
+  *n_out = no;
+  *n_esc = (uint32_t)(esc.size() / 3);
+  const size_t ext_w = ((size_t)we * ext.size() + 31) / 32;
+  const size_t at = var.size();
+  var.resize(at + ext_w, 0u);
+  for (size_t k = 0; k < ext.size(); ++k) put_bits(var.data() + at, (uint64_t)k * we, ext[k], we);
+  var.insert(var.end(), esc.begin(), esc.end());
+}
+
+static int pack_host_f64(const double* x, int64_t n, const SmqSmaqParams* p, uint8_t* out,
+                         size_t out_bytes, char* ws, size_t ws_bytes, int n_threads) {
+  SmqSmaqStatsF64 st;
+  uint64_t base = 0;
+  const int rc = stats_f64(x, n, p, nullptr, ws, ws_bytes, n_threads, &st, &base);
+  if (rc) return rc;
+  memcpy(ws, &st, sizeof(st));  // the header the device packer leaves in its workspace
+  PackF64Ctx P;
+  P.x = x;
+  P.gam = reinterpret_cast<const double*>(p->bn_gamma);
+  P.bet = reinterpret_cast<const double*>(p->bn_beta);
+  P.channels = p->bn_channels;
+  P.inner = p->bn_inner;
+  P.n = n;
+  P.c = elem_f64_consts(st, *p);
+  P.key = rng_key(p->seed);
+  P.off = p->offset + base;
+  P.wm = p->num_bits_main - 1;
+  P.wo = p->num_bits_outlier - 1;
+  P.we = P.wo > P.wm ? P.wo - P.wm : 0;
+  const bool bn = p->bn_gamma != nullptr, sr = p->stochastic_rounding != 0;
+  const int64_t nb = (n + kPB - 1) / kPB;
+  const size_t fk = pk_fixed_words(P.wm);
+  uint64_t* dir = reinterpret_cast<uint64_t*>(out + sizeof(SmqPackedHeader));
+  uint32_t* fixed = reinterpret_cast<uint32_t*>(dir + pk_dir_entries(nb));
+  std::vector<std::vector<uint32_t>> var((size_t)nb);
+  std::vector<uint32_t> nout((size_t)nb), nesc((size_t)nb);
+  const int64_t tasks = (nb + kPackTaskBlocks - 1) / kPackTaskBlocks;
+  const std::function<void(int64_t)> fn = [&](int64_t t) {
+    const int64_t b1 = std::min(nb, (t + 1) * kPackTaskBlocks);
+    for (int64_t b = t * kPackTaskBlocks; b < b1; ++b) {
+      uint32_t* fx = fixed + (size_t)b * fk;
+      auto& v = var[(size_t)b];
+      if (sr) {
+        if (bn) pack_block_host_f64<kRoundHash, true>(P, b, fx, v, &nout[b], &nesc[b]);
+        else pack_block_host_f64<kRoundHash, false>(P, b, fx, v, &nout[b], &nesc[b]);
+      } else {
+        if (bn) pack_block_host_f64<kRoundTrunc, true>(P, b, fx, v, &nout[b], &nesc[b]);
+        else pack_block_host_f64<kRoundTrunc, false>(P, b, fx, v, &nout[b], &nesc[b]);
+      }
+    }
+  };
+  pool().run(tasks, threads_for(n_threads), fn);
+  uint64_t off = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    dir[b] = off | ((uint64_t)nout[b] << 38) | ((uint64_t)nesc[b] << 51);
+    off += var[(size_t)b].size();
+  }
+  if (nb & 1) dir[nb] = 0;
+  uint32_t* vr = fixed + (size_t)nb * fk;
+  const size_t bn_words = bn ? 4 * (size_t)p->bn_channels : 0;
+  const size_t total = sizeof(SmqPackedHeader) + 8 * (size_t)pk_dir_entries(nb) +
+                       4 * ((size_t)nb * fk + off + bn_words);
+  if (total > out_bytes) {
+    set_error("cpu compress_f64: stream of %zu bytes exceeds the buffer (%zu)", total, out_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  uint64_t at = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    const auto& v = var[(size_t)b];
+    if (!v.empty()) memcpy(vr + at, v.data(), 4 * v.size());
+    at += v.size();
+  }
+  if (bn) {
+    double* tab = reinterpret_cast<double*>(vr + off);
+    memcpy(tab, p->bn_gamma, 8 * (size_t)p->bn_channels);
+    memcpy(tab + p->bn_channels, p->bn_beta, 8 * (size_t)p->bn_channels);
+  }
+  const RangeRecips R = range_recips(p->range_main, p->range_outlier);
+  SmqPackedHeader h;
+  memset(&h, 0, sizeof(h));
+  h.magic = SMQ_PACK_MAGIC;
+  h.version = SMQ_PACK_VERSION;
+  h.n = n;
+  h.block_elems = kPB;
+  h.n_blocks = (uint32_t)nb;
+  h.num_bits_main = p->num_bits_main;
+  h.num_bits_outlier = p->num_bits_outlier;
+  h.flags = SMQ_PACK_FLAG_F64 | (p->all_positive ? SMQ_PACK_FLAG_ALL_POSITIVE : 0u) |
+            (R.safe_q ? SMQ_PACK_FLAG_SAFE_Q : 0u) |
+            (p->main_std_dev_threshold < 0.0f ? SMQ_PACK_FLAG_BOTH_SIDES : 0u) |
+            (bn ? SMQ_PACK_FLAG_BN : 0u);
+  h.thr = p->main_std_dev_threshold;
+  h.range_main = p->range_main;
+  h.range_outlier = p->range_outlier;
+  h.mean = (float)st.mean;
+  h.std_dev = (float)st.std_dev;
+  h.inv_range_main = 1.0 / (double)p->range_main;
+  h.inv_range_outlier = 1.0 / (double)p->range_outlier;
+  h.data_words = off;
+  h.total_bytes = total;
+  h.bn_channels = bn ? (uint32_t)p->bn_channels : 0u;
+  h.bn_inner = bn ? p->bn_inner : 0;
+  h.mean_f64 = st.mean;
+  h.std_dev_f64 = st.std_dev;
+  memcpy(out, &h, sizeof(h));
+  return SMQ_OK;
+}
+
+static int unpack_host_f64(const uint8_t* in, double* y, int64_t n, int n_threads) {
+  SmqPackedHeader h;
+  memcpy(&h, in, sizeof(h));
+  if (h.magic != SMQ_PACK_MAGIC || h.version != SMQ_PACK_VERSION || h.n != n ||
+      h.block_elems != (uint32_t)kPB || h.n_blocks != (uint32_t)((n + kPB - 1) / kPB) ||
+      !(h.flags & SMQ_PACK_FLAG_F64) || h.num_bits_main < 2 || h.num_bits_main > 25 ||
+      h.num_bits_outlier < 3 || h.num_bits_outlier > 25) {
+    set_error("cpu decompress_f64: not a version-%u float64 stream of %lld elements",
+              SMQ_PACK_VERSION, (long long)n);
+    return SMQ_ERR_INVALID;
+  }
+  const int wm = h.num_bits_main - 1, wo = h.num_bits_outlier - 1, we = wo > wm ? wo - wm : 0;
+  const int64_t nb = h.n_blocks;
+  const size_t fk = pk_fixed_words(wm);
+  const uint64_t* dir = reinterpret_cast<const uint64_t*>(in + sizeof(SmqPackedHeader));
+  const uint32_t* fixed = reinterpret_cast<const uint32_t*>(dir + pk_dir_entries(nb));
+  const uint32_t* vr = fixed + (size_t)nb * fk;
+  const bool bn = (h.flags & SMQ_PACK_FLAG_BN) != 0, ap = (h.flags & 1u) != 0;
+  const bool both = (h.flags & SMQ_PACK_FLAG_BOTH_SIDES) != 0;
+  const double* g = bn ? reinterpret_cast<const double*>(vr + h.data_words) : nullptr;
+  const double* bb = bn ? g + h.bn_channels : nullptr;
+  ElemF64 c;
+  memset(&c, 0, sizeof(c));
+  c.mean = h.mean_f64;
+  c.sd = h.std_dev_f64;
+  c.sthr = (double)h.thr;
+  c.snthr = -c.sthr;
+  c.zh = (double)(0.0f * -h.thr);
+  c.zl = (double)(0.0f * h.thr);
+  c.r_main = (double)h.range_main;
+  c.r_out = (double)h.range_outlier;
+  const int64_t tasks = (nb + kPackTaskBlocks - 1) / kPackTaskBlocks;
+  const std::function<void(int64_t)> fn = [&](int64_t t) {
+    std::vector<double> qb(kPB);
+    std::vector<uint8_t> sides(kPB);  // bit 0: hi, bit 1: lo
+    const uint8_t both2 = both ? 3 : 0;
+    const int64_t b1 = std::min(nb, (t + 1) * kPackTaskBlocks);
+    for (int64_t b = t * kPackTaskBlocks; b < b1; ++b) {
+      const int64_t e0 = b * kPB, m = std::min<int64_t>(kPB, n - e0);
+      const uint64_t d = dir[b];
+      const uint64_t vbase = d & ((1ull << 38) - 1ull);
+      const uint32_t n_out = (uint32_t)((d >> 38) & 0x1fffu), n_esc = (uint32_t)(d >> 51);
+      const uint32_t* fx = fixed + (size_t)b * fk;
+      const uint32_t* ext = vr + vbase;
+      const uint32_t* esc = ext + ((size_t)we * n_out + 31) / 32;
+      uint32_t rank = 0;
+      for (int64_t e = 0; e < m; ++e) {
+        uint32_t code = get_bits(fx + 128, (uint64_t)e * wm, wm);
+        if ((fx[e >> 5] >> (e & 31)) & 1u) {
+          if (we > 0) code |= get_bits(ext, (uint64_t)rank * we, we) << wm;
+          ++rank;
+          const uint32_t side = (code >> (wo - 1)) & 1u;
+          const double mag = (double)(code & ((1u << (wo - 1)) - 1u));
+          qb[(size_t)e] = side ? -mag : mag;
+          sides[(size_t)e] = side ? 2 : 1;
+        } else {
+          qb[(size_t)e] = (double)((code >= (1u << (wm - 1))) ? (int32_t)code - (1 << wm)
+                                                              : (int32_t)code);
+          sides[(size_t)e] = both2;
+        }
+      }
+      for (uint32_t k = 0; k < n_esc; ++k)
+        if (esc[3 * k] < (uint32_t)m)
+          qb[esc[3 * k]] = __builtin_bit_cast(double, (uint64_t)esc[3 * k + 1] |
+                                                          ((uint64_t)esc[3 * k + 2] << 32));
+      for (int64_t e = 0; e < m; ++e) {
+        const bool hi = sides[(size_t)e] & 1, lo = sides[(size_t)e] & 2;
+        double out = smaq_dequant_f64<false, false>(qb[(size_t)e], hi, lo, c, 1.0, 0.0);
+        if (bn) {
+          const int64_t ch = ((e0 + e) / h.bn_inner) % (int64_t)h.bn_channels;
+          out = (out * g[ch]) + bb[ch];
+        }
+        if (ap) out = (out < 0.0) ? 0.0 : out;
+        y[e0 + e] = out;
+      }
+    }
+  };
+  pool().run(tasks, threads_for(n_threads), fn);
+  return SMQ_OK;
+}
+
 }  // namespace cpu
 }  // namespace smq
 
@@ -1214,6 +1481,57 @@ int smq_cpu_smaq_decompress(const void* packed, float* y, int64_t n, int n_threa
     return SMQ_ERR_INVALID;
   }
   return cpu::unpack_host(static_cast<const uint8_t*>(packed), y, n, n_threads);
+}
+
+int smq_cpu_smaq_compress_f64(const double* x, int64_t n, const SmqSmaqParams* p, void* packed,
+                              size_t packed_bytes, void* ws, size_t ws_bytes, int n_threads) {
+  int rc = smaq_validate(p, SMQ_DTYPE_F32);
+  if (rc) return rc;
+  if (n < 1 || !x || !packed) {
+    set_error("cpu compress_f64: n must be >= 1, x and packed non-NULL");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->num_bits_main < 2 || p->num_bits_main > 25 || p->num_bits_outlier < 3 ||
+      p->num_bits_outlier > 25) {
+    set_error("cpu compress_f64: needs 2 <= num_bits_main <= 25 and 3 <= num_bits_outlier <= 25");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->main_std_dev_threshold_f64 == 0.0 || !(p->clamp_hi_f64 > 0.0)) {
+    set_error("cpu compress_f64: params.main_std_dev_threshold_f64 / clamp_*_f64 unset");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->bn_gamma && (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1)) {
+    set_error("cpu compress_f64: batch-norm parameters incomplete");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->stats_source == SMQ_STATS_INJECTED) {
+    set_error("cpu compress_f64: computes its statistics (SMQ_STATS_WORKSPACE or _SAMPLED*)");
+    return SMQ_ERR_INVALID;
+  }
+  const size_t bound = smq_smaq_pack_bound_f64(n, p->num_bits_main, p->num_bits_outlier,
+                                               p->bn_gamma ? p->bn_channels : 0);
+  if (packed_bytes < bound) {
+    set_error("cpu compress_f64: packed buffer too small: need %zu bytes, got %zu", bound,
+              packed_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  const int64_t k = p->stats_source == SMQ_STATS_SAMPLED_DEVICE
+                        ? std::min<int64_t>(p->num_samples, n) : 0;
+  const size_t need = k > 0 ? smq_smaq_workspace_bytes_sampled(n, k) : smq_smaq_workspace_bytes(n);
+  if (!ws || ws_bytes < need) {
+    set_error("cpu compress_f64: workspace too small: need %zu bytes, got %zu", need, ws_bytes);
+    return SMQ_ERR_WORKSPACE;
+  }
+  return cpu::pack_host_f64(x, n, p, static_cast<uint8_t*>(packed), packed_bytes,
+                            static_cast<char*>(ws), ws_bytes, n_threads);
+}
+
+int smq_cpu_smaq_decompress_f64(const void* packed, double* y, int64_t n, int n_threads) {
+  if (n < 1 || !packed || !y) {
+    set_error("cpu decompress_f64: n must be >= 1, packed and y non-NULL");
+    return SMQ_ERR_INVALID;
+  }
+  return cpu::unpack_host_f64(static_cast<const uint8_t*>(packed), y, n, n_threads);
 }
 
 int smq_cpu_float_quant(const void* x, int dtype_in, void* y, int dtype_out, int64_t n,

@@ -272,33 +272,14 @@ __global__ __launch_bounds__(kBlock) void smaq_f64_apply_kernel(ApplyF64Args A) 
   }
 }
 
-static int smaq_f64_impl(const double* x, double* y, int64_t n, const SmqSmaqParams* p,
-                         const double* uniforms, const SmqSmaqStatsF64* stats_in, void* ws,
-                         size_t ws_bytes, hipStream_t st) {
-  int rc = smaq_validate(p, SMQ_DTYPE_F32);
-  if (rc) return rc;
-  if (n < 1 || !x || !y) {
-    set_error("smaq f64: n >= 1 and non-NULL x, y required");
-    return SMQ_ERR_INVALID;
-  }
-  if (p->main_std_dev_threshold_f64 == 0.0 || !(p->clamp_hi_f64 > 0.0)) {
-    set_error("smaq f64: params.main_std_dev_threshold_f64 / clamp_*_f64 unset "
-              "(smq_smaq_params_set fills them)");
-    return SMQ_ERR_INVALID;
-  }
-  if (p->bn_gamma && (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1)) {
-    set_error("smaq f64: batch-norm parameters incomplete");
-    return SMQ_ERR_INVALID;
-  }
-  if (!ws || ws_bytes < smq_smaq_workspace_bytes(n)) {
-    set_error("smaq f64: workspace too small: need %zu bytes", smq_smaq_workspace_bytes(n));
-    return SMQ_ERR_WORKSPACE;
-  }
-  const int64_t tiles = (n + kBlock * kF64Per - 1) / (kBlock * kF64Per);
-  if (tiles > 0x7fffffffLL) {
-    set_error("smaq f64: tensor too large");
-    return SMQ_ERR_INVALID;
-  }
+}  // namespace smq
+
+// The statistics of an fp64 call into the workspace header (SmqSmaqStatsF64 at offset 0): full,
+// sampled (host-given or device-drawn, any k) or injected (smaq_host.h; the packed codec's too).
+int smq::launch_stats_f64(const double* x, int64_t n, const SmqSmaqParams* p,
+                          const SmqSmaqStatsF64* stats_in, void* ws, size_t ws_bytes,
+                          hipStream_t st) {
+  int rc = SMQ_OK;
   char* wb = (char*)ws;
   StatsF64Args S;
   memset(&S, 0, sizeof(S));
@@ -375,13 +356,48 @@ static int smaq_f64_impl(const double* x, double* y, int64_t n, const SmqSmaqPar
       hipLaunchKernelGGL(smaq_f64_inject_kernel, dim3(1), dim3(kWave), 0, st, stats_in, S);
     }
   }
+  return check_launch("smaq_f64 statistics");
+}
+
+namespace smq {
+
+static int smaq_f64_impl(const double* x, double* y, int64_t n, const SmqSmaqParams* p,
+                         const double* uniforms, const SmqSmaqStatsF64* stats_in, void* ws,
+                         size_t ws_bytes, hipStream_t st) {
+  int rc = smaq_validate(p, SMQ_DTYPE_F32);
+  if (rc) return rc;
+  if (n < 1 || !x || !y) {
+    set_error("smaq f64: n >= 1 and non-NULL x, y required");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->main_std_dev_threshold_f64 == 0.0 || !(p->clamp_hi_f64 > 0.0)) {
+    set_error("smaq f64: params.main_std_dev_threshold_f64 / clamp_*_f64 unset "
+              "(smq_smaq_params_set fills them)");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->bn_gamma && (!p->bn_beta || p->bn_channels < 1 || p->bn_inner < 1)) {
+    set_error("smaq f64: batch-norm parameters incomplete");
+    return SMQ_ERR_INVALID;
+  }
+  if (!ws || ws_bytes < smq_smaq_workspace_bytes(n)) {
+    set_error("smaq f64: workspace too small: need %zu bytes", smq_smaq_workspace_bytes(n));
+    return SMQ_ERR_WORKSPACE;
+  }
+  const int64_t tiles = (n + kBlock * kF64Per - 1) / (kBlock * kF64Per);
+  if (tiles > 0x7fffffffLL) {
+    set_error("smaq f64: tensor too large");
+    return SMQ_ERR_INVALID;
+  }
+  rc = launch_stats_f64(x, n, p, stats_in, ws, ws_bytes, st);
+  if (rc) return rc;
+  char* wb = (char*)ws;
   ApplyF64Args A;
   memset(&A, 0, sizeof(A));
   A.x = x;
   A.y = y;
   A.n = n;
   A.uniforms = uniforms;
-  A.hdr = S.hdr;
+  A.hdr = (const SmqSmaqStatsF64*)wb;
   A.out_slots = (unsigned long long*)(wb + SmaqWsLayout::kSlots);
   A.p = *p;
   A.key = rng_key(p->seed);

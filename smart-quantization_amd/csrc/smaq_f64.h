@@ -71,32 +71,46 @@ struct ElemF64 {
   double r_main, r_out;    // fp32 ranges
 };
 
-template <int RM, bool BN, bool AP>
-__host__ __device__ __forceinline__ double smaq_elem_f64(double v, double u, const ElemF64& c,
-                                                         bool& outlier, double g, double b) {
+// smart.py:144-169: the code q (an integer-valued double, or +-inf / NaN) and the outlier sides.
+template <int RM, bool BN>
+__host__ __device__ __forceinline__ double smaq_quant_f64(double v, double u, const ElemF64& c,
+                                                          bool& hi, bool& lo, double g, double b) {
   if (BN) v = (v - b) / g;                             // (data - beta) / gamma
   const double z = (v - c.mean) / c.sc;               // (data - mean) / std.clamp(...)
-  const bool hi = z > c.thr, lo = z < c.nthr;
+  hi = z > c.thr;
+  lo = z < c.nthr;
   const bool o = hi || lo;
   const double a = (hi ? c.snthr : c.zh) + (lo ? c.sthr : c.zl);  // scalars
   const double r = o ? c.r_out : c.r_main;             // ranges
   const double d = (z + a) * r;
-  double q;
-  if (RM == kRoundTrunc) {
-    q = trunc(d);
-  } else {
-    const double f = floor(d);                         // _round_stochastic
-    const double fr = d - f;
-    double t = ((RM == kRoundHash) ? fma(u, -0x1p-24, fr) : (fr - u)) + 0.5;
-    t = (t < 0.0) ? 0.0 : t;                           // F.relu
-    q = f + rint(t);                                   // .round(): half to even
-  }
+  if (RM == kRoundTrunc) return trunc(d);
+  const double f = floor(d);                           // _round_stochastic
+  const double fr = d - f;
+  double t = ((RM == kRoundHash) ? fma(u, -0x1p-24, fr) : (fr - u)) + 0.5;
+  t = (t < 0.0) ? 0.0 : t;                             // F.relu
+  return f + rint(t);                                  // .round(): half to even
+}
+
+// smart.py:171-182: de-quantise q with its sides (the packed codec's decoder shares it).
+template <bool BN, bool AP>
+__host__ __device__ __forceinline__ double smaq_dequant_f64(double q, bool hi, bool lo,
+                                                            const ElemF64& c, double g, double b) {
+  const double a = (hi ? c.snthr : c.zh) + (lo ? c.sthr : c.zl);  // scalars
+  const double r = (hi || lo) ? c.r_out : c.r_main;    // ranges
   double out = (q / r) - a;
   out = (out * c.sd) + c.mean;
   if (BN) out = (out * g) + b;
   if (AP) out = (out < 0.0) ? 0.0 : out;               // clamp_min(0.0)
-  outlier = o;
   return out;
+}
+
+template <int RM, bool BN, bool AP>
+__host__ __device__ __forceinline__ double smaq_elem_f64(double v, double u, const ElemF64& c,
+                                                         bool& outlier, double g, double b) {
+  bool hi, lo;
+  const double q = smaq_quant_f64<RM, BN>(v, u, c, hi, lo, g, b);
+  outlier = hi || lo;
+  return smaq_dequant_f64<BN, AP>(q, hi, lo, c, g, b);
 }
 
 __host__ __device__ inline ElemF64 elem_f64_consts(const SmqSmaqStatsF64& st, const SmqSmaqParams& p) {

@@ -31,5 +31,9 @@ int float_quant_f64(const double* x, void* y, int dtype_out, int64_t n, int exp_
                     uint64_t offset, uint64_t* offset_counter, float max_value, hipStream_t st);
 // Parameter block + dtype validation (sets the thread's last error).
 int smaq_validate(const SmqSmaqParams* p, int dtype);
+// The statistics of an fp64 call (full / sampled / injected) into the workspace header
+// (SmqSmaqStatsF64 at offset 0; fp64.hip): the unpacked round trip's and the fp64 packer's.
+int launch_stats_f64(const double* x, int64_t n, const SmqSmaqParams* p,
+                     const SmqSmaqStatsF64* stats_in, void* ws, size_t ws_bytes, hipStream_t st);
 
 }  // namespace smq

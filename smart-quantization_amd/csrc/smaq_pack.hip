@@ -78,6 +78,7 @@ struct PackArgs {
   uint32_t flags;
   uint32_t lds_words;        // dynamic LDS of the packing kernels (PackLds::words)
   uint32_t inline_scan;      // the var kernel sums the group prefixes itself (no scan launch)
+  uint32_t forward;          // blocks in address order (measurement knob SMQ_PACK_FORWARD)
   const float* bn_gamma;     // BN variant (general packer only), else NULL
   const float* bn_beta;
   int64_t bn_channels, bn_inner;
@@ -420,7 +421,7 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
 template <int RM, int TIN, bool VEC, bool FULL, int WM, int WO, bool EXT>
 __global__ __launch_bounds__(kBlock) void smaq_pack_block_kernel(PackArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t b = FULL ? A.n_full - 1 - blockIdx.x : A.n_blocks - 1;
+  const uint32_t b = FULL ? (A.forward ? blockIdx.x : A.n_full - 1 - blockIdx.x) : A.n_blocks - 1;
   // the subnormal-quotient check only where quot_check_for() asks for it (one uniform branch)
   if (A.stats->quot_check)
     pack_block_body<RM, TIN, VEC, FULL, true, WM, WO, EXT>(A, b, lds);
@@ -529,8 +530,9 @@ __device__ void write_header(const PackArgs& A, uint64_t carry, int tid, int nth
     h->error = 0u;
     h->bn_channels = A.bn_gamma ? (uint32_t)A.bn_channels : 0u;
     h->bn_inner = A.bn_gamma ? A.bn_inner : 0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) h->reserved[i] = 0u;
+    h->mean_f64 = 0.0;
+    h->std_dev_f64 = 0.0;
+    h->reserved[0] = h->reserved[1] = 0u;
     if (A.n_blocks & 1u) A.dir[A.n_blocks] = 0ull;  // the directory's padding entry
   }
   if (A.bn_gamma) {  // the BN table after the variable region (which the var kernel fills next)
@@ -1420,6 +1422,11 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.scratch = (uint32_t*)(wb + L.scratch);
   A.n_groups = n_groups;
   A.inline_scan = n_groups <= kInlineScanGroups ? 1u : 0u;
+  static const int fwd_env = [] {
+    const char* e = knob_env("SMQ_PACK_FORWARD");
+    return e ? atoi(e) : 0;
+  }();
+  A.forward = fwd_env ? 1u : 0u;
   A.thr = p->main_std_dev_threshold;
   A.r_main = p->range_main;
   A.r_out = p->range_outlier;

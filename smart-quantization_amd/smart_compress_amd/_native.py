@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get(
     "SMQ_LIB", os.path.join(os.path.dirname(_PKG_DIR), "lib", "libsmq.so")
 )
 
-SMQ_ABI_VERSION = 7
+SMQ_ABI_VERSION = 8
 SMQ_MAX_SAMPLES = 64
 SMQ_MAX_DEVICE_SAMPLES = 4096
 SMQ_MAX_DRAW_SAMPLES = 1 << 28
@@ -121,7 +121,9 @@ class SmqPackedHeader(ctypes.Structure):
         ("error", ctypes.c_uint32),
         ("bn_channels", ctypes.c_uint32),
         ("bn_inner", ctypes.c_int64),
-        ("reserved", ctypes.c_uint32 * 6),
+        ("mean_f64", ctypes.c_double),
+        ("std_dev_f64", ctypes.c_double),
+        ("reserved", ctypes.c_uint32 * 2),
     ]
 
 
@@ -131,6 +133,7 @@ SMQ_PACK_FLAG_ALL_POSITIVE = 1
 SMQ_PACK_FLAG_SAFE_Q = 2
 SMQ_PACK_FLAG_BOTH_SIDES = 4
 SMQ_PACK_FLAG_BN = 8
+SMQ_PACK_FLAG_F64 = 16
 
 
 class SmqTensorDesc(ctypes.Structure):
@@ -281,6 +284,14 @@ SIGNATURES = {
                                      _SZ, _I32]),
     "smq_cpu_smaq_decompress": (_I32, [_P, _P, _I64, _I32]),
     "smq_smaq_decompress_ex": (_I32, [_P, _P, _I64, _I32, _I32, _P]),
+    "smq_smaq_pack_bound_f64": (_SZ, [_I64, _I32, _I32, _I64]),
+    "smq_smaq_pack_workspace_bytes_f64": (_SZ, [_I64, _I64]),
+    "smq_smaq_compress_f64": (_I32, [_P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P, _SZ,
+                                     _P]),
+    "smq_smaq_decompress_f64": (_I32, [_P, _P, _I64, _I32, _I32, _P]),
+    "smq_cpu_smaq_compress_f64": (_I32, [_P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P,
+                                         _SZ, _I32]),
+    "smq_cpu_smaq_decompress_f64": (_I32, [_P, _P, _I64, _I32]),
     "smq_cpu_threads": (_I32, []),
     "smq_cpu_smaq_roundtrip": (
         _I32,

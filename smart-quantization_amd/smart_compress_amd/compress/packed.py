@@ -12,6 +12,9 @@ the container of include/smq.h ("Packed SmaQ container"):
   built by ``smq_smaq_compress`` (statistics + three packing launches);
 * ``decompress(p)`` -> fp32 tensor, bit-identical to what ``SmartFP`` returns for the same input,
   flags and random stream (``smq_smaq_decompress_ex``, one launch);
+* float64 tensors: the fp64 chain's codes (smart.py on a float64 tensor, as ``SmartFP`` runs it) in a
+  float64 stream (flag SMQ_PACK_FLAG_F64: 3-word escapes, fp64 statistics; ``smq_smaq_compress_f64``
+  / ``smq_cpu_smaq_compress_f64``), decoded to float64 — again bit-identical to ``SmartFP``;
 * ``__call__`` = decompress(compress(x)), a drop-in SmaQ codec whose ``new_size`` log is the real
   stream size.
 
@@ -49,11 +52,12 @@ class SmaqPacked:
     fp32 bytes (smart.py:123-128)."""
 
     def __init__(self, data: torch.Tensor, shape: torch.Size, n: int, raw: bool = False,
-                 widths=None, total: Optional[int] = None):
+                 widths=None, total: Optional[int] = None, dtype: torch.dtype = torch.float32):
         self.data = data
         self.shape = torch.Size(shape)
         self.n = int(n)
         self.raw = raw
+        self.dtype = dtype    # of the decoded values (float64: a float64 stream; raw: as kept)
         self.widths = widths  # (num_bits_main, num_bits_outlier) the stream was written with
         # the stream size when known on the host (raw data: all of it)
         self._total = int(data.numel()) if raw else total
@@ -72,7 +76,7 @@ class SmaqPacked:
         if total == self.data.numel():
             return self
         return SmaqPacked(self.data[:total].clone(), self.shape, self.n, widths=self.widths,
-                          total=total)
+                          total=total, dtype=self.dtype)
 
     @property
     def bits_per_element(self) -> float:
@@ -104,15 +108,19 @@ class SmartFPPacked(SmartFP):
         hp = self.hparams
         numel = data.numel()
         if numel < hp.min_size:  # smart.py:123-128: kept as is
-            raw = data.detach().to(torch.float32).contiguous().reshape(-1).view(torch.uint8)
-            return SmaqPacked(raw.clone(), data.shape, numel, raw=True)
+            kdt = torch.float64 if data.dtype == torch.float64 else torch.float32
+            raw = data.detach().to(kdt).contiguous().reshape(-1).view(torch.uint8)
+            return SmaqPacked(raw.clone(), data.shape, numel, raw=True, dtype=kdt)
         if hp.main_std_dev_threshold != hp.main_std_dev_threshold:
             raise NotImplementedError("SmartFPPacked: main_std_dev_threshold is NaN")
         N.require_supported(data, "SmartFPPacked")
+        if data.dtype == torch.float64:
+            return self._compress_f64(data, all_positive, batch_norm_stats, out)
         code = N.DTYPE_CODES.get(data.dtype)
         if code is None:
             raise NotImplementedError(
-                f"SmartFPPacked: dtype {data.dtype} is not supported (float32/float16/bfloat16)")
+                f"SmartFPPacked: dtype {data.dtype} is not supported "
+                "(float32/float16/bfloat16/float64)")
         if data.dtype == torch.float16 and hp.precision != 16:
             raise RuntimeError("value cannot be converted to type c10::Half without overflow")
         x = data.contiguous()
@@ -150,14 +158,64 @@ class SmartFPPacked(SmartFP):
         # the stream size stays on the device (SmaqPacked.nbytes / compact read it when asked)
         return SmaqPacked(out, data.shape, numel, widths=widths)
 
+    def _compress_f64(self, data, all_positive, batch_norm_stats, out):
+        """float64 data: the fp64 chain (SmartFP._call_f64's) in a float64 stream."""
+        hp = self.hparams
+        numel = data.numel()
+        x = data.contiguous()
+        lib = N.lib()
+        cpu = N.on_cpu(x)
+        p = self._params(numel, all_positive, torch.float64, None if cpu else x.device)
+        keep = None
+        if hp.use_batch_norm and batch_norm_stats is not None:
+            keep = self._bind_batch_norm(p, x, batch_norm_stats)  # fp64 parameters
+        bound = lib.smq_smaq_pack_bound_f64(numel, hp.num_bits_main, hp.num_bits_outlier,
+                                            p.bn_channels if keep is not None else 0)
+        widths = (hp.num_bits_main, hp.num_bits_outlier)
+        if cpu:
+            buf = torch.empty(bound, dtype=torch.uint8)
+            ws = N.cpu_workspace("smaq", self.workspace_bytes(numel))
+            N.check(lib.smq_cpu_smaq_compress_f64(x.data_ptr(), numel, p, buf.data_ptr(),
+                                                  buf.numel(), ws.data_ptr(), ws.numel(),
+                                                  N.cpu_threads()), "smq_cpu_smaq_compress_f64")
+            del keep
+            total = int(buf[_TOTAL_OFF:_TOTAL_OFF + 8].numpy().view(np.uint64)[0])
+            return SmaqPacked(buf[:total].clone(), data.shape, numel, widths=widths, total=total,
+                              dtype=torch.float64)
+        if out is None:
+            out = torch.empty(bound, dtype=torch.uint8, device=x.device)
+        elif out.dtype != torch.uint8 or out.device != x.device or out.numel() < bound:
+            raise ValueError(f"SmartFPPacked.compress: out must be a uint8 buffer of >= {bound} "
+                             f"bytes on {x.device}")
+        k = p.num_samples if p.stats_source == N.SMQ_STATS_SAMPLED_DEVICE else 0
+        ws = N.workspace("smaq_pack_f64", x.device, lib.smq_smaq_pack_workspace_bytes_f64(numel, k))
+        N.check(lib.smq_smaq_compress_f64(x.data_ptr(), numel, p, out.data_ptr(), out.numel(),
+                                          ws.data_ptr(), ws.numel(), N.stream_ptr(x.device)),
+                "smq_smaq_compress_f64")
+        del keep
+        return SmaqPacked(out, data.shape, numel, widths=widths, dtype=torch.float64)
+
     def decompress(self, packed: SmaqPacked) -> torch.Tensor:
         """fp32 values, bit-identical to ``SmartFP`` on the compressed tensor (same flags and random
         stream), on the device the stream is on (a CPU stream: ``smq_cpu_smaq_decompress``)."""
         if packed.raw:
-            return packed.data.view(torch.float32).reshape(packed.shape).clone()
+            return packed.data.view(packed.dtype).reshape(packed.shape).clone()
         N.require_supported(packed.data, "SmartFPPacked.decompress")
-        y = torch.empty(packed.shape, dtype=torch.float32, device=packed.data.device)
         lib = N.lib()
+        if packed.dtype == torch.float64:
+            y = torch.empty(packed.shape, dtype=torch.float64, device=packed.data.device)
+            if N.on_cpu(packed.data):
+                N.check(lib.smq_cpu_smaq_decompress_f64(packed.data.data_ptr(), y.data_ptr(),
+                                                        packed.n, N.cpu_threads()),
+                        "smq_cpu_smaq_decompress_f64")
+            else:
+                bm, bo = packed.widths if packed.widths is not None else (
+                    packed.header()["num_bits_main"], packed.header()["num_bits_outlier"])
+                N.check(lib.smq_smaq_decompress_f64(packed.data.data_ptr(), y.data_ptr(), packed.n,
+                                                    bm, bo, N.stream_ptr(y.device)),
+                        "smq_smaq_decompress_f64")
+            return y
+        y = torch.empty(packed.shape, dtype=torch.float32, device=packed.data.device)
         if N.on_cpu(packed.data):
             N.check(lib.smq_cpu_smaq_decompress(packed.data.data_ptr(), y.data_ptr(), packed.n,
                                                 N.cpu_threads()), "smq_cpu_smaq_decompress")

@@ -99,7 +99,7 @@ class PackedActivations:
         codec = self.codec
         hp = codec.hparams
         if (self._hooks is None or tag != FORWARD_TAG or x.numel() < hp.min_size
-                or not x.is_cuda):
+                or not x.is_cuda or x.dtype == torch.float64):
             return codec(x, tag=tag, all_positive=all_positive, batch_norm_stats=batch_norm_stats,
                          **kw)
         n = x.numel()
