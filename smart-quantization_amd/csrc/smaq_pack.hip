@@ -150,6 +150,9 @@ __device__ __forceinline__ float pack_cthr(const PackArgs& A) {
   return (TIN == kF32 || A.bn_gamma) ? A.thr : round_in<TIN>(A.thr);
 }
 
+// Keep a (uniform) value in a VGPR: an empty asm the compiler cannot see through.
+#define PIN_VGPR(v) asm volatile("" : "+v"(v))
+
 // OR a chunk of up to 64 bits at bit pos of an LDS bit stream (two or three words; the third only
 // when bits land there).
 __device__ __forceinline__ void or_bits64(uint32_t* base, uint32_t pos, uint64_t chunk) {
@@ -236,6 +239,11 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
   const uint32_t ppos0 = 4u * (uint32_t)wm * (uint32_t)tid;
   const uint32_t pw0 = ppos0 >> 5, psft = ppos0 & 31u;
   const QuadRun R = quad_run(A.key, A.offset + c.rng_off + (uint64_t)e0, kPB / 4);
+  // the selects of pack_quant take two non-inline operands (T_m / r_main / r_out are SGPR values):
+  // without a VGPR copy the compiler re-materialises one per slot (v_mov_b32) — pinned once here
+  PIN_VGPR(c.thr);
+  PIN_VGPR(c.r_main);
+  PIN_VGPR(c.r_out);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int el = 1024 * k + 4 * tid;
@@ -612,11 +620,11 @@ __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_d
   for (uint32_t i = tid; i < ext_words(we, n_out); i += kBlock) out[i] = ext[i];
 }
 
-// One workgroup per group of kGroup blocks: wave 0 turns the blocks' sizes into their offsets
-// (group prefix + DPP scan) and directory entries; each wave then copies the variable sections of
-// every fourth block from its scratch slot to the stream (a lane copies words lane, lane + 64, ...;
-// four blocks' loads in flight before their stores); blocks whose section outgrew the slot are
-// re-coded from x by the whole workgroup (recode_var_section).
+// One workgroup per group of kGroup blocks: each wave requests the sections of its 16 blocks from
+// their scratch slots (a lane holds words lane, lane + 64, lane + 128, lane + 192 of each), the
+// workgroup sums the group prefix meanwhile, every wave turns the 64 sizes into offsets (DPP scan;
+// wave 0 writes the directory entries) and stores its blocks' sections; blocks whose section
+// outgrew the slot are re-coded from x (pack_recode_blocks, the workgroups after the groups).
 template <int RM, int TIN, bool EXT>
 __device__ void pack_recode_blocks(const PackArgs& A, uint32_t wg, uint32_t per, uint32_t* lds);
 
@@ -625,9 +633,6 @@ __device__ void pack_recode_blocks(const PackArgs& A, uint32_t wg, uint32_t per,
 template <int RM, int TIN, int WM, int WO, bool EXT>
 __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A, uint32_t per) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];  // re-code: 128 * we words
-  __shared__ uint32_t s_off[kGroup + 1];   // group-relative word offsets (s_off[64] = total)
-  __shared__ uint64_t s_base;
-  __shared__ unsigned long long s_over;    // blocks of the group re-coded from x
   if (blockIdx.x >= A.n_groups) {
     pack_recode_blocks<RM, TIN, EXT>(A, blockIdx.x - A.n_groups, per, lds);
     return;
@@ -638,67 +643,54 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A, uint3
   const uint32_t g = blockIdx.x;
   const uint32_t b0 = g * kGroup;
   const uint32_t nb = min((uint32_t)kGroup, A.n_blocks - b0);
+  // every wave: the group's 64 sizes (one meta word per lane), then the first 256 words of its 16
+  // blocks' sections requested at once — in flight while the group prefix is summed (round 5: the
+  // copy had waited for the prefix and gone 4 blocks per round trip, 24-25 us at 256M)
+  uint32_t sz = 0u, t = 0u, fsz = 0u;  // fsz: the section's size; sz: the words copied here
+  if ((uint32_t)lane < nb) {
+    const uint32_t m = A.meta[b0 + lane];
+    t = m & ~kMetaRecode;
+    fsz = ext_words(we, t & 0xffffu) + 2u * (t >> 16);
+    sz = (m & kMetaRecode) ? 0u : fsz;  // a re-coded block is written by pack_recode_blocks
+  }
+  constexpr int kB = kGroup / (kBlock / kWave);  // 16 blocks per wave
+  constexpr int kW = 4;  // words per lane and block in the first round (256: most sections at 6/8 bits)
+  uint32_t v[kB][kW];
+#pragma unroll
+  for (int q = 0; q < kB; ++q) {
+    const uint32_t j = (uint32_t)(w * kB + q);
+    const uint32_t szq = (uint32_t)__builtin_amdgcn_readlane((int)sz, (int)j);
+    const uint32_t* src = A.scratch + (size_t)(b0 + j) * kVarCap;
+#pragma unroll
+    for (int r = 0; r < kW; ++r) {
+      const uint32_t i = (uint32_t)lane + (uint32_t)r * kWave;
+      if (i < szq) v[q][r] = src[i];
+    }
+  }
   uint64_t ibase = 0;
   if (A.inline_scan) {
     uint32_t total;
     ibase = group_prefix(A, g, total);
     if (g == 0) write_header(A, total, tid, kBlock);
   }
-  if (tid < kWave) {
-    uint32_t sz = 0u, t = 0u;
-    bool rec = false;
-    if ((uint32_t)lane < nb) {
-      const uint32_t m = A.meta[b0 + lane];
-      rec = (m & kMetaRecode) != 0u;
-      t = m & ~kMetaRecode;
-      sz = ext_words(we, t & 0xffffu) + 2u * (t >> 16);
-    }
-    const uint32_t incl = wave_incl_scan_u32(sz);
-    const uint32_t ex = incl - sz;
-    const uint64_t base = A.inline_scan ? ibase : A.gpre[g];
-    s_off[lane] = ex;
-    if (lane == kWave - 1) s_off[kGroup] = incl;
-    if ((uint32_t)lane < nb)
-      A.dir[b0 + lane] = (base + ex) | ((uint64_t)(t & 0xffffu) << 38) | ((uint64_t)(t >> 16) << 51);
-    const unsigned long long over = __ballot(rec);
-    if (lane == 0) {
-      s_base = base;
-      s_over = over;
-    }
-  }
-  __syncthreads();
-  const uint64_t base = s_base;
-  const unsigned long long over = s_over;
+  // offsets and directory entries: every wave holds the 64 sizes (no LDS hand-off)
+  const uint64_t base = A.inline_scan ? ibase : A.gpre[g];
+  const uint32_t fex = wave_incl_scan_u32(fsz) - fsz;
+  if (w == 0 && (uint32_t)lane < nb)
+    A.dir[b0 + lane] = (base + fex) | ((uint64_t)(t & 0xffffu) << 38) | ((uint64_t)(t >> 16) << 51);
   uint32_t* out = A.var + base;
-  constexpr int kB = 4;  // blocks per step of a wave
-  constexpr int kW = 4;  // words per lane and block per step (256 words: most sections at 6/8 bits)
-  for (uint32_t j0 = (uint32_t)w * kB; j0 < nb; j0 += kB * (kBlock / kWave)) {
-    uint32_t v[kB][kW];
 #pragma unroll
-    for (int q = 0; q < kB; ++q) {
-      const uint32_t j = j0 + q;
-      const bool ok = j < nb && !((over >> j) & 1ull);
-      const uint32_t o0 = ok ? s_off[j] : 0u, sz = ok ? s_off[j + 1] - o0 : 0u;
-      const uint32_t* src = A.scratch + (size_t)(b0 + j) * kVarCap;
+  for (int q = 0; q < kB; ++q) {
+    const uint32_t j = (uint32_t)(w * kB + q);
+    const uint32_t szq = (uint32_t)__builtin_amdgcn_readlane((int)sz, (int)j);
+    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)fex, (int)j);
+    const uint32_t* src = A.scratch + (size_t)(b0 + j) * kVarCap;
 #pragma unroll
-      for (int r = 0; r < kW; ++r) {
-        const uint32_t i = (uint32_t)lane + (uint32_t)r * kWave;
-        if (i < sz) v[q][r] = src[i];
-      }
+    for (int r = 0; r < kW; ++r) {
+      const uint32_t i = (uint32_t)lane + (uint32_t)r * kWave;
+      if (i < szq) out[o0 + i] = v[q][r];
     }
-#pragma unroll
-    for (int q = 0; q < kB; ++q) {
-      const uint32_t j = j0 + q;
-      const bool ok = j < nb && !((over >> j) & 1ull);
-      const uint32_t o0 = ok ? s_off[j] : 0u, sz = ok ? s_off[j + 1] - o0 : 0u;
-      const uint32_t* src = A.scratch + (size_t)(b0 + j) * kVarCap;
-#pragma unroll
-      for (int r = 0; r < kW; ++r) {
-        const uint32_t i = (uint32_t)lane + (uint32_t)r * kWave;
-        if (i < sz) out[o0 + i] = v[q][r];
-      }
-      for (uint32_t i = (uint32_t)lane + kW * kWave; i < sz; i += kWave) out[o0 + i] = src[i];
-    }
+    for (uint32_t i = (uint32_t)lane + kW * kWave; i < szq; i += kWave) out[o0 + i] = src[i];
   }
 }
 
