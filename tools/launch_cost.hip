@@ -67,6 +67,22 @@ int main() {
     smq_smaq_roundtrip(x, SMQ_DTYPE_F32, y, n, &p, nullptr, ws, wsb, st);
   });
   const double t_err = us_per(reps, [&] { (void)hipGetLastError(); });
+  // the same 256-B-argument launch through hipModuleLaunchKernel with the function handle looked up
+  // once (hipLaunchKernel resolves the host stub on every call)
+  hipFunction_t fn;
+  (void)hipGetFuncBySymbol(&fn, reinterpret_cast<const void*>(&empty_kernel<256>));
+  size_t asz = sizeof(big);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &big, HIP_LAUNCH_PARAM_BUFFER_SIZE, &asz,
+                 HIP_LAUNCH_PARAM_END};
+  const double t_mod = us_per(reps, [&] {
+    (void)hipModuleLaunchKernel(fn, 16, 1, 1, 1024, 1, 1, 0, st, nullptr, cfg);
+  });
+  void* kargs[] = {&big};
+  const double t_lk = us_per(reps, [&] {
+    (void)hipLaunchKernel(reinterpret_cast<const void*>(&empty_kernel<256>), dim3(16), dim3(1024),
+                          kargs, 0, st);
+  });
+  std::printf("{\"module_launch_us\": %.3f, \"hipLaunchKernel_us\": %.3f}\n", t_mod, t_lk);
   std::printf("{\"empty_launch_us\": %.3f, \"empty_launch_1wg_us\": %.3f, \"smq_smaq_roundtrip_us\": %.3f, "
               "\"hipGetLastError_us\": %.3f, \"args16_us\": %.3f, \"args64_us\": %.3f, "
               "\"args1024_us\": %.3f, \"args16_nonblocking_us\": %.3f}\n", t_empty, t_empty_small,
