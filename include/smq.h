@@ -554,6 +554,22 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
 int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
                          void* packed, size_t packed_bytes, void* workspace,
                          size_t workspace_bytes, uint32_t flags, void* stream);
+/* Bytes of a stream's parts that do not depend on the data: header, directory, fixed region. */
+size_t smq_smaq_pack_fixed_bytes(int64_t n, int num_bits_main);
+/* y = smq_smaq_roundtrip(x) AND the stream of the same call (the codes whose decoding is y, bit for
+ * bit): one statistics pass (the single launch up to 8,388,611 elements, else the statistics and
+ * apply launches) whose record the packing launches then read — no statistics launch of their own,
+ * no decode of the stream to get y. The random stream advances once (n counters), as for either
+ * call alone. Same params, workspace (smq_smaq_pack_workspace_bytes[_sampled]) and statistics
+ * sources as smq_smaq_compress; x must not alias y. packed_bytes may be anything from
+ * smq_smaq_pack_fixed_bytes up: a variable section (or the BN table) that would end past the
+ * buffer is not written, and header.total_bytes > packed_bytes then tells the caller that the
+ * stream did not fit (it must not be decoded). With packed_bytes >= smq_smaq_pack_bound[_bn] the
+ * stream equals smq_smaq_compress's byte for byte. Reference: smart.py:110-190 (y) and its
+ * log_size codes (smart.py:184-188) kept for real (README.md:25-28). */
+int smq_smaq_roundtrip_compress(const void* x, int dtype, float* y, int64_t n,
+                                const SmqSmaqParams* params, void* packed, size_t packed_bytes,
+                                void* workspace, size_t workspace_bytes, void* stream);
 /* Decode a stream of n elements into y (fp32). n must equal the header's n (a stream with another
  * n or a bad magic leaves y untouched). */
 int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream);

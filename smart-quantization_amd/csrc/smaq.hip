@@ -1419,3 +1419,36 @@ int smq_smaq_roundtrip_f32(const float* x, float* y, int64_t n, const SmqSmaqPar
 }
 
 }  // extern "C"
+
+namespace smq {
+
+int roundtrip_for_pack(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                       void* ws, size_t ws_bytes, hipStream_t st, uint32_t* zero, uint32_t zero_n,
+                       bool* zeroed) {
+  *zeroed = false;
+  int rc = validate_params(p);
+  if (!rc) rc = check_dtype(dtype);
+  if (!rc) rc = check_tensor_args(x, y, n);
+  if (rc) return rc;
+  if (p->stats_source == SMQ_STATS_INJECTED) {
+    set_error("roundtrip_compress: statistics must be computed (not SMQ_STATS_INJECTED)");
+    return SMQ_ERR_INVALID;
+  }
+  if (p->stats_source == SMQ_STATS_WORKSPACE && ws &&
+      fused_eligible(x, dtype, y, n, p, nullptr, ws_bytes)) {
+    // the single launch: its workgroup 0 writes the record to the header and clears `zero`
+    const RangeRecips R = range_recips(p->range_main, p->range_outlier);
+    FusedCall c{x, dtype, y, n, p, range_coef_for(p, n), R.inv_main, R.inv_out, ws, 0, ws_bytes,
+                zero, zero_n};
+    *zeroed = zero != nullptr;
+    return launch_fused(c, st);
+  }
+  if (p->stats_source == SMQ_STATS_WORKSPACE) {  // finalised into the header, never deferred
+    rc = launch_stats(x, dtype, n, p, ws, ws_bytes, st, nullptr, nullptr, zero, zero_n);
+    if (rc) return rc;
+    *zeroed = zero != nullptr;
+  }
+  return launch_apply(x, dtype, y, n, p, nullptr, nullptr, ws, ws_bytes, st);
+}
+
+}  // namespace smq

@@ -163,6 +163,8 @@ struct FusedArgs {
   int all_pos, count, range, test_late;
   int poll_sleep;   // s_sleep between poll passes
   uint64_t* trace;  // experiment builds (-DSMQ_FUSED_TRACE=1): 16 timestamps per workgroup
+  uint32_t* zero;   // cleared by workgroup 0 (the packer's group sums: roundtrip_compress), or NULL
+  uint32_t zero_n;
 };
 
 // s_memrealtime stamps (100 MHz) of workgroup milestones, experiment builds only
@@ -343,6 +345,8 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   const int64_t base = (int64_t)b * V * kSmallT + threadIdx.x;
   const uint64_t steal_ticks = A.test_late ? 2000 : kFusedStealTicks;
   FSTAMP(0);
+  if (A.zero && b == 0)
+    for (uint32_t i = threadIdx.x; i < A.zero_n; i += kSmallT) A.zero[i] = 0u;
   if (A.test_late && 2 * b >= G && G > 1) {  // test aid: half of the grid starts ~500 us late
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < 50000) __builtin_amdgcn_s_sleep(127);
@@ -733,6 +737,8 @@ int launch_fused(const FusedCall& c, hipStream_t st) {
   }();
   F.poll_sleep = poll_sleep;
   F.trace = nullptr;
+  F.zero = c.zero;
+  F.zero_n = c.zero_n;
 #if SMQ_FUSED_TRACE
   if (c.ws_bytes >= SmaqWsLayout::kTotal + 16 * 8 * (size_t)kSmallMaxG)
     F.trace = (uint64_t*)(base + SmaqWsLayout::kTotal);

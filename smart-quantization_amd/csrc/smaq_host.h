@@ -12,6 +12,12 @@ namespace smq {
 int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,
                   size_t ws_bytes, hipStream_t st, uint32_t* zero = nullptr, uint32_t zero_n = 0,
                   bool* zeroed = nullptr);
+// smq_smaq_roundtrip (y = SmartFP(x)) whose statistics record ends in the workspace header for a
+// packer that follows (smq_smaq_roundtrip_compress): the single launch where it applies, else the
+// statistics launch without deferral and the apply. zero / zero_n as for prepare_stats.
+int roundtrip_for_pack(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                       void* ws, size_t ws_bytes, hipStream_t st, uint32_t* zero, uint32_t zero_n,
+                       bool* zeroed);
 // Full statistics of x (the single-tensor statistics launch, finalised by its last workgroup) into
 // *out instead of the workspace header (multi-tensor calls: tensors above the small partition).
 int stats_into(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,

@@ -79,6 +79,8 @@ struct PackArgs {
   uint32_t lds_words;        // dynamic LDS of the packing kernels (PackLds::words)
   uint32_t inline_scan;      // the var kernel sums the group prefixes itself (no scan launch)
   uint32_t forward;          // blocks in address order (measurement knob SMQ_PACK_FORWARD)
+  uint64_t cap_words;        // words of the variable region (+ BN table) the buffer holds: a
+                             // section that would end past it is not written
   const float* bn_gamma;     // BN variant (general packer only), else NULL
   const float* bn_beta;
   int64_t bn_channels, bn_inner;
@@ -543,7 +545,8 @@ __device__ void write_header(const PackArgs& A, uint64_t carry, int tid, int nth
     h->reserved[0] = h->reserved[1] = 0u;
     if (A.n_blocks & 1u) A.dir[A.n_blocks] = 0ull;  // the directory's padding entry
   }
-  if (A.bn_gamma) {  // the BN table after the variable region (which the var kernel fills next)
+  if (A.bn_gamma && carry + 2ull * (uint64_t)A.bn_channels <= A.cap_words) {
+    // the BN table after the variable region (which the var kernel fills next)
     float* t = reinterpret_cast<float*>(A.var + carry);
     for (int64_t i = tid; i < A.bn_channels; i += nthr) {
       t[i] = A.bn_gamma[i];
@@ -682,8 +685,9 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A, uint3
 #pragma unroll
   for (int q = 0; q < kB; ++q) {
     const uint32_t j = (uint32_t)(w * kB + q);
-    const uint32_t szq = (uint32_t)__builtin_amdgcn_readlane((int)sz, (int)j);
     const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)fex, (int)j);
+    uint32_t szq = (uint32_t)__builtin_amdgcn_readlane((int)sz, (int)j);
+    if (base + o0 + szq > A.cap_words) szq = 0u;  // past the buffer (a capacity-bounded stream)
     const uint32_t* src = A.scratch + (size_t)(b0 + j) * kVarCap;
 #pragma unroll
     for (int r = 0; r < kW; ++r) {
@@ -734,7 +738,9 @@ __device__ void pack_recode_blocks(const PackArgs& A, uint32_t wg, uint32_t per,
       if (lane == kWave - 1) s_dst = (A.inline_scan ? gbase : A.gpre[g]) + before;
     }
     __syncthreads();
-    recode_var_section<RM, TIN, EXT>(A, b, s_dst, lds, s_cnt);
+    const uint32_t t = A.meta[b] & ~kMetaRecode;
+    if (s_dst + ext_words(we, t & 0xffffu) + 2u * (t >> 16) <= A.cap_words)
+      recode_var_section<RM, TIN, EXT>(A, b, s_dst, lds, s_cnt);
     __syncthreads();
   }
 }
@@ -1338,10 +1344,14 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
   return smq_smaq_compress_ex(x, dtype, n, p, packed, packed_bytes, ws, ws_bytes, 0u, stream);
 }
 
-int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParams* p,
+}  // extern "C"
+
+// smq_smaq_compress_ex (y == NULL: the statistics launch first) and smq_smaq_roundtrip_compress
+// (y != NULL: SmartFP's round trip into y first, whose statistics record the packer then reads;
+// packed_bytes may be below the bound, down to the stream's fixed part).
+static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, float* y,
                          void* packed, size_t packed_bytes, void* ws, size_t ws_bytes,
-                         uint32_t flags, void* stream) {
-  (void)flags;  // SMQ_PACK_TICKETED / SMQ_PACK_SINGLE: accepted, one packer (see smq.h)
+                         hipStream_t st) {
   int rc = smaq_validate(p, dtype);
   if (rc) return rc;
   if (n < 1 || !x || !packed) {
@@ -1375,9 +1385,13 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   }
   const size_t bound = smq_smaq_pack_bound_bn(n, p->num_bits_main, p->num_bits_outlier,
                                               p->bn_gamma ? p->bn_channels : 0);
-  if (packed_bytes < bound) {
-    set_error("compress: packed buffer too small: need %zu bytes (smq_smaq_pack_bound%s), got %zu",
-              bound, p->bn_gamma ? "_bn" : "", packed_bytes);
+  const size_t fixed = smq_smaq_pack_fixed_bytes(n, p->num_bits_main);
+  if (packed_bytes < (y ? fixed : bound)) {
+    set_error("compress: packed buffer too small: need %zu bytes (%s), got %zu",
+              y ? fixed : bound,
+              y ? "smq_smaq_pack_fixed_bytes" : (p->bn_gamma ? "smq_smaq_pack_bound_bn"
+                                                             : "smq_smaq_pack_bound"),
+              packed_bytes);
     return SMQ_ERR_WORKSPACE;
   }
   const int64_t k_draw = p->stats_source == SMQ_STATS_SAMPLED_DEVICE
@@ -1387,12 +1401,16 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
     set_error("compress: workspace too small: need %zu bytes, got %zu", L.total, ws_bytes);
     return SMQ_ERR_WORKSPACE;
   }
-  hipStream_t st = (hipStream_t)stream;
   // the statistics own the first region (sized for the multi-workgroup draw above 4096 samples)
   char* wb = (char*)ws;
   const uint32_t n_groups = (uint32_t)(((size_t)nb + kGroup - 1) / kGroup);
   bool zeroed = false;  // the group sums start at zero: cleared by the statistics launch
-  rc = prepare_stats(x, dtype, n, p, ws, L.meta, st, (uint32_t*)(wb + L.gsum), n_groups, &zeroed);
+  if (y)
+    rc = roundtrip_for_pack(x, dtype, y, n, p, ws, L.meta, st, (uint32_t*)(wb + L.gsum), n_groups,
+                            &zeroed);
+  else
+    rc = prepare_stats(x, dtype, n, p, ws, L.meta, st, (uint32_t*)(wb + L.gsum), n_groups,
+                       &zeroed);
   if (rc) return rc;
   PackArgs A;
   memset(&A, 0, sizeof(A));
@@ -1407,6 +1425,7 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
   A.dir = (uint64_t*)((char*)packed + sizeof(SmqPackedHeader));
   A.fixed = (uint32_t*)(A.dir + dir_entries(nb));
   A.var = A.fixed + (size_t)nb * fixed_words(A.wm);
+  A.cap_words = packed_bytes >= bound ? ~0ull : (uint64_t)((packed_bytes - fixed) / 4);
   A.stats = (const SmqSmaqStats*)ws;
   A.meta = (uint32_t*)(wb + L.meta);
   A.gsum = (uint32_t*)(wb + L.gsum);
@@ -1451,6 +1470,35 @@ int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParam
     else launch_pack<kRoundTrunc, kBF16>(A, vec, ext, st);
   }
   return check_launch("smaq_pack_block_kernel / smaq_pack_var_kernel");
+}
+
+extern "C" {
+
+int smq_smaq_compress_ex(const void* x, int dtype, int64_t n, const SmqSmaqParams* p,
+                         void* packed, size_t packed_bytes, void* ws, size_t ws_bytes,
+                         uint32_t flags, void* stream) {
+  (void)flags;  // SMQ_PACK_TICKETED / SMQ_PACK_SINGLE: accepted, one packer (see smq.h)
+  return compress_impl(x, dtype, n, p, nullptr, packed, packed_bytes, ws, ws_bytes,
+                       (hipStream_t)stream);
+}
+
+size_t smq_smaq_pack_fixed_bytes(int64_t n, int num_bits_main) {
+  if (n < 1) return sizeof(SmqPackedHeader);
+  const int wm = num_bits_main - 1;
+  const int64_t nb = n_blocks_of(n);
+  return sizeof(SmqPackedHeader) + 8 * (size_t)dir_entries(nb) +
+         4 * (size_t)nb * fixed_words(wm < 1 ? 1 : wm);
+}
+
+int smq_smaq_roundtrip_compress(const void* x, int dtype, float* y, int64_t n,
+                                const SmqSmaqParams* p, void* packed, size_t packed_bytes,
+                                void* ws, size_t ws_bytes, void* stream) {
+  if (!y) {
+    set_error("roundtrip_compress: y must be a device pointer");
+    return SMQ_ERR_INVALID;
+  }
+  return compress_impl(x, dtype, n, p, y, packed, packed_bytes, ws, ws_bytes,
+                       (hipStream_t)stream);
 }
 
 static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int bo, void* stream) {

@@ -279,6 +279,8 @@ struct FusedCall {
   void* ws;
   int test_late;
   size_t ws_bytes;
+  uint32_t* zero = nullptr;  // words the launch clears (the packer's group sums), or NULL
+  uint32_t zero_n = 0;
 };
 int launch_fused(const FusedCall& c, hipStream_t st);
 

@@ -158,6 +158,53 @@ class SmartFPPacked(SmartFP):
         # the stream size stays on the device (SmaqPacked.nbytes / compact read it when asked)
         return SmaqPacked(out, data.shape, numel, widths=widths)
 
+    def roundtrip_compress(self, data: torch.Tensor, all_positive: bool = False,
+                           batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                           capacity: Optional[int] = None) -> Tuple[torch.Tensor, SmaqPacked]:
+        """``(y, p)``: ``y`` what ``SmartFP`` returns for ``data`` (smart.py:110-190) and ``p`` its
+        stream — ``decompress(p) == y`` bit for bit — from one statistics pass
+        (``smq_smaq_roundtrip_compress``: the round trip, then the packing launches on its
+        statistics; no decode to get ``y``). ``capacity``: bytes of the stream buffer (default
+        ``smq_smaq_pack_bound``); a smaller one holds the stream when it fits, which
+        ``p.nbytes <= capacity`` tells (a stream that did not fit must not be decoded).
+        CPU and float64 tensors: ``compress`` then ``decompress`` (the same values)."""
+        hp = self.hparams
+        numel = data.numel()
+        if (numel < hp.min_size or N.on_cpu(data) or data.dtype == torch.float64
+                or hp.main_std_dev_threshold != hp.main_std_dev_threshold):
+            p = self.compress(data, all_positive, batch_norm_stats)
+            return self.decompress(p), p
+        N.require_supported(data, "SmartFPPacked")
+        code = N.DTYPE_CODES.get(data.dtype)
+        if code is None:
+            raise NotImplementedError(
+                f"SmartFPPacked: dtype {data.dtype} is not supported "
+                "(float32/float16/bfloat16/float64)")
+        if data.dtype == torch.float16 and hp.precision != 16:
+            raise RuntimeError("value cannot be converted to type c10::Half without overflow")
+        x = data.contiguous()
+        lib = N.lib()
+        p = self._params(numel, all_positive, x.dtype, x.device)
+        keep = None
+        if hp.use_batch_norm and batch_norm_stats is not None:
+            keep = self._bind_batch_norm(p, x, batch_norm_stats)
+        if capacity is None:
+            capacity = lib.smq_smaq_pack_bound_bn(numel, hp.num_bits_main, hp.num_bits_outlier,
+                                                  p.bn_channels if keep is not None else 0)
+        out = torch.empty(int(capacity), dtype=torch.uint8, device=x.device)
+        y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        sampled = p.stats_source == N.SMQ_STATS_SAMPLED_DEVICE
+        nws = (lib.smq_smaq_pack_workspace_bytes_sampled(numel, p.num_samples) if sampled
+               else lib.smq_smaq_pack_workspace_bytes(numel))
+        ws = N.workspace("smaq_pack", x.device, nws)
+        N.check(lib.smq_smaq_roundtrip_compress(x.data_ptr(), code, y.data_ptr(), numel, p,
+                                                out.data_ptr(), out.numel(), ws.data_ptr(),
+                                                ws.numel(), N.stream_ptr(x.device)),
+                "smq_smaq_roundtrip_compress")
+        del keep
+        return y, SmaqPacked(out, data.shape, numel,
+                             widths=(hp.num_bits_main, hp.num_bits_outlier))
+
     def _compress_f64(self, data, all_positive, batch_norm_stats, out):
         """float64 data: the fp64 chain (SmartFP._call_f64's) in a float64 stream."""
         hp = self.hparams

@@ -15,12 +15,12 @@ random stream (include/smq.h "Packed SmaQ container"). Inside ``with activations
 it again: the gradients equal those of the unpacked SmaQ run bit for bit, while a saved activation
 takes ~8 bits per element (6/8-bit codes) instead of 32.
 
-Memory without host synchronisation per call: the packer writes into a scratch stream of the
-worst-case size (``smq_smaq_pack_bound``, reused: one per device and stream), and the saved copy
-is a device-to-device copy of its first ``capacity`` bytes — the fixed region (known from n) plus
-room for every element being an outlier and 1 % escapes (``stream_capacity``). Only a stream larger
-than that (escape-heavy data) would be cut, so until its size is checked the saved ``y`` is kept
-too: checks run in batches — one host synchronisation reads every pending stream's size — when
+Memory without host synchronisation per call: ``y`` and its stream come from one call
+(``SmartFPPacked.roundtrip_compress``: SmartFP's round trip, then the packing launches on its
+statistics), the stream written straight into a buffer of ``capacity`` bytes — the fixed region
+(known from n) plus room for every element being an outlier and 1 % escapes (``stream_capacity``).
+Only a stream larger than that (escape-heavy data) does not fit, which its header records, so until
+its size is checked the saved ``y`` is kept too: checks run in batches — one host synchronisation reads every pending stream's size — when
 the pending ``y`` exceed ``verify_bytes`` (32 MiB: the memory the mode may hold beyond the streams)
 and when the context exits; a checked stream drops its
 ``y``, a cut one (never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
@@ -78,20 +78,12 @@ class PackedActivations:
         self._live: Dict[int, _Entry] = {}  # data_ptr of a forward output -> its stream
         self._pending: List[_Saved] = []     # saved, size not yet checked (y still held)
         self._pending_bytes = 0
-        self._scratch: Dict[tuple, torch.Tensor] = {}
         self._hooks = None
         self.saved_packed = 0    # saved tensors held as streams (since construction)
         self.saved_bytes = 0     # the distinct verified streams' bytes
         self.saved_capacity = 0  # and the bytes allocated for them
         self.saved_elements = 0  # and their elements
         self.kept_fp32 = 0       # streams cut at their capacity (the activation kept instead)
-
-    def _scratch_for(self, device: torch.device, nbytes: int) -> torch.Tensor:
-        key = (device.index, N.stream_ptr(device))
-        buf = self._scratch.get(key)
-        if buf is None or buf.numel() < nbytes:
-            buf = self._scratch[key] = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        return buf
 
     # -- the compress_fn of register_autograd_module ---------------------------------------------
     def __call__(self, x: torch.Tensor, tag: str = None, all_positive=False,
@@ -105,15 +97,12 @@ class PackedActivations:
         n = x.numel()
         bn = batch_norm_stats is not None and hp.use_batch_norm
         channels = (1 if hp.bn_scalar_params else x.shape[1]) if bn else 0
-        lib = N.lib()
-        bound = lib.smq_smaq_pack_bound_bn(n, hp.num_bits_main, hp.num_bits_outlier, channels)
-        scratch = self._scratch_for(x.device, bound)
-        full = codec.compress(x, all_positive, batch_norm_stats, out=scratch)
-        y = codec.decompress(full)
+        cap = stream_capacity(n, hp.num_bits_main, hp.num_bits_outlier, channels)
+        # y and its stream from one statistics pass, the stream straight into a buffer of the
+        # capacity (a stream that does not fit is flagged by its header: verify() keeps y then)
+        y, full = codec.roundtrip_compress(x, all_positive, batch_norm_stats, capacity=cap)
         codec.log_size(tag, n * 32, lambda: full.nbytes * 8)
-        cap = min(bound, stream_capacity(n, hp.num_bits_main, hp.num_bits_outlier, channels))
-        data = torch.empty(cap, dtype=torch.uint8, device=x.device)
-        data.copy_(scratch[:cap])  # stream order: before the next call reuses the scratch
+        data = full.data
         e = _Entry()
         key = y.data_ptr()
         e.ref = weakref.ref(y, lambda _r, k=key, d=self._live: d.pop(k, None))

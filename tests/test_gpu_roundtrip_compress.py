@@ -1,0 +1,156 @@
+"""smq_smaq_roundtrip_compress / SmartFPPacked.roundtrip_compress on the GPU: y and the stream of one
+call from one statistics pass.
+
+* y equals SmartFP(x) bit for bit (same flags, seed and stream position) and the stream equals
+  SmartFPPacked.compress(x)'s byte for byte — on the single-launch sizes (V = 1..8 groups per lane,
+  one workgroup, ragged tails) and the two-launch sizes above 8,388,611 elements, for fp32 and
+  half inputs, all_positive, the BN variant and sampled statistics;
+* decompress(stream) == y, and the random stream advances once per call (a second call equals the
+  second SmartFP call);
+* a buffer below the bound: the stream is written when it fits (bytes equal), and when it does not
+  the header's total_bytes exceeds the buffer and nothing is written past it.
+Reference: smart.py:110-190 (y), smart.py:184-188 / README.md:25-28 (the codes kept).
+"""
+
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import same_f32, smaq_hparams
+
+pytestmark = pytest.mark.gpu
+
+
+def _codecs(seed=7, offset=11, **over):
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+
+    hp = smaq_hparams(**over)
+    a, b, c = SmartFPPacked(hp), SmartFP(hp), SmartFPPacked(hp)
+    for k in (a, b, c):
+        k.rng.seed, k.rng.offset = seed, offset
+    return hp, a, b, c
+
+
+def _stream(p):
+    return p.data[:p.nbytes].cpu().numpy()
+
+
+SIZES = [5, 1000, 4097, 70_000, 1 << 20, 1_500_000, 2_500_001, 4 << 20, 6_500_000, 7 << 20,
+         8_388_608, 8_388_611, 9_000_003]
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_y_and_stream_equal_the_separate_calls(n):
+    hp, rc, ref, pk = _codecs()
+    gen = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(n, generator=gen, device="cuda") * 1.7 - 0.3
+    y, p = rc.roundtrip_compress(x)
+    y_ref = ref(x)
+    q = pk.compress(x)
+    y_dec = rc.decompress(p)
+    torch.cuda.synchronize()
+    assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
+    assert same_f32(y_dec.cpu().numpy(), y_ref.cpu().numpy())
+    a, b = _stream(p), _stream(q)
+    assert a.size == b.size and np.array_equal(a, b), int(np.argmax(a[:b.size] != b[:a.size]))
+    # the stream advanced once: the next call equals the next SmartFP call
+    y2, _ = rc.roundtrip_compress(x)
+    assert same_f32(y2.cpu().numpy(), ref(x).cpu().numpy())
+
+
+@pytest.mark.parametrize("case", ["all_positive", "trunc", "range", "sampled", "f16", "bf16",
+                                  "bits_4_6"])
+def test_variants(case):
+    over, dtype, ap = {}, torch.float32, False
+    if case == "all_positive":
+        ap = True
+    elif case == "trunc":
+        over["stochastic_rounding"] = False
+    elif case == "range":
+        over["use_range_std_dev"] = True
+    elif case == "sampled":
+        over.update(use_sample_stats=True, num_samples=64)
+    elif case in ("f16", "bf16"):
+        dtype = torch.float16 if case == "f16" else torch.bfloat16
+        over["precision"] = 16
+    elif case == "bits_4_6":
+        over.update(num_bits_main=4, num_bits_outlier=6)
+    hp, rc, ref, pk = _codecs(**over)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    for n in (300_001, 3 << 20, 9 << 20):
+        x = (torch.randn(n, generator=gen, device="cuda") * 2.0 + 0.25).to(dtype)
+        if ap:
+            x = torch.relu(x)
+        y, p = rc.roundtrip_compress(x, all_positive=ap)
+        y_ref = ref(x, all_positive=ap)
+        q = pk.compress(x, all_positive=ap)
+        torch.cuda.synchronize()
+        assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), (case, n)
+        assert same_f32(rc.decompress(p).cpu().numpy(), y_ref.cpu().numpy()), (case, n)
+        a, b = _stream(p), _stream(q)
+        assert np.array_equal(a, b), (case, n)
+
+
+def test_batch_norm_variant():
+    hp, rc, ref, pk = _codecs(use_batch_norm=True)
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(32, 24, 20, 20, generator=gen, device="cuda") * 1.5
+    g = torch.rand(24, generator=gen, device="cuda") + 0.5
+    b = torch.randn(24, generator=gen, device="cuda") * 0.1
+    y, p = rc.roundtrip_compress(x, batch_norm_stats=(g, b))
+    y_ref = ref(x, batch_norm_stats=(g, b))
+    q = pk.compress(x, batch_norm_stats=(g, b))
+    torch.cuda.synchronize()
+    assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
+    assert np.array_equal(_stream(p), _stream(q))
+    assert same_f32(rc.decompress(p).cpu().numpy(), y_ref.cpu().numpy())
+
+
+def _raw_call(x, n, cap, guard=4096):
+    """The C-ABI with a buffer of cap bytes followed by a guard region of 0xAB bytes."""
+    from smart_compress_amd import _native as N
+
+    hp, rc, _, _ = _codecs()
+    lib = N.lib()
+    p = rc._params(n, False, torch.float32, x.device)
+    buf = torch.full((cap + guard,), 0xAB, dtype=torch.uint8, device="cuda")
+    y = torch.empty(n, device="cuda")
+    ws = torch.empty(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    rc_ = lib.smq_smaq_roundtrip_compress(x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p,
+                                          buf.data_ptr(), cap, ws.data_ptr(), ws.numel(),
+                                          N.stream_ptr(x.device))
+    torch.cuda.synchronize()
+    hdr = N.SmqPackedHeader.from_buffer_copy(bytes(buf[:128].cpu().numpy()))
+    return rc_, buf.cpu().numpy(), hdr, y
+
+
+def test_capacity_bounded_buffer():
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    n = 1_000_003
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.randn(n, generator=gen, device="cuda")
+    bound = lib.smq_smaq_pack_bound(n, 6, 8)
+    rc0, full, hdr0, y0 = _raw_call(x, n, bound, 0)
+    assert rc0 == 0
+    total = int(hdr0.total_bytes)
+    fixed = lib.smq_smaq_pack_fixed_bytes(n, 6)
+    assert fixed < total < bound
+    # exactly the stream's size: the same bytes
+    rc1, b1, hdr1, y1 = _raw_call(x, n, total)
+    assert rc1 == 0 and int(hdr1.total_bytes) == total
+    assert np.array_equal(b1[:total], full[:total]) and (b1[total:] == 0xAB).all()
+    assert same_f32(y1.cpu().numpy(), y0.cpu().numpy())
+    # too small: flagged by total_bytes, nothing written past the buffer, y still complete
+    small = fixed + (total - fixed) // 3
+    rc2, b2, hdr2, y2 = _raw_call(x, n, small)
+    assert rc2 == 0 and int(hdr2.total_bytes) == total > small
+    assert (b2[small:] == 0xAB).all()
+    assert np.array_equal(b2[:fixed], full[:fixed])
+    assert same_f32(y2.cpu().numpy(), y0.cpu().numpy())
+    # below the fixed part: refused
+    rc3, _, _, _ = _raw_call(x, n, fixed - 8)
+    assert rc3 == -2  # SMQ_ERR_WORKSPACE
+    assert b"smq_smaq_pack_fixed_bytes" in lib.smq_last_error()

@@ -1,0 +1,125 @@
+"""Where a ResNet-34 / CIFAR b128 step with PackedActivations spends its time (measurement script,
+not product): ms/step of SmartFP eager and of PackedActivations with the default verify budget and
+with verification only at context exit (no host synchronisation inside the forward), each
+interleaved over rounds; then the host time of one forward without the GPU waiting (the forward
+enqueued behind 100 large GEMMs, synchronised afterwards) and a cProfile of the packed steps.
+
+python tools/saved_ab.py [rounds]"""
+
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "smart-quantization_amd"), os.path.join(REPO, "tests")]
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+from argparse import Namespace  # noqa: E402
+
+import bench  # noqa: E402
+from helpers import smaq_hparams  # noqa: E402
+from smart_compress_amd.compress.packed import SmartFPPacked  # noqa: E402
+from smart_compress_amd.compress.smart import SmartFP  # noqa: E402
+from smart_compress_amd.util.pytorch.autograd import register_autograd_module  # noqa: E402
+from smart_compress_amd.util.pytorch.saved import PackedActivations  # noqa: E402
+
+dev = torch.device("cuda", 0)
+flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
+
+
+def build(kind):
+    torch.manual_seed(0)
+    net = bench._ResNet().to(dev)
+    opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9)
+    acts = None
+    if kind == "smartfp":
+        codec = SmartFP(smaq_hparams())
+        register_autograd_module(net, codec, flags)
+    else:
+        codec = SmartFPPacked(smaq_hparams())
+        acts = PackedActivations(codec, verify_bytes=(32 << 20) if kind == "packed32M" else (1 << 40))
+        register_autograd_module(net, acts, flags)
+    return net, opt, acts
+
+
+x = torch.randn(128, 3, 32, 32, device=dev)
+t = torch.randint(0, 10, (128,), device=dev)
+
+
+def make_step(net, opt, acts):
+    def fwd():
+        if acts is None:
+            return F.cross_entropy(net(x), t)
+        with acts:
+            return F.cross_entropy(net(x), t)
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        loss = fwd()
+        loss.backward()
+        opt.step()
+    return step, fwd
+
+
+def timed(step, k=20):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / k * 1e3
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    kinds = ["smartfp", "packed32M", "packed_exit"]
+    global busy
+    busy = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    built = {k: build(k) for k in kinds}
+    steps = {k: make_step(*built[k]) for k in kinds}
+    for k in kinds:
+        for _ in range(3):
+            steps[k][0]()
+    res = {k: [] for k in kinds}
+    for _ in range(rounds):
+        for k in kinds:
+            res[k].append(round(timed(steps[k][0]), 3))
+    print("ms/step", res, flush=True)
+    # host time of one forward with the device busy: the enqueue cost alone (no sync inside for
+    # packed_exit; packed32M's verify syncs stall on the busy kernel and are excluded by using
+    # packed_exit)
+    for k in ("smartfp", "packed_exit"):
+        step, fwd = steps[k]
+        hs = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            for _ in range(100):  # tens of ms of device busy time ahead of the forward
+                busy @ busy
+            acts = built[k][2]
+            if acts is not None:
+                acts.__enter__()
+            t0 = time.perf_counter()
+            loss = F.cross_entropy(built[k][0](x), t)
+            hs.append((time.perf_counter() - t0) * 1e3)  # before the context's exit verify
+            if acts is not None:
+                acts.__exit__(None, None, None)
+            torch.cuda.synchronize()
+            loss.backward()
+            torch.cuda.synchronize()
+        print(f"host forward ms ({k}, device busy):", [round(v, 3) for v in hs], flush=True)
+    acts = built["packed32M"][2]
+    print("packed32M stats", acts.stats(), flush=True)
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(3):
+        steps["packed32M"][0]()
+    torch.cuda.synchronize()
+    pr.disable()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(22)
+
+
+if __name__ == "__main__":
+    main()
