@@ -20,21 +20,25 @@ Memory without host synchronisation per call: ``y`` and its stream come from one
 statistics), the stream written straight into a buffer of ``capacity`` bytes — the fixed region
 (known from n) plus room for every element being an outlier and 1 % escapes (``stream_capacity``).
 Only a stream larger than that (escape-heavy data) does not fit, which its header records, so until
-its size is checked the saved ``y`` is kept too: checks run in batches — one host synchronisation reads every pending stream's size — when
-the pending ``y`` exceed ``verify_bytes`` (32 MiB: the memory the mode may hold beyond the streams)
-and when the context exits; a checked stream drops its
-``y``, a cut one (never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
-Backward-direction calls (grad-maps, never saved) and calls outside the context run as the plain
-codec call.
+its size is checked the saved ``y`` is kept too. The sizes travel to the host without a
+synchronisation (a device gather, an asynchronous copy to pinned memory, an event), in batches
+of ``verify_bytes`` (32 MiB) of pending ``y``; a batch whose sizes have arrived drops the ``y`` of
+every stream that fit, and the host waits (for the oldest batch's event only) when more than
+``verify_bytes`` are still on their way, and at the context's exit. A stream that did not fit
+(never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
+Backward-direction calls (grad-maps, never saved) and calls outside the context run as SmartFP's
+own call (the same values as the codec's decompress(compress(x)), one launch instead of five).
 """
 
 import weakref
-from typing import Dict, List, Optional
+from collections import deque
+from typing import Deque, Dict, List, Optional
 
 import torch
 
 from ... import _native as N
 from ...compress.packed import SmaqPacked, SmartFPPacked, _HDR_BYTES, _TOTAL_OFF
+from ...compress.smart import SmartFP
 
 __all__ = ["PackedActivations", "stream_capacity"]
 
@@ -78,6 +82,9 @@ class PackedActivations:
         self._live: Dict[int, _Entry] = {}  # data_ptr of a forward output -> its stream
         self._pending: List[_Saved] = []     # saved, size not yet checked (y still held)
         self._pending_bytes = 0
+        # batches whose sizes are on their way to the host: (event, pinned sizes, handles, bytes)
+        self._inflight: Deque[tuple] = deque()
+        self._inflight_bytes = 0
         self._hooks = None
         self.saved_packed = 0    # saved tensors held as streams (since construction)
         self.saved_bytes = 0     # the distinct verified streams' bytes
@@ -92,8 +99,10 @@ class PackedActivations:
         hp = codec.hparams
         if (self._hooks is None or tag != FORWARD_TAG or x.numel() < hp.min_size
                 or not x.is_cuda or x.dtype == torch.float64):
-            return codec(x, tag=tag, all_positive=all_positive, batch_norm_stats=batch_norm_stats,
-                         **kw)
+            # a value nobody keeps as a stream (a grad-map, a call outside the context): SmartFP's
+            # own call (one launch up to 8.4M elements), the values decompress(compress(x)) has
+            return SmartFP.__call__(codec, x, tag=tag, all_positive=all_positive,
+                                    batch_norm_stats=batch_norm_stats, **kw)
         n = x.numel()
         bn = batch_norm_stats is not None and hp.use_batch_norm
         channels = (1 if hp.bn_scalar_params else x.shape[1]) if bn else 0
@@ -135,7 +144,10 @@ class PackedActivations:
         self._pending.append(h)
         self._pending_bytes += 4 * y.numel()
         if self._pending_bytes > self.verify_bytes:
-            self.verify()
+            self._request_sizes()
+            # the batches whose sizes have arrived drop their activations; more than the budget
+            # still in flight: wait for the oldest batch only (its work is usually done by then)
+            self._harvest(self.verify_bytes)
         return h
 
     @staticmethod
@@ -147,25 +159,49 @@ class PackedActivations:
         return h
 
     def verify(self) -> None:
-        """Check every pending stream's size against its capacity: one host synchronisation
-        (every header's total_bytes in one copy); a stream that fits drops its activation."""
+        """Check every pending stream's size against its capacity (waiting for the sizes still on
+        their way); a stream that fits drops its activation, one that does not keeps it."""
+        self._request_sizes()
+        self._harvest(0)
+
+    def _request_sizes(self) -> None:
+        """Every pending stream's header total_bytes, gathered on the device and copied to pinned
+        host memory without synchronising; an event marks when they are there."""
         hs = self._pending
         if not hs:
             return
-        sizes = torch.cat([h.packed.data[_TOTAL_OFF:_TOTAL_OFF + 8] for h in hs]).cpu()
-        for h, total in zip(hs, sizes.view(torch.int64).tolist()):
-            cap = h.packed.data.numel()
-            if total <= cap:
-                h.packed._total = int(total)
-                h.y = None
-                self.saved_bytes += int(total)
-                self.saved_capacity += cap
-                self.saved_elements += h.packed.n
-            else:
-                h.packed = None
-                self.kept_fp32 += 1
+        sizes = torch.cat([h.packed.data[_TOTAL_OFF:_TOTAL_OFF + 8] for h in hs])
+        host = torch.empty(sizes.numel(), dtype=torch.uint8, pin_memory=True)
+        host.copy_(sizes, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(sizes.device))
+        self._inflight.append((ev, host, hs, self._pending_bytes))
+        self._inflight_bytes += self._pending_bytes
         self._pending = []
         self._pending_bytes = 0
+
+    def _harvest(self, max_inflight_bytes: int) -> None:
+        """Finish the batches whose sizes have arrived, oldest first; wait for the oldest while
+        more than max_inflight_bytes of activations still wait on theirs."""
+        while self._inflight:
+            ev, host, hs, nbytes = self._inflight[0]
+            if not ev.query():
+                if self._inflight_bytes <= max_inflight_bytes:
+                    return
+                ev.synchronize()
+            self._inflight.popleft()
+            self._inflight_bytes -= nbytes
+            for h, total in zip(hs, host.view(torch.int64).tolist()):
+                cap = h.packed.data.numel()
+                if total <= cap:
+                    h.packed._total = int(total)
+                    h.y = None
+                    self.saved_bytes += int(total)
+                    self.saved_capacity += cap
+                    self.saved_elements += h.packed.n
+                else:  # did not fit its capacity: the activation stays the saved value
+                    h.packed = None
+                    self.kept_fp32 += 1
 
     def __enter__(self):
         self._hooks = torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack)
