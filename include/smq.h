@@ -570,6 +570,15 @@ size_t smq_smaq_pack_fixed_bytes(int64_t n, int num_bits_main);
 int smq_smaq_roundtrip_compress(const void* x, int dtype, float* y, int64_t n,
                                 const SmqSmaqParams* params, void* packed, size_t packed_bytes,
                                 void* workspace, size_t workspace_bytes, void* stream);
+/* The same with the packing launches on pack_stream (NULL or == stream: one stream): they wait for
+ * stream's statistics by an event and then overlap what the caller enqueues on stream next (y is
+ * ready on stream as usual). The caller orders every reader of the stream after pack_stream and
+ * keeps x, packed and the workspace alive (and the workspace unused by other calls) until
+ * pack_stream has passed them. */
+int smq_smaq_roundtrip_compress_ex(const void* x, int dtype, float* y, int64_t n,
+                                   const SmqSmaqParams* params, void* packed, size_t packed_bytes,
+                                   void* workspace, size_t workspace_bytes, void* stream,
+                                   void* pack_stream);
 /* Decode a stream of n elements into y (fp32). n must equal the header's n (a stream with another
  * n or a bad magic leaves y untouched). */
 int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream);

@@ -556,14 +556,18 @@ __device__ void write_header(const PackArgs& A, uint64_t carry, int tid, int nth
 }
 
 // The variable section of block b re-coded from x straight to the stream at var_dst (a block
-// whose section outgrew its scratch slot: more than ~kVarCap / 2 escapes). A rare path built for a
-// small register footprint, so the common copy path of smaq_pack_var_kernel keeps its occupancy:
-// 16 passes of 256 consecutive elements, one per thread; outlier and escape ranks by wave ballots
-// and the passes' running totals; the outlier bits are ORed into LDS (ext, 128 * we words) and
-// copied out at the end, the escapes are written directly.
+// whose section outgrew its scratch slot: more than kSegEsc escapes in a 256-element segment, as
+// real activations give when a channel sits far from the tensor's mean). One pass with every load
+// in flight at once: thread t codes elements 256 j + t (j = 0..15, element order = (j, t)) into
+// registers, one ballot pair per j counts each wave's outliers and escapes, wave 0 scans the 64
+// (j, wave) counts, and every element is placed at its rank: outlier bits ORed into LDS (ext,
+// 128 * we words, copied out at the end), escapes written directly. Two barriers per block where
+// the round-4 form (two sweeps of 16 dependent load/ballot/barrier steps) took 30-60 us.
 template <int RM, int TIN, bool EXT>
 __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_dst, uint32_t* ext,
                                    uint32_t* s_cnt) {
+  constexpr int J = kPB / kBlock;  // 16 elements per thread
+  static_assert(J * (kBlock / kWave) == kWave, "one (j, wave) count per lane of the scan");
   const int wm = A.wm, wo = A.wo, we = wo > wm ? wo - wm : 0;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int64_t e0 = (int64_t)b * kPB;
@@ -571,55 +575,60 @@ __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_d
   ElemConsts c;
   init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, pack_cthr<TIN>(A));
   const uint32_t hm = 1u << (wm - 1), side = 1u << (wo - 1);
-  for (uint32_t i = tid; i < 128u * (uint32_t)we; i += kBlock) ext[i] = 0u;
-  __syncthreads();
-  // pass 0 counts the block's outliers (its escapes follow the outlier bits: ext_words(we, n_out)
-  // words); pass 1 places the outlier bits and writes the escapes
-  uint32_t n_out = 0u;
-#pragma unroll 1
-  for (int pass = we > 0 ? 0 : 1; pass < 2; ++pass) {
-    uint32_t r_out = 0u, r_esc = 0u;
-    uint32_t* out = A.var + var_dst + ext_words(we, n_out);
-#pragma unroll 1
-    for (int j = 0; j < kPB / kBlock; ++j) {
-      const int el = j * kBlock + tid;
-      bool o = false, lo = false, esc = false;
-      float q = 0.0f;
-      uint32_t code = 0u;
-      if (el < n_el) {
-        const float u = (RM == kRoundHash) ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)(e0 + el)) : 0.0f;
-        q = EXT ? ext_quant<RM, TIN, true>(A, load1<TIN>(A.x, e0 + el), u, c, e0 + el, o, lo)
-                : pack_quant<RM, TIN, true>(load1<TIN>(A.x, e0 + el), u, c, o, lo);
-        code = code_sel(q, o, lo, hm, side, 2u * hm, esc);
-      }
-      const unsigned long long bo = __ballot(o), be = __ballot(esc);
-      const uint32_t ro = __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u));
-      const uint32_t re = __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
-      if (lane == 0) s_cnt[w] = (uint32_t)__popcll(bo) | ((uint32_t)__popcll(be) << 16);
-      __syncthreads();
-      uint32_t before = 0u, tot = 0u;
+  float xv[J];
 #pragma unroll
-      for (int v = 0; v < kBlock / kWave; ++v) {
-        const uint32_t t = s_cnt[v];
-        before += v < w ? t : 0u;
-        tot += t;
-      }
-      __syncthreads();
-      if (pass == 1) {
-        const uint32_t ko = r_out + (before & 0xffffu) + ro, ke = r_esc + (before >> 16) + re;
-        if (o && we > 0) or_bits32(ext, (uint32_t)we * ko, code >> wm);  // we <= 23 bits
-        if (esc) {
-          out[2u * ke] = (uint32_t)el;
-          out[2u * ke + 1u] = q == q ? __float_as_uint(q) : 0x7fc00000u;
-        }
-      }
-      r_out += tot & 0xffffu;
-      r_esc += tot >> 16;
+  for (int j = 0; j < J; ++j) {
+    const int el = j * kBlock + tid;
+    xv[j] = el < n_el ? load1<TIN>(A.x, e0 + el) : 0.0f;
+  }
+  for (uint32_t i = tid; i < 128u * (uint32_t)we; i += kBlock) ext[i] = 0u;
+  uint32_t hib[J], qb[J], om = 0u, emk = 0u;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int el = j * kBlock + tid;
+    bool o = false, lo = false, esc = false;
+    float q = 0.0f;
+    uint32_t code = 0u;
+    if (el < n_el) {
+      const float u = (RM == kRoundHash) ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)(e0 + el)) : 0.0f;
+      q = EXT ? ext_quant<RM, TIN, true>(A, xv[j], u, c, e0 + el, o, lo)
+              : pack_quant<RM, TIN, true>(xv[j], u, c, o, lo);
+      code = code_sel(q, o, lo, hm, side, 2u * hm, esc);
     }
-    n_out = r_out;
+    hib[j] = code >> wm;
+    qb[j] = q == q ? __float_as_uint(q) : 0x7fc00000u;  // one NaN pattern
+    om |= o ? 1u << j : 0u;
+    emk |= esc ? 1u << j : 0u;
+    const unsigned long long bo = __ballot(o), be = __ballot(esc);
+    if (lane == 0) s_cnt[j * (kBlock / kWave) + w] = (uint32_t)__popcll(bo) | ((uint32_t)__popcll(be) << 16);
   }
   __syncthreads();
+  if (w == 0) {  // (j, wave) counts in element order -> exclusive bases
+    const uint32_t v = s_cnt[lane];
+    const uint32_t inc = wave_incl_scan_u32(v);
+    s_cnt[kWave + lane] = inc - v;
+    if (lane == kWave - 1) s_cnt[2 * kWave] = inc;
+  }
+  __syncthreads();
+  const uint32_t n_out = s_cnt[2 * kWave] & 0xffffu;
   uint32_t* out = A.var + var_dst;
+  uint32_t* eout = out + ext_words(we, n_out);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const bool o = (om >> j) & 1u, esc = (emk >> j) & 1u;
+    const unsigned long long bo = __ballot(o), be = __ballot(esc);
+    const uint32_t base = s_cnt[kWave + j * (kBlock / kWave) + w];
+    if (o && we > 0) {
+      const uint32_t ro = __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u));
+      or_bits32(ext, (uint32_t)we * ((base & 0xffffu) + ro), hib[j]);  // we <= 23 bits
+    }
+    if (esc) {
+      const uint32_t k = (base >> 16) + __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
+      eout[2u * k] = (uint32_t)(j * kBlock + tid);
+      eout[2u * k + 1u] = qb[j];
+    }
+  }
+  __syncthreads();
   for (uint32_t i = tid; i < ext_words(we, n_out); i += kBlock) out[i] = ext[i];
 }
 
@@ -706,7 +715,7 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_var_kernel(PackArgs A, uint3
 // sizes of the group's blocks before it (from meta).
 template <int RM, int TIN, bool EXT>
 __device__ void pack_recode_blocks(const PackArgs& A, uint32_t wg, uint32_t per, uint32_t* lds) {
-  __shared__ uint32_t s_cnt[kBlock / kWave];
+  __shared__ uint32_t s_cnt[2 * kWave + 1];
   __shared__ uint32_t list[kBlock];
   __shared__ uint32_t n_list;
   __shared__ uint64_t s_dst;
@@ -1346,12 +1355,27 @@ int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* 
 
 }  // extern "C"
 
+// An event to order a second stream after the first (a small per-thread ring: a wait enqueued on
+// the second stream captures the event's state at that moment, so the event is free to be recorded
+// again by a later call).
+static hipEvent_t fork_event() {
+  constexpr int kRing = 16;
+  thread_local hipEvent_t ring[kRing] = {};
+  thread_local int next = 0;
+  hipEvent_t& e = ring[next];
+  next = (next + 1) % kRing;
+  if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+  return e;
+}
+
 // smq_smaq_compress_ex (y == NULL: the statistics launch first) and smq_smaq_roundtrip_compress
 // (y != NULL: SmartFP's round trip into y first, whose statistics record the packer then reads;
 // packed_bytes may be below the bound, down to the stream's fixed part).
+// pst: the stream of the packing launches (NULL: st); a different one waits for st's statistics by
+// an event (smq_smaq_roundtrip_compress_ex).
 static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, float* y,
                          void* packed, size_t packed_bytes, void* ws, size_t ws_bytes,
-                         hipStream_t st) {
+                         hipStream_t st, hipStream_t pst = nullptr) {
   int rc = smaq_validate(p, dtype);
   if (rc) return rc;
   if (n < 1 || !x || !packed) {
@@ -1459,6 +1483,14 @@ static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParam
   const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
   const bool sr = p->stochastic_rounding != 0;
   if (!zeroed) fill_async(A.gsum, 0u, A.n_groups, st);  // (sampled statistics: smq_common.h)
+  if (pst && pst != st) {  // the packing launches on their own stream, behind the statistics
+    const hipEvent_t ev = fork_event();
+    if (!ev || hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(pst, ev, 0) != hipSuccess) {
+      set_error("roundtrip_compress: cannot order the pack stream after the statistics");
+      return SMQ_ERR_LAUNCH;
+    }
+    st = pst;
+  }
   if (dtype == SMQ_DTYPE_F32) {
     if (sr) launch_pack<kRoundHash, kF32>(A, vec, ext, st);
     else launch_pack<kRoundTrunc, kF32>(A, vec, ext, st);
@@ -1499,6 +1531,17 @@ int smq_smaq_roundtrip_compress(const void* x, int dtype, float* y, int64_t n,
   }
   return compress_impl(x, dtype, n, p, y, packed, packed_bytes, ws, ws_bytes,
                        (hipStream_t)stream);
+}
+
+int smq_smaq_roundtrip_compress_ex(const void* x, int dtype, float* y, int64_t n,
+                                   const SmqSmaqParams* p, void* packed, size_t packed_bytes,
+                                   void* ws, size_t ws_bytes, void* stream, void* pack_stream) {
+  if (!y) {
+    set_error("roundtrip_compress: y must be a device pointer");
+    return SMQ_ERR_INVALID;
+  }
+  return compress_impl(x, dtype, n, p, y, packed, packed_bytes, ws, ws_bytes,
+                       (hipStream_t)stream, (hipStream_t)pack_stream);
 }
 
 static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int bo, void* stream) {

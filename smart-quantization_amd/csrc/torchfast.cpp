@@ -15,6 +15,8 @@
 //   smaq_autograd(state, x, codec, bwd)     Compressor.forward for a SmartFP codec: the forward
 //                                           call plus a C++ Node whose backward compresses the
 //                                           grad-map the same way (autograd.py:37-47)
+//   smaq_packed(state, x, ap, getter, frac) PackedActivations' forward call: y and its SmaQ stream
+//                                           (smq_smaq_roundtrip_compress, util/pytorch/saved.py)
 //   s2fp8(x, check_inf, rng, getter)        one S2FP8 call on an fp32 device tensor
 //
 // The state object (a capsule of a shared SmaqState) holds the flag templates of the parameter
@@ -134,6 +136,7 @@ struct SmaqState {
   PyRef rng_dict;          // codec.rng.__dict__
   PyRef ws_getter;
   WsSlot ws;
+  WsSlot pws;  // the packed codec's workspace (smaq_packed)
 };
 using StatePtr = std::shared_ptr<SmaqState>;
 
@@ -253,6 +256,79 @@ PyObject* smaq(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
     case kStale: Py_RETURN_NOTIMPLEMENTED;
     default: return nullptr;
   }
+}
+
+// Bytes of a stream of n elements with every element an outlier and escape_frac of them escaped
+// (util/pytorch/saved.py stream_capacity, the same integer arithmetic).
+size_t stream_capacity(int64_t n, int bm, int bo, double escape_frac) {
+  const int64_t nb = (n + SMQ_PACK_BLOCK - 1) / SMQ_PACK_BLOCK;
+  const int64_t wm = bm - 1, wo = bo - 1, we = wo > wm ? wo - wm : 0;
+  const int64_t fixed_words = 128 + 128 * wm;
+  const int64_t var_words = (we * n + 31) / 32 + nb + 2 * ((int64_t)(escape_frac * (double)n) + nb);
+  return (size_t)((int64_t)sizeof(SmqPackedHeader) + 8 * (nb + (nb & 1)) +
+                  4 * (nb * fixed_words + var_words));
+}
+
+// smaq_packed(state, x, all_positive, pack_ws_getter, escape_frac) -> (y, stream) | None |
+// NotImplemented: PackedActivations' forward call (util/pytorch/saved.py) in one C call — y as
+// smaq() returns it and its stream (smq_smaq_roundtrip_compress) in a new buffer of
+// stream_capacity bytes. The same declines as smaq().
+PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
+  if (nargs != 5) {
+    PyErr_SetString(PyExc_TypeError, "smaq_packed(state, x, all_positive, getter, escape_frac)");
+    return nullptr;
+  }
+  StatePtr* sp = state_of(a[0]);
+  if (!sp) return nullptr;
+  SmaqState& s = **sp;
+  if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
+  const int ap = PyObject_IsTrue(a[2]);
+  if (ap < 0) return nullptr;
+  const double frac = PyFloat_AsDouble(a[4]);
+  if (frac == -1.0 && PyErr_Occurred()) return nullptr;
+  for (int i = 0; i < kSnap; ++i)
+    if (PyDict_GetItem(s.hp_dict.o, g_snap_keys[i]) != s.snap[i].o) Py_RETURN_NOTIMPLEMENTED;
+  const at::Tensor& t = THPVariable_Unpack(a[1]);
+  if (s.decline || !t.is_cuda()) Py_RETURN_NONE;
+  int code;
+  switch (t.scalar_type()) {
+    case at::kFloat: code = SMQ_DTYPE_F32; break;
+    case at::kBFloat16: code = SMQ_DTYPE_BF16; break;
+    case at::kHalf:
+      if (!s.allow_f16) Py_RETURN_NONE;
+      code = SMQ_DTYPE_F16;
+      break;
+    default: Py_RETURN_NONE;
+  }
+  const int64_t n = t.numel();
+  if (n < s.min_size) Py_RETURN_NONE;
+  at::Tensor x = t.is_contiguous() ? t : t.detach().contiguous();
+  const int dev = x.get_device();
+  const hipStream_t st = c10::hip::getCurrentHIPStream(dev).stream();
+  if (!ws_lookup(s.pws, a[3], dev, st, smq_smaq_pack_workspace_bytes(n))) return nullptr;
+  SmqSmaqParams p = s.tmpl[ap ? 1 : 0];
+  const size_t cap = stream_capacity(n, p.num_bits_main, p.num_bits_outlier, frac);
+  if (!rng_take(s.rng_dict.o, (uint64_t)n, &p.seed, &p.offset)) return nullptr;
+  at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kFloat));
+  at::Tensor data = at::empty({(int64_t)cap}, x.options().dtype(at::kByte));
+  const int rc = smq_smaq_roundtrip_compress(x.const_data_ptr(), code, y.mutable_data_ptr<float>(),
+                                             n, &p, data.mutable_data_ptr(), cap, s.pws.ptr,
+                                             s.pws.bytes, st);
+  if (rc) {
+    PyErr_Format(PyExc_RuntimeError, "smq_smaq_roundtrip_compress failed (rc=%d): %s", rc,
+                 smq_last_error());
+    return nullptr;
+  }
+  PyObject* yo = THPVariable_Wrap(std::move(y));
+  PyObject* dobj = yo ? THPVariable_Wrap(std::move(data)) : nullptr;
+  if (!dobj) {
+    Py_XDECREF(yo);
+    return nullptr;
+  }
+  PyObject* r = PyTuple_Pack(2, yo, dobj);
+  Py_DECREF(yo);
+  Py_DECREF(dobj);
+  return r;
 }
 
 // ---- the autograd wrapper (autograd.py:18-47: Compressor with a SmartFP compress_fn) -----------
@@ -390,6 +466,8 @@ PyMethodDef kMethods[] = {
     {"smaq_autograd",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_autograd)), METH_FASTCALL,
      "Compressor.forward with a SmartFP codec: y and its SmaqCompressBackward node"},
+    {"smaq_packed", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_packed)),
+     METH_FASTCALL, "PackedActivations' forward call: (y, stream) (smq_smaq_roundtrip_compress)"},
     {"s2fp8", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(s2fp8)), METH_FASTCALL,
      "one eager S2FP8 call on an fp32 device tensor (smq_s2fp8_roundtrip), or None"},
     {nullptr, nullptr, 0, nullptr}};

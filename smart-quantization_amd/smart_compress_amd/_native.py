@@ -282,6 +282,8 @@ SIGNATURES = {
     "smq_smaq_pack_fixed_bytes": (_SZ, [_I64, _I32]),
     "smq_smaq_roundtrip_compress": (_I32, [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams),
                                            _P, _SZ, _P, _SZ, _P]),
+    "smq_smaq_roundtrip_compress_ex": (_I32, [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams),
+                                              _P, _SZ, _P, _SZ, _P, _P]),
     "smq_smaq_pack_workspace_bytes_sampled": (_SZ, [_I64, _I64]),
     "smq_cpu_smaq_compress": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P,
                                      _SZ, _I32]),

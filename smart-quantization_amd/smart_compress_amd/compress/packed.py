@@ -160,13 +160,19 @@ class SmartFPPacked(SmartFP):
 
     def roundtrip_compress(self, data: torch.Tensor, all_positive: bool = False,
                            batch_norm_stats: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                           capacity: Optional[int] = None) -> Tuple[torch.Tensor, SmaqPacked]:
+                           capacity: Optional[int] = None, pack_stream=None,
+                           workspace: Optional[torch.Tensor] = None
+                           ) -> Tuple[torch.Tensor, SmaqPacked]:
         """``(y, p)``: ``y`` what ``SmartFP`` returns for ``data`` (smart.py:110-190) and ``p`` its
         stream — ``decompress(p) == y`` bit for bit — from one statistics pass
         (``smq_smaq_roundtrip_compress``: the round trip, then the packing launches on its
         statistics; no decode to get ``y``). ``capacity``: bytes of the stream buffer (default
         ``smq_smaq_pack_bound``); a smaller one holds the stream when it fits, which
         ``p.nbytes <= capacity`` tells (a stream that did not fit must not be decoded).
+        ``pack_stream``: a torch stream for the packing launches (they wait for the statistics
+        on the current stream, then overlap what follows it; ``smq_smaq_roundtrip_compress_ex``) —
+        the caller then orders readers of the stream after it and passes a ``workspace`` (uint8,
+        ``smq_smaq_pack_workspace_bytes``) no other call uses until ``pack_stream`` has passed.
         CPU and float64 tensors: ``compress`` then ``decompress`` (the same values)."""
         hp = self.hparams
         numel = data.numel()
@@ -196,11 +202,15 @@ class SmartFPPacked(SmartFP):
         sampled = p.stats_source == N.SMQ_STATS_SAMPLED_DEVICE
         nws = (lib.smq_smaq_pack_workspace_bytes_sampled(numel, p.num_samples) if sampled
                else lib.smq_smaq_pack_workspace_bytes(numel))
-        ws = N.workspace("smaq_pack", x.device, nws)
-        N.check(lib.smq_smaq_roundtrip_compress(x.data_ptr(), code, y.data_ptr(), numel, p,
-                                                out.data_ptr(), out.numel(), ws.data_ptr(),
-                                                ws.numel(), N.stream_ptr(x.device)),
-                "smq_smaq_roundtrip_compress")
+        ws = N.workspace("smaq_pack", x.device, nws) if workspace is None else workspace
+        N.check(lib.smq_smaq_roundtrip_compress_ex(
+            x.data_ptr(), code, y.data_ptr(), numel, p, out.data_ptr(), out.numel(),
+            ws.data_ptr(), ws.numel(), N.stream_ptr(x.device),
+            None if pack_stream is None else pack_stream.cuda_stream),
+            "smq_smaq_roundtrip_compress_ex")
+        if pack_stream is not None:  # read there: not reused before pack_stream has passed
+            for t in (x, out) + (tuple(keep) if keep is not None else ()):
+                t.record_stream(pack_stream)
         del keep
         return y, SmaqPacked(out, data.shape, numel,
                              widths=(hp.num_bits_main, hp.num_bits_outlier))
@@ -291,3 +301,8 @@ class SmartFPPacked(SmartFP):
             # the real stream size, read (one synchronisation) only if the ratio is measured
             self.log_size(tag, numel * 32, lambda: packed.nbytes * 8)
             return y
+
+    # __call__ returns SmartFP's values for the same flags and random stream; only its log_size
+    # differs (the real stream size), and the C hot path declines calls that log: SmartFP's C path
+    # (the single launch, its autograd node) serves this codec as well
+    _smartfp_call = __call__

@@ -256,8 +256,9 @@ class SmartFP(CompressionAlgorithmBase):
         hp = self.hparams
         d = hp if isinstance(hp, dict) else getattr(hp, "__dict__", None)
         hot = False
+        call = type(self).__call__
         if (T is not None and not self._graph_safe and type(d) is dict
-                and type(self).__call__ is SmartFP.__call__):
+                and (call is SmartFP.__call__ or call is getattr(type(self), "_smartfp_call", None))):
             hot = T.smaq_state(bytes(self._flag_params(False)), bytes(self._flag_params(True)),
                                d, self.rng.__dict__, N.ws_getter("smaq"))
         object.__setattr__(self, "_hot", hot)

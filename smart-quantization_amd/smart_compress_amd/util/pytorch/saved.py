@@ -26,6 +26,14 @@ of ``verify_bytes`` (32 MiB) of pending ``y``; a batch whose sizes have arrived 
 every stream that fit, and the host waits (for the oldest batch's event only) when more than
 ``verify_bytes`` are still on their way, and at the context's exit. A stream that did not fit
 (never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
+The forward call is one C call where it applies (csrc/torchfast.cpp ``smaq_packed``: SmartFP's
+parameter template, the output allocations and ``smq_smaq_roundtrip_compress``). Overlap
+(opt-in, ``overlap=True``): the packing launches of a forward call run on a side stream — they
+wait for the call's statistics by an event and then run beside the next layers, each call with
+one of a ring of workspaces the current stream waits for before reusing; backward (and the size
+checks) are ordered after the side stream. It costs ~20 us of host time per call (events, stream
+waits, record_stream), which an eager ResNet-34 step cannot spare (15.0 -> 19.2 ms/step,
+profiles/r5x_saved_ab.txt).
 Backward-direction calls (grad-maps, never saved) and calls outside the context run as SmartFP's
 own call (the same values as the codec's decompress(compress(x)), one launch instead of five).
 """
@@ -39,10 +47,12 @@ import torch
 from ... import _native as N
 from ...compress.packed import SmaqPacked, SmartFPPacked, _HDR_BYTES, _TOTAL_OFF
 from ...compress.smart import SmartFP
+from ..globals import Globals
 
 __all__ = ["PackedActivations", "stream_capacity"]
 
 FORWARD_TAG = "forward_autograd"
+ESCAPE_FRAC = 0.01  # a saved stream's capacity: every element an outlier and 1 % escapes
 
 
 def stream_capacity(n: int, num_bits_main: int, num_bits_outlier: int, bn_channels: int = 0,
@@ -70,15 +80,23 @@ class _Saved:
 
 
 class _Entry:
-    __slots__ = ("ref", "packed", "cap", "version", "shape", "stride", "dtype", "handle")
+    __slots__ = ("ref", "packed", "version", "shape", "stride", "dtype", "handle")
 
 
 class PackedActivations:
-    def __init__(self, codec: SmartFPPacked, verify_bytes: int = 32 << 20):
+    def __init__(self, codec: SmartFPPacked, verify_bytes: int = 32 << 20, overlap: bool = False):
         if not isinstance(codec, SmartFPPacked):
             raise TypeError("PackedActivations needs a SmartFPPacked codec")
         self.codec = codec
         self.verify_bytes = int(verify_bytes)
+        # overlap: the packing launches of each forward call on a side stream (they wait for the
+        # call's statistics, then run beside the next layers), with a ring of _RING workspaces
+        self.overlap = bool(overlap)
+        self._side: Dict[int, torch.cuda.Stream] = {}
+        self._ring: Dict[int, List[list]] = {}  # device -> [[workspace, event recorded after], ...]
+        self._ring_next = 0
+        self._joined = True
+        self._getter = N.ws_getter("smaq_pack")
         self._live: Dict[int, _Entry] = {}  # data_ptr of a forward output -> its stream
         self._pending: List[_Saved] = []     # saved, size not yet checked (y still held)
         self._pending_bytes = 0
@@ -103,24 +121,83 @@ class PackedActivations:
             # own call (one launch up to 8.4M elements), the values decompress(compress(x)) has
             return SmartFP.__call__(codec, x, tag=tag, all_positive=all_positive,
                                     batch_norm_stats=batch_norm_stats, **kw)
+        if not self.overlap and (batch_norm_stats is None or not hp.use_batch_norm):
+            # the C call (csrc/torchfast.cpp smaq_packed): y and its stream in one call
+            hot = codec._hot
+            if hot is None:
+                hot = codec._build_hot()
+            r = None
+            if hot is not False and Globals.profiler is None and codec._trace is None:
+                r = N._torch_fast.smaq_packed(hot, x, all_positive, self._getter, ESCAPE_FRAC)
+                if r is NotImplemented:  # a flag changed: rebuild the state
+                    hot = codec._build_hot()
+                    r = (N._torch_fast.smaq_packed(hot, x, all_positive, self._getter,
+                                                   ESCAPE_FRAC) if hot is not False else None)
+            if r is not None and r is not NotImplemented:
+                y, data = r
+                return self._register(y, SmaqPacked(data, x.shape, x.numel(),
+                                                    widths=(hp.num_bits_main,
+                                                            hp.num_bits_outlier)))
         n = x.numel()
         bn = batch_norm_stats is not None and hp.use_batch_norm
         channels = (1 if hp.bn_scalar_params else x.shape[1]) if bn else 0
-        cap = stream_capacity(n, hp.num_bits_main, hp.num_bits_outlier, channels)
+        cap = stream_capacity(n, hp.num_bits_main, hp.num_bits_outlier, channels, ESCAPE_FRAC)
         # y and its stream from one statistics pass, the stream straight into a buffer of the
         # capacity (a stream that does not fit is flagged by its header: verify() keeps y then)
-        y, full = codec.roundtrip_compress(x, all_positive, batch_norm_stats, capacity=cap)
+        if self.overlap:
+            side, ws = self._slot(x.device, n)
+            self._joined = False
+            y, full = codec.roundtrip_compress(x, all_positive, batch_norm_stats, capacity=cap,
+                                               pack_stream=side, workspace=ws[0])
+            ws[1].record(side)  # this slot's workspace is free again once side has passed here
+        else:
+            y, full = codec.roundtrip_compress(x, all_positive, batch_norm_stats, capacity=cap)
         codec.log_size(tag, n * 32, lambda: full.nbytes * 8)
-        data = full.data
+        return self._register(y, full)
+
+    def _register(self, y: torch.Tensor, packed: SmaqPacked) -> torch.Tensor:
+        """Remember y's stream until autograd saves y (or y dies)."""
         e = _Entry()
         key = y.data_ptr()
         e.ref = weakref.ref(y, lambda _r, k=key, d=self._live: d.pop(k, None))
-        e.packed = SmaqPacked(data, full.shape, n, widths=full.widths)
-        e.cap, e.version = cap, y._version
+        e.packed = packed
+        e.version = y._version
         e.shape, e.stride, e.dtype = y.shape, y.stride(), y.dtype
         e.handle = None
         self._live[key] = e
         return y
+
+    _RING = 4
+
+    def _slot(self, device: torch.device, n: int):
+        """The side stream of device and the next ring slot [workspace, event], its workspace at
+        least the packer's for n elements. The current stream waits (on the device) until the
+        side stream has finished the slot's previous call."""
+        di = device.index if device.index is not None else torch.cuda.current_device()
+        side = self._side.get(di)
+        if side is None:
+            side = self._side[di] = torch.cuda.Stream(device)
+            self._ring[di] = [[None, torch.cuda.Event()] for _ in range(self._RING)]
+        slot = self._ring[di][self._ring_next % self._RING]
+        self._ring_next += 1
+        cur = torch.cuda.current_stream(device)
+        cur.wait_event(slot[1])  # (a never-recorded event is complete)
+        lib = N.lib()
+        hp = self.codec.hparams
+        k = min(n, hp.num_samples) if hp.use_sample_stats else 0
+        need = (lib.smq_smaq_pack_workspace_bytes_sampled(n, k) if k
+                else lib.smq_smaq_pack_workspace_bytes(n))
+        if slot[0] is None or slot[0].numel() < need:
+            # zero-filled once (the workspace needs no initialisation, include/smq.h); allocated
+            # on the current stream, which has just waited for the old one's last side use
+            slot[0] = torch.zeros(max(need, 1 << 20), dtype=torch.uint8, device=device)
+        return side, slot
+
+    def _join(self) -> None:
+        """Order the current stream after every packing launch enqueued on the side streams."""
+        for di, side in self._side.items():
+            torch.cuda.current_stream(di).wait_stream(side)
+        self._joined = True
 
     # -- saved_tensors_hooks ------------------------------------------------------------------------
     def _pack(self, t: torch.Tensor):
@@ -150,11 +227,12 @@ class PackedActivations:
             self._harvest(self.verify_bytes)
         return h
 
-    @staticmethod
-    def _unpack(h):
+    def _unpack(self, h):
         if isinstance(h, _Saved):
             if h.y is not None:  # not checked yet, or cut at its capacity: the activation itself
                 return h.y
+            if not self._joined:  # a backward inside the context: after the packing launches
+                self._join()
             return h.codec.decompress(h.packed)
         return h
 
@@ -170,11 +248,15 @@ class PackedActivations:
         hs = self._pending
         if not hs:
             return
-        sizes = torch.cat([h.packed.data[_TOTAL_OFF:_TOTAL_OFF + 8] for h in hs])
-        host = torch.empty(sizes.numel(), dtype=torch.uint8, pin_memory=True)
-        host.copy_(sizes, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(sizes.device))
+        dev = hs[0].packed.data.device
+        # the headers are written by the packing launches: read them on their stream
+        st = self._side.get(dev.index) if self.overlap else None
+        with torch.cuda.stream(st if st is not None else torch.cuda.current_stream(dev)):
+            sizes = torch.cat([h.packed.data[_TOTAL_OFF:_TOTAL_OFF + 8] for h in hs])
+            host = torch.empty(sizes.numel(), dtype=torch.uint8, pin_memory=True)
+            host.copy_(sizes, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
         self._inflight.append((ev, host, hs, self._pending_bytes))
         self._inflight_bytes += self._pending_bytes
         self._pending = []
@@ -211,6 +293,7 @@ class PackedActivations:
     def __exit__(self, *exc):
         hooks, self._hooks = self._hooks, None
         try:
+            self._join()  # backward decodes the streams on the current stream
             self.verify()
         finally:
             self._live.clear()

@@ -29,8 +29,8 @@ def _eq(a, b):
     return torch.equal(a.view(torch.int32), b.view(torch.int32))
 
 
-@pytest.mark.parametrize("inplace", [False, True])
-def test_packed_saved_activations_bitexact(inplace):
+@pytest.mark.parametrize("inplace,overlap", [(False, True), (True, True), (False, False)])
+def test_packed_saved_activations_bitexact(inplace, overlap):
     from smart_compress_amd.compress import SmartFP, SmartFPPacked
     from smart_compress_amd.util.pytorch.autograd import register_autograd_module
     from smart_compress_amd.util.pytorch.saved import PackedActivations
@@ -42,7 +42,7 @@ def test_packed_saved_activations_bitexact(inplace):
         net = _net(inplace).cuda()
         codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
         codec.rng.seed, codec.rng.offset = 21, 0
-        acts = PackedActivations(codec, verify_bytes=8 << 20) if packed else None
+        acts = PackedActivations(codec, verify_bytes=8 << 20, overlap=overlap) if packed else None
         register_autograd_module(net, acts if packed else codec, flags)
         opt = torch.optim.SGD(net.parameters(), lr=0.05, momentum=0.9)
         g = torch.Generator(device="cuda").manual_seed(9)
@@ -136,3 +136,32 @@ def test_packed_saved_outside_context_and_backward_calls():
         assert _eq(acts(x, tag="backward_autograd"), ref(x))
         assert _eq(acts(x, tag="forward_autograd"), ref(x))
     assert pk.rng.offset == ref.rng.offset
+
+
+def test_backward_inside_the_context_waits_for_the_packer():
+    """A backward run while the context is still open decodes streams whose packing launches ran on
+    the side stream: the decode is ordered after them (the gradient equals SmartFP's)."""
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import Compressor
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(3 << 20, device="cuda", generator=g)
+    res = []
+    for packed in (False, True):
+        codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
+        codec.rng.seed, codec.rng.offset = 8, 0
+        acts = PackedActivations(codec, verify_bytes=1 << 10) if packed else None
+        comp = Compressor(acts if packed else codec)
+        w = torch.linspace(0.5, 1.5, x.numel(), device="cuda").requires_grad_(True)
+        if packed:
+            with acts:
+                y = comp(x * w)
+                loss = (y * y).sum()
+                acts.verify()  # the activation dropped: backward must decode the stream
+                loss.backward()
+        else:
+            y = comp(x * w)
+            (y * y).sum().backward()
+        res.append((y.detach(), w.grad.clone()))
+    assert _eq(res[0][0], res[1][0]) and _eq(res[0][1], res[1][1])

@@ -1,6 +1,6 @@
 """Where a ResNet-34 / CIFAR b128 step with PackedActivations spends its time (measurement script,
-not product): ms/step of SmartFP eager and of PackedActivations with the default verify budget and
-with verification only at context exit (no host synchronisation inside the forward), each
+not product): ms/step of SmartFP eager and of PackedActivations (default: one stream, the C
+forward call) and with its packing launches overlapped on a side stream, each
 interleaved over rounds; then the host time of one forward without the GPU waiting (the forward
 enqueued behind 100 large GEMMs, synchronised afterwards) and a cProfile of the packed steps.
 
@@ -40,7 +40,7 @@ def build(kind):
         register_autograd_module(net, codec, flags)
     else:
         codec = SmartFPPacked(smaq_hparams())
-        acts = PackedActivations(codec, verify_bytes=(32 << 20) if kind == "packed32M" else (1 << 40))
+        acts = PackedActivations(codec, overlap=kind == "packed_overlap")
         register_autograd_module(net, acts, flags)
     return net, opt, acts
 
@@ -75,7 +75,7 @@ def timed(step, k=20):
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    kinds = ["smartfp", "packed32M", "packed_exit"]
+    kinds = ["smartfp", "packed", "packed_overlap"]
     global busy
     busy = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     built = {k: build(k) for k in kinds}
@@ -88,10 +88,9 @@ def main():
         for k in kinds:
             res[k].append(round(timed(steps[k][0]), 3))
     print("ms/step", res, flush=True)
-    # host time of one forward with the device busy: the enqueue cost alone (no sync inside for
-    # packed_exit; packed32M's verify syncs stall on the busy kernel and are excluded by using
-    # packed_exit)
-    for k in ("smartfp", "packed_exit"):
+    # host time of one forward with the device busy: the enqueue cost alone (until the context's
+    # exit; a verify inside the forward would wait for the busy device, so the budget is lifted)
+    for k in kinds:
         step, fwd = steps[k]
         hs = []
         for _ in range(5):
@@ -100,22 +99,24 @@ def main():
                 busy @ busy
             acts = built[k][2]
             if acts is not None:
+                acts.verify_bytes = 1 << 40
                 acts.__enter__()
             t0 = time.perf_counter()
             loss = F.cross_entropy(built[k][0](x), t)
             hs.append((time.perf_counter() - t0) * 1e3)  # before the context's exit verify
             if acts is not None:
                 acts.__exit__(None, None, None)
+                acts.verify_bytes = 32 << 20
             torch.cuda.synchronize()
             loss.backward()
             torch.cuda.synchronize()
         print(f"host forward ms ({k}, device busy):", [round(v, 3) for v in hs], flush=True)
-    acts = built["packed32M"][2]
-    print("packed32M stats", acts.stats(), flush=True)
+    acts = built["packed"][2]
+    print("packed stats", acts.stats(), flush=True)
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(3):
-        steps["packed32M"][0]()
+        steps["packed"][0]()
     torch.cuda.synchronize()
     pr.disable()
     pstats.Stats(pr).sort_stats("tottime").print_stats(22)

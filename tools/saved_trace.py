@@ -15,7 +15,7 @@ import saved_ab  # noqa: E402
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    kind = sys.argv[2] if len(sys.argv) > 2 else "packed_exit"
+    kind = sys.argv[2] if len(sys.argv) > 2 else "packed"
     net, opt, acts = saved_ab.build(kind)
     step, _ = saved_ab.make_step(net, opt, acts)
     for _ in range(3 + steps):
