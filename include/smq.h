@@ -539,9 +539,11 @@ size_t smq_smaq_pack_workspace_bytes(int64_t n);
 /* Statistics (full / sampled / range, params as smq_smaq_stats) then the packing launches: codes,
  * fixed sections and variable-section sizes (one workgroup per block), a scan of the group sizes
  * (header), the variable sections moved to their prefix (one workgroup per 64 blocks; a block
- * whose section outgrew its scratch slot is re-coded from x there). No launch waits on another
- * workgroup and the host is never synchronised; the stream incl. header.total_bytes is written on
- * the device. packed_bytes >= smq_smaq_pack_bound (smq_smaq_pack_bound_bn with params->bn_gamma:
+ * whose section outgrew its scratch slot is re-coded from x there). Up to 2048 blocks (8,388,608
+ * elements; 16-B aligned x, T_m > 0, no BN term) the packing is ONE launch instead: each block
+ * finds its variable section's offset by a decoupled look-back over the blocks before it and
+ * writes it in place; the bytes are the same. The host is never synchronised; the stream incl.
+ * header.total_bytes is written on the device. packed_bytes >= smq_smaq_pack_bound (smq_smaq_pack_bound_bn with params->bn_gamma:
  * the BN variant, whose parameters are copied into the stream). Any threshold but NaN. */
 int smq_smaq_compress(const void* x, int dtype, int64_t n, const SmqSmaqParams* params,
                       void* packed, size_t packed_bytes, void* workspace, size_t workspace_bytes,

@@ -81,6 +81,8 @@ struct PackArgs {
   uint32_t forward;          // blocks in address order (measurement knob SMQ_PACK_FORWARD)
   uint64_t cap_words;        // words of the variable region (+ BN table) the buffer holds: a
                              // section that would end past it is not written
+  uint32_t lb;               // one launch: the blocks' variable offsets by a look-back (pack_lookback)
+  unsigned long long* lb_status;  // [n_blocks] status granules, zeroed by the statistics launch
   const float* bn_gamma;     // BN variant (general packer only), else NULL
   const float* bn_beta;
   int64_t bn_channels, bn_inner;
@@ -188,12 +190,95 @@ struct PackLds {
   }
 };
 
+__device__ void write_header(const PackArgs& A, uint64_t carry, int tid, int nthr);
+template <int RM, int TIN, bool EXT>
+__device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_dst, uint32_t* ext,
+                                   uint32_t* s_cnt);
+
+// Blocks up to which the packer runs as ONE launch (smaq_pack_lb_kernel): 2048 blocks = 8,388,608
+// elements, the activation sizes (below it the scratch round trip and the var launch are latency).
+constexpr uint32_t kLbMaxBlocks = 2048;
+constexpr int kLbWin = kBlock;  // predecessors examined per round trip (one per thread)
+
+// Decoupled look-back (one launch, blocks in index order; a workgroup only waits on blocks of lower
+// index, dispatched before it, so no co-residency is assumed): block b publishes its section's
+// words as an aggregate the moment they are counted, looks back over windows of kLbWin predecessors
+// for the nearest inclusive prefix (every block between it and b holding its aggregate), and
+// publishes its own inclusive prefix. A status granule is ONE 64-bit sc1 store, (flag << 32) |
+// words, flag 1 = aggregate, 2 = inclusive, 0 = not yet: the statistics launch of the same call
+// cleared them (a generation tag kept in the workspace instead was clobbered when calls of other
+// sizes laid the workspace out differently, and stale granules passed for the current call's).
+// Returns the words of the blocks before b (every thread).
+__device__ __forceinline__ uint64_t pack_lookback(const PackArgs& A, uint32_t b, uint32_t own) {
+  __shared__ unsigned long long s_bi[kBlock / kWave], s_bv[kBlock / kWave];
+  __shared__ unsigned long long s_sum[kBlock / kWave];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  if (tid == 0) st_sc1_u64(A.lb_status + b, ((b == 0 ? 2ull : 1ull) << 32) | own);
+  if (b == 0) return 0;
+  uint64_t acc = 0;
+  int64_t hi = (int64_t)b - 1;
+  for (;;) {
+    // thread t looks at block hi - t (t = 0: the nearest)
+    const int64_t j = hi - tid;
+    const uint64_t g = j >= 0 ? ld_sc1_u64(A.lb_status + j) : 0ull;
+    const bool valid = j >= 0 && (g >> 32) != 0u;
+    const bool incl = valid && (g >> 32) == 2u;
+    const unsigned long long bi = __ballot(incl), bv = __ballot(valid);
+    if (lane == 0) {
+      s_bi[w] = bi;
+      s_bv[w] = bv;
+    }
+    lds_barrier();
+    // the nearest inclusive, and whether every block before it (in this window) is valid
+    int t_i = kLbWin;
+    bool ok = true;
+#pragma unroll
+    for (int v = 0; v < kBlock / kWave; ++v) {
+      const unsigned long long vi = s_bi[v], vv = s_bv[v];
+      if (t_i == kLbWin) {
+        if (vi) {
+          const int c = __builtin_ctzll(vi);
+          t_i = kWave * v + c;
+          const unsigned long long below = c ? ((1ull << c) - 1ull) : 0ull;
+          ok = ok && (vv & below) == below;
+        } else {
+          // blocks before 0 (j < 0) never occur without an inclusive nearer: block 0 is one
+          ok = ok && vv == ~0ull;
+        }
+      }
+    }
+    lds_barrier();  // (the next round's writes of s_bi / s_bv)
+    if (!ok) {  // a block between is still coding: look again
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    // the words of blocks t <= t_i of this window (t_i itself: its inclusive prefix)
+    uint64_t v = (tid <= t_i) ? (g & 0xffffffffull) : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    if (lane == 0) s_sum[w] = v;
+    lds_barrier();
+    uint64_t tot = 0;
+#pragma unroll
+    for (int u = 0; u < kBlock / kWave; ++u) tot += s_sum[u];
+    lds_barrier();
+    acc += tot;
+    if (t_i < kLbWin) break;
+    hi -= kLbWin;
+  }
+  if (tid == 0) st_sc1_u64(A.lb_status + b, (2ull << 32) | (acc + own));
+  return acc;
+}
+
 // One block (smaq_pack_block_kernel): codes of its elements, its fixed image in LDS -> the stream
 // at b * F, outlier ranks and escapes -> the variable section in the block's scratch slot (unless
 // it outgrows kVarCap or a segment's escape list: then the var kernel re-codes the block), the
 // section's size -> meta / the group sum.
 // EXT: the general element (ext_quant; instantiated with runtime widths only).
-template <int RM, int TIN, bool VEC, bool FULL, bool SUB, int WM, int WO, bool EXT>
+// LB: the single-launch packer (smaq_pack_lb_kernel): the section goes straight to its place in the
+// variable region (offset by pack_lookback, directory entry written here; an escape-heavy block is
+// re-coded to it at once), no scratch slot, meta or group sum; the last block writes the header.
+template <int RM, int TIN, bool VEC, bool FULL, bool SUB, int WM, int WO, bool EXT, bool LB = false>
 __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, uint32_t* lds) {
   constexpr int kWE = (WM > 0 && WO > 0) ? (WO > WM ? WO - WM : 0) : -1;  // -1: runtime
   const int wm = WM > 0 ? WM : A.wm, wo = WO > 0 ? WO : A.wo;
@@ -375,6 +460,14 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
   const uint32_t var_words = n_ext + 2u * n_esc;
   const bool fits = !seg_over && var_words <= (uint32_t)kVarCap;
   uint32_t* dst = A.scratch + (size_t)b * kVarCap;
+  uint64_t vbase = 0;  // LB: the section's word offset in the variable region
+  if (LB) {
+    vbase = pack_lookback(A, b, var_words);
+    dst = A.var + vbase;
+    if (tid == 0)
+      A.dir[b] = vbase | ((uint64_t)n_out << 38) | ((uint64_t)n_esc << 51);
+  }
+  const bool room = !LB || vbase + var_words <= A.cap_words;  // (a capacity-bounded stream)
   if (we > 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -399,7 +492,7 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
     }
   }
   // escapes: thread t copies entries t % 16 and t % 16 + 16 of segment t / 16 to their rank
-  if (fits && n_esc) {
+  if (fits && room && n_esc) {
     const int s = tid >> 4;
     const uint32_t sb = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * s, (int)sexcl) >> 16;
     const uint32_t sc = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * s, (int)own) >> 16;
@@ -418,12 +511,16 @@ __device__ __forceinline__ void pack_block_body(const PackArgs& A, uint32_t b, u
   uint4* fdst = reinterpret_cast<uint4*>(A.fixed + (size_t)b * F);
   const uint4* fsrc = reinterpret_cast<const uint4*>(lds);
   for (uint32_t i = tid; i < F / 4u; i += kBlock) fdst[i] = fsrc[i];
-  if (tid == 0) {
+  if (!LB && tid == 0) {
     A.meta[b] = n_out | (n_esc << 16) | (fits ? 0u : kMetaRecode);
     atomicAdd(A.gsum + b / kGroup, var_words);
   }
-  if (fits)
+  if (fits && room)
     for (uint32_t i = tid; i < n_ext; i += kBlock) dst[i] = ext[i];
+  if (LB && !fits && room)  // escape-heavy: re-coded from x to its place (its LDS: ext, elist)
+    recode_var_section<RM, TIN, EXT>(A, b, vbase, ext, elist);
+  if (LB && b == A.n_blocks - 1)  // every block's inclusive prefix is out: the header
+    write_header(A, vbase + var_words, tid, kBlock);
 }
 
 // One workgroup per full block, in reverse address order: the statistics sweep just read x front
@@ -437,6 +534,22 @@ __global__ __launch_bounds__(kBlock) void smaq_pack_block_kernel(PackArgs A) {
     pack_block_body<RM, TIN, VEC, FULL, true, WM, WO, EXT>(A, b, lds);
   else
     pack_block_body<RM, TIN, VEC, FULL, false, WM, WO, EXT>(A, b, lds);
+}
+
+// The single launch up to kLbMaxBlocks blocks: blocks in index order (the look-back's), the short
+// last block in the same grid.
+template <int RM, int TIN, bool VEC, int WM, int WO, bool EXT>
+__global__ __launch_bounds__(kBlock) void smaq_pack_lb_kernel(PackArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t b = blockIdx.x;
+  const bool full = b < A.n_full;
+  if (A.stats->quot_check) {
+    if (full) pack_block_body<RM, TIN, VEC, true, true, WM, WO, EXT, true>(A, b, lds);
+    else pack_block_body<RM, TIN, false, false, true, WM, WO, EXT, true>(A, b, lds);
+  } else {
+    if (full) pack_block_body<RM, TIN, VEC, true, false, WM, WO, EXT, true>(A, b, lds);
+    else pack_block_body<RM, TIN, false, false, false, WM, WO, EXT, true>(A, b, lds);
+  }
 }
 
 constexpr int kScanThreads = 1024;
@@ -555,19 +668,20 @@ __device__ void write_header(const PackArgs& A, uint64_t carry, int tid, int nth
   }
 }
 
-// The variable section of block b re-coded from x straight to the stream at var_dst (a block
-// whose section outgrew its scratch slot: more than kSegEsc escapes in a 256-element segment, as
-// real activations give when a channel sits far from the tensor's mean). One pass with every load
-// in flight at once: thread t codes elements 256 j + t (j = 0..15, element order = (j, t)) into
-// registers, one ballot pair per j counts each wave's outliers and escapes, wave 0 scans the 64
-// (j, wave) counts, and every element is placed at its rank: outlier bits ORed into LDS (ext,
-// 128 * we words, copied out at the end), escapes written directly. Two barriers per block where
-// the round-4 form (two sweeps of 16 dependent load/ballot/barrier steps) took 30-60 us.
+// The variable section of block b re-coded from x straight to the stream at var_dst (a block whose
+// section outgrew its scratch slot, or, in the one-launch packer, more than kSegEsc escapes in a
+// 256-element segment: real activations give such blocks when a channel sits far from the tensor's
+// mean). 16 passes of 256 consecutive elements, one per thread; outlier and escape ranks by wave
+// ballots and the passes' running totals; the outlier bits are ORed into LDS (ext, 128 * we words)
+// and copied out at the end, the escapes are written directly. Slow per block, but its few
+// registers keep the var kernel's copy path and the one-launch packer at their occupancy. (Round 5,
+// measured, not kept: a register-resident form — every load in flight, two barriers — cut a
+// re-coded block's time, but inlined it raised the var launch from 18.4 to 24.8 us at 256M and the
+// one-launch packer from 67 to 89 VGPRs for the same device time per ResNet-34 step; called out of
+// line, the var launch took 46 us.)
 template <int RM, int TIN, bool EXT>
 __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_dst, uint32_t* ext,
                                    uint32_t* s_cnt) {
-  constexpr int J = kPB / kBlock;  // 16 elements per thread
-  static_assert(J * (kBlock / kWave) == kWave, "one (j, wave) count per lane of the scan");
   const int wm = A.wm, wo = A.wo, we = wo > wm ? wo - wm : 0;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int64_t e0 = (int64_t)b * kPB;
@@ -575,60 +689,55 @@ __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_d
   ElemConsts c;
   init_consts(c, A.stats, A.thr, A.r_main, A.r_out, A.inv_r_main, A.inv_r_out, pack_cthr<TIN>(A));
   const uint32_t hm = 1u << (wm - 1), side = 1u << (wo - 1);
-  float xv[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int el = j * kBlock + tid;
-    xv[j] = el < n_el ? load1<TIN>(A.x, e0 + el) : 0.0f;
-  }
   for (uint32_t i = tid; i < 128u * (uint32_t)we; i += kBlock) ext[i] = 0u;
-  uint32_t hib[J], qb[J], om = 0u, emk = 0u;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int el = j * kBlock + tid;
-    bool o = false, lo = false, esc = false;
-    float q = 0.0f;
-    uint32_t code = 0u;
-    if (el < n_el) {
-      const float u = (RM == kRoundHash) ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)(e0 + el)) : 0.0f;
-      q = EXT ? ext_quant<RM, TIN, true>(A, xv[j], u, c, e0 + el, o, lo)
-              : pack_quant<RM, TIN, true>(xv[j], u, c, o, lo);
-      code = code_sel(q, o, lo, hm, side, 2u * hm, esc);
-    }
-    hib[j] = code >> wm;
-    qb[j] = q == q ? __float_as_uint(q) : 0x7fc00000u;  // one NaN pattern
-    om |= o ? 1u << j : 0u;
-    emk |= esc ? 1u << j : 0u;
-    const unsigned long long bo = __ballot(o), be = __ballot(esc);
-    if (lane == 0) s_cnt[j * (kBlock / kWave) + w] = (uint32_t)__popcll(bo) | ((uint32_t)__popcll(be) << 16);
-  }
   __syncthreads();
-  if (w == 0) {  // (j, wave) counts in element order -> exclusive bases
-    const uint32_t v = s_cnt[lane];
-    const uint32_t inc = wave_incl_scan_u32(v);
-    s_cnt[kWave + lane] = inc - v;
-    if (lane == kWave - 1) s_cnt[2 * kWave] = inc;
-  }
-  __syncthreads();
-  const uint32_t n_out = s_cnt[2 * kWave] & 0xffffu;
-  uint32_t* out = A.var + var_dst;
-  uint32_t* eout = out + ext_words(we, n_out);
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const bool o = (om >> j) & 1u, esc = (emk >> j) & 1u;
-    const unsigned long long bo = __ballot(o), be = __ballot(esc);
-    const uint32_t base = s_cnt[kWave + j * (kBlock / kWave) + w];
-    if (o && we > 0) {
+  // pass 0 counts the block's outliers (its escapes follow the outlier bits: ext_words(we, n_out)
+  // words); pass 1 places the outlier bits and writes the escapes
+  uint32_t n_out = 0u;
+#pragma unroll 1
+  for (int pass = we > 0 ? 0 : 1; pass < 2; ++pass) {
+    uint32_t r_out = 0u, r_esc = 0u;
+    uint32_t* out = A.var + var_dst + ext_words(we, n_out);
+#pragma unroll 1
+    for (int j = 0; j < kPB / kBlock; ++j) {
+      const int el = j * kBlock + tid;
+      bool o = false, lo = false, esc = false;
+      float q = 0.0f;
+      uint32_t code = 0u;
+      if (el < n_el) {
+        const float u = (RM == kRoundHash) ? rng_hu(A.key, A.offset + c.rng_off + (uint64_t)(e0 + el)) : 0.0f;
+        q = EXT ? ext_quant<RM, TIN, true>(A, load1<TIN>(A.x, e0 + el), u, c, e0 + el, o, lo)
+                : pack_quant<RM, TIN, true>(load1<TIN>(A.x, e0 + el), u, c, o, lo);
+        code = code_sel(q, o, lo, hm, side, 2u * hm, esc);
+      }
+      const unsigned long long bo = __ballot(o), be = __ballot(esc);
       const uint32_t ro = __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u));
-      or_bits32(ext, (uint32_t)we * ((base & 0xffffu) + ro), hib[j]);  // we <= 23 bits
+      const uint32_t re = __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
+      if (lane == 0) s_cnt[w] = (uint32_t)__popcll(bo) | ((uint32_t)__popcll(be) << 16);
+      __syncthreads();
+      uint32_t before = 0u, tot = 0u;
+#pragma unroll
+      for (int v = 0; v < kBlock / kWave; ++v) {
+        const uint32_t t = s_cnt[v];
+        before += v < w ? t : 0u;
+        tot += t;
+      }
+      __syncthreads();
+      if (pass == 1) {
+        const uint32_t ko = r_out + (before & 0xffffu) + ro, ke = r_esc + (before >> 16) + re;
+        if (o && we > 0) or_bits32(ext, (uint32_t)we * ko, code >> wm);  // we <= 23 bits
+        if (esc) {
+          out[2u * ke] = (uint32_t)el;
+          out[2u * ke + 1u] = q == q ? __float_as_uint(q) : 0x7fc00000u;
+        }
+      }
+      r_out += tot & 0xffffu;
+      r_esc += tot >> 16;
     }
-    if (esc) {
-      const uint32_t k = (base >> 16) + __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
-      eout[2u * k] = (uint32_t)(j * kBlock + tid);
-      eout[2u * k + 1u] = qb[j];
-    }
+    n_out = r_out;
   }
   __syncthreads();
+  uint32_t* out = A.var + var_dst;
   for (uint32_t i = tid; i < ext_words(we, n_out); i += kBlock) out[i] = ext[i];
 }
 
@@ -764,6 +873,13 @@ __host__ __device__ inline uint32_t rare_per(uint32_t nb) {
 template <int RM, int TIN, int WM, int WO, bool EXT>
 void launch_pack_w(const PackArgs& A, bool vec, hipStream_t st) {
   const size_t lds = 4 * (size_t)A.lds_words;
+  if constexpr (!EXT) {  // (the general element keeps the three-launch form: A.lb is 0 there)
+    if (A.lb && vec) {  // (an unaligned x keeps the three-launch form too)
+      hipLaunchKernelGGL((smaq_pack_lb_kernel<RM, TIN, true, WM, WO, false>), dim3(A.n_blocks),
+                         dim3(kBlock), lds, st, A);
+      return;
+    }
+  }
   if (A.n_full > 0) {
     if (vec)
       hipLaunchKernelGGL((smaq_pack_block_kernel<RM, TIN, true, true, WM, WO, EXT>), dim3(A.n_full),
@@ -1428,13 +1544,19 @@ static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParam
   // the statistics own the first region (sized for the multi-workgroup draw above 4096 samples)
   char* wb = (char*)ws;
   const uint32_t n_groups = (uint32_t)(((size_t)nb + kGroup - 1) / kGroup);
-  bool zeroed = false;  // the group sums start at zero: cleared by the statistics launch
+  // up to kLbMaxBlocks blocks (16-B aligned x, the packer's own element): ONE packing launch with
+  // a look-back whose status granules (start of the scratch region) must start at zero; else the
+  // three launches, whose group sums must. Either way the statistics launch clears them.
+  const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
+  const bool lb = (uint32_t)nb <= kLbMaxBlocks && vec &&
+                  !(p->bn_gamma || !(p->main_std_dev_threshold > 0.0f));
+  uint32_t* zero = lb ? (uint32_t*)(wb + L.scratch) : (uint32_t*)(wb + L.gsum);
+  const uint32_t zero_n = lb ? 2u * (uint32_t)nb : n_groups;
+  bool zeroed = false;
   if (y)
-    rc = roundtrip_for_pack(x, dtype, y, n, p, ws, L.meta, st, (uint32_t*)(wb + L.gsum), n_groups,
-                            &zeroed);
+    rc = roundtrip_for_pack(x, dtype, y, n, p, ws, L.meta, st, zero, zero_n, &zeroed);
   else
-    rc = prepare_stats(x, dtype, n, p, ws, L.meta, st, (uint32_t*)(wb + L.gsum), n_groups,
-                       &zeroed);
+    rc = prepare_stats(x, dtype, n, p, ws, L.meta, st, zero, zero_n, &zeroed);
   if (rc) return rc;
   PackArgs A;
   memset(&A, 0, sizeof(A));
@@ -1480,9 +1602,10 @@ static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParam
             (A.thr < 0.0f ? SMQ_PACK_FLAG_BOTH_SIDES : 0u) | (p->bn_gamma ? SMQ_PACK_FLAG_BN : 0u);
   const bool ext = p->bn_gamma || !(A.thr > 0.0f);
   A.lds_words = PackLds::words(A.wm, we);
-  const bool vec = aligned_to(x, dtype == SMQ_DTYPE_F32 ? 16 : 8);
   const bool sr = p->stochastic_rounding != 0;
-  if (!zeroed) fill_async(A.gsum, 0u, A.n_groups, st);  // (sampled statistics: smq_common.h)
+  A.lb = lb ? 1u : 0u;
+  A.lb_status = (unsigned long long*)(wb + L.scratch);
+  if (!zeroed) fill_async(zero, 0u, zero_n, st);  // (sampled statistics: smq_common.h)
   if (pst && pst != st) {  // the packing launches on their own stream, behind the statistics
     const hipEvent_t ev = fork_event();
     if (!ev || hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(pst, ev, 0) != hipSuccess) {

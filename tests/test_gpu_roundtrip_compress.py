@@ -154,3 +154,38 @@ def test_capacity_bounded_buffer():
     rc3, _, _, _ = _raw_call(x, n, fixed - 8)
     assert rc3 == -2  # SMQ_ERR_WORKSPACE
     assert b"smq_smaq_pack_fixed_bytes" in lib.smq_last_error()
+
+
+def test_one_launch_packer_workspace_reuse():
+    """The one-launch packer (up to 2048 blocks) and the three-launch form (above) alternating on
+    ONE workspace that starts as random bytes: every stream equals the one a fresh zeroed
+    workspace gives (the look-back's status granules carry the call's generation; nothing the
+    other launches write lands in their region)."""
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    hp, rc, _, _ = _codecs()
+    gen = torch.Generator(device="cuda").manual_seed(13)
+    # (64 and 32 blocks alternating: the layout of the workspace moves with n — the pattern that
+    # once let a stale status granule pass for the current call's)
+    sizes = [1_000_003, 9_000_000, 4096 * 2048, 70_000, 9_000_000, 1_000_003] + [262_144, 131_072] * 4
+    xs = {n: torch.randn(n, generator=gen, device="cuda") * 1.3 for n in set(sizes)}
+    big = max(lib.smq_smaq_pack_workspace_bytes(n) for n in sizes)
+    ws = torch.randint(0, 256, (big,), dtype=torch.uint8, device="cuda", generator=gen)
+
+    def stream(n, w):
+        p = rc._params(n, False, torch.float32, xs[n].device)
+        p.offset = 77  # the same draws for both workspaces
+        bound = lib.smq_smaq_pack_bound(n, 6, 8)
+        out = torch.empty(bound, dtype=torch.uint8, device="cuda")
+        assert lib.smq_smaq_compress(xs[n].data_ptr(), N.SMQ_DTYPE_F32, n, p, out.data_ptr(),
+                                     bound, w.data_ptr(), w.numel(),
+                                     N.stream_ptr(xs[n].device)) == 0
+        torch.cuda.synchronize()
+        hdr = N.SmqPackedHeader.from_buffer_copy(bytes(out[:128].cpu().numpy()))
+        return out[:int(hdr.total_bytes)].cpu().numpy()
+
+    for n in sizes:
+        fresh = torch.zeros(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8,
+                            device="cuda")
+        assert np.array_equal(stream(n, ws), stream(n, fresh)), n
