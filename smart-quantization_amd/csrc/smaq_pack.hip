@@ -197,7 +197,10 @@ __device__ void recode_var_section(const PackArgs& A, uint32_t b, uint64_t var_d
 
 // Blocks up to which the packer runs as ONE launch (smaq_pack_lb_kernel): 2048 blocks = 8,388,608
 // elements, the activation sizes (below it the scratch round trip and the var launch are latency).
-constexpr uint32_t kLbMaxBlocks = 2048;
+#ifndef SMQ_LB_MAX_BLOCKS  // (experiment builds: tools/build_variant.py -DSMQ_LB_MAX_BLOCKS=...)
+#define SMQ_LB_MAX_BLOCKS 2048
+#endif
+constexpr uint32_t kLbMaxBlocks = SMQ_LB_MAX_BLOCKS;
 constexpr int kLbWin = kBlock;  // predecessors examined per round trip (one per thread)
 
 // Decoupled look-back (one launch, blocks in index order; a workgroup only waits on blocks of lower
