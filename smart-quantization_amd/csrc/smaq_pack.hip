@@ -1367,9 +1367,7 @@ __device__ __forceinline__ void unpack_run(UnpackArgs A, uint32_t b0, int nblk, 
 // LDS (kVarLds); else the one short last block (kVarAny).
 // WM / WO: the 6/8-bit default's widths, or 0 (any widths, from the caller or the header).
 template <int WM, int WO, bool FULL>
-__global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t g = A.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+__device__ __forceinline__ void unpack_main_body(const UnpackArgs& A, uint32_t g, uint32_t* lds) {
   const uint32_t b0 = FULL ? g * (uint32_t)kUnpackPer : A.nb - 1;
   const int nblk = FULL ? (int)min((uint32_t)kUnpackPer, A.n_full - b0) : 1;
   // the stream is this call's (magic, n) before any directory entry is read: a caller's n beyond
@@ -1382,13 +1380,18 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
   unpack_run<WM, WO, FULL, FULL ? kVarLds : kVarAny>(A, b0, nblk, dent, lds);
 }
 
+template <int WM, int WO, bool FULL>
+__global__ __launch_bounds__(kBlock) void smaq_unpack_kernel(UnpackArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  unpack_main_body<WM, WO, FULL>(A, A.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x, lds);
+}
+
 // The full blocks whose variable section outgrew kVarCap (escape-heavy data; none on N(0,1)):
 // kBlock directory entries per workgroup, the listed blocks decoded from the stream one by one.
+// wg: the workgroup's index among the big-block workgroups; list / n_list: its LDS list
 template <int WM, int WO>
-__global__ __launch_bounds__(kBlock) void smaq_unpack_big_kernel(UnpackArgs A) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ uint32_t list[kBlock];
-  __shared__ uint32_t n_list;
+__device__ __forceinline__ void unpack_big_body(const UnpackArgs& A, uint32_t wg, uint32_t* lds,
+                                                uint32_t* list, uint32_t& n_list) {
   int wm, wo;
   UnpackArgs W = A;
   if (!unpack_widths(W, wm, wo)) return;
@@ -1396,7 +1399,7 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_big_kernel(UnpackArgs A) {
   const int we = wo > wm ? wo - wm : 0;
   if (threadIdx.x == 0) n_list = 0u;
   __syncthreads();
-  const uint32_t b = blockIdx.x * A.big_per + threadIdx.x;
+  const uint32_t b = wg * A.big_per + threadIdx.x;
   if (threadIdx.x < A.big_per && b < A.n_full) {
     const uint64_t d = A.dir[b];
     const uint32_t n_out = (uint32_t)(d >> 38) & 0x1fffu, n_esc = (uint32_t)(d >> 51);
@@ -1409,6 +1412,30 @@ __global__ __launch_bounds__(kBlock) void smaq_unpack_big_kernel(UnpackArgs A) {
     const uint64_t d = A.dir[list[i]];
     unpack_run<WM, WO, true, kVarMem>(A, list[i], 1, &d, lds);
   }
+}
+
+template <int WM, int WO>
+__global__ __launch_bounds__(kBlock) void smaq_unpack_big_kernel(UnpackArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t list[kBlock];
+  __shared__ uint32_t n_list;
+  unpack_big_body<WM, WO>(A, blockIdx.x, lds, list, n_list);
+}
+
+// Streams of up to kLbMaxBlocks blocks (the activation sizes): the decode in ONE launch instead of
+// two or three — workgroups [0, main_g) decode kUnpackPer full blocks each, [main_g, main_g + big_g)
+// the big blocks, the last one (if n is not a multiple of the block) the short final block. Its
+// registers are the three bodies' maximum, which a single wave of workgroups can afford.
+template <int WM, int WO>
+__global__ __launch_bounds__(kBlock) void smaq_unpack_small_kernel(UnpackArgs A, uint32_t main_g,
+                                                                  uint32_t big_g) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t list[kBlock];
+  __shared__ uint32_t n_list;
+  const uint32_t bx = blockIdx.x;
+  if (bx < main_g) unpack_main_body<WM, WO, true>(A, bx, lds);
+  else if (bx < main_g + big_g) unpack_big_body<WM, WO>(A, bx - main_g, lds, list, n_list);
+  else unpack_main_body<WM, WO, false>(A, 0, lds);
 }
 
 inline bool aligned_to(const void* p, unsigned a) { return ((uintptr_t)p & (a - 1)) == 0; }
@@ -1713,8 +1740,16 @@ static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int 
   if (A.big_per > (uint32_t)kBlock) A.big_per = kBlock;
   const unsigned grid = (unsigned)((A.n_full + kUnpackPer - 1) / kUnpackPer);
   const bool w57 = bm == 6 && bo == 8;  // the default widths, known from the caller
+  const unsigned big_g = grid ? (unsigned)((A.n_full + A.big_per - 1) / A.big_per) : 0u;
+  const bool small = A.nb <= kLbMaxBlocks;  // one launch (smaq_unpack_small_kernel)
+  const unsigned small_g = grid + big_g + (A.n_full < A.nb ? 1u : 0u);
 #define SMQ_UNPACK_LAUNCH(WMV, WOV)                                                                \
   do {                                                                                            \
+    if (small) {                                                                                  \
+      hipLaunchKernelGGL((smaq_unpack_small_kernel<WMV, WOV>), dim3(small_g), dim3(kBlock),        \
+                         A.lds_bytes, st, A, grid, big_g);                                        \
+      break;                                                                                      \
+    }                                                                                             \
     if (grid) {                                                                                   \
       hipLaunchKernelGGL((smaq_unpack_kernel<WMV, WOV, true>), dim3(grid), dim3(kBlock),           \
                          A.lds_bytes, st, A);                                                     \
