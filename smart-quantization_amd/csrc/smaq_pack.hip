@@ -22,6 +22,10 @@
 // interleaved codes of two widths in element order, so every block needed its prefix before its
 // first code could be placed: 2 B/elem of records went to HBM and back (1.45x the algorithmic
 // bytes).
+// Up to 2048 blocks (8,388,608 elements: the activation sizes) both directions are ONE launch after
+// the statistics: smaq_pack_lb_kernel codes a block and places its variable section by a decoupled
+// look-back over the blocks before it (no scratch, no var launch), smaq_unpack_small_kernel decodes
+// the full, big and short last blocks in one grid. Same bytes, same values.
 // decompress = one launch, one workgroup per block: fixed section + variable section -> LDS, mask
 //   prefix popcounts for the outlier ranks, escapes via an LDS bitmask + O(1) rank, then
 //   smaq_dequant (or a per-block table of it for narrow codes) — the same arithmetic as the
