@@ -17,6 +17,7 @@
 //                                           grad-map the same way (autograd.py:37-47)
 //   smaq_packed(state, x, ap, getter, frac) PackedActivations' forward call: y and its SmaQ stream
 //                                           (smq_smaq_roundtrip_compress, util/pytorch/saved.py)
+//   smaq_unpacked(data, shape, n, bm, bo)   its backward decode (smq_smaq_decompress_ex)
 //   s2fp8(x, check_inf, rng, getter)        one S2FP8 call on an fp32 device tensor
 //
 // The state object (a capsule of a shared SmaqState) holds the flag templates of the parameter
@@ -41,6 +42,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "smq.h"
 
@@ -331,6 +333,38 @@ PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   return r;
 }
 
+// smaq_unpacked(data, shape, n, num_bits_main, num_bits_outlier) -> y: PackedActivations' backward
+// decode (SmartFPPacked.decompress of a device stream written with these widths) in one C call: y
+// allocated with the stream's shape, smq_smaq_decompress_ex on the current stream.
+PyObject* smaq_unpacked(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
+  if (nargs != 5 || !THPVariable_Check(a[0]) || !PyTuple_Check(a[1])) {
+    PyErr_SetString(PyExc_TypeError, "smaq_unpacked(data, shape, n, bm, bo)");
+    return nullptr;
+  }
+  const at::Tensor& data = THPVariable_Unpack(a[0]);
+  if (!data.is_cuda()) {
+    PyErr_SetString(PyExc_ValueError, "smaq_unpacked: the stream must be on a ROCm device");
+    return nullptr;
+  }
+  const Py_ssize_t nd = PyTuple_GET_SIZE(a[1]);
+  std::vector<int64_t> shape((size_t)nd);
+  for (Py_ssize_t i = 0; i < nd; ++i) shape[(size_t)i] = PyLong_AsLongLong(PyTuple_GET_ITEM(a[1], i));
+  const int64_t n = PyLong_AsLongLong(a[2]);
+  const int bm = (int)PyLong_AsLong(a[3]), bo = (int)PyLong_AsLong(a[4]);
+  if (PyErr_Occurred()) return nullptr;
+  const int dev = data.get_device();
+  const hipStream_t st = c10::hip::getCurrentHIPStream(dev).stream();
+  at::Tensor y = at::empty(shape, data.options().dtype(at::kFloat));
+  const int rc = smq_smaq_decompress_ex(data.const_data_ptr(), y.mutable_data_ptr<float>(), n, bm,
+                                        bo, st);
+  if (rc) {
+    PyErr_Format(PyExc_RuntimeError, "smq_smaq_decompress_ex failed (rc=%d): %s", rc,
+                 smq_last_error());
+    return nullptr;
+  }
+  return THPVariable_Wrap(std::move(y));
+}
+
 // ---- the autograd wrapper (autograd.py:18-47: Compressor with a SmartFP compress_fn) -----------
 // The backward of `y = compress(x)` is `compress(grad_y)` (tag "backward_autograd"); with the
 // backward direction switched off the grad passes unchanged (autograd.py:40-41).
@@ -468,6 +502,9 @@ PyMethodDef kMethods[] = {
      "Compressor.forward with a SmartFP codec: y and its SmaqCompressBackward node"},
     {"smaq_packed", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_packed)),
      METH_FASTCALL, "PackedActivations' forward call: (y, stream) (smq_smaq_roundtrip_compress)"},
+    {"smaq_unpacked",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_unpacked)), METH_FASTCALL,
+     "PackedActivations' backward decode of a device stream (smq_smaq_decompress_ex)"},
     {"s2fp8", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(s2fp8)), METH_FASTCALL,
      "one eager S2FP8 call on an fp32 device tensor (smq_s2fp8_roundtrip), or None"},
     {nullptr, nullptr, 0, nullptr}};
