@@ -26,6 +26,7 @@ thread) for FP8 / S2FP8, on a bounded sample.
 """
 
 import argparse
+import collections
 import json
 import os
 import sys
@@ -1005,18 +1006,24 @@ def run_autograd(args, world, rank, device):
     t = torch.randint(0, 10, (batch,), device=device)
     flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
 
-    def build(compress, sizes=None, packed=False):
+    def build(compress, sizes=None, packed=False, ratio=False):
         """The network; with compression the SmartFP codec itself is registered (train.py:198-213
         passes the codec instance), so Compressor takes the codec's C autograd path. sizes: a list
         that records the element count of every codec call instead (one counting step). packed:
-        the activations autograd saves are held as SmaQ streams (util/pytorch/saved.py)."""
+        the activations autograd saves are held as SmaQ streams (util/pytorch/saved.py). ratio:
+        --measure_compression_ratio, as every reference training script runs (scripts/train.ps1),
+        logging into a bounded in-memory sink (the logger's own cost is not the codec's)."""
         torch.manual_seed(0)
         net = (_ResNet() if resnet else _vgg_cifar()).to(device)
         opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9)
         codec = None
         if compress:
-            codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
+            codec = (SmartFPPacked if packed else SmartFP)(
+                smaq_hparams(measure_compression_ratio=ratio))
             codec.rng.seed = 3000 + rank
+            if ratio:
+                sink = collections.deque(maxlen=1 << 14)
+                codec.log = lambda k, v, _s=sink, **kw: _s.append((k, v))
             fn = PackedActivations(codec) if packed else codec
             if sizes is not None:
                 def fn(v, tag=None, **kw):
@@ -1053,9 +1060,15 @@ def run_autograd(args, world, rank, device):
     results = {}
     # (the graph variant last: its capture keeps a private memory pool alive, which would count in
     # the following variants' allocated memory)
-    for name in ("uncompressed", "smaq_eager", "smaq_eager_packed_saved", "smaq_graph"):
+    variants = ["uncompressed", "smaq_eager", "smaq_eager_ratio", "smaq_eager_packed_saved",
+                "smaq_graph"]
+    if args.variants:  # a subset (profiling passes), always with the uncompressed baseline
+        keep = set(args.variants.split(",")) | {"uncompressed"}
+        variants = [v for v in variants if v in keep]
+    for name in variants:
         packed = name == "smaq_eager_packed_saved"
-        net, opt, codec = build(name != "uncompressed", packed=packed)
+        net, opt, codec = build(name != "uncompressed", packed=packed,
+                                ratio=name == "smaq_eager_ratio")
         step = step_fn(net, opt, codec if packed else None)
         if name == "smaq_graph":
             codec.graph_safe(device=device)
@@ -1100,16 +1113,24 @@ def run_autograd(args, world, rank, device):
                 "bits_per_element": round(st["bits_per_element"], 3) if st["bits_per_element"] else None}
         del net, opt, codec, run
     base_ms = results["uncompressed"]["ms_per_step"]
-    for name in ("smaq_eager", "smaq_graph", "smaq_eager_packed_saved"):
+    for name in variants[1:]:
         codec_ms = results[name]["ms_per_step"] - base_ms
         results[name]["codec_ms_per_step"] = round(codec_ms, 4)
         results[name]["codec_gbps_12B"] = round(12.0 * elems / (codec_ms * 1e-3) / 1e9, 1) \
             if codec_ms > 0 else None
         results[name]["codec_gbps_alg"] = round(alg_bytes / (codec_ms * 1e-3) / 1e9, 1) \
             if codec_ms > 0 else None
-    g_ms = results["smaq_graph"]["ms_per_step"]
-    g_codec = results["smaq_graph"]["codec_ms_per_step"]
-    g_gbps = results["smaq_graph"]["codec_gbps_alg"]
+    if "smaq_eager_ratio" in results and "smaq_eager" in results:
+        results["smaq_eager_ratio"]["vs_smaq_eager"] = round(
+            results["smaq_eager_ratio"]["ms_per_step"] / results["smaq_eager"]["ms_per_step"], 4)
+    if "smaq_eager_packed_saved" in results and "smaq_eager" in results:
+        results["smaq_eager_packed_saved"]["vs_smaq_eager"] = round(
+            results["smaq_eager_packed_saved"]["ms_per_step"] / results["smaq_eager"]["ms_per_step"],
+            4)
+    head = "smaq_graph" if "smaq_graph" in results else variants[-1]
+    g_ms = results[head]["ms_per_step"]
+    g_codec = results[head]["codec_ms_per_step"]
+    g_gbps = results[head]["codec_gbps_alg"]
     # HBM bytes of the step's SmaQ launches from the committed PMC passes
     # (tools/autograd_profile.py -> profiles/traffic_<config>.json)
     traffic = None
@@ -1132,6 +1153,7 @@ def run_autograd(args, world, rank, device):
             # the codec's share of the graph step (compressed - uncompressed) over the bytes its
             # calls must move (8 B/elem single launch, 12 B/elem above): every call as one number
             "roofline": {"bound": "hbm", "kernel": "all SmaQ launches of the step",
+                         "variant": head,
                          "achieved": g_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(g_gbps / HBM_PEAK_GBPS, 4) if g_gbps else None,
                          "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": g_codec,
@@ -1201,6 +1223,45 @@ def run_mock(args, world, rank, device):
             "rank_ms_per_step": HOST.get("rank_ms_per_step")}
 
 
+def run_mock_multi(args, world, rank, device):
+    """Device-free stand-in of run_multi for the launcher tests: 148 numpy tensors per rank (its own
+    seed) summed per step; the same line keys."""
+    rng = np.random.default_rng(2000 + rank)
+    ts = [rng.standard_normal(1 << 10).astype(np.float32) for _ in range(148)]
+    n = sum(t.size for t in ts)
+
+    def step():
+        for t in ts:
+            t.sum()
+
+    elapsed = time_steps(step, args.steps, args.warmup, world, device)
+    total = sum_over_ranks(12.0 * n * args.steps, world, device)
+    return {"metric": "mock multi", "value": round(total / elapsed / 1e9, 6), "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "scaling": "weak", "config": {"workload": "mock_multi", "tensors": len(ts),
+                                          "elements_per_gpu": n, "parallelism": f"replicas{world}"},
+            "roofline": None}
+
+
+# BASELINE config 5 is the one the weak-scaling curve is quoted on (fused multi-tensor SmaQ over
+# every ResNet-34 weight + grad tensor, each rank its own tensors): the headline config's N-rank job
+# measures it after the headline, so a `--gpus N` run carries both curves' points. Nested, so
+# `value` stays the headline metric the driver computes its scaling from.
+NESTED = {"smaq": ("c5_multi", run_multi), "mock": ("c5_multi", run_mock_multi)}
+
+
+def attach_nested(res, nested, args, world, rank, device):
+    """Run the nested workload on every rank (the same barriers and max-over-ranks timing) and put
+    its line under res[name] with every rank's own ms/step."""
+    name, runner = nested
+    m = runner(args, world, rank, device)
+    out = {k: m[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "ms_per_step",
+                             "scaling", "config", "roofline")}
+    out["rank_ms_per_step"] = HOST.get("rank_ms_per_step")
+    out["pct_hbm_peak"] = round(100.0 * m["value"] / world / HBM_PEAK_GBPS, 4)
+    res[name] = out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1211,6 +1272,10 @@ def main():
                              "autograd", "autograd_resnet34", "smaq_cpu", "mock"])
     ap.add_argument("--elements", type=int, default=0, help="override elements (smaq configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variants", default="",
+                    help="--config autograd*: comma list of variants to run (uncompressed always)")
+    ap.add_argument("--no-multi", action="store_true",
+                    help="--config smaq: skip the nested C5 multi-tensor line (c5_multi)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
@@ -1228,6 +1293,8 @@ def main():
     res = runner(args, world, rank, device)
     if world > 1:
         res.setdefault("rank_ms_per_step", HOST.get("rank_ms_per_step"))
+    if args.config in NESTED and not args.no_multi and not args.elements:
+        attach_nested(res, NESTED[args.config], args, world, rank, device)
         res["launcher"] = "self" if os.environ.get("TORCHELASTIC_RUN_ID") is None else "torchrun"
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and args.config in CPU_BASELINES:

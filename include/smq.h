@@ -287,6 +287,38 @@ int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqS
 int smq_smaq_roundtrip_ex(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                           const float* uniforms, void* ws, size_t ws_bytes, uint32_t flags,
                           void* stream);
+
+/* ---- --measure_compression_ratio without a host synchronisation ----
+ * The reference logs, per SmartFP call, new_size = sum(is_outlier) * num_bits_outlier +
+ * sum(~is_outlier) * num_bits_main and compression_ratio = orig_size / new_size with orig_size =
+ * 32 n (smart.py:184-188, base.py:72-102), converting each to a Python float (a device->host sync
+ * per call). These entry points leave the values on the device, as fp64 (exact: < 2^53), for the
+ * logger to read when it consumes them. */
+typedef struct SmqSizeRecord {
+  unsigned long long slots[8];   /* outlier-count partials: ZERO on entry (a fresh record per call) */
+  unsigned long long arrived;    /* workgroups counted: ZERO on entry */
+  unsigned long long reserved[3];
+  double n_outlier;              /* written by the call: sum(is_outlier) */
+  double new_size;               /* n_outlier * bo + (n - n_outlier) * bm */
+  double compression_ratio;      /* orig_size / new_size (IEEE fp64 division: Python's int / int) */
+  double orig_size;              /* 32 n */
+} SmqSizeRecord;
+/* smq_smaq_roundtrip (params.count_outliers is implied) whose outlier count and log_size values
+ * land in rec: the single launch counts into rec->slots and its last workgroup writes the values
+ * (no extra launch); the other paths count into the workspace slots and one small launch reads
+ * them (smq_smaq_size_metrics). rec: device memory, zero-initialised, used by this call only. */
+int smq_smaq_roundtrip_counted(const void* x, int dtype, float* y, int64_t n,
+                               const SmqSmaqParams* p, void* ws, size_t ws_bytes,
+                               SmqSizeRecord* rec, void* stream);
+/* The log_size values of the last count_outliers call on the single-tensor workspace ws (n its
+ * element count) into rec->n_outlier .. orig_size (rec's other fields are not touched). */
+int smq_smaq_size_metrics(const void* ws, int64_t n, int num_bits_main, int num_bits_outlier,
+                          SmqSizeRecord* rec, void* stream);
+/* The same for the `count` tensors of a multi-tensor call (their statistics records in its
+ * workspace, n[t] their element counts, a device int64 array): out[4t .. 4t+3] = n_outlier,
+ * new_size, compression_ratio, orig_size of tensor t (fp64, device). */
+int smq_smaq_multi_size_metrics(const void* ws, const int64_t* n, int count, int num_bits_main,
+                                int num_bits_outlier, double* out, void* stream);
 /* fp64 data (smart.py:130-182 on a float64 tensor): statistics, z-score, stochastic or truncating
  * rounding and de-quantisation in fp64, output fp64; every stats_source (k of SMQ_STATS_SAMPLED_DEVICE
  * up to SMQ_MAX_DRAW_SAMPLES with a workspace of smq_smaq_workspace_bytes_sampled), BN

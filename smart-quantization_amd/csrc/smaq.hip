@@ -1402,6 +1402,103 @@ int smq_smaq_roundtrip(const void* x, int dtype, float* y, int64_t n, const SmqS
   return smq_smaq_roundtrip_ex(x, dtype, y, n, p, uniforms, ws, ws_bytes, 0u, stream);
 }
 
+// --measure_compression_ratio on the device (smart.py:184-188, base.py:72-102): the single launch
+// counts into the caller's zeroed record and its last workgroup writes the values; every other path
+// counts into the workspace slots, then smaq_size_metrics_kernel reads them.
+int smq_smaq_roundtrip_counted(const void* x, int dtype, float* y, int64_t n,
+                               const SmqSmaqParams* p, void* ws, size_t ws_bytes,
+                               SmqSizeRecord* rec, void* stream) {
+  int rc = validate_params(p);
+  if (!rc) rc = check_dtype(dtype);
+  if (!rc) rc = check_tensor_args(x, y, n);
+  if (rc) return rc;
+  if (!rec) {
+    set_error("roundtrip_counted: rec must be a device pointer");
+    return SMQ_ERR_INVALID;
+  }
+  SmqSmaqParams q = *p;
+  q.count_outliers = 1;
+  if (q.stats_source == SMQ_STATS_WORKSPACE && ws && fused_eligible(x, dtype, y, n, &q, nullptr,
+                                                                   ws_bytes)) {
+    const RangeRecips R = range_recips(q.range_main, q.range_outlier);
+    FusedCall c{x, dtype, y, n, &q, range_coef_for(&q, n), R.inv_main, R.inv_out, ws, 0, ws_bytes};
+    c.rec = rec;
+    return launch_fused(c, (hipStream_t)stream);
+  }
+  rc = smq_smaq_roundtrip_ex(x, dtype, y, n, &q, nullptr, ws, ws_bytes, 0u, stream);
+  if (rc) return rc;
+  return smq_smaq_size_metrics(ws, n, q.num_bits_main, q.num_bits_outlier, rec, stream);
+}
+
+}  // extern "C"
+
+namespace smq {
+
+// n_out = the sum of `slots` uint64 counts (one wave); the log_size values into rec.
+__global__ __launch_bounds__(kWave) void smaq_size_metrics_kernel(
+    const unsigned long long* __restrict__ slots, int nslots, int64_t n, int bm, int bo,
+    SmqSizeRecord* rec) {
+  unsigned long long v = 0;
+  for (int i = threadIdx.x; i < nslots; i += kWave) v += slots[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  if (threadIdx.x == 0) {
+    const double no = (double)v;
+    const double ns = no * (double)bo + (double)(n - (int64_t)v) * (double)bm;
+    const double orig = 32.0 * (double)n;
+    rec->n_outlier = no;
+    rec->new_size = ns;
+    rec->compression_ratio = orig / ns;
+    rec->orig_size = orig;
+  }
+}
+
+// Multi-tensor call: tensor t's n_outlier from its statistics record, one thread per tensor.
+__global__ __launch_bounds__(256) void smaq_multi_size_metrics_kernel(
+    const SmqSmaqStats* __restrict__ st, const int64_t* __restrict__ n, int count, int bm, int bo,
+    double* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= count) return;
+  const unsigned long long v = st[t].n_outlier;
+  const int64_t nt = n[t];
+  const double no = (double)v;
+  const double ns = no * (double)bo + (double)(nt - (int64_t)v) * (double)bm;
+  const double orig = 32.0 * (double)nt;
+  out[4 * t] = no;
+  out[4 * t + 1] = ns;
+  out[4 * t + 2] = orig / ns;
+  out[4 * t + 3] = orig;
+}
+
+}  // namespace smq
+
+extern "C" {
+
+int smq_smaq_size_metrics(const void* ws, int64_t n, int num_bits_main, int num_bits_outlier,
+                          SmqSizeRecord* rec, void* stream) {
+  if (!ws || !rec || n < 1) {
+    set_error("size_metrics: ws and rec must be device pointers, n >= 1");
+    return SMQ_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(smaq_size_metrics_kernel, dim3(1), dim3(kWave), 0, (hipStream_t)stream,
+                     (const unsigned long long*)((const char*)ws + SmaqWsLayout::kSlots),
+                     (int)SMQ_WS_OUTLIER_SLOTS, n, num_bits_main, num_bits_outlier, rec);
+  return check_launch("smaq_size_metrics_kernel");
+}
+
+int smq_smaq_multi_size_metrics(const void* ws, const int64_t* n, int count, int num_bits_main,
+                                int num_bits_outlier, double* out, void* stream) {
+  if (count < 0 || (count > 0 && (!ws || !n || !out))) {
+    set_error("multi_size_metrics: ws, n and out must be device pointers");
+    return SMQ_ERR_INVALID;
+  }
+  if (count == 0) return SMQ_OK;
+  hipLaunchKernelGGL(smaq_multi_size_metrics_kernel, dim3((unsigned)((count + 255) / 256)),
+                     dim3(256), 0, (hipStream_t)stream, (const SmqSmaqStats*)ws, n, count,
+                     num_bits_main, num_bits_outlier, out);
+  return check_launch("smaq_multi_size_metrics_kernel");
+}
+
 int smq_smaq_stats_f32(const float* x, int64_t n, const SmqSmaqParams* p, void* ws,
                        size_t ws_bytes, void* stream) {
   return smq_smaq_stats(x, SMQ_DTYPE_F32, n, p, ws, ws_bytes, stream);
@@ -1421,6 +1518,20 @@ int smq_smaq_roundtrip_f32(const float* x, float* y, int64_t n, const SmqSmaqPar
 }  // extern "C"
 
 namespace smq {
+
+int roundtrip_pack_fused(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                         void* ws, size_t ws_bytes, const FusedPackCall& k, hipStream_t st) {
+  static const bool on = [] {  // measurement knob SMQ_FUSED_PACK=0: the round trip + packer launches
+    const char* e = knob_env("SMQ_FUSED_PACK");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (!on || p->stats_source != SMQ_STATS_WORKSPACE || !ws ||
+      !fused_eligible(x, dtype, y, n, p, nullptr, ws_bytes))
+    return kFusedPackDeclined;
+  const RangeRecips R = range_recips(p->range_main, p->range_outlier);
+  FusedCall c{x, dtype, y, n, p, range_coef_for(p, n), R.inv_main, R.inv_out, ws, 0, ws_bytes};
+  return launch_fused_pack(c, k, st);
+}
 
 int roundtrip_for_pack(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                        void* ws, size_t ws_bytes, hipStream_t st, uint32_t* zero, uint32_t zero_n,

@@ -38,6 +38,7 @@
 
 #include "smq_common.h"
 #include "smaq_elem.h"
+#include "smaq_pack_common.h"
 #include "smaq_small.h"
 
 namespace smq {
@@ -165,7 +166,49 @@ struct FusedArgs {
   uint64_t* trace;  // experiment builds (-DSMQ_FUSED_TRACE=1): 16 timestamps per workgroup
   uint32_t* zero;   // cleared by workgroup 0 (the packer's group sums: roundtrip_compress), or NULL
   uint32_t zero_n;
+  SmqSizeRecord* rec;  // counted call (count = 1, out_slots = rec->slots): the last workgroup to
+                       // have added its count writes the log_size values
+  int bm, bo;
+  // PACK variant (smq_smaq_roundtrip_compress): the call's packed stream, written from registers
+  struct {
+    SmqPackedHeader* hdr;
+    uint64_t* dir;
+    uint32_t* fixed;
+    uint32_t* var;
+    uint64_t cap_words;        // words of the variable region the buffer holds
+    uint32_t n_blocks, flags;
+    unsigned long long* look;  // [G] epoch-tagged aggregates: replica 0, granules 1024 + b
+    uint32_t lds_off;          // word offset of the pack area in the dynamic LDS
+  } pk;
 };
+
+// The log_size values of a counted call from its n_outlier (smart.py:184-188, base.py:84-88).
+__device__ __forceinline__ void size_record_finish(SmqSizeRecord* rec, uint64_t n_out, int64_t n,
+                                                   int bm, int bo) {
+  const double no = (double)n_out;
+  const double ns = no * (double)bo + (double)(n - (int64_t)n_out) * (double)bm;  // exact (< 2^53)
+  const double orig = 32.0 * (double)n;
+  rec->n_outlier = no;
+  rec->new_size = ns;
+  rec->compression_ratio = orig / ns;
+  rec->orig_size = orig;
+}
+
+// Counted call: this workgroup's count s into the record's slot, then its arrival; the last one
+// (every add has returned before its arrival was issued) sums the slots and writes the values.
+__device__ __forceinline__ void size_record_arrive(SmqSizeRecord* rec, unsigned long long s, int b,
+                                                   int G, int64_t n, int bm, int bo) {
+  if (s) (void)__hip_atomic_fetch_add(rec->slots + (b & 7), s, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long prev = __hip_atomic_fetch_add(&rec->arrived, 1ull, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+  if (prev != (unsigned long long)G - 1ull) return;
+  unsigned long long t = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    t += __hip_atomic_load(rec->slots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  size_record_finish(rec, t, n, bm, bo);
+}
 
 // s_memrealtime stamps (100 MHz) of workgroup milestones, experiment builds only
 #ifndef SMQ_FUSED_TRACE
@@ -330,7 +373,384 @@ __device__ __forceinline__ uint32_t fused_tail(const FusedArgs& A, const ElemCon
   return (uint32_t)bt;
 }
 
+// ------------------------------------------------------------------------------------------------
+// PACK: the single launch that also writes the call's packed stream (smq_smaq_roundtrip_compress:
+// PackedActivations' forward call, util/pytorch/saved.py; format: include/smq.h "Packed SmaQ
+// container"). Group u of workgroup b IS block b * V + u of the format (4096 elements, thread t
+// holding elements 4t .. 4t+3 of it, wave w its rank segment w), so right after the transform has
+// computed a group's codes (the apply's own smaq_quant) the workgroup builds the block from
+// registers: the outlier mask (DPP group ORs), the wm-bit code plane (LDS ORs) -> the fixed section
+// at its index-determined place; the outlier bits above the plane and the escapes (wave scans + the
+// 16 segment counts) -> the block's variable section, kept in LDS. After its V blocks the workgroup
+// publishes their total size as ONE epoch-tagged granule (the statistics granules' epoch: no
+// clearing), sums the granules of the workgroups before it (dispatched earlier: no co-residency
+// assumption) and stores its sections and directory entries at that prefix; the last workgroup
+// writes the header. The stream is byte for byte the one the look-back packer
+// (smaq_pack_lb_kernel) writes after the same round trip — x is read once for y AND the stream.
+// ------------------------------------------------------------------------------------------------
+constexpr int kPkEsc = 128;  // escapes a block's LDS section holds (more: re-coded from x, rare)
+__host__ __device__ inline uint32_t pk_var_words(int we) {
+  return 128u * (uint32_t)we + 2u * kPkEsc;
+}
+// pack area (words): two fixed images (mask + plane), the escape staging (kSegs lists of kSegEsc
+// pairs), the 16 segment counts, 4 x 4 words of block meta, 4 uint64 of the prefix reduction, then
+// the V variable sections
+__host__ __device__ inline uint32_t pk_seg_off(int wm) {
+  return 2u * fixed_words(wm) + 2u * kSegs * kSegEsc;
+}
+__host__ __device__ inline uint32_t pk_meta_off(int wm) { return pk_seg_off(wm) + kSegs; }
+__host__ __device__ inline uint32_t pk_red_off(int wm) { return pk_meta_off(wm) + 16u; }
+__host__ __device__ inline uint32_t pk_var_off(int wm) { return pk_red_off(wm) + 8u; }
+__host__ __device__ inline uint32_t pk_lds_words(int wm, int we, int V) {
+  return pk_var_off(wm) + (uint32_t)V * pk_var_words(we);
+}
+
+// Block B's variable section re-coded from x straight to dst (a block with more escapes than its
+// LDS section holds): 4 passes of 1024 consecutive elements, outlier / escape ranks by wave ballots
+// and the passes' running totals (smaq_pack.hip recode_var_section for a 1024-thread workgroup).
+// ext: 128 * we words of LDS, s_cnt: 16 words.
+template <int RM, int TIN>
+__device__ __noinline__ void fused_recode(const FusedArgs& A, const ElemConsts& c, uint64_t off,
+                                          uint32_t B, uint32_t* dst, uint32_t* ext,
+                                          uint32_t* s_cnt, int wm, int wo) {
+  const int we = wo > wm ? wo - wm : 0;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  const int64_t e0 = (int64_t)B * kPB;
+  const int n_el = (int)min((int64_t)kPB, A.n - e0);
+  const uint32_t hm = 1u << (wm - 1), side = 1u << (wo - 1);
+  for (uint32_t i = tid; i < 128u * (uint32_t)we; i += kSmallT) ext[i] = 0u;
+  __syncthreads();
+  uint32_t n_out = 0u;
+#pragma unroll 1
+  for (int pass = we > 0 ? 0 : 1; pass < 2; ++pass) {
+    uint32_t r_out = 0u, r_esc = 0u;
+    uint32_t* out = dst + ext_words(we, n_out);
+#pragma unroll 1
+    for (int jj = 0; jj < kPB / kSmallT; ++jj) {
+      const int el = jj * kSmallT + tid;
+      bool o = false, esc = false;
+      float q = 0.0f;
+      uint32_t code = 0u;
+      if (el < n_el) {
+        const float u = (RM == kRoundHash) ? rng_hu(A.key, off + (uint64_t)(e0 + el)) : 0.0f;
+        bool hi, lo;
+        q = smaq_quant<RM, false, TIN, true>(load1<TIN>(A.x, e0 + el), u, c, hi, lo);
+        o = hi | lo;
+        code = code_sel(q, o, lo, hm, side, 2u * hm, esc);
+      }
+      const unsigned long long bo = __ballot(o), be = __ballot(esc);
+      const uint32_t ro = __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u));
+      const uint32_t re = __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
+      if (lane == 0) s_cnt[w] = (uint32_t)__popcll(bo) | ((uint32_t)__popcll(be) << 16);
+      __syncthreads();
+      uint32_t before = 0u, tot = 0u;
+#pragma unroll
+      for (int v = 0; v < kSmallWaves; ++v) {
+        const uint32_t t = s_cnt[v];
+        before += v < w ? t : 0u;
+        tot += t;
+      }
+      __syncthreads();
+      if (pass == 1) {
+        const uint32_t ko = r_out + (before & 0xffffu) + ro, ke = r_esc + (before >> 16) + re;
+        if (o && we > 0) or_bits32(ext, (uint32_t)we * ko, code >> wm);
+        if (esc) {
+          out[2u * ke] = (uint32_t)el;
+          out[2u * ke + 1u] = q == q ? __float_as_uint(q) : 0x7fc00000u;
+        }
+      }
+      r_out += tot & 0xffffu;
+      r_esc += tot >> 16;
+    }
+    n_out = r_out;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < ext_words(we, n_out); i += kSmallT) dst[i] = ext[i];
+}
+
+// The transform of the registers (fused_transform) that also packs every group as its block.
+// Returns the outliers counted (the log_size count, as fused_transform).
+template <int RM, int V, int TIN, bool AP, bool SUB, bool PRE, int DL, int WM, int WO>
+__device__ __forceinline__ uint32_t fused_transform_pack(const FusedArgs& A, const float4 (&vr)[V],
+                                                         const float4* park, const float (&uu)[V][4],
+                                                         const ElemConsts& c, int64_t base,
+                                                         uint64_t off, uint32_t* pk) {
+  constexpr int VR = V < 4 ? V : 4;
+  constexpr int kWE = (WM > 0 && WO > 0) ? (WO > WM ? WO - WM : 0) : -1;
+  const int wm = WM > 0 ? WM : A.bm - 1, wo = WO > 0 ? WO : A.bo - 1;
+  const int we = kWE >= 0 ? kWE : (wo > wm ? wo - wm : 0);
+  const uint32_t F = fixed_words(wm), VA = pk_var_words(we);
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  uint32_t* elist = pk + 2u * F;          // [kSegs][kSegEsc][2]
+  uint32_t* seg = pk + pk_seg_off(wm);
+  uint32_t* meta = pk + pk_meta_off(wm);  // [4][4]: words, n_out | n_esc << 16, fits
+  const uint32_t pmask = (1u << wm) - 1u;
+  const uint32_t hm = 1u << (wm - 1), side = 1u << (wo - 1), lim_m = 2u * hm;
+  const uint32_t msh = 4u * (uint32_t)(lane & 7);
+  const bool mwriter = (lane & 7) == 7;
+  const uint32_t ppos0 = 4u * (uint32_t)wm * (uint32_t)tid;
+  const uint32_t pw0 = ppos0 >> 5, psft = ppos0 & 31u;
+  uint32_t n_out_all = 0;
+  float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const uint32_t B = (uint32_t)blockIdx.x * (uint32_t)V + (uint32_t)u;
+    if (B >= A.pk.n_blocks) break;  // (uniform: the grid's last workgroup may hold fewer blocks)
+    const int64_t j = base + (int64_t)u * kSmallT;
+    const bool valid = j < A.nv;
+    const float4 x4 = u < VR ? vr[u] : park[(u - VR) * kSmallT + threadIdx.x];
+    float u0 = uu[u][0], u1 = uu[u][1], u2 = uu[u][2], u3 = uu[u][3];
+    if (u < DL) {
+      const float4 wv = park[((V > 4 ? V - 4 : 0) + u) * kSmallT + threadIdx.x];
+      u0 = wv.x;
+      u1 = wv.y;
+      u2 = wv.z;
+      u3 = wv.w;
+    } else if (RM == kRoundHash && !PRE) {
+      rng_hu4(A.key, off + ((uint64_t)j << 2), u0, u1, u2, u3);
+    }
+    const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+    const float us[4] = {u0, u1, u2, u3};
+    float ys[4];
+    uint32_t code[4], on = 0u, en = 0u;
+    float qv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool hi, lo, esc;
+      qv[i] = smaq_quant<RM, false, TIN, SUB>(xs[i], us[i], c, hi, lo);
+      ys[i] = smaq_dequant<false, AP, false, false>(qv[i], hi, lo, c);
+      const bool o = hi | lo;
+      code[i] = valid ? code_sel(qv[i], o, lo, hm, side, lim_m, esc) : 0u;
+      on |= (valid && o) ? (1u << i) : 0u;
+      en |= (valid && esc) ? (1u << i) : 0u;
+    }
+    if (valid) {
+      store_stream(y4 + j, make_float4(ys[0], ys[1], ys[2], ys[3]));
+      n_out_all += (uint32_t)__popc(on);
+    }
+    uint32_t* img = pk + (uint32_t)(u & 1) * F;
+    uint32_t* mask = img;
+    uint32_t* plane = img + kMaskWords;
+    uint32_t* var = pk + pk_var_off(wm) + (uint32_t)u * VA;
+    // outlier mask: the nibbles of 8 consecutive lanes make a word
+    const uint32_t mw = group8_or_to_last(on << msh);
+    if (mwriter) mask[tid >> 3] = mw;
+    // plane: the low wm bits of the 4 codes at bit wm * 4t
+    if (4 * wm <= 32) {
+      uint32_t ch = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ch |= (code[i] & pmask) << (wm * i);
+      atomicOr(plane + pw0, ch << psft);
+      if (psft + 4u * (uint32_t)wm > 32u) atomicOr(plane + pw0 + 1, ch >> (32u - psft));
+    } else if (wm <= 16) {
+      uint64_t ch = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ch |= (uint64_t)(code[i] & pmask) << (wm * i);
+      if (ch) or_bits64(plane, ppos0, ch);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {
+        const uint64_t ch = (uint64_t)(code[i] & pmask) | ((uint64_t)(code[i + 1] & pmask) << wm);
+        if (ch) or_bits64(plane, (uint32_t)wm * (uint32_t)(4 * tid + i), ch);
+      }
+    }
+    // outlier bits above the plane, in element order
+    uint64_t ech = 0u;
+    uint32_t ev[4] = {0u, 0u, 0u, 0u};
+    if (we > 0) {
+      if (4 * we <= 32) {
+        const uint32_t s1 = (uint32_t)we * (on & 1u);
+        const uint32_t s2 = (uint32_t)we * (uint32_t)__popc(on & 3u);
+        const uint32_t s3 = (uint32_t)we * (uint32_t)__popc(on & 7u);
+        ech = (code[0] >> wm) | ((code[1] >> wm) << s1) | ((code[2] >> wm) << s2) |
+              ((code[3] >> wm) << s3);
+      } else if (we <= 16) {
+        uint32_t sft = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if ((on >> i) & 1u) {
+            ech |= (uint64_t)(code[i] >> wm) << sft;
+            sft += (uint32_t)we;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ev[i] = code[i] >> wm;
+      }
+    }
+    const uint32_t cnt = (uint32_t)__popc(on) | ((uint32_t)__popc(en) << 16);
+    const uint32_t incl = wave_incl_scan_u32(cnt);
+    const uint32_t pre = incl - cnt;
+    if (lane == kWave - 1) seg[w] = incl;
+    uint32_t gfirst = 0u;
+    if (kWE == 2) {  // the 8 lanes of a group own consecutive ranks: one run in the last lane
+      const uint32_t po = pre & 0xffffu;
+      gfirst = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (lane & ~7), (int)po);
+      const uint64_t ch = (uint64_t)(uint32_t)ech << (2u * (po - gfirst));
+      const uint32_t glo = group8_or_to_last((uint32_t)ch), ghi = group8_or_to_last((uint32_t)(ch >> 32));
+      ech = ((uint64_t)ghi << 32) | glo;
+    }
+    if (__builtin_expect(en != 0u, 0)) {  // escapes (rare): the segment's list at their rank
+      uint32_t r = pre >> 16;
+      uint32_t* L = elist + 2 * kSegEsc * w;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if ((en >> i) & 1u) {
+          if (r < (uint32_t)kSegEsc) {
+            const float qe = qv[i];
+            L[2 * r] = 4u * (uint32_t)tid + (uint32_t)i;
+            L[2 * r + 1] = qe == qe ? __float_as_uint(qe) : 0x7fc00000u;
+          }
+          ++r;
+        }
+      }
+    }
+    lds_barrier();
+    // the other image's plane for the next block (its last reader, block u - 1's fixed store, is
+    // behind the barrier above; its first writer, block u + 1, behind the one below)
+    if (u + 1 < V) {
+      uint32_t* np = pk + (uint32_t)((u + 1) & 1) * F + kMaskWords;
+      for (uint32_t i = tid; i < 128u * (uint32_t)wm; i += kSmallT) np[i] = 0u;
+    }
+    // segment bases (lanes 0-15 of every wave scan the 16 counts by DPP row shifts)
+    const uint32_t own = lane < kSegs ? seg[lane] : 0u;
+    uint32_t sincl = own;
+    sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x111, 0xf, 0xf, false);
+    sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x112, 0xf, 0xf, false);
+    sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x114, 0xf, 0xf, false);
+    sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x118, 0xf, 0xf, false);
+    const uint32_t sexcl = sincl - own;
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)sincl, kSegs - 1);
+    const bool seg_over = __ballot(lane < kSegs && (own >> 16) > (uint32_t)kSegEsc) != 0ull;
+    const uint32_t n_o = tot & 0xffffu, n_e = tot >> 16;
+    const uint32_t n_ext = ext_words(we, n_o);
+    const bool fits = !seg_over && n_e <= (uint32_t)kPkEsc;
+    const uint32_t sbase = (uint32_t)__builtin_amdgcn_readlane((int)sexcl, w);
+    if (we > 0 && (kWE == 2 || on)) {
+      if (kWE == 2) {
+        if (mwriter && ech) or_bits64(var, 2u * ((sbase & 0xffffu) + gfirst), ech);
+      } else {
+        const uint32_t r_out = (sbase + pre) & 0xffffu;
+        if (4 * we <= 32) {
+          or_bits32(var, (uint32_t)we * r_out, (uint32_t)ech);
+        } else if (we <= 16) {
+          or_bits64(var, (uint32_t)we * r_out, ech);
+        } else {
+          uint32_t r = r_out;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if ((on >> i) & 1u) or_bits64(var, (uint32_t)we * r++, ev[i]);
+        }
+      }
+    }
+    // escapes: lane l of wave w copies entry l of segment w's list to its rank
+    if (fits && n_e) {
+      const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)own, w) >> 16;
+      if ((uint32_t)lane < sc) {
+        const uint32_t* L = elist + 2 * kSegEsc * w;
+        const uint32_t r = (sbase >> 16) + (uint32_t)lane;
+        var[n_ext + 2u * r] = L[2 * lane];
+        var[n_ext + 2u * r + 1u] = L[2 * lane + 1];
+      }
+    }
+    if (tid == 0) {
+      meta[4 * u] = n_ext + 2u * n_e;
+      meta[4 * u + 1] = n_o | (n_e << 16);
+      meta[4 * u + 2] = fits ? 1u : 0u;
+    }
+    lds_barrier();
+    // the fixed section (mask + plane, F words) at B * F, 16-B stores
+    uint4* fdst = reinterpret_cast<uint4*>(A.pk.fixed + (size_t)B * F);
+    const uint4* fsrc = reinterpret_cast<const uint4*>(img);
+    for (uint32_t i = tid; i < F / 4u; i += kSmallT) fdst[i] = fsrc[i];
+  }
+  return n_out_all;
+}
+
+// After the transform: the workgroup's blocks' variable sections and directory entries at the
+// prefix of the workgroups before it, the header by the last one.
 template <int RM, int V, int TIN>
+__device__ __forceinline__ void fused_pack_finish(const FusedArgs& A, const ElemConsts& c,
+                                                  uint64_t off, uint32_t epoch,
+                                                  const SmqSmaqStats& st, uint32_t* pk) {
+  const int wm = A.bm - 1, wo = A.bo - 1, we = wo > wm ? wo - wm : 0;
+  const uint32_t VA = pk_var_words(we);
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  const int b = blockIdx.x, G = A.G;
+  const uint32_t* meta = pk + pk_meta_off(wm);
+  unsigned long long* s_red = reinterpret_cast<unsigned long long*>(pk + pk_red_off(wm));
+  const uint32_t B0 = (uint32_t)b * (uint32_t)V;
+  const int nbk = (int)min((uint32_t)V, A.pk.n_blocks - B0);
+  uint32_t agg = 0u;
+  for (int u = 0; u < nbk; ++u) agg += meta[4 * u];
+  if (tid == 0 && b + 1 < G)  // (the last workgroup's aggregate is nobody's prefix)
+    st_sc1_u64(A.pk.look + b, ((unsigned long long)epoch << 32) | agg);
+  // the aggregates of workgroups 0 .. b-1 (dispatched before this one), one per thread
+  unsigned long long v = 0ull;
+  if (tid < b) {
+    for (;;) {
+      const unsigned long long g = ld_sc1_u64(A.pk.look + tid);
+      if ((uint32_t)(g >> 32) == epoch) {
+        v = g & 0xffffffffull;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  if (b > 0) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    if (lane == 0 && w < 4) s_red[w] = v;  // (b < 256: waves 0-3 hold the aggregates)
+  }
+  lds_barrier();
+  uint64_t vb = b > 0 ? (uint64_t)(s_red[0] + s_red[1] + s_red[2] + s_red[3]) : 0ull;
+  for (int u = 0; u < nbk; ++u) {
+    const uint32_t B = B0 + (uint32_t)u;
+    const uint32_t words = meta[4 * u], cnt = meta[4 * u + 1];
+    if (tid == 0)
+      A.pk.dir[B] = vb | ((uint64_t)(cnt & 0xffffu) << 38) | ((uint64_t)(cnt >> 16) << 51);
+    if (vb + words <= A.pk.cap_words) {  // (a capacity-bounded stream: sections past it unwritten)
+      uint32_t* src = pk + pk_var_off(wm) + (uint32_t)u * VA;
+      uint32_t* dst = A.pk.var + vb;
+      if (meta[4 * u + 2]) {
+        for (uint32_t i = tid; i < words; i += kSmallT) dst[i] = src[i];
+      } else {  // more escapes than its LDS section holds: re-coded from x (its area as scratch)
+        fused_recode<RM, TIN>(A, c, off, B, dst, src, pk + pk_seg_off(wm), wm, wo);
+      }
+    }
+    vb += words;
+  }
+  if (b == G - 1 && tid == 0) {  // every workgroup's aggregate is in vb: the header
+    SmqPackedHeader* h = A.pk.hdr;
+    h->magic = SMQ_PACK_MAGIC;
+    h->version = SMQ_PACK_VERSION;
+    h->n = A.n;
+    h->block_elems = kPB;
+    h->n_blocks = A.pk.n_blocks;
+    h->num_bits_main = A.bm;
+    h->num_bits_outlier = A.bo;
+    h->flags = A.pk.flags;
+    h->thr = A.thr;
+    h->range_main = A.r_main;
+    h->range_outlier = A.r_out;
+    h->mean = st.mean;
+    h->std_dev = st.std_dev;
+    h->inv_range_main = A.inv_r_main;
+    h->inv_range_outlier = A.inv_r_out;
+    h->data_words = vb;
+    h->total_bytes = sizeof(SmqPackedHeader) + 8ull * dir_entries(A.pk.n_blocks) +
+                     4ull * A.pk.n_blocks * fixed_words(wm) + 4ull * vb;
+    h->error = 0u;
+    h->bn_channels = 0u;
+    h->bn_inner = 0;
+    h->mean_f64 = 0.0;
+    h->std_dev_f64 = 0.0;
+    h->reserved[0] = h->reserved[1] = 0u;
+    if (A.pk.n_blocks & 1u) A.pk.dir[A.pk.n_blocks] = 0ull;  // the directory's padding entry
+  }
+}
+
+template <int RM, int V, int TIN, bool PACK = false, int PWM = 0, int PWO = 0>
 __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   __shared__ SmallWaveLds W;
   __shared__ SmqSmaqStats sst;
@@ -363,6 +783,12 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   // consumed them: registers for more than four groups would spill across the gather
   constexpr int VR = V < 4 ? V : 4;
   extern __shared__ float4 park[];
+  uint32_t* pk = reinterpret_cast<uint32_t*>(park) + A.pk.lds_off;  // (PACK)
+  if constexpr (PACK) {  // the planes and outlier-bit areas are built by ORs: zero, loads in flight
+    const int wm = A.bm - 1, we = A.bo > A.bm ? A.bo - A.bm : 0;
+    const uint32_t words = pk_lds_words(wm, we, V);
+    for (uint32_t i = threadIdx.x; i < words; i += kSmallT) pk[i] = 0u;
+  }
   const double shift = stats_shift<TIN>(A.x, A.n);
   const uint32_t gen = G > 1 ? ld_sc1_u32(A.gen) : 0u;
   const uint64_t ctr_word = A.ctr ? ld_sc1_u64(A.ctr) : 0ull;
@@ -580,7 +1006,17 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   uniform_consts(c);  // LDS reads land in VGPRs: the constants are wave-uniform, keep them in SGPRs
   const bool tail = b == G - 1 && threadIdx.x < (int)(A.n & 3);
   uint32_t n_out;
-  if (sst.quot_check) {
+  if constexpr (PACK) {
+    if (sst.quot_check) {
+      n_out = A.all_pos
+                  ? fused_transform_pack<RM, V, TIN, true, true, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk)
+                  : fused_transform_pack<RM, V, TIN, false, true, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk);
+    } else {
+      n_out = A.all_pos
+                  ? fused_transform_pack<RM, V, TIN, true, false, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk)
+                  : fused_transform_pack<RM, V, TIN, false, false, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk);
+    }
+  } else if (sst.quot_check) {
     if (A.all_pos) {
       n_out = fused_transform<RM, V, TIN, true, true, PRE, DL>(A, v, park, uu, c, base, off);
       if (tail) n_out += fused_tail<RM, TIN, true, true>(A, c, off);
@@ -615,9 +1051,11 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       unsigned long long s = 0;
 #pragma unroll
       for (int w = 0; w < kSmallWaves; ++w) s += sh_cnt[w];
-      if (s) atomicAdd(A.out_slots + (b & (SMQ_WS_OUTLIER_SLOTS - 1)), s);
+      if (A.rec) size_record_arrive(A.rec, s, b, G, A.n, A.bm, A.bo);
+      else if (s) atomicAdd(A.out_slots + (b & (SMQ_WS_OUTLIER_SLOTS - 1)), s);
     }
   }
+  if constexpr (PACK) fused_pack_finish<RM, V, TIN>(A, c, off, epoch, sst, pk);
   // the last workgroup of its residue arrives on the top word; the last residue's advances the
   // generation and the stream and re-arms the arrival words. Every workgroup has read the
   // generation, the stream position and the granules before its add.
@@ -699,11 +1137,10 @@ static int launch_fused_rm(const FusedArgs& F, int V, hipStream_t st) {
   }
 }
 
-int launch_fused(const FusedCall& c, hipStream_t st) {
+static void fused_args(const FusedCall& c, FusedArgs& F) {
   const SmqSmaqParams* p = c.p;
   const SmallGeom g = small_geom(c.n);
   char* base = (char*)c.ws;
-  FusedArgs F;
   memset(&F, 0, sizeof(F));
   F.x = c.x;
   F.y = c.y;
@@ -743,7 +1180,18 @@ int launch_fused(const FusedCall& c, hipStream_t st) {
   if (c.ws_bytes >= SmaqWsLayout::kTotal + 16 * 8 * (size_t)kSmallMaxG)
     F.trace = (uint64_t*)(base + SmaqWsLayout::kTotal);
 #endif
-  if (p->count_outliers) fill_async(F.out_slots, 0ull, SMQ_WS_OUTLIER_SLOTS, st);
+  F.rec = c.rec;
+  F.bm = p->num_bits_main;
+  F.bo = p->num_bits_outlier;
+  if (c.rec) F.count = 1;  // (the record's slots are zero: no fill)
+}
+
+int launch_fused(const FusedCall& c, hipStream_t st) {
+  const SmqSmaqParams* p = c.p;
+  const SmallGeom g = small_geom(c.n);
+  FusedArgs F;
+  fused_args(c, F);
+  if (!c.rec && p->count_outliers) fill_async(F.out_slots, 0ull, SMQ_WS_OUTLIER_SLOTS, st);
   const bool sr = p->stochastic_rounding != 0;
   if (c.dtype == SMQ_DTYPE_F32)
     return sr ? launch_fused_rm<kRoundHash, kF32>(F, g.V, st)
@@ -753,6 +1201,69 @@ int launch_fused(const FusedCall& c, hipStream_t st) {
               : launch_fused_rm<kRoundTrunc, kF16>(F, g.V, st);
   return sr ? launch_fused_rm<kRoundHash, kBF16>(F, g.V, st)
             : launch_fused_rm<kRoundTrunc, kBF16>(F, g.V, st);
+}
+
+// ---- PACK (smq_smaq_roundtrip_compress) ---------------------------------------------------------
+template <int RM, int V, int WM, int WO>
+static int launch_fused_pack_v(FusedArgs& F, hipStream_t st) {
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&smaq_fused_kernel<RM, V, kF32, true, WM, WO>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLds);
+  if (attr != hipSuccess) {
+    set_error("smaq_fused_kernel (PACK): hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed: %s",
+              hipGetErrorString(attr));
+    return SMQ_ERR_LAUNCH;
+  }
+  const int wm = F.bm - 1, we = F.bo > F.bm ? F.bo - F.bm : 0;
+  const int need = 4 * (int)(F.pk.lds_off + pk_lds_words(wm, we, V));
+  const int lds = need > fused_lds_bytes(V) ? need : fused_lds_bytes(V);
+  hipLaunchKernelGGL((smaq_fused_kernel<RM, V, kF32, true, WM, WO>), dim3((unsigned)F.G),
+                     dim3(kSmallT), lds, st, F);
+  return check_launch("smaq_fused_kernel (PACK)");
+}
+
+template <int RM, int WM, int WO>
+static int launch_fused_pack_rm(FusedArgs& F, int V, hipStream_t st) {
+  switch (V) {
+    case 1: return launch_fused_pack_v<RM, 1, WM, WO>(F, st);
+    case 2: return launch_fused_pack_v<RM, 2, WM, WO>(F, st);
+    case 3: return launch_fused_pack_v<RM, 3, WM, WO>(F, st);
+    default: return launch_fused_pack_v<RM, 4, WM, WO>(F, st);
+  }
+}
+
+int launch_fused_pack(const FusedCall& c, const FusedPackCall& k, hipStream_t st) {
+  const SmqSmaqParams* p = c.p;
+  // fp32 x (16-B aligned: fused_eligible), whole float4 groups, full statistics without the
+  // range form (its granules would overlap the aggregates'), T_m > 0, no BN term, V <= 4
+  if (c.dtype != SMQ_DTYPE_F32 || (c.n & 3) || p->use_range_std_dev || p->bn_gamma ||
+      !(p->main_std_dev_threshold > 0.0f) || c.rec)
+    return kFusedPackDeclined;
+  const SmallGeom g = small_geom(c.n);
+  const int wm = p->num_bits_main - 1, wo = p->num_bits_outlier - 1;
+  const int we = wo > wm ? wo - wm : 0;
+  if (g.V > 4 || wm < 1 || wm > kMaxWidth || wo < 2 || wo > kMaxWidth) return kFusedPackDeclined;
+  const uint32_t lds_off = (uint32_t)fused_draw_groups(g.V) * kSmallT * 4u;  // after the draws
+  if (4ull * (lds_off + pk_lds_words(wm, we, g.V)) > (unsigned long long)kFusedLds)
+    return kFusedPackDeclined;
+  FusedArgs F;
+  fused_args(c, F);
+  F.pk.hdr = k.hdr;
+  F.pk.dir = k.dir;
+  F.pk.fixed = k.fixed;
+  F.pk.var = k.var;
+  F.pk.cap_words = k.cap_words;
+  F.pk.n_blocks = k.n_blocks;
+  F.pk.flags = k.flags;
+  F.pk.look = F.gran + SmaqWsLayout::kFusedPackLook;
+  F.pk.lds_off = lds_off;
+  if (p->count_outliers) fill_async(F.out_slots, 0ull, SMQ_WS_OUTLIER_SLOTS, st);
+  const bool sr = p->stochastic_rounding != 0;
+  if (wm == 5 && wo == 7)  // the 6/8-bit default
+    return sr ? launch_fused_pack_rm<kRoundHash, 5, 7>(F, g.V, st)
+              : launch_fused_pack_rm<kRoundTrunc, 5, 7>(F, g.V, st);
+  return sr ? launch_fused_pack_rm<kRoundHash, 0, 0>(F, g.V, st)
+            : launch_fused_pack_rm<kRoundTrunc, 0, 0>(F, g.V, st);
 }
 
 }  // namespace smq

@@ -18,6 +18,12 @@ int prepare_stats(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, v
 int roundtrip_for_pack(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
                        void* ws, size_t ws_bytes, hipStream_t st, uint32_t* zero, uint32_t zero_n,
                        bool* zeroed);
+// smq_smaq_roundtrip_compress's y AND stream from one launch where its shape allows (the single
+// launch's PACK variant, smaq_fused.hip): kFusedPackDeclined (smaq_small.h) when it does not —
+// nothing enqueued then.
+struct FusedPackCall;
+int roundtrip_pack_fused(const void* x, int dtype, float* y, int64_t n, const SmqSmaqParams* p,
+                         void* ws, size_t ws_bytes, const FusedPackCall& k, hipStream_t st);
 // Full statistics of x (the single-tensor statistics launch, finalised by its last workgroup) into
 // *out instead of the workspace header (multi-tensor calls: tensors above the small partition).
 int stats_into(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, void* ws,

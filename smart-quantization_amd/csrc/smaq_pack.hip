@@ -37,27 +37,13 @@
 
 #include "smaq_elem.h"
 #include "smaq_host.h"
+#include "smaq_pack_common.h"
+#include "smaq_small.h"
 #include "smq.h"
 #include "smq_common.h"
 
 namespace smq {
 namespace {
-
-constexpr int kPB = SMQ_PACK_BLOCK;          // 4096 elements per block
-constexpr int kMaskWords = kPB / 32;         // 128
-constexpr int kMaxWidth = 24;                // widest code (num_bits - 1)
-constexpr int kGroup = 64;                   // blocks per group sum (one per lane of a wave)
-constexpr int kVarCap = 768;                 // scratch words per block for its variable section
-constexpr int kSegs = 16;                    // rank segments of a block: 4 slots x 4 waves
-
-static_assert(sizeof(SmqPackedHeader) == 128, "packed header layout");
-
-// directory entries incl. the padding that keeps the fixed region 16-B aligned
-__host__ __device__ inline int64_t dir_entries(int64_t nb) { return (nb + 1) & ~(int64_t)1; }
-__host__ __device__ inline uint32_t fixed_words(int wm) { return kMaskWords + 128u * (uint32_t)wm; }
-__host__ __device__ inline uint32_t ext_words(int we, uint32_t n_out) {
-  return ((uint32_t)we * n_out + 31u) / 32u;
-}
 
 struct PackArgs {
   const void* x;
@@ -116,23 +102,6 @@ __device__ __forceinline__ float pack_quant(float v, float u, const ElemConsts& 
   return f + __builtin_rintf(t);
 }
 
-// Code of one element (smq.h format rules), branch-free integer form: v = q + 2^(wm-1) for a main
-// (fits: v < 2^wm; the code is v ^ 2^(wm-1) = q's wm-bit two's complement), |q| on the element's
-// side for an outlier (fits: v < 2^(wo-1); the code is side << (wo-1) | v). |q| > 2^24, inf and NaN
-// always escape; an escaped main codes 0, an escaped outlier its side bit alone.
-// hm = 2^(wm-1), side = 2^(wo-1), lim_m = 2^wm
-__device__ __forceinline__ uint32_t code_sel(float q, bool o, bool lo, uint32_t hm, uint32_t side,
-                                             uint32_t lim_m, bool& esc) {
-  const int qi = (int)q;
-  const bool big = !(__builtin_fabsf(q) <= 0x1p24f);     // also NaN
-  const uint32_t hsel = o ? 0u : hm;
-  const uint32_t vv = lo ? (uint32_t)(-qi) : (uint32_t)qi + hsel;
-  const uint32_t lim = o ? side : lim_m;
-  esc = big | !(vv < lim);
-  const uint32_t sb = lo ? side : 0u;
-  return esc ? sb : ((vv ^ hsel) | sb);
-}
-
 // The general packer's element (EXT kernels: the BN variant, T_m <= 0): smaq_quant itself, the
 // apply's own function, with the BN term of element e. The mask bit is "exactly one side" (o); an
 // element with both sides (T_m < 0) codes as a main element; lo_side = below -T_m alone.
@@ -161,28 +130,6 @@ __device__ __forceinline__ float pack_cthr(const PackArgs& A) {
 // Keep a (uniform) value in a VGPR: an empty asm the compiler cannot see through.
 #define PIN_VGPR(v) asm volatile("" : "+v"(v))
 
-// OR a chunk of up to 64 bits at bit pos of an LDS bit stream (two or three words; the third only
-// when bits land there).
-__device__ __forceinline__ void or_bits64(uint32_t* base, uint32_t pos, uint64_t chunk) {
-  const uint32_t sft = pos & 31u, w0 = pos >> 5;
-  const uint64_t lo = chunk << sft;
-  const uint32_t hi = sft ? (uint32_t)(chunk >> (64u - sft)) : 0u;
-  if ((uint32_t)lo) atomicOr(base + w0, (uint32_t)lo);
-  if ((uint32_t)(lo >> 32)) atomicOr(base + w0 + 1, (uint32_t)(lo >> 32));
-  if (hi) atomicOr(base + w0 + 2, hi);
-}
-
-// OR a chunk of up to 32 bits at bit pos of an LDS bit stream (one or two words).
-__device__ __forceinline__ void or_bits32(uint32_t* base, uint32_t pos, uint32_t chunk) {
-  const uint32_t sft = pos & 31u, w0 = pos >> 5;
-  atomicOr(base + w0, chunk << sft);
-  const uint32_t hi = sft ? (chunk >> (32u - sft)) : 0u;
-  if (hi) atomicOr(base + w0 + 1, hi);
-}
-
-// Escapes of one rank segment (256 elements) a block keeps in LDS before the segment bases are
-// known; a segment with more (an escape-heavy block) makes the var kernel re-code the block.
-constexpr int kSegEsc = 32;
 // meta bit: the block's variable section is not in its scratch slot (re-code it)
 constexpr uint32_t kMetaRecode = 1u << 31;
 
@@ -931,6 +878,7 @@ struct UnpackArgs {
   uint32_t n_full;     // blocks of SMQ_PACK_BLOCK elements
   uint32_t lds_bytes;  // dynamic LDS of the launch (the widths' need, or the widest)
   uint32_t big_per;    // smaq_unpack_big_kernel: full blocks per workgroup (rare_per, <= kBlock)
+  uint32_t per;        // full blocks per workgroup of the main body (1 .. kUnpackPer)
 };
 
 // Decode table of narrow codes (both widths <= 8 bits: the 6/8-bit default): every main code
@@ -1372,8 +1320,8 @@ __device__ __forceinline__ void unpack_run(UnpackArgs A, uint32_t b0, int nblk, 
 // WM / WO: the 6/8-bit default's widths, or 0 (any widths, from the caller or the header).
 template <int WM, int WO, bool FULL>
 __device__ __forceinline__ void unpack_main_body(const UnpackArgs& A, uint32_t g, uint32_t* lds) {
-  const uint32_t b0 = FULL ? g * (uint32_t)kUnpackPer : A.nb - 1;
-  const int nblk = FULL ? (int)min((uint32_t)kUnpackPer, A.n_full - b0) : 1;
+  const uint32_t b0 = FULL ? g * A.per : A.nb - 1;
+  const int nblk = FULL ? (int)min(A.per, A.n_full - b0) : 1;
   // the stream is this call's (magic, n) before any directory entry is read: a caller's n beyond
   // the stream's would index past its directory (one scalar load; the rest of the header is
   // checked in unpack_run)
@@ -1587,6 +1535,22 @@ static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParam
   uint32_t* zero = lb ? (uint32_t*)(wb + L.scratch) : (uint32_t*)(wb + L.gsum);
   const uint32_t zero_n = lb ? 2u * (uint32_t)nb : n_groups;
   bool zeroed = false;
+  if (y && lb && (!pst || pst == st)) {
+    // the round trip's single launch writes the stream too (smaq_fused.hip PACK): x read once
+    const int wm = p->num_bits_main - 1;
+    FusedPackCall k;
+    k.hdr = (SmqPackedHeader*)packed;
+    k.dir = (uint64_t*)((char*)packed + sizeof(SmqPackedHeader));
+    k.fixed = (uint32_t*)(k.dir + dir_entries(nb));
+    k.var = k.fixed + (size_t)nb * fixed_words(wm);
+    k.cap_words = packed_bytes >= bound ? ~0ull : (uint64_t)((packed_bytes - fixed) / 4);
+    k.n_blocks = (uint32_t)nb;
+    const RangeRecips R0 = range_recips(p->range_main, p->range_outlier);
+    k.flags = (p->all_positive ? SMQ_PACK_FLAG_ALL_POSITIVE : 0u) |
+              (R0.safe_q ? SMQ_PACK_FLAG_SAFE_Q : 0u);
+    rc = roundtrip_pack_fused(x, dtype, y, n, p, ws, L.meta, k, st);
+    if (rc != kFusedPackDeclined) return rc;
+  }
   if (y)
     rc = roundtrip_for_pack(x, dtype, y, n, p, ws, L.meta, st, zero, zero_n, &zeroed);
   else
@@ -1742,7 +1706,11 @@ static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int 
   // another by their workgroup: about 1024 workgroups, so a tensor's big blocks decode in parallel
   A.big_per = rare_per(A.n_full);
   if (A.big_per > (uint32_t)kBlock) A.big_per = kBlock;
-  const unsigned grid = (unsigned)((A.n_full + kUnpackPer - 1) / kUnpackPer);
+  // up to 1024 blocks (the activation sizes: 64 - 1024 blocks, a fraction of the chip's 8 decoder
+  // workgroups per CU) one block per workgroup, so a small stream's blocks decode side by side;
+  // above, two (both blocks' loads in flight before the first is decoded)
+  A.per = A.nb <= 1024u ? 1u : (uint32_t)kUnpackPer;
+  const unsigned grid = (unsigned)((A.n_full + A.per - 1) / A.per);
   const bool w57 = bm == 6 && bo == 8;  // the default widths, known from the caller
   const unsigned big_g = grid ? (unsigned)((A.n_full + A.big_per - 1) / A.big_per) : 0u;
   const bool small = A.nb <= kLbMaxBlocks;  // one launch (smaq_unpack_small_kernel)

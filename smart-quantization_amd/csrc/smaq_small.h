@@ -281,7 +281,22 @@ struct FusedCall {
   size_t ws_bytes;
   uint32_t* zero = nullptr;  // words the launch clears (the packer's group sums), or NULL
   uint32_t zero_n = 0;
+  SmqSizeRecord* rec = nullptr;  // smq_smaq_roundtrip_counted: count into it, last workgroup
+                                 // writes the log_size values (no fill, no extra launch)
 };
 int launch_fused(const FusedCall& c, hipStream_t st);
+
+// The single launch that also writes the call's packed stream (smq_smaq_roundtrip_compress,
+// smaq_fused.hip PACK): the stream's regions (include/smq.h "Packed SmaQ container").
+struct FusedPackCall {
+  SmqPackedHeader* hdr;
+  uint64_t* dir;
+  uint32_t* fixed;
+  uint32_t* var;
+  uint64_t cap_words;  // words of the variable region the buffer holds
+  uint32_t n_blocks, flags;
+};
+constexpr int kFusedPackDeclined = 1;  // not this call's shape: nothing launched
+int launch_fused_pack(const FusedCall& c, const FusedPackCall& k, hipStream_t st);
 
 }  // namespace smq

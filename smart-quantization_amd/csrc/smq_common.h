@@ -412,6 +412,10 @@ struct SmaqWsLayout {
   static constexpr int kFusedRep = 8;
   static constexpr int kFusedWords = 6;  // s1 low / high, s2 low / high, min, max
   static constexpr size_t kFusedEnd = kFusedGran + 8 * (size_t)kFusedRep * kFusedWords * 256;
+  // the PACK variant's per-workgroup aggregates (granule index in replica 0, behind the 4-word
+  // partials of 256 workgroups; the range form's 6-word partials, which it never runs with, reach
+  // here but carry other calls' epochs)
+  static constexpr size_t kFusedPackLook = 1024;
   static constexpr size_t kTotal = kFusedEnd;
 };
 static_assert(SmaqWsLayout::kTagCounters + 8 * SmaqWsLayout::kTagWords <= SMQ_WS_FUSED_OFFSET,

@@ -11,7 +11,9 @@
 // workspace lookup, the offset update, the argument conversion), the Python autograd Function
 // around it as much again in each direction. Here:
 //
-//   smaq(state, x, all_positive, bn)        one SmartFP call on the at::Tensor (smq_smaq_roundtrip)
+//   smaq(state, x, all_positive, bn)        one SmartFP call on the at::Tensor (smq_smaq_roundtrip;
+//                                           with ratio logging smq_smaq_roundtrip_counted and
+//                                           (y, values): the log_size values stay on the device)
 //   smaq_autograd(state, x, codec, bwd)     Compressor.forward for a SmartFP codec: the forward
 //                                           call plus a C++ Node whose backward compresses the
 //                                           grad-map the same way (autograd.py:37-47)
@@ -24,7 +26,7 @@
 // block, built by the Python codec from its hparams, and a snapshot of the hparams values they were
 // built from: a flag changed between calls returns NotImplemented and the codec rebuilds the state.
 // Anything this path does not handle (CPU tensors, float64, sampled or range statistics, BN terms,
-// ratio logging, graph-safe streams, tensors below min_size) returns None and the codec takes its
+// graph-safe streams, tensors below min_size) returns None and the codec takes its
 // general Python path (in the backward node: the Python codec object is called). Values are those
 // of the Python path bit for bit: the same entry point, parameter block and stream positions, taken
 // in the same call order. Host code only; nothing here crosses the C-ABI (include/smq.h).
@@ -33,6 +35,7 @@
 
 #include <ATen/core/Tensor.h>
 #include <ATen/ops/empty.h>
+#include <ATen/ops/zeros.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/csrc/autograd/function.h>
 #include <torch/csrc/autograd/functions/utils.h>
@@ -95,6 +98,36 @@ bool ws_lookup(WsSlot& w, PyObject* getter, int dev, hipStream_t st, size_t need
   return true;
 }
 
+// --measure_compression_ratio: one zeroed SmqSizeRecord per call (smq_smaq_roundtrip_counted) from
+// a pool per (device, stream) — one zero-fill per kPoolRecs calls, on the stream that uses the
+// records. The values the logger gets are views of the record (kept alive by them).
+constexpr int64_t kPoolRecs = 2048;
+constexpr int64_t kRecWords = (int64_t)(sizeof(SmqSizeRecord) / 8);  // 16
+static_assert(sizeof(SmqSizeRecord) == 128, "SmqSizeRecord layout");
+struct RecPool {
+  int dev = -1;
+  hipStream_t st = nullptr;
+  at::Tensor buf;  // int64 [kPoolRecs * kRecWords]
+  int64_t next = kPoolRecs;
+};
+RecPool g_rec_pool;
+
+// The next record (its device pointer) and the fp64 view [n_outlier, new_size, ratio, orig_size]
+// of its values.
+SmqSizeRecord* rec_take(const at::Tensor& like, hipStream_t st, at::Tensor* values) {
+  RecPool& P = g_rec_pool;
+  const int dev = like.get_device();
+  if (P.next >= kPoolRecs || P.dev != dev || P.st != st) {
+    P.buf = at::zeros({kPoolRecs * kRecWords}, like.options().dtype(at::kLong));
+    P.dev = dev;
+    P.st = st;
+    P.next = 0;
+  }
+  const int64_t i = P.next++;
+  *values = P.buf.view(at::kDouble).narrow(0, i * kRecWords + 12, 4);
+  return reinterpret_cast<SmqSizeRecord*>(P.buf.data_ptr<int64_t>() + i * kRecWords);
+}
+
 // rng.__dict__ holds seed / offset (smart_compress_amd/_native.py RngState); the call takes n
 // positions of the stream, under the GIL, as RngState.take.
 PyObject* g_seed = nullptr;
@@ -132,7 +165,8 @@ struct SmaqState {
   int64_t min_size = 8;
   bool allow_f16 = false;  // precision 16 (smart.py:154's clamp on a half tensor otherwise raises)
   bool use_bn = false;
-  bool decline = false;    // range or sampled statistics, ratio logging: the Python path
+  bool decline = false;    // range or sampled statistics: the Python path
+  bool count = false;      // --measure_compression_ratio: counted calls (smq_smaq_roundtrip_counted)
   PyRef hp_dict;           // hparams.__dict__
   PyRef snap[kSnap];       // its values when the templates were built
   PyRef rng_dict;          // codec.rng.__dict__
@@ -183,11 +217,27 @@ PyObject* smaq_state(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
     Py_XINCREF(v);
     s->snap[i].o = v;
   }
-  if (s->snap[8].o) s->min_size = PyLong_AsLongLong(s->snap[8].o);
-  s->allow_f16 = s->snap[9].o && PyLong_AsLong(s->snap[9].o) == 16;
+  // min_size / precision other than Python ints (a hand-built Namespace, a config file): the
+  // Python path, which accepts them, serves the calls
+  if (s->snap[8].o) {
+    s->min_size = PyLong_Check(s->snap[8].o) ? PyLong_AsLongLong(s->snap[8].o) : -1;
+    if (s->min_size == -1 && (PyErr_Occurred() || !PyLong_Check(s->snap[8].o))) {
+      PyErr_Clear();
+      s->decline = true;
+    }
+  }
+  if (s->snap[9].o) {
+    const long prec = PyLong_Check(s->snap[9].o) ? PyLong_AsLong(s->snap[9].o) : -1;
+    if (prec == -1 && (PyErr_Occurred() || !PyLong_Check(s->snap[9].o))) {
+      PyErr_Clear();
+      s->decline = true;
+    }
+    s->allow_f16 = prec == 16;
+  }
   s->use_bn = s->snap[10].o && PyObject_IsTrue(s->snap[10].o) == 1;
-  for (int i = 5; i <= 7; ++i)  // use_range_std_dev, measure_compression_ratio, use_sample_stats
+  for (int i = 5; i <= 7; i += 2)  // use_range_std_dev, use_sample_stats
     if (s->snap[i].o && PyObject_IsTrue(s->snap[i].o) == 1) s->decline = true;
+  s->count = s->snap[6].o && PyObject_IsTrue(s->snap[6].o) == 1;  // measure_compression_ratio
   s->rng_dict.o = a[3];
   Py_INCREF(a[3]);
   s->ws_getter.o = a[4];
@@ -203,10 +253,13 @@ enum RunResult { kError = -1, kDecline = 0, kDone = 1, kStale = 2 };
 
 // One SmartFP call on t (GIL held): kDone with *out set, kDecline (the Python path handles it),
 // kStale (the hparams changed since the state was built), kError (Python error set).
-RunResult smaq_run(SmaqState& s, const at::Tensor& t, bool all_positive, at::Tensor* out) {
+// rec: with ratio logging, the fp64 [n_outlier, new_size, compression_ratio, orig_size] values of
+// the call (device); a caller that passes none gets kDecline for a counting codec.
+RunResult smaq_run(SmaqState& s, const at::Tensor& t, bool all_positive, at::Tensor* out,
+                   at::Tensor* rec = nullptr) {
   for (int i = 0; i < kSnap; ++i)
     if (PyDict_GetItem(s.hp_dict.o, g_snap_keys[i]) != s.snap[i].o) return kStale;
-  if (s.decline || !t.is_cuda()) return kDecline;
+  if (s.decline || !t.is_cuda() || (s.count && !rec)) return kDecline;
   int code;
   switch (t.scalar_type()) {
     case at::kFloat: code = SMQ_DTYPE_F32; break;
@@ -225,9 +278,21 @@ RunResult smaq_run(SmaqState& s, const at::Tensor& t, bool all_positive, at::Ten
   if (!ws_lookup(s.ws, s.ws_getter.o, dev, st, smq_smaq_workspace_bytes(n))) return kError;
   SmqSmaqParams p = s.tmpl[all_positive ? 1 : 0];
   if (!rng_take(s.rng_dict.o, (uint64_t)n, &p.seed, &p.offset)) return kError;
+  if (s.count) {  // a graph capture would keep the pool's records: the Python path refuses it
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+      return kDecline;
+  }
   at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kFloat));
-  const int rc = smq_smaq_roundtrip(x.const_data_ptr(), code, y.mutable_data_ptr<float>(), n, &p,
-                                    nullptr, s.ws.ptr, s.ws.bytes, st);
+  int rc;
+  if (s.count) {
+    SmqSizeRecord* r = rec_take(x, st, rec);
+    rc = smq_smaq_roundtrip_counted(x.const_data_ptr(), code, y.mutable_data_ptr<float>(), n, &p,
+                                    s.ws.ptr, s.ws.bytes, r, st);
+  } else {
+    rc = smq_smaq_roundtrip(x.const_data_ptr(), code, y.mutable_data_ptr<float>(), n, &p, nullptr,
+                            s.ws.ptr, s.ws.bytes, st);
+  }
   if (rc) {
     PyErr_Format(PyExc_RuntimeError, "smq_smaq_roundtrip failed (rc=%d): %s", rc,
                  smq_last_error());
@@ -235,6 +300,19 @@ RunResult smaq_run(SmaqState& s, const at::Tensor& t, bool all_positive, at::Ten
   }
   *out = std::move(y);
   return kDone;
+}
+
+PyObject* g_log_rec = nullptr;  // "_log_size_record"
+PyObject* g_fwd_tag = nullptr;  // "forward_autograd"
+
+// codec._log_size_record(tag, values) (GIL held): the counted call's log_size, values on the device
+bool log_record(PyObject* codec, PyObject* tag, at::Tensor&& rec) {
+  PyObject* rv = THPVariable_Wrap(std::move(rec));
+  if (!rv) return false;
+  PyObject* r = PyObject_CallMethodObjArgs(codec, g_log_rec, tag, rv, nullptr);
+  Py_DECREF(rv);
+  Py_XDECREF(r);
+  return r != nullptr;
 }
 
 // smaq(state, x, all_positive, batch_norm_stats) -> y | None (not handled here) |
@@ -251,13 +329,25 @@ PyObject* smaq(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
   const int ap = PyObject_IsTrue(a[2]);
   if (ap < 0) return nullptr;
-  at::Tensor y;
-  switch (smaq_run(s, THPVariable_Unpack(a[1]), ap != 0, &y)) {
-    case kDone: return THPVariable_Wrap(std::move(y));
+  at::Tensor y, rec;
+  switch (smaq_run(s, THPVariable_Unpack(a[1]), ap != 0, &y, &rec)) {
+    case kDone: break;
     case kDecline: Py_RETURN_NONE;
     case kStale: Py_RETURN_NOTIMPLEMENTED;
     default: return nullptr;
   }
+  if (!s.count) return THPVariable_Wrap(std::move(y));
+  // ratio logging: (y, values) — the codec logs them under the call's tag
+  PyObject* yo = THPVariable_Wrap(std::move(y));
+  PyObject* ro = yo ? THPVariable_Wrap(std::move(rec)) : nullptr;
+  if (!ro) {
+    Py_XDECREF(yo);
+    return nullptr;
+  }
+  PyObject* r = PyTuple_Pack(2, yo, ro);
+  Py_DECREF(yo);
+  Py_DECREF(ro);
+  return r;
 }
 
 // Bytes of a stream of n elements with every element an outlier and escape_frac of them escaped
@@ -291,7 +381,7 @@ PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   for (int i = 0; i < kSnap; ++i)
     if (PyDict_GetItem(s.hp_dict.o, g_snap_keys[i]) != s.snap[i].o) Py_RETURN_NOTIMPLEMENTED;
   const at::Tensor& t = THPVariable_Unpack(a[1]);
-  if (s.decline || !t.is_cuda()) Py_RETURN_NONE;
+  if (s.decline || s.count || !t.is_cuda()) Py_RETURN_NONE;
   int code;
   switch (t.scalar_type()) {
     case at::kFloat: code = SMQ_DTYPE_F32; break;
@@ -377,8 +467,9 @@ struct SmaqCompressBackward : public torch::autograd::Node {
     if (!task_should_compute_output(0)) return {at::Tensor()};
     if (!g.defined() || !state) return {g};
     PyGILState_STATE gs = PyGILState_Ensure();
-    at::Tensor out;
-    RunResult r = smaq_run(*state, g, false, &out);
+    at::Tensor out, rec;
+    RunResult r = smaq_run(*state, g, false, &out, &rec);
+    if (r == kDone && state->count && !log_record(codec.o, g_bwd_tag, std::move(rec))) r = kError;
     if (r == kDecline || r == kStale) {  // the codec's own call (it rebuilds a stale state)
       PyObject* gv = THPVariable_Wrap(g);
       PyObject* res = nullptr;
@@ -439,13 +530,14 @@ PyObject* smaq_autograd(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   const int bwd = PyObject_IsTrue(a[3]);
   if (bwd < 0) return nullptr;
   const at::Tensor& x = THPVariable_Unpack(a[1]);
-  at::Tensor y;
-  switch (smaq_run(**sp, x, false, &y)) {
+  at::Tensor y, rec;
+  switch (smaq_run(**sp, x, false, &y, &rec)) {
     case kDone: break;
     case kDecline: Py_RETURN_NONE;
     case kStale: Py_RETURN_NOTIMPLEMENTED;
     default: return nullptr;
   }
+  if ((*sp)->count && !log_record(a[2], g_fwd_tag, std::move(rec))) return nullptr;
   if (torch::autograd::compute_requires_grad(x)) {
     auto node = std::shared_ptr<SmaqCompressBackward>(new SmaqCompressBackward(),
                                                       torch::autograd::deleteNode);
@@ -519,6 +611,8 @@ PyMODINIT_FUNC PyInit__smqtorch(void) {
   g_offset = PyUnicode_InternFromString("offset");
   g_tag = PyUnicode_InternFromString("tag");
   g_bwd_tag = PyUnicode_InternFromString("backward_autograd");
+  g_fwd_tag = PyUnicode_InternFromString("forward_autograd");
+  g_log_rec = PyUnicode_InternFromString("_log_size_record");
   for (int i = 0; i < kSnap; ++i) g_snap_keys[i] = PyUnicode_InternFromString(kSnapKeys[i]);
   return PyModule_Create(&kModule);
 }

@@ -136,6 +136,20 @@ SMQ_PACK_FLAG_BN = 8
 SMQ_PACK_FLAG_F64 = 16
 
 
+class SmqSizeRecord(ctypes.Structure):
+    """include/smq.h SmqSizeRecord: a counted call's outlier count and log_size values (fp64, on
+    the device; smq_smaq_roundtrip_counted)."""
+    _fields_ = [
+        ("slots", ctypes.c_uint64 * 8),
+        ("arrived", ctypes.c_uint64),
+        ("reserved", ctypes.c_uint64 * 3),
+        ("n_outlier", ctypes.c_double),
+        ("new_size", ctypes.c_double),
+        ("compression_ratio", ctypes.c_double),
+        ("orig_size", ctypes.c_double),
+    ]
+
+
 class SmqTensorDesc(ctypes.Structure):
     _fields_ = [
         ("x", ctypes.c_void_p),
@@ -240,6 +254,12 @@ SIGNATURES = {
         _I32,
         [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _P, _SZ, _U32, _P],
     ),
+    "smq_smaq_roundtrip_counted": (
+        _I32,
+        [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P, _P],
+    ),
+    "smq_smaq_size_metrics": (_I32, [_P, _I64, _I32, _I32, _P, _P]),
+    "smq_smaq_multi_size_metrics": (_I32, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "smq_smaq_multi_plan_bytes": (_SZ, [ctypes.POINTER(_I64), _I32]),
     "smq_smaq_multi_plan_build": (_I32, [ctypes.POINTER(SmqTensorDesc), _I32, _P, _SZ]),
     "smq_smaq_multi_workspace_bytes": (_SZ, [ctypes.POINTER(_I64), _I32]),

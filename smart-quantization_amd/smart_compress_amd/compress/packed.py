@@ -175,6 +175,12 @@ class SmartFPPacked(SmartFP):
         ``smq_smaq_pack_workspace_bytes``) no other call uses until ``pack_stream`` has passed.
         CPU and float64 tensors: ``compress`` then ``decompress`` (the same values)."""
         hp = self.hparams
+        if pack_stream is not None and workspace is None:
+            # the shared per-(device, stream) workspace would be cleared and rewritten by the next
+            # call on the current stream while pack_stream may still read it
+            raise ValueError("roundtrip_compress: pack_stream needs a private workspace "
+                             "(smq_smaq_pack_workspace_bytes) that no other call uses until "
+                             "pack_stream has passed")
         numel = data.numel()
         if (numel < hp.min_size or N.on_cpu(data) or data.dtype == torch.float64
                 or hp.main_std_dev_threshold != hp.main_std_dev_threshold):

@@ -246,9 +246,14 @@ class SmartFP(CompressionAlgorithmBase):
     # graph-safe switch are replaced (__setattr__), or when the C side finds a flag changed.
     _hot = None
 
+    # the attributes the C state is built from: the hparams, the random stream, the graph-safe
+    # switch and the constants the reference reads on every call (smart.py:154, 162)
+    _HOT_INPUTS = frozenset(("hparams", "rng", "_graph_safe", "range_normal", "range_outlier",
+                             "clamped_range"))
+
     def __setattr__(self, name, value):
         object.__setattr__(self, name, value)
-        if name in ("hparams", "rng", "_graph_safe"):
+        if name in SmartFP._HOT_INPUTS:
             object.__setattr__(self, "_hot", None)
 
     def _build_hot(self):
@@ -299,13 +304,14 @@ class SmartFP(CompressionAlgorithmBase):
             hot = self._build_hot()
         if hot is not False and Globals.profiler is None and self._trace is None:
             y = N._torch_fast.smaq(hot, data, all_positive, batch_norm_stats)
-            if y is not None:
-                if y is not NotImplemented:
-                    return y
-                if self._build_hot() is not False:  # a flag changed: rebuild, call again
-                    y = N._torch_fast.smaq(self._hot, data, all_positive, batch_norm_stats)
-                    if y is not None:
-                        return y
+            if y is NotImplemented and self._build_hot() is not False:
+                # a flag changed: rebuild, call again
+                y = N._torch_fast.smaq(self._hot, data, all_positive, batch_norm_stats)
+            if y is not None and y is not NotImplemented:
+                if type(y) is tuple:  # --measure_compression_ratio: (y, its log_size values)
+                    y, rec = y
+                    self._log_size_record(tag, rec)
+                return y
         # Without the binding (or on graph-safe streams): the same call through the CPython
         # fast-call binding (ctypes' argument conversion costs ~4 us). Everything else: _call,
         # under torch.no_grad as smart.py:110.
@@ -435,6 +441,18 @@ class SmartFP(CompressionAlgorithmBase):
 
         self.log_size(tag, numel * 32, new_size if hp.measure_compression_ratio else None)
         return y
+
+    def _log_size_record(self, tag, rec: torch.Tensor):
+        """log_size of a counted call (csrc/torchfast.cpp, smq_smaq_roundtrip_counted): ``rec`` is
+        the call's fp64 device tensor [n_outlier, new_size, compression_ratio, orig_size], written
+        by the call itself. The metrics are logged as 0-dim device tensors — the same values the
+        host path logs as floats (smart.py:184-188, base.py:72-102), converted only when the logger
+        consumes them, so a measuring step has no host synchronisation per call."""
+        _, new, ratio, orig = rec.unbind()
+        self._emit({"compression_ratio": ratio, f"compression_ratio_{tag}": ratio,
+                    "new_size": new, f"new_size_{tag}": new,
+                    "orig_size": orig, f"orig_size_{tag}": orig},
+                   custom=tag.startswith("optimizer_"))
 
     # bench.py sets an event recorder here: an event pair on the codec's stream around the call's
     # launches (the product entry point either way)

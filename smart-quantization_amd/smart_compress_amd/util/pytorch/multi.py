@@ -69,7 +69,9 @@ class SmaqMulti:
         dev_t = host_t.to(device)
         ws_bytes = lib.smq_smaq_multi_workspace_bytes(sizes, count)
         ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=device)
-        plan = dict(host=host, dev=dev_t, ws=ws, count=count, dtype=N.DTYPE_CODES[xs[0].dtype])
+        plan = dict(host=host, dev=dev_t, ws=ws, count=count, dtype=N.DTYPE_CODES[xs[0].dtype],
+                    n=torch.tensor([x.numel() for x in xs], dtype=torch.int64, device=device),
+                    rels=list(rels))
         if len(self._plans) > 16:
             self._plans.clear()
         self._plans[key] = plan
@@ -143,13 +145,24 @@ class SmaqMulti:
             p.seed, p.offset = self.rng.take(total)
             p.offset_counter = None
         st = N.stream_ptr(device)
-        fn = N.lib().smq_smaq_multi
+        lib = N.lib()
+        fn = lib.smq_smaq_multi
+        hp = self.hparams
+        metrics = [] if hp.measure_compression_ratio else None
         for plan in plans:
             rc = fn(plan["dev"].data_ptr(), ctypes.addressof(plan["host"]), plan["dtype"], p,
                     plan["ws"].data_ptr(), plan["ws"].numel(), st)
             if rc:
                 N.check(rc, "smq_smaq_multi")
-        self._last = dict(plans=plans, rels=rels, sel=sel,
+            if metrics is not None:
+                # the per-tensor log_size values on the device (no host synchronisation): one
+                # small launch reads every tensor's outlier count from its statistics record
+                out = torch.empty((plan["count"], 4), dtype=torch.float64, device=device)
+                N.check(lib.smq_smaq_multi_size_metrics(
+                    plan["ws"].data_ptr(), plan["n"].data_ptr(), plan["count"], hp.num_bits_main,
+                    hp.num_bits_outlier, out.data_ptr(), st), "smq_smaq_multi_size_metrics")
+                metrics.append(out)
+        self._last = dict(plans=plans, rels=rels, sel=sel, metrics=metrics,
                           base=None if self._graph_safe else p.offset)
 
     @torch.no_grad()
@@ -208,6 +221,20 @@ class SmaqMulti:
         if last["base"] is None:
             raise RuntimeError("offset_of: the stream position is on the device (graph-safe mode)")
         return last["base"] + last["rels"][last["sel"].index(t)]
+
+    def size_records(self):
+        """--measure_compression_ratio: per selected tensor of the last call (list order), its fp64
+        device values [n_outlier, new_size, compression_ratio, orig_size] (smart.py:184-188),
+        written by smq_smaq_multi_size_metrics — read without a host synchronisation."""
+        last = self._last
+        if last is None or last["metrics"] is None:
+            return None
+        out = [None] * len(last["sel"])
+        pos = {r: j for j, r in enumerate(last["rels"])}
+        for plan, m in zip(last["plans"], last["metrics"]):
+            for t, row in zip(range(plan["count"]), m.unbind()):
+                out[pos[plan["rels"][t]]] = row
+        return out
 
     def read_stats(self):
         """Statistics of the last call's selected tensors, in list order."""

@@ -117,16 +117,24 @@ class OptimLP(Optimizer):
                 kwargs = {"all_positive": True} if all_pos[i] else {}
                 assign(i, fn(t, **kwargs))
 
-    @staticmethod
-    def _log_fused(codec: SmartFP, tag: str, multi: SmaqMulti, xs: Sequence[torch.Tensor]):
+    # the per-tensor log_size values of a fused call stay on the device (SmaqMulti.size_records:
+    # no host synchronisation per optimizer step); False: read the counts on the host instead
+    device_metrics = True
+
+    @classmethod
+    def _log_fused(cls, codec: SmartFP, tag: str, multi: SmaqMulti, xs: Sequence[torch.Tensor]):
         hp = codec.hparams
         if not hp.measure_compression_ratio:
             return
-        stats = multi.read_stats() if multi.last_selected else []
+        recs = multi.size_records() if cls.device_metrics and multi.last_selected else None
+        stats = multi.read_stats() if recs is None and multi.last_selected else []
         for t, x in enumerate(xs):
             n = x.numel()
             if n < hp.min_size:
                 codec.log_ratio(tag, n * 32, 32, 32)  # smart.py:125
+                continue
+            if recs is not None:
+                codec._log_size_record(tag, recs[multi.index_of(t)])
                 continue
             n_out = stats[multi.index_of(t)]["n_outlier"]
             codec.log_size(tag, n * 32, n_out * hp.num_bits_outlier + (n - n_out) * hp.num_bits_main)

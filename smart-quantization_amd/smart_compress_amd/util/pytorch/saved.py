@@ -71,12 +71,33 @@ def stream_capacity(n: int, num_bits_main: int, num_bits_outlier: int, bn_channe
 
 class _Saved:
     """What autograd holds instead of a saved activation: the stream (and, until its size is
-    checked, the activation itself)."""
+    checked, the activation itself), the activation's version counter value when it was saved and
+    a weak reference to it (saved_tensors_hooks turn off autograd's own in-place check: _unpack
+    repeats it)."""
 
-    __slots__ = ("packed", "y", "codec")
+    __slots__ = ("packed", "y", "codec", "version", "ref", "modified")
 
-    def __init__(self, packed: SmaqPacked, y: torch.Tensor, codec: SmartFPPacked):
+    def __init__(self, packed: SmaqPacked, y: torch.Tensor, codec: SmartFPPacked, version: int,
+                 ref):
         self.packed, self.y, self.codec = packed, y, codec
+        self.version, self.ref, self.modified = version, ref, None
+
+    def check_version(self) -> None:
+        """Raise autograd's in-place error when the saved activation was modified after it was
+        saved (checked on the activation while it is held, at the size check before it is dropped,
+        and through the weak reference while it lives)."""
+        if self.modified is None:
+            y = self.y if self.y is not None else self.ref()
+            if y is None or y._version == self.version:
+                return
+            self.modified = (tuple(y.shape), y._version)
+        shape, v = self.modified
+        raise RuntimeError(
+            "one of the variables needed for gradient computation has been modified by an inplace "
+            f"operation: [torch.cuda.FloatTensor {list(shape)}], which is a SmaQ-compressed "
+            f"activation saved as a packed stream; is at version {v}; expected version "
+            f"{self.version} instead. (util/pytorch/saved.py: PackedActivations repeats autograd's "
+            "check, which saved_tensors_hooks disable.)")
 
 
 class _Entry:
@@ -217,7 +238,7 @@ class PackedActivations:
         self.saved_packed += 1
         if e.handle is not None:  # saved again (another consumer): the same stream
             return e.handle
-        h = e.handle = _Saved(e.packed, y, self.codec)
+        h = e.handle = _Saved(e.packed, y, self.codec, e.version, e.ref)
         self._pending.append(h)
         self._pending_bytes += 4 * y.numel()
         if self._pending_bytes > self.verify_bytes:
@@ -229,6 +250,7 @@ class PackedActivations:
 
     def _unpack(self, h):
         if isinstance(h, _Saved):
+            h.check_version()
             if h.y is not None:  # not checked yet, or cut at its capacity: the activation itself
                 return h.y
             if not self._joined:  # a backward inside the context: after the packing launches
@@ -279,6 +301,8 @@ class PackedActivations:
             self._inflight_bytes -= nbytes
             for h, total in zip(hs, host.view(torch.int64).tolist()):
                 cap = h.packed.data.numel()
+                if h.y._version != h.version:  # modified in place since saved: backward raises
+                    h.modified = (tuple(h.y.shape), h.y._version)
                 if total <= cap:
                     h.packed._total = int(total)
                     h.y = None

@@ -44,6 +44,7 @@ def test_struct_layouts_match_header():
 #include <stddef.h>
 #include "smq.h"
 int main(void) {
+  printf("%zu %zu\n", sizeof(SmqSizeRecord), offsetof(SmqSizeRecord, n_outlier));
   printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(SmqSmaqParams),
          sizeof(SmqSmaqStats), sizeof(SmqTensorDesc), sizeof(SmqS2fp8Stats),
          offsetof(SmqSmaqParams, seed), offsetof(SmqSmaqParams, bn_gamma),
@@ -60,6 +61,8 @@ int main(void) {
         exe = os.path.join(d, "l")
         subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), c, "-o", exe])
         got = list(map(int, subprocess.check_output([exe]).split()))
+    assert got[:2] == [ctypes.sizeof(N.SmqSizeRecord), N.SmqSizeRecord.n_outlier.offset] == [128, 96]
+    got = got[2:]
     want = [ctypes.sizeof(N.SmqSmaqParams), ctypes.sizeof(N.SmqSmaqStats),
             ctypes.sizeof(N.SmqTensorDesc), ctypes.sizeof(N.SmqS2fp8Stats),
             N.SmqSmaqParams.seed.offset, N.SmqSmaqParams.bn_gamma.offset,

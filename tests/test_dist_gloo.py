@@ -57,6 +57,16 @@ def test_bench_self_launch_n_ranks(n):
     assert len(set(line["seeds"])) == n
     assert len(line["rank_ms_per_step"]) == n and all(t > 0 for t in line["rank_ms_per_step"])
     assert line["scaling"] == "weak"
+    # the nested multi-tensor line (BASELINE config 5's weak-scaling curve; run_multi on a GPU box)
+    m = line["c5_multi"]
+    assert m["n_gpus"] == n and m["scaling"] == "weak" and m["config"]["tensors"] == 148
+    assert m["config"]["parallelism"] == f"replicas{n}"
+    assert len(m["rank_ms_per_step"]) == n and all(t > 0 for t in m["rank_ms_per_step"])
+    # value = every rank's bytes / the slowest rank's time (its ms_per_step)
+    total = 12.0 * m["config"]["elements_per_gpu"] * n * m["steps"]
+    assert m["value"] == pytest.approx(total / (m["ms_per_step"] * 1e-3 * m["steps"]) / 1e9,
+                                       rel=2e-3, abs=2e-6)
+    assert m["ms_per_step"] >= max(m["rank_ms_per_step"]) * 0.999
 
 
 def test_bench_self_launch_failing_rank_propagates():

@@ -104,6 +104,16 @@ def test_smartfp_c_path_flags_changed_and_declined():
         else:
             assert _eq(y1, y2), change
         assert fast.rng.offset == slow.rng.offset
+    # the constants the reference reads per call (smart.py:154, 162), assigned after the first
+    # call: the C state is rebuilt from them
+    for attr, val in (("range_normal", 11.0), ("range_outlier", 30.0),
+                      ("clamped_range", (1e-4, 1e4))):
+        for c in (fast, slow):
+            setattr(c, attr, val)
+        _python_path(slow)
+        y1, y2 = fast(x), slow(x)
+        assert _eq(y1, y2), attr
+        assert fast._hot not in (None, False)
     for c in (fast, slow):
         c.rng = RngState(1234)
     _python_path(slow)  # (replacing rng re-keys, i.e. resets, the C state)
@@ -249,3 +259,16 @@ def test_s2fp8_c_path_equals_python_path():
     for a, b in zip(outs[0][:3], outs[1][:3]):
         assert _eq(a, b)
     assert outs[0][3] == outs[1][3]
+
+
+@pytest.mark.parametrize("field,value", [("min_size", 8.0), ("precision", "32")])
+def test_smartfp_c_path_declines_non_int_hparams(field, value):
+    """min_size / precision that are not Python ints (a hand-built Namespace, a config file): the C
+    state declines instead of raising, and the Python path serves the call with the same result."""
+    _N()
+    hp = smaq_hparams()
+    setattr(hp, field, value)
+    fast, slow = _pair(hp)
+    x = torch.randn(70_000, device="cuda")
+    assert _eq(fast(x), slow(x))
+    assert fast.rng.offset == slow.rng.offset

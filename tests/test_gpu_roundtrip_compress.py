@@ -189,3 +189,116 @@ def test_one_launch_packer_workspace_reuse():
         fresh = torch.zeros(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8,
                             device="cuda")
         assert np.array_equal(stream(n, ws), stream(n, fresh)), n
+
+
+# The single launch that also packs (smaq_fused.hip PACK: fp32, n % 4 == 0, up to 4 groups per
+# lane, T_m > 0, no BN / range statistics): block b * V + u is built from workgroup b's registers
+# right after its transform, the variable sections placed by one granule per workgroup. Its stream
+# must be the look-back packer's byte for byte (compress() never takes it: y == NULL there).
+PACK_SIZES = [4096, 8192, 12_288, 4096 * 255 + 8, 262_144, (1 << 20) + 4, 2 << 20,
+              3 * (1 << 20) + 4000, 4 << 20, 4_194_300]
+
+
+@pytest.mark.parametrize("n", PACK_SIZES)
+@pytest.mark.parametrize("case", ["default", "all_positive", "trunc", "bits_4_6", "bits_5_7"])
+def test_fused_pack_stream_equals_compress(n, case):
+    over, ap = {}, False
+    if case == "all_positive":
+        ap = True
+    elif case == "trunc":
+        over["stochastic_rounding"] = False
+    elif case == "bits_4_6":
+        over.update(num_bits_main=4, num_bits_outlier=6)
+    elif case == "bits_5_7":
+        over.update(num_bits_main=5, num_bits_outlier=7)
+    hp, rc, ref, pk = _codecs(**over)
+    gen = torch.Generator(device="cuda").manual_seed(n + len(case))
+    x = torch.randn(n, generator=gen, device="cuda") * 1.7 - 0.3
+    if ap:
+        x = torch.relu(x)
+    for _ in range(2):  # twice: consecutive calls on one workspace (epochs advance)
+        y, p = rc.roundtrip_compress(x, all_positive=ap)
+        y_ref = ref(x, all_positive=ap)
+        q = pk.compress(x, all_positive=ap)
+        torch.cuda.synchronize()
+        assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy()), (n, case)
+        a, b = _stream(p), _stream(q)
+        assert a.size == b.size and np.array_equal(a, b), (n, case, int(np.argmax(a != b)))
+        assert same_f32(rc.decompress(p).cpu().numpy(), y_ref.cpu().numpy()), (n, case)
+
+
+@pytest.mark.parametrize("n", [1 << 20, 3 << 20, 4 << 20])
+def test_fused_pack_escape_heavy_blocks(n):
+    """Activations whose channels sit far from the tensor's mean escape by the hundreds per block
+    (more than the block's LDS section holds, and than a segment's list): those blocks are re-coded
+    from x into their place; every other block keeps its LDS section. Same bytes as compress()."""
+    hp, rc, ref, pk = _codecs()
+    gen = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(n, generator=gen, device="cuda")
+    x[: n // 64] += 40.0            # a run of blocks far above the mean: every element escapes
+    x[n // 2: n // 2 + 300] = -1e5  # one block with 300 escapes in a row
+    x[n - 4096 + 17: n - 4096 + 60] = 3e4  # the last block: 43 escapes in one segment
+    y, p = rc.roundtrip_compress(x)
+    y_ref = ref(x)
+    q = pk.compress(x)
+    torch.cuda.synchronize()
+    assert same_f32(y.cpu().numpy(), y_ref.cpu().numpy())
+    a, b = _stream(p), _stream(q)
+    assert a.size == b.size and np.array_equal(a, b)
+    assert same_f32(rc.decompress(p).cpu().numpy(), y_ref.cpu().numpy())
+
+
+def test_fused_pack_capacity_bounded_buffer():
+    """The PACK launch with a buffer below the stream's size: total_bytes flags it, nothing is
+    written past the buffer, the fixed part and y are complete."""
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    n = 1_000_000
+    gen = torch.Generator(device="cuda").manual_seed(19)
+    x = torch.randn(n, generator=gen, device="cuda")
+    rc0, full, hdr0, y0 = _raw_call(x, n, lib.smq_smaq_pack_bound(n, 6, 8), 0)
+    total = int(hdr0.total_bytes)
+    fixed = lib.smq_smaq_pack_fixed_bytes(n, 6)
+    assert rc0 == 0 and fixed < total
+    rc1, b1, hdr1, y1 = _raw_call(x, n, total)
+    assert rc1 == 0 and int(hdr1.total_bytes) == total
+    assert np.array_equal(b1[:total], full[:total]) and (b1[total:] == 0xAB).all()
+    small = fixed + (total - fixed) // 3
+    rc2, b2, hdr2, y2 = _raw_call(x, n, small)
+    assert rc2 == 0 and int(hdr2.total_bytes) == total > small
+    assert (b2[small:] == 0xAB).all() and np.array_equal(b2[:fixed], full[:fixed])
+    assert same_f32(y2.cpu().numpy(), y0.cpu().numpy())
+
+
+def test_fused_pack_workspace_of_random_bytes():
+    """The PACK launch's aggregates are epoch-tagged granules: a workspace of random bytes, reused
+    across sizes and by the other packers, gives the fresh workspace's streams."""
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    hp, rc, _, _ = _codecs()
+    gen = torch.Generator(device="cuda").manual_seed(23)
+    sizes = [1 << 20, 4 << 20, 262_144, 9_000_000, 1 << 20, 65_536, 4 << 20]
+    xs = {n: torch.randn(n, generator=gen, device="cuda") * 1.1 for n in set(sizes)}
+    big = max(lib.smq_smaq_pack_workspace_bytes(n) for n in sizes)
+    ws = torch.randint(0, 256, (big,), dtype=torch.uint8, device="cuda", generator=gen)
+
+    def stream(n, w):
+        p = rc._params(n, False, torch.float32, xs[n].device)
+        p.offset = 91
+        bound = lib.smq_smaq_pack_bound(n, 6, 8)
+        out = torch.empty(bound, dtype=torch.uint8, device="cuda")
+        y = torch.empty(n, device="cuda")
+        assert lib.smq_smaq_roundtrip_compress(xs[n].data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n,
+                                               p, out.data_ptr(), bound, w.data_ptr(), w.numel(),
+                                               N.stream_ptr(xs[n].device)) == 0
+        torch.cuda.synchronize()
+        hdr = N.SmqPackedHeader.from_buffer_copy(bytes(out[:128].cpu().numpy()))
+        return out[:int(hdr.total_bytes)].cpu().numpy(), y.cpu().numpy()
+
+    for n in sizes:
+        fresh = torch.zeros(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8,
+                            device="cuda")
+        (a, ya), (b, yb) = stream(n, ws), stream(n, fresh)
+        assert np.array_equal(a, b) and same_f32(ya, yb), n

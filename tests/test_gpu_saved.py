@@ -138,9 +138,11 @@ def test_packed_saved_outside_context_and_backward_calls():
     assert pk.rng.offset == ref.rng.offset
 
 
-def test_backward_inside_the_context_waits_for_the_packer():
+@pytest.mark.parametrize("overlap", [True, False])
+def test_backward_inside_the_context_waits_for_the_packer(overlap):
     """A backward run while the context is still open decodes streams whose packing launches ran on
-    the side stream: the decode is ordered after them (the gradient equals SmartFP's)."""
+    the side stream (overlap=True: _unpack joins the side stream first): the decode is ordered
+    after them (the gradient equals SmartFP's)."""
     from smart_compress_amd.compress import SmartFP, SmartFPPacked
     from smart_compress_amd.util.pytorch.autograd import Compressor
     from smart_compress_amd.util.pytorch.saved import PackedActivations
@@ -151,7 +153,8 @@ def test_backward_inside_the_context_waits_for_the_packer():
     for packed in (False, True):
         codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
         codec.rng.seed, codec.rng.offset = 8, 0
-        acts = PackedActivations(codec, verify_bytes=1 << 10) if packed else None
+        acts = (PackedActivations(codec, verify_bytes=1 << 10, overlap=overlap) if packed
+                else None)
         comp = Compressor(acts if packed else codec)
         w = torch.linspace(0.5, 1.5, x.numel(), device="cuda").requires_grad_(True)
         if packed:
@@ -159,9 +162,50 @@ def test_backward_inside_the_context_waits_for_the_packer():
                 y = comp(x * w)
                 loss = (y * y).sum()
                 acts.verify()  # the activation dropped: backward must decode the stream
+                assert acts._joined == (not overlap)  # overlap: the side stream not joined yet
                 loss.backward()
+                assert acts._joined
         else:
             y = comp(x * w)
             (y * y).sum().backward()
         res.append((y.detach(), w.grad.clone()))
     assert _eq(res[0][0], res[1][0]) and _eq(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("when", ["held", "verified", "modified_then_verified"])
+def test_inplace_change_after_save_raises(when):
+    """saved_tensors_hooks switch off autograd's version check; PackedActivations repeats it, so an
+    activation modified in place after a multiply saved it raises autograd's error in backward (as
+    the reference, whose autograd saves y itself, autograd.py:30-42) — whether the saved value is
+    still the held activation or already the stream, and whether the change came before or after
+    the size check that dropped the activation."""
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import Compressor
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    x = torch.randn(1 << 18, device="cuda")
+    w = torch.linspace(0.5, 1.5, x.numel(), device="cuda").requires_grad_(True)
+    # the reference behaviour: plain SmartFP, y saved by the multiply, then changed in place
+    comp = Compressor(SmartFP(smaq_hparams()))
+    y = comp(x * w)
+    loss = (y * w).sum()
+    y.add_(1.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        loss.backward()
+    codec = SmartFPPacked(smaq_hparams())
+    acts = PackedActivations(codec, verify_bytes=1 << 40)
+    comp = Compressor(acts)
+    with acts:
+        y = comp(x * w)
+        loss = (y * w).sum()  # saves y (held until its size is checked)
+        if when == "verified":
+            acts.verify()     # y dropped: the saved value is now the stream
+            y.add_(1.0)
+        elif when == "modified_then_verified":
+            y.add_(1.0)
+            acts.verify()
+        else:
+            y.add_(1.0)
+        with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+            loss.backward()
+    assert acts.stats()["saved_packed"] == 1

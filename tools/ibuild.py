@@ -29,8 +29,12 @@ for cmd, pr in procs:
     out, _ = pr.communicate()
     if pr.returncode:
         sys.exit(f"hipcc failed: {' '.join(cmd)}\n{out.decode()}")
-link = [G.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o", G.LIB, *objs]
+# linked next to the library, then renamed over it: a reader (a gpurun upload) sees the old or the
+# new file, never a partial one
+tmp = G.LIB + ".tmp"
+link = [G.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o", tmp, *objs]
 r = subprocess.run(link, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
 if r.returncode:
     sys.exit(f"link failed\n{r.stdout.decode()}")
+os.replace(tmp, G.LIB)
 print("linked", G.LIB)
