@@ -388,21 +388,24 @@ __device__ __forceinline__ uint32_t fused_tail(const FusedArgs& A, const ElemCon
 // writes the header. The stream is byte for byte the one the look-back packer
 // (smaq_pack_lb_kernel) writes after the same round trip — x is read once for y AND the stream.
 // ------------------------------------------------------------------------------------------------
-constexpr int kPkEsc = 128;  // escapes a block's LDS section holds (more: re-coded from x, rare)
-__host__ __device__ inline uint32_t pk_var_words(int we) {
-  return 128u * (uint32_t)we + 2u * kPkEsc;
+// Escapes a block's LDS section holds: every element up to 3 groups per lane (the dynamic LDS is
+// free there), kPkEscV4 at 4 (the rounding draws hold 64 KiB of it); a block with more is re-coded
+// from x into its place.
+constexpr int kPkEscV4 = 256;
+__host__ __device__ inline uint32_t pk_esc_cap(int V) { return V <= 3 ? (uint32_t)kPB : (uint32_t)kPkEscV4; }
+__host__ __device__ inline uint32_t pk_var_words(int we, int V) {
+  return 128u * (uint32_t)we + 2u * pk_esc_cap(V);
 }
-// pack area (words): two fixed images (mask + plane), the escape staging (kSegs lists of kSegEsc
-// pairs), the 16 segment counts, 4 x 4 words of block meta, 4 uint64 of the prefix reduction, then
-// the V variable sections
-__host__ __device__ inline uint32_t pk_seg_off(int wm) {
-  return 2u * fixed_words(wm) + 2u * kSegs * kSegEsc;
-}
+// pack area (words): two fixed images (mask + plane), the 16 segment counts, 4 x 4 words of block
+// meta, 4 uint64 of the prefix reduction, 4 x 16 wave totals, then the V variable sections
+// (outlier bits, escapes)
+__host__ __device__ inline uint32_t pk_seg_off(int wm) { return 2u * fixed_words(wm); }
 __host__ __device__ inline uint32_t pk_meta_off(int wm) { return pk_seg_off(wm) + kSegs; }
 __host__ __device__ inline uint32_t pk_red_off(int wm) { return pk_meta_off(wm) + 16u; }
-__host__ __device__ inline uint32_t pk_var_off(int wm) { return pk_red_off(wm) + 8u; }
+__host__ __device__ inline uint32_t pk_tot_off(int wm) { return pk_red_off(wm) + 8u; }
+__host__ __device__ inline uint32_t pk_var_off(int wm) { return pk_tot_off(wm) + 64u; }
 __host__ __device__ inline uint32_t pk_lds_words(int wm, int we, int V) {
-  return pk_var_off(wm) + (uint32_t)V * pk_var_words(we);
+  return pk_var_off(wm) + (uint32_t)V * pk_var_words(we, V);
 }
 
 // Block B's variable section re-coded from x straight to dst (a block with more escapes than its
@@ -410,7 +413,7 @@ __host__ __device__ inline uint32_t pk_lds_words(int wm, int we, int V) {
 // and the passes' running totals (smaq_pack.hip recode_var_section for a 1024-thread workgroup).
 // ext: 128 * we words of LDS, s_cnt: 16 words.
 template <int RM, int TIN>
-__device__ __noinline__ void fused_recode(const FusedArgs& A, const ElemConsts& c, uint64_t off,
+__device__ __forceinline__ void fused_recode(const FusedArgs& A, const ElemConsts& c, uint64_t off,
                                           uint32_t B, uint32_t* dst, uint32_t* ext,
                                           uint32_t* s_cnt, int wm, int wo) {
   const int we = wo > wm ? wo - wm : 0;
@@ -474,14 +477,14 @@ template <int RM, int V, int TIN, bool AP, bool SUB, bool PRE, int DL, int WM, i
 __device__ __forceinline__ uint32_t fused_transform_pack(const FusedArgs& A, const float4 (&vr)[V],
                                                          const float4* park, const float (&uu)[V][4],
                                                          const ElemConsts& c, int64_t base,
-                                                         uint64_t off, uint32_t* pk) {
+                                                         uint64_t off, uint32_t* pk,
+                                                         uint32_t epoch) {
   constexpr int VR = V < 4 ? V : 4;
   constexpr int kWE = (WM > 0 && WO > 0) ? (WO > WM ? WO - WM : 0) : -1;
   const int wm = WM > 0 ? WM : A.bm - 1, wo = WO > 0 ? WO : A.bo - 1;
   const int we = kWE >= 0 ? kWE : (wo > wm ? wo - wm : 0);
-  const uint32_t F = fixed_words(wm), VA = pk_var_words(we);
+  const uint32_t F = fixed_words(wm), VA = pk_var_words(we, V);
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-  uint32_t* elist = pk + 2u * F;          // [kSegs][kSegEsc][2]
   uint32_t* seg = pk + pk_seg_off(wm);
   uint32_t* meta = pk + pk_meta_off(wm);  // [4][4]: words, n_out | n_esc << 16, fits
   const uint32_t pmask = (1u << wm) - 1u;
@@ -492,8 +495,16 @@ __device__ __forceinline__ uint32_t fused_transform_pack(const FusedArgs& A, con
   const uint32_t pw0 = ppos0 >> 5, psft = ppos0 & 31u;
   uint32_t n_out_all = 0;
   float4* __restrict__ y4 = reinterpret_cast<float4*>(A.y);
+  // Phase A: every group's codes and its blocks' sizes first, so the workgroup's aggregate goes
+  // out before the stream is built — the wait for the predecessors' aggregates then overlaps the
+  // y stores and the block images (phase B). q and the sides stay in registers between the phases.
+  float qa[V][4];
+  uint32_t hla[V];  // bit i: z > T of element i, bit 4 + i: z < -T
+  uint32_t* tots = pk + pk_tot_off(wm);  // [V][16] wave totals: outliers | escapes << 16
 #pragma unroll
   for (int u = 0; u < V; ++u) {
+    hla[u] = 0u;
+    qa[u][0] = qa[u][1] = qa[u][2] = qa[u][3] = 0.0f;
     const uint32_t B = (uint32_t)blockIdx.x * (uint32_t)V + (uint32_t)u;
     if (B >= A.pk.n_blocks) break;  // (uniform: the grid's last workgroup may hold fewer blocks)
     const int64_t j = base + (int64_t)u * kSmallT;
@@ -511,13 +522,45 @@ __device__ __forceinline__ uint32_t fused_transform_pack(const FusedArgs& A, con
     }
     const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
     const float us[4] = {u0, u1, u2, u3};
+    uint32_t cnt = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool hi, lo, esc;
+      qa[u][i] = smaq_quant<RM, false, TIN, SUB>(xs[i], us[i], c, hi, lo);
+      hla[u] |= (hi ? 1u << i : 0u) | (lo ? 16u << i : 0u);
+      (void)code_sel(qa[u][i], hi | lo, lo, hm, side, lim_m, esc);
+      cnt += valid ? ((hi | lo) ? 1u : 0u) + (esc ? 0x10000u : 0u) : 0u;
+    }
+    const uint32_t wt = wave_sum_u32(cnt);
+    if (lane == 0) tots[16 * u + w] = wt;
+  }
+  lds_barrier();
+  if (tid == 0 && blockIdx.x + 1 < A.G) {  // (the last workgroup's aggregate is nobody's prefix)
+    uint32_t agg = 0u;
+    for (int u = 0; u < V; ++u) {
+      if ((uint32_t)blockIdx.x * (uint32_t)V + (uint32_t)u >= A.pk.n_blocks) break;
+      uint32_t t = 0u;
+#pragma unroll
+      for (int ww = 0; ww < kSmallWaves; ++ww) t += tots[16 * u + ww];
+      agg += ext_words(we, t & 0xffffu) + 2u * (t >> 16);
+    }
+    st_sc1_u64(A.pk.look + blockIdx.x, ((unsigned long long)epoch << 32) | agg);
+  }
+  // Phase B: per block, y and the block's image from the registers
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const uint32_t B = (uint32_t)blockIdx.x * (uint32_t)V + (uint32_t)u;
+    if (B >= A.pk.n_blocks) break;
+    const int64_t j = base + (int64_t)u * kSmallT;
+    const bool valid = j < A.nv;
     float ys[4];
     uint32_t code[4], on = 0u, en = 0u;
     float qv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      bool hi, lo, esc;
-      qv[i] = smaq_quant<RM, false, TIN, SUB>(xs[i], us[i], c, hi, lo);
+      bool esc;
+      const bool hi = (hla[u] >> i) & 1u, lo = (hla[u] >> (4 + i)) & 1u;
+      qv[i] = qa[u][i];
       ys[i] = smaq_dequant<false, AP, false, false>(qv[i], hi, lo, c);
       const bool o = hi | lo;
       code[i] = valid ? code_sel(qv[i], o, lo, hm, side, lim_m, esc) : 0u;
@@ -590,21 +633,6 @@ __device__ __forceinline__ uint32_t fused_transform_pack(const FusedArgs& A, con
       const uint32_t glo = group8_or_to_last((uint32_t)ch), ghi = group8_or_to_last((uint32_t)(ch >> 32));
       ech = ((uint64_t)ghi << 32) | glo;
     }
-    if (__builtin_expect(en != 0u, 0)) {  // escapes (rare): the segment's list at their rank
-      uint32_t r = pre >> 16;
-      uint32_t* L = elist + 2 * kSegEsc * w;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if ((en >> i) & 1u) {
-          if (r < (uint32_t)kSegEsc) {
-            const float qe = qv[i];
-            L[2 * r] = 4u * (uint32_t)tid + (uint32_t)i;
-            L[2 * r + 1] = qe == qe ? __float_as_uint(qe) : 0x7fc00000u;
-          }
-          ++r;
-        }
-      }
-    }
     lds_barrier();
     // the other image's plane for the next block (its last reader, block u - 1's fixed store, is
     // behind the barrier above; its first writer, block u + 1, behind the one below)
@@ -621,10 +649,9 @@ __device__ __forceinline__ uint32_t fused_transform_pack(const FusedArgs& A, con
     sincl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sincl, 0x118, 0xf, 0xf, false);
     const uint32_t sexcl = sincl - own;
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)sincl, kSegs - 1);
-    const bool seg_over = __ballot(lane < kSegs && (own >> 16) > (uint32_t)kSegEsc) != 0ull;
     const uint32_t n_o = tot & 0xffffu, n_e = tot >> 16;
     const uint32_t n_ext = ext_words(we, n_o);
-    const bool fits = !seg_over && n_e <= (uint32_t)kPkEsc;
+    const bool fits = n_e <= pk_esc_cap(V);
     const uint32_t sbase = (uint32_t)__builtin_amdgcn_readlane((int)sexcl, w);
     if (we > 0 && (kWE == 2 || on)) {
       if (kWE == 2) {
@@ -643,14 +670,17 @@ __device__ __forceinline__ uint32_t fused_transform_pack(const FusedArgs& A, con
         }
       }
     }
-    // escapes: lane l of wave w copies entry l of segment w's list to its rank
-    if (fits && n_e) {
-      const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)own, w) >> 16;
-      if ((uint32_t)lane < sc) {
-        const uint32_t* L = elist + 2 * kSegEsc * w;
-        const uint32_t r = (sbase >> 16) + (uint32_t)lane;
-        var[n_ext + 2u * r] = L[2 * lane];
-        var[n_ext + 2u * r + 1u] = L[2 * lane + 1];
+    // escapes (their q still in registers): each straight to its rank in the block's list
+    if (__builtin_expect(en != 0u, 0) && fits) {
+      uint32_t r = (sbase >> 16) + (pre >> 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if ((en >> i) & 1u) {
+          const float qe = qv[i];
+          var[n_ext + 2u * r] = 4u * (uint32_t)tid + (uint32_t)i;
+          var[n_ext + 2u * r + 1u] = qe == qe ? __float_as_uint(qe) : 0x7fc00000u;
+          ++r;
+        }
       }
     }
     if (tid == 0) {
@@ -674,18 +704,15 @@ __device__ __forceinline__ void fused_pack_finish(const FusedArgs& A, const Elem
                                                   uint64_t off, uint32_t epoch,
                                                   const SmqSmaqStats& st, uint32_t* pk) {
   const int wm = A.bm - 1, wo = A.bo - 1, we = wo > wm ? wo - wm : 0;
-  const uint32_t VA = pk_var_words(we);
+  const uint32_t VA = pk_var_words(we, V);
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const int b = blockIdx.x, G = A.G;
   const uint32_t* meta = pk + pk_meta_off(wm);
   unsigned long long* s_red = reinterpret_cast<unsigned long long*>(pk + pk_red_off(wm));
   const uint32_t B0 = (uint32_t)b * (uint32_t)V;
   const int nbk = (int)min((uint32_t)V, A.pk.n_blocks - B0);
-  uint32_t agg = 0u;
-  for (int u = 0; u < nbk; ++u) agg += meta[4 * u];
-  if (tid == 0 && b + 1 < G)  // (the last workgroup's aggregate is nobody's prefix)
-    st_sc1_u64(A.pk.look + b, ((unsigned long long)epoch << 32) | agg);
-  // the aggregates of workgroups 0 .. b-1 (dispatched before this one), one per thread
+  // the aggregates of workgroups 0 .. b-1 (dispatched before this one; published by their phase
+  // A, fused_transform_pack), one per thread
   unsigned long long v = 0ull;
   if (tid < b) {
     for (;;) {
@@ -786,8 +813,12 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   uint32_t* pk = reinterpret_cast<uint32_t*>(park) + A.pk.lds_off;  // (PACK)
   if constexpr (PACK) {  // the planes and outlier-bit areas are built by ORs: zero, loads in flight
     const int wm = A.bm - 1, we = A.bo > A.bm ? A.bo - A.bm : 0;
-    const uint32_t words = pk_lds_words(wm, we, V);
-    for (uint32_t i = threadIdx.x; i < words; i += kSmallT) pk[i] = 0u;
+    uint32_t* plane0 = pk + kMaskWords;  // (image 1's plane: in block 0's iteration)
+    for (uint32_t i = threadIdx.x; i < 128u * (uint32_t)wm; i += kSmallT) plane0[i] = 0u;
+    for (int u = 0; u < V; ++u) {
+      uint32_t* ext = pk + pk_var_off(wm) + (uint32_t)u * pk_var_words(we, V);
+      for (uint32_t i = threadIdx.x; i < 128u * (uint32_t)we; i += kSmallT) ext[i] = 0u;
+    }
   }
   const double shift = stats_shift<TIN>(A.x, A.n);
   const uint32_t gen = G > 1 ? ld_sc1_u32(A.gen) : 0u;
@@ -1009,12 +1040,12 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   if constexpr (PACK) {
     if (sst.quot_check) {
       n_out = A.all_pos
-                  ? fused_transform_pack<RM, V, TIN, true, true, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk)
-                  : fused_transform_pack<RM, V, TIN, false, true, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk);
+                  ? fused_transform_pack<RM, V, TIN, true, true, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk, epoch)
+                  : fused_transform_pack<RM, V, TIN, false, true, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk, epoch);
     } else {
       n_out = A.all_pos
-                  ? fused_transform_pack<RM, V, TIN, true, false, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk)
-                  : fused_transform_pack<RM, V, TIN, false, false, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk);
+                  ? fused_transform_pack<RM, V, TIN, true, false, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk, epoch)
+                  : fused_transform_pack<RM, V, TIN, false, false, PRE, DL, PWM, PWO>(A, v, park, uu, c, base, off, pk, epoch);
     }
   } else if (sst.quot_check) {
     if (A.all_pos) {
