@@ -41,6 +41,7 @@
 #include <torch/csrc/autograd/functions/utils.h>
 #include <torch/csrc/autograd/python_variable.h>
 
+#include <cstddef>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -112,20 +113,27 @@ struct RecPool {
 };
 RecPool g_rec_pool;
 
-// The next record (its device pointer) and the fp64 view [n_outlier, new_size, ratio, orig_size]
-// of its values.
-SmqSizeRecord* rec_take(const at::Tensor& like, hipStream_t st, at::Tensor* values) {
+// A counted call's log_size values as the logger gets them: 0-dim fp64 device views of its record.
+struct RecValues {
+  at::Tensor ratio, new_size, orig_size;
+};
+
+// The next record (its device pointer) and the views of its values.
+SmqSizeRecord* rec_take(const at::Tensor& like, hipStream_t st, RecValues* values) {
   RecPool& P = g_rec_pool;
   const int dev = like.get_device();
   if (P.next >= kPoolRecs || P.dev != dev || P.st != st) {
-    P.buf = at::zeros({kPoolRecs * kRecWords}, like.options().dtype(at::kLong));
+    P.buf = at::zeros({kPoolRecs * kRecWords}, like.options().dtype(at::kDouble));
     P.dev = dev;
     P.st = st;
     P.next = 0;
   }
   const int64_t i = P.next++;
-  *values = P.buf.view(at::kDouble).narrow(0, i * kRecWords + 12, 4);
-  return reinterpret_cast<SmqSizeRecord*>(P.buf.data_ptr<int64_t>() + i * kRecWords);
+  const int64_t v = i * kRecWords + (int64_t)(offsetof(SmqSizeRecord, n_outlier) / 8);
+  values->new_size = P.buf.select(0, v + 1);
+  values->ratio = P.buf.select(0, v + 2);
+  values->orig_size = P.buf.select(0, v + 3);
+  return reinterpret_cast<SmqSizeRecord*>(P.buf.data_ptr<double>() + i * kRecWords);
 }
 
 // rng.__dict__ holds seed / offset (smart_compress_amd/_native.py RngState); the call takes n
@@ -253,10 +261,10 @@ enum RunResult { kError = -1, kDecline = 0, kDone = 1, kStale = 2 };
 
 // One SmartFP call on t (GIL held): kDone with *out set, kDecline (the Python path handles it),
 // kStale (the hparams changed since the state was built), kError (Python error set).
-// rec: with ratio logging, the fp64 [n_outlier, new_size, compression_ratio, orig_size] values of
-// the call (device); a caller that passes none gets kDecline for a counting codec.
+// rec: with ratio logging, the call's compression_ratio / new_size / orig_size (0-dim fp64 device
+// views of its record); a caller that passes none gets kDecline for a counting codec.
 RunResult smaq_run(SmaqState& s, const at::Tensor& t, bool all_positive, at::Tensor* out,
-                   at::Tensor* rec = nullptr) {
+                   RecValues* rec = nullptr) {
   for (int i = 0; i < kSnap; ++i)
     if (PyDict_GetItem(s.hp_dict.o, g_snap_keys[i]) != s.snap[i].o) return kStale;
   if (s.decline || !t.is_cuda() || (s.count && !rec)) return kDecline;
@@ -305,12 +313,28 @@ RunResult smaq_run(SmaqState& s, const at::Tensor& t, bool all_positive, at::Ten
 PyObject* g_log_rec = nullptr;  // "_log_size_record"
 PyObject* g_fwd_tag = nullptr;  // "forward_autograd"
 
-// codec._log_size_record(tag, values) (GIL held): the counted call's log_size, values on the device
-bool log_record(PyObject* codec, PyObject* tag, at::Tensor&& rec) {
-  PyObject* rv = THPVariable_Wrap(std::move(rec));
-  if (!rv) return false;
-  PyObject* r = PyObject_CallMethodObjArgs(codec, g_log_rec, tag, rv, nullptr);
-  Py_DECREF(rv);
+// (ratio, new_size, orig_size) as a new tuple of tensors, or NULL (Python error set)
+PyObject* rec_tuple(RecValues&& v) {
+  PyObject* a = THPVariable_Wrap(std::move(v.ratio));
+  PyObject* b = a ? THPVariable_Wrap(std::move(v.new_size)) : nullptr;
+  PyObject* c = b ? THPVariable_Wrap(std::move(v.orig_size)) : nullptr;
+  PyObject* r = c ? PyTuple_Pack(3, a, b, c) : nullptr;
+  Py_XDECREF(a);
+  Py_XDECREF(b);
+  Py_XDECREF(c);
+  return r;
+}
+
+// codec._log_size_record(tag, ratio, new_size, orig_size) (GIL held): the counted call's log_size,
+// values on the device
+bool log_record(PyObject* codec, PyObject* tag, RecValues&& rec) {
+  PyObject* a = THPVariable_Wrap(std::move(rec.ratio));
+  PyObject* b = a ? THPVariable_Wrap(std::move(rec.new_size)) : nullptr;
+  PyObject* c = b ? THPVariable_Wrap(std::move(rec.orig_size)) : nullptr;
+  PyObject* r = c ? PyObject_CallMethodObjArgs(codec, g_log_rec, tag, a, b, c, nullptr) : nullptr;
+  Py_XDECREF(a);
+  Py_XDECREF(b);
+  Py_XDECREF(c);
   Py_XDECREF(r);
   return r != nullptr;
 }
@@ -329,7 +353,8 @@ PyObject* smaq(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
   const int ap = PyObject_IsTrue(a[2]);
   if (ap < 0) return nullptr;
-  at::Tensor y, rec;
+  at::Tensor y;
+  RecValues rec;
   switch (smaq_run(s, THPVariable_Unpack(a[1]), ap != 0, &y, &rec)) {
     case kDone: break;
     case kDecline: Py_RETURN_NONE;
@@ -337,9 +362,9 @@ PyObject* smaq(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
     default: return nullptr;
   }
   if (!s.count) return THPVariable_Wrap(std::move(y));
-  // ratio logging: (y, values) — the codec logs them under the call's tag
+  // ratio logging: (y, (ratio, new_size, orig_size)) — the codec logs them under the call's tag
   PyObject* yo = THPVariable_Wrap(std::move(y));
-  PyObject* ro = yo ? THPVariable_Wrap(std::move(rec)) : nullptr;
+  PyObject* ro = yo ? rec_tuple(std::move(rec)) : nullptr;
   if (!ro) {
     Py_XDECREF(yo);
     return nullptr;
@@ -467,7 +492,8 @@ struct SmaqCompressBackward : public torch::autograd::Node {
     if (!task_should_compute_output(0)) return {at::Tensor()};
     if (!g.defined() || !state) return {g};
     PyGILState_STATE gs = PyGILState_Ensure();
-    at::Tensor out, rec;
+    at::Tensor out;
+    RecValues rec;
     RunResult r = smaq_run(*state, g, false, &out, &rec);
     if (r == kDone && state->count && !log_record(codec.o, g_bwd_tag, std::move(rec))) r = kError;
     if (r == kDecline || r == kStale) {  // the codec's own call (it rebuilds a stale state)
@@ -530,7 +556,8 @@ PyObject* smaq_autograd(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   const int bwd = PyObject_IsTrue(a[3]);
   if (bwd < 0) return nullptr;
   const at::Tensor& x = THPVariable_Unpack(a[1]);
-  at::Tensor y, rec;
+  at::Tensor y;
+  RecValues rec;
   switch (smaq_run(**sp, x, false, &y, &rec)) {
     case kDone: break;
     case kDecline: Py_RETURN_NONE;

@@ -30,7 +30,7 @@ import torch
 
 from .. import _native as N
 from ..util.globals import Globals, profile
-from .base import CompressionAlgorithmBase
+from .base import CompressionAlgorithmBase, _reduce_fx
 
 _F32 = {}
 _WS_BYTES = {}  # (numel, device-drawn samples or -1) -> workspace bytes
@@ -71,6 +71,7 @@ _SMAQ_FLAGS = (
 )
 
 _range_coef_cache = {}
+_SIZE_FX = {"reduce_fx": _reduce_fx, "tbptt_reduce_fx": _reduce_fx}  # base.py's "*size*" metrics
 
 
 def quot_check_for(sc: float) -> int:
@@ -310,7 +311,7 @@ class SmartFP(CompressionAlgorithmBase):
             if y is not None and y is not NotImplemented:
                 if type(y) is tuple:  # --measure_compression_ratio: (y, its log_size values)
                     y, rec = y
-                    self._log_size_record(tag, rec)
+                    self._log_size_record(tag, *rec)
                 return y
         # Without the binding (or on graph-safe streams): the same call through the CPython
         # fast-call binding (ctypes' argument conversion costs ~4 us). Everything else: _call,
@@ -442,17 +443,30 @@ class SmartFP(CompressionAlgorithmBase):
         self.log_size(tag, numel * 32, new_size if hp.measure_compression_ratio else None)
         return y
 
-    def _log_size_record(self, tag, rec: torch.Tensor):
-        """log_size of a counted call (csrc/torchfast.cpp, smq_smaq_roundtrip_counted): ``rec`` is
-        the call's fp64 device tensor [n_outlier, new_size, compression_ratio, orig_size], written
-        by the call itself. The metrics are logged as 0-dim device tensors — the same values the
-        host path logs as floats (smart.py:184-188, base.py:72-102), converted only when the logger
-        consumes them, so a measuring step has no host synchronisation per call."""
-        _, new, ratio, orig = rec.unbind()
-        self._emit({"compression_ratio": ratio, f"compression_ratio_{tag}": ratio,
-                    "new_size": new, f"new_size_{tag}": new,
-                    "orig_size": orig, f"orig_size_{tag}": orig},
-                   custom=tag.startswith("optimizer_"))
+    _size_keys = {}  # tag -> the six metric names (the f-strings of base.log_size, built once)
+
+    def _log_size_record(self, tag, ratio, new_size, orig_size):
+        """log_size of a counted call (csrc/torchfast.cpp, smq_smaq_roundtrip_counted): the values
+        are 0-dim fp64 device tensors the call itself wrote — the same values the host path logs
+        as floats (smart.py:184-188, base.py:72-102), converted only when the logger consumes them,
+        so a measuring step has no host synchronisation per call. Same keys, order, reduce_fx and
+        log / log_custom routing as CompressionAlgorithmBase.log_size."""
+        keys = SmartFP._size_keys.get(tag)
+        if keys is None:
+            keys = SmartFP._size_keys[tag] = (
+                "compression_ratio", f"compression_ratio_{tag}", "new_size", f"new_size_{tag}",
+                "orig_size", f"orig_size_{tag}", tag.startswith("optimizer_"))
+        if keys[6] and self.log_custom is not None:
+            self.log_custom({keys[0]: ratio, keys[1]: ratio, keys[2]: new_size,
+                             keys[3]: new_size, keys[4]: orig_size, keys[5]: orig_size})
+            return
+        log, fx = self.log, _SIZE_FX
+        log(keys[0], ratio)
+        log(keys[1], ratio)
+        log(keys[2], new_size, **fx)
+        log(keys[3], new_size, **fx)
+        log(keys[4], orig_size, **fx)
+        log(keys[5], orig_size, **fx)
 
     # bench.py sets an event recorder here: an event pair on the codec's stream around the call's
     # launches (the product entry point either way)

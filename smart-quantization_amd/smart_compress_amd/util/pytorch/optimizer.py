@@ -134,7 +134,8 @@ class OptimLP(Optimizer):
                 codec.log_ratio(tag, n * 32, 32, 32)  # smart.py:125
                 continue
             if recs is not None:
-                codec._log_size_record(tag, recs[multi.index_of(t)])
+                _, new, ratio, orig = recs[multi.index_of(t)].unbind()
+                codec._log_size_record(tag, ratio, new, orig)
                 continue
             n_out = stats[multi.index_of(t)]["n_outlier"]
             codec.log_size(tag, n * 32, n_out * hp.num_bits_outlier + (n - n_out) * hp.num_bits_main)

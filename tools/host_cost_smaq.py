@@ -71,7 +71,19 @@ def main():
             v.sum().backward()
         return f
 
+    # --measure_compression_ratio (the reference scripts' setting): the counted C path, logging
+    # into a bounded sink
+    import collections
+    sink = collections.deque(maxlen=4096)
+    cr = SmartFP(smaq_hparams(measure_compression_ratio=True))
+    cr.log = lambda k, v, **kw: sink.append((k, v))
+    cr(x, tag="t")
+    comp_r = Compressor(cr)
+    chain_r = [Compressor(cr) for _ in range(16)]
     out = {
+        "smartfp_call_counted": per_call(lambda: cr(x, tag="t")),
+        "autograd_fwd_counted": per_call(lambda: comp_r(xg)),
+        "autograd_chain16_fwd_bwd_counted": per_call(chain_fn(chain_r), 300),
         "smartfp_call": per_call(lambda: c(x)),
         "smartfp_call_python_path": per_call(lambda: slow(x)),
         "autograd_fwd": per_call(lambda: comp(xg)),
@@ -96,6 +108,7 @@ def main():
     pr.enable()
     for _ in range(2000):
         c(x)
+        cr(x, tag="t")
     pr.disable()
     torch.cuda.synchronize()
     pstats.Stats(pr).sort_stats("tottime").print_stats(14)

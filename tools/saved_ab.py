@@ -4,7 +4,8 @@ forward call) and with its packing launches overlapped on a side stream, each
 interleaved over rounds; then the host time of one forward without the GPU waiting (the forward
 enqueued behind 100 large GEMMs, synchronised afterwards) and a cProfile of the packed steps.
 
-python tools/saved_ab.py [rounds]"""
+python tools/saved_ab.py [rounds] [kinds: comma list of smartfp, smartfp_ratio, packed,
+packed_overlap]"""
 
 import cProfile
 import os
@@ -35,8 +36,14 @@ def build(kind):
     net = bench._ResNet().to(dev)
     opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9)
     acts = None
-    if kind == "smartfp":
-        codec = SmartFP(smaq_hparams())
+    if kind in ("smartfp", "smartfp_ratio"):
+        # smartfp_ratio: --measure_compression_ratio (every reference script's setting), logged
+        # into a bounded in-memory sink (bench.py autograd smaq_eager_ratio)
+        codec = SmartFP(smaq_hparams(measure_compression_ratio=kind == "smartfp_ratio"))
+        if kind == "smartfp_ratio":
+            import collections
+            sink = collections.deque(maxlen=1 << 14)
+            codec.log = lambda k, v, _s=sink, **kw: _s.append((k, v))
         register_autograd_module(net, codec, flags)
     else:
         codec = SmartFPPacked(smaq_hparams())
@@ -75,7 +82,7 @@ def timed(step, k=20):
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    kinds = ["smartfp", "packed", "packed_overlap"]
+    kinds = (sys.argv[2] if len(sys.argv) > 2 else "smartfp,packed,packed_overlap").split(",")
     global busy
     busy = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     built = {k: build(k) for k in kinds}
@@ -111,6 +118,8 @@ def main():
             loss.backward()
             torch.cuda.synchronize()
         print(f"host forward ms ({k}, device busy):", [round(v, 3) for v in hs], flush=True)
+    if "packed" not in built:
+        return
     acts = built["packed"][2]
     print("packed stats", acts.stats(), flush=True)
     pr = cProfile.Profile()
