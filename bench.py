@@ -1123,6 +1123,12 @@ def run_autograd(args, world, rank, device):
     if "smaq_eager_ratio" in results and "smaq_eager" in results:
         results["smaq_eager_ratio"]["vs_smaq_eager"] = round(
             results["smaq_eager_ratio"]["ms_per_step"] / results["smaq_eager"]["ms_per_step"], 4)
+    tpk = os.path.join(REPO, "profiles", f"traffic_{args.config}_packed.json")
+    if "smaq_eager_packed_saved" in results and os.path.exists(tpk):
+        # HBM bytes per step of the packed-saved variant's codec launches (PMC passes,
+        # tools/saved_traffic.py)
+        with open(tpk) as f:
+            results["smaq_eager_packed_saved"]["traffic"] = json.load(f)["hbm_bytes_per_step"]
     if "smaq_eager_packed_saved" in results and "smaq_eager" in results:
         results["smaq_eager_packed_saved"]["vs_smaq_eager"] = round(
             results["smaq_eager_packed_saved"]["ms_per_step"] / results["smaq_eager"]["ms_per_step"],
