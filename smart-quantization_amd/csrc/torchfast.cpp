@@ -19,6 +19,8 @@
 //                                           grad-map the same way (autograd.py:37-47)
 //   smaq_packed(state, x, ap, getter, frac) PackedActivations' forward call: y and its SmaQ stream
 //                                           (smq_smaq_roundtrip_compress, util/pytorch/saved.py)
+//   smaq_packed_autograd(state, x, acts, bwd, getter, frac)  the same call from Compressor.forward,
+//                                           y with the SmaqCompressBackward node
 //   smaq_unpacked(data, shape, n, bm, bo)   its backward decode (smq_smaq_decompress_ex)
 //   s2fp8(x, check_inf, rng, getter)        one S2FP8 call on an fp32 device tensor
 //
@@ -192,12 +194,17 @@ StatePtr* state_of(PyObject* cap) {
   return static_cast<StatePtr*>(PyCapsule_GetPointer(cap, "smq.SmaqState"));
 }
 
-// smaq_state(template_bytes_allpos0, template_bytes_allpos1, hparams_dict, rng_dict, ws_getter)
+// smaq_state(template_bytes_allpos0, template_bytes_allpos1, hparams_dict, rng_dict, ws_getter
+//            [, allow_count]): allow_count False — the ratio-logging calls decline (a subclass
+//            codec whose log_size values are not SmartFP's)
 PyObject* smaq_state(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
-  if (nargs != 5) {
-    PyErr_SetString(PyExc_TypeError, "smaq_state(tmpl0, tmpl1, hparams_dict, rng_dict, ws_getter)");
+  if (nargs != 5 && nargs != 6) {
+    PyErr_SetString(PyExc_TypeError,
+                    "smaq_state(tmpl0, tmpl1, hparams_dict, rng_dict, ws_getter[, allow_count])");
     return nullptr;
   }
+  const int allow_count = nargs == 6 ? PyObject_IsTrue(a[5]) : 1;
+  if (allow_count < 0) return nullptr;
   Py_buffer b0, b1;
   if (PyObject_GetBuffer(a[0], &b0, PyBUF_SIMPLE) < 0) return nullptr;
   if (PyObject_GetBuffer(a[1], &b1, PyBUF_SIMPLE) < 0) {
@@ -246,6 +253,7 @@ PyObject* smaq_state(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   for (int i = 5; i <= 7; i += 2)  // use_range_std_dev, use_sample_stats
     if (s->snap[i].o && PyObject_IsTrue(s->snap[i].o) == 1) s->decline = true;
   s->count = s->snap[6].o && PyObject_IsTrue(s->snap[6].o) == 1;  // measure_compression_ratio
+  if (s->count && !allow_count) s->decline = true;
   s->rng_dict.o = a[3];
   Py_INCREF(a[3]);
   s->ws_getter.o = a[4];
@@ -386,46 +394,33 @@ size_t stream_capacity(int64_t n, int bm, int bo, double escape_frac) {
                   4 * (nb * fixed_words + var_words));
 }
 
-// smaq_packed(state, x, all_positive, pack_ws_getter, escape_frac) -> (y, stream) | None |
-// NotImplemented: PackedActivations' forward call (util/pytorch/saved.py) in one C call — y as
-// smaq() returns it and its stream (smq_smaq_roundtrip_compress) in a new buffer of
-// stream_capacity bytes. The same declines as smaq().
-PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
-  if (nargs != 5) {
-    PyErr_SetString(PyExc_TypeError, "smaq_packed(state, x, all_positive, getter, escape_frac)");
-    return nullptr;
-  }
-  StatePtr* sp = state_of(a[0]);
-  if (!sp) return nullptr;
-  SmaqState& s = **sp;
-  if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
-  const int ap = PyObject_IsTrue(a[2]);
-  if (ap < 0) return nullptr;
-  const double frac = PyFloat_AsDouble(a[4]);
-  if (frac == -1.0 && PyErr_Occurred()) return nullptr;
+// PackedActivations' forward call on t (GIL held): y as smaq_run computes it and its stream
+// (smq_smaq_roundtrip_compress) in a new buffer of stream_capacity bytes. The same declines as
+// smaq_run (and ratio logging: PackedActivations logs the stream's own size).
+RunResult packed_run(SmaqState& s, const at::Tensor& t, bool ap, PyObject* getter, double frac,
+                     at::Tensor* y_out, at::Tensor* data_out) {
   for (int i = 0; i < kSnap; ++i)
-    if (PyDict_GetItem(s.hp_dict.o, g_snap_keys[i]) != s.snap[i].o) Py_RETURN_NOTIMPLEMENTED;
-  const at::Tensor& t = THPVariable_Unpack(a[1]);
-  if (s.decline || s.count || !t.is_cuda()) Py_RETURN_NONE;
+    if (PyDict_GetItem(s.hp_dict.o, g_snap_keys[i]) != s.snap[i].o) return kStale;
+  if (s.decline || s.count || !t.is_cuda()) return kDecline;
   int code;
   switch (t.scalar_type()) {
     case at::kFloat: code = SMQ_DTYPE_F32; break;
     case at::kBFloat16: code = SMQ_DTYPE_BF16; break;
     case at::kHalf:
-      if (!s.allow_f16) Py_RETURN_NONE;
+      if (!s.allow_f16) return kDecline;
       code = SMQ_DTYPE_F16;
       break;
-    default: Py_RETURN_NONE;
+    default: return kDecline;
   }
   const int64_t n = t.numel();
-  if (n < s.min_size) Py_RETURN_NONE;
+  if (n < s.min_size) return kDecline;
   at::Tensor x = t.is_contiguous() ? t : t.detach().contiguous();
   const int dev = x.get_device();
   const hipStream_t st = c10::hip::getCurrentHIPStream(dev).stream();
-  if (!ws_lookup(s.pws, a[3], dev, st, smq_smaq_pack_workspace_bytes(n))) return nullptr;
+  if (!ws_lookup(s.pws, getter, dev, st, smq_smaq_pack_workspace_bytes(n))) return kError;
   SmqSmaqParams p = s.tmpl[ap ? 1 : 0];
   const size_t cap = stream_capacity(n, p.num_bits_main, p.num_bits_outlier, frac);
-  if (!rng_take(s.rng_dict.o, (uint64_t)n, &p.seed, &p.offset)) return nullptr;
+  if (!rng_take(s.rng_dict.o, (uint64_t)n, &p.seed, &p.offset)) return kError;
   at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kFloat));
   at::Tensor data = at::empty({(int64_t)cap}, x.options().dtype(at::kByte));
   const int rc = smq_smaq_roundtrip_compress(x.const_data_ptr(), code, y.mutable_data_ptr<float>(),
@@ -434,8 +429,15 @@ PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   if (rc) {
     PyErr_Format(PyExc_RuntimeError, "smq_smaq_roundtrip_compress failed (rc=%d): %s", rc,
                  smq_last_error());
-    return nullptr;
+    return kError;
   }
+  *y_out = std::move(y);
+  *data_out = std::move(data);
+  return kDone;
+}
+
+// (y, data) as a new tuple, or NULL
+PyObject* pair_of(at::Tensor&& y, at::Tensor&& data) {
   PyObject* yo = THPVariable_Wrap(std::move(y));
   PyObject* dobj = yo ? THPVariable_Wrap(std::move(data)) : nullptr;
   if (!dobj) {
@@ -446,6 +448,29 @@ PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   Py_DECREF(yo);
   Py_DECREF(dobj);
   return r;
+}
+
+// smaq_packed(state, x, all_positive, pack_ws_getter, escape_frac) -> (y, stream) | None |
+// NotImplemented: PackedActivations' forward call (util/pytorch/saved.py) in one C call.
+PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
+  if (nargs != 5) {
+    PyErr_SetString(PyExc_TypeError, "smaq_packed(state, x, all_positive, getter, escape_frac)");
+    return nullptr;
+  }
+  StatePtr* sp = state_of(a[0]);
+  if (!sp) return nullptr;
+  if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
+  const int ap = PyObject_IsTrue(a[2]);
+  if (ap < 0) return nullptr;
+  const double frac = PyFloat_AsDouble(a[4]);
+  if (frac == -1.0 && PyErr_Occurred()) return nullptr;
+  at::Tensor y, data;
+  switch (packed_run(**sp, THPVariable_Unpack(a[1]), ap != 0, a[3], frac, &y, &data)) {
+    case kDone: return pair_of(std::move(y), std::move(data));
+    case kDecline: Py_RETURN_NONE;
+    case kStale: Py_RETURN_NOTIMPLEMENTED;
+    default: return nullptr;
+  }
 }
 
 // smaq_unpacked(data, shape, n, num_bits_main, num_bits_outlier) -> y: PackedActivations' backward
@@ -577,6 +602,44 @@ PyObject* smaq_autograd(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   return THPVariable_Wrap(std::move(y));
 }
 
+// smaq_packed_autograd(state, x, acts, backward, pack_ws_getter, escape_frac) -> (y, stream) |
+// None | NotImplemented: Compressor.forward with PackedActivations inside its context
+// (util/pytorch/saved.py): the packed forward call (packed_run) and the SmaqCompressBackward node,
+// whose backward is the codec's plain call on the grad-map (what PackedActivations does for
+// backward-direction calls); its declines go to acts(grad, tag="backward_autograd").
+PyObject* smaq_packed_autograd(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
+  if (nargs != 6) {
+    PyErr_SetString(PyExc_TypeError,
+                    "smaq_packed_autograd(state, x, acts, backward, getter, escape_frac)");
+    return nullptr;
+  }
+  StatePtr* sp = state_of(a[0]);
+  if (!sp) return nullptr;
+  if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
+  const int bwd = PyObject_IsTrue(a[3]);
+  if (bwd < 0) return nullptr;
+  const double frac = PyFloat_AsDouble(a[5]);
+  if (frac == -1.0 && PyErr_Occurred()) return nullptr;
+  const at::Tensor& x = THPVariable_Unpack(a[1]);
+  at::Tensor y, data;
+  switch (packed_run(**sp, x, false, a[4], frac, &y, &data)) {
+    case kDone: break;
+    case kDecline: Py_RETURN_NONE;
+    case kStale: Py_RETURN_NOTIMPLEMENTED;
+    default: return nullptr;
+  }
+  if (torch::autograd::compute_requires_grad(x)) {
+    auto node = std::shared_ptr<SmaqCompressBackward>(new SmaqCompressBackward(),
+                                                      torch::autograd::deleteNode);
+    if (bwd) node->state = *sp;
+    node->codec.o = a[2];
+    Py_INCREF(a[2]);
+    node->set_next_edges(torch::autograd::collect_next_edges(x));
+    torch::autograd::set_history(y, node);
+  }
+  return pair_of(std::move(y), std::move(data));
+}
+
 // ---- S2FP8 (fp32 device tensors at precision 32, s2fp8.py:27-48) --------------------------------
 WsSlot g_s2_ws;
 
@@ -621,6 +684,9 @@ PyMethodDef kMethods[] = {
      "Compressor.forward with a SmartFP codec: y and its SmaqCompressBackward node"},
     {"smaq_packed", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_packed)),
      METH_FASTCALL, "PackedActivations' forward call: (y, stream) (smq_smaq_roundtrip_compress)"},
+    {"smaq_packed_autograd",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_packed_autograd)),
+     METH_FASTCALL, "Compressor.forward with PackedActivations: (y, stream), y with its node"},
     {"smaq_unpacked",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(smaq_unpacked)), METH_FASTCALL,
      "PackedActivations' backward decode of a device stream (smq_smaq_decompress_ex)"},

@@ -263,10 +263,14 @@ class SmartFP(CompressionAlgorithmBase):
         d = hp if isinstance(hp, dict) else getattr(hp, "__dict__", None)
         hot = False
         call = type(self).__call__
+        own = call is SmartFP.__call__
         if (T is not None and not self._graph_safe and type(d) is dict
-                and (call is SmartFP.__call__ or call is getattr(type(self), "_smartfp_call", None))):
+                and (own or call is getattr(type(self), "_smartfp_call", None))):
+            # a subclass whose __call__ returns SmartFP's values shares the C state, but not its
+            # ratio logging (allow_count False: counted calls decline): the counted values are
+            # SmartFP's bit counts, SmartFPPacked logs the real stream size
             hot = T.smaq_state(bytes(self._flag_params(False)), bytes(self._flag_params(True)),
-                               d, self.rng.__dict__, N.ws_getter("smaq"))
+                               d, self.rng.__dict__, N.ws_getter("smaq"), own)
         object.__setattr__(self, "_hot", hot)
         return hot
 

@@ -176,6 +176,36 @@ class PackedActivations:
         codec.log_size(tag, n * 32, lambda: full.nbytes * 8)
         return self._register(y, full)
 
+    def _autograd_fast(self, x: torch.Tensor, backward: bool):
+        """Compressor.forward for this compress_fn in C (util/pytorch/autograd.py): inside the
+        context, the packed forward call and a C++ autograd node whose backward is the codec's plain
+        call on the grad-map (as __call__ serves backward-direction calls); outside it, the codec's
+        own C autograd path. None when the C path does not take the call (the Python Function
+        then does: the same calls and values)."""
+        codec = self.codec
+        if self._hooks is None:
+            return codec._autograd_fast(x, backward)
+        if self.overlap or not x.is_cuda or Globals.profiler is not None or codec._trace is not None:
+            return None
+        hot = codec._hot
+        if hot is None:
+            hot = codec._build_hot()
+        if hot is False:
+            return None
+        T = N._torch_fast
+        r = T.smaq_packed_autograd(hot, x, self, backward, self._getter, ESCAPE_FRAC)
+        if r is NotImplemented:  # a flag changed: rebuild the state
+            hot = codec._build_hot()
+            if hot is False:
+                return None
+            r = T.smaq_packed_autograd(hot, x, self, backward, self._getter, ESCAPE_FRAC)
+        if r is None or r is NotImplemented:
+            return None
+        y, data = r
+        hp = codec.hparams
+        return self._register(y, SmaqPacked(data, x.shape, x.numel(),
+                                            widths=(hp.num_bits_main, hp.num_bits_outlier)))
+
     def _register(self, y: torch.Tensor, packed: SmaqPacked) -> torch.Tensor:
         """Remember y's stream until autograd saves y (or y dies)."""
         e = _Entry()

@@ -46,8 +46,10 @@ def build(kind):
             codec.log = lambda k, v, _s=sink, **kw: _s.append((k, v))
         register_autograd_module(net, codec, flags)
     else:
+        # packed_v<MiB>: PackedActivations with verify_bytes = <MiB> MiB (default 32)
+        vb = int(kind[len("packed_v"):]) << 20 if kind.startswith("packed_v") else 32 << 20
         codec = SmartFPPacked(smaq_hparams())
-        acts = PackedActivations(codec, overlap=kind == "packed_overlap")
+        acts = PackedActivations(codec, verify_bytes=vb, overlap=kind == "packed_overlap")
         register_autograd_module(net, acts, flags)
     return net, opt, acts
 
