@@ -265,6 +265,13 @@ def test_integration_doc_binding_matches_the_library_struct():
     lib_fields = [(f[0], getattr(N.SmqSmaqParams, f[0]).offset) for f in N.SmqSmaqParams._fields_]
     doc_fields = [(f[0], getattr(mirror, f[0]).offset) for f in mirror._fields_]
     assert doc_fields == lib_fields
+    # the ratio-logging record mirror (round 6) likewise
+    block = re.search(r"class SmqSizeRecord\(ctypes.Structure\):.*?\)\][^\n]*\n", doc, flags=re.S).group(0)
+    exec(block, ns)
+    rec = ns["SmqSizeRecord"]
+    assert C.sizeof(rec) == C.sizeof(N.SmqSizeRecord) == 128
+    assert [(f[0], getattr(rec, f[0]).offset) for f in rec._fields_] == \
+        [(f[0], getattr(N.SmqSizeRecord, f[0]).offset) for f in N.SmqSizeRecord._fields_]
 
 
 def test_shipped_library_reads_no_environment():
