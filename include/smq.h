@@ -613,6 +613,24 @@ int smq_smaq_roundtrip_compress_ex(const void* x, int dtype, float* y, int64_t n
                                    const SmqSmaqParams* params, void* packed, size_t packed_bytes,
                                    void* workspace, size_t workspace_bytes, void* stream,
                                    void* pack_stream);
+/* smq_smaq_roundtrip_compress whose launch that writes the header also stores header.total_bytes
+ * into *notify as a 32-bit value (SMQ_NOTIFY_SATURATED when it is 2^32 - 1 or more; NULL: none),
+ * by a system-scope store: with notify in host-mapped coherent memory (hipHostMalloc with
+ * hipHostMallocCoherent) the host sees whether the stream fitted its buffer as soon as the launch
+ * has written it — no event, no copy, no synchronisation. The caller sets *notify to
+ * SMQ_NOTIFY_PENDING before the call. notify must be 4-byte aligned. Reference: the log_size
+ * total (smart.py:184-188) PackedActivations needs to drop the fp32 activation (README.md:25). */
+#define SMQ_NOTIFY_PENDING 0xFFFFFFFFu
+#define SMQ_NOTIFY_SATURATED 0xFFFFFFFEu
+int smq_smaq_roundtrip_compress_notify(const void* x, int dtype, float* y, int64_t n,
+                                       const SmqSmaqParams* params, void* packed,
+                                       size_t packed_bytes, void* workspace,
+                                       size_t workspace_bytes, uint32_t* notify, void* stream);
+/* count notify words in host-mapped coherent memory (hipHostMalloc, coherent | mapped | portable:
+ * one address for the host and every device), each set to SMQ_NOTIFY_PENDING; NULL on failure. Free
+ * with smq_notify_free once no launch that may still write them is in flight. */
+uint32_t* smq_notify_alloc(int64_t count);
+void smq_notify_free(uint32_t* words);
 /* Decode a stream of n elements into y (fp32). n must equal the header's n (a stream with another
  * n or a bad magic leaves y untouched). */
 int smq_smaq_decompress(const void* packed, float* y, int64_t n, void* stream);

@@ -179,6 +179,7 @@ struct FusedArgs {
     uint32_t n_blocks, flags;
     unsigned long long* look;  // [G] epoch-tagged aggregates: replica 0, granules 1024 + b
     uint32_t lds_off;          // word offset of the pack area in the dynamic LDS
+    uint32_t* notify;          // total_bytes also here (notify_total), or NULL
   } pk;
 };
 
@@ -767,6 +768,7 @@ __device__ __forceinline__ void fused_pack_finish(const FusedArgs& A, const Elem
     h->data_words = vb;
     h->total_bytes = sizeof(SmqPackedHeader) + 8ull * dir_entries(A.pk.n_blocks) +
                      4ull * A.pk.n_blocks * fixed_words(wm) + 4ull * vb;
+    notify_total(A.pk.notify, h->total_bytes);
     h->error = 0u;
     h->bn_channels = 0u;
     h->bn_inner = 0;
@@ -1286,6 +1288,7 @@ int launch_fused_pack(const FusedCall& c, const FusedPackCall& k, hipStream_t st
   F.pk.cap_words = k.cap_words;
   F.pk.n_blocks = k.n_blocks;
   F.pk.flags = k.flags;
+  F.pk.notify = k.notify;
   F.pk.look = F.gran + SmaqWsLayout::kFusedPackLook;
   F.pk.lds_off = lds_off;
   if (p->count_outliers) fill_async(F.out_slots, 0ull, SMQ_WS_OUTLIER_SLOTS, st);

@@ -76,6 +76,7 @@ struct PackArgs {
   const float* bn_gamma;     // BN variant (general packer only), else NULL
   const float* bn_beta;
   int64_t bn_channels, bn_inner;
+  uint32_t* notify;          // total_bytes also here (notify_total), or NULL
 };
 
 // smart.py:151-169 for one element, as smaq_quant computes it (same IEEE ops in the same order, so
@@ -604,6 +605,7 @@ __device__ void write_header(const PackArgs& A, uint64_t carry, int tid, int nth
     const uint64_t bn_words = A.bn_gamma ? 2ull * (uint64_t)A.bn_channels : 0ull;
     h->total_bytes = sizeof(SmqPackedHeader) + 8ull * dir_entries(A.n_blocks) +
                      4ull * A.n_blocks * fixed_words(A.wm) + 4ull * (carry + bn_words);
+    notify_total(A.notify, h->total_bytes);
     h->error = 0u;
     h->bn_channels = A.bn_gamma ? (uint32_t)A.bn_channels : 0u;
     h->bn_inner = A.bn_gamma ? A.bn_inner : 0;
@@ -1473,7 +1475,7 @@ static hipEvent_t fork_event() {
 // an event (smq_smaq_roundtrip_compress_ex).
 static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParams* p, float* y,
                          void* packed, size_t packed_bytes, void* ws, size_t ws_bytes,
-                         hipStream_t st, hipStream_t pst = nullptr) {
+                         hipStream_t st, hipStream_t pst = nullptr, uint32_t* notify = nullptr) {
   int rc = smaq_validate(p, dtype);
   if (rc) return rc;
   if (n < 1 || !x || !packed) {
@@ -1545,6 +1547,7 @@ static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParam
     k.var = k.fixed + (size_t)nb * fixed_words(wm);
     k.cap_words = packed_bytes >= bound ? ~0ull : (uint64_t)((packed_bytes - fixed) / 4);
     k.n_blocks = (uint32_t)nb;
+    k.notify = notify;
     const RangeRecips R0 = range_recips(p->range_main, p->range_outlier);
     k.flags = (p->all_positive ? SMQ_PACK_FLAG_ALL_POSITIVE : 0u) |
               (R0.safe_q ? SMQ_PACK_FLAG_SAFE_Q : 0u);
@@ -1603,6 +1606,7 @@ static int compress_impl(const void* x, int dtype, int64_t n, const SmqSmaqParam
   const bool sr = p->stochastic_rounding != 0;
   A.lb = lb ? 1u : 0u;
   A.lb_status = (unsigned long long*)(wb + L.scratch);
+  A.notify = notify;
   if (!zeroed) fill_async(zero, 0u, zero_n, st);  // (sampled statistics: smq_common.h)
   if (pst && pst != st) {  // the packing launches on their own stream, behind the statistics
     const hipEvent_t ev = fork_event();
@@ -1663,6 +1667,48 @@ int smq_smaq_roundtrip_compress_ex(const void* x, int dtype, float* y, int64_t n
   }
   return compress_impl(x, dtype, n, p, y, packed, packed_bytes, ws, ws_bytes,
                        (hipStream_t)stream, (hipStream_t)pack_stream);
+}
+
+uint32_t* smq_notify_alloc(int64_t count) {
+  if (count < 1 || count > (1ll << 28)) {
+    set_error("notify_alloc: count must be in [1, 2^28]");
+    return nullptr;
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, (size_t)count * 4,
+                    hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess ||
+      !p) {
+    set_error("notify_alloc: hipHostMalloc of %lld words failed", (long long)count);
+    return nullptr;
+  }
+  void* d = nullptr;  // kernels write the words through the host address: it must be the device's
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || d != p) {
+    (void)hipHostFree(p);
+    set_error("notify_alloc: host-mapped memory has a different device address");
+    return nullptr;
+  }
+  uint32_t* w = (uint32_t*)p;
+  for (int64_t i = 0; i < count; ++i) w[i] = SMQ_NOTIFY_PENDING;
+  return w;
+}
+
+void smq_notify_free(uint32_t* words) {
+  if (words) (void)hipHostFree(words);
+}
+
+int smq_smaq_roundtrip_compress_notify(const void* x, int dtype, float* y, int64_t n,
+                                       const SmqSmaqParams* p, void* packed, size_t packed_bytes,
+                                       void* ws, size_t ws_bytes, uint32_t* notify, void* stream) {
+  if (!y) {
+    set_error("roundtrip_compress: y must be a device pointer");
+    return SMQ_ERR_INVALID;
+  }
+  if (((uintptr_t)notify & 3u) != 0) {
+    set_error("roundtrip_compress_notify: notify must be 4-byte aligned");
+    return SMQ_ERR_INVALID;
+  }
+  return compress_impl(x, dtype, n, p, y, packed, packed_bytes, ws, ws_bytes,
+                       (hipStream_t)stream, nullptr, notify);
 }
 
 static int decompress_impl(const void* packed, float* y, int64_t n, int bm, int bo, void* stream) {

@@ -66,4 +66,13 @@ __device__ __forceinline__ void or_bits32(uint32_t* base, uint32_t pos, uint32_t
 // known; a segment with more (an escape-heavy block) makes the var kernel re-code the block.
 constexpr int kSegEsc = 32;
 
+// The stream's total_bytes for a caller that learns it without an event or a copy
+// (smq_smaq_roundtrip_compress_notify): a system-scope store of the saturated 32-bit value, so
+// host-mapped coherent memory holds it as soon as the header is written. NULL: no notification.
+__device__ __forceinline__ void notify_total(uint32_t* p, uint64_t total) {
+  if (p)
+    __hip_atomic_store(p, total < SMQ_NOTIFY_SATURATED ? (uint32_t)total : SMQ_NOTIFY_SATURATED,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace smq

@@ -295,6 +295,7 @@ struct FusedPackCall {
   uint32_t* var;
   uint64_t cap_words;  // words of the variable region the buffer holds
   uint32_t n_blocks, flags;
+  uint32_t* notify;     // total_bytes also here (smq_smaq_roundtrip_compress_notify), or NULL
 };
 constexpr int kFusedPackDeclined = 1;  // not this call's shape: nothing launched
 int launch_fused_pack(const FusedCall& c, const FusedPackCall& k, hipStream_t st);

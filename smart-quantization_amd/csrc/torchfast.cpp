@@ -17,10 +17,12 @@
 //   smaq_autograd(state, x, codec, bwd)     Compressor.forward for a SmartFP codec: the forward
 //                                           call plus a C++ Node whose backward compresses the
 //                                           grad-map the same way (autograd.py:37-47)
-//   smaq_packed(state, x, ap, getter, frac) PackedActivations' forward call: y and its SmaQ stream
-//                                           (smq_smaq_roundtrip_compress, util/pytorch/saved.py)
-//   smaq_packed_autograd(state, x, acts, bwd, getter, frac)  the same call from Compressor.forward,
-//                                           y with the SmaqCompressBackward node
+//   smaq_packed(state, x, ap, getter, frac[, notify])  PackedActivations' forward call: y and its
+//                                           SmaQ stream (smq_smaq_roundtrip_compress_notify,
+//                                           util/pytorch/saved.py; notify: the address of a
+//                                           host-mapped word that receives the stream's size)
+//   smaq_packed_autograd(state, x, acts, bwd, getter, frac[, notify])  the same call from
+//                                           Compressor.forward, y with the SmaqCompressBackward node
 //   smaq_unpacked(data, shape, n, bm, bo)   its backward decode (smq_smaq_decompress_ex)
 //   s2fp8(x, check_inf, rng, getter)        one S2FP8 call on an fp32 device tensor
 //
@@ -395,10 +397,11 @@ size_t stream_capacity(int64_t n, int bm, int bo, double escape_frac) {
 }
 
 // PackedActivations' forward call on t (GIL held): y as smaq_run computes it and its stream
-// (smq_smaq_roundtrip_compress) in a new buffer of stream_capacity bytes. The same declines as
-// smaq_run (and ratio logging: PackedActivations logs the stream's own size).
+// (smq_smaq_roundtrip_compress_notify) in a new buffer of stream_capacity bytes, its size also into
+// *notify (NULL: not). The same declines as smaq_run (and ratio logging: PackedActivations logs the
+// stream's own size).
 RunResult packed_run(SmaqState& s, const at::Tensor& t, bool ap, PyObject* getter, double frac,
-                     at::Tensor* y_out, at::Tensor* data_out) {
+                     uint32_t* notify, at::Tensor* y_out, at::Tensor* data_out) {
   for (int i = 0; i < kSnap; ++i)
     if (PyDict_GetItem(s.hp_dict.o, g_snap_keys[i]) != s.snap[i].o) return kStale;
   if (s.decline || s.count || !t.is_cuda()) return kDecline;
@@ -423,11 +426,11 @@ RunResult packed_run(SmaqState& s, const at::Tensor& t, bool ap, PyObject* gette
   if (!rng_take(s.rng_dict.o, (uint64_t)n, &p.seed, &p.offset)) return kError;
   at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kFloat));
   at::Tensor data = at::empty({(int64_t)cap}, x.options().dtype(at::kByte));
-  const int rc = smq_smaq_roundtrip_compress(x.const_data_ptr(), code, y.mutable_data_ptr<float>(),
-                                             n, &p, data.mutable_data_ptr(), cap, s.pws.ptr,
-                                             s.pws.bytes, st);
+  const int rc = smq_smaq_roundtrip_compress_notify(
+      x.const_data_ptr(), code, y.mutable_data_ptr<float>(), n, &p, data.mutable_data_ptr(), cap,
+      s.pws.ptr, s.pws.bytes, notify, st);
   if (rc) {
-    PyErr_Format(PyExc_RuntimeError, "smq_smaq_roundtrip_compress failed (rc=%d): %s", rc,
+    PyErr_Format(PyExc_RuntimeError, "smq_smaq_roundtrip_compress_notify failed (rc=%d): %s", rc,
                  smq_last_error());
     return kError;
   }
@@ -450,13 +453,25 @@ PyObject* pair_of(at::Tensor&& y, at::Tensor&& data) {
   return r;
 }
 
-// smaq_packed(state, x, all_positive, pack_ws_getter, escape_frac) -> (y, stream) | None |
-// NotImplemented: PackedActivations' forward call (util/pytorch/saved.py) in one C call.
+// The optional notify argument: None or the address (an int) of a host-mapped word; false on a
+// Python error.
+bool notify_arg(PyObject* const* a, Py_ssize_t nargs, Py_ssize_t i, uint32_t** out) {
+  *out = nullptr;
+  if (nargs <= i || a[i] == Py_None) return true;
+  *out = (uint32_t*)PyLong_AsVoidPtr(a[i]);
+  return !PyErr_Occurred();
+}
+
+// smaq_packed(state, x, all_positive, pack_ws_getter, escape_frac[, notify]) -> (y, stream) | None
+// | NotImplemented: PackedActivations' forward call (util/pytorch/saved.py) in one C call.
 PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
-  if (nargs != 5) {
-    PyErr_SetString(PyExc_TypeError, "smaq_packed(state, x, all_positive, getter, escape_frac)");
+  if (nargs != 5 && nargs != 6) {
+    PyErr_SetString(PyExc_TypeError,
+                    "smaq_packed(state, x, all_positive, getter, escape_frac[, notify])");
     return nullptr;
   }
+  uint32_t* notify;
+  if (!notify_arg(a, nargs, 5, &notify)) return nullptr;
   StatePtr* sp = state_of(a[0]);
   if (!sp) return nullptr;
   if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
@@ -465,7 +480,7 @@ PyObject* smaq_packed(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   const double frac = PyFloat_AsDouble(a[4]);
   if (frac == -1.0 && PyErr_Occurred()) return nullptr;
   at::Tensor y, data;
-  switch (packed_run(**sp, THPVariable_Unpack(a[1]), ap != 0, a[3], frac, &y, &data)) {
+  switch (packed_run(**sp, THPVariable_Unpack(a[1]), ap != 0, a[3], frac, notify, &y, &data)) {
     case kDone: return pair_of(std::move(y), std::move(data));
     case kDecline: Py_RETURN_NONE;
     case kStale: Py_RETURN_NOTIMPLEMENTED;
@@ -602,17 +617,19 @@ PyObject* smaq_autograd(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
   return THPVariable_Wrap(std::move(y));
 }
 
-// smaq_packed_autograd(state, x, acts, backward, pack_ws_getter, escape_frac) -> (y, stream) |
-// None | NotImplemented: Compressor.forward with PackedActivations inside its context
+// smaq_packed_autograd(state, x, acts, backward, pack_ws_getter, escape_frac[, notify]) ->
+// (y, stream) | None | NotImplemented: Compressor.forward with PackedActivations inside its context
 // (util/pytorch/saved.py): the packed forward call (packed_run) and the SmaqCompressBackward node,
 // whose backward is the codec's plain call on the grad-map (what PackedActivations does for
 // backward-direction calls); its declines go to acts(grad, tag="backward_autograd").
 PyObject* smaq_packed_autograd(PyObject*, PyObject* const* a, Py_ssize_t nargs) {
-  if (nargs != 6) {
+  if (nargs != 6 && nargs != 7) {
     PyErr_SetString(PyExc_TypeError,
-                    "smaq_packed_autograd(state, x, acts, backward, getter, escape_frac)");
+                    "smaq_packed_autograd(state, x, acts, backward, getter, escape_frac[, notify])");
     return nullptr;
   }
+  uint32_t* notify;
+  if (!notify_arg(a, nargs, 6, &notify)) return nullptr;
   StatePtr* sp = state_of(a[0]);
   if (!sp) return nullptr;
   if (!THPVariable_Check(a[1])) Py_RETURN_NONE;
@@ -622,7 +639,7 @@ PyObject* smaq_packed_autograd(PyObject*, PyObject* const* a, Py_ssize_t nargs) 
   if (frac == -1.0 && PyErr_Occurred()) return nullptr;
   const at::Tensor& x = THPVariable_Unpack(a[1]);
   at::Tensor y, data;
-  switch (packed_run(**sp, x, false, a[4], frac, &y, &data)) {
+  switch (packed_run(**sp, x, false, a[4], frac, notify, &y, &data)) {
     case kDone: break;
     case kDecline: Py_RETURN_NONE;
     case kStale: Py_RETURN_NOTIMPLEMENTED;

@@ -129,6 +129,8 @@ class SmqPackedHeader(ctypes.Structure):
 
 SMQ_PACK_MAGIC = 0x50514D53
 SMQ_PACK_BLOCK = 4096
+SMQ_NOTIFY_PENDING = 0xFFFFFFFF    # a notify word not written yet (smq_smaq_roundtrip_compress_notify)
+SMQ_NOTIFY_SATURATED = 0xFFFFFFFE  # a stream of 2^32 - 1 bytes or more
 SMQ_PACK_FLAG_ALL_POSITIVE = 1
 SMQ_PACK_FLAG_SAFE_Q = 2
 SMQ_PACK_FLAG_BOTH_SIDES = 4
@@ -304,6 +306,11 @@ SIGNATURES = {
                                            _P, _SZ, _P, _SZ, _P]),
     "smq_smaq_roundtrip_compress_ex": (_I32, [_P, _I32, _P, _I64, ctypes.POINTER(SmqSmaqParams),
                                               _P, _SZ, _P, _SZ, _P, _P]),
+    "smq_smaq_roundtrip_compress_notify": (_I32, [_P, _I32, _P, _I64,
+                                                  ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P, _SZ,
+                                                  _P, _P]),
+    "smq_notify_alloc": (_P, [_I64]),
+    "smq_notify_free": (None, [_P]),
     "smq_smaq_pack_workspace_bytes_sampled": (_SZ, [_I64, _I64]),
     "smq_cpu_smaq_compress": (_I32, [_P, _I32, _I64, ctypes.POINTER(SmqSmaqParams), _P, _SZ, _P,
                                      _SZ, _I32]),

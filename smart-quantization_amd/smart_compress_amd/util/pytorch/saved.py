@@ -22,9 +22,9 @@ statistics), the stream written straight into a buffer of ``capacity`` bytes —
 Only a stream larger than that (escape-heavy data) does not fit, which its header records, so until
 its size is checked the saved ``y`` is kept too. The sizes travel to the host without a
 synchronisation (a device gather, an asynchronous copy to pinned memory, an event), in batches
-of ``verify_bytes`` (32 MiB) of pending ``y``; a batch whose sizes have arrived drops the ``y`` of
-every stream that fit, and the host waits (for the oldest batch's event only) when more than
-``verify_bytes`` are still on their way, and at the context's exit. A stream that did not fit
+of ``verify_batch`` (8 MiB) of pending ``y``; a batch whose sizes have arrived drops the ``y`` of
+every stream that fit, and the host waits (for the oldest batches' events only) when more than
+``verify_bytes`` (32 MiB) are still on their way, and at the context's exit. A stream that did not fit
 (never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
 The forward call is one C call where it applies (csrc/torchfast.cpp ``smaq_packed``: SmartFP's
 parameter template, the output allocations and ``smq_smaq_roundtrip_compress``). Overlap
@@ -38,10 +38,13 @@ Backward-direction calls (grad-maps, never saved) and calls outside the context 
 own call (the same values as the codec's decompress(compress(x)), one launch instead of five).
 """
 
+import ctypes
+import time
 import weakref
 from collections import deque
 from typing import Deque, Dict, List, Optional
 
+import numpy as np
 import torch
 
 from ... import _native as N
@@ -69,18 +72,82 @@ def stream_capacity(n: int, num_bits_main: int, num_bits_outlier: int, bn_channe
             + 8 * bn_channels)
 
 
+class _NotifyRing:
+    """Words of host-mapped coherent memory (smq_notify_alloc) into which the forward calls' packing
+    launches store their stream's size (smq_smaq_roundtrip_compress_notify): the host reads whether
+    a stream fitted its capacity with a load — no event, copy or synchronisation per call. One ring
+    per process, never freed (a launch in flight may still write a word). A word is free to take
+    again once no handle holds it and its last launch has written it (a word still pending may be
+    written late: never re-armed under it)."""
+
+    WORDS = 1 << 14
+
+    def __init__(self):
+        ptr = N.lib().smq_notify_alloc(self.WORDS)
+        if not ptr:
+            raise RuntimeError("smq_notify_alloc failed: "
+                               + N.lib().smq_last_error().decode(errors="replace"))
+        self.base = ptr
+        self.words = np.ctypeslib.as_array((ctypes.c_uint32 * self.WORDS).from_address(ptr))
+        self.words[:] = 0  # free
+        self.held = bytearray(self.WORDS)
+        self.next = 0
+
+    def take(self) -> Optional[int]:
+        """A word armed (SMQ_NOTIFY_PENDING) for the next call, or None when the next few are
+        still busy (the call then takes the event path)."""
+        w, held = self.words, self.held
+        for _ in range(16):
+            i = self.next
+            self.next = (i + 1) % self.WORDS
+            if not held[i] and w[i] != N.SMQ_NOTIFY_PENDING:
+                held[i] = 1
+                w[i] = N.SMQ_NOTIFY_PENDING
+                return i
+        return None
+
+    def release(self, i: int, written: bool = True) -> None:
+        """Nobody reads word i any more; written=False: no launch will write it (the call was
+        declined or failed)."""
+        if not written:
+            self.words[i] = 0
+        self.held[i] = 0
+
+
+_RING: Optional[_NotifyRing] = None
+
+
+def _notify_ring() -> Optional[_NotifyRing]:
+    global _RING
+    if _RING is None:
+        try:
+            _RING = _NotifyRing()
+        except (RuntimeError, OSError, AttributeError):
+            _RING = False  # no host-mapped memory here: every call takes the event path
+    return _RING or None
+
+
+def _drop_entry(live: dict, key: int, ring) -> None:
+    """The weak reference's callback: a forward output died before (or after) being saved."""
+    e = live.pop(key, None)
+    if e is not None and e.slot is not None:
+        ring.release(e.slot)
+        e.slot = None
+
+
 class _Saved:
     """What autograd holds instead of a saved activation: the stream (and, until its size is
     checked, the activation itself), the activation's version counter value when it was saved and
     a weak reference to it (saved_tensors_hooks turn off autograd's own in-place check: _unpack
-    repeats it)."""
+    repeats it), and the notify word its size arrives in (None: the event path)."""
 
-    __slots__ = ("packed", "y", "codec", "version", "ref", "modified")
+    __slots__ = ("packed", "y", "codec", "version", "ref", "modified", "slot")
 
     def __init__(self, packed: SmaqPacked, y: torch.Tensor, codec: SmartFPPacked, version: int,
-                 ref):
+                 ref, slot: Optional[int] = None):
         self.packed, self.y, self.codec = packed, y, codec
         self.version, self.ref, self.modified = version, ref, None
+        self.slot = slot
 
     def check_version(self) -> None:
         """Raise autograd's in-place error when the saved activation was modified after it was
@@ -101,15 +168,20 @@ class _Saved:
 
 
 class _Entry:
-    __slots__ = ("ref", "packed", "version", "shape", "stride", "dtype", "handle")
+    __slots__ = ("ref", "packed", "version", "shape", "stride", "dtype", "handle", "slot")
 
 
 class PackedActivations:
-    def __init__(self, codec: SmartFPPacked, verify_bytes: int = 32 << 20, overlap: bool = False):
+    def __init__(self, codec: SmartFPPacked, verify_bytes: int = 32 << 20, overlap: bool = False,
+                 verify_batch: Optional[int] = None):
         if not isinstance(codec, SmartFPPacked):
             raise TypeError("PackedActivations needs a SmartFPPacked codec")
         self.codec = codec
         self.verify_bytes = int(verify_bytes)
+        # the event path (calls without a notify word): a size request per verify_batch bytes of
+        # saved activations (default: the budget; smaller batches cost more host time per step
+        # than the waits they save, profiles/r6p_saved_ab.txt)
+        self.verify_batch = int(verify_batch) if verify_batch is not None else self.verify_bytes
         # overlap: the packing launches of each forward call on a side stream (they wait for the
         # call's statistics, then run beside the next layers), with a ring of _RING workspaces
         self.overlap = bool(overlap)
@@ -121,6 +193,10 @@ class PackedActivations:
         self._live: Dict[int, _Entry] = {}  # data_ptr of a forward output -> its stream
         self._pending: List[_Saved] = []     # saved, size not yet checked (y still held)
         self._pending_bytes = 0
+        # saved with a notify word: size not read yet (y still held), in call order
+        self._notified: Deque[_Saved] = deque()
+        self._notified_bytes = 0
+        self._notify: Optional[_NotifyRing] = None  # the process's ring, at the first C call
         # batches whose sizes are on their way to the host: (event, pinned sizes, handles, bytes)
         self._inflight: Deque[tuple] = deque()
         self._inflight_bytes = 0
@@ -149,16 +225,23 @@ class PackedActivations:
                 hot = codec._build_hot()
             r = None
             if hot is not False and Globals.profiler is None and codec._trace is None:
-                r = N._torch_fast.smaq_packed(hot, x, all_positive, self._getter, ESCAPE_FRAC)
-                if r is NotImplemented:  # a flag changed: rebuild the state
-                    hot = codec._build_hot()
-                    r = (N._torch_fast.smaq_packed(hot, x, all_positive, self._getter,
-                                                   ESCAPE_FRAC) if hot is not False else None)
+                slot, addr = self._arm()
+                try:
+                    r = N._torch_fast.smaq_packed(hot, x, all_positive, self._getter, ESCAPE_FRAC,
+                                                  addr)
+                    if r is NotImplemented:  # a flag changed: rebuild the state
+                        hot = codec._build_hot()
+                        r = (N._torch_fast.smaq_packed(hot, x, all_positive, self._getter,
+                                                       ESCAPE_FRAC, addr)
+                             if hot is not False else None)
+                finally:
+                    if slot is not None and (r is None or r is NotImplemented):
+                        self._notify.release(slot, written=False)
             if r is not None and r is not NotImplemented:
                 y, data = r
                 return self._register(y, SmaqPacked(data, x.shape, x.numel(),
                                                     widths=(hp.num_bits_main,
-                                                            hp.num_bits_outlier)))
+                                                            hp.num_bits_outlier)), slot)
         n = x.numel()
         bn = batch_norm_stats is not None and hp.use_batch_norm
         channels = (1 if hp.bn_scalar_params else x.shape[1]) if bn else 0
@@ -193,28 +276,49 @@ class PackedActivations:
         if hot is False:
             return None
         T = N._torch_fast
-        r = T.smaq_packed_autograd(hot, x, self, backward, self._getter, ESCAPE_FRAC)
-        if r is NotImplemented:  # a flag changed: rebuild the state
-            hot = codec._build_hot()
-            if hot is False:
-                return None
-            r = T.smaq_packed_autograd(hot, x, self, backward, self._getter, ESCAPE_FRAC)
+        slot, addr = self._arm()
+        r = None
+        try:
+            r = T.smaq_packed_autograd(hot, x, self, backward, self._getter, ESCAPE_FRAC, addr)
+            if r is NotImplemented:  # a flag changed: rebuild the state
+                hot = codec._build_hot()
+                r = (T.smaq_packed_autograd(hot, x, self, backward, self._getter, ESCAPE_FRAC,
+                                            addr) if hot is not False else None)
+        finally:
+            if slot is not None and (r is None or r is NotImplemented):
+                self._notify.release(slot, written=False)
         if r is None or r is NotImplemented:
             return None
         y, data = r
         hp = codec.hparams
         return self._register(y, SmaqPacked(data, x.shape, x.numel(),
-                                            widths=(hp.num_bits_main, hp.num_bits_outlier)))
+                                            widths=(hp.num_bits_main, hp.num_bits_outlier)), slot)
 
-    def _register(self, y: torch.Tensor, packed: SmaqPacked) -> torch.Tensor:
-        """Remember y's stream until autograd saves y (or y dies)."""
+    def _arm(self):
+        """(word index, its address) for the next C call's size notification, or (None, None)."""
+        ring = self._notify
+        if ring is None:
+            ring = self._notify = _notify_ring()
+            if ring is None:
+                return None, None
+        i = ring.take()
+        return (None, None) if i is None else (i, ring.base + 4 * i)
+
+    def _register(self, y: torch.Tensor, packed: SmaqPacked,
+                  slot: Optional[int] = None) -> torch.Tensor:
+        """Remember y's stream (and the notify word its size arrives in) until autograd saves y
+        (or y dies)."""
         e = _Entry()
         key = y.data_ptr()
-        e.ref = weakref.ref(y, lambda _r, k=key, d=self._live: d.pop(k, None))
+        old = self._live.get(key)
+        if old is not None and old.slot is not None:
+            self._notify.release(old.slot)
+        e.ref = weakref.ref(y, lambda _r, k=key, d=self._live, g=self._notify: _drop_entry(d, k, g))
         e.packed = packed
         e.version = y._version
         e.shape, e.stride, e.dtype = y.shape, y.stride(), y.dtype
         e.handle = None
+        e.slot = slot
         self._live[key] = e
         return y
 
@@ -268,13 +372,22 @@ class PackedActivations:
         self.saved_packed += 1
         if e.handle is not None:  # saved again (another consumer): the same stream
             return e.handle
-        h = e.handle = _Saved(e.packed, y, self.codec, e.version, e.ref)
+        h = e.handle = _Saved(e.packed, y, self.codec, e.version, e.ref, e.slot)
+        if e.slot is not None:  # its size arrives in a notify word: read, never requested
+            e.slot = None  # (the handle holds the word now)
+            self._notified.append(h)
+            self._notified_bytes += 4 * y.numel()
+            # the streams whose sizes are there drop their activations; more than the budget
+            # still waiting: wait for the oldest ones (earlier calls, usually done by then)
+            self._poll(self.verify_bytes)
+            return h
         self._pending.append(h)
         self._pending_bytes += 4 * y.numel()
-        if self._pending_bytes > self.verify_bytes:
+        if self._pending_bytes > self.verify_batch:
             self._request_sizes()
             # the batches whose sizes have arrived drop their activations; more than the budget
-            # still in flight: wait for the oldest batch only (its work is usually done by then)
+            # still in flight: wait for the oldest batches only (their work is usually done by
+            # then; the batch just requested is waited for only when it alone exceeds the budget)
             self._harvest(self.verify_bytes)
         return h
 
@@ -297,6 +410,63 @@ class PackedActivations:
         their way); a stream that fits drops its activation, one that does not keeps it."""
         self._request_sizes()
         self._harvest(0)
+        self._poll(0)
+
+    def _poll(self, max_waiting_bytes: int) -> None:
+        """Finish the notified handles whose size words are written, oldest first; wait for the
+        oldest while more than max_waiting_bytes of activations still wait on theirs."""
+        q, ring = self._notified, self._notify
+        words = ring.words if ring is not None else None
+        while q:
+            h = q[0]
+            total = int(words[h.slot])
+            if total == N.SMQ_NOTIFY_PENDING:
+                if self._notified_bytes <= max_waiting_bytes:
+                    return
+                total = self._wait_word(h)
+            q.popleft()
+            self._notified_bytes -= 4 * h.packed.n
+            ring.release(h.slot)
+            h.slot = None
+            if total == N.SMQ_NOTIFY_SATURATED:  # 4 GiB or more: the header has the size
+                total = int(h.packed.data[_TOTAL_OFF:_TOTAL_OFF + 8].view(torch.int64).item())
+            self._finish(h, total)
+
+    def _wait_word(self, h: _Saved) -> int:
+        """Spin on h's notify word (its launch is queued before everything enqueued since). After
+        a second without it, the stream is synchronised and the header read instead (a launch
+        that did not notify: never expected)."""
+        words, i = self._notify.words, h.slot
+        t0 = time.perf_counter()
+        spins = 0
+        while True:
+            v = int(words[i])
+            if v != N.SMQ_NOTIFY_PENDING:
+                return v
+            spins += 1
+            if spins > 256:  # past ~50 us: short sleeps (which also let other threads run)
+                if time.perf_counter() - t0 > 1.0:
+                    torch.cuda.synchronize(h.packed.data.device)
+                    v = int(words[i])
+                    if v != N.SMQ_NOTIFY_PENDING:
+                        return v
+                    return int(h.packed.data[_TOTAL_OFF:_TOTAL_OFF + 8].view(torch.int64).item())
+                time.sleep(1e-5)
+
+    def _finish(self, h: _Saved, total: int) -> None:
+        """h's stream size is known: drop the activation if the stream fitted its buffer."""
+        cap = h.packed.data.numel()
+        if h.y._version != h.version:  # modified in place since saved: backward raises
+            h.modified = (tuple(h.y.shape), h.y._version)
+        if total <= cap:
+            h.packed._total = int(total)
+            h.y = None
+            self.saved_bytes += int(total)
+            self.saved_capacity += cap
+            self.saved_elements += h.packed.n
+        else:  # did not fit its capacity: the activation stays the saved value
+            h.packed = None
+            self.kept_fp32 += 1
 
     def _request_sizes(self) -> None:
         """Every pending stream's header total_bytes, gathered on the device and copied to pinned
@@ -330,18 +500,7 @@ class PackedActivations:
             self._inflight.popleft()
             self._inflight_bytes -= nbytes
             for h, total in zip(hs, host.view(torch.int64).tolist()):
-                cap = h.packed.data.numel()
-                if h.y._version != h.version:  # modified in place since saved: backward raises
-                    h.modified = (tuple(h.y.shape), h.y._version)
-                if total <= cap:
-                    h.packed._total = int(total)
-                    h.y = None
-                    self.saved_bytes += int(total)
-                    self.saved_capacity += cap
-                    self.saved_elements += h.packed.n
-                else:  # did not fit its capacity: the activation stays the saved value
-                    h.packed = None
-                    self.kept_fp32 += 1
+                self._finish(h, total)
 
     def __enter__(self):
         self._hooks = torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack)
@@ -354,6 +513,11 @@ class PackedActivations:
             self._join()  # backward decodes the streams on the current stream
             self.verify()
         finally:
+            ring = self._notify
+            for e in self._live.values():
+                if e.slot is not None:
+                    ring.release(e.slot)
+                    e.slot = None
             self._live.clear()
             hooks.__exit__(*exc)
         return False

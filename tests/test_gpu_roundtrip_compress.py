@@ -13,6 +13,8 @@ Reference: smart.py:110-190 (y), smart.py:184-188 / README.md:25-28 (the codes k
 """
 
 
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -302,3 +304,69 @@ def test_fused_pack_workspace_of_random_bytes():
                             device="cuda")
         (a, ya), (b, yb) = stream(n, ws), stream(n, fresh)
         assert np.array_equal(a, b) and same_f32(ya, yb), n
+
+
+# smq_smaq_roundtrip_compress_notify: the launch that writes the header also stores total_bytes
+# into a host-mapped word (PackedActivations reads it instead of an event + copy per batch).
+@pytest.mark.parametrize("n,case", [(1 << 20, "pack"), (4 << 20, "pack"), (6_000_000, "lookback"),
+                                    (1_000_003, "lookback"), (9_000_000, "three_launch"),
+                                    (1 << 20, "bn"), (1 << 20, "small_buffer"),
+                                    (3 << 20, "escape_heavy")])
+def test_notify_word_equals_header_total(n, case):
+    from smart_compress_amd import _native as N
+
+    lib = N.lib()
+    hp, rc, _, _ = _codecs()
+    gen = torch.Generator(device="cuda").manual_seed(n % 977 + len(case))
+    x = torch.randn(n, generator=gen, device="cuda") * 1.4
+    if case == "escape_heavy":
+        x[: n // 64] += 40.0
+    bn_args = None
+    if case == "bn":
+        x = x.view(64, 16, -1)
+        g = torch.rand(16, generator=gen, device="cuda") + 0.5
+        b = torch.randn(16, generator=gen, device="cuda") * 0.1
+        bn_args = (g, b)
+    words = lib.smq_notify_alloc(4)
+    assert words
+    try:
+        w = np.ctypeslib.as_array((ctypes.c_uint32 * 4).from_address(words))
+        assert (w == N.SMQ_NOTIFY_PENDING).all()  # armed by the allocation
+        w[1] = 12345  # a neighbour the launch must leave alone
+        p = rc._params(n, False, torch.float32, x.device)
+        if bn_args is not None:  # the BN variant (smart.py:136-149): the general packer
+            p.bn_gamma, p.bn_beta = bn_args[0].data_ptr(), bn_args[1].data_ptr()
+            p.bn_channels, p.bn_inner = 16, x.shape[2]
+        bound = (lib.smq_smaq_pack_bound_bn(n, 6, 8, 16) if bn_args is not None
+                 else lib.smq_smaq_pack_bound(n, 6, 8))
+        cap = bound
+        if case == "small_buffer":
+            cap = lib.smq_smaq_pack_fixed_bytes(n, 6) + 4096
+        out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        y = torch.empty(n, device="cuda")
+        ws = torch.zeros(lib.smq_smaq_pack_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+        assert lib.smq_smaq_roundtrip_compress_notify(
+            x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p, out.data_ptr(), cap,
+            ws.data_ptr(), ws.numel(), ctypes.c_void_p(words), N.stream_ptr(x.device)) == 0, \
+            lib.smq_last_error()
+        torch.cuda.synchronize()
+        hdr = N.SmqPackedHeader.from_buffer_copy(bytes(out[:128].cpu().numpy()))
+        assert int(w[0]) == int(hdr.total_bytes), (case, int(w[0]), int(hdr.total_bytes))
+        assert int(w[1]) == 12345 and int(w[2]) == N.SMQ_NOTIFY_PENDING
+        if case == "small_buffer":
+            assert int(w[0]) > cap  # did not fit: the word says so as the header does
+        # a NULL word: the plain call's bytes
+        out2 = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        assert lib.smq_smaq_roundtrip_compress_notify(
+            x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p, out2.data_ptr(), cap,
+            ws.data_ptr(), ws.numel(), None, N.stream_ptr(x.device)) == 0
+        torch.cuda.synchronize()
+        t = min(int(hdr.total_bytes), cap)
+        if case != "small_buffer":
+            assert torch.equal(out[:t], out2[:t])
+        # misaligned word: refused
+        assert lib.smq_smaq_roundtrip_compress_notify(
+            x.data_ptr(), N.SMQ_DTYPE_F32, y.data_ptr(), n, p, out2.data_ptr(), cap,
+            ws.data_ptr(), ws.numel(), ctypes.c_void_p(words + 2), N.stream_ptr(x.device)) != 0
+    finally:
+        lib.smq_notify_free(ctypes.c_void_p(words))

@@ -80,6 +80,9 @@ def test_packed_saved_activations_bitexact(inplace, overlap):
     st = acts.stats()
     assert st["saved_packed"] >= 8 and 6.0 < st["bits_per_element"] < 9.0, st
     assert st["kept_fp32"] == 0 and st["allocated_bits_per_element"] < 10.5, st
+    if not overlap:  # the C calls' sizes came through notify words, every word released since
+        assert acts._notify is not None and not any(acts._notify.held)
+        assert not acts._notified and not acts._inflight and not acts._pending
     # the memory held between forward and backward shrinks by the packed activations' share
     # (second step: the first one also allocates workspaces)
     assert held_b[1] < 0.8 * held_a[1], (held_a, held_b)

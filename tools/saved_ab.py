@@ -5,7 +5,9 @@ interleaved over rounds; then the host time of one forward without the GPU waiti
 enqueued behind 100 large GEMMs, synchronised afterwards) and a cProfile of the packed steps.
 
 python tools/saved_ab.py [rounds] [kinds: comma list of smartfp, smartfp_ratio, packed,
-packed_overlap]"""
+packed_overlap, packed_event (sizes by batch requests and events instead of notify words),
+packed_v<MiB> (verify_bytes), packed_b<MiB> (the event path's batch)]
+Also prints each kind's step peak above the memory resident before it."""
 
 import cProfile
 import os
@@ -48,8 +50,16 @@ def build(kind):
     else:
         # packed_v<MiB>: PackedActivations with verify_bytes = <MiB> MiB (default 32)
         vb = int(kind[len("packed_v"):]) << 20 if kind.startswith("packed_v") else 32 << 20
+        # packed_b<MiB>: verify_batch = <MiB> MiB for the event path (default verify_bytes); b0:
+        # one batch per budget (round 6's first form: the host waited for the call it had enqueued)
+        vbat = None
+        if kind.startswith("packed_b"):
+            vbat = int(kind[len("packed_b"):]) << 20 or vb
         codec = SmartFPPacked(smaq_hparams())
-        acts = PackedActivations(codec, verify_bytes=vb, overlap=kind == "packed_overlap")
+        acts = PackedActivations(codec, verify_bytes=vb, overlap=kind == "packed_overlap",
+                                 verify_batch=vbat)
+        if kind == "packed_event":  # round 6's first form: sizes by batch requests + events
+            acts._arm = lambda: (None, None)
         register_autograd_module(net, acts, flags)
     return net, opt, acts
 
@@ -97,6 +107,15 @@ def main():
         for k in kinds:
             res[k].append(round(timed(steps[k][0]), 3))
     print("ms/step", res, flush=True)
+    mem = {}
+    for k in kinds:  # one step's peak above the memory resident before it (bench.py's measure)
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated(dev)
+        torch.cuda.reset_peak_memory_stats(dev)
+        steps[k][0]()
+        torch.cuda.synchronize()
+        mem[k] = round((torch.cuda.max_memory_allocated(dev) - base) / 2**20, 1)
+    print("step peak above resident MiB", mem, flush=True)
     # host time of one forward with the device busy: the enqueue cost alone (until the context's
     # exit; a verify inside the forward would wait for the busy device, so the budget is lifted)
     for k in kinds:
