@@ -1107,6 +1107,7 @@ def run_autograd(args, world, rank, device):
             results[name].update(codec_calls_per_step=calls_per,
                                  compressed_elements_per_step=elems)
         if packed:
+            codec.verify()  # (the last step's sizes: nothing waits for them at the context's exit)
             st = codec.stats()
             results[name]["saved_streams"] = {
                 "saved_tensors_packed_per_step": round(st["saved_packed"] / (args.steps + args.warmup + 2), 1),

@@ -15,17 +15,23 @@ random stream (include/smq.h "Packed SmaQ container"). Inside ``with activations
 it again: the gradients equal those of the unpacked SmaQ run bit for bit, while a saved activation
 takes ~8 bits per element (6/8-bit codes) instead of 32.
 
-Memory without host synchronisation per call: ``y`` and its stream come from one call
+Memory without host synchronisation per call or per step: ``y`` and its stream come from one call
 (``SmartFPPacked.roundtrip_compress``: SmartFP's round trip, then the packing launches on its
 statistics), the stream written straight into a buffer of ``capacity`` bytes — the fixed region
 (known from n) plus room for every element being an outlier and 1 % escapes (``stream_capacity``).
 Only a stream larger than that (escape-heavy data) does not fit, which its header records, so until
-its size is checked the saved ``y`` is kept too. The sizes travel to the host without a
-synchronisation (a device gather, an asynchronous copy to pinned memory, an event), in batches
-of ``verify_batch`` (8 MiB) of pending ``y``; a batch whose sizes have arrived drops the ``y`` of
-every stream that fit, and the host waits (for the oldest batches' events only) when more than
-``verify_bytes`` (32 MiB) are still on their way, and at the context's exit. A stream that did not fit
-(never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
+its size is checked the saved ``y`` is kept too. The size reaches the host without a
+synchronisation: the C forward call (csrc/torchfast.cpp ``smaq_packed``) hands the library a word of
+host-mapped coherent memory (``smq_smaq_roundtrip_compress_notify``) into which the launch that writes
+the stream's header stores its total_bytes, and the host reads it with a load. Each save reads the
+words that are there (oldest first: a stream that fit drops its ``y``) and waits — for the oldest
+word only, i.e. an earlier call, usually done by then — while more than 256 MiB of activations are
+still waiting (``verify_bytes`` sets it); nothing waits at the context's exit (the rest are read by
+later saves, unpacks or the next entry: ``y`` stays the saved value until then). Calls that take the
+Python path (no notify word) send their sizes in batches of ``verify_batch`` bytes instead (a device
+gather, an asynchronous copy to pinned memory, an event; 32 MiB of held activations at most by
+default), settled at the context's exit. A stream
+that did not fit (never seen on N(0,1)-like data) keeps ``y`` as the saved value instead.
 The forward call is one C call where it applies (csrc/torchfast.cpp ``smaq_packed``: SmartFP's
 parameter template, the output allocations and ``smq_smaq_roundtrip_compress``). Overlap
 (opt-in, ``overlap=True``): the packing launches of a forward call run on a side stream — they
@@ -172,12 +178,18 @@ class _Entry:
 
 
 class PackedActivations:
-    def __init__(self, codec: SmartFPPacked, verify_bytes: int = 32 << 20, overlap: bool = False,
-                 verify_batch: Optional[int] = None):
+    def __init__(self, codec: SmartFPPacked, verify_bytes: Optional[int] = None,
+                 overlap: bool = False, verify_batch: Optional[int] = None):
         if not isinstance(codec, SmartFPPacked):
             raise TypeError("PackedActivations needs a SmartFPPacked codec")
         self.codec = codec
-        self.verify_bytes = int(verify_bytes)
+        # activations held while their sizes are on their way, before the host waits: notified
+        # calls (a load per size: a large budget costs no host time; the ResNet-34 step's peak is
+        # the same with 32 MiB and 1024 MiB, profiles/r6s_saved_ab.txt) and the event path's
+        # batches (whose requests cost host time and whose held activations raised the peak:
+        # 286 / 311 / 363 MiB at 32 / 64 / 128 MiB, profiles/r6o_saved_ab_verify_bytes.txt)
+        self.notify_bytes = int(verify_bytes) if verify_bytes is not None else 256 << 20
+        self.verify_bytes = int(verify_bytes) if verify_bytes is not None else 32 << 20
         # the event path (calls without a notify word): a size request per verify_batch bytes of
         # saved activations (default: the budget; smaller batches cost more host time per step
         # than the waits they save, profiles/r6p_saved_ab.txt)
@@ -206,6 +218,8 @@ class PackedActivations:
         self.saved_capacity = 0  # and the bytes allocated for them
         self.saved_elements = 0  # and their elements
         self.kept_fp32 = 0       # streams cut at their capacity (the activation kept instead)
+        self.size_waits = 0      # times the host waited for a notify word (over the budget)
+        self.size_wait_s = 0.0   # and the seconds it waited
 
     # -- the compress_fn of register_autograd_module ---------------------------------------------
     def __call__(self, x: torch.Tensor, tag: str = None, all_positive=False,
@@ -379,7 +393,7 @@ class PackedActivations:
             self._notified_bytes += 4 * y.numel()
             # the streams whose sizes are there drop their activations; more than the budget
             # still waiting: wait for the oldest ones (earlier calls, usually done by then)
-            self._poll(self.verify_bytes)
+            self._poll(self.notify_bytes)
             return h
         self._pending.append(h)
         self._pending_bytes += 4 * y.numel()
@@ -393,6 +407,8 @@ class PackedActivations:
 
     def _unpack(self, h):
         if isinstance(h, _Saved):
+            if self._notified:  # the sizes that are there by now drop their activations
+                self._poll(self.notify_bytes)
             h.check_version()
             if h.y is not None:  # not checked yet, or cut at its capacity: the activation itself
                 return h.y
@@ -439,9 +455,11 @@ class PackedActivations:
         words, i = self._notify.words, h.slot
         t0 = time.perf_counter()
         spins = 0
+        self.size_waits += 1
         while True:
             v = int(words[i])
             if v != N.SMQ_NOTIFY_PENDING:
+                self.size_wait_s += time.perf_counter() - t0
                 return v
             spins += 1
             if spins > 256:  # past ~50 us: short sleeps (which also let other threads run)
@@ -503,6 +521,8 @@ class PackedActivations:
                 self._finish(h, total)
 
     def __enter__(self):
+        if self._notified:  # (handles of an earlier step whose sizes nobody has read yet)
+            self._poll(self.notify_bytes)
         self._hooks = torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack)
         self._hooks.__enter__()
         return self
@@ -511,7 +531,13 @@ class PackedActivations:
         hooks, self._hooks = self._hooks, None
         try:
             self._join()  # backward decodes the streams on the current stream
-            self.verify()
+            # the event path's batches are settled here; notified handles are not waited for (that
+            # would hold the host until the device has run the whole forward, and backward could not
+            # be enqueued behind it): they keep their activation, within the budget, until their
+            # words are read — by the next save, unpack or context entry
+            self._request_sizes()
+            self._harvest(0)
+            self._poll(self.notify_bytes)
         finally:
             ring = self._notify
             for e in self._live.values():
@@ -530,4 +556,5 @@ class PackedActivations:
                 "saved_stream_bytes": self.saved_bytes,
                 "bits_per_element": 8.0 * self.saved_bytes / el if el else None,
                 "allocated_bits_per_element": 8.0 * self.saved_capacity / el if el else None,
-                "kept_fp32": self.kept_fp32}
+                "kept_fp32": self.kept_fp32, "size_waits": self.size_waits,
+                "size_wait_s": self.size_wait_s}

@@ -48,13 +48,14 @@ def build(kind):
             codec.log = lambda k, v, _s=sink, **kw: _s.append((k, v))
         register_autograd_module(net, codec, flags)
     else:
-        # packed_v<MiB>: PackedActivations with verify_bytes = <MiB> MiB (default 32)
-        vb = int(kind[len("packed_v"):]) << 20 if kind.startswith("packed_v") else 32 << 20
+        # packed_v<MiB>: PackedActivations with verify_bytes = <MiB> MiB (default: 256 for the
+        # notified calls, 32 for the event path)
+        vb = int(kind[len("packed_v"):]) << 20 if kind.startswith("packed_v") else None
         # packed_b<MiB>: verify_batch = <MiB> MiB for the event path (default verify_bytes); b0:
         # one batch per budget (round 6's first form: the host waited for the call it had enqueued)
         vbat = None
         if kind.startswith("packed_b"):
-            vbat = int(kind[len("packed_b"):]) << 20 or vb
+            vbat = int(kind[len("packed_b"):]) << 20 or None
         codec = SmartFPPacked(smaq_hparams())
         acts = PackedActivations(codec, verify_bytes=vb, overlap=kind == "packed_overlap",
                                  verify_batch=vbat)
@@ -83,7 +84,10 @@ def make_step(net, opt, acts):
     return step, fwd
 
 
-def timed(step, k=20):
+STEPS_PER_ROUND = 20
+
+
+def timed(step, k=STEPS_PER_ROUND):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(k):
@@ -103,10 +107,17 @@ def main():
         for _ in range(3):
             steps[k][0]()
     res = {k: [] for k in kinds}
+    w0 = {k: (built[k][2].size_waits, built[k][2].size_wait_s) for k in kinds
+          if built[k][2] is not None}
     for _ in range(rounds):
         for k in kinds:
             res[k].append(round(timed(steps[k][0]), 3))
     print("ms/step", res, flush=True)
+    nsteps = rounds * STEPS_PER_ROUND
+    print("host waits for sizes per step (count, ms)",
+          {k: (round((built[k][2].size_waits - w[0]) / nsteps, 2),
+               round((built[k][2].size_wait_s - w[1]) * 1e3 / nsteps, 3)) for k, w in w0.items()},
+          flush=True)
     mem = {}
     for k in kinds:  # one step's peak above the memory resident before it (bench.py's measure)
         torch.cuda.synchronize()
@@ -127,14 +138,15 @@ def main():
                 busy @ busy
             acts = built[k][2]
             if acts is not None:
-                acts.verify_bytes = 1 << 40
+                budgets = acts.verify_bytes, acts.notify_bytes
+                acts.verify_bytes = acts.notify_bytes = 1 << 40
                 acts.__enter__()
             t0 = time.perf_counter()
             loss = F.cross_entropy(built[k][0](x), t)
             hs.append((time.perf_counter() - t0) * 1e3)  # before the context's exit verify
             if acts is not None:
                 acts.__exit__(None, None, None)
-                acts.verify_bytes = 32 << 20
+                acts.verify_bytes, acts.notify_bytes = budgets
             torch.cuda.synchronize()
             loss.backward()
             torch.cuda.synchronize()
