@@ -295,8 +295,10 @@ int smq_smaq_roundtrip_ex(const void* x, int dtype, float* y, int64_t n, const S
  * per call). These entry points leave the values on the device, as fp64 (exact: < 2^53), for the
  * logger to read when it consumes them. */
 typedef struct SmqSizeRecord {
-  unsigned long long slots[8];   /* outlier-count partials: ZERO on entry (a fresh record per call) */
-  unsigned long long arrived;    /* workgroups counted: ZERO on entry */
+  unsigned long long slots[8];   /* per residue b % 8 of the workgroups: outlier-count partial (low
+                                    40 bits) and arrivals (above); ZERO on entry (a fresh record per
+                                    call) */
+  unsigned long long arrived;    /* residues counted: ZERO on entry */
   unsigned long long reserved[3];
   double n_outlier;              /* written by the call: sum(is_outlier) */
   double new_size;               /* n_outlier * bo + (n - n_outlier) * bm */

@@ -195,19 +195,32 @@ __device__ __forceinline__ void size_record_finish(SmqSizeRecord* rec, uint64_t 
   rec->orig_size = orig;
 }
 
-// Counted call: this workgroup's count s into the record's slot, then its arrival; the last one
-// (every add has returned before its arrival was issued) sums the slots and writes the values.
+// Counted call: this workgroup's count s AND its arrival in ONE returning atomic on its residue's
+// slot (count in the low 40 bits, arrivals above: 32 same-address atomics per word at G = 256
+// instead of 256 on one word, ~12 ns each); the last of a residue then arrives on the top word, and
+// the last of those (every slot add has returned before its residue's top add was issued) sums the
+// slots' counts and writes the values.
+constexpr int kRecArrShift = 40;
 __device__ __forceinline__ void size_record_arrive(SmqSizeRecord* rec, unsigned long long s, int b,
                                                    int G, int64_t n, int bm, int bo) {
-  if (s) (void)__hip_atomic_fetch_add(rec->slots + (b & 7), s, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long prev = __hip_atomic_fetch_add(&rec->arrived, 1ull, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-  if (prev != (unsigned long long)G - 1ull) return;
+  if (G == 1) {
+    size_record_finish(rec, s, n, bm, bo);
+    return;
+  }
+  const int r = b & 7;
+  const unsigned long long prev = __hip_atomic_fetch_add(
+      rec->slots + r, s + (1ull << kRecArrShift), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int in_res = G / 8 + (r < (G & 7) ? 1 : 0);  // workgroups b < G with b % 8 == r
+  if ((int)(prev >> kRecArrShift) != in_res - 1) return;
+  const int residues = G < 8 ? G : 8;
+  const unsigned long long top = __hip_atomic_fetch_add(&rec->arrived, 1ull, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+  if (top != (unsigned long long)residues - 1ull) return;
   unsigned long long t = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i)
-    t += __hip_atomic_load(rec->slots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t += __hip_atomic_load(rec->slots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+         ((1ull << kRecArrShift) - 1ull);
   size_record_finish(rec, t, n, bm, bo);
 }
 

@@ -122,6 +122,17 @@ struct RecValues {
   at::Tensor ratio, new_size, orig_size;
 };
 
+// A 0-dim view of element off of buf, built directly (no dispatcher round trip: select() cost
+// ~0.5 us of host time per view, three per counted call). A plain tensor sharing buf's storage,
+// as select() returns for a buf that does not require grad.
+at::Tensor scalar_view(const at::Tensor& buf, int64_t off) {
+  auto impl = c10::make_intrusive<c10::TensorImpl>(c10::Storage(buf.storage()), buf.key_set(),
+                                                   buf.dtype());
+  impl->set_storage_offset(off);
+  impl->set_sizes_contiguous({});
+  return at::Tensor(std::move(impl));
+}
+
 // The next record (its device pointer) and the views of its values.
 SmqSizeRecord* rec_take(const at::Tensor& like, hipStream_t st, RecValues* values) {
   RecPool& P = g_rec_pool;
@@ -134,9 +145,9 @@ SmqSizeRecord* rec_take(const at::Tensor& like, hipStream_t st, RecValues* value
   }
   const int64_t i = P.next++;
   const int64_t v = i * kRecWords + (int64_t)(offsetof(SmqSizeRecord, n_outlier) / 8);
-  values->new_size = P.buf.select(0, v + 1);
-  values->ratio = P.buf.select(0, v + 2);
-  values->orig_size = P.buf.select(0, v + 3);
+  values->new_size = scalar_view(P.buf, v + 1);
+  values->ratio = scalar_view(P.buf, v + 2);
+  values->orig_size = scalar_view(P.buf, v + 3);
   return reinterpret_cast<SmqSizeRecord*>(P.buf.data_ptr<double>() + i * kRecWords);
 }
 

@@ -464,13 +464,13 @@ class SmartFP(CompressionAlgorithmBase):
             self.log_custom({keys[0]: ratio, keys[1]: ratio, keys[2]: new_size,
                              keys[3]: new_size, keys[4]: orig_size, keys[5]: orig_size})
             return
-        log, fx = self.log, _SIZE_FX
+        log, fx = self.log, _reduce_fx  # (= **_SIZE_FX, without a kwargs dict per call)
         log(keys[0], ratio)
         log(keys[1], ratio)
-        log(keys[2], new_size, **fx)
-        log(keys[3], new_size, **fx)
-        log(keys[4], orig_size, **fx)
-        log(keys[5], orig_size, **fx)
+        log(keys[2], new_size, reduce_fx=fx, tbptt_reduce_fx=fx)
+        log(keys[3], new_size, reduce_fx=fx, tbptt_reduce_fx=fx)
+        log(keys[4], orig_size, reduce_fx=fx, tbptt_reduce_fx=fx)
+        log(keys[5], orig_size, reduce_fx=fx, tbptt_reduce_fx=fx)
 
     # bench.py sets an event recorder here: an event pair on the codec's stream around the call's
     # launches (the product entry point either way)
