@@ -166,6 +166,7 @@ struct FusedArgs {
   uint64_t* trace;  // experiment builds (-DSMQ_FUSED_TRACE=1): 16 timestamps per workgroup
   uint32_t* zero;   // cleared by workgroup 0 (the packer's group sums: roundtrip_compress), or NULL
   uint32_t zero_n;
+  unsigned long long* rec_gran;  // counted call, full statistics: [G] epoch-tagged counts (or NULL)
   SmqSizeRecord* rec;  // counted call (count = 1, out_slots = rec->slots): the last workgroup to
                        // have added its count writes the log_size values
   int bm, bo;
@@ -228,6 +229,9 @@ __device__ __forceinline__ void size_record_arrive(SmqSizeRecord* rec, unsigned 
 #ifndef SMQ_FUSED_TRACE
 #define SMQ_FUSED_TRACE 0
 #endif
+// The thread that issues this workgroup's arrivals: wave 1's lane 0, so a wait for an atomic's
+// return never holds wave 0 (the reduce and finalise) or the barrier after it.
+constexpr int kArriveThread = kWave;
 #if SMQ_FUSED_TRACE
 #define FSTAMP(i)                                                                   \
   do {                                                                              \
@@ -975,7 +979,7 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
     // count this workgroup past the wait now, on its residue's word (eight words of <= 32 arrivals
     // each instead of one word of 256: same-address atomics serialise at ~12 ns each); the
     // returned word is looked at only after the transform
-    if (threadIdx.x == 0) left_old = arrive_tagged_issue(A.sub + (b & 7) * kSubStride);
+    if (threadIdx.x == kArriveThread) left_old = arrive_tagged_issue(A.sub + (b & 7) * kSubStride);
     if (wave == 0) {
       // reduce_partials_w0's order: lane l adds partials 4l .. 4l+3 from 0.0, then one ascending
       // butterfly
@@ -1097,7 +1101,9 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       unsigned long long s = 0;
 #pragma unroll
       for (int w = 0; w < kSmallWaves; ++w) s += sh_cnt[w];
-      if (A.rec) size_record_arrive(A.rec, s, b, G, A.n, A.bm, A.bo);
+      if (A.rec_gran && G > 1)  // one epoch-tagged granule; the call's last workgroup sums them
+        st_sc1_u64(A.rec_gran + b, ((uint64_t)epoch << 32) | (uint32_t)s);
+      else if (A.rec) size_record_arrive(A.rec, s, b, G, A.n, A.bm, A.bo);
       else if (s) atomicAdd(A.out_slots + (b & (SMQ_WS_OUTLIER_SLOTS - 1)), s);
     }
   }
@@ -1105,8 +1111,30 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
   // the last workgroup of its residue arrives on the top word; the last residue's advances the
   // generation and the stream and re-arms the arrival words. Every workgroup has read the
   // generation, the stream position and the granules before its add.
-  if (G > 1 && threadIdx.x == 0 &&
-      arrive_sharded_finish(A.left, A.sub, kSubStride, b, G, gen, left_old)) {
+  const bool last = G > 1 && threadIdx.x == kArriveThread &&
+                    arrive_sharded_finish(A.left, A.sub, kSubStride, b, G, gen, left_old);
+  if (A.rec_gran && G > 1) {
+    // counted call: the last workgroup (every other one is past the gather, so running: no
+    // co-residency question) sums the workgroups' count granules of this epoch into the record —
+    // no returning atomic at every workgroup's end
+    if (threadIdx.x == kArriveThread) smiss[0] = last ? 1 : 0;
+    lds_barrier();
+    if (smiss[0] && wave == 0) {
+      unsigned long long tot = 0;
+      for (int k0 = 0; k0 < G; k0 += kWave) {
+        const int k = k0 + lane;
+        if (k < G) {
+          uint64_t g;
+          while ((uint32_t)((g = ld_sc1_u64(A.rec_gran + k)) >> 32) != epoch) fused_sleep(1);
+          tot += (uint32_t)g;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, kWave);
+      if (lane == 0) size_record_finish(A.rec, tot, A.n, A.bm, A.bo);
+    }
+  }
+  if (last) {
     st_sc1_u32(A.gen, gen + 1u);
     if (A.ctr) st_sc1_u64(A.ctr, off0 + (uint64_t)A.n);
     rearm_sharded(A.left, A.sub, kSubStride, gen + 1u);
@@ -1230,6 +1258,9 @@ static void fused_args(const FusedCall& c, FusedArgs& F) {
   F.bm = p->num_bits_main;
   F.bo = p->num_bits_outlier;
   if (c.rec) F.count = 1;  // (the record's slots are zero: no fill)
+  // the counts as granules in replica 1's spare words (behind its 4-word partials: the range form's
+  // 6-word partials use them, so it keeps the record's atomics)
+  F.rec_gran = (c.rec && !F.range) ? F.gran + SmaqWsLayout::kFusedRecGran : nullptr;
 }
 
 int launch_fused(const FusedCall& c, hipStream_t st) {

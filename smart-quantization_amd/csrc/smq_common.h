@@ -416,6 +416,8 @@ struct SmaqWsLayout {
   // partials of 256 workgroups; the range form's 6-word partials, which it never runs with, reach
   // here but carry other calls' epochs)
   static constexpr size_t kFusedPackLook = 1024;
+  // a counted call's per-workgroup outlier counts (granule index: replica 1's spare words)
+  static constexpr size_t kFusedRecGran = 256 * kFusedWords + 1024;
   static constexpr size_t kTotal = kFusedEnd;
 };
 static_assert(SmaqWsLayout::kTagCounters + 8 * SmaqWsLayout::kTagWords <= SMQ_WS_FUSED_OFFSET,
