@@ -1024,7 +1024,12 @@ def run_autograd(args, world, rank, device):
             if ratio:
                 sink = collections.deque(maxlen=1 << 14)
                 codec.log = lambda k, v, _s=sink, **kw: _s.append((k, v))
-            fn = PackedActivations(codec) if packed else codec
+            fn = codec
+            if packed:
+                fn = PackedActivations(codec, verify_bytes=(args.saved_budget << 20
+                                                            if args.saved_budget else None))
+                if args.saved_exit >= 0:  # (measurement option: the exit's wait, MiB)
+                    fn.exit_bytes = args.saved_exit << 20
             if sizes is not None:
                 def fn(v, tag=None, **kw):
                     sizes.append(v.numel())
@@ -1281,6 +1286,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variants", default="",
                     help="--config autograd*: comma list of variants to run (uncompressed always)")
+    ap.add_argument("--saved-budget", type=int, default=0,
+                    help="autograd packed-saved variant: PackedActivations verify_bytes, MiB "
+                         "(0: its default)")
+    ap.add_argument("--saved-exit", type=int, default=-1,
+                    help="autograd packed-saved variant: PackedActivations exit_bytes, MiB "
+                         "(-1: its default)")
     ap.add_argument("--no-multi", action="store_true",
                     help="--config smaq: skip the nested C5 multi-tensor line (c5_multi)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)

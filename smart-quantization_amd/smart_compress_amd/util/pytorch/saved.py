@@ -25,9 +25,9 @@ synchronisation: the C forward call (csrc/torchfast.cpp ``smaq_packed``) hands t
 host-mapped coherent memory (``smq_smaq_roundtrip_compress_notify``) into which the launch that writes
 the stream's header stores its total_bytes, and the host reads it with a load. Each save reads the
 words that are there (oldest first: a stream that fit drops its ``y``) and waits — for the oldest
-word only, i.e. an earlier call, usually done by then — while more than 256 MiB of activations are
-still waiting (``verify_bytes`` sets it); nothing waits at the context's exit (the rest are read by
-later saves, unpacks or the next entry: ``y`` stays the saved value until then). Calls that take the
+word only, i.e. an earlier call, usually done by then — while more than 64 MiB of activations are
+still waiting (``verify_bytes`` sets it), at the context's exit too (the rest are read by later
+saves, unpacks or the next entry: ``y`` stays the saved value until then). Calls that take the
 Python path (no notify word) send their sizes in batches of ``verify_batch`` bytes instead (a device
 gather, an asynchronous copy to pinned memory, an event; 32 MiB of held activations at most by
 default), settled at the context's exit. A stream
@@ -184,11 +184,16 @@ class PackedActivations:
             raise TypeError("PackedActivations needs a SmartFPPacked codec")
         self.codec = codec
         # activations held while their sizes are on their way, before the host waits: notified
-        # calls (a load per size: a large budget costs no host time; the ResNet-34 step's peak is
-        # the same with 32 MiB and 1024 MiB, profiles/r6s_saved_ab.txt) and the event path's
-        # batches (whose requests cost host time and whose held activations raised the peak:
-        # 286 / 311 / 363 MiB at 32 / 64 / 128 MiB, profiles/r6o_saved_ab_verify_bytes.txt)
-        self.notify_bytes = int(verify_bytes) if verify_bytes is not None else 256 << 20
+        # calls (a load per size) and the event path's batches (whose requests cost host time).
+        # A larger budget lets the host run further ahead of the device (fewer waits) and holds
+        # more activations at once: ResNet-34 / VGG packed steps at 32 / 64 / 256 MiB — 1.21 /
+        # 1.18 / 1.13 and 1.22 / 1.16 / 1.12 x their SmartFP step, peaks 273 / 275 / 273 and
+        # 238 / 263 / 314 MiB against 333 and 292 uncompressed (profiles/r6zb_saved_budget.txt)
+        self.notify_bytes = int(verify_bytes) if verify_bytes is not None else 64 << 20
+        # at the context's exit: wait until at most this much is still unchecked; what is left is
+        # held into backward (its size words are read by later unpacks). Waiting for all of it
+        # holds the host until the device has run the whole forward (ResNet-34: +0.6 ms per step)
+        self.exit_bytes = self.notify_bytes
         self.verify_bytes = int(verify_bytes) if verify_bytes is not None else 32 << 20
         # the event path (calls without a notify word): a size request per verify_batch bytes of
         # saved activations (default: the budget; smaller batches cost more host time per step
@@ -531,13 +536,13 @@ class PackedActivations:
         hooks, self._hooks = self._hooks, None
         try:
             self._join()  # backward decodes the streams on the current stream
-            # the event path's batches are settled here; notified handles are not waited for (that
-            # would hold the host until the device has run the whole forward, and backward could not
-            # be enqueued behind it): they keep their activation, within the budget, until their
-            # words are read — by the next save, unpack or context entry
+            # the event path's batches are settled here; notified handles are waited for only down
+            # to exit_bytes (waiting for all would hold the host until the device has run the whole
+            # forward, and backward could not be enqueued behind it): the rest keep their
+            # activation until their words are read — by the next save, unpack or context entry
             self._request_sizes()
             self._harvest(0)
-            self._poll(self.notify_bytes)
+            self._poll(self.exit_bytes)
         finally:
             ring = self._notify
             for e in self._live.values():
