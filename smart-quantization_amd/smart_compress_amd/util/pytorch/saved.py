@@ -174,7 +174,7 @@ class _Saved:
 
 
 class _Entry:
-    __slots__ = ("ref", "packed", "version", "shape", "stride", "dtype", "handle", "slot")
+    __slots__ = ("ref", "packed", "version", "shape", "stride", "dtype", "handle", "slot", "site")
 
 
 class PackedActivations:
@@ -214,6 +214,14 @@ class PackedActivations:
         self._notified: Deque[_Saved] = deque()
         self._notified_bytes = 0
         self._notify: Optional[_NotifyRing] = None  # the process's ring, at the first C call
+        # call sites (the k-th forward call of a step): packed this step, saved as streams this
+        # step, and those whose packing is skipped (see _take_site)
+        self._site = 0
+        self._packed_sites: set = set()
+        self._used_sites: set = set()
+        self._skip: frozenset = frozenset()
+        self._steps = 0
+        self.skipped_packs = 0
         # batches whose sizes are on their way to the host: (event, pinned sizes, handles, bytes)
         self._inflight: Deque[tuple] = deque()
         self._inflight_bytes = 0
@@ -235,6 +243,11 @@ class PackedActivations:
                 or not x.is_cuda or x.dtype == torch.float64):
             # a value nobody keeps as a stream (a grad-map, a call outside the context): SmartFP's
             # own call (one launch up to 8.4M elements), the values decompress(compress(x)) has
+            return SmartFP.__call__(codec, x, tag=tag, all_positive=all_positive,
+                                    batch_norm_stats=batch_norm_stats, **kw)
+        site = self._take_site()
+        if site in self._skip:  # its output was never saved as a stream lately: SmartFP's call
+            self.skipped_packs += 1
             return SmartFP.__call__(codec, x, tag=tag, all_positive=all_positive,
                                     batch_norm_stats=batch_norm_stats, **kw)
         if not self.overlap and (batch_norm_stats is None or not hp.use_batch_norm):
@@ -260,7 +273,7 @@ class PackedActivations:
                 y, data = r
                 return self._register(y, SmaqPacked(data, x.shape, x.numel(),
                                                     widths=(hp.num_bits_main,
-                                                            hp.num_bits_outlier)), slot)
+                                                            hp.num_bits_outlier)), slot, site)
         n = x.numel()
         bn = batch_norm_stats is not None and hp.use_batch_norm
         channels = (1 if hp.bn_scalar_params else x.shape[1]) if bn else 0
@@ -276,7 +289,7 @@ class PackedActivations:
         else:
             y, full = codec.roundtrip_compress(x, all_positive, batch_norm_stats, capacity=cap)
         codec.log_size(tag, n * 32, lambda: full.nbytes * 8)
-        return self._register(y, full)
+        return self._register(y, full, None, site)
 
     def _autograd_fast(self, x: torch.Tensor, backward: bool):
         """Compressor.forward for this compress_fn in C (util/pytorch/autograd.py): inside the
@@ -294,6 +307,14 @@ class PackedActivations:
             hot = codec._build_hot()
         if hot is False:
             return None
+        site = self._take_site()
+        if site in self._skip:  # its output was never saved as a stream lately: SmartFP's C call
+            r = codec._autograd_fast(x, backward)
+            if r is None:  # (the Python Function then calls __call__, which takes this site)
+                self._site -= 1
+            else:
+                self.skipped_packs += 1
+            return r
         T = N._torch_fast
         slot, addr = self._arm()
         r = None
@@ -307,11 +328,27 @@ class PackedActivations:
             if slot is not None and (r is None or r is NotImplemented):
                 self._notify.release(slot, written=False)
         if r is None or r is NotImplemented:
+            self._site -= 1  # (the Python Function then calls __call__, which takes this site)
             return None
         y, data = r
         hp = codec.hparams
         return self._register(y, SmaqPacked(data, x.shape, x.numel(),
-                                            widths=(hp.num_bits_main, hp.num_bits_outlier)), slot)
+                                            widths=(hp.num_bits_main, hp.num_bits_outlier)), slot,
+                              site)
+
+    # Forward calls whose outputs the model saves only after changing them in place (an in-place
+    # ReLU, BasicBlock's `out += identity`) are packed for nothing: their stream no longer describes
+    # the saved tensor. A model calls its codec in the same order every step, so the k-th forward
+    # call of a step (its "site") whose stream was not saved in the last step runs as SmartFP's
+    # own call the next time (the same values and random stream; the output is then saved as
+    # itself, as it would have been). Every _REPROBE steps every site packs again, so a site whose
+    # output starts being saved is found. ResNet-34: 60 of 132 packs per step skipped.
+    _REPROBE = 64
+
+    def _take_site(self) -> int:
+        site = self._site
+        self._site += 1
+        return site
 
     def _arm(self):
         """(word index, its address) for the next C call's size notification, or (None, None)."""
@@ -323,8 +360,8 @@ class PackedActivations:
         i = ring.take()
         return (None, None) if i is None else (i, ring.base + 4 * i)
 
-    def _register(self, y: torch.Tensor, packed: SmaqPacked,
-                  slot: Optional[int] = None) -> torch.Tensor:
+    def _register(self, y: torch.Tensor, packed: SmaqPacked, slot: Optional[int] = None,
+                  site: int = -1) -> torch.Tensor:
         """Remember y's stream (and the notify word its size arrives in) until autograd saves y
         (or y dies)."""
         e = _Entry()
@@ -338,7 +375,9 @@ class PackedActivations:
         e.shape, e.stride, e.dtype = y.shape, y.stride(), y.dtype
         e.handle = None
         e.slot = slot
+        e.site = site
         self._live[key] = e
+        self._packed_sites.add(site)
         return y
 
     _RING = 4
@@ -392,6 +431,7 @@ class PackedActivations:
         if e.handle is not None:  # saved again (another consumer): the same stream
             return e.handle
         h = e.handle = _Saved(e.packed, y, self.codec, e.version, e.ref, e.slot)
+        self._used_sites.add(e.site)
         if e.slot is not None:  # its size arrives in a notify word: read, never requested
             e.slot = None  # (the handle holds the word now)
             self._notified.append(h)
@@ -528,6 +568,9 @@ class PackedActivations:
     def __enter__(self):
         if self._notified:  # (handles of an earlier step whose sizes nobody has read yet)
             self._poll(self.notify_bytes)
+        self._site = 0
+        self._packed_sites = set()
+        self._used_sites = set()
         self._hooks = torch.autograd.graph.saved_tensors_hooks(self._pack, self._unpack)
         self._hooks.__enter__()
         return self
@@ -543,6 +586,13 @@ class PackedActivations:
             self._request_sizes()
             self._harvest(0)
             self._poll(self.exit_bytes)
+            # the sites packed this step whose stream nobody saved are skipped from now on (with
+            # the ones skipped already), until the next re-probe step packs every site again
+            self._steps += 1
+            if self._steps % self._REPROBE == 0:
+                self._skip = frozenset()
+            else:
+                self._skip = frozenset(self._skip | (self._packed_sites - self._used_sites))
         finally:
             ring = self._notify
             for e in self._live.values():
@@ -561,5 +611,6 @@ class PackedActivations:
                 "saved_stream_bytes": self.saved_bytes,
                 "bits_per_element": 8.0 * self.saved_bytes / el if el else None,
                 "allocated_bits_per_element": 8.0 * self.saved_capacity / el if el else None,
-                "kept_fp32": self.kept_fp32, "size_waits": self.size_waits,
+                "kept_fp32": self.kept_fp32, "skipped_packs": self.skipped_packs,
+                "size_waits": self.size_waits,
                 "size_wait_s": self.size_wait_s}

@@ -79,6 +79,8 @@ def test_packed_saved_activations_bitexact(inplace, overlap):
         assert all(_eq(p, q) for p, q in zip(ga, gb))
     acts.verify()  # (sizes not read by the last unpacks: nothing waits for them at the exit)
     st = acts.stats()
+    # the second step skipped the packing of the outputs the first one did not save as streams
+    assert st["skipped_packs"] > 0, st
     assert st["saved_packed"] >= 8 and 6.0 < st["bits_per_element"] < 9.0, st
     assert st["kept_fp32"] == 0 and st["allocated_bits_per_element"] < 10.5, st
     if not overlap:  # the C calls' sizes came through notify words, every word released since
@@ -214,3 +216,43 @@ def test_inplace_change_after_save_raises(when):
         with pytest.raises(RuntimeError, match="modified by an inplace operation"):
             loss.backward()
     assert acts.stats()["saved_packed"] == 1
+
+
+def test_skipped_site_that_gets_saved_stays_exact():
+    """A call site whose stream went unsaved in one step runs as SmartFP's own call in the next
+    (saved_tensors_hooks then see an output with no stream: it is saved as itself). When that
+    step does save it, the values and gradients are still SmartFP's; the re-probe step packs it
+    again."""
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import Compressor
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(1 << 18, device="cuda", generator=g)
+    ref = SmartFP(smaq_hparams())
+    pk = SmartFPPacked(smaq_hparams())
+    for c in (ref, pk):
+        c.rng.seed, c.rng.offset = 5, 0
+    acts = PackedActivations(pk)
+    acts._REPROBE = 3
+    comp_p, comp_r = Compressor(acts), Compressor(ref)
+    for step, saves in enumerate((False, True, True, True)):
+        res = []
+        for comp in (comp_r, comp_p):
+            w = torch.linspace(0.5, 1.5, x.numel(), device="cuda").requires_grad_(True)
+            if comp is comp_p:
+                with acts:
+                    y = comp(x * w)
+                    loss = (y * y).sum() if saves else y.sum()  # (y * y saves y; sum does not)
+            else:
+                y = comp(x * w)
+                loss = (y * y).sum() if saves else y.sum()
+            loss.backward()
+            res.append((y.detach(), w.grad.clone()))
+        assert _eq(res[0][0], res[1][0]) and _eq(res[0][1], res[1][1]), step
+        acts.verify()
+        st = acts.stats()
+        # step 0 packs (unsaved); steps 1-2 skip the site; step 2 is the re-probe's last skipped
+        # step (the skip set clears after 3 steps), step 3 packs and saves a stream again
+        assert st["skipped_packs"] == {0: 0, 1: 1, 2: 2, 3: 2}[step], (step, st)
+    assert st["saved_packed"] == 2 and pk.rng.offset == ref.rng.offset  # (y * y: y saved twice)

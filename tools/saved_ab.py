@@ -6,6 +6,7 @@ enqueued behind 100 large GEMMs, synchronised afterwards) and a cProfile of the 
 
 python tools/saved_ab.py [rounds] [kinds: comma list of smartfp, smartfp_ratio, packed,
 packed_overlap, packed_event (sizes by batch requests and events instead of notify words),
+packed_noskip (every forward output packed, also those never saved as streams),
 packed_v<MiB> (verify_bytes), packed_b<MiB> (the event path's batch)]
 Also prints each kind's step peak above the memory resident before it."""
 
@@ -61,6 +62,8 @@ def build(kind):
                                  verify_batch=vbat)
         if kind == "packed_event":  # round 6's first form: sizes by batch requests + events
             acts._arm = lambda: (None, None)
+        if kind == "packed_noskip":  # every forward output packed (no call-site skipping)
+            acts._REPROBE = 1
         register_autograd_module(net, acts, flags)
     return net, opt, acts
 
