@@ -421,6 +421,9 @@ class PackedActivations:
         if t._version != e.version:  # modified in place since (e.g. an in-place ReLU): its stream
             if e.handle is None:     # no longer describes it
                 self._live.pop(key, None)
+                if e.slot is not None:  # (its notify word: nobody reads it now)
+                    self._notify.release(e.slot)
+                    e.slot = None
             return t
         if t.shape != e.shape or t.stride() != e.stride or t.dtype != e.dtype:
             return t  # a view of it

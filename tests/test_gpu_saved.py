@@ -29,7 +29,8 @@ def _eq(a, b):
     return torch.equal(a.view(torch.int32), b.view(torch.int32))
 
 
-@pytest.mark.parametrize("inplace,overlap", [(False, True), (True, True), (False, False)])
+@pytest.mark.parametrize("inplace,overlap", [(False, True), (True, True), (False, False),
+                                             (True, False)])
 def test_packed_saved_activations_bitexact(inplace, overlap):
     from smart_compress_amd.compress import SmartFP, SmartFPPacked
     from smart_compress_amd.util.pytorch.autograd import register_autograd_module
