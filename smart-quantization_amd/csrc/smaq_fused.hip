@@ -1101,8 +1101,10 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
       unsigned long long s = 0;
 #pragma unroll
       for (int w = 0; w < kSmallWaves; ++w) s += sh_cnt[w];
-      if (A.rec_gran && G > 1)  // one epoch-tagged granule; the call's last workgroup sums them
+      if (A.rec_gran && G > 1) {  // one epoch-tagged granule; the call's last workgroup sums them
         st_sc1_u64(A.rec_gran + b, ((uint64_t)epoch << 32) | (uint32_t)s);
+        smiss[1] = (int)s;  // (its own count: the last workgroup does not read its granule back)
+      }
       else if (A.rec) size_record_arrive(A.rec, s, b, G, A.n, A.bm, A.bo);
       else if (s) atomicAdd(A.out_slots + (b & (SMQ_WS_OUTLIER_SLOTS - 1)), s);
     }
@@ -1120,14 +1122,24 @@ __global__ __launch_bounds__(kSmallT) void smaq_fused_kernel(FusedArgs A) {
     if (threadIdx.x == kArriveThread) smiss[0] = last ? 1 : 0;
     lds_barrier();
     if (smiss[0] && wave == 0) {
-      unsigned long long tot = 0;
-      for (int k0 = 0; k0 < G; k0 += kWave) {
-        const int k = k0 + lane;
-        if (k < G) {
-          uint64_t g;
-          while ((uint32_t)((g = ld_sc1_u64(A.rec_gran + k)) >> 32) != epoch) fused_sleep(1);
-          tot += (uint32_t)g;
+      // every granule's load issued before any is looked at (one round trip, not G / 64), then
+      // the missing ones polled
+      constexpr int K = kSmallMaxG / kWave;
+      uint64_t g[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const int k = lane + i * kWave;
+        g[i] = (k < G && k != b) ? ld_sc1_u64(A.rec_gran + k) : ((uint64_t)epoch << 32);
+      }
+      unsigned long long tot = lane == 0 ? (unsigned long long)(uint32_t)smiss[1] : 0ull;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const int k = lane + i * kWave;
+        while ((uint32_t)(g[i] >> 32) != epoch) {
+          fused_sleep(1);
+          g[i] = ld_sc1_u64(A.rec_gran + k);
         }
+        if (k < G && k != b) tot += (uint32_t)g[i];
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, kWave);
