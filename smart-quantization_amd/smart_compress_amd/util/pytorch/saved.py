@@ -40,6 +40,8 @@ one of a ring of workspaces the current stream waits for before reusing; backwar
 checks) are ordered after the side stream. It costs ~20 us of host time per call (events, stream
 waits, record_stream), which an eager ResNet-34 step cannot spare (15.0 -> 19.2 ms/step,
 profiles/r5x_saved_ab.txt).
+float64 activations are held as float64 streams (``SmartFPPacked.compress`` then its decode: SmartFP's
+fp64 chain bit for bit; autograd.py:64-72 compresses whatever dtype the layer produces).
 Backward-direction calls (grad-maps, never saved) and calls outside the context run as SmartFP's
 own call (the same values as the codec's decompress(compress(x)), one launch instead of five).
 """
@@ -240,7 +242,7 @@ class PackedActivations:
         codec = self.codec
         hp = codec.hparams
         if (self._hooks is None or tag != FORWARD_TAG or x.numel() < hp.min_size
-                or not x.is_cuda or x.dtype == torch.float64):
+                or not x.is_cuda):
             # a value nobody keeps as a stream (a grad-map, a call outside the context): SmartFP's
             # own call (one launch up to 8.4M elements), the values decompress(compress(x)) has
             return SmartFP.__call__(codec, x, tag=tag, all_positive=all_positive,

@@ -257,3 +257,44 @@ def test_skipped_site_that_gets_saved_stays_exact():
         # step (the skip set clears after 3 steps), step 3 packs and saves a stream again
         assert st["skipped_packs"] == {0: 0, 1: 1, 2: 2, 3: 2}[step], (step, st)
     assert st["saved_packed"] == 2 and pk.rng.offset == ref.rng.offset  # (y * y: y saved twice)
+
+
+def test_packed_saved_float64_activations_bitexact():
+    """A float64 model (autograd.py:64-72 compresses whatever dtype a layer produces): its saved
+    activations are held as float64 streams (SMQ_PACK_FLAG_F64) and the gradients equal the
+    SmartFP run's bit for bit."""
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import register_autograd_module
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
+
+    def run(packed):
+        torch.manual_seed(5)
+        net = nn.Sequential(nn.Linear(256, 512), nn.ReLU(), nn.Linear(512, 512), nn.Tanh(),
+                            nn.Linear(512, 10)).cuda().double()
+        codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
+        codec.rng.seed, codec.rng.offset = 8, 0
+        acts = PackedActivations(codec) if packed else None
+        register_autograd_module(net, acts if packed else codec, flags)
+        g = torch.Generator(device="cuda").manual_seed(4)
+        x = torch.randn(512, 256, device="cuda", generator=g, dtype=torch.float64,
+                        requires_grad=True)
+        if packed:
+            with acts:
+                loss = net(x).square().mean()
+        else:
+            loss = net(x).square().mean()
+        loss.backward()
+        return (loss.detach(), x.grad.clone(), [p.grad.clone() for p in net.parameters()],
+                codec.rng.offset, acts)
+
+    la, xa, ga, off_a, _ = run(False)
+    lb, xb, gb, off_b, acts = run(True)
+    assert off_a == off_b > 0
+    v = lambda t: t.view(torch.int64)  # noqa: E731
+    assert torch.equal(v(la), v(lb)) and torch.equal(v(xa), v(xb))
+    assert all(torch.equal(v(p), v(q)) for p, q in zip(ga, gb))
+    acts.verify()
+    st = acts.stats()
+    assert st["saved_packed"] >= 2 and st["kept_fp32"] == 0, st
