@@ -93,14 +93,22 @@ def register_autograd_module(model: nn.Module, compress_fn, hparams: Namespace):
     compressor = Compressor(compress_fn, forward=hparams.compress_forward,
                             backward=hparams.compress_backward)
     use_bn = bool(getattr(hparams, "use_batch_norm", False))
+    from .saved import replayable
 
     def wrap(module: nn.Module):
         if not is_valid_layer_type(module):
             return
         inner = module.forward
         bn = use_bn and type(module) == nn.BatchNorm2d
+        # PackedActivations: an in-place activation on a codec output is noted before it runs, so
+        # the value it leaves is saved as that output's stream with the activation replayed
+        note = getattr(compress_fn, "note_inplace", None)
+        if note is not None and not replayable(module):
+            note = None
 
         def forward(*args, **kwargs):
+            if note is not None and args:
+                note(module, args[0])
             y = inner(*args, **kwargs)
             if bn:
                 return compressor(y, {"batch_norm_stats": (module.weight.detach(),

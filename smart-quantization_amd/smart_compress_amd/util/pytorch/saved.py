@@ -149,13 +149,16 @@ class _Saved:
     a weak reference to it (saved_tensors_hooks turn off autograd's own in-place check: _unpack
     repeats it), and the notify word its size arrives in (None: the event path)."""
 
-    __slots__ = ("packed", "y", "codec", "version", "ref", "modified", "slot")
+    __slots__ = ("packed", "y", "codec", "version", "ref", "modified", "slot", "replay")
 
     def __init__(self, packed: SmaqPacked, y: torch.Tensor, codec: SmartFPPacked, version: int,
-                 ref, slot: Optional[int] = None):
+                 ref, slot: Optional[int] = None, replay: Optional[torch.nn.Module] = None):
         self.packed, self.y, self.codec = packed, y, codec
         self.version, self.ref, self.modified = version, ref, None
         self.slot = slot
+        # an in-place activation module the saved value went through after the codec (its class
+        # forward is replayed on the decoded stream: the same op on the same bits)
+        self.replay = replay
 
     def check_version(self) -> None:
         """Raise autograd's in-place error when the saved activation was modified after it was
@@ -176,7 +179,21 @@ class _Saved:
 
 
 class _Entry:
-    __slots__ = ("ref", "packed", "version", "shape", "stride", "dtype", "handle", "slot", "site")
+    __slots__ = ("ref", "packed", "version", "shape", "stride", "dtype", "handle", "slot", "site",
+                 "post")
+
+
+# In-place activation modules whose op on a codec output can be replayed on its decoded stream:
+# deterministic elementwise functions of the values alone whose in-place ATen op (one version bump)
+# saves its result for backward. (Hardtanh / ReLU6 / SiLU / Hardswish / Hardsigmoid / Mish save a
+# clone of their input instead: nothing of the codec output's storage is saved.) Exact types only.
+_REPLAYABLE = (torch.nn.ReLU, torch.nn.LeakyReLU, torch.nn.ELU, torch.nn.CELU, torch.nn.SELU)
+
+
+def replayable(module: torch.nn.Module) -> bool:
+    """Whether PackedActivations can hold the output of ``module`` applied in place to a codec
+    output as that output's stream plus the module (util/pytorch/autograd.py asks, per module)."""
+    return type(module) in _REPLAYABLE and bool(getattr(module, "inplace", False))
 
 
 class PackedActivations:
@@ -224,6 +241,7 @@ class PackedActivations:
         self._skip: frozenset = frozenset()
         self._steps = 0
         self.skipped_packs = 0
+        self.saved_replayed = 0  # of saved_packed: with an in-place activation replayed
         # batches whose sizes are on their way to the host: (event, pinned sizes, handles, bytes)
         self._inflight: Deque[tuple] = deque()
         self._inflight_bytes = 0
@@ -378,6 +396,7 @@ class PackedActivations:
         e.handle = None
         e.slot = slot
         e.site = site
+        e.post = None
         self._live[key] = e
         self._packed_sites.add(site)
         return y
@@ -414,6 +433,19 @@ class PackedActivations:
             torch.cuda.current_stream(di).wait_stream(side)
         self._joined = True
 
+    def note_inplace(self, module: torch.nn.Module, x) -> None:
+        """An in-place activation module (``replayable``) is about to run on x: when x is a codec
+        output of this step not modified since, remember the module, so that the value it leaves
+        (one version later) is saved as x's stream with the module replayed on the decoded values
+        (ResNet's ``relu(bn1(...))``: the stream of bn1's output instead of the fp32 activation).
+        Called by register_autograd_module's wrapper before the module's forward."""
+        if self._hooks is None or type(x) is not torch.Tensor or not x.is_cuda:
+            return
+        e = self._live.get(x.data_ptr())
+        if (e is not None and e.version == x._version and x.shape == e.shape
+                and x.stride() == e.stride and x.dtype == e.dtype):
+            e.post = (module, x._version)
+
     # -- saved_tensors_hooks ------------------------------------------------------------------------
     def _pack(self, t: torch.Tensor):
         key = t.data_ptr() if t.is_cuda else None
@@ -421,6 +453,10 @@ class PackedActivations:
         if e is None:
             return t  # not a forward output of this codec
         if t._version != e.version:  # modified in place since (e.g. an in-place ReLU): its stream
+            post = e.post            # (with the op replayed, when note_inplace saw it coming)
+            if (post is not None and t._version == post[1] + 1 and t.shape == e.shape
+                    and t.stride() == e.stride and t.dtype == e.dtype):
+                return self._save_replayed(e, t, post[0])
             if e.handle is None:     # no longer describes it
                 self._live.pop(key, None)
                 if e.slot is not None:  # (its notify word: nobody reads it now)
@@ -436,6 +472,24 @@ class PackedActivations:
         if e.handle is not None:  # saved again (another consumer): the same stream
             return e.handle
         h = e.handle = _Saved(e.packed, y, self.codec, e.version, e.ref, e.slot)
+        return self._hold(e, h, y)
+
+    def _save_replayed(self, e: _Entry, t: torch.Tensor, module: torch.nn.Module):
+        """t: the codec output of entry e after the in-place module op note_inplace recorded (one
+        version later): held as e's stream and the module, replayed in _unpack."""
+        y = e.ref()
+        if y is None:
+            return t
+        self.saved_packed += 1
+        self.saved_replayed += 1
+        e.post = None
+        e.version = t._version  # (a later save of the same value shares the handle)
+        slot = e.slot if e.handle is None else None  # (else the earlier handle holds the word)
+        h = e.handle = _Saved(e.packed, y, self.codec, e.version, e.ref, slot, replay=module)
+        return self._hold(e, h, y)
+
+    def _hold(self, e: _Entry, h: _Saved, y: torch.Tensor):
+        """A new handle: its size comes through its notify word or the event path's batches."""
         self._used_sites.add(e.site)
         if e.slot is not None:  # its size arrives in a notify word: read, never requested
             e.slot = None  # (the handle holds the word now)
@@ -467,8 +521,13 @@ class PackedActivations:
             p = h.packed
             T = N._torch_fast
             if T is not None and p.widths is not None and p.dtype == torch.float32 and not p.raw:
-                return T.smaq_unpacked(p.data, tuple(p.shape), p.n, p.widths[0], p.widths[1])
-            return h.codec.decompress(p)
+                d = T.smaq_unpacked(p.data, tuple(p.shape), p.n, p.widths[0], p.widths[1])
+            else:
+                d = h.codec.decompress(p)
+            if h.replay is not None:  # the in-place activation the saved value went through
+                with torch.no_grad():
+                    d = type(h.replay).forward(h.replay, d)
+            return d
         return h
 
     def verify(self) -> None:
@@ -617,5 +676,6 @@ class PackedActivations:
                 "bits_per_element": 8.0 * self.saved_bytes / el if el else None,
                 "allocated_bits_per_element": 8.0 * self.saved_capacity / el if el else None,
                 "kept_fp32": self.kept_fp32, "skipped_packs": self.skipped_packs,
+                "saved_replayed": self.saved_replayed,
                 "size_waits": self.size_waits,
                 "size_wait_s": self.size_wait_s}

@@ -84,6 +84,9 @@ def test_packed_saved_activations_bitexact(inplace, overlap):
     assert st["skipped_packs"] > 0, st
     assert st["saved_packed"] >= 8 and 6.0 < st["bits_per_element"] < 9.0, st
     assert st["kept_fp32"] == 0 and st["allocated_bits_per_element"] < 10.5, st
+    # in-place ReLUs on the BatchNorm outputs: their values saved as the BN output's stream with
+    # the ReLU replayed on the decoded values
+    assert (st["saved_replayed"] > 0) == inplace, st
     if not overlap:  # the C calls' sizes came through notify words, every word released since
         assert acts._notify is not None and not any(acts._notify.held)
         assert not acts._notified and not acts._inflight and not acts._pending
@@ -298,3 +301,74 @@ def test_packed_saved_float64_activations_bitexact():
     acts.verify()
     st = acts.stats()
     assert st["saved_packed"] >= 2 and st["kept_fp32"] == 0, st
+
+
+@pytest.mark.parametrize("act", ["relu", "leaky", "elu", "celu", "selu"])
+def test_inplace_activation_replayed_bitexact(act):
+    """An in-place activation module applied to a codec output (ResNet's relu(bn1(x))): its value
+    is saved as the codec output's stream and the module replayed on the decoded values in
+    backward; loss and every gradient equal the SmartFP run's bit for bit."""
+    from smart_compress_amd.compress import SmartFP, SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import register_autograd_module
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    make = {"relu": lambda: nn.ReLU(inplace=True),
+            "leaky": lambda: nn.LeakyReLU(0.1, inplace=True),
+            "elu": lambda: nn.ELU(0.7, inplace=True),
+            "celu": lambda: nn.CELU(1.3, inplace=True),
+            "selu": lambda: nn.SELU(inplace=True)}[act]
+    flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
+
+    def run(packed):
+        torch.manual_seed(11)
+        net = nn.Sequential(nn.Linear(128, 1024), make(), nn.Linear(1024, 1024), nn.LayerNorm(1024),
+                            make(), nn.Linear(1024, 10)).cuda()
+        codec = (SmartFPPacked if packed else SmartFP)(smaq_hparams())
+        codec.rng.seed, codec.rng.offset = 6, 0
+        acts = PackedActivations(codec) if packed else None
+        register_autograd_module(net, acts if packed else codec, flags)
+        g = torch.Generator(device="cuda").manual_seed(2)
+        out = []
+        for _ in range(2):
+            x = torch.randn(512, 128, device="cuda", generator=g, requires_grad=True)
+            net.zero_grad()
+            if packed:
+                with acts:
+                    loss = net(x).square().mean()
+            else:
+                loss = net(x).square().mean()
+            loss.backward()
+            out.append((loss.detach(), x.grad.clone(), [p.grad.clone() for p in net.parameters()]))
+        return out, codec.rng.offset, acts
+
+    a, off_a, _ = run(False)
+    b, off_b, acts = run(True)
+    assert off_a == off_b > 0
+    for (la, xa, ga), (lb, xb, gb) in zip(a, b):
+        assert _eq(la, lb) and _eq(xa, xb)
+        assert all(_eq(p, q) for p, q in zip(ga, gb))
+    acts.verify()
+    st = acts.stats()
+    assert st["saved_replayed"] >= 2 and st["kept_fp32"] == 0, st
+
+
+def test_inplace_activation_then_modified_raises():
+    """A replayed activation's value modified in place again after it was saved: backward raises
+    autograd's in-place error (saved_tensors_hooks switch autograd's own check off)."""
+    from smart_compress_amd.compress import SmartFPPacked
+    from smart_compress_amd.util.pytorch.autograd import register_autograd_module
+    from smart_compress_amd.util.pytorch.saved import PackedActivations
+
+    flags = Namespace(compress_forward=True, compress_backward=True, use_batch_norm=False)
+    lin, relu = nn.Linear(64, 4096).cuda(), nn.ReLU(inplace=True)
+    acts = PackedActivations(SmartFPPacked(smaq_hparams()))
+    register_autograd_module(nn.Sequential(lin), acts, flags)
+    x = torch.randn(64, 64, device="cuda", requires_grad=True)
+    with acts:
+        y = lin(x)
+        acts.note_inplace(relu, y)
+        z = torch.relu_(y)  # saved (the replayed handle)
+        z.mul_(2.0)         # ... and modified after it was saved
+        loss = z.sum()
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        loss.backward()
