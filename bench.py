@@ -1030,6 +1030,7 @@ def run_autograd(args, world, rank, device):
                                                             if args.saved_budget else None))
                 if args.saved_exit >= 0:  # (measurement option: the exit's wait, MiB)
                     fn.exit_bytes = args.saved_exit << 20
+                fn.replay_inplace = not args.saved_no_replay  # (measurement option)
             if sizes is not None:
                 def fn(v, tag=None, **kw):
                     sizes.append(v.numel())
@@ -1292,6 +1293,9 @@ def main():
     ap.add_argument("--saved-exit", type=int, default=-1,
                     help="autograd packed-saved variant: PackedActivations exit_bytes, MiB "
                          "(-1: its default)")
+    ap.add_argument("--saved-no-replay", action="store_true",
+                    help="autograd packed-saved variant: in-place activations of codec outputs "
+                         "saved as fp32 (PackedActivations replay_inplace=False)")
     ap.add_argument("--no-multi", action="store_true",
                     help="--config smaq: skip the nested C5 multi-tensor line (c5_multi)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)

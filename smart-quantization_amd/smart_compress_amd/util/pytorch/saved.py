@@ -198,7 +198,8 @@ def replayable(module: torch.nn.Module) -> bool:
 
 class PackedActivations:
     def __init__(self, codec: SmartFPPacked, verify_bytes: Optional[int] = None,
-                 overlap: bool = False, verify_batch: Optional[int] = None):
+                 overlap: bool = False, verify_batch: Optional[int] = None,
+                 replay_inplace: bool = True):
         if not isinstance(codec, SmartFPPacked):
             raise TypeError("PackedActivations needs a SmartFPPacked codec")
         self.codec = codec
@@ -221,6 +222,11 @@ class PackedActivations:
         # overlap: the packing launches of each forward call on a side stream (they wait for the
         # call's statistics, then run beside the next layers), with a ring of _RING workspaces
         self.overlap = bool(overlap)
+        # in-place activations on codec outputs (note_inplace): their values held as the output's
+        # stream with the activation replayed in backward (ResNet-34: step peak 275 -> 215 MiB, at
+        # +0.2 ms of codec device time per step: the streams of the BN outputs the in-place ReLUs
+        # change are packed and decoded, and the ReLUs replayed); False: saved as fp32
+        self.replay_inplace = bool(replay_inplace)
         self._side: Dict[int, torch.cuda.Stream] = {}
         self._ring: Dict[int, List[list]] = {}  # device -> [[workspace, event recorded after], ...]
         self._ring_next = 0
@@ -439,12 +445,11 @@ class PackedActivations:
         (one version later) is saved as x's stream with the module replayed on the decoded values
         (ResNet's ``relu(bn1(...))``: the stream of bn1's output instead of the fp32 activation).
         Called by register_autograd_module's wrapper before the module's forward."""
-        if self._hooks is None or type(x) is not torch.Tensor or not x.is_cuda:
+        if self._hooks is None or not self.replay_inplace or type(x) is not torch.Tensor:
             return
-        e = self._live.get(x.data_ptr())
-        if (e is not None and e.version == x._version and x.shape == e.shape
-                and x.stride() == e.stride and x.dtype == e.dtype):
-            e.post = (module, x._version)
+        e = self._live.get(x.data_ptr())  # (shape, strides, dtype: checked by _pack)
+        if e is not None and e.version == x._version:
+            e.post = (module, e.version)
 
     # -- saved_tensors_hooks ------------------------------------------------------------------------
     def _pack(self, t: torch.Tensor):

@@ -7,6 +7,7 @@ enqueued behind 100 large GEMMs, synchronised afterwards) and a cProfile of the 
 python tools/saved_ab.py [rounds] [kinds: comma list of smartfp, smartfp_ratio, packed,
 packed_overlap, packed_event (sizes by batch requests and events instead of notify words),
 packed_noskip (every forward output packed, also those never saved as streams),
+packed_noreplay (in-place activations of codec outputs saved as fp32, not replayed),
 packed_v<MiB> (verify_bytes), packed_b<MiB> (the event path's batch)]
 Also prints each kind's step peak above the memory resident before it."""
 
@@ -64,6 +65,8 @@ def build(kind):
             acts._arm = lambda: (None, None)
         if kind == "packed_noskip":  # every forward output packed (no call-site skipping)
             acts._REPROBE = 1
+        if kind == "packed_noreplay":  # in-place ReLUs of codec outputs saved as fp32 (round 6)
+            acts.replay_inplace = False
         register_autograd_module(net, acts, flags)
     return net, opt, acts
 
