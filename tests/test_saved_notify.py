@@ -97,3 +97,62 @@ def test_poll_waits_for_the_oldest_only_over_budget():
     acts._poll(acts.verify_bytes)
     t.join()
     assert a.y is None and b.y is not None and list(acts._notified) == [b]
+
+
+def test_replayable_activation_modules():
+    """The in-place activation modules whose result can be held as the codec output's stream plus
+    the module (their in-place op saves its result): exact types, inplace=True only."""
+    import torch.nn as nn
+
+    from smart_compress_amd.util.pytorch.saved import replayable
+
+    assert all(replayable(m) for m in (nn.ReLU(True), nn.LeakyReLU(0.2, True), nn.ELU(inplace=True),
+                                       nn.CELU(inplace=True), nn.SELU(True)))
+    # out of place, or in-place ops that save a clone of their input (nothing of the output's
+    # storage is saved, so there is nothing to replay)
+    assert not any(replayable(m) for m in (nn.ReLU(), nn.SiLU(True), nn.ReLU6(True),
+                                           nn.Hardtanh(inplace=True), nn.Hardswish(True),
+                                           nn.Conv2d(1, 1, 1)))
+
+    class MyReLU(nn.ReLU):
+        pass
+
+    assert not replayable(MyReLU(True))  # (a subclass may change forward)
+
+
+def test_autograd_wrapper_notes_inplace_activations_before_they_run():
+    """register_autograd_module (autograd.py:50-77) tells a compress_fn with note_inplace about a
+    replayable module's input before the module runs (the value not yet changed), and about no
+    other module."""
+    import torch.nn as nn
+    from argparse import Namespace
+
+    from smart_compress_amd.util.pytorch.autograd import register_autograd_module
+
+    seen = []
+
+    class Fn:
+        def __call__(self, x, tag=None, **kw):
+            return x.clone()
+
+        def note_inplace(self, module, x):
+            seen.append((type(module).__name__, x.clone()))
+
+    net = nn.Sequential(nn.Linear(4, 4), nn.ReLU(inplace=True), nn.Tanh(), nn.ReLU())
+    register_autograd_module(net, Fn(), Namespace(compress_forward=True, compress_backward=True))
+    x = torch.randn(3, 4)
+    h = net[0](x).detach()
+    net(x)
+    assert [s[0] for s in seen] == ["ReLU"] and torch.equal(seen[0][1], h)
+
+
+def test_roundtrip_compress_side_stream_needs_private_workspace():
+    """roundtrip_compress with pack_stream but no workspace raises (the shared per-stream
+    workspace would be rewritten by the next call on the current stream while pack_stream reads
+    it)."""
+    import pytest
+
+    from smart_compress_amd.compress import SmartFPPacked
+
+    with pytest.raises(ValueError, match="private workspace"):
+        SmartFPPacked(smaq_hparams()).roundtrip_compress(torch.randn(4096), pack_stream=object())
