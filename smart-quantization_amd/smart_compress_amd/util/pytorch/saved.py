@@ -530,7 +530,10 @@ class PackedActivations:
             else:
                 d = h.codec.decompress(p)
             if h.replay is not None:  # the in-place activation the saved value went through
-                with torch.no_grad():
+                if torch.is_grad_enabled():  # (backward runs without grad mode unless
+                    with torch.no_grad():    # create_graph asks for it)
+                        d = type(h.replay).forward(h.replay, d)
+                else:
                     d = type(h.replay).forward(h.replay, d)
             return d
         return h
