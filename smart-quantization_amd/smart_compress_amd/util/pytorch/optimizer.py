@@ -19,7 +19,6 @@ passthrough, and the same ``optimizer_*`` compression-ratio logs when measuring.
 quantiser (or non-contiguous / non-fp32 tensor) is called per tensor exactly like the reference.
 """
 
-import copy
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -58,17 +57,10 @@ def _fusable(fn) -> Optional[SmartFP]:
     """The SmartFP behind a wrap_optimizer quantiser (any statistics mode: full, range-std or
     sampled — SmaqMulti computes each exactly as the per-tensor call would)."""
     if isinstance(fn, TaggedQuant) and isinstance(fn.codec, SmartFP):
+        hp = fn.codec.hparams
+        if hp.use_sample_stats and hp.num_samples > N.SMQ_MAX_DEVICE_SAMPLES:
+            return None  # the multi-workgroup draw runs per tensor (SmartFP)
         return fn.codec
-    return None
-
-
-def _fuse_limit(codec: SmartFP) -> Optional[int]:
-    """Largest tensor a fused call takes (None: any). Sampled statistics with more than
-    SMQ_MAX_DEVICE_SAMPLES samples (smart.py:86-91): the multi-workgroup draw runs per tensor
-    (SmartFP); tensors of at most that many elements draw k = n either way and stay fused."""
-    hp = codec.hparams
-    if hp.use_sample_stats and hp.num_samples > N.SMQ_MAX_DEVICE_SAMPLES:
-        return N.SMQ_MAX_DEVICE_SAMPLES
     return None
 
 
@@ -102,43 +94,28 @@ class OptimLP(Optimizer):
     # -- helpers -----------------------------------------------------------------------------------
     def _apply(self, fn, tensors: Sequence[torch.Tensor], all_pos: Sequence[bool],
                assign: Callable[[int, torch.Tensor], None], inplace: bool = True):
-        """Quantise ``tensors`` with ``fn``: one fused launch pair per run of consecutive fusable
-        tensors (in place, or into new tensors handed to ``assign`` when the inputs' storage must
-        survive), the reference's per-tensor calls for the others with their results handed to
-        ``assign`` — in list order, so every tensor draws the random stream a per-tensor loop
-        would give it."""
+        """Quantise ``tensors`` with ``fn``: one fused launch pair when possible (in place, or into
+        new tensors handed to ``assign`` when the inputs' storage must survive), else the
+        reference's per-tensor calls with their results handed to ``assign``."""
         codec = _fusable(fn)
-        limit = _fuse_limit(codec) if codec is not None else None
-        run: List[int] = []
+        fused = [i for i, t in enumerate(tensors) if codec is not None and _fusable_tensor(t)]
+        if fused:
+            multi = self._multi.get(id(fn))
+            if multi is None:
+                multi = self._multi[id(fn)] = SmaqMulti(codec.hparams, rng=codec.rng)
+            multi._graph_safe = codec._graph_safe  # same stream, same mode (device counter or host)
+            xs = [tensors[i] for i in fused]
+            ys = multi(xs, xs if inplace else None, all_positive=[all_pos[i] for i in fused])
+            self._log_fused(codec, fn.tag, multi, xs)
+            if not inplace:
+                for i, y in zip(fused, ys):
+                    if y is not tensors[i]:  # below min_size the reference returns the input
+                        assign(i, y)
+        done = set(fused)
         for i, t in enumerate(tensors):
-            if codec is not None and _fusable_tensor(t) and (limit is None or t.numel() <= limit):
-                run.append(i)
-                continue
-            if run:
-                self._fused(fn, codec, limit, tensors, all_pos, run, assign, inplace)
-                run = []
-            kwargs = {"all_positive": True} if all_pos[i] else {}
-            assign(i, fn(t, **kwargs))
-        if run:
-            self._fused(fn, codec, limit, tensors, all_pos, run, assign, inplace)
-
-    def _fused(self, fn, codec: SmartFP, limit: Optional[int], tensors, all_pos, run: List[int],
-               assign, inplace: bool):
-        multi = self._multi.get(id(fn))
-        if multi is None:
-            hp = codec.hparams
-            if limit is not None:  # (its tensors hold at most `limit` elements: k = n either way)
-                hp = copy.copy(hp)
-                hp.num_samples = limit
-            multi = self._multi[id(fn)] = SmaqMulti(hp, rng=codec.rng)
-        multi._graph_safe = codec._graph_safe  # same stream, same mode (device counter or host)
-        xs = [tensors[i] for i in run]
-        ys = multi(xs, xs if inplace else None, all_positive=[all_pos[i] for i in run])
-        self._log_fused(codec, fn.tag, multi, xs)
-        if not inplace:
-            for i, y in zip(run, ys):
-                if y is not tensors[i]:  # below min_size the reference returns the input
-                    assign(i, y)
+            if i not in done:
+                kwargs = {"all_positive": True} if all_pos[i] else {}
+                assign(i, fn(t, **kwargs))
 
     # the per-tensor log_size values of a fused call stay on the device (SmaqMulti.size_records:
     # no host synchronisation per optimizer step); False: read the counts on the host instead

@@ -112,38 +112,3 @@ def test_layer_tables_match_reference_names():
     assert q.is_valid_layer_type(nn.Dropout(), layer_types=["dropout"])
     with pytest.raises(AssertionError):
         q.is_valid_layer_type(nn.ReLU(), layer_types=["nope"])
-
-
-def test_optimlp_fuses_runs_in_list_order(monkeypatch):
-    """OptimLP._apply (optimizer.py:79-127 loops): runs of consecutive fusable tensors go to one
-    fused call each and the others to the quantiser per tensor, interleaved in list order (so
-    every tensor draws the random stream the per-tensor loop gives it); with sampled statistics
-    above SMQ_MAX_DEVICE_SAMPLES only tensors of at most that many elements are fusable. Host
-    logic only: the fused call is recorded, not launched."""
-    import torch
-
-    from helpers import smaq_hparams
-    from smart_compress_amd.compress.smart import SmartFP
-    from smart_compress_amd.util.pytorch import optimizer as O
-
-    events = []
-    monkeypatch.setattr(O, "_fusable_tensor", lambda t: True)
-    monkeypatch.setattr(O.OptimLP, "_fused",
-                        lambda self, fn, codec, limit, ts, ap, run, assign, inplace:
-                        events.append(("fused", tuple(run), limit)))
-    codec = SmartFP(smaq_hparams(use_sample_stats=True, num_samples=5000))
-    fn = O.TaggedQuant(codec, "optimizer_grad")
-    monkeypatch.setattr(O.TaggedQuant, "__call__",
-                        lambda self, t, **kw: events.append(("call", t.numel())) or t)
-    opt = O.OptimLP(torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=0.1), grad_quant=fn)
-    sizes = [100, 5000, 200, 300, 6000, 50]
-    got = {}
-    opt._apply(fn, [torch.zeros(n) for n in sizes], [False] * len(sizes),
-               lambda i, q: got.__setitem__(i, q.numel()))
-    assert events == [("fused", (0,), 4096), ("call", 5000), ("fused", (2, 3), 4096),
-                      ("call", 6000), ("fused", (5,), 4096)]
-    assert got == {1: 5000, 4: 6000}
-    events.clear()
-    codec.hparams.num_samples = 16  # at or below the device draw limit: one run
-    opt._apply(fn, [torch.zeros(n) for n in sizes], [False] * len(sizes), lambda i, q: None)
-    assert events == [("fused", tuple(range(6)), None)]

@@ -225,34 +225,3 @@ def test_acc_quant_keeps_full_precision_accumulator(fused):
     for p in opt.param_groups[0]["params"]:
         assert p.data.data_ptr() == opt.weight_acc[p].data_ptr()
     assert len(params) == len(opt.weight_acc)
-
-
-@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
-def test_fused_runs_sampled_above_device_draw_limit(opt_name):
-    """--use_sample_stats with --num_samples above SMQ_MAX_DEVICE_SAMPLES (smart.py:86-91): the
-    tensors of at most 4096 elements (k = n) stay fused, a larger one (the 5760-element linear
-    weight: k = 5000, the multi-workgroup draw) runs as its own SmartFP call, in list order — every
-    parameter equals the per-tensor loop's bit for bit."""
-    from smart_compress_amd.compress.smart import SmartFP
-    from smart_compress_amd.util.pytorch.optimizer import OptimLP, wrap_optimizer
-
-    results, fused_calls = [], None
-    for fused in (True, False):
-        model = _model()
-        base = (torch.optim.SGD(_groups(model), lr=0.1, momentum=0.9) if opt_name == "sgd"
-                else torch.optim.Adam(_groups(model), lr=1e-2))
-        codec = SmartFP(smaq_hparams(use_sample_stats=True, num_samples=5000, smq_seed=5))
-        if fused:
-            opt = wrap_optimizer(base, codec, _flags())
-        else:
-            opt = OptimLP(base,
-                          weight_quant=lambda t, **kw: codec(t, tag="optimizer_weight", **kw),
-                          grad_quant=lambda t, **kw: codec(t, tag="optimizer_grad", **kw),
-                          momentum_quant=lambda t, **kw: codec(t, tag="optimizer_momentum", **kw))
-        _train(model, opt)
-        if fused:
-            fused_calls = len(opt._multi)
-        results.append([p.detach().cpu().numpy() for p in model.parameters()])
-    assert fused_calls == 3  # grads, weights, momenta: each fused where it could be
-    for a, b in zip(*results):
-        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
