@@ -530,10 +530,7 @@ class PackedActivations:
             else:
                 d = h.codec.decompress(p)
             if h.replay is not None:  # the in-place activation the saved value went through
-                if torch.is_grad_enabled():  # (backward runs without grad mode unless
-                    with torch.no_grad():    # create_graph asks for it)
-                        d = type(h.replay).forward(h.replay, d)
-                else:
+                with torch.no_grad():
                     d = type(h.replay).forward(h.replay, d)
             return d
         return h
